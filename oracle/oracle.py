@@ -1,0 +1,205 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes front-end of the C oracle (oracle/pp_oracle.c).
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may import this
+module, and only as the checker (or the timed CPU baseline).  The product path
+(``rs-pathplanning_amd/``) never imports, links or executes anything under ``oracle/``.
+
+Parity status: unpinned against the Rust crate (it cannot be built or run here, and it ships no
+golden vectors — SURVEY.md K3/K7); pinned against the independent pure-Python restatement
+(oracle/dubins_py.py) through tests/golden/.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+_lock = threading.Lock()
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH) or (
+        os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "pp_oracle.c"))
+    ):
+        subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "all"], check=True)
+    return LIB_PATH
+
+
+class Scene(C.Structure):
+    _fields_ = [
+        ("minx", C.c_double), ("maxx", C.c_double), ("miny", C.c_double), ("maxy", C.c_double),
+        ("m", C.c_int),
+        ("cx", C.POINTER(C.c_double)), ("cy", C.POINTER(C.c_double)), ("r2", C.POINTER(C.c_double)),
+        ("turn_radius", C.c_double), ("step_size", C.c_double),
+    ]
+
+
+class Tree(C.Structure):
+    _fields_ = [
+        ("x", C.POINTER(C.c_double)), ("y", C.POINTER(C.c_double)),
+        ("yaw", C.POINTER(C.c_double)), ("parent", C.POINTER(C.c_int32)),
+        ("cap", C.c_int), ("n", C.c_int),
+    ]
+
+
+def lib():
+    global _lib
+    with _lock:
+        if _lib is None:
+            build()
+            L = C.CDLL(LIB_PATH)
+            dp = C.POINTER(C.c_double)
+            L.orc_dubins.argtypes = [dp, dp, dp, dp, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), dp]
+            L.orc_dubins.restype = C.c_int
+            L.orc_dubins_n_point.argtypes = [dp]
+            L.orc_dubins_n_point.restype = C.c_int
+            L.orc_rng_u64.argtypes = [C.c_uint64, C.c_uint64]
+            L.orc_rng_u64.restype = C.c_uint64
+            L.orc_gen_range.argtypes = [C.c_uint64, C.c_uint64, C.c_double, C.c_double]
+            L.orc_gen_range.restype = C.c_double
+            L.orc_mod2pi.argtypes = [C.c_double]
+            L.orc_mod2pi.restype = C.c_double
+            L.orc_pi_2_pi.argtypes = [C.c_double]
+            L.orc_pi_2_pi.restype = C.c_double
+            L.orc_verify_line.argtypes = [C.POINTER(Scene), dp, dp, C.c_int]
+            L.orc_verify_line.restype = C.c_int
+            L.orc_nearest.argtypes = [dp, dp, C.c_int, C.c_double, C.c_double, dp]
+            L.orc_nearest.restype = C.c_int
+            L.orc_rrt_extend.argtypes = [C.POINTER(Scene), C.POINTER(Tree), C.c_uint64, C.c_int64,
+                                         C.c_int64, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int8)]
+            L.orc_rrt_extend.restype = C.c_int64
+            L.orc_verify_candidate.argtypes = [C.POINTER(Scene), C.POINTER(Tree), C.c_double,
+                                               C.c_double, C.c_int, C.c_int, dp]
+            L.orc_verify_candidate.restype = C.c_int
+            _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+# ------------------------------------------------------------------------------ dubins
+def dubins(sx, sy, syaw, ex, ey, eyaw, turn_radius, step_size):
+    """dubins_path_planning (dubins.rs:401-428): (px, py, pyaw, word, cost) or None."""
+    L = lib()
+    conf = np.array([sx, sy, syaw, ex, ey, eyaw, turn_radius, step_size], dtype=np.float64)
+    cap = L.orc_dubins_n_point(_dp(conf))
+    if cap <= 0:
+        return None
+    px, py, pyaw = (np.zeros(cap) for _ in range(3))
+    n, word, cost = C.c_int(0), C.c_int(-1), C.c_double(0.0)
+    r = L.orc_dubins(_dp(conf), _dp(px), _dp(py), _dp(pyaw), cap, C.byref(n), C.byref(word), C.byref(cost))
+    if r < 0:
+        raise RuntimeError("orc_dubins failed")
+    if r == 0:
+        return None
+    k = n.value
+    return px[:k].copy(), py[:k].copy(), pyaw[:k].copy(), word.value, cost.value
+
+
+def gen_range(seed, ctr, low, high):
+    return lib().orc_gen_range(seed, ctr, low, high)
+
+
+def rng_u64(seed, ctr):
+    return lib().orc_rng_u64(seed, ctr)
+
+
+def mod2pi(x):
+    return lib().orc_mod2pi(x)
+
+
+def pi_2_pi(x):
+    return lib().orc_pi_2_pi(x)
+
+
+# ------------------------------------------------------------------------------- scene
+class OracleScene:
+    """Space::new (rrt.rs:81-122) restated for the oracle: bounds rectangle shrunk by width/2,
+    discs inflated by width/2 (Q10)."""
+
+    def __init__(self, bounds, width, circles, turn_radius, step_size):
+        half = width / 2.0
+        x0, y0, x1, y1 = bounds
+        self.minx, self.miny, self.maxx, self.maxy = x0 + half, y0 + half, x1 - half, y1 - half
+        circ = np.asarray(circles, dtype=np.float64).reshape(-1, 3)
+        self.cx = np.ascontiguousarray(circ[:, 0])
+        self.cy = np.ascontiguousarray(circ[:, 1])
+        reff = circ[:, 2] + half
+        self.r2 = np.ascontiguousarray(reff * reff)
+        self.turn_radius = float(turn_radius)
+        self.step_size = float(step_size)
+        self._c = Scene(self.minx, self.maxx, self.miny, self.maxy, len(self.cx), _dp(self.cx),
+                        _dp(self.cy), _dp(self.r2), self.turn_radius, self.step_size)
+
+    @classmethod
+    def from_raw(cls, raw):
+        return cls(raw["bounds"], raw["robot"][0], raw["circles"], raw["robot"][2], raw["step_size"])
+
+    def as_dict(self):
+        return {"minx": self.minx, "maxx": self.maxx, "miny": self.miny, "maxy": self.maxy,
+                "cx": self.cx, "cy": self.cy, "r2": self.r2, "turn_radius": self.turn_radius,
+                "step_size": self.step_size}
+
+    def verify_line(self, xs, ys):
+        xs = np.ascontiguousarray(xs, dtype=np.float64)
+        ys = np.ascontiguousarray(ys, dtype=np.float64)
+        return bool(lib().orc_verify_line(C.byref(self._c), _dp(xs), _dp(ys), len(xs)))
+
+
+class OracleTree:
+    """SoA f64 tree, root first (RRT::new, rrt.rs:335-355)."""
+
+    def __init__(self, start, cap):
+        self.x = np.zeros(cap)
+        self.y = np.zeros(cap)
+        self.yaw = np.zeros(cap)
+        self.parent = np.full(cap, -1, dtype=np.int32)
+        self.x[0], self.y[0], self.yaw[0] = start
+        self._c = Tree(_dp(self.x), _dp(self.y), _dp(self.yaw),
+                       self.parent.ctypes.data_as(C.POINTER(C.c_int32)), cap, 1)
+
+    @property
+    def n(self):
+        return self._c.n
+
+    def arrays(self):
+        n = self.n
+        return self.x[:n].copy(), self.y[:n].copy(), self.yaw[:n].copy(), self.parent[:n].copy()
+
+
+def rrt_extend(scene: OracleScene, tree: OracleTree, seed: int, it0: int, n_iter: int,
+               full_reverify: bool = False):
+    """Sequential extend for iterations [it0, it0+n_iter).  Returns (accepted, log_nn, log_acc)."""
+    log_nn = np.zeros(n_iter, dtype=np.int32)
+    log_acc = np.zeros(n_iter, dtype=np.int8)
+    acc = lib().orc_rrt_extend(C.byref(scene._c), C.byref(tree._c), seed, it0, n_iter,
+                               int(full_reverify), log_nn.ctypes.data_as(C.POINTER(C.c_int32)),
+                               log_acc.ctypes.data_as(C.POINTER(C.c_int8)))
+    if acc < 0:
+        raise RuntimeError("orc_rrt_extend failed (capacity?)")
+    return acc, log_nn, log_acc
+
+
+def nearest(X, Y, qx, qy):
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    Y = np.ascontiguousarray(Y, dtype=np.float64)
+    d2 = C.c_double(0)
+    i = lib().orc_nearest(_dp(X), _dp(Y), len(X), qx, qy, C.byref(d2))
+    return i, d2.value
+
+
+def verify_candidate(scene: OracleScene, tree: OracleTree, x, y, parent, full_reverify=False):
+    yaw = C.c_double(0)
+    ok = lib().orc_verify_candidate(C.byref(scene._c), C.byref(tree._c), x, y, parent,
+                                    int(full_reverify), C.byref(yaw))
+    if ok < 0:
+        raise RuntimeError("orc_verify_candidate failed")
+    return bool(ok), yaw.value

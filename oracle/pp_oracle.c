@@ -1,0 +1,522 @@
+/*
+ * pp_oracle.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of tsturzl/rs-pathplanning's RRT extend hot path (Dubins steer + nearest
+ * neighbour + collision verify), used as the parity checker for the HIP product path.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library,
+ * and only as the checker / the timed CPU baseline — never as the thing shipped or measured.
+ *
+ * Parity status: the reference is Rust and cannot be built here (no cargo/rustc, crates.io
+ * deps not vendored) and it ships no golden vectors or tests.  This file is
+ * therefore "parity unpinned" against the crate itself; it is pinned against (a) an independent
+ * pure-Python restatement (oracle/dubins_py.py) through the committed fixtures in tests/golden/,
+ * and (b) the reference-supplied known inputs of examples/dubins/src/main.rs:131-164 and
+ * benches/all.rs:8-42,102-111.
+ *
+ * Compile with -ffp-contract=off and no fast-math: Rust never contracts a*b+c into an FMA, and
+ * every expression below keeps the reference's left-to-right evaluation order.  sin/cos/atan2/
+ * acos/hypot come from the platform libm, exactly as Rust's std f64 methods do on Linux.
+ *
+ * Build-defined deviations:
+ *   Q7  seeded counter RNG (SplitMix64) in place of rand::thread_rng, same draw order (x then y)
+ *       and the same [1,2)-mantissa float construction as rand 0.7's UniformFloat::sample_single;
+ *   Q8  sequential spec (one rayon thread) in place of the 4-thread pool;
+ *   Q9  exact brute-force NN on dx*dx+dy*dy, lowest index wins ties (rstar's pruning is inexact);
+ *   Q10 obstacles are analytic discs of radius r + robot.width/2 and the bounds an axis-aligned
+ *       rectangle shrunk by robot.width/2; polyline-vs-disc uses exact segment distance.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_PI 3.14159265358979323846 /* == std::f64::consts::PI */
+#define ORC_TWO_PI (2.0 * ORC_PI)
+
+/* ---------------------------------------------------------------- dubins.rs restatement */
+
+/* dubins.rs:14-16 */
+static double fmodr(double x, double y) { return x - y * floor(x / y); }
+/* dubins.rs:18-20 */
+double orc_mod2pi(double theta) { return fmodr(theta, ORC_TWO_PI); }
+/* dubins.rs:22-24 — Rust `%` on f64 is C fmod (truncated); negative inputs are not wrapped. */
+double orc_pi_2_pi(double angle) { return fmod(angle + ORC_PI, ORC_TWO_PI) - ORC_PI; }
+
+enum { M_L = 0, M_S = 1, M_R = 2 };
+/* word order of ALL_PLANNERS, dubins.rs:291 */
+enum { W_LSL = 0, W_RSR = 1, W_LSR = 2, W_RSL = 3, W_RLR = 4, W_LRL = 5 };
+static const int WORD_MODES[6][3] = {
+    {M_L, M_S, M_L}, {M_R, M_S, M_R}, {M_L, M_S, M_R},
+    {M_R, M_S, M_L}, {M_R, M_L, M_R}, {M_L, M_R, M_L}};
+
+typedef struct { int ok; double t, p, q; } orc_word;
+
+/* dubins.rs:27-48 */
+static orc_word lsl(double alpha, double beta, double d) {
+    orc_word w = {0, 0, 0, 0};
+    double sa = sin(alpha), sb = sin(beta), ca = cos(alpha), cb = cos(beta);
+    double c_ab = cos(alpha - beta);
+    double tmp0 = d + sa - sb;
+    double p_squared = 2.0 + (d * d) - (2.0 * c_ab) + (2.0 * d * (sa - sb));
+    if (p_squared < 0.0) return w;
+    double tmp1 = atan2(cb - ca, tmp0);
+    w.t = orc_mod2pi(-alpha + tmp1);
+    w.p = sqrt(p_squared);
+    w.q = orc_mod2pi(beta - tmp1);
+    w.ok = 1;
+    return w;
+}
+/* dubins.rs:51-71 */
+static orc_word rsr(double alpha, double beta, double d) {
+    orc_word w = {0, 0, 0, 0};
+    double sa = sin(alpha), sb = sin(beta), ca = cos(alpha), cb = cos(beta);
+    double c_ab = cos(alpha - beta);
+    double tmp0 = d - sa + sb;
+    double p_squared = 2.0 + (d * d) - (2.0 * c_ab) + (2.0 * d * (sb - sa));
+    if (p_squared < 0.0) return w;
+    double tmp1 = atan2(ca - cb, tmp0);
+    w.t = orc_mod2pi(alpha - tmp1);
+    w.p = sqrt(p_squared);
+    w.q = orc_mod2pi(-beta + tmp1);
+    w.ok = 1;
+    return w;
+}
+/* dubins.rs:74-92 */
+static orc_word lsr(double alpha, double beta, double d) {
+    orc_word w = {0, 0, 0, 0};
+    double sa = sin(alpha), sb = sin(beta), ca = cos(alpha), cb = cos(beta);
+    double c_ab = cos(alpha - beta);
+    double p_squared = -2.0 + (d * d) + (2.0 * c_ab) + (2.0 * d * (sa + sb));
+    if (p_squared < 0.0) return w;
+    double p = sqrt(p_squared);
+    double tmp = atan2(-ca - cb, d + sa + sb) - atan2(-2.0, p);
+    w.t = orc_mod2pi(-alpha + tmp);
+    w.p = p;
+    w.q = orc_mod2pi(-orc_mod2pi(beta) + tmp);
+    w.ok = 1;
+    return w;
+}
+/* dubins.rs:95-113 */
+static orc_word rsl(double alpha, double beta, double d) {
+    orc_word w = {0, 0, 0, 0};
+    double sa = sin(alpha), sb = sin(beta), ca = cos(alpha), cb = cos(beta);
+    double c_ab = cos(alpha - beta);
+    double p_squared = -2.0 + (d * d) + (2.0 * c_ab) - (2.0 * d * (sa + sb));
+    if (p_squared < 0.0) return w;
+    double p = sqrt(p_squared);
+    double tmp = atan2(ca + cb, d - sa - sb) - atan2(2.0, p);
+    w.t = orc_mod2pi(alpha - tmp);
+    w.p = p;
+    w.q = orc_mod2pi(beta - tmp);
+    w.ok = 1;
+    return w;
+}
+/* dubins.rs:116-133 */
+static orc_word rlr(double alpha, double beta, double d) {
+    orc_word w = {0, 0, 0, 0};
+    double sa = sin(alpha), sb = sin(beta), ca = cos(alpha), cb = cos(beta);
+    double c_ab = cos(alpha - beta);
+    double tmp_rlr = (6.0 - d * d + 2.0 * c_ab + 2.0 * d * (sa - sb)) / 8.0;
+    if (fabs(tmp_rlr) > 1.0) return w;
+    double p = orc_mod2pi(2.0 * ORC_PI - acos(tmp_rlr));
+    double t = orc_mod2pi(alpha - atan2(ca - cb, d - sa + sb) + orc_mod2pi(p / 2.0));
+    double q = orc_mod2pi(alpha - beta - t + orc_mod2pi(p));
+    w.t = t; w.p = p; w.q = q; w.ok = 1;
+    return w;
+}
+/* dubins.rs:136-153 */
+static orc_word lrl(double alpha, double beta, double d) {
+    orc_word w = {0, 0, 0, 0};
+    double sa = sin(alpha), sb = sin(beta), ca = cos(alpha), cb = cos(beta);
+    double c_ab = cos(alpha - beta);
+    double tmp_lrl = (6.0 - d * d + 2.0 * c_ab + 2.0 * d * (-sa + sb)) / 8.0;
+    if (fabs(tmp_lrl) > 1.0) return w;
+    double p = orc_mod2pi(2.0 * ORC_PI - acos(tmp_lrl));
+    double t = orc_mod2pi(-alpha - atan2(ca - cb, d + sa - sb) + p / 2.0);
+    double q = orc_mod2pi(orc_mod2pi(beta) - alpha - t + orc_mod2pi(p));
+    w.t = t; w.p = p; w.q = q; w.ok = 1;
+    return w;
+}
+
+typedef orc_word (*planner_fn)(double, double, double);
+static const planner_fn ALL_PLANNERS[6] = {lsl, rsr, lsr, rsl, rlr, lrl}; /* dubins.rs:291 */
+
+/* dubins.rs:155-198 (directions are not part of the returned path and are omitted) */
+static void interpolate(int ind, double length, int mode, double max_curvature, double origin_x,
+                        double origin_y, double origin_yaw, double* path_x, double* path_y,
+                        double* path_yaw) {
+    if (mode == M_S) {
+        path_x[ind] = origin_x + length / max_curvature * cos(origin_yaw);
+        path_y[ind] = origin_y + length / max_curvature * sin(origin_yaw);
+        path_yaw[ind] = origin_yaw;
+    } else {
+        double ldx = sin(length) / max_curvature;
+        double ldy = 0.0;
+        if (mode == M_L)
+            ldy = (1.0 - cos(length)) / max_curvature;
+        else
+            ldy = (1.0 - cos(length)) / -max_curvature;
+        double gdx = cos(-origin_yaw) * ldx + sin(-origin_yaw) * ldy;
+        double gdy = -sin(-origin_yaw) * ldx + cos(-origin_yaw) * ldy;
+        path_x[ind] = origin_x + gdx;
+        path_y[ind] = origin_y + gdy;
+    }
+    if (mode == M_L)
+        path_yaw[ind] = origin_yaw + length;
+    else if (mode == M_R)
+        path_yaw[ind] = origin_yaw - length;
+}
+
+/* dubins.rs:200-289.  Returns the kept length after the trailing-zero trim, or -1 when an index
+ * would run past n_point (Rust panics there; unreachable for finite inputs). */
+static int generate_local_course(const double lengths[3], const int mode[3], double max_curvature,
+                                 double step_size, double* path_x, double* path_y, double* path_yaw,
+                                 int n_point) {
+    int ind = 1;
+    double ll = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        int m = mode[i];
+        double l = lengths[i];
+        double d = (l > 0.0) ? step_size : -step_size;
+        double origin_x = path_x[ind], origin_y = path_y[ind], origin_yaw = path_yaw[ind];
+        ind -= 1;
+        double pd;
+        if (i >= 1 && (lengths[i - 1] * lengths[i]) > 0.0)
+            pd = -d - ll;
+        else
+            pd = d - ll;
+        while (fabs(pd) <= fabs(l)) {
+            ind += 1;
+            if (ind >= n_point) return -1;
+            interpolate(ind, pd, m, max_curvature, origin_x, origin_y, origin_yaw, path_x, path_y,
+                        path_yaw);
+            pd += d;
+        }
+        ll = l - pd - d;
+        ind += 1;
+        if (ind >= n_point) return -1;
+        interpolate(ind, l, m, max_curvature, origin_x, origin_y, origin_yaw, path_x, path_y,
+                    path_yaw);
+    }
+    int len = n_point;
+    if (len <= 1) return 0; /* dubins.rs:274-279 (then 281 would panic on the empty vec) */
+    /* dubins.rs:281-288: read the last element, then pop while the value read was 0.0 —
+     * this pops every trailing zero AND the first non-zero element behind them. */
+    double last = path_x[len - 1];
+    while (len >= 1 && last == 0.0) {
+        last = path_x[len - 1];
+        len -= 1;
+    }
+    return len;
+}
+
+/* dubins.rs:326-399.  Writes LOCAL-frame points.  Returns 1 and fills outputs on Some, 0 on None,
+ * -1 on capacity overflow (cap < n_point) or the unreachable index panic. */
+static int from_origin(double dx, double dy, double eyaw, double c, double step_size, double* px,
+                       double* py, double* pyaw, int cap, int* n_out, int* word_out,
+                       double* cost_out, double* lengths_out) {
+    double hyp = hypot(dx, dy);
+    double d = hyp * c;
+    double theta = orc_mod2pi(atan2(dy, dx));
+    double alpha = orc_mod2pi(-theta);
+    double beta = orc_mod2pi(eyaw - theta);
+
+    double bcost = INFINITY;
+    int bword = -1;
+    double bt = 0, bp = 0, bq = 0;
+    for (int i = 0; i < 6; ++i) {
+        orc_word w = ALL_PLANNERS[i](alpha, beta, d);
+        if (w.ok) {
+            double cost = fabs(w.t) + fabs(w.p) + fabs(w.q);
+            if (bcost > cost) { /* strict: first minimum wins (dubins.rs:354) */
+                bt = w.t; bp = w.p; bq = w.q; bword = i; bcost = cost;
+            }
+        }
+    }
+    if (bword < 0) return 0;
+    double lengths[3] = {bt, bp, bq};
+    double total_length = 0.0; /* Iterator::sum folds from 0.0 */
+    for (int i = 0; i < 3; ++i) total_length += lengths[i];
+    double q = trunc(total_length / step_size);
+    if (!(q >= 0.0) || q > 1e9) return -1;
+    int n_point = (int)q + 3 + 4;
+    if (n_point > cap) return -1;
+    for (int i = 0; i < n_point; ++i) px[i] = py[i] = pyaw[i] = 0.0;
+    int n = generate_local_course(lengths, WORD_MODES[bword], c, step_size, px, py, pyaw, n_point);
+    if (n < 0) return -1;
+    *n_out = n;
+    *word_out = bword;
+    *cost_out = bcost;
+    if (lengths_out) { lengths_out[0] = bt; lengths_out[1] = bp; lengths_out[2] = bq; }
+    return 1;
+}
+
+/* Upper bound on n_point for a given configuration is not known before the word is chosen; this
+ * helper returns the n_point that dubins_path_planning would allocate (0 on None). */
+int orc_dubins_n_point(const double conf[8]) {
+    double sx = conf[0], sy = conf[1], syaw = conf[2], ex0 = conf[3], ey0 = conf[4], eyaw = conf[5];
+    double R = conf[6], step = conf[7];
+    double ex = ex0 - sx, ey = ey0 - sy, c = 1.0 / R;
+    double lex = cos(syaw) * ex + sin(syaw) * ey;
+    double ley = -(sin(syaw)) * ex + cos(syaw) * ey;
+    double leyaw = eyaw - syaw;
+    double hyp = hypot(lex, ley), d = hyp * c;
+    double theta = orc_mod2pi(atan2(ley, lex));
+    double alpha = orc_mod2pi(-theta), beta = orc_mod2pi(leyaw - theta);
+    double bcost = INFINITY, tot = 0;
+    int bword = -1;
+    for (int i = 0; i < 6; ++i) {
+        orc_word w = ALL_PLANNERS[i](alpha, beta, d);
+        if (w.ok) {
+            double cost = fabs(w.t) + fabs(w.p) + fabs(w.q);
+            if (bcost > cost) { bcost = cost; bword = i; tot = ((0.0 + w.t) + w.p) + w.q; }
+        }
+    }
+    if (bword < 0) return 0;
+    return (int)trunc(tot / step) + 7;
+}
+
+/* dubins.rs:401-428.  conf = {sx, sy, syaw, ex, ey, eyaw, turn_radius, step_size}
+ * (DubinsConfig, dubins.rs:315-324).  Returns 1 (Some), 0 (None) or -1 (cap too small). */
+int orc_dubins(const double conf[8], double* px, double* py, double* pyaw, int cap, int* n,
+               int* word, double* cost) {
+    double sx = conf[0], sy = conf[1], syaw = conf[2], ex0 = conf[3], ey0 = conf[4], eyaw = conf[5];
+    double turn_radius = conf[6], step_size = conf[7];
+    double ex = ex0 - sx;
+    double ey = ey0 - sy;
+    double c = 1.0 / turn_radius;
+    double lex = cos(syaw) * ex + sin(syaw) * ey;
+    double ley = -(sin(syaw)) * ex + cos(syaw) * ey;
+    double leyaw = eyaw - syaw;
+    int r = from_origin(lex, ley, leyaw, c, step_size, px, py, pyaw, cap, n, word, cost, NULL);
+    if (r != 1) return r;
+    double cs = cos(-syaw), sn = sin(-syaw);
+    for (int i = 0; i < *n; ++i) {
+        double x = px[i], y = py[i];
+        px[i] = cs * x + sn * y + sx;
+        py[i] = -sn * x + cs * y + sy;
+        pyaw[i] = orc_pi_2_pi(pyaw[i] + syaw);
+    }
+    return 1;
+}
+
+/* ------------------------------------------------------------------ seeded sampling (Q7) */
+
+/* SplitMix64 output number `ctr` of the stream seeded with `seed`. */
+uint64_t orc_rng_u64(uint64_t seed, uint64_t ctr) {
+    uint64_t z = seed + (ctr + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+/* rand 0.7 UniformFloat<f64>::sample_single structure: 52 random mantissa bits under exponent 0
+ * give [1,2); minus 1; times scale; plus low.  The (measure-zero) res >= high case narrows the
+ * scale by one ulp and retries with the same bits instead of drawing again. */
+double orc_gen_range(uint64_t seed, uint64_t ctr, double low, double high) {
+    uint64_t bits = (orc_rng_u64(seed, ctr) >> 12) | 0x3FF0000000000000ULL;
+    double value1_2;
+    memcpy(&value1_2, &bits, sizeof value1_2);
+    double value0_1 = value1_2 - 1.0;
+    double scale = high - low;
+    for (;;) {
+        double res = value0_1 * scale + low;
+        if (res < high) return res;
+        scale = nextafter(scale, 0.0);
+    }
+}
+
+/* ------------------------------------------------------------------------ scene (Q10) */
+
+typedef struct {
+    double minx, maxx, miny, maxy; /* bbox of the shrunken bounds (rrt.rs:82-106) */
+    int m;                         /* obstacle discs */
+    const double* cx;
+    const double* cy;
+    const double* r2; /* (r + width/2)^2 */
+    double turn_radius;  /* Robot.max_steer (rrt.rs:37-39 → 424) */
+    double step_size;
+} orc_scene;
+
+typedef struct {
+    double* x;
+    double* y;
+    double* yaw;
+    int32_t* parent;
+    int cap;
+    int n;
+} orc_tree;
+
+/* polyline segment vs closed disc: exact closest point on the segment */
+static int seg_hits_disc(double ax, double ay, double bx, double by, double cx, double cy,
+                         double r2) {
+    double vx = bx - ax, vy = by - ay;
+    double wx = cx - ax, wy = cy - ay;
+    double l2 = vx * vx + vy * vy;
+    double t = 0.0;
+    if (l2 > 0.0) {
+        t = (wx * vx + wy * vy) / l2;
+        if (t < 0.0) t = 0.0;
+        else if (t > 1.0) t = 1.0;
+    }
+    double ex = wx - t * vx, ey = wy - t * vy;
+    return ex * ex + ey * ey <= r2;
+}
+
+static int in_bounds(const orc_scene* sc, double x, double y) {
+    return x >= sc->minx && x <= sc->maxx && y >= sc->miny && y <= sc->maxy;
+}
+
+/* Space::verify, rrt.rs:124-137: bounds.contains(line) && no obstacle intersects the line.
+ * A one-point line is tested as a point (degenerate segment). */
+int orc_verify_line(const orc_scene* sc, const double* x, const double* y, int n) {
+    if (n <= 0) return 1;
+    for (int i = 0; i < n; ++i)
+        if (!in_bounds(sc, x[i], y[i])) return 0;
+    if (n == 1) {
+        for (int k = 0; k < sc->m; ++k)
+            if (seg_hits_disc(x[0], y[0], x[0], y[0], sc->cx[k], sc->cy[k], sc->r2[k])) return 0;
+        return 1;
+    }
+    for (int k = 0; k < sc->m; ++k)
+        for (int i = 0; i + 1 < n; ++i)
+            if (seg_hits_disc(x[i], y[i], x[i + 1], y[i + 1], sc->cx[k], sc->cy[k], sc->r2[k]))
+                return 0;
+    return 1;
+}
+
+/* exact brute-force NN (Q9): argmin dx*dx+dy*dy, lowest index wins ties */
+int orc_nearest(const double* X, const double* Y, int n, double qx, double qy, double* d2_out) {
+    int best = -1;
+    double bd = INFINITY;
+    for (int i = 0; i < n; ++i) {
+        double dx = qx - X[i], dy = qy - Y[i];
+        double d2 = dx * dx + dy * dy;
+        if (d2 < bd) { bd = d2; best = i; }
+    }
+    if (d2_out) *d2_out = bd;
+    return best;
+}
+
+/* compute_yaw, rrt.rs:267-271 */
+static double compute_yaw(double fx, double fy, double tx, double ty) {
+    return atan2(ty - fy, tx - fx);
+}
+
+/* growable point buffer for line building */
+typedef struct { double* x; double* y; int n, cap; } pbuf;
+static int pbuf_push(pbuf* b, double x, double y) {
+    if (b->n == b->cap) {
+        int nc = b->cap ? 2 * b->cap : 1024;
+        double* nx = (double*)realloc(b->x, sizeof(double) * nc);
+        double* ny = (double*)realloc(b->y, sizeof(double) * nc);
+        if (!nx || !ny) { free(nx); free(ny); return -1; }
+        b->x = nx; b->y = ny; b->cap = nc;
+    }
+    b->x[b->n] = x; b->y[b->n] = y; b->n++;
+    return 0;
+}
+
+/* scratch for one Dubins segment */
+typedef struct { double* px; double* py; double* pyaw; int cap; } dscratch;
+static int dscratch_fit(dscratch* s, int need) {
+    if (need <= s->cap) return 0;
+    int nc = need + 1024;
+    double* a = (double*)realloc(s->px, sizeof(double) * nc);
+    double* b = (double*)realloc(s->py, sizeof(double) * nc);
+    double* c = (double*)realloc(s->pyaw, sizeof(double) * nc);
+    if (!a || !b || !c) return -1;
+    s->px = a; s->py = b; s->pyaw = c; s->cap = nc;
+    return 0;
+}
+
+/* one edge of line_to_origin (rrt.rs:295-315): the Dubins polyline child→parent, or [(sx,sy)]
+ * when the steer fails.  Appends to `b`. */
+static int push_edge(pbuf* b, dscratch* s, double sx, double sy, double syaw, double ex, double ey,
+                     double eyaw, double R, double step) {
+    double conf[8] = {sx, sy, syaw, ex, ey, eyaw, R, step};
+    int need = orc_dubins_n_point(conf);
+    if (need > 0 && dscratch_fit(s, need) != 0) return -1;
+    int n = 0, word = -1;
+    double cost = 0;
+    int r = (need > 0) ? orc_dubins(conf, s->px, s->py, s->pyaw, s->cap, &n, &word, &cost) : 0;
+    if (r < 0) return -1;
+    if (r == 0) return pbuf_push(b, sx, sy);
+    for (int i = 0; i < n; ++i)
+        if (pbuf_push(b, s->px[i], s->py[i])) return -1;
+    return 0;
+}
+
+/* RRT::verify_node(Node::new(sample, tree[p])) — rrt.rs:169-175, 414-426.
+ * full_reverify=1 builds the whole line_to_origin (rrt.rs:291-321) like the reference; 0 verifies
+ * edge(new→p) ++ [p] only (the ancestors' part was verified at their insert). */
+static int verify_candidate(const orc_scene* sc, const orc_tree* tr, double x, double y, double yaw,
+                            int p, int full_reverify, pbuf* b, dscratch* s) {
+    b->n = 0;
+    double R = sc->turn_radius, step = sc->step_size;
+    if (push_edge(b, s, x, y, yaw, tr->x[p], tr->y[p], tr->yaw[p], R, step)) return -1;
+    int cur = p;
+    if (!full_reverify) {
+        if (pbuf_push(b, tr->x[cur], tr->y[cur])) return -1;
+    } else {
+        for (;;) {
+            int pp = tr->parent[cur];
+            if (pp < 0) {
+                if (pbuf_push(b, tr->x[cur], tr->y[cur])) return -1;
+                break;
+            }
+            if (push_edge(b, s, tr->x[cur], tr->y[cur], tr->yaw[cur], tr->x[pp], tr->y[pp],
+                          tr->yaw[pp], R, step))
+                return -1;
+            cur = pp;
+        }
+    }
+    return orc_verify_line(sc, b->x, b->y, b->n);
+}
+
+/* Sequential spec of RRT::plan_one's extend (rrt.rs:583-589) for iterations [it0, it0+n_iter):
+ * rand_point (x then y) → exact NN → Node::new → verify_node → insert.  check_finish is a
+ * separate row.  Per-iteration logs: nearest index and accepted flag.
+ * Returns the number of accepted nodes, or -1 (allocation / capacity failure). */
+int64_t orc_rrt_extend(const orc_scene* sc, orc_tree* tr, uint64_t seed, int64_t it0,
+                       int64_t n_iter, int full_reverify, int32_t* log_nn, int8_t* log_acc) {
+    pbuf b = {0};
+    dscratch s = {0};
+    int64_t acc = 0;
+    for (int64_t k = 0; k < n_iter; ++k) {
+        uint64_t it = (uint64_t)(it0 + k);
+        double x = orc_gen_range(seed, 2 * it, sc->minx, sc->maxx);
+        double y = orc_gen_range(seed, 2 * it + 1, sc->miny, sc->maxy);
+        int p = orc_nearest(tr->x, tr->y, tr->n, x, y, NULL);
+        if (log_nn) log_nn[k] = p;
+        int ok = 0;
+        if (p >= 0) {
+            double yaw = compute_yaw(x, y, tr->x[p], tr->y[p]);
+            ok = verify_candidate(sc, tr, x, y, yaw, p, full_reverify, &b, &s);
+            if (ok < 0) { acc = -1; break; }
+            if (ok) {
+                if (tr->n >= tr->cap) { acc = -1; break; }
+                tr->x[tr->n] = x; tr->y[tr->n] = y; tr->yaw[tr->n] = yaw; tr->parent[tr->n] = p;
+                tr->n++;
+                acc++;
+            }
+        }
+        if (log_acc) log_acc[k] = (int8_t)ok;
+    }
+    free(b.x); free(b.y);
+    free(s.px); free(s.py); free(s.pyaw);
+    return acc;
+}
+
+/* verify a single candidate against the tree (for per-candidate parity checks) */
+int orc_verify_candidate(const orc_scene* sc, const orc_tree* tr, double x, double y, int p,
+                         int full_reverify, double* yaw_out) {
+    pbuf b = {0};
+    dscratch s = {0};
+    double yaw = compute_yaw(x, y, tr->x[p], tr->y[p]);
+    if (yaw_out) *yaw_out = yaw;
+    int ok = verify_candidate(sc, tr, x, y, yaw, p, full_reverify, &b, &s);
+    free(b.x); free(b.y);
+    free(s.px); free(s.py); free(s.pyaw);
+    return ok;
+}

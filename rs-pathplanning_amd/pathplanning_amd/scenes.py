@@ -1,0 +1,123 @@
+"""Synthetic scenes (host-side input data, no GPU needed).
+
+* ``bench6`` — the reference's only fully specified scene, ``benches/all.rs:8-42`` (config 1).
+* ``field512`` — BASELINE.json config 2/3/4: 1024 random discs on a 512x512 rectangle.
+
+A raw scene is a plain dict: ``bounds`` (x0, y0, x1, y1) of the un-shrunk rectangle, ``robot``
+(width, height, max_steer) as in ``Robot::new`` (rrt.rs:25), ``circles`` (M, 3) array of
+(cx, cy, r) as built by ``create_circle`` (rrt.rs:43), ``start``/``goal`` (x, y, yaw),
+``max_iter`` and ``step_size`` as passed to ``RRT::new`` (rrt.rs:335-343).
+"""
+from __future__ import annotations
+
+import math
+import struct
+
+import numpy as np
+
+_M64 = (1 << 64) - 1
+
+
+def rng_u64(seed: int, ctr: int) -> int:
+    """SplitMix64 output ``ctr`` of the stream ``seed`` — the build's seeded replacement for
+    ``rand::thread_rng`` (rrt.rs:140).  Mirrors pp_rng_u64 in the C-ABI."""
+    z = (seed + (ctr + 1) * 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def gen_range(seed: int, ctr: int, low: float, high: float) -> float:
+    """rand 0.7 ``gen_range(low, high)`` for f64 (UniformFloat::sample_single) on the seeded
+    stream: 52 random bits under exponent 0 → [1, 2) → minus 1 → ``* scale + low``."""
+    bits = (rng_u64(seed, ctr) >> 12) | 0x3FF0000000000000
+    value0_1 = struct.unpack("<d", struct.pack("<Q", bits))[0] - 1.0
+    scale = high - low
+    while True:
+        res = value0_1 * scale + low
+        if res < high:
+            return res
+        scale = math.nextafter(scale, 0.0)
+
+
+def to_radians(deg: float) -> float:
+    """Rust ``f64::to_radians``: ``self * (PI / 180.0)``."""
+    return deg * (math.pi / 180.0)
+
+
+def bench6() -> dict:
+    """benches/all.rs:8-42 (config 1)."""
+    circles = np.array(
+        [[5.0, 5.0, 1.0], [3.0, 6.0, 2.0], [3.0, 8.0, 2.0], [3.0, 10.0, 2.0],
+         [7.0, 5.0, 2.0], [9.0, 5.0, 2.0]], dtype=np.float64)
+    return {
+        "name": "bench6",
+        "bounds": (-6.0, -6.0, 15.0, 15.0),
+        "robot": (1.0, 1.0, 0.8),
+        "circles": circles,
+        "start": (-5.0, -5.0, to_radians(-45.0)),
+        "goal": (6.0, 10.0, to_radians(45.0)),
+        "max_iter": 8000,
+        "step_size": 0.1,
+    }
+
+
+def field512(n_obstacles: int = 1024, seed: int = 1234, size: float = 512.0,
+             r_lo: float = 2.0, r_hi: float = 8.0, robot_width: float = 1.0,
+             turn_radius: float = 4.0, step_size: float = 0.1,
+             start=(8.0, 8.0, 0.0), goal=(504.0, 504.0, math.pi / 2.0),
+             max_iter: int = 2000) -> dict:
+    """BASELINE.json config 2: ``n_obstacles`` discs, centres U(0, size), r ~ U(r_lo, r_hi) from
+    the seeded stream ``seed`` (attempt a draws counters 3a, 3a+1, 3a+2).  Discs whose inflated
+    radius (plus a 1.0 margin) covers the start or the goal are rejected and redrawn."""
+    half = robot_width / 2.0
+    circles = []
+    a = 0
+    while len(circles) < n_obstacles:
+        cx = gen_range(seed, 3 * a, 0.0, size)
+        cy = gen_range(seed, 3 * a + 1, 0.0, size)
+        r = gen_range(seed, 3 * a + 2, r_lo, r_hi)
+        a += 1
+        lim = r + half + 1.0
+        bad = False
+        for (px, py, _) in (start, goal):
+            dx, dy = cx - px, cy - py
+            if dx * dx + dy * dy <= lim * lim:
+                bad = True
+        if not bad:
+            circles.append((cx, cy, r))
+    return {
+        "name": f"field{int(size)}_m{n_obstacles}_s{seed}",
+        "bounds": (0.0, 0.0, size, size),
+        "robot": (robot_width, robot_width, turn_radius),
+        "circles": np.array(circles, dtype=np.float64).reshape(-1, 3),
+        "start": tuple(start),
+        "goal": tuple(goal),
+        "max_iter": max_iter,
+        "step_size": step_size,
+    }
+
+
+def query_endpoints(raw: dict, q: int, seed_base: int = 0):
+    """Config 3: start/goal of query ``q`` drawn from free space by the seeded stream q.
+    Rejection-samples points whose inflated-disc clearance is > 1.0; yaw U(-pi, pi)."""
+    x0, y0, x1, y1 = raw["bounds"]
+    half = raw["robot"][0] / 2.0
+    circ = raw["circles"]
+
+    def free(x, y):
+        d2 = (circ[:, 0] - x) ** 2 + (circ[:, 1] - y) ** 2
+        lim = circ[:, 2] + half + 1.0
+        return bool(np.all(d2 > lim * lim))
+
+    out = []
+    ctr = 0
+    s = seed_base + q
+    while len(out) < 2:
+        x = gen_range(s, ctr, x0 + half + 1.0, x1 - half - 1.0)
+        y = gen_range(s, ctr + 1, y0 + half + 1.0, y1 - half - 1.0)
+        yaw = gen_range(s, ctr + 2, -math.pi, math.pi)
+        ctr += 3
+        if free(x, y):
+            out.append((x, y, yaw))
+    return out[0], out[1]
