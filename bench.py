@@ -1,0 +1,250 @@
+"""RRT extend iterations/s (2D Dubins, 1k obstacles) — BASELINE.json config 2 on MI355X.
+
+A step = one speculative window of K = 4096 extend iterations (sample, exact nearest neighbour,
+Dubins steer, sampled-arc collision check, insert — plan_one minus check_finish) on a tree grown
+beforehand to 100k nodes, with the sequential semantics of the reference (results independent
+of K).  With --gpus N (torchrun), every rank grows its own independent replica tree on its own
+GPU (seed 42 + rank): the path shards by planning query with no data-path collective, so scaling
+is weak and `value` is the iterations of all ranks / the slowest rank's time.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline accounting.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rs-pathplanning_amd"))
+
+F32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, Peak FP32 (vector), spec
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md, HBM3E peak, spec
+FLOP_PER_EVAL = 5             # dx, dy (2 sub), dx*dx (mul), + dy*dy (fma = 2)
+BYTES_PER_EVAL = 8            # f32 x + f32 y of one SoA node
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--window", type=int, default=4096)
+    ap.add_argument("--nodes", type=int, default=100_000, help="tree size before timing")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="bounded CPU-baseline sample per variant (rank 0, N=1 only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-size-sweep", action="store_true")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only: barrier + max-time reduce
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend="gloo", rank=rank, world_size=world)
+    return dist, world, rank, local
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def allreduce_max(dist, v):
+    if dist is None:
+        return v
+    import torch
+
+    t = torch.tensor([float(v)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(dist, v):
+    if dist is None:
+        return v
+    import torch
+
+    t = torch.tensor([float(v)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def make_planner(raw, seed, window, device):
+    from pathplanning_amd import rrt
+
+    sx, sy, syaw = raw["start"]
+    gx, gy, gyaw = raw["goal"]
+    return rrt.RRT((sx, sy), syaw, (gx, gy), gyaw, raw["max_iter"], raw["step_size"],
+                   rrt.Space.from_raw(raw), seed=seed, window=window, device=device,
+                   capacity=1 << 18)
+
+
+def timed_windows(p, n_windows, window):
+    p.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n_windows):
+        p.extend(window)
+    p.synchronize()
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(raw, p, args):
+    """The oracle restatement (oracle/, C, one core) on the SAME workload: continue the GPU's
+    100k-node tree for a bounded, time-capped sample of iterations, (a) re-verifying the whole
+    line to the root like the reference's verify_node (rrt.rs:414-426) and (b) incrementally."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (cpu_baseline leg: the oracle is the timed CPU port here)
+
+    x, y, yaw, par = p.tree()
+    it0 = p.iteration()
+    sc = oracle.OracleScene.from_raw(raw)
+    out = {}
+    for name, full in (("full_reverify", True), ("incremental", False)):
+        tr = oracle.OracleTree(raw["start"], len(x) + 200_000)
+        n = len(x)
+        tr.x[:n], tr.y[:n], tr.yaw[:n], tr.parent[:n] = x, y, yaw, par
+        tr._c.n = n
+        done, chunk, t_used = 0, 1, 0.0
+        while t_used < args.cpu_seconds:
+            t0 = time.perf_counter()
+            oracle.rrt_extend(sc, tr, args.seed, it0 + done, chunk, full_reverify=full)
+            t_used += time.perf_counter() - t0
+            done += chunk
+            chunk = min(chunk * 2, 4096)
+        out[name] = (done / t_used, done, t_used)
+    return out
+
+
+def load_traffic():
+    """HBM bytes per nn_scan launch from the committed rocprofv3 PMC summary (or None)."""
+    path = os.path.join(ROOT, "profiles", "nn_scan_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
+def main():
+    args = parse()
+    dist, world, rank, local = dist_setup(args)
+    from pathplanning_amd import scenes
+
+    raw = scenes.field512()
+    p = make_planner(raw, args.seed + rank, args.window, local)
+    sweep = {}
+    # grow the tree (untimed); on the way time a few windows at 1k and 10k nodes
+    marks = [] if args.no_size_sweep else [1_000, 10_000]
+    while p.tree_size() < args.nodes:
+        if marks and p.tree_size() >= marks[0]:
+            m = marks.pop(0)
+            n0, it0 = p.tree_size(), p.iteration()
+            dt = timed_windows(p, 5, args.window)
+            sweep[str(m)] = {"iterations_per_s": (p.iteration() - it0) / dt, "tree_nodes": n0}
+        p.extend(args.window)
+    for _ in range(args.warmup):
+        p.extend(args.window)
+    p.synchronize()
+
+    n_start = p.tree_size()
+    p.reset_stats()
+    p.set_profiling(True)
+    barrier(dist)
+    p.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        p.extend(args.window)
+    p.synchronize()
+    t_local = time.perf_counter() - t0
+    barrier(dist)
+    p.set_profiling(False)
+    st = p.stats()
+    t_max = allreduce_max(dist, t_local)
+    iters_total = allreduce_sum(dist, st["iterations"])
+    value = iters_total / t_max
+    sweep[str(args.nodes)] = {"iterations_per_s": st["iterations"] / t_local, "tree_nodes": n_start}
+
+    # dominant kernel (nn_scan): algorithmic work per launch / average launch duration (HIP events)
+    launches = max(st["nn_scan_launches"], 1)
+    avg_ms = st["nn_scan_ms"] / launches
+    evals_per_launch = st["node_evals"] / launches
+    achieved_tflops = evals_per_launch * FLOP_PER_EVAL / (avg_ms * 1e-3) / 1e12
+    roofline = {
+        "kernel": "nn_scan",
+        "bound": "valu",
+        "achieved": round(achieved_tflops, 3),
+        "peak": F32_VALU_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved_tflops / F32_VALU_PEAK_TFLOPS, 4),
+        "traffic": load_traffic(),
+        "avg_launch_ms": round(avg_ms, 5),
+        "evals_per_launch": int(evals_per_launch),
+        "algorithmic_hbm_view": {
+            "bytes_per_eval": BYTES_PER_EVAL,
+            "achieved_GBs": round(evals_per_launch * BYTES_PER_EVAL / (avg_ms * 1e-3) / 1e9, 1),
+            "peak_GBs": HBM_PEAK_GBS,
+            "note": "8 B/eval as if every eval read its node from HBM (SURVEY §8d); > peak means "
+                    "the batch reuses each node across 256 samples per wave, so VALU is the bound",
+        },
+        "steer_avg_launch_ms": round(st["steer_ms"] / max(st["steer_launches"], 1), 5),
+    }
+
+    line = {
+        "metric": "RRT extend iterations/sec (2D Dubins, 1k obstacles)",
+        "value": round(value, 1),
+        "unit": "iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * t_max / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": "config2: field512 (1024 discs r~U(2,8), 512x512), R=4.0, step 0.1, "
+                        f"K={args.window} candidates/window, tree grown to {args.nodes} nodes",
+            "window": args.window,
+            "tree_nodes_at_start": n_start,
+            "obstacles": len(raw["circles"]),
+            "parallelism": f"replicas{world}",
+            "nn_screen_dtype": "f32 (exact f64 rescan of near-ties)",
+        },
+        "node_evals_per_s_per_gpu": round(st["node_evals"] / t_local, 1),
+        "sizes": sweep,
+        "stats": {k: st[k] for k in ("iterations", "accepted", "windows", "truncations",
+                                     "repair_rounds", "repairs", "literal_repairs", "nn_flagged")},
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(raw, p, args)
+        v, n, t = cb["full_reverify"]
+        vi, ni, ti = cb["incremental"]
+        line["cpu_baseline"] = {
+            "value": round(v, 2), "unit": "iterations/s", "cores": 1, "kind": "port",
+            "sample": f"{n} iterations continuing the same {n_start}-node tree (seed "
+                      f"{args.seed}), re-verifying the whole line to the root like "
+                      f"rrt.rs:414-426, {t:.1f} s on 1 host core",
+            "incremental_verify": {"value": round(vi, 2), "iterations": ni,
+                                   "seconds": round(ti, 2)},
+        }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    p.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

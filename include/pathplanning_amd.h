@@ -1,0 +1,137 @@
+/*
+ * pathplanning_amd.h — C ABI of the MI355X-native RRT extend hot path.
+ *
+ * Drop-in boundary for tsturzl/rs-pathplanning's `rrt` / `dubins` public API (src/lib.rs:5-6):
+ * a Rust host binds these symbols through a thin `extern "C"` block and keeps
+ * its own types; everything here is plain pointers, sizes and status codes.
+ *
+ * Conventions
+ *   - Every int-returning call returns PP_OK (0) or a negative PP_ERR_* code; no exception or
+ *     panic crosses the boundary.  pp_last_error() gives the calling thread's last message.
+ *   - The caller owns every host buffer; a context owns its device memory and HIP stream.
+ *   - A context is not thread-safe: use one context per host thread (and per GPU).
+ *   - Where the reference returns Option::None the ABI reports it in an output field
+ *     (word = -1, idx = -1, ok = 0), not as an error.
+ *   - The product path is HIP only: every compute call fails with PP_ERR_NO_DEVICE when no
+ *     gfx950 device is present.  There is no CPU fallback.
+ */
+#ifndef PATHPLANNING_AMD_H
+#define PATHPLANNING_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PP_ABI_VERSION 1
+
+#define PP_OK 0
+#define PP_ERR_INVALID_ARGUMENT (-1)
+#define PP_ERR_HIP (-2)
+#define PP_ERR_NO_DEVICE (-3)
+#define PP_ERR_CAPACITY (-4)
+#define PP_ERR_STATE (-5)          /* no scene / no planner configured yet */
+#define PP_ERR_STEER_OVERFLOW (-6) /* generate_local_course would index past n_point (panic) */
+
+typedef struct pp_ctx pp_ctx;
+
+/* DubinsConfig, src/dubins.rs:315-324 (field order and meaning kept) */
+typedef struct pp_dubins_config {
+    double sx, sy, syaw;
+    double ex, ey, eyaw;
+    double turn_radius;
+    double step_size;
+} pp_dubins_config;
+
+/* Counters of the batched extend driver (since pp_rrt_new or the last pp_rrt_reset_stats). */
+typedef struct pp_stats {
+    int64_t iterations;       /* extend iterations consumed (plan_one calls, minus check_finish) */
+    int64_t accepted;         /* nodes inserted */
+    int64_t windows;          /* speculative windows launched */
+    int64_t truncations;      /* windows cut short by an in-window candidate-list overflow */
+    int64_t repair_rounds;    /* extra steer launches for parents that changed inside a window */
+    int64_t repairs;          /* candidates re-steered in those rounds */
+    int64_t literal_repairs;  /* candidates re-run on the literal single-lane path */
+    int64_t nn_flagged;       /* samples whose f32 NN screen needed the exact f64 rescan */
+    int64_t node_evals;       /* sample-node distance evaluations of the NN screen */
+    double nn_scan_ms;        /* device time of nn_scan (HIP events; only when profiling is on) */
+    int64_t nn_scan_launches;
+    double steer_ms;          /* device time of steer_slots (HIP events; profiling on) */
+    int64_t steer_launches;
+} pp_stats;
+
+int pp_abi_version(void);
+const char* pp_last_error(void);
+/* number of visible HIP devices (0 when none); never fails on a CPU-only host */
+int pp_device_count(int* n);
+
+int pp_create(int device, pp_ctx** out);
+int pp_destroy(pp_ctx* ctx);
+int pp_synchronize(pp_ctx* ctx);
+
+/* ------------------------------------------------------------- seeded sampling (host) */
+/* SplitMix64 output `ctr` of stream `seed`: the build's replacement for rand::thread_rng
+ * (src/rrt.rs:140).  Draw 2*it is x, 2*it+1 is y of iteration `it`. */
+uint64_t pp_rng_u64(uint64_t seed, uint64_t ctr);
+/* rand 0.7 gen_range(low, high) for f64 on that stream (src/rrt.rs:142-143) */
+double pp_gen_range(uint64_t seed, uint64_t ctr, double low, double high);
+
+/* --------------------------------------------------------------- dubins (src/dubins.rs) */
+double pp_mod2pi(double theta);   /* dubins.rs:18-20 */
+double pp_pi_2_pi(double angle);  /* dubins.rs:22-24 */
+/* dubins_path_planning (dubins.rs:401-428) for n configurations on the GPU.  Output slot i of
+ * px/py/pyaw is [i*cap, i*cap+cap).  word[i] is the ALL_PLANNERS index (0 LSL, 1 RSR, 2 LSR,
+ * 3 RSL, 4 RLR, 5 LRL) or -1 for None; n_points[i] the kept point count; cost[i] the normalised
+ * cost.  A configuration whose n_point exceeds cap gets word -2 and the call returns
+ * PP_ERR_CAPACITY after filling the others. */
+int pp_dubins_path_planning_batch(pp_ctx* ctx, const pp_dubins_config* confs, int n, int cap,
+                                  double* px, double* py, double* pyaw, int32_t* n_points,
+                                  int32_t* word, double* cost);
+
+/* ------------------------------------------------------------------ scene (src/rrt.rs) */
+/* Space::new(bounds, Robot::new(width, height, max_steer), obstacles) (rrt.rs:25,81-122) with
+ * the bounds an axis-aligned rectangle (x0, y0)-(x1, y1) and the obstacles create_circle discs
+ * (rrt.rs:43-60) given as centres and radii.  Bounds shrink and discs grow by width/2. */
+int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double robot_width,
+                 double robot_height, double max_steer, const double* cx, const double* cy,
+                 const double* r, int m);
+/* the shrunken bounds bbox (minx, maxx, miny, maxy) sampled by Space::rand_point (rrt.rs:84-106) */
+int pp_space_get_bounds(pp_ctx* ctx, double out_minx_maxx_miny_maxy[4]);
+
+/* ----------------------------------------------------------------- planner (src/rrt.rs) */
+/* RRT::new(start, start_yaw, goal, goal_yaw, max_iter, step_size, space) (rrt.rs:335-355) plus
+ * the sampling seed and an initial node capacity (grown on demand). */
+int pp_rrt_new(pp_ctx* ctx, double sx, double sy, double syaw, double gx, double gy, double gyaw,
+               int64_t max_iter, double step_size, uint64_t seed, int64_t capacity);
+/* candidates per speculative window (K; default 4096).  Results do not depend on K. */
+int pp_rrt_set_window(pp_ctx* ctx, int k);
+/* n_iter iterations of plan_one's extend (rrt.rs:583-589: rand_point, get_nearest_node,
+ * Node::new, verify_node, insert) with the sequential semantics of one rayon thread. */
+int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted);
+/* one plan_one extend (rrt.rs:583-589); *accepted = 1 when the node was inserted */
+int pp_rrt_plan_one(pp_ctx* ctx, int32_t* accepted);
+int pp_rrt_tree_size(pp_ctx* ctx, int64_t* n);
+int pp_rrt_iteration(pp_ctx* ctx, int64_t* it);
+/* copy the tree out (root first): coordinates, yaw (Node.yaw, rrt.rs:161-166), parent (-1 root) */
+int pp_rrt_tree_export(pp_ctx* ctx, double* x, double* y, double* yaw, int32_t* parent,
+                       int64_t cap, int64_t* n);
+/* RRT::get_nearest_node (rrt.rs:378-391) for k points: exact nearest by dx*dx+dy*dy, lowest
+ * index on ties; d2 may be NULL */
+int pp_rrt_get_nearest_node_batch(pp_ctx* ctx, const double* qx, const double* qy, int k,
+                                  int32_t* idx, double* d2);
+/* RRT::verify_node(Node::new(point, tree[parent])) (rrt.rs:169-175, 414-426) for k candidates:
+ * ok[i] = 1 when the line to the root verifies; yaw[i] = the new node's yaw (may be NULL) */
+int pp_rrt_verify_node_batch(pp_ctx* ctx, const double* x, const double* y,
+                             const int32_t* parent, int k, uint8_t* ok, double* yaw);
+
+int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out);
+int pp_rrt_reset_stats(pp_ctx* ctx);
+/* record HIP events around the hot kernels (adds a little host overhead per window) */
+int pp_set_profiling(pp_ctx* ctx, int enabled);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PATHPLANNING_AMD_H */

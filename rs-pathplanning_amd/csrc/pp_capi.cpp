@@ -1,0 +1,839 @@
+// pp_capi.cpp — host side of the MI355X RRT extend path: context, scene, device-resident tree,
+// the speculative window driver with its sequential-consistency resolve, and the C ABI
+// (include/pathplanning_amd.h).
+//
+// Extend semantics: iteration it samples (x, y) from the seeded stream, takes
+// the exact nearest node of the tree as it stands after iterations < it, steers child→parent with
+// Dubins, verifies, inserts.  The GPU evaluates a window of K iterations against the tree
+// snapshot at the window start; the host then replays the window in order:
+//   * sample j's true parent is the nearest of {snapshot NN} ∪ {accepted window samples i < j};
+//     window_pairs lists the i that are strictly nearer than the snapshot NN, so the parent is
+//     the first accepted entry of that list in (d2, i) order, or the snapshot NN;
+//   * the verdict for (j, parent) was precomputed for the snapshot NN and for every listed i
+//     under i's own snapshot parent; only a parent that itself changed needs a repair launch.
+// The result is identical to the one-at-a-time sequential spec for every K.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pathplanning_amd.h"
+#include "pp_device.h"
+#include "pp_kernels.h"
+
+using namespace ppamd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define PP_HIP(expr)                                                                         \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return set_err(PP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+template <typename T>
+struct DBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t reserve(size_t count) {
+        if (count <= n) return hipSuccess;
+        release();
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1) * sizeof(T));
+        if (e == hipSuccess) n = count;
+        else p = nullptr;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    ~DBuf() { release(); }
+};
+
+template <typename T>
+struct HBuf {  // pinned host staging
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t reserve(size_t count) {
+        if (count <= n) return hipSuccess;
+        release();
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1) * sizeof(T),
+                                     hipHostMallocDefault);
+        if (e == hipSuccess) n = count;
+        else p = nullptr;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    ~HBuf() { release(); }
+};
+
+constexpr int kPrefetch = 1024;  // candidate entries copied back with the first batch
+
+}  // namespace
+
+struct pp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+
+    // ---- scene (Space)
+    bool has_scene = false;
+    double minx = 0, maxx = 0, miny = 0, maxy = 0;
+    double width = 0, height = 0, max_steer = 0;
+    int m = 0;
+    DBuf<double> d_cx, d_cy, d_r2, d_rcull;
+
+    // ---- planner (RRT)
+    bool has_rrt = false;
+    double start[3] = {0, 0, 0}, goal[3] = {0, 0, 0};
+    int64_t max_iter = 0;
+    double step = 0.1;
+    uint64_t seed = 0;
+    int64_t it = 0;    // next iteration index (RNG counter base)
+    int64_t n = 0;     // tree nodes
+    int64_t cap = 0;   // tree capacity
+    double eps_coord = 0.0;
+    DBuf<float> x32, y32;
+    DBuf<double> X, Y, YAW;
+    DBuf<int> PAR;
+
+    // ---- window buffers
+    int K = 4096;
+    int Kcap = 0;
+    DBuf<double> wsx, wsy;
+    DBuf<float> pbest, psecond;
+    DBuf<int> pidx;
+    DBuf<int> nn_idx;
+    DBuf<double> nn_d2;
+    DBuf<int> flag_list;
+    DBuf<int> counters;  // [0] nn flagged, [1] candidate entries
+    DBuf<int> cand_cnt;
+    DBuf<CandEntry> cand;
+    DBuf<int> snap_status, spec_status, task_status;
+    DBuf<double> snap_yaw, spec_yaw, task_yaw;
+    DBuf<SteerTask> tasks;
+    DBuf<double> lit_scratch;
+    DBuf<CommitEntry> commits;
+
+    HBuf<int> h_counters, h_cand_cnt, h_nn_idx, h_snap_status, h_spec_status, h_task_status;
+    HBuf<double> h_snap_yaw, h_spec_yaw, h_task_yaw, h_d2;
+    HBuf<CandEntry> h_cand;
+    HBuf<SteerTask> h_tasks;
+    HBuf<CommitEntry> h_commits;
+
+    // ---- stats / profiling
+    pp_stats stats{};
+    bool prof = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+
+    ~pp_ctx() {
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    SceneDev scene_dev() const {
+        SceneDev s;
+        s.minx = minx;
+        s.maxx = maxx;
+        s.miny = miny;
+        s.maxy = maxy;
+        s.turn_radius = max_steer;
+        s.step_size = step;
+        s.m = m;
+        s.cx = d_cx.p;
+        s.cy = d_cy.p;
+        s.r2 = d_r2.p;
+        s.rcull = d_rcull.p;
+        return s;
+    }
+    TreeDev tree_dev() const {
+        TreeDev t;
+        t.x32 = x32.p;
+        t.y32 = y32.p;
+        t.x = X.p;
+        t.y = Y.p;
+        t.yaw = YAW.p;
+        t.n = (int)n;
+        return t;
+    }
+};
+
+namespace {
+
+int check_ctx(pp_ctx* c, bool need_scene, bool need_rrt) {
+    if (!c) return set_err(PP_ERR_INVALID_ARGUMENT, "null context");
+    if (need_scene && !c->has_scene) return set_err(PP_ERR_STATE, "pp_space_new has not been called");
+    if (need_rrt && !c->has_rrt) return set_err(PP_ERR_STATE, "pp_rrt_new has not been called");
+    PP_HIP(hipSetDevice(c->device));
+    return PP_OK;
+}
+
+int ensure_window(pp_ctx* c, int K) {
+    if (K <= c->Kcap) return PP_OK;
+    const size_t k = (size_t)K;
+    PP_HIP(c->wsx.reserve(k));
+    PP_HIP(c->wsy.reserve(k));
+    PP_HIP(c->pbest.reserve(k * kMaxChunks));
+    PP_HIP(c->psecond.reserve(k * kMaxChunks));
+    PP_HIP(c->pidx.reserve(k * kMaxChunks));
+    PP_HIP(c->nn_idx.reserve(k));
+    PP_HIP(c->nn_d2.reserve(k));
+    PP_HIP(c->flag_list.reserve(k));
+    PP_HIP(c->counters.reserve(2));
+    PP_HIP(c->cand_cnt.reserve(k));
+    PP_HIP(c->cand.reserve(k * kCandCap));
+    PP_HIP(c->snap_status.reserve(k));
+    PP_HIP(c->snap_yaw.reserve(k));
+    PP_HIP(c->spec_status.reserve(k * kCandCap));
+    PP_HIP(c->spec_yaw.reserve(k * kCandCap));
+    PP_HIP(c->tasks.reserve(k));
+    PP_HIP(c->task_status.reserve(k));
+    PP_HIP(c->task_yaw.reserve(k));
+    PP_HIP(c->commits.reserve(k));
+    PP_HIP(c->h_counters.reserve(2));
+    PP_HIP(c->h_cand_cnt.reserve(k));
+    PP_HIP(c->h_nn_idx.reserve(k));
+    PP_HIP(c->h_snap_status.reserve(k));
+    PP_HIP(c->h_snap_yaw.reserve(k));
+    PP_HIP(c->h_d2.reserve(k));
+    PP_HIP(c->h_cand.reserve(k * kCandCap));
+    PP_HIP(c->h_spec_status.reserve(k * kCandCap));
+    PP_HIP(c->h_spec_yaw.reserve(k * kCandCap));
+    PP_HIP(c->h_tasks.reserve(k));
+    PP_HIP(c->h_task_status.reserve(k));
+    PP_HIP(c->h_task_yaw.reserve(k));
+    PP_HIP(c->h_commits.reserve(k));
+    c->Kcap = K;
+    return PP_OK;
+}
+
+template <typename T>
+int grow_copy(pp_ctx* c, DBuf<T>& b, size_t old_n, size_t new_cap) {
+    DBuf<T> nb;
+    PP_HIP(nb.reserve(new_cap));
+    if (old_n)
+        PP_HIP(hipMemcpyAsync(nb.p, b.p, old_n * sizeof(T), hipMemcpyDeviceToDevice, c->stream));
+    PP_HIP(hipStreamSynchronize(c->stream));
+    std::swap(b.p, nb.p);
+    std::swap(b.n, nb.n);
+    return PP_OK;
+}
+
+int ensure_tree(pp_ctx* c, int64_t need) {
+    if (need <= c->cap) return PP_OK;
+    int64_t nc = std::max<int64_t>(need, c->cap * 2);
+    nc = std::max<int64_t>(nc, 1024);
+    int r;
+    if ((r = grow_copy(c, c->x32, c->n, nc))) return r;
+    if ((r = grow_copy(c, c->y32, c->n, nc))) return r;
+    if ((r = grow_copy(c, c->X, c->n, nc))) return r;
+    if ((r = grow_copy(c, c->Y, c->n, nc))) return r;
+    if ((r = grow_copy(c, c->YAW, c->n, nc))) return r;
+    if ((r = grow_copy(c, c->PAR, c->n, nc))) return r;
+    c->cap = nc;
+    return PP_OK;
+}
+
+int ensure_literal_scratch(pp_ctx* c) {
+    PP_HIP(c->lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
+    return PP_OK;
+}
+
+double sample_x(const pp_ctx* c, int64_t it) {
+    return gen_range(c->seed, 2 * (uint64_t)it, c->minx, c->maxx);
+}
+double sample_y(const pp_ctx* c, int64_t it) {
+    return gen_range(c->seed, 2 * (uint64_t)it + 1, c->miny, c->maxy);
+}
+
+// One speculative window of W iterations starting at c->it.  Consumes W_eff <= W iterations.
+int run_window(pp_ctx* c, int W, int64_t* consumed, int64_t* accepted) {
+    int r;
+    if ((r = ensure_window(c, std::max(W, c->K)))) return r;
+    if ((r = ensure_tree(c, c->n + W))) return r;
+    hipStream_t st = c->stream;
+    const SceneDev sc = c->scene_dev();
+    const TreeDev tr = c->tree_dev();
+
+    PP_HIP(launch_sample(st, c->seed, c->it, W, c->minx, c->maxx, c->miny, c->maxy, c->wsx.p,
+                         c->wsy.p));
+    PP_HIP(launch_nn(st, tr, c->wsx.p, c->wsy.p, W, c->Kcap, c->pbest.p, c->psecond.p, c->pidx.p,
+                     c->eps_coord, c->nn_idx.p, c->nn_d2.p, c->flag_list.p, c->counters.p,
+                     c->prof ? c->ev[0] : nullptr, c->prof ? c->ev[1] : nullptr));
+    PP_HIP(launch_pairs(st, c->wsx.p, c->wsy.p, c->nn_d2.p, W, c->cand_cnt.p, c->cand.p,
+                        c->counters.p + 1));
+    if (c->prof) PP_HIP(hipEventRecord(c->ev[2], st));
+    PP_HIP(launch_steer_window(st, sc, tr, c->wsx.p, c->wsy.p, c->nn_idx.p, c->cand.p,
+                               c->counters.p + 1, W, c->snap_status.p, c->snap_yaw.p,
+                               c->spec_status.p, c->spec_yaw.p));
+    if (c->prof) PP_HIP(hipEventRecord(c->ev[3], st));
+    const size_t w = (size_t)W;
+    PP_HIP(hipMemcpyAsync(c->h_counters.p, c->counters.p, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(c->h_cand_cnt.p, c->cand_cnt.p, w * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(c->h_nn_idx.p, c->nn_idx.p, w * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(c->h_snap_status.p, c->snap_status.p, w * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(c->h_snap_yaw.p, c->snap_yaw.p, w * sizeof(double), hipMemcpyDeviceToHost, st));
+    const size_t pre = std::min<size_t>(kPrefetch, w * kCandCap);
+    PP_HIP(hipMemcpyAsync(c->h_cand.p, c->cand.p, pre * sizeof(CandEntry), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(c->h_spec_status.p, c->spec_status.p, pre * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(c->h_spec_yaw.p, c->spec_yaw.p, pre * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    const int nflag = c->h_counters.p[0];
+    const int ncomp = c->h_counters.p[1];
+    if ((size_t)ncomp > pre) {
+        const size_t rest = (size_t)ncomp - pre;
+        PP_HIP(hipMemcpyAsync(c->h_cand.p + pre, c->cand.p + pre, rest * sizeof(CandEntry), hipMemcpyDeviceToHost, st));
+        PP_HIP(hipMemcpyAsync(c->h_spec_status.p + pre, c->spec_status.p + pre, rest * sizeof(int), hipMemcpyDeviceToHost, st));
+        PP_HIP(hipMemcpyAsync(c->h_spec_yaw.p + pre, c->spec_yaw.p + pre, rest * sizeof(double), hipMemcpyDeviceToHost, st));
+        PP_HIP(hipStreamSynchronize(st));
+    }
+    c->stats.windows++;
+    c->stats.nn_flagged += nflag;
+    c->stats.node_evals += (int64_t)W * c->n;
+    if (c->prof) {
+        float ms = 0.f;
+        PP_HIP(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        c->stats.nn_scan_ms += ms;
+        c->stats.nn_scan_launches++;
+        PP_HIP(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+        c->stats.steer_ms += ms;
+        c->stats.steer_launches++;
+    }
+
+    // ---- group candidate entries per sample, each list in (d2, i) order
+    const CandEntry* E = c->h_cand.p;
+    std::vector<int> off(w + 1, 0), order(ncomp);
+    for (int e = 0; e < ncomp; ++e) off[E[e].j + 1]++;
+    for (size_t j = 0; j < w; ++j) off[j + 1] += off[j];
+    {
+        std::vector<int> fill(off.begin(), off.end() - 1);
+        for (int e = 0; e < ncomp; ++e) order[fill[E[e].j]++] = e;
+    }
+    for (size_t j = 0; j < w; ++j)
+        if (off[j + 1] - off[j] > 1)
+            std::sort(order.begin() + off[j], order.begin() + off[j + 1], [&](int a, int b) {
+                if (E[a].d2 != E[b].d2) return E[a].d2 < E[b].d2;
+                return E[a].i < E[b].i;
+            });
+
+    // ---- sequential-consistency resolve
+    std::vector<int8_t> state(w, 0);  // 0 unresolved, 1 accepted, 2 rejected
+    std::vector<int> par_win(w, -1);  // -1: the snapshot NN, else the window sample index
+    std::vector<double> yaw(w, 0.0);
+    std::vector<int8_t> rep_have(w, 0), rep_lit(w, 0);
+    std::vector<int> rep_status(w, 0);
+    std::vector<double> rep_yaw(w, 0.0);
+    int W_eff = W;
+    std::vector<int> need_j, need_par;
+    std::vector<int8_t> need_lit;
+    for (;;) {
+        need_j.clear();
+        need_par.clear();
+        need_lit.clear();
+        for (int j = 0; j < W_eff; ++j) {
+            if (state[j]) continue;
+            if (c->h_cand_cnt.p[j] > kCandCap) {  // list incomplete: stop the window here
+                W_eff = j;
+                c->stats.truncations++;
+                break;
+            }
+            int parent = -1, slot = -1;
+            bool blocked = false;
+            for (int q = off[j]; q < off[j + 1]; ++q) {
+                const int e = order[q];
+                const int i = E[e].i;
+                if (state[i] == 1) {
+                    parent = i;
+                    slot = e;
+                    break;
+                }
+                if (state[i] == 0) {
+                    blocked = true;
+                    break;
+                }
+            }
+            if (blocked) continue;
+            int status = -1;
+            double y = 0.0;
+            if (rep_have[j]) {
+                status = rep_status[j];
+                y = rep_yaw[j];
+            } else if (parent < 0) {
+                status = c->h_snap_status.p[j];
+                y = c->h_snap_yaw.p[j];
+            } else if (par_win[parent] < 0) {
+                status = c->h_spec_status.p[slot];
+                y = c->h_spec_yaw.p[slot];
+            }
+            if (status < 0) {
+                need_j.push_back(j);
+                need_par.push_back(parent);
+                need_lit.push_back(0);
+                continue;
+            }
+            if (status == kLiteral) {
+                if (rep_lit[j]) return set_err(PP_ERR_HIP, "literal steer path returned kLiteral");
+                need_j.push_back(j);
+                need_par.push_back(parent);
+                need_lit.push_back(1);
+                continue;
+            }
+            if (status == kError)
+                return set_err(PP_ERR_STEER_OVERFLOW,
+                               "generate_local_course would index past n_point (the reference panics)");
+            state[j] = status == kAccept ? 1 : 2;
+            par_win[j] = parent;
+            yaw[j] = y;
+        }
+        if (need_j.empty()) break;
+        // repair launch: (child j, its final parent) with the parent's true pose
+        const int nt = (int)need_j.size();
+        bool any_lit = false;
+        for (int t = 0; t < nt; ++t) {
+            const int j = need_j[t], p = need_par[t];
+            SteerTask tk;
+            tk.x = sample_x(c, c->it + j);
+            tk.y = sample_y(c, c->it + j);
+            if (p < 0) {
+                tk.pnode = c->h_nn_idx.p[j];
+                tk.px = tk.py = tk.pyaw = 0.0;
+            } else {
+                tk.pnode = -1;
+                tk.px = sample_x(c, c->it + p);
+                tk.py = sample_y(c, c->it + p);
+                tk.pyaw = yaw[p];
+            }
+            tk.literal = need_lit[t];
+            any_lit |= tk.literal != 0;
+            c->h_tasks.p[t] = tk;
+        }
+        if (any_lit && (r = ensure_literal_scratch(c))) return r;
+        PP_HIP(hipMemcpyAsync(c->tasks.p, c->h_tasks.p, nt * sizeof(SteerTask), hipMemcpyHostToDevice, st));
+        PP_HIP(launch_steer_tasks(st, sc, tr, c->tasks.p, nt, c->task_status.p, c->task_yaw.p,
+                                  any_lit ? c->lit_scratch.p : nullptr));
+        PP_HIP(hipMemcpyAsync(c->h_task_status.p, c->task_status.p, nt * sizeof(int), hipMemcpyDeviceToHost, st));
+        PP_HIP(hipMemcpyAsync(c->h_task_yaw.p, c->task_yaw.p, nt * sizeof(double), hipMemcpyDeviceToHost, st));
+        PP_HIP(hipStreamSynchronize(st));
+        for (int t = 0; t < nt; ++t) {
+            const int j = need_j[t];
+            rep_have[j] = 1;
+            rep_status[j] = c->h_task_status.p[t];
+            rep_yaw[j] = c->h_task_yaw.p[t];
+            if (need_lit[t]) rep_lit[j] = 1;
+        }
+        c->stats.repair_rounds++;
+        c->stats.repairs += nt;
+        for (int t = 0; t < nt; ++t) c->stats.literal_repairs += need_lit[t];
+    }
+
+    // ---- commit: insert the accepted samples in sequential order (rrt.rs:586-589)
+    std::vector<int> node_of(W_eff, -1);
+    int nnew = 0;
+    for (int j = 0; j < W_eff; ++j) {
+        if (state[j] != 1) continue;
+        node_of[j] = (int)c->n + nnew;
+        CommitEntry ce;
+        ce.j = j;
+        ce.parent = par_win[j] < 0 ? -1 : node_of[par_win[j]];
+        ce.yaw = yaw[j];
+        c->h_commits.p[nnew++] = ce;
+    }
+    if (nnew) {
+        PP_HIP(hipMemcpyAsync(c->commits.p, c->h_commits.p, nnew * sizeof(CommitEntry), hipMemcpyHostToDevice, st));
+        PP_HIP(launch_append(st, c->commits.p, nnew, (int)c->n, c->wsx.p, c->wsy.p, c->nn_idx.p,
+                             c->x32.p, c->y32.p, c->X.p, c->Y.p, c->YAW.p, c->PAR.p));
+        // the pinned commit buffer is rewritten by the next window: wait for the copy
+        PP_HIP(hipStreamSynchronize(st));
+    }
+    c->n += nnew;
+    c->it += W_eff;
+    c->stats.iterations += W_eff;
+    c->stats.accepted += nnew;
+    *consumed = W_eff;
+    *accepted = nnew;
+    return PP_OK;
+}
+
+}  // namespace
+
+// ===================================================================================== C ABI
+
+extern "C" {
+
+int pp_abi_version(void) { return PP_ABI_VERSION; }
+
+const char* pp_last_error(void) { return g_err.c_str(); }
+
+int pp_device_count(int* n) {
+    if (!n) return set_err(PP_ERR_INVALID_ARGUMENT, "null output");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return PP_OK;
+}
+
+int pp_create(int device, pp_ctx** out) {
+    if (!out) return set_err(PP_ERR_INVALID_ARGUMENT, "null output");
+    *out = nullptr;
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0)
+        return set_err(PP_ERR_NO_DEVICE, "no HIP device visible (the product path has no CPU fallback)");
+    if (device < 0 || device >= cnt) return set_err(PP_ERR_INVALID_ARGUMENT, "device index out of range");
+    PP_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    PP_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_err(PP_ERR_NO_DEVICE, std::string("built for gfx950, device is ") + prop.gcnArchName);
+    pp_ctx* c = new pp_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+    if (e != hipSuccess) {
+        delete c;
+        return set_err(PP_ERR_HIP, std::string("stream/event create: ") + hipGetErrorString(e));
+    }
+    *out = c;
+    return PP_OK;
+}
+
+int pp_destroy(pp_ctx* ctx) {
+    if (!ctx) return PP_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    delete ctx;
+    return PP_OK;
+}
+
+int pp_synchronize(pp_ctx* ctx) {
+    int r = check_ctx(ctx, false, false);
+    if (r) return r;
+    PP_HIP(hipStreamSynchronize(ctx->stream));
+    return PP_OK;
+}
+
+uint64_t pp_rng_u64(uint64_t seed, uint64_t ctr) { return rng_u64(seed, ctr); }
+
+double pp_gen_range(uint64_t seed, uint64_t ctr, double low, double high) {
+    return gen_range(seed, ctr, low, high);
+}
+
+double pp_mod2pi(double theta) { return mod2pi(theta); }
+
+double pp_pi_2_pi(double angle) { return pi_2_pi(angle); }
+
+int pp_dubins_path_planning_batch(pp_ctx* ctx, const pp_dubins_config* confs, int n, int cap,
+                                  double* px, double* py, double* pyaw, int32_t* n_points,
+                                  int32_t* word, double* cost) {
+    int r = check_ctx(ctx, false, false);
+    if (r) return r;
+    if (n < 0 || cap <= 0 || (n > 0 && (!confs || !px || !py || !pyaw || !n_points || !word || !cost)))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad dubins batch arguments");
+    if (n == 0) return PP_OK;
+    for (int i = 0; i < n; ++i)
+        if (!(confs[i].turn_radius > 0.0) || !(confs[i].step_size > 0.0))
+            return set_err(PP_ERR_INVALID_ARGUMENT, "turn_radius and step_size must be > 0");
+    static_assert(sizeof(pp_dubins_config) == 8 * sizeof(double), "DubinsConfig layout");
+    const size_t nn = (size_t)n, tot = nn * (size_t)cap;
+    DBuf<double> dconf, dpx, dpy, dpyaw, dcost;
+    DBuf<int> dn, dword, dstat;
+    PP_HIP(dconf.reserve(nn * 8));
+    PP_HIP(dpx.reserve(tot));
+    PP_HIP(dpy.reserve(tot));
+    PP_HIP(dpyaw.reserve(tot));
+    PP_HIP(dcost.reserve(nn));
+    PP_HIP(dn.reserve(nn));
+    PP_HIP(dword.reserve(nn));
+    PP_HIP(dstat.reserve(nn));
+    hipStream_t st = ctx->stream;
+    PP_HIP(hipMemcpyAsync(dconf.p, confs, nn * 8 * sizeof(double), hipMemcpyHostToDevice, st));
+    PP_HIP(launch_dubins_batch(st, dconf.p, n, cap, dpx.p, dpy.p, dpyaw.p, dn.p, dword.p, dcost.p, dstat.p));
+    std::vector<int> stat(nn), nv(nn), wv(nn);
+    PP_HIP(hipMemcpyAsync(px, dpx.p, tot * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(py, dpy.p, tot * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(pyaw, dpyaw.p, tot * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(cost, dcost.p, nn * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(nv.data(), dn.p, nn * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(wv.data(), dword.p, nn * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(stat.data(), dstat.p, nn * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    bool overflow = false;
+    for (size_t i = 0; i < nn; ++i) {
+        if (stat[i] == kSteerOverflow) {
+            overflow = true;
+            word[i] = -2;
+            n_points[i] = 0;
+        } else if (stat[i] == kSteerNone) {
+            word[i] = -1;
+            n_points[i] = 0;
+        } else {
+            word[i] = wv[i];
+            n_points[i] = nv[i];
+        }
+    }
+    if (overflow) return set_err(PP_ERR_CAPACITY, "a configuration needs more than cap points");
+    return PP_OK;
+}
+
+int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double robot_width,
+                 double robot_height, double max_steer, const double* cx, const double* cy,
+                 const double* r, int m) {
+    int rc = check_ctx(ctx, false, false);
+    if (rc) return rc;
+    if (m < 0 || (m > 0 && (!cx || !cy || !r)))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad obstacle arrays");
+    if (!(robot_width >= 0.0) || !(max_steer > 0.0))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "robot width must be >= 0 and max_steer > 0");
+    // Space::new, rrt.rs:82-111: bounds offset by -width/2, obstacles by +width/2
+    const double half = robot_width / 2.0;
+    const double minx = x0 + half, maxx = x1 - half, miny = y0 + half, maxy = y1 - half;
+    if (!(minx < maxx) || !(miny < maxy))  // gen_range asserts low < high (rrt.rs:142-143)
+        return set_err(PP_ERR_INVALID_ARGUMENT, "shrunken bounds are empty");
+    std::vector<double> r2(m), rc_(m);
+    for (int k = 0; k < m; ++k) {
+        const double reff = r[k] + half;
+        r2[k] = reff * reff;
+        rc_[k] = reff * (1.0 + 1e-9) + 1e-9;
+    }
+    const size_t mm = (size_t)std::max(m, 1);
+    PP_HIP(ctx->d_cx.reserve(mm));
+    PP_HIP(ctx->d_cy.reserve(mm));
+    PP_HIP(ctx->d_r2.reserve(mm));
+    PP_HIP(ctx->d_rcull.reserve(mm));
+    if (m > 0) {
+        PP_HIP(hipMemcpy(ctx->d_cx.p, cx, m * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_cy.p, cy, m * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_r2.p, r2.data(), m * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_rcull.p, rc_.data(), m * sizeof(double), hipMemcpyHostToDevice));
+    }
+    ctx->minx = minx;
+    ctx->maxx = maxx;
+    ctx->miny = miny;
+    ctx->maxy = maxy;
+    ctx->width = robot_width;
+    ctx->height = robot_height;
+    ctx->max_steer = max_steer;
+    ctx->m = m;
+    ctx->has_scene = true;
+    ctx->has_rrt = false;  // a planner belongs to one Space (RRT::new moves it in, rrt.rs:342)
+    return PP_OK;
+}
+
+int pp_space_get_bounds(pp_ctx* ctx, double out[4]) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (!out) return set_err(PP_ERR_INVALID_ARGUMENT, "null output");
+    out[0] = ctx->minx;
+    out[1] = ctx->maxx;
+    out[2] = ctx->miny;
+    out[3] = ctx->maxy;
+    return PP_OK;
+}
+
+int pp_rrt_new(pp_ctx* ctx, double sx, double sy, double syaw, double gx, double gy, double gyaw,
+               int64_t max_iter, double step_size, uint64_t seed, int64_t capacity) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (!(step_size > 0.0) || max_iter < 0)
+        return set_err(PP_ERR_INVALID_ARGUMENT, "step_size must be > 0 and max_iter >= 0");
+    ctx->has_rrt = false;
+    ctx->n = 0;
+    ctx->it = 0;
+    ctx->start[0] = sx;
+    ctx->start[1] = sy;
+    ctx->start[2] = syaw;
+    ctx->goal[0] = gx;
+    ctx->goal[1] = gy;
+    ctx->goal[2] = gyaw;
+    ctx->max_iter = max_iter;
+    ctx->step = step_size;
+    ctx->seed = seed;
+    ctx->stats = pp_stats{};
+    if ((r = ensure_tree(ctx, std::max<int64_t>(capacity, 1024)))) return r;
+    // f32 screen tolerance: coordinates are rounded to f32 with error <= max|c| * 2^-24
+    double mx = std::max({std::fabs(ctx->minx), std::fabs(ctx->maxx), std::fabs(ctx->miny),
+                          std::fabs(ctx->maxy), std::fabs(sx), std::fabs(sy)});
+    ctx->eps_coord = mx * std::ldexp(1.0, -23);
+    // RRT::new inserts the root (rrt.rs:344-346)
+    const float fx = (float)sx, fy = (float)sy;
+    const int par = -1;
+    PP_HIP(hipMemcpy(ctx->x32.p, &fx, sizeof(float), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->y32.p, &fy, sizeof(float), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->X.p, &sx, sizeof(double), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->Y.p, &sy, sizeof(double), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->YAW.p, &syaw, sizeof(double), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->PAR.p, &par, sizeof(int), hipMemcpyHostToDevice));
+    ctx->n = 1;
+    if ((r = ensure_window(ctx, ctx->K))) return r;
+    ctx->has_rrt = true;
+    return PP_OK;
+}
+
+int pp_rrt_set_window(pp_ctx* ctx, int k) {
+    if (!ctx) return set_err(PP_ERR_INVALID_ARGUMENT, "null context");
+    if (k < 1 || k > (1 << 20)) return set_err(PP_ERR_INVALID_ARGUMENT, "window must be in [1, 2^20]");
+    ctx->K = k;
+    return PP_OK;
+}
+
+int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (n_iter < 0) return set_err(PP_ERR_INVALID_ARGUMENT, "n_iter < 0");
+    int64_t acc_total = 0, left = n_iter;
+    while (left > 0) {
+        const int W = (int)std::min<int64_t>(left, ctx->K);
+        int64_t used = 0, acc = 0;
+        if ((r = run_window(ctx, W, &used, &acc))) return r;
+        left -= used;
+        acc_total += acc;
+    }
+    if (n_accepted) *n_accepted = acc_total;
+    return PP_OK;
+}
+
+int pp_rrt_plan_one(pp_ctx* ctx, int32_t* accepted) {
+    int64_t acc = 0;
+    int r = pp_rrt_extend(ctx, 1, &acc);
+    if (r) return r;
+    if (accepted) *accepted = (int32_t)acc;
+    return PP_OK;
+}
+
+int pp_rrt_tree_size(pp_ctx* ctx, int64_t* n) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (!n) return set_err(PP_ERR_INVALID_ARGUMENT, "null output");
+    *n = ctx->n;
+    return PP_OK;
+}
+
+int pp_rrt_iteration(pp_ctx* ctx, int64_t* it) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (!it) return set_err(PP_ERR_INVALID_ARGUMENT, "null output");
+    *it = ctx->it;
+    return PP_OK;
+}
+
+int pp_rrt_tree_export(pp_ctx* ctx, double* x, double* y, double* yaw, int32_t* parent,
+                       int64_t cap, int64_t* n) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (n) *n = ctx->n;
+    if (cap < ctx->n) return set_err(PP_ERR_CAPACITY, "export buffer smaller than the tree");
+    const size_t k = (size_t)ctx->n;
+    hipStream_t st = ctx->stream;
+    if (x) PP_HIP(hipMemcpyAsync(x, ctx->X.p, k * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (y) PP_HIP(hipMemcpyAsync(y, ctx->Y.p, k * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (yaw) PP_HIP(hipMemcpyAsync(yaw, ctx->YAW.p, k * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (parent) PP_HIP(hipMemcpyAsync(parent, ctx->PAR.p, k * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    return PP_OK;
+}
+
+int pp_rrt_get_nearest_node_batch(pp_ctx* ctx, const double* qx, const double* qy, int k,
+                                  int32_t* idx, double* d2) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (k < 0 || (k > 0 && (!qx || !qy || !idx))) return set_err(PP_ERR_INVALID_ARGUMENT, "bad arguments");
+    hipStream_t st = ctx->stream;
+    const TreeDev tr = ctx->tree_dev();
+    for (int b = 0; b < k; b += ctx->Kcap) {
+        const int nb = std::min(ctx->Kcap, k - b);
+        PP_HIP(hipMemcpyAsync(ctx->wsx.p, qx + b, nb * sizeof(double), hipMemcpyHostToDevice, st));
+        PP_HIP(hipMemcpyAsync(ctx->wsy.p, qy + b, nb * sizeof(double), hipMemcpyHostToDevice, st));
+        PP_HIP(launch_nn(st, tr, ctx->wsx.p, ctx->wsy.p, nb, ctx->Kcap, ctx->pbest.p,
+                         ctx->psecond.p, ctx->pidx.p, ctx->eps_coord, ctx->nn_idx.p, ctx->nn_d2.p,
+                         ctx->flag_list.p, ctx->counters.p, nullptr, nullptr));
+        PP_HIP(hipMemcpyAsync(idx + b, ctx->nn_idx.p, nb * sizeof(int), hipMemcpyDeviceToHost, st));
+        if (d2) PP_HIP(hipMemcpyAsync(d2 + b, ctx->nn_d2.p, nb * sizeof(double), hipMemcpyDeviceToHost, st));
+        PP_HIP(hipStreamSynchronize(st));
+    }
+    return PP_OK;
+}
+
+int pp_rrt_verify_node_batch(pp_ctx* ctx, const double* x, const double* y,
+                             const int32_t* parent, int k, uint8_t* ok, double* yaw) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (k < 0 || (k > 0 && (!x || !y || !parent || !ok))) return set_err(PP_ERR_INVALID_ARGUMENT, "bad arguments");
+    for (int i = 0; i < k; ++i)
+        if (parent[i] < 0 || parent[i] >= ctx->n)
+            return set_err(PP_ERR_INVALID_ARGUMENT, "parent index outside the tree");
+    hipStream_t st = ctx->stream;
+    const SceneDev sc = ctx->scene_dev();
+    const TreeDev tr = ctx->tree_dev();
+    for (int b = 0; b < k; b += ctx->Kcap) {
+        const int nb = std::min(ctx->Kcap, k - b);
+        for (int pass = 0; pass < 2; ++pass) {
+            int nt = 0;
+            std::vector<int> which;
+            for (int i = 0; i < nb; ++i) {
+                if (pass == 1 && ctx->h_task_status.p[i] != kLiteral) continue;
+                SteerTask tk;
+                tk.x = x[b + i];
+                tk.y = y[b + i];
+                tk.px = tk.py = tk.pyaw = 0.0;
+                tk.pnode = parent[b + i];
+                tk.literal = pass;
+                ctx->h_tasks.p[nt++] = tk;
+                which.push_back(i);
+            }
+            if (nt == 0) break;
+            if (pass == 1 && (r = ensure_literal_scratch(ctx))) return r;
+            std::vector<int> stv(nt);
+            std::vector<double> yv(nt);
+            PP_HIP(hipMemcpyAsync(ctx->tasks.p, ctx->h_tasks.p, nt * sizeof(SteerTask), hipMemcpyHostToDevice, st));
+            PP_HIP(launch_steer_tasks(st, sc, tr, ctx->tasks.p, nt, ctx->task_status.p,
+                                      ctx->task_yaw.p, pass ? ctx->lit_scratch.p : nullptr));
+            PP_HIP(hipMemcpyAsync(stv.data(), ctx->task_status.p, nt * sizeof(int), hipMemcpyDeviceToHost, st));
+            PP_HIP(hipMemcpyAsync(yv.data(), ctx->task_yaw.p, nt * sizeof(double), hipMemcpyDeviceToHost, st));
+            PP_HIP(hipStreamSynchronize(st));
+            for (int t = 0; t < nt; ++t) {
+                const int i = which[t];
+                if (stv[t] == kError)
+                    return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
+                ctx->h_task_status.p[i] = stv[t];
+                ok[b + i] = stv[t] == kAccept ? 1 : 0;
+                if (yaw) yaw[b + i] = yv[t];
+            }
+        }
+    }
+    return PP_OK;
+}
+
+int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out) {
+    if (!ctx || !out) return set_err(PP_ERR_INVALID_ARGUMENT, "null argument");
+    *out = ctx->stats;
+    return PP_OK;
+}
+
+int pp_rrt_reset_stats(pp_ctx* ctx) {
+    if (!ctx) return set_err(PP_ERR_INVALID_ARGUMENT, "null context");
+    ctx->stats = pp_stats{};
+    return PP_OK;
+}
+
+int pp_set_profiling(pp_ctx* ctx, int enabled) {
+    if (!ctx) return set_err(PP_ERR_INVALID_ARGUMENT, "null context");
+    ctx->prof = enabled != 0;
+    return PP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,335 @@
+// pp_device.h — device-side building blocks of the RRT extend hot path (gfx950, f64 steer).
+//
+// Restates the arithmetic of tsturzl/rs-pathplanning src/dubins.rs (mod2pi, the six Dubins
+// words, interpolate, generate_local_course) and of src/rrt.rs (compute_yaw, Space::verify) for
+// device code.  Every expression keeps the reference's left-to-right evaluation order and the
+// library is compiled with -ffp-contract=off, so results differ from the Rust crate only by the
+// ulp-level differences between ocml's and glibc's sin/cos/atan2/acos/hypot.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pp_types.h"
+
+namespace ppamd {
+
+constexpr double kPi = 3.14159265358979323846;  // std::f64::consts::PI
+constexpr double kTwoPi = 2.0 * kPi;
+
+// dubins.rs:14-20
+__host__ __device__ inline double mod2pi(double theta) {
+    return theta - kTwoPi * floor(theta / kTwoPi);
+}
+// dubins.rs:22-24 (Rust `%` == fmod: truncated, negative angles are not wrapped)
+__host__ __device__ inline double pi_2_pi(double angle) {
+    return fmod(angle + kPi, kTwoPi) - kPi;
+}
+
+// Mode {L, S, R} (dubins.rs:4-9) and the ALL_PLANNERS order (dubins.rs:291).
+enum : int { kModeL = 0, kModeS = 1, kModeR = 2 };
+__host__ __device__ inline int word_mode(int word, int seg) {
+    // LSL, RSR, LSR, RSL, RLR, LRL
+    const int first = (word == 0 || word == 2 || word == 5) ? kModeL : kModeR;
+    const int mid = (word < 4) ? kModeS : (word == 4 ? kModeL : kModeR);
+    const int last = (word == 0 || word == 3 || word == 5) ? kModeL : kModeR;
+    return seg == 0 ? first : (seg == 1 ? mid : last);
+}
+
+struct Word {
+    int ok;
+    double t, p, q;
+};
+
+// The six closed forms share sin/cos(alpha), sin/cos(beta) and cos(alpha - beta); each is
+// computed once here (the reference recomputes identical values per word).
+struct Trig {
+    double sa, sb, ca, cb, c_ab;
+};
+__device__ inline Trig make_trig(double alpha, double beta) {
+    Trig g;
+    g.sa = sin(alpha);
+    g.sb = sin(beta);
+    g.ca = cos(alpha);
+    g.cb = cos(beta);
+    g.c_ab = cos(alpha - beta);
+    return g;
+}
+
+// dubins.rs:27-48
+__device__ inline Word word_lsl(double alpha, double beta, double d, const Trig& g) {
+    Word w{0, 0.0, 0.0, 0.0};
+    double tmp0 = d + g.sa - g.sb;
+    double p_squared = 2.0 + (d * d) - (2.0 * g.c_ab) + (2.0 * d * (g.sa - g.sb));
+    if (p_squared < 0.0) return w;
+    double tmp1 = atan2(g.cb - g.ca, tmp0);
+    w.t = mod2pi(-alpha + tmp1);
+    w.p = sqrt(p_squared);
+    w.q = mod2pi(beta - tmp1);
+    w.ok = 1;
+    return w;
+}
+// dubins.rs:51-71
+__device__ inline Word word_rsr(double alpha, double beta, double d, const Trig& g) {
+    Word w{0, 0.0, 0.0, 0.0};
+    double tmp0 = d - g.sa + g.sb;
+    double p_squared = 2.0 + (d * d) - (2.0 * g.c_ab) + (2.0 * d * (g.sb - g.sa));
+    if (p_squared < 0.0) return w;
+    double tmp1 = atan2(g.ca - g.cb, tmp0);
+    w.t = mod2pi(alpha - tmp1);
+    w.p = sqrt(p_squared);
+    w.q = mod2pi(-beta + tmp1);
+    w.ok = 1;
+    return w;
+}
+// dubins.rs:74-92
+__device__ inline Word word_lsr(double alpha, double beta, double d, const Trig& g) {
+    Word w{0, 0.0, 0.0, 0.0};
+    double p_squared = -2.0 + (d * d) + (2.0 * g.c_ab) + (2.0 * d * (g.sa + g.sb));
+    if (p_squared < 0.0) return w;
+    double p = sqrt(p_squared);
+    double tmp = atan2(-g.ca - g.cb, d + g.sa + g.sb) - atan2(-2.0, p);
+    w.t = mod2pi(-alpha + tmp);
+    w.p = p;
+    w.q = mod2pi(-mod2pi(beta) + tmp);
+    w.ok = 1;
+    return w;
+}
+// dubins.rs:95-113
+__device__ inline Word word_rsl(double alpha, double beta, double d, const Trig& g) {
+    Word w{0, 0.0, 0.0, 0.0};
+    double p_squared = -2.0 + (d * d) + (2.0 * g.c_ab) - (2.0 * d * (g.sa + g.sb));
+    if (p_squared < 0.0) return w;
+    double p = sqrt(p_squared);
+    double tmp = atan2(g.ca + g.cb, d - g.sa - g.sb) - atan2(2.0, p);
+    w.t = mod2pi(alpha - tmp);
+    w.p = p;
+    w.q = mod2pi(beta - tmp);
+    w.ok = 1;
+    return w;
+}
+// dubins.rs:116-133
+__device__ inline Word word_rlr(double alpha, double beta, double d, const Trig& g) {
+    Word w{0, 0.0, 0.0, 0.0};
+    double tmp_rlr = (6.0 - d * d + 2.0 * g.c_ab + 2.0 * d * (g.sa - g.sb)) / 8.0;
+    if (fabs(tmp_rlr) > 1.0) return w;
+    double p = mod2pi(2.0 * kPi - acos(tmp_rlr));
+    double t = mod2pi(alpha - atan2(g.ca - g.cb, d - g.sa + g.sb) + mod2pi(p / 2.0));
+    double q = mod2pi(alpha - beta - t + mod2pi(p));
+    w.t = t;
+    w.p = p;
+    w.q = q;
+    w.ok = 1;
+    return w;
+}
+// dubins.rs:136-153
+__device__ inline Word word_lrl(double alpha, double beta, double d, const Trig& g) {
+    Word w{0, 0.0, 0.0, 0.0};
+    double tmp_lrl = (6.0 - d * d + 2.0 * g.c_ab + 2.0 * d * (-g.sa + g.sb)) / 8.0;
+    if (fabs(tmp_lrl) > 1.0) return w;
+    double p = mod2pi(2.0 * kPi - acos(tmp_lrl));
+    double t = mod2pi(-alpha - atan2(g.ca - g.cb, d + g.sa - g.sb) + p / 2.0);
+    double q = mod2pi(mod2pi(beta) - alpha - t + mod2pi(p));
+    w.t = t;
+    w.p = p;
+    w.q = q;
+    w.ok = 1;
+    return w;
+}
+
+// Result of the word selection of dubins_path_planning_from_origin (dubins.rs:333-363).
+struct Steer {
+    int word;  // -1 = None (no feasible word)
+    double t, p, q, cost;
+};
+
+// dubins.rs:333-363: evaluate LSL, RSR, LSR, RSL, RLR, LRL in order and keep the first strict
+// minimum of |t|+|p|+|q|.  All lanes compute the same (wave-uniform) values.
+__device__ inline Steer select_word(double lex, double ley, double leyaw, double c) {
+    const double hyp = hypot(lex, ley);
+    const double d = hyp * c;
+    const double theta = mod2pi(atan2(ley, lex));
+    const double alpha = mod2pi(-theta);
+    const double beta = mod2pi(leyaw - theta);
+    const Trig g = make_trig(alpha, beta);
+    Steer s{-1, 0.0, 0.0, 0.0, 0.0};
+    double bcost = __builtin_inf();
+    Word w[6];
+    w[0] = word_lsl(alpha, beta, d, g);
+    w[1] = word_rsr(alpha, beta, d, g);
+    w[2] = word_lsr(alpha, beta, d, g);
+    w[3] = word_rsl(alpha, beta, d, g);
+    w[4] = word_rlr(alpha, beta, d, g);
+    w[5] = word_lrl(alpha, beta, d, g);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        if (w[i].ok) {
+            double cost = fabs(w[i].t) + fabs(w[i].p) + fabs(w[i].q);
+            if (bcost > cost) {
+                s.word = i;
+                s.t = w[i].t;
+                s.p = w[i].p;
+                s.q = w[i].q;
+                bcost = cost;
+            }
+        }
+    }
+    s.cost = bcost;
+    return s;
+}
+
+struct Pose {
+    double x, y, yaw;
+};
+
+// dubins.rs:155-198 (x, y, yaw of one sample; directions are not part of the output)
+__device__ inline Pose interp_local(int mode, double length, double max_curvature, Pose o) {
+    Pose r;
+    if (mode == kModeS) {
+        r.x = o.x + length / max_curvature * cos(o.yaw);
+        r.y = o.y + length / max_curvature * sin(o.yaw);
+        r.yaw = o.yaw;
+    } else {
+        double ldx = sin(length) / max_curvature;
+        double ldy;
+        if (mode == kModeL)
+            ldy = (1.0 - cos(length)) / max_curvature;
+        else
+            ldy = (1.0 - cos(length)) / -max_curvature;
+        double gdx = cos(-o.yaw) * ldx + sin(-o.yaw) * ldy;
+        double gdy = -sin(-o.yaw) * ldx + cos(-o.yaw) * ldy;
+        r.x = o.x + gdx;
+        r.y = o.y + gdy;
+        r.yaw = o.yaw;
+    }
+    if (mode == kModeL)
+        r.yaw = o.yaw + length;
+    else if (mode == kModeR)
+        r.yaw = o.yaw - length;
+    return r;
+}
+
+// Literal single-thread restatement of dubins_path_planning (dubins.rs:326-428) writing WORLD
+// points: the slow path for the measure-zero trim cases, and the pp_dubins_batch API.
+// Returns kSteerSome / kSteerNone / kSteerOverflow (cap < n_point or the Rust index panic).
+__device__ inline int dubins_literal(double sx, double sy, double syaw, double ex0, double ey0,
+                                     double eyaw, double turn_radius, double step_size, double* px,
+                                     double* py, double* pyaw, int cap, int* n_out, int* word_out,
+                                     double* cost_out) {
+    const double ex = ex0 - sx, ey = ey0 - sy;
+    const double c = 1.0 / turn_radius;
+    const double lex = cos(syaw) * ex + sin(syaw) * ey;
+    const double ley = -(sin(syaw)) * ex + cos(syaw) * ey;
+    const double leyaw = eyaw - syaw;
+    const Steer s = select_word(lex, ley, leyaw, c);
+    if (s.word < 0) return kSteerNone;
+    const double lengths[3] = {s.t, s.p, s.q};
+    double total = 0.0;
+    total += s.t;
+    total += s.p;
+    total += s.q;
+    const double nq = trunc(total / step_size);
+    if (!(nq >= 0.0) || nq > 1.0e8) return kSteerOverflow;
+    const int n_point = (int)nq + 3 + 4;
+    if (n_point > cap) return kSteerOverflow;
+    for (int i = 0; i < n_point; ++i) px[i] = py[i] = pyaw[i] = 0.0;
+    // generate_local_course, dubins.rs:200-272
+    int ind = 1;
+    double ll = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        const int m = word_mode(s.word, i);
+        const double l = lengths[i];
+        const double d = (l > 0.0) ? step_size : -step_size;
+        const Pose o{px[ind], py[ind], pyaw[ind]};
+        ind -= 1;
+        double pd = (i >= 1 && (lengths[i - 1] * lengths[i]) > 0.0) ? (-d - ll) : (d - ll);
+        while (fabs(pd) <= fabs(l)) {
+            ind += 1;
+            if (ind >= n_point) return kSteerOverflow;
+            Pose r = interp_local(m, pd, c, o);
+            px[ind] = r.x;
+            py[ind] = r.y;
+            pyaw[ind] = r.yaw;
+            pd += d;
+        }
+        ll = l - pd - d;
+        ind += 1;
+        if (ind >= n_point) return kSteerOverflow;
+        Pose r = interp_local(m, l, c, o);
+        px[ind] = r.x;
+        py[ind] = r.y;
+        pyaw[ind] = r.yaw;
+    }
+    // trailing-zero trim, dubins.rs:281-288 (pops every trailing 0.0 plus one more element)
+    int len = n_point;
+    double last = px[len - 1];
+    while (len >= 1 && last == 0.0) {
+        last = px[len - 1];
+        len -= 1;
+    }
+    // back to the world frame, dubins.rs:412-422
+    const double cs = cos(-syaw), sn = sin(-syaw);
+    for (int i = 0; i < len; ++i) {
+        const double x = px[i], y = py[i];
+        px[i] = cs * x + sn * y + sx;
+        py[i] = -sn * x + cs * y + sy;
+        pyaw[i] = pi_2_pi(pyaw[i] + syaw);
+    }
+    *n_out = len;
+    *word_out = s.word;
+    *cost_out = s.cost;
+    return kSteerSome;
+}
+
+// Polyline segment vs closed disc: exact closest point of the segment.
+__device__ inline bool seg_hits_disc(double ax, double ay, double bx, double by, double cx,
+                                     double cy, double r2) {
+    const double vx = bx - ax, vy = by - ay;
+    const double wx = cx - ax, wy = cy - ay;
+    const double l2 = vx * vx + vy * vy;
+    double t = 0.0;
+    if (l2 > 0.0) {
+        t = (wx * vx + wy * vy) / l2;
+        if (t < 0.0)
+            t = 0.0;
+        else if (t > 1.0)
+            t = 1.0;
+    }
+    const double ex = wx - t * vx, ey = wy - t * vy;
+    return ex * ex + ey * ey <= r2;
+}
+
+// --------------------------------------------------------- seeded sampling
+// SplitMix64 output `ctr` of the stream `seed` (replaces rand::thread_rng, rrt.rs:140).
+__host__ __device__ inline uint64_t rng_u64(uint64_t seed, uint64_t ctr) {
+    uint64_t z = seed + (ctr + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+// rand 0.7 UniformFloat<f64>::sample_single: [1,2) from 52 random bits, minus 1, * scale + low
+// (rrt.rs:142-143).  res >= high (measure zero) narrows scale by one ulp with the same bits.
+__host__ __device__ inline double gen_range(uint64_t seed, uint64_t ctr, double low, double high) {
+    const uint64_t bits = (rng_u64(seed, ctr) >> 12) | 0x3FF0000000000000ULL;
+    const double value0_1 = __builtin_bit_cast(double, bits) - 1.0;
+    double scale = high - low;
+    for (;;) {
+        const double res = value0_1 * scale + low;
+        if (res < high) return res;
+        scale = nextafter(scale, 0.0);
+    }
+}
+
+// ------------------------------------------------------------------------- wave helpers
+__device__ inline double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ inline double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+
+}  // namespace ppamd

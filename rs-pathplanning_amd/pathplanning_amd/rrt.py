@@ -1,0 +1,242 @@
+"""``pathplanning::rrt`` (src/rrt.rs) with the extend hot path on the GPU.
+
+Same names and argument meaning as the crate: ``Robot``, ``create_circle``, ``Space``, ``Node``,
+``RRT`` with ``get_nearest_node``, ``get_random_node``, ``verify_node``, ``plan_one`` and the
+batched ``extend``.  Build-defined differences: obstacles are analytic discs
+and the bounds an axis-aligned rectangle (Q10), sampling is a seeded stream (Q7), iterations run
+with the sequential semantics of one rayon thread (Q8), the nearest neighbour is exact (Q9).
+``plan()``'s goal-connect / shortcut / path materialisation (``check_finish``, ``optimize``,
+``finalize``) is the next row of the build and is not provided yet.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _ffi
+
+
+class Robot:  # rrt.rs:16-40
+    def __init__(self, width: float, height: float, max_steer: float):
+        self.width = float(width)
+        self.height = float(height)
+        self.max_steer = float(max_steer)  # used as the Dubins turn radius (rrt.rs:37-39 → 424)
+
+    def get_width(self) -> float:
+        return self.width
+
+    def get_steer(self) -> float:
+        return self.max_steer
+
+
+@dataclass(frozen=True)
+class Circle:
+    """Analytic stand-in for ``create_circle``'s polygon (rrt.rs:43-60)."""
+    cx: float
+    cy: float
+    r: float
+
+
+def create_circle(center, radius: float) -> Circle:  # rrt.rs:43
+    return Circle(float(center[0]), float(center[1]), float(radius))
+
+
+def _rect_of(bounds):
+    b = np.asarray(bounds, dtype=np.float64)
+    if b.shape == (4,):
+        return tuple(b)
+    # polygon ring: accepted when it is an axis-aligned rectangle
+    xs, ys = b[:, 0], b[:, 1]
+    x0, x1, y0, y1 = xs.min(), xs.max(), ys.min(), ys.max()
+    if not np.all((np.isclose(xs, x0) | np.isclose(xs, x1)) & (np.isclose(ys, y0) | np.isclose(ys, y1))):
+        raise ValueError("bounds must be an axis-aligned rectangle (polygon bounds: next row)")
+    return (x0, y0, x1, y1)
+
+
+class Space:  # rrt.rs:70-159
+    def __init__(self, bounds, robot: Robot, obstacle_list):
+        self.raw_bounds = _rect_of(bounds)
+        self.robot = robot
+        obs = list(obstacle_list)
+        self.circles = np.array([[o.cx, o.cy, o.r] for o in obs], dtype=np.float64).reshape(-1, 3)
+        half = robot.get_width() / 2.0  # rrt.rs:82
+        x0, y0, x1, y1 = self.raw_bounds
+        self.minx, self.miny, self.maxx, self.maxy = x0 + half, y0 + half, x1 - half, y1 - half
+
+    @classmethod
+    def from_raw(cls, raw: dict) -> "Space":
+        return cls(raw["bounds"], Robot(*raw["robot"]),
+                   [create_circle((c[0], c[1]), c[2]) for c in raw["circles"]])
+
+    def get_steer(self) -> float:
+        return self.robot.get_steer()
+
+    def get_bounds(self):
+        """bbox of the shrunken bounds (minx, maxx, miny, maxy) — what rand_point samples."""
+        return (self.minx, self.maxx, self.miny, self.maxy)
+
+    def get_obs(self):
+        """inflated discs (cx, cy, r + width/2) (rrt.rs:108-111, 152-154)."""
+        half = self.robot.get_width() / 2.0
+        c = self.circles.copy()
+        c[:, 2] += half
+        return c
+
+    def _upload(self, ctx: _ffi.Context):
+        c = np.ascontiguousarray(self.circles)
+        cx, cy, r = (np.ascontiguousarray(c[:, k]) for k in range(3))
+        dp = C.POINTER(C.c_double)
+        x0, y0, x1, y1 = self.raw_bounds
+        _ffi.check(_ffi.lib().pp_space_new(
+            ctx.handle, x0, y0, x1, y1, self.robot.width, self.robot.height,
+            self.robot.max_steer, cx.ctypes.data_as(dp), cy.ctypes.data_as(dp),
+            r.ctypes.data_as(dp), len(cx)))
+
+
+@dataclass
+class Node:  # rrt.rs:161-214 (a view of one tree row)
+    index: int
+    x: float
+    y: float
+    yaw: float
+    parent: int  # -1 for the root
+
+    def get_point(self):
+        return (self.x, self.y)
+
+    def get_yaw(self):
+        return self.yaw
+
+
+class RRT:  # rrt.rs:325-620
+    """``RRT::new(start, start_yaw, goal, goal_yaw, max_iter, step_size, space)`` (rrt.rs:335).
+
+    Extra keyword arguments: ``seed`` (sampling stream), ``device`` (GPU ordinal), ``window``
+    (candidates evaluated per speculative GPU batch; results do not depend on it), ``capacity``
+    (initial node capacity, grown on demand)."""
+
+    def __init__(self, start, start_yaw, goal, goal_yaw, max_iter, step_size, space: Space,
+                 seed: int = 0, device: int = 0, window: int = 4096, capacity: int = 1 << 16,
+                 ctx: _ffi.Context | None = None):
+        self.ctx = ctx or _ffi.Context(device)
+        self.space = space
+        self.goal = (float(goal[0]), float(goal[1]))
+        self.goal_yaw = float(goal_yaw)
+        self.max_iter = int(max_iter)
+        self.step_size = float(step_size)
+        self.seed = int(seed)
+        space._upload(self.ctx)
+        _ffi.check(_ffi.lib().pp_rrt_set_window(self.ctx.handle, int(window)))
+        _ffi.check(_ffi.lib().pp_rrt_new(
+            self.ctx.handle, float(start[0]), float(start[1]), float(start_yaw), self.goal[0],
+            self.goal[1], self.goal_yaw, self.max_iter, self.step_size, self.seed, int(capacity)))
+
+    # ---------------------------------------------------------------- hot path
+    def extend(self, n_iter: int) -> int:
+        """``n_iter`` × plan_one's extend (rrt.rs:583-589); returns the nodes inserted."""
+        acc = C.c_int64(0)
+        _ffi.check(_ffi.lib().pp_rrt_extend(self.ctx.handle, int(n_iter), C.byref(acc)))
+        return acc.value
+
+    def plan_one(self) -> bool:
+        """plan_one's extend (rrt.rs:583-589): True when the node was inserted."""
+        acc = C.c_int32(0)
+        _ffi.check(_ffi.lib().pp_rrt_plan_one(self.ctx.handle, C.byref(acc)))
+        return bool(acc.value)
+
+    def set_window(self, k: int):
+        _ffi.check(_ffi.lib().pp_rrt_set_window(self.ctx.handle, int(k)))
+
+    # ---------------------------------------------------------------- queries
+    def tree_size(self) -> int:
+        n = C.c_int64(0)
+        _ffi.check(_ffi.lib().pp_rrt_tree_size(self.ctx.handle, C.byref(n)))
+        return n.value
+
+    def iteration(self) -> int:
+        it = C.c_int64(0)
+        _ffi.check(_ffi.lib().pp_rrt_iteration(self.ctx.handle, C.byref(it)))
+        return it.value
+
+    def tree(self):
+        """(x, y, yaw, parent) arrays, root first."""
+        n = self.tree_size()
+        x, y, yaw = np.zeros(n), np.zeros(n), np.zeros(n)
+        par = np.zeros(n, dtype=np.int32)
+        out = C.c_int64(0)
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        _ffi.check(_ffi.lib().pp_rrt_tree_export(
+            self.ctx.handle, x.ctypes.data_as(dp), y.ctypes.data_as(dp), yaw.ctypes.data_as(dp),
+            par.ctypes.data_as(ip), n, C.byref(out)))
+        return x, y, yaw, par
+
+    def node(self, i: int) -> Node:
+        x, y, yaw, par = self.tree()
+        return Node(i, x[i], y[i], yaw[i], int(par[i]))
+
+    def get_nearest_node_batch(self, qx, qy):
+        """RRT::get_nearest_node (rrt.rs:378-391) for many points: (index, d2) arrays."""
+        qx = np.ascontiguousarray(qx, dtype=np.float64)
+        qy = np.ascontiguousarray(qy, dtype=np.float64)
+        k = len(qx)
+        idx = np.zeros(k, dtype=np.int32)
+        d2 = np.zeros(k)
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        _ffi.check(_ffi.lib().pp_rrt_get_nearest_node_batch(
+            self.ctx.handle, qx.ctypes.data_as(dp), qy.ctypes.data_as(dp), k,
+            idx.ctypes.data_as(ip), d2.ctypes.data_as(dp)))
+        return idx, d2
+
+    def get_nearest_node(self, point) -> int:
+        idx, _ = self.get_nearest_node_batch([point[0]], [point[1]])
+        return int(idx[0])
+
+    def get_random_node(self, it: int | None = None):
+        """rrt.rs:406-412: (x, y, nearest index, yaw) of iteration ``it``'s sample (default: the
+        next iteration) — does not advance the planner."""
+        it = self.iteration() if it is None else int(it)
+        x0, x1, y0, y1 = self.space.get_bounds()
+        x = _ffi.lib().pp_gen_range(self.seed, 2 * it, x0, x1)
+        y = _ffi.lib().pp_gen_range(self.seed, 2 * it + 1, y0, y1)
+        p = self.get_nearest_node((x, y))
+        tx, ty, _, _ = self.tree()
+        return x, y, p, float(np.arctan2(ty[p] - y, tx[p] - x))
+
+    def verify_node_batch(self, x, y, parent):
+        """verify_node(Node::new(point, tree[parent])) (rrt.rs:169-175, 414-426): (ok, yaw)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        parent = np.ascontiguousarray(parent, dtype=np.int32)
+        k = len(x)
+        ok = np.zeros(k, dtype=np.uint8)
+        yaw = np.zeros(k)
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        _ffi.check(_ffi.lib().pp_rrt_verify_node_batch(
+            self.ctx.handle, x.ctypes.data_as(dp), y.ctypes.data_as(dp),
+            parent.ctypes.data_as(ip), k, ok.ctypes.data_as(C.POINTER(C.c_uint8)),
+            yaw.ctypes.data_as(dp)))
+        return ok.astype(bool), yaw
+
+    def verify_node(self, x, y, parent) -> bool:
+        ok, _ = self.verify_node_batch([x], [y], [parent])
+        return bool(ok[0])
+
+    # ---------------------------------------------------------------- instrumentation
+    def stats(self) -> dict:
+        s = _ffi.StatsC()
+        _ffi.check(_ffi.lib().pp_rrt_get_stats(self.ctx.handle, C.byref(s)))
+        return s.as_dict()
+
+    def reset_stats(self):
+        _ffi.check(_ffi.lib().pp_rrt_reset_stats(self.ctx.handle))
+
+    def set_profiling(self, on: bool):
+        _ffi.check(_ffi.lib().pp_set_profiling(self.ctx.handle, int(bool(on))))
+
+    def synchronize(self):
+        _ffi.check(_ffi.lib().pp_synchronize(self.ctx.handle))
+
+    def close(self):
+        self.ctx.close()

@@ -1,0 +1,103 @@
+"""Generate the golden fixtures under tests/golden/ from the pure-Python restatement
+(oracle/dubins_py.py).
+
+The reference ships no golden vectors and cannot be built or run here, so the
+expected outputs come from this independent restatement; the inputs are the reference's own
+known configurations (examples/dubins/src/main.rs:131-164, benches/all.rs:8-42,102-111) plus a
+seeded random battery and the build's config-2 field.  The C oracle and the HIP path are checked
+against these files.  Re-run with:  python tests/golden/gen_golden.py
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import random
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "rs-pathplanning_amd"))
+
+import dubins_py as P  # noqa: E402
+from pathplanning_amd import scenes  # noqa: E402  (host-side input data only)
+
+
+def rad(d):
+    return d * (math.pi / 180.0)
+
+
+KNOWN = {
+    # examples/dubins/src/main.rs:131-153 (conf1) and 155-164 (conf2): R = 0.5, step 0.01
+    "A": (1.0, 1.0, rad(45.0), -3.0, -3.0, rad(-45.0), 0.5, 0.01),
+    "B": (-3.0, -3.0, rad(-45.0), 1.0, 1.0, rad(45.0), 0.5, 0.01),
+    # benches/all.rs:102-111 (c: 1.0 read as turn_radius 1.0), step 0.1
+    "C": (1.0, 1.0, rad(45.0), -3.0, -3.0, rad(-45.0), 1.0, 0.1),
+}
+
+
+def dubins_record(conf, full=True):
+    r = P.dubins_path_planning(*conf)
+    if r is None:
+        return {"conf": list(conf), "word": -1}
+    px, py, pyaw, word, cost = r
+    rec = {"conf": list(conf), "word": word, "cost": cost, "n": len(px),
+           "sum_x": math.fsum(px), "sum_y": math.fsum(py), "sum_yaw": math.fsum(pyaw)}
+    if full:
+        rec.update(px=px, py=py, pyaw=pyaw)
+    else:
+        rec.update(head=[px[:3], py[:3], pyaw[:3]], tail=[px[-3:], py[-3:], pyaw[-3:]])
+    return rec
+
+
+def battery(n=400, seed=20261015):
+    rnd = random.Random(seed)
+    out = []
+    for i in range(n):
+        c = [rnd.uniform(-25, 25), rnd.uniform(-25, 25), rnd.uniform(-7, 7),
+             rnd.uniform(-25, 25), rnd.uniform(-25, 25), rnd.uniform(-7, 7),
+             rnd.choice([0.5, 0.8, 1.0, 4.0]), rnd.choice([0.01, 0.05, 0.1, 0.3])]
+        k = i % 10
+        if k == 0:  # identical positions (the node-to-itself case)
+            c[3], c[4] = c[0], c[1]
+        elif k == 1:  # identical poses
+            c[3], c[4], c[5] = c[0], c[1], c[2]
+        elif k == 2:  # very short hop
+            c[3], c[4] = c[0] + rnd.uniform(-1e-3, 1e-3), c[1] + rnd.uniform(-1e-3, 1e-3)
+        out.append(dubins_record(tuple(c), full=False))
+    return out
+
+
+def rrt_record(raw, seed, n_iter):
+    from oracle import OracleScene  # noqa: E402  (scene arithmetic only)
+
+    sc = OracleScene.from_raw(raw).as_dict()
+    tree = {"x": [raw["start"][0]], "y": [raw["start"][1]], "yaw": [raw["start"][2]],
+            "parent": [-1]}
+    log = P.rrt_extend(sc, tree, seed, 0, n_iter)
+    return {"scene": raw["name"], "seed": seed, "n_iter": n_iter, "x": tree["x"], "y": tree["y"],
+            "yaw": tree["yaw"], "parent": tree["parent"], "log_nn": [a for a, _ in log],
+            "log_acc": [b for _, b in log]}
+
+
+def main():
+    known = {k: dubins_record(v) for k, v in KNOWN.items()}
+    with open(os.path.join(HERE, "dubins_known.json"), "w") as f:
+        json.dump(known, f)
+    with open(os.path.join(HERE, "dubins_battery.json"), "w") as f:
+        json.dump(battery(), f)
+    b6 = scenes.bench6()
+    recs = [rrt_record(b6, s, 400) for s in range(4)]
+    with open(os.path.join(HERE, "rrt_bench6.json"), "w") as f:
+        json.dump(recs, f)
+    field = scenes.field512()
+    with open(os.path.join(HERE, "rrt_field512.json"), "w") as f:
+        json.dump([rrt_record(field, 42, 1200)], f)
+    for k, v in known.items():
+        print(k, P.WORD_NAMES[v["word"]], v["cost"], v["n"])
+    print("bench6 nodes:", [len(r["x"]) for r in recs])
+
+
+if __name__ == "__main__":
+    main()

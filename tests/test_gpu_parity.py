@@ -1,0 +1,313 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Tolerances (north star: "within 1e-5 f32"): node coordinates, parents, nearest indices, accept
+flags, Dubins words and point counts are compared EXACTLY; yaw and Dubins point coordinates,
+which go through ocml's f64 sin/cos/atan2 instead of glibc's, within 1e-9 absolute.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+ANG_TOL = 1e-9
+PT_TOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def ctx(pkg):
+    c = pkg.Context(0)
+    yield c
+    c.close()
+
+
+def _planner(pkg, raw, seed, window, ctx=None, capacity=1 << 16):
+    from pathplanning_amd import rrt
+
+    sx, sy, syaw = raw["start"]
+    gx, gy, gyaw = raw["goal"]
+    return rrt.RRT((sx, sy), syaw, (gx, gy), gyaw, raw["max_iter"], raw["step_size"],
+                   rrt.Space.from_raw(raw), seed=seed, window=window, capacity=capacity, ctx=ctx)
+
+
+def _oracle_tree(oracle_mod, raw, seed, n_iter, cap=1 << 17):
+    sc = oracle_mod.OracleScene.from_raw(raw)
+    tr = oracle_mod.OracleTree(raw["start"], cap)
+    acc, nn, la = oracle_mod.rrt_extend(sc, tr, seed, 0, n_iter)
+    return tr.arrays(), acc, nn, la
+
+
+def _assert_same_tree(got, exp):
+    x, y, yaw, par = got
+    ex, ey, eyaw, epar = exp
+    assert len(x) == len(ex), (len(x), len(ex))
+    assert np.array_equal(x, ex) and np.array_equal(y, ey)
+    assert np.array_equal(par, epar)
+    assert np.max(np.abs(yaw - eyaw)) <= ANG_TOL
+
+
+# ------------------------------------------------------------------------------------ dubins
+def _dubins_configs(n, seed):
+    from pathplanning_amd.dubins import DubinsConfig
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        c = [rng.uniform(-25, 25), rng.uniform(-25, 25), rng.uniform(-7, 7),
+             rng.uniform(-25, 25), rng.uniform(-25, 25), rng.uniform(-7, 7),
+             float(rng.choice([0.5, 0.8, 1.0, 4.0])), float(rng.choice([0.05, 0.1, 0.3]))]
+        k = i % 8
+        if k == 0:
+            c[3], c[4] = c[0], c[1]
+        elif k == 1:
+            c[3], c[4], c[5] = c[0], c[1], c[2]
+        elif k == 2:
+            c[3], c[4] = c[0] + rng.uniform(-1e-3, 1e-3), c[1] + rng.uniform(-1e-3, 1e-3)
+        elif k == 3:  # axis-aligned straight lines (zero-length arcs, the ll carry quirk)
+            c[4], c[2], c[5] = c[1], 0.0, 0.0
+        out.append(DubinsConfig(*c))
+    return out
+
+
+def _cmp_dubins(got, exp):
+    if exp is None:
+        assert got is None
+        return
+    assert got is not None
+    px, py, pyaw, mode, cost = got
+    epx, epy, epyaw, eword, ecost = exp
+    from pathplanning_amd.dubins import WORD_MODES
+
+    assert mode == WORD_MODES[eword]
+    assert len(px) == len(epx)
+    assert abs(cost - ecost) <= 1e-12 * max(1.0, abs(ecost))
+    if len(px):
+        assert np.max(np.abs(px - epx)) <= PT_TOL and np.max(np.abs(py - epy)) <= PT_TOL
+        d = np.abs(pyaw - epyaw)
+        d = np.minimum(d, np.abs(d - 2 * math.pi))
+        assert np.max(d) <= ANG_TOL
+
+
+def test_dubins_known_configs(pkg, ctx):
+    from pathplanning_amd.dubins import DubinsConfig, dubins_path_planning_batch
+
+    known = load_golden("dubins_known.json")
+    recs = list(known.values())
+    got = dubins_path_planning_batch([DubinsConfig(*r["conf"]) for r in recs], ctx)
+    for g, r in zip(got, recs):
+        _cmp_dubins(g, (np.array(r["px"]), np.array(r["py"]), np.array(r["pyaw"]), r["word"],
+                        r["cost"]))
+
+
+def test_dubins_battery_vs_oracle(pkg, ctx, oracle_mod):
+    from pathplanning_amd.dubins import dubins_path_planning_batch
+
+    confs = _dubins_configs(6000, 1)
+    got = dubins_path_planning_batch(confs, ctx)
+    for c, g in zip(confs, got):
+        _cmp_dubins(g, oracle_mod.dubins(c.sx, c.sy, c.syaw, c.ex, c.ey, c.eyaw, c.turn_radius,
+                                         c.step_size))
+
+
+def test_dubins_capacity_error(pkg, ctx):
+    from pathplanning_amd.dubins import DubinsConfig, dubins_path_planning_batch
+
+    with pytest.raises(pkg.PPError) as e:
+        dubins_path_planning_batch([DubinsConfig(0, 0, 0, 50, 0, 0, 1.0, 0.1)], ctx, cap=8)
+    assert e.value.code == pkg._ffi.PP_ERR_CAPACITY
+
+
+# ------------------------------------------------------------------------------ extend parity
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_bench6_golden_trees(pkg, ctx, seed):
+    from pathplanning_amd import scenes
+
+    rec = load_golden("rrt_bench6.json")[seed]
+    p = _planner(pkg, scenes.bench6(), rec["seed"], 64, ctx)
+    p.extend(rec["n_iter"])
+    _assert_same_tree(p.tree(), (np.array(rec["x"]), np.array(rec["y"]), np.array(rec["yaw"]),
+                                 np.array(rec["parent"], dtype=np.int32)))
+
+
+@pytest.mark.parametrize("window", [1, 7, 256, 4096])
+def test_bench6_full_run_any_window(pkg, ctx, oracle_mod, window):
+    """config 1: the whole max_iter = 8000 run of benches/all.rs, identical for every K."""
+    from pathplanning_amd import scenes
+
+    raw = scenes.bench6()
+    n_iter = 8000 if window >= 256 else 1500
+    exp, acc, _, _ = _oracle_tree(oracle_mod, raw, 11, n_iter)
+    p = _planner(pkg, raw, 11, window, ctx)
+    assert p.extend(n_iter) == acc
+    assert p.iteration() == n_iter
+    _assert_same_tree(p.tree(), exp)
+
+
+def test_field512_golden(pkg, ctx):
+    from pathplanning_amd import scenes
+
+    rec = load_golden("rrt_field512.json")[0]
+    p = _planner(pkg, scenes.field512(), rec["seed"], 4096, ctx)
+    p.extend(rec["n_iter"])
+    _assert_same_tree(p.tree(), (np.array(rec["x"]), np.array(rec["y"]), np.array(rec["yaw"]),
+                                 np.array(rec["parent"], dtype=np.int32)))
+
+
+def test_field512_config2_parity(pkg, ctx, oracle_mod):
+    """config 2 scene, K = 4096, 40k iterations (about 9k nodes) against the sequential oracle."""
+    from pathplanning_amd import scenes
+
+    raw = scenes.field512()
+    exp, acc, _, _ = _oracle_tree(oracle_mod, raw, 42, 40000)
+    p = _planner(pkg, raw, 42, 4096, ctx)
+    assert p.extend(40000) == acc
+    _assert_same_tree(p.tree(), exp)
+    st = p.stats()
+    assert st["iterations"] == 40000 and st["accepted"] == acc
+
+
+def test_extend_is_incremental(pkg, ctx, oracle_mod):
+    """extend(a) then extend(b) == extend(a + b) == the oracle, across ragged window edges."""
+    from pathplanning_amd import scenes
+
+    raw = scenes.bench6()
+    exp, _, _, _ = _oracle_tree(oracle_mod, raw, 5, 3000)
+    p = _planner(pkg, raw, 5, 512, ctx)
+    for n in (1, 2, 997, 3, 1024, 973):
+        p.extend(n)
+    assert p.iteration() == 3000
+    _assert_same_tree(p.tree(), exp)
+
+
+def test_plan_one_matches_oracle_log(pkg, ctx, oracle_mod):
+    from pathplanning_amd import scenes
+
+    raw = scenes.bench6()
+    _, _, _, la = _oracle_tree(oracle_mod, raw, 9, 200)
+    p = _planner(pkg, raw, 9, 4096, ctx)
+    got = [p.plan_one() for _ in range(200)]
+    assert got == [bool(v) for v in la]
+
+
+# ------------------------------------------------------------------ nearest neighbour / verify
+def test_nearest_batch_exact(pkg, ctx, oracle_mod):
+    from pathplanning_amd import scenes
+
+    raw = scenes.field512()
+    p = _planner(pkg, raw, 3, 4096, ctx)
+    p.extend(30000)
+    x, y, _, _ = p.tree()
+    rng = np.random.default_rng(0)
+    qx = rng.uniform(0, 512, 5000)
+    qy = rng.uniform(0, 512, 5000)
+    # exact ties and near-ties: queries on nodes, and midpoints of node pairs
+    k = min(len(x) - 1, 400)
+    qx[:k], qy[:k] = x[1:k + 1], y[1:k + 1]
+    qx[k:2 * k] = 0.5 * (x[:k] + x[1:k + 1])
+    qy[k:2 * k] = 0.5 * (y[:k] + y[1:k + 1])
+    idx, d2 = p.get_nearest_node_batch(qx, qy)
+    for i in range(len(qx)):
+        ei, ed2 = oracle_mod.nearest(x, y, qx[i], qy[i])
+        assert idx[i] == ei and d2[i] == ed2, i
+
+
+def test_nearest_duplicate_points_lowest_index(pkg, ctx):
+    """a query placed exactly on a node returns that node (d2 = 0 beats every other node)."""
+    from pathplanning_amd import rrt
+
+    space = rrt.Space((-10, -10, 10, 10), rrt.Robot(0.0, 0.0, 1.0), [])
+    p = rrt.RRT((0.0, 0.0), 0.0, (5.0, 5.0), 0.0, 100, 0.1, space, ctx=ctx)
+    p.extend(300)
+    x, y, _, _ = p.tree()
+    idx, _ = p.get_nearest_node_batch(x, y)
+    assert np.array_equal(idx, np.arange(len(x)))
+
+
+def test_verify_node_batch_vs_oracle(pkg, ctx, oracle_mod):
+    from pathplanning_amd import scenes
+
+    raw = scenes.field512()
+    p = _planner(pkg, raw, 8, 4096, ctx)
+    p.extend(8000)
+    x, y, yaw, par = p.tree()
+    sc = oracle_mod.OracleScene.from_raw(raw)
+    otr = oracle_mod.OracleTree(raw["start"], len(x) + 1)
+    otr.x[:len(x)], otr.y[:len(x)], otr.yaw[:len(x)], otr.parent[:len(x)] = x, y, yaw, par
+    otr._c.n = len(x)
+    rng = np.random.default_rng(1)
+    k = 3000
+    cx = rng.uniform(0.5, 511.5, k)
+    cy = rng.uniform(0.5, 511.5, k)
+    cp = rng.integers(0, len(x), k).astype(np.int32)
+    # edge cases: candidate exactly at its parent (yaw = atan2(0, 0)); far parents
+    cx[:20], cy[:20] = x[cp[:20]], y[cp[:20]]
+    ok, gyaw = p.verify_node_batch(cx, cy, cp)
+    for i in range(k):
+        eok, eyaw = oracle_mod.verify_candidate(sc, otr, cx[i], cy[i], int(cp[i]))
+        assert ok[i] == eok, i
+        assert abs(gyaw[i] - eyaw) <= ANG_TOL
+
+
+# ------------------------------------------------------------------------- full-size properties
+def test_100k_tree_properties(pkg, ctx, oracle_mod):
+    """BASELINE config 2 at full size: grow past 100k nodes, then check size-independent
+    properties — every node's parent is its exact nearest among the nodes before it, and its
+    edge verifies — on a random subset, plus K-invariance on a prefix."""
+    from pathplanning_amd import scenes
+
+    raw = scenes.field512()
+    p = _planner(pkg, raw, 42, 4096, ctx, capacity=1 << 18)
+    while p.tree_size() < 100_000:
+        p.extend(65536)
+    x, y, yaw, par = p.tree()
+    n = len(x)
+    assert par[0] == -1 and np.all(par[1:] < np.arange(1, n)) and np.all(par[1:] >= 0)
+    rng = np.random.default_rng(2)
+    sample = rng.choice(np.arange(1, n), 400, replace=False)
+    sc = oracle_mod.OracleScene.from_raw(raw)
+    otr = oracle_mod.OracleTree(raw["start"], n + 1)
+    otr.x[:n], otr.y[:n], otr.yaw[:n], otr.parent[:n] = x, y, yaw, par
+    for v in sample:
+        ei, _ = oracle_mod.nearest(x[:v], y[:v], x[v], y[v])
+        assert par[v] == ei, v
+        otr._c.n = v  # the tree as it stood when v was inserted
+        ok, eyaw = oracle_mod.verify_candidate(sc, otr, x[v], y[v], int(par[v]))
+        assert ok and abs(eyaw - yaw[v]) <= ANG_TOL, v
+    # K-invariance: the first 60k iterations with K = 1000 give the same prefix
+    q = _planner(pkg, raw, 42, 1000, ctx)
+    q.extend(60000)
+    qx, qy, qyaw, qpar = q.tree()
+    m = len(qx)
+    assert np.array_equal(qx, x[:m]) and np.array_equal(qpar, par[:m])
+
+
+def test_empty_scene_and_blocked_root(pkg, ctx):
+    from pathplanning_amd import rrt
+
+    # no obstacles: every sample is accepted
+    space = rrt.Space((0, 0, 50, 50), rrt.Robot(1.0, 1.0, 2.0), [])
+    p = rrt.RRT((25.0, 25.0), 0.0, (40.0, 40.0), 0.0, 100, 0.1, space, ctx=ctx)
+    # a sample that lands inside the shrunk bounds but whose Dubins loop leaves them is rejected,
+    # so "every" is not guaranteed; count is checked against the bound instead
+    acc = p.extend(500)
+    assert 0 < acc <= 500 and p.tree_size() == acc + 1
+    # root inside an obstacle: every junction ends at the root, nothing is ever accepted
+    space = rrt.Space((0, 0, 50, 50), rrt.Robot(1.0, 1.0, 2.0), [rrt.create_circle((25, 25), 3.0)])
+    p = rrt.RRT((25.0, 25.0), 0.0, (40.0, 40.0), 0.0, 100, 0.1, space, ctx=ctx)
+    assert p.extend(2000) == 0 and p.tree_size() == 1
+
+
+def test_errors_are_codes(pkg, ctx):
+    from pathplanning_amd import rrt
+
+    space = rrt.Space((0, 0, 10, 10), rrt.Robot(1.0, 1.0, 1.0), [])
+    p = rrt.RRT((5.0, 5.0), 0.0, (8.0, 8.0), 0.0, 10, 0.1, space, ctx=ctx)
+    with pytest.raises(pkg.PPError) as e:
+        p.verify_node_batch([1.0], [1.0], [5])  # parent outside the tree
+    assert e.value.code == pkg._ffi.PP_ERR_INVALID_ARGUMENT
+    with pytest.raises(pkg.PPError) as e:
+        rrt.RRT((5.0, 5.0), 0.0, (8.0, 8.0), 0.0, 10, 0.0, space, ctx=ctx)  # step 0
+    assert e.value.code == pkg._ffi.PP_ERR_INVALID_ARGUMENT
