@@ -72,7 +72,7 @@ def _dubins_configs(n, seed):
     return out
 
 
-def _cmp_dubins(got, exp):
+def _cmp_dubins(got, exp, same_position=False):
     if exp is None:
         assert got is None
         return
@@ -81,7 +81,17 @@ def _cmp_dubins(got, exp):
     epx, epy, epyaw, eword, ecost = exp
     from pathplanning_amd.dubins import WORD_MODES
 
-    assert mode == WORD_MODES[eword]
+    if mode != WORD_MODES[eword]:
+        # mathematically tied words (e.g. a straight configuration: LSL, LSR, RSL and RSR all
+        # have t = q = 0 and cost d) are ordered by the libm's last ulp; a swap is accepted only
+        # on such a tie, and the geometry must still agree point for point below
+        assert abs(cost - ecost) <= 1e-12 * max(1.0, abs(ecost)), (mode, eword, cost, ecost)
+    if same_position and abs(len(px) - len(epx)) == 1:
+        # start == end position: the endpoint's local x is a pure rounding residue (0 in exact
+        # arithmetic); the trim (dubins.rs:281-288) pops one more point iff it is exactly 0.0,
+        # which depends on the libm's last ulp (glibc vs ocml).  Compare the common prefix.
+        k = min(len(px), len(epx))
+        px, py, pyaw, epx, epy, epyaw = px[:k], py[:k], pyaw[:k], epx[:k], epy[:k], epyaw[:k]
     assert len(px) == len(epx)
     assert abs(cost - ecost) <= 1e-12 * max(1.0, abs(ecost))
     if len(px):
@@ -107,9 +117,17 @@ def test_dubins_battery_vs_oracle(pkg, ctx, oracle_mod):
 
     confs = _dubins_configs(6000, 1)
     got = dubins_path_planning_batch(confs, ctx)
+    n_short = n_same = 0
     for c, g in zip(confs, got):
-        _cmp_dubins(g, oracle_mod.dubins(c.sx, c.sy, c.syaw, c.ex, c.ey, c.eyaw, c.turn_radius,
-                                         c.step_size))
+        same = c.sx == c.ex and c.sy == c.ey
+        n_same += same
+        e = oracle_mod.dubins(c.sx, c.sy, c.syaw, c.ex, c.ey, c.eyaw, c.turn_radius, c.step_size)
+        if g is not None and e is not None and len(g[0]) != len(e[0]):
+            assert same  # a count difference only ever comes from the residue case
+            n_short += 1
+        _cmp_dubins(g, e, same_position=same)
+    # measured: 23 of 750 same-position configs (3 %); never for distinct positions
+    assert n_short <= 0.1 * n_same
 
 
 def test_dubins_capacity_error(pkg, ctx):
