@@ -104,7 +104,7 @@ int pp_space_get_bounds(pp_ctx* ctx, double out_minx_maxx_miny_maxy[4]);
  * the sampling seed and an initial node capacity (grown on demand). */
 int pp_rrt_new(pp_ctx* ctx, double sx, double sy, double syaw, double gx, double gy, double gyaw,
                int64_t max_iter, double step_size, uint64_t seed, int64_t capacity);
-/* candidates per speculative window (K; default 4096).  Results do not depend on K. */
+/* candidates per speculative window (K in [1, 4096]; default 4096).  Results do not depend on K. */
 int pp_rrt_set_window(pp_ctx* ctx, int k);
 /* n_iter iterations of plan_one's extend (rrt.rs:583-589: rand_point, get_nearest_node,
  * Node::new, verify_node, insert) with the sequential semantics of one rayon thread. */

@@ -1,17 +1,18 @@
-// pp_capi.cpp — host side of the MI355X RRT extend path: context, scene, device-resident tree,
-// the speculative window driver with its sequential-consistency resolve, and the C ABI
-// (include/pathplanning_amd.h).
+// pp_capi.cpp — host side of the MI355X RRT extend path: context, scene, device-resident tree and
+// planner state, the window enqueue loop, and the C ABI (include/pathplanning_amd.h).
 //
 // Extend semantics: iteration it samples (x, y) from the seeded stream, takes
 // the exact nearest node of the tree as it stands after iterations < it, steers child→parent with
 // Dubins, verifies, inserts.  The GPU evaluates a window of K iterations against the tree
-// snapshot at the window start; the host then replays the window in order:
+// snapshot at the window start, and a one-workgroup resolve kernel replays the window in order:
 //   * sample j's true parent is the nearest of {snapshot NN} ∪ {accepted window samples i < j};
 //     window_pairs lists the i that are strictly nearer than the snapshot NN, so the parent is
 //     the first accepted entry of that list in (d2, i) order, or the snapshot NN;
 //   * the verdict for (j, parent) was precomputed for the snapshot NN and for every listed i
-//     under i's own snapshot parent; only a parent that itself changed needs a repair launch.
-// The result is identical to the one-at-a-time sequential spec for every K.
+//     under i's own snapshot parent; only a parent that itself changed needs a repair steer.
+// The result is identical to the one-at-a-time sequential spec for every K.  All planner state
+// (it, n, counters) lives in device memory, so the host enqueues windows back to back and
+// synchronises once per batch of windows.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -83,7 +84,7 @@ struct HBuf {  // pinned host staging
     ~HBuf() { release(); }
 };
 
-constexpr int kPrefetch = 1024;  // candidate entries copied back with the first batch
+constexpr int kMaxBatch = 64;  // windows enqueued between two host synchronisations
 
 }  // namespace
 
@@ -104,42 +105,38 @@ struct pp_ctx {
     int64_t max_iter = 0;
     double step = 0.1;
     uint64_t seed = 0;
-    int64_t it = 0;    // next iteration index (RNG counter base)
-    int64_t n = 0;     // tree nodes
-    int64_t cap = 0;   // tree capacity
+    int64_t it = 0;   // mirror of DevState.it (exact after every synchronisation)
+    int64_t n = 0;    // mirror of DevState.n
+    int64_t cap = 0;  // tree capacity
     double eps_coord = 0.0;
     DBuf<float> x32, y32;
     DBuf<double> X, Y, YAW;
     DBuf<int> PAR;
+    DBuf<DevState> d_state, d_api_state;
+    HBuf<DevState> h_state;
 
-    // ---- window buffers
+    // ---- window buffers (sized for Kcap)
     int K = 4096;
     int Kcap = 0;
-    DBuf<double> wsx, wsy;
+    DBuf<double> wsx, wsy, nn_d2, rs_d2, snap_yaw;
     DBuf<float> pbest, psecond;
-    DBuf<int> pidx;
-    DBuf<int> nn_idx;
-    DBuf<double> nn_d2;
-    DBuf<int> flag_list;
-    DBuf<int> counters;  // [0] nn flagged, [1] candidate entries
-    DBuf<int> cand_cnt;
+    DBuf<int> pidx, nn_idx, flag_list, rs_idx, cand_cnt, snap_status;
     DBuf<CandEntry> cand;
-    DBuf<int> snap_status, spec_status, task_status;
-    DBuf<double> snap_yaw, spec_yaw, task_yaw;
+    DBuf<int> r_order, r_rep;
+    DBuf<double> r_repyaw;
+    DBuf<double> lit_scratch;  // resolve: one literal buffer per wave
+    // verify_node API
     DBuf<SteerTask> tasks;
-    DBuf<double> lit_scratch;
-    DBuf<CommitEntry> commits;
-
-    HBuf<int> h_counters, h_cand_cnt, h_nn_idx, h_snap_status, h_spec_status, h_task_status;
-    HBuf<double> h_snap_yaw, h_spec_yaw, h_task_yaw, h_d2;
-    HBuf<CandEntry> h_cand;
+    DBuf<int> task_status;
+    DBuf<double> task_yaw;
+    DBuf<double> api_lit_scratch;
     HBuf<SteerTask> h_tasks;
-    HBuf<CommitEntry> h_commits;
 
-    // ---- stats / profiling
-    pp_stats stats{};
+    // ---- profiling
     bool prof = false;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    std::vector<hipEvent_t> ev;  // 4 per window of a batch
+    double nn_scan_ms = 0.0, steer_ms = 0.0;
+    int64_t nn_scan_launches = 0, steer_launches = 0;
 
     ~pp_ctx() {
         for (auto& e : ev)
@@ -169,8 +166,36 @@ struct pp_ctx {
         t.x = X.p;
         t.y = Y.p;
         t.yaw = YAW.p;
-        t.n = (int)n;
+        t.parent = PAR.p;
         return t;
+    }
+    WindowArgs window_args(DevState* st) const {
+        WindowArgs a;
+        a.K = Kcap;
+        a.seed = seed;
+        a.eps_coord = eps_coord;
+        a.st = st;
+        a.sc = scene_dev();
+        a.tr = tree_dev();
+        a.wsx = wsx.p;
+        a.wsy = wsy.p;
+        a.pbest = pbest.p;
+        a.psecond = psecond.p;
+        a.pidx = pidx.p;
+        a.nn_idx = nn_idx.p;
+        a.nn_d2 = nn_d2.p;
+        a.flag_list = flag_list.p;
+        a.rs_d2 = rs_d2.p;
+        a.rs_idx = rs_idx.p;
+        a.cand_cnt = cand_cnt.p;
+        a.cand = cand.p;
+        a.snap_status = snap_status.p;
+        a.snap_yaw = snap_yaw.p;
+        a.rs.order = r_order.p;
+        a.rs.rep = r_rep.p;
+        a.rs.repyaw = r_repyaw.p;
+        a.lit_scratch = lit_scratch.p;
+        return a;
     }
 };
 
@@ -184,7 +209,10 @@ int check_ctx(pp_ctx* c, bool need_scene, bool need_rrt) {
     return PP_OK;
 }
 
+// The window pipeline is compiled for window sizes that are multiples of 256 (nn_scan sample
+// blocks); any requested K runs inside a buffer of round_up(K, 256).
 int ensure_window(pp_ctx* c, int K) {
+    K = (K + 255) & ~255;
     if (K <= c->Kcap) return PP_OK;
     const size_t k = (size_t)K;
     PP_HIP(c->wsx.reserve(k));
@@ -195,30 +223,20 @@ int ensure_window(pp_ctx* c, int K) {
     PP_HIP(c->nn_idx.reserve(k));
     PP_HIP(c->nn_d2.reserve(k));
     PP_HIP(c->flag_list.reserve(k));
-    PP_HIP(c->counters.reserve(2));
+    PP_HIP(c->rs_d2.reserve(k * kMaxChunks));
+    PP_HIP(c->rs_idx.reserve(k * kMaxChunks));
     PP_HIP(c->cand_cnt.reserve(k));
     PP_HIP(c->cand.reserve(k * kCandCap));
     PP_HIP(c->snap_status.reserve(k));
     PP_HIP(c->snap_yaw.reserve(k));
-    PP_HIP(c->spec_status.reserve(k * kCandCap));
-    PP_HIP(c->spec_yaw.reserve(k * kCandCap));
+    PP_HIP(c->r_order.reserve(k * kCandCap));
+    PP_HIP(c->r_rep.reserve(k));
+    PP_HIP(c->r_repyaw.reserve(k));
     PP_HIP(c->tasks.reserve(k));
     PP_HIP(c->task_status.reserve(k));
     PP_HIP(c->task_yaw.reserve(k));
-    PP_HIP(c->commits.reserve(k));
-    PP_HIP(c->h_counters.reserve(2));
-    PP_HIP(c->h_cand_cnt.reserve(k));
-    PP_HIP(c->h_nn_idx.reserve(k));
-    PP_HIP(c->h_snap_status.reserve(k));
-    PP_HIP(c->h_snap_yaw.reserve(k));
-    PP_HIP(c->h_d2.reserve(k));
-    PP_HIP(c->h_cand.reserve(k * kCandCap));
-    PP_HIP(c->h_spec_status.reserve(k * kCandCap));
-    PP_HIP(c->h_spec_yaw.reserve(k * kCandCap));
     PP_HIP(c->h_tasks.reserve(k));
-    PP_HIP(c->h_task_status.reserve(k));
-    PP_HIP(c->h_task_yaw.reserve(k));
-    PP_HIP(c->h_commits.reserve(k));
+    PP_HIP(c->lit_scratch.reserve((size_t)(kResolveThreads / 64) * 3 * kLiteralCap));
     c->Kcap = K;
     return PP_OK;
 }
@@ -237,6 +255,7 @@ int grow_copy(pp_ctx* c, DBuf<T>& b, size_t old_n, size_t new_cap) {
 
 int ensure_tree(pp_ctx* c, int64_t need) {
     if (need <= c->cap) return PP_OK;
+    if (need > (int64_t)0x7fff0000) return set_err(PP_ERR_CAPACITY, "tree larger than 2^31 nodes");
     int64_t nc = std::max<int64_t>(need, c->cap * 2);
     nc = std::max<int64_t>(nc, 1024);
     int r;
@@ -250,223 +269,12 @@ int ensure_tree(pp_ctx* c, int64_t need) {
     return PP_OK;
 }
 
-int ensure_literal_scratch(pp_ctx* c) {
-    PP_HIP(c->lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
-    return PP_OK;
-}
-
-double sample_x(const pp_ctx* c, int64_t it) {
-    return gen_range(c->seed, 2 * (uint64_t)it, c->minx, c->maxx);
-}
-double sample_y(const pp_ctx* c, int64_t it) {
-    return gen_range(c->seed, 2 * (uint64_t)it + 1, c->miny, c->maxy);
-}
-
-// One speculative window of W iterations starting at c->it.  Consumes W_eff <= W iterations.
-int run_window(pp_ctx* c, int W, int64_t* consumed, int64_t* accepted) {
-    int r;
-    if ((r = ensure_window(c, std::max(W, c->K)))) return r;
-    if ((r = ensure_tree(c, c->n + W))) return r;
-    hipStream_t st = c->stream;
-    const SceneDev sc = c->scene_dev();
-    const TreeDev tr = c->tree_dev();
-
-    PP_HIP(launch_sample(st, c->seed, c->it, W, c->minx, c->maxx, c->miny, c->maxy, c->wsx.p,
-                         c->wsy.p));
-    PP_HIP(launch_nn(st, tr, c->wsx.p, c->wsy.p, W, c->Kcap, c->pbest.p, c->psecond.p, c->pidx.p,
-                     c->eps_coord, c->nn_idx.p, c->nn_d2.p, c->flag_list.p, c->counters.p,
-                     c->prof ? c->ev[0] : nullptr, c->prof ? c->ev[1] : nullptr));
-    PP_HIP(launch_pairs(st, c->wsx.p, c->wsy.p, c->nn_d2.p, W, c->cand_cnt.p, c->cand.p,
-                        c->counters.p + 1));
-    if (c->prof) PP_HIP(hipEventRecord(c->ev[2], st));
-    PP_HIP(launch_steer_window(st, sc, tr, c->wsx.p, c->wsy.p, c->nn_idx.p, c->cand.p,
-                               c->counters.p + 1, W, c->snap_status.p, c->snap_yaw.p,
-                               c->spec_status.p, c->spec_yaw.p));
-    if (c->prof) PP_HIP(hipEventRecord(c->ev[3], st));
-    const size_t w = (size_t)W;
-    PP_HIP(hipMemcpyAsync(c->h_counters.p, c->counters.p, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-    PP_HIP(hipMemcpyAsync(c->h_cand_cnt.p, c->cand_cnt.p, w * sizeof(int), hipMemcpyDeviceToHost, st));
-    PP_HIP(hipMemcpyAsync(c->h_nn_idx.p, c->nn_idx.p, w * sizeof(int), hipMemcpyDeviceToHost, st));
-    PP_HIP(hipMemcpyAsync(c->h_snap_status.p, c->snap_status.p, w * sizeof(int), hipMemcpyDeviceToHost, st));
-    PP_HIP(hipMemcpyAsync(c->h_snap_yaw.p, c->snap_yaw.p, w * sizeof(double), hipMemcpyDeviceToHost, st));
-    const size_t pre = std::min<size_t>(kPrefetch, w * kCandCap);
-    PP_HIP(hipMemcpyAsync(c->h_cand.p, c->cand.p, pre * sizeof(CandEntry), hipMemcpyDeviceToHost, st));
-    PP_HIP(hipMemcpyAsync(c->h_spec_status.p, c->spec_status.p, pre * sizeof(int), hipMemcpyDeviceToHost, st));
-    PP_HIP(hipMemcpyAsync(c->h_spec_yaw.p, c->spec_yaw.p, pre * sizeof(double), hipMemcpyDeviceToHost, st));
-    PP_HIP(hipStreamSynchronize(st));
-    const int nflag = c->h_counters.p[0];
-    const int ncomp = c->h_counters.p[1];
-    if ((size_t)ncomp > pre) {
-        const size_t rest = (size_t)ncomp - pre;
-        PP_HIP(hipMemcpyAsync(c->h_cand.p + pre, c->cand.p + pre, rest * sizeof(CandEntry), hipMemcpyDeviceToHost, st));
-        PP_HIP(hipMemcpyAsync(c->h_spec_status.p + pre, c->spec_status.p + pre, rest * sizeof(int), hipMemcpyDeviceToHost, st));
-        PP_HIP(hipMemcpyAsync(c->h_spec_yaw.p + pre, c->spec_yaw.p + pre, rest * sizeof(double), hipMemcpyDeviceToHost, st));
-        PP_HIP(hipStreamSynchronize(st));
+int ensure_events(pp_ctx* c, size_t count) {
+    while (c->ev.size() < count) {
+        hipEvent_t e;
+        PP_HIP(hipEventCreate(&e));
+        c->ev.push_back(e);
     }
-    c->stats.windows++;
-    c->stats.nn_flagged += nflag;
-    c->stats.node_evals += (int64_t)W * c->n;
-    if (c->prof) {
-        float ms = 0.f;
-        PP_HIP(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
-        c->stats.nn_scan_ms += ms;
-        c->stats.nn_scan_launches++;
-        PP_HIP(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
-        c->stats.steer_ms += ms;
-        c->stats.steer_launches++;
-    }
-
-    // ---- group candidate entries per sample, each list in (d2, i) order
-    const CandEntry* E = c->h_cand.p;
-    std::vector<int> off(w + 1, 0), order(ncomp);
-    for (int e = 0; e < ncomp; ++e) off[E[e].j + 1]++;
-    for (size_t j = 0; j < w; ++j) off[j + 1] += off[j];
-    {
-        std::vector<int> fill(off.begin(), off.end() - 1);
-        for (int e = 0; e < ncomp; ++e) order[fill[E[e].j]++] = e;
-    }
-    for (size_t j = 0; j < w; ++j)
-        if (off[j + 1] - off[j] > 1)
-            std::sort(order.begin() + off[j], order.begin() + off[j + 1], [&](int a, int b) {
-                if (E[a].d2 != E[b].d2) return E[a].d2 < E[b].d2;
-                return E[a].i < E[b].i;
-            });
-
-    // ---- sequential-consistency resolve
-    std::vector<int8_t> state(w, 0);  // 0 unresolved, 1 accepted, 2 rejected
-    std::vector<int> par_win(w, -1);  // -1: the snapshot NN, else the window sample index
-    std::vector<double> yaw(w, 0.0);
-    std::vector<int8_t> rep_have(w, 0), rep_lit(w, 0);
-    std::vector<int> rep_status(w, 0);
-    std::vector<double> rep_yaw(w, 0.0);
-    int W_eff = W;
-    std::vector<int> need_j, need_par;
-    std::vector<int8_t> need_lit;
-    for (;;) {
-        need_j.clear();
-        need_par.clear();
-        need_lit.clear();
-        for (int j = 0; j < W_eff; ++j) {
-            if (state[j]) continue;
-            if (c->h_cand_cnt.p[j] > kCandCap) {  // list incomplete: stop the window here
-                W_eff = j;
-                c->stats.truncations++;
-                break;
-            }
-            int parent = -1, slot = -1;
-            bool blocked = false;
-            for (int q = off[j]; q < off[j + 1]; ++q) {
-                const int e = order[q];
-                const int i = E[e].i;
-                if (state[i] == 1) {
-                    parent = i;
-                    slot = e;
-                    break;
-                }
-                if (state[i] == 0) {
-                    blocked = true;
-                    break;
-                }
-            }
-            if (blocked) continue;
-            int status = -1;
-            double y = 0.0;
-            if (rep_have[j]) {
-                status = rep_status[j];
-                y = rep_yaw[j];
-            } else if (parent < 0) {
-                status = c->h_snap_status.p[j];
-                y = c->h_snap_yaw.p[j];
-            } else if (par_win[parent] < 0) {
-                status = c->h_spec_status.p[slot];
-                y = c->h_spec_yaw.p[slot];
-            }
-            if (status < 0) {
-                need_j.push_back(j);
-                need_par.push_back(parent);
-                need_lit.push_back(0);
-                continue;
-            }
-            if (status == kLiteral) {
-                if (rep_lit[j]) return set_err(PP_ERR_HIP, "literal steer path returned kLiteral");
-                need_j.push_back(j);
-                need_par.push_back(parent);
-                need_lit.push_back(1);
-                continue;
-            }
-            if (status == kError)
-                return set_err(PP_ERR_STEER_OVERFLOW,
-                               "generate_local_course would index past n_point (the reference panics)");
-            state[j] = status == kAccept ? 1 : 2;
-            par_win[j] = parent;
-            yaw[j] = y;
-        }
-        if (need_j.empty()) break;
-        // repair launch: (child j, its final parent) with the parent's true pose
-        const int nt = (int)need_j.size();
-        bool any_lit = false;
-        for (int t = 0; t < nt; ++t) {
-            const int j = need_j[t], p = need_par[t];
-            SteerTask tk;
-            tk.x = sample_x(c, c->it + j);
-            tk.y = sample_y(c, c->it + j);
-            if (p < 0) {
-                tk.pnode = c->h_nn_idx.p[j];
-                tk.px = tk.py = tk.pyaw = 0.0;
-            } else {
-                tk.pnode = -1;
-                tk.px = sample_x(c, c->it + p);
-                tk.py = sample_y(c, c->it + p);
-                tk.pyaw = yaw[p];
-            }
-            tk.literal = need_lit[t];
-            any_lit |= tk.literal != 0;
-            c->h_tasks.p[t] = tk;
-        }
-        if (any_lit && (r = ensure_literal_scratch(c))) return r;
-        PP_HIP(hipMemcpyAsync(c->tasks.p, c->h_tasks.p, nt * sizeof(SteerTask), hipMemcpyHostToDevice, st));
-        PP_HIP(launch_steer_tasks(st, sc, tr, c->tasks.p, nt, c->task_status.p, c->task_yaw.p,
-                                  any_lit ? c->lit_scratch.p : nullptr));
-        PP_HIP(hipMemcpyAsync(c->h_task_status.p, c->task_status.p, nt * sizeof(int), hipMemcpyDeviceToHost, st));
-        PP_HIP(hipMemcpyAsync(c->h_task_yaw.p, c->task_yaw.p, nt * sizeof(double), hipMemcpyDeviceToHost, st));
-        PP_HIP(hipStreamSynchronize(st));
-        for (int t = 0; t < nt; ++t) {
-            const int j = need_j[t];
-            rep_have[j] = 1;
-            rep_status[j] = c->h_task_status.p[t];
-            rep_yaw[j] = c->h_task_yaw.p[t];
-            if (need_lit[t]) rep_lit[j] = 1;
-        }
-        c->stats.repair_rounds++;
-        c->stats.repairs += nt;
-        for (int t = 0; t < nt; ++t) c->stats.literal_repairs += need_lit[t];
-    }
-
-    // ---- commit: insert the accepted samples in sequential order (rrt.rs:586-589)
-    std::vector<int> node_of(W_eff, -1);
-    int nnew = 0;
-    for (int j = 0; j < W_eff; ++j) {
-        if (state[j] != 1) continue;
-        node_of[j] = (int)c->n + nnew;
-        CommitEntry ce;
-        ce.j = j;
-        ce.parent = par_win[j] < 0 ? -1 : node_of[par_win[j]];
-        ce.yaw = yaw[j];
-        c->h_commits.p[nnew++] = ce;
-    }
-    if (nnew) {
-        PP_HIP(hipMemcpyAsync(c->commits.p, c->h_commits.p, nnew * sizeof(CommitEntry), hipMemcpyHostToDevice, st));
-        PP_HIP(launch_append(st, c->commits.p, nnew, (int)c->n, c->wsx.p, c->wsy.p, c->nn_idx.p,
-                             c->x32.p, c->y32.p, c->X.p, c->Y.p, c->YAW.p, c->PAR.p));
-        // the pinned commit buffer is rewritten by the next window: wait for the copy
-        PP_HIP(hipStreamSynchronize(st));
-    }
-    c->n += nnew;
-    c->it += W_eff;
-    c->stats.iterations += W_eff;
-    c->stats.accepted += nnew;
-    *consumed = W_eff;
-    *accepted = nnew;
     return PP_OK;
 }
 
@@ -503,10 +311,12 @@ int pp_create(int device, pp_ctx** out) {
     pp_ctx* c = new pp_ctx();
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+    if (e == hipSuccess) e = c->d_state.reserve(1);
+    if (e == hipSuccess) e = c->d_api_state.reserve(1);
+    if (e == hipSuccess) e = c->h_state.reserve(2);
     if (e != hipSuccess) {
         delete c;
-        return set_err(PP_ERR_HIP, std::string("stream/event create: ") + hipGetErrorString(e));
+        return set_err(PP_ERR_HIP, std::string("context setup: ") + hipGetErrorString(e));
     }
     *out = c;
     return PP_OK;
@@ -652,6 +462,7 @@ int pp_rrt_new(pp_ctx* ctx, double sx, double sy, double syaw, double gx, double
     if (!(step_size > 0.0) || max_iter < 0)
         return set_err(PP_ERR_INVALID_ARGUMENT, "step_size must be > 0 and max_iter >= 0");
     ctx->has_rrt = false;
+    PP_HIP(hipStreamSynchronize(ctx->stream));
     ctx->n = 0;
     ctx->it = 0;
     ctx->start[0] = sx;
@@ -663,8 +474,10 @@ int pp_rrt_new(pp_ctx* ctx, double sx, double sy, double syaw, double gx, double
     ctx->max_iter = max_iter;
     ctx->step = step_size;
     ctx->seed = seed;
-    ctx->stats = pp_stats{};
+    ctx->nn_scan_ms = ctx->steer_ms = 0.0;
+    ctx->nn_scan_launches = ctx->steer_launches = 0;
     if ((r = ensure_tree(ctx, std::max<int64_t>(capacity, 1024)))) return r;
+    if ((r = ensure_window(ctx, ctx->K))) return r;
     // f32 screen tolerance: coordinates are rounded to f32 with error <= max|c| * 2^-24
     double mx = std::max({std::fabs(ctx->minx), std::fabs(ctx->maxx), std::fabs(ctx->miny),
                           std::fabs(ctx->maxy), std::fabs(sx), std::fabs(sy)});
@@ -678,15 +491,20 @@ int pp_rrt_new(pp_ctx* ctx, double sx, double sy, double syaw, double gx, double
     PP_HIP(hipMemcpy(ctx->Y.p, &sy, sizeof(double), hipMemcpyHostToDevice));
     PP_HIP(hipMemcpy(ctx->YAW.p, &syaw, sizeof(double), hipMemcpyHostToDevice));
     PP_HIP(hipMemcpy(ctx->PAR.p, &par, sizeof(int), hipMemcpyHostToDevice));
+    DevState s{};
+    s.it = 0;
+    s.n = 1;
+    PP_HIP(hipMemcpy(ctx->d_state.p, &s, sizeof(DevState), hipMemcpyHostToDevice));
+    ctx->h_state.p[0] = s;
     ctx->n = 1;
-    if ((r = ensure_window(ctx, ctx->K))) return r;
     ctx->has_rrt = true;
     return PP_OK;
 }
 
 int pp_rrt_set_window(pp_ctx* ctx, int k) {
     if (!ctx) return set_err(PP_ERR_INVALID_ARGUMENT, "null context");
-    if (k < 1 || k > (1 << 20)) return set_err(PP_ERR_INVALID_ARGUMENT, "window must be in [1, 2^20]");
+    if (k < 1 || k > kMaxWindow)
+        return set_err(PP_ERR_INVALID_ARGUMENT, "window must be in [1, 4096] (resolve state lives in LDS)");
     ctx->K = k;
     return PP_OK;
 }
@@ -695,15 +513,46 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
     int r = check_ctx(ctx, true, true);
     if (r) return r;
     if (n_iter < 0) return set_err(PP_ERR_INVALID_ARGUMENT, "n_iter < 0");
-    int64_t acc_total = 0, left = n_iter;
-    while (left > 0) {
-        const int W = (int)std::min<int64_t>(left, ctx->K);
-        int64_t used = 0, acc = 0;
-        if ((r = run_window(ctx, W, &used, &acc))) return r;
-        left -= used;
-        acc_total += acc;
+    if ((r = ensure_window(ctx, ctx->K))) return r;
+    const int64_t target = ctx->it + n_iter;
+    const int64_t n_before = ctx->n;
+    hipStream_t st = ctx->stream;
+    while (ctx->it < target) {
+        const int K = ctx->K;
+        const int64_t nw64 = std::min<int64_t>((target - ctx->it + K - 1) / K, kMaxBatch);
+        const int nw = (int)nw64;
+        if ((r = ensure_tree(ctx, ctx->n + (int64_t)nw * K))) return r;
+        WindowArgs a = ctx->window_args(ctx->d_state.p);
+        a.K = K;
+        a.target = target;
+        if (ctx->prof && (r = ensure_events(ctx, 4 * (size_t)nw))) return r;
+        const int64_t windows_before = ctx->h_state.p[0].windows;
+        for (int w = 0; w < nw; ++w)
+            PP_HIP(launch_window(st, a, ctx->prof ? &ctx->ev[4 * w] : nullptr));
+        PP_HIP(hipMemcpyAsync(ctx->h_state.p, ctx->d_state.p, sizeof(DevState), hipMemcpyDeviceToHost, st));
+        PP_HIP(hipStreamSynchronize(st));
+        const DevState& s = ctx->h_state.p[0];
+        if (s.error)
+            return set_err(PP_ERR_STEER_OVERFLOW,
+                           "generate_local_course would index past n_point (the reference panics)");
+        if (s.it <= ctx->it && nw > 0 && s.windows == windows_before)
+            return set_err(PP_ERR_HIP, "extend made no progress");
+        if (ctx->prof) {
+            const int64_t active = std::min<int64_t>(s.windows - windows_before, nw);
+            for (int64_t w = 0; w < active; ++w) {
+                float ms = 0.f;
+                PP_HIP(hipEventElapsedTime(&ms, ctx->ev[4 * w], ctx->ev[4 * w + 1]));
+                ctx->nn_scan_ms += ms;
+                PP_HIP(hipEventElapsedTime(&ms, ctx->ev[4 * w + 2], ctx->ev[4 * w + 3]));
+                ctx->steer_ms += ms;
+            }
+            ctx->nn_scan_launches += active;
+            ctx->steer_launches += active;
+        }
+        ctx->it = s.it;
+        ctx->n = s.n;
     }
-    if (n_accepted) *n_accepted = acc_total;
+    if (n_accepted) *n_accepted = ctx->n - n_before;
     return PP_OK;
 }
 
@@ -753,14 +602,17 @@ int pp_rrt_get_nearest_node_batch(pp_ctx* ctx, const double* qx, const double* q
     if (r) return r;
     if (k < 0 || (k > 0 && (!qx || !qy || !idx))) return set_err(PP_ERR_INVALID_ARGUMENT, "bad arguments");
     hipStream_t st = ctx->stream;
-    const TreeDev tr = ctx->tree_dev();
+    WindowArgs a = ctx->window_args(ctx->d_api_state.p);
     for (int b = 0; b < k; b += ctx->Kcap) {
         const int nb = std::min(ctx->Kcap, k - b);
+        DevState* hs = &ctx->h_state.p[1];
+        *hs = DevState{};
+        hs->W = nb;
+        hs->n = (int)ctx->n;
+        PP_HIP(hipMemcpyAsync(ctx->d_api_state.p, hs, sizeof(DevState), hipMemcpyHostToDevice, st));
         PP_HIP(hipMemcpyAsync(ctx->wsx.p, qx + b, nb * sizeof(double), hipMemcpyHostToDevice, st));
         PP_HIP(hipMemcpyAsync(ctx->wsy.p, qy + b, nb * sizeof(double), hipMemcpyHostToDevice, st));
-        PP_HIP(launch_nn(st, tr, ctx->wsx.p, ctx->wsy.p, nb, ctx->Kcap, ctx->pbest.p,
-                         ctx->psecond.p, ctx->pidx.p, ctx->eps_coord, ctx->nn_idx.p, ctx->nn_d2.p,
-                         ctx->flag_list.p, ctx->counters.p, nullptr, nullptr));
+        PP_HIP(launch_nearest(st, a));
         PP_HIP(hipMemcpyAsync(idx + b, ctx->nn_idx.p, nb * sizeof(int), hipMemcpyDeviceToHost, st));
         if (d2) PP_HIP(hipMemcpyAsync(d2 + b, ctx->nn_d2.p, nb * sizeof(double), hipMemcpyDeviceToHost, st));
         PP_HIP(hipStreamSynchronize(st));
@@ -779,13 +631,14 @@ int pp_rrt_verify_node_batch(pp_ctx* ctx, const double* x, const double* y,
     hipStream_t st = ctx->stream;
     const SceneDev sc = ctx->scene_dev();
     const TreeDev tr = ctx->tree_dev();
+    std::vector<int> status(ctx->Kcap);
     for (int b = 0; b < k; b += ctx->Kcap) {
         const int nb = std::min(ctx->Kcap, k - b);
         for (int pass = 0; pass < 2; ++pass) {
             int nt = 0;
             std::vector<int> which;
             for (int i = 0; i < nb; ++i) {
-                if (pass == 1 && ctx->h_task_status.p[i] != kLiteral) continue;
+                if (pass == 1 && status[i] != kLiteral) continue;
                 SteerTask tk;
                 tk.x = x[b + i];
                 tk.y = y[b + i];
@@ -796,12 +649,13 @@ int pp_rrt_verify_node_batch(pp_ctx* ctx, const double* x, const double* y,
                 which.push_back(i);
             }
             if (nt == 0) break;
-            if (pass == 1 && (r = ensure_literal_scratch(ctx))) return r;
+            if (pass == 1)
+                PP_HIP(ctx->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
             std::vector<int> stv(nt);
             std::vector<double> yv(nt);
             PP_HIP(hipMemcpyAsync(ctx->tasks.p, ctx->h_tasks.p, nt * sizeof(SteerTask), hipMemcpyHostToDevice, st));
             PP_HIP(launch_steer_tasks(st, sc, tr, ctx->tasks.p, nt, ctx->task_status.p,
-                                      ctx->task_yaw.p, pass ? ctx->lit_scratch.p : nullptr));
+                                      ctx->task_yaw.p, pass ? ctx->api_lit_scratch.p : nullptr));
             PP_HIP(hipMemcpyAsync(stv.data(), ctx->task_status.p, nt * sizeof(int), hipMemcpyDeviceToHost, st));
             PP_HIP(hipMemcpyAsync(yv.data(), ctx->task_yaw.p, nt * sizeof(double), hipMemcpyDeviceToHost, st));
             PP_HIP(hipStreamSynchronize(st));
@@ -809,7 +663,7 @@ int pp_rrt_verify_node_batch(pp_ctx* ctx, const double* x, const double* y,
                 const int i = which[t];
                 if (stv[t] == kError)
                     return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
-                ctx->h_task_status.p[i] = stv[t];
+                status[i] = stv[t];
                 ok[b + i] = stv[t] == kAccept ? 1 : 0;
                 if (yaw) yaw[b + i] = yv[t];
             }
@@ -820,13 +674,46 @@ int pp_rrt_verify_node_batch(pp_ctx* ctx, const double* x, const double* y,
 
 int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out) {
     if (!ctx || !out) return set_err(PP_ERR_INVALID_ARGUMENT, "null argument");
-    *out = ctx->stats;
+    int r = check_ctx(ctx, false, false);
+    if (r) return r;
+    pp_stats s{};
+    if (ctx->has_rrt) {
+        PP_HIP(hipMemcpyAsync(ctx->h_state.p, ctx->d_state.p, sizeof(DevState), hipMemcpyDeviceToHost, ctx->stream));
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+        const DevState& d = ctx->h_state.p[0];
+        s.iterations = d.iterations;
+        s.accepted = d.accepted;
+        s.windows = d.windows;
+        s.truncations = d.truncations;
+        s.repair_rounds = d.repair_rounds;
+        s.repairs = d.repairs;
+        s.literal_repairs = d.literal_repairs;
+        s.nn_flagged = d.nn_flagged;
+        s.node_evals = d.node_evals;
+    }
+    s.nn_scan_ms = ctx->nn_scan_ms;
+    s.nn_scan_launches = ctx->nn_scan_launches;
+    s.steer_ms = ctx->steer_ms;
+    s.steer_launches = ctx->steer_launches;
+    *out = s;
     return PP_OK;
 }
 
 int pp_rrt_reset_stats(pp_ctx* ctx) {
-    if (!ctx) return set_err(PP_ERR_INVALID_ARGUMENT, "null context");
-    ctx->stats = pp_stats{};
+    int r = check_ctx(ctx, false, false);
+    if (r) return r;
+    if (ctx->has_rrt) {
+        PP_HIP(hipMemcpyAsync(ctx->h_state.p, ctx->d_state.p, sizeof(DevState), hipMemcpyDeviceToHost, ctx->stream));
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+        DevState d = ctx->h_state.p[0];
+        d.iterations = d.accepted = d.windows = d.truncations = d.repair_rounds = d.repairs =
+            d.literal_repairs = d.nn_flagged = d.node_evals = 0;
+        ctx->h_state.p[0] = d;
+        PP_HIP(hipMemcpyAsync(ctx->d_state.p, ctx->h_state.p, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    ctx->nn_scan_ms = ctx->steer_ms = 0.0;
+    ctx->nn_scan_launches = ctx->steer_launches = 0;
     return PP_OK;
 }
 

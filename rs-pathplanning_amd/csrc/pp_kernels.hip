@@ -1,15 +1,16 @@
 // pp_kernels.hip — hand-written CDNA4 (gfx950) kernels of the RRT extend hot path.
 //
-//   nn_scan          K samples x N tree nodes, f32 SoA screen (s_load-broadcast nodes, 4 queries
-//                    per lane, exact top-2 per lane, LDS merge of the 4 waves)       rrt.rs:378-391
-//   nn_finalize      merge the node-chunk partials, flag near-ties, exact f64 d^2 of the winner
-//   nn_rescan        exact f64 brute force for the flagged (near-tie) samples only
-//   window_pairs     per sample: the earlier samples of the same window that are strictly nearer
-//                    than its snapshot NN (the candidates of the sequential-consistency resolve)
-//   steer_slots      one wave per (sample, parent) slot: compute_yaw + Dubins steer + sampled-arc
-//                    collision check, fused, f64                rrt.rs:169-175,414-426, dubins.rs
-//   steer_tasks      the same for an explicit task list (repairs; literal single-lane path)
-//   dubins_batch     one lane per DubinsConfig: dubins_path_planning, literal (API surface)
+// Window pipeline (one speculative window of K iterations, device-resident state):
+//   window_begin   Space::rand_point for the window's iterations (seeded stream)   rrt.rs:139-146
+//   nn_scan        K samples x N tree nodes, f32 SoA screen: scalar-broadcast nodes, 4 samples
+//                  per lane, exact per-lane top-2, XCD-aware chunk mapping         rrt.rs:378-391
+//   nn_finalize    merge the 64 chunk partials, flag near-ties, exact f64 d2 of the winner
+//   nn_rescan      exact f64 brute force of the flagged samples, chunk-parallel
+//   window_pairs   earlier samples of the same window strictly nearer than the snapshot NN
+//   steer_window   one wave per (sample, parent): compute_yaw + Dubins steer + sampled-arc
+//                  collision, fused, f64                        rrt.rs:169-175,414-426, dubins.rs
+//   resolve        one workgroup: sequential-consistency replay, repairs, in-order insert
+// API kernels: steer_tasks (verify_node batch), nn_fix (nearest batch), dubins_batch.
 //
 // No MFMA anywhere: there is no dense contraction on this path.
 #include <hip/hip_runtime.h>
@@ -203,54 +204,8 @@ __device__ int steer_collide_literal(const SceneDev& sc, double x, double y, dou
     return __shfl(st, 0);
 }
 
-// ------------------------------------------------------------------------- steer kernels
-
-// Tasks [0, W): sample j → its snapshot NN (tree node nn_idx[j]).  Tasks [W, W + *ncomp):
-// candidate entry e: sample E.j → window sample E.i, with E.i's yaw taken under ITS snapshot
-// parent (the speculation the host resolve validates).
-__global__ __launch_bounds__(256) void steer_window_kernel(
-    SceneDev sc, TreeDev tr, const double* __restrict__ wsx, const double* __restrict__ wsy,
-    const int* __restrict__ nn_idx, const CandEntry* __restrict__ cand,
-    const int* __restrict__ ncomp, int W, int* __restrict__ snap_status,
-    double* __restrict__ snap_yaw, int* __restrict__ spec_status, double* __restrict__ spec_yaw) {
-    const int lane = threadIdx.x & 63;
-    const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    const int total = W + *ncomp;
-    for (int t = gw; t < total; t += nw) {
-        int j;
-        double px, py, pyaw;
-        if (t < W) {
-            j = t;
-            const int p = nn_idx[j];
-            px = tr.x[p];
-            py = tr.y[p];
-            pyaw = tr.yaw[p];
-        } else {
-            const CandEntry ce = cand[t - W];
-            j = ce.j;
-            const int ni = nn_idx[ce.i];
-            px = wsx[ce.i];
-            py = wsy[ce.i];
-            pyaw = atan2(tr.y[ni] - py, tr.x[ni] - px);
-        }
-        const double x = wsx[j], y = wsy[j];
-        const double yaw = atan2(py - y, px - x);  // compute_yaw, rrt.rs:267-271
-        const int st = steer_collide_fast(sc, x, y, yaw, px, py, pyaw);
-        if (lane == 0) {
-            if (t < W) {
-                snap_status[t] = st;
-                snap_yaw[t] = yaw;
-            } else {
-                spec_status[t - W] = st;
-                spec_yaw[t - W] = yaw;
-            }
-        }
-    }
-}
-
-// Explicit tasks (repairs, the verify_node API); waves <= kLiteralWaves so each wave owns one
-// literal scratch buffer.
+// Explicit tasks (the verify_node API); waves <= kLiteralWaves so each wave owns one literal
+// scratch buffer.
 __global__ __launch_bounds__(256) void steer_tasks_kernel(SceneDev sc, TreeDev tr,
                                                           const SteerTask* __restrict__ tasks,
                                                           int n, int* __restrict__ out_status,
@@ -269,55 +224,19 @@ __global__ __launch_bounds__(256) void steer_tasks_kernel(SceneDev sc, TreeDev t
             pyaw = tr.yaw[tk.pnode];
         }
         const double yaw = atan2(py - tk.y, px - tk.x);
-        int st;
+        int s;
         if (tk.literal && bx)
-            st = steer_collide_literal(sc, tk.x, tk.y, yaw, px, py, pyaw, bx, bx + kLiteralCap,
-                                       bx + 2 * kLiteralCap);
+            s = steer_collide_literal(sc, tk.x, tk.y, yaw, px, py, pyaw, bx, bx + kLiteralCap,
+                                      bx + 2 * kLiteralCap);
         else if (tk.literal)
-            st = kError;
+            s = kError;
         else
-            st = steer_collide_fast(sc, tk.x, tk.y, yaw, px, py, pyaw);
+            s = steer_collide_fast(sc, tk.x, tk.y, yaw, px, py, pyaw);
         if (lane == 0) {
-            out_status[t] = st;
+            out_status[t] = s;
             out_yaw[t] = yaw;
         }
     }
-}
-
-// Space::rand_point for iterations [it0, it0 + W): x = draw 2*it, y = draw 2*it + 1
-// (rrt.rs:139-146 on the seeded stream).
-__global__ __launch_bounds__(256) void sample_kernel(uint64_t seed, int64_t it0, int W, double minx,
-                                                     double maxx, double miny, double maxy,
-                                                     double* __restrict__ wsx,
-                                                     double* __restrict__ wsy) {
-    const int j = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (j >= W) return;
-    const uint64_t it = (uint64_t)(it0 + j);
-    wsx[j] = gen_range(seed, 2 * it, minx, maxx);
-    wsy[j] = gen_range(seed, 2 * it + 1, miny, maxy);
-}
-
-// insert (rrt.rs:586-589) of the resolved, accepted window samples, in sequential order
-__global__ __launch_bounds__(256) void append_kernel(const CommitEntry* __restrict__ ents, int n_new,
-                                                     int n0, const double* __restrict__ wsx,
-                                                     const double* __restrict__ wsy,
-                                                     const int* __restrict__ nn_idx,
-                                                     float* __restrict__ x32,
-                                                     float* __restrict__ y32, double* __restrict__ X,
-                                                     double* __restrict__ Y,
-                                                     double* __restrict__ YAW,
-                                                     int* __restrict__ PAR) {
-    const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (r >= n_new) return;
-    const CommitEntry e = ents[r];
-    const int node = n0 + r;
-    const double x = wsx[e.j], y = wsy[e.j];
-    X[node] = x;
-    Y[node] = y;
-    x32[node] = (float)x;
-    y32[node] = (float)y;
-    YAW[node] = e.yaw;
-    PAR[node] = e.parent >= 0 ? e.parent : nn_idx[e.j];
 }
 
 // --------------------------------------------------------------------------------- dubins
@@ -344,10 +263,49 @@ __global__ __launch_bounds__(64) void dubins_batch_kernel(const double* __restri
     status_out[i] = r;
 }
 
-// ------------------------------------------------------------------------- nearest neighbour
+// ------------------------------------------------------------------------- window pipeline
+//
+// One speculative window = window_begin → nn_scan → nn_finalize → nn_rescan → window_pairs →
+// steer_window → resolve, all reading the device-resident DevState, so the host enqueues windows
+// back to back and synchronises once per batch.
 
-constexpr int kQPL = 4;                // samples per lane
-constexpr int kQPB = 64 * kQPL;        // samples per workgroup (all 4 waves share them)
+constexpr int kQPL = 4;          // samples per lane in nn_scan
+constexpr int kQPB = 64 * kQPL;  // samples per nn_scan workgroup (all 4 waves share them)
+
+__host__ __device__ inline int nn_chunk_len(int n) {
+    int cl = (n + kMaxChunks - 1) / kMaxChunks;
+    if (cl < 512) cl = 512;
+    return (cl + 31) & ~31;
+}
+__host__ __device__ inline int nn_chunks(int n) {
+    const int cl = nn_chunk_len(n);
+    return (n + cl - 1) / cl;
+}
+
+// Space::rand_point for iterations [it, it + W) of the window (rrt.rs:139-146, seeded: Q7):
+// x = draw 2*it, y = draw 2*it + 1.  Also opens the window: W = min(K, target - it).
+__global__ __launch_bounds__(256) void window_begin_kernel(DevState* st, int K, int64_t target,
+                                                           uint64_t seed,
+                                                           double minx, double maxx, double miny,
+                                                           double maxy, double* __restrict__ wsx,
+                                                           double* __restrict__ wsy,
+                                                           int* __restrict__ cand_cnt) {
+    const int64_t it = st->it;
+    const int64_t rem = target - it;
+    const int W = (rem <= 0 || st->error) ? 0 : (rem < K ? (int)rem : K);
+    const int j = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (j == 0) {
+        st->W = W;
+        st->flag_count = 0;
+        st->ncomp = 0;
+    }
+    if (j < W) {
+        const uint64_t itj = (uint64_t)(it + j);
+        wsx[j] = gen_range(seed, 2 * itj, minx, maxx);
+        wsy[j] = gen_range(seed, 2 * itj + 1, miny, maxy);
+        cand_cnt[j] = 0;
+    }
+}
 
 struct Top2 {
     float b, s;
@@ -369,35 +327,44 @@ __device__ inline Top2 merge_top2(Top2 a, Top2 c) {
     return r;
 }
 
-// grid (ceil(nq / 256), n_chunks), 256 threads.  Each wave scans a quarter of the chunk; tree
-// coordinates are wave-uniform loads (scalar cache, broadcast as SGPR operands) and every lane
-// holds 4 samples, so one node feeds 4 distance evaluations per lane.
-__global__ __launch_bounds__(256) void nn_scan_kernel(const float* __restrict__ nx,
-                                                      const float* __restrict__ ny, int n_nodes,
+// RRT::get_nearest_node screen (rrt.rs:378-391): f32 SoA nodes x W samples.  Grid = nqb * 64
+// blocks (nqb sample blocks x 64 node chunks), mapped XCD-aware so the nqb blocks that stream the
+// same node chunk share one XCD's L2.  Each wave scans a quarter of the chunk; node coordinates
+// are wave-uniform scalar loads used as SGPR operands; every lane holds 4 samples and keeps an
+// exact per-lane top-2 (best, second, index of best).
+__global__ __launch_bounds__(256) void nn_scan_kernel(const DevState* __restrict__ st,
+                                                      const float* __restrict__ nx,
+                                                      const float* __restrict__ ny,
                                                       const double* __restrict__ qx,
-                                                      const double* __restrict__ qy, int nq,
-                                                      int chunk_len, int stride,
-                                                      float* __restrict__ pbest,
+                                                      const double* __restrict__ qy, int nqb,
+                                                      int stride, float* __restrict__ pbest,
                                                       float* __restrict__ psecond,
                                                       int* __restrict__ pidx) {
     __shared__ float s_b[4][kQPB];
     __shared__ float s_s[4][kQPB];
     __shared__ int s_i[4][kQPB];
+    const int W = st->W, n = st->n;
+    const int G = gridDim.x;  // multiple of 8 (kMaxChunks chunks per sample block)
+    const int b = blockIdx.x;
+    const int t = (b & 7) * (G >> 3) + (b >> 3);
+    const int qb = t % nqb, c = t / nqb;
+    const int chunk_len = nn_chunk_len(n);
+    const int c0 = c * chunk_len;
+    if (c0 >= n || qb * kQPB >= W) return;
+    const int c1 = min(c0 + chunk_len, n);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int qbase = blockIdx.x * kQPB;
+    const int qbase = qb * kQPB;
     float qxr[kQPL], qyr[kQPL], best[kQPL], second[kQPL];
     int bi[kQPL];
 #pragma unroll
     for (int r = 0; r < kQPL; ++r) {
         const int q = qbase + r * 64 + lane;
-        qxr[r] = q < nq ? (float)qx[q] : 0.0f;
-        qyr[r] = q < nq ? (float)qy[q] : 0.0f;
+        qxr[r] = q < W ? (float)qx[q] : 0.0f;
+        qyr[r] = q < W ? (float)qy[q] : 0.0f;
         best[r] = __builtin_inff();
         second[r] = __builtin_inff();
         bi[r] = -1;
     }
-    const int c0 = blockIdx.y * chunk_len;
-    const int c1 = min(c0 + chunk_len, n_nodes);
     const int per = (((c1 - c0) + 3) / 4 + 7) & ~7;
     // wave-uniform range: readfirstlane lets the compiler use scalar loads for the nodes
     const int w0 = __builtin_amdgcn_readfirstlane(min(c0 + wave * per, c1));
@@ -446,35 +413,61 @@ __global__ __launch_bounds__(256) void nn_scan_kernel(const float* __restrict__ 
         s_i[wave][r * 64 + lane] = bi[r];
     }
     __syncthreads();
-    // wave w merges sample group r = w across the 4 waves (ascending node ranges)
-    const int slot = wave * 64 + lane;
-    Top2 t{s_b[0][slot], s_s[0][slot], s_i[0][slot]};
+    const int slot = wave * 64 + lane;  // wave w merges sample group r = w across the 4 waves
+    Top2 tt{s_b[0][slot], s_s[0][slot], s_i[0][slot]};
 #pragma unroll
-    for (int w = 1; w < 4; ++w) t = merge_top2(t, Top2{s_b[w][slot], s_s[w][slot], s_i[w][slot]});
+    for (int w = 1; w < 4; ++w) tt = merge_top2(tt, Top2{s_b[w][slot], s_s[w][slot], s_i[w][slot]});
     const int q = qbase + slot;
-    if (q < nq) {
-        const size_t o = (size_t)blockIdx.y * stride + q;
-        pbest[o] = t.b;
-        psecond[o] = t.s;
-        pidx[o] = t.i;
+    if (q < W) {
+        const size_t o = (size_t)c * stride + q;
+        pbest[o] = tt.b;
+        psecond[o] = tt.s;
+        pidx[o] = tt.i;
     }
 }
 
-// one thread per sample: merge chunk partials, decide whether the f32 winner is certainly the
-// exact f64 winner (margin test against the f32 rounding bound), else queue an exact rescan.
+// 64 samples per workgroup: wave w merges chunks w, w+4, ... for its lane's sample, then wave 0
+// merges the 4 and decides whether the f32 winner is certainly the exact f64 winner (margin test
+// against the f32 rounding bound).  Certain: exact f64 d2 of the winner.  Else: queue for the
+// exact rescan, nn_idx = -(slot + 1).
 __global__ __launch_bounds__(256) void nn_finalize_kernel(
-    const float* __restrict__ pbest, const float* __restrict__ psecond,
-    const int* __restrict__ pidx, int n_chunks, int stride, int nq, const double* __restrict__ qx,
+    DevState* __restrict__ st, const float* __restrict__ pbest, const float* __restrict__ psecond,
+    const int* __restrict__ pidx, int stride, const double* __restrict__ qx,
     const double* __restrict__ qy, const double* __restrict__ X, const double* __restrict__ Y,
     double eps_coord, int* __restrict__ out_idx, double* __restrict__ out_d2,
-    int* __restrict__ flag_list, int* __restrict__ flag_count) {
-    const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (q >= nq) return;
-    Top2 t{pbest[q], psecond[q], pidx[q]};
-    for (int c = 1; c < n_chunks; ++c) {
-        const size_t o = (size_t)c * stride + q;
-        t = merge_top2(t, Top2{pbest[o], psecond[o], pidx[o]});
+    int* __restrict__ flag_list) {
+    __shared__ float s_b[4][64];
+    __shared__ float s_s[4][64];
+    __shared__ int s_i[4][64];
+    const int W = st->W, n = st->n;
+    if ((int)blockIdx.x * 64 >= W) return;
+    const int n_chunks = nn_chunks(n);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int q = blockIdx.x * 64 + lane;
+    Top2 t{__builtin_inff(), __builtin_inff(), -1};
+    if (q < W) {
+        constexpr int kPer = kMaxChunks / 4;
+        float vb[kPer], vs[kPer];
+        int vi[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {  // all loads in flight before the merge
+            const int c = wave + 4 * u;
+            const size_t o = (size_t)c * stride + q;
+            const bool ok = c < n_chunks;
+            vb[u] = ok ? pbest[o] : __builtin_inff();
+            vs[u] = ok ? psecond[o] : __builtin_inff();
+            vi[u] = ok ? pidx[o] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) t = merge_top2(t, Top2{vb[u], vs[u], vi[u]});
     }
+    s_b[wave][lane] = t.b;
+    s_s[wave][lane] = t.s;
+    s_i[wave][lane] = t.i;
+    __syncthreads();
+    if (wave != 0 || q >= W) return;
+#pragma unroll
+    for (int w = 1; w < 4; ++w) t = merge_top2(t, Top2{s_b[w][lane], s_s[w][lane], s_i[w][lane]});
     bool flag = t.i < 0 || !(t.b < __builtin_inff());
     if (!flag && t.s < __builtin_inff()) {
         const double D1 = sqrt((double)t.b), D2 = sqrt((double)t.s);
@@ -482,9 +475,9 @@ __global__ __launch_bounds__(256) void nn_finalize_kernel(
         flag = !(D2 - D1 > tau);
     }
     if (flag) {
-        const int e = atomicAdd(flag_count, 1);
-        flag_list[e] = q;
-        out_idx[q] = -1;
+        const int f = atomicAdd(&st->flag_count, 1);
+        flag_list[f] = q;
+        out_idx[q] = -(f + 1);
     } else {
         const double dx = qx[q] - X[t.i], dy = qy[q] - Y[t.i];
         out_idx[q] = t.i;
@@ -492,25 +485,29 @@ __global__ __launch_bounds__(256) void nn_finalize_kernel(
     }
 }
 
-// exact f64 brute force (lowest index wins ties) for the flagged samples; grid-stride over the
-// flagged list, one workgroup per sample.
-__global__ __launch_bounds__(256) void nn_rescan_kernel(const int* __restrict__ flag_list,
-                                                        const int* __restrict__ flag_count,
+// Exact f64 brute force for the flagged samples: grid (kMaxChunks node chunks, kRescanSlots);
+// workgroup (c, s) scans chunk c for flagged samples s, s + kRescanSlots, ... and writes the
+// chunk's (d2, lowest index) partial; final_nn merges the partials.
+__global__ __launch_bounds__(256) void nn_rescan_kernel(const DevState* __restrict__ st,
+                                                        const int* __restrict__ flag_list,
                                                         const double* __restrict__ qx,
                                                         const double* __restrict__ qy,
                                                         const double* __restrict__ X,
-                                                        const double* __restrict__ Y, int n,
-                                                        int* __restrict__ out_idx,
-                                                        double* __restrict__ out_d2) {
+                                                        const double* __restrict__ Y,
+                                                        double* __restrict__ rs_d2,
+                                                        int* __restrict__ rs_idx) {
     __shared__ double s_d[256];
     __shared__ int s_i[256];
-    const int cnt = *flag_count;
-    for (int e = blockIdx.x; e < cnt; e += gridDim.x) {
-        const int q = flag_list[e];
+    const int cnt = st->flag_count, n = st->n;
+    const int c = blockIdx.x;
+    const int cl = (n + kMaxChunks - 1) / kMaxChunks;
+    const int c0 = min(c * cl, n), c1 = min(c0 + cl, n);
+    for (int f = blockIdx.y; f < cnt; f += gridDim.y) {
+        const int q = flag_list[f];
         const double x = qx[q], y = qy[q];
         double best = __builtin_inf();
         int bi = 0x7fffffff;
-        for (int k = threadIdx.x; k < n; k += 256) {
+        for (int k = c0 + (int)threadIdx.x; k < c1; k += 256) {
             const double dx = x - X[k], dy = y - Y[k];
             const double d2 = dx * dx + dy * dy;
             if (d2 < best) {
@@ -533,112 +530,453 @@ __global__ __launch_bounds__(256) void nn_rescan_kernel(const int* __restrict__ 
             __syncthreads();
         }
         if (threadIdx.x == 0) {
-            out_idx[q] = s_i[0];
-            out_d2[q] = s_d[0];
+            rs_d2[(size_t)f * kMaxChunks + c] = s_d[0];
+            rs_idx[(size_t)f * kMaxChunks + c] = s_i[0] == 0x7fffffff ? -1 : s_i[0];
         }
         __syncthreads();
     }
 }
 
-// one wave per sample j: the earlier window samples i < j with d2(j, i) < D2_j (its snapshot
-// NN's squared distance).  cand_cnt[j] is the exact count; the first kCandCap of them (ascending
-// i) are appended to the compact list `cand` (slots reserved with one atomic per sample).
-__global__ __launch_bounds__(256) void window_pairs_kernel(const double* __restrict__ wsx,
+// The snapshot nearest node of window sample j (exact), merging the rescan partials if flagged.
+__device__ inline int final_nn(int j, const int* __restrict__ nn_idx,
+                               const double* __restrict__ nn_d2, const double* __restrict__ rs_d2,
+                               const int* __restrict__ rs_idx, double* d2_out) {
+    const int i = nn_idx[j];
+    if (i >= 0) {
+        if (d2_out) *d2_out = nn_d2[j];
+        return i;
+    }
+    const size_t f = (size_t)(-i - 1);
+    double bd = __builtin_inf();
+    int bi = 0x7fffffff;
+    for (int c = 0; c < kMaxChunks; ++c) {
+        const int ci = rs_idx[f * kMaxChunks + c];
+        const double cd = rs_d2[f * kMaxChunks + c];
+        if (ci >= 0 && (cd < bd || (cd == bd && ci < bi))) {
+            bd = cd;
+            bi = ci;
+        }
+    }
+    if (d2_out) *d2_out = bd;
+    return bi;
+}
+
+// API path (pp_rrt_get_nearest_node_batch): write the merged result of the flagged samples.
+__global__ __launch_bounds__(256) void nn_fix_kernel(const DevState* __restrict__ st,
+                                                     int* __restrict__ nn_idx,
+                                                     double* __restrict__ nn_d2,
+                                                     const double* __restrict__ rs_d2,
+                                                     const int* __restrict__ rs_idx) {
+    const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= st->W || nn_idx[q] >= 0) return;
+    double d2;
+    const int i = final_nn(q, nn_idx, nn_d2, rs_d2, rs_idx, &d2);
+    nn_idx[q] = i;
+    nn_d2[q] = d2;
+}
+
+// Window pairs: for every sample j, the earlier samples i < j of the same window that are
+// strictly nearer than j's snapshot NN (the candidates of the sequential-consistency resolve).
+// One wave per (j-tile, i-tile) of the lower triangle: lane l owns sample j = 64*jt + l and the
+// i-tile's coordinates sit one per lane, broadcast step by step with v_readlane.  Hits are rare
+// and appended with atomics (cand_cnt[j] is the exact count, at most kCandCap entries of each j
+// are stored).
+__device__ inline double readlane_f64(double v, int k) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), k);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), k);
+    return __hiloint2double(hi, lo);
+}
+
+__global__ __launch_bounds__(256) void window_pairs_kernel(DevState* __restrict__ st,
+                                                           const double* __restrict__ wsx,
                                                            const double* __restrict__ wsy,
-                                                           const double* __restrict__ nn_d2, int W,
+                                                           const int* __restrict__ nn_idx,
+                                                           const double* __restrict__ nn_d2,
+                                                           const double* __restrict__ rs_d2,
+                                                           const int* __restrict__ rs_idx,
                                                            int* __restrict__ cand_cnt,
-                                                           CandEntry* __restrict__ cand,
-                                                           int* __restrict__ ncomp) {
+                                                           CandEntry* __restrict__ cand) {
+    const int W = st->W;
+    const int g = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    int jt = (int)((sqrt(8.0 * g + 1.0) - 1.0) * 0.5);
+    while ((jt + 1) * (jt + 2) / 2 <= g) ++jt;
+    while (jt * (jt + 1) / 2 > g) --jt;
+    const int it = g - jt * (jt + 1) / 2;
+    if (jt * 64 >= W) return;
     const int lane = threadIdx.x & 63;
-    const int j = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    if (j >= W) return;
-    const double x = wsx[j], y = wsy[j], D2 = nn_d2[j];
-    int cnt = 0;
-    for (int base = 0; base < j; base += 64) {
-        const int i = base + lane;
-        bool hit = false;
-        if (i < j) {
-            const double dx = x - wsx[i], dy = y - wsy[i];
-            hit = dx * dx + dy * dy < D2;
-        }
-        cnt += __popcll(__ballot(hit));
+    const int j = jt * 64 + lane;
+    const int i0 = it * 64;
+    const bool valid = j < W;
+    double xj = 0.0, yj = 0.0, D2 = -1.0;
+    if (valid) {
+        xj = wsx[j];
+        yj = wsy[j];
+        (void)final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, &D2);
     }
-    if (cnt == 0) {
-        if (lane == 0) cand_cnt[j] = 0;
-        return;
-    }
-    const int keep = cnt < kCandCap ? cnt : kCandCap;
-    int slot0 = 0;
-    if (lane == 0) slot0 = atomicAdd(ncomp, keep);
-    slot0 = __shfl(slot0, 0);
-    int w = 0;
-    for (int base = 0; base < j && w < keep; base += 64) {
-        const int i = base + lane;
-        bool hit = false;
-        double d2 = 0.0;
-        if (i < j) {
-            const double dx = x - wsx[i], dy = y - wsy[i];
-            d2 = dx * dx + dy * dy;
-            hit = d2 < D2;
+    const int il = i0 + lane;
+    const double xi = il < W ? wsx[il] : 0.0;
+    const double yi = il < W ? wsy[il] : 0.0;
+#pragma unroll 16
+    for (int k = 0; k < 64; ++k) {
+        const double xk = readlane_f64(xi, k), yk = readlane_f64(yi, k);
+        const double dx = xj - xk, dy = yj - yk;
+        const double d2 = dx * dx + dy * dy;
+        const int i = i0 + k;
+        if (valid && i < j && d2 < D2) {
+            const int cpos = atomicAdd(&cand_cnt[j], 1);
+            if (cpos < kCandCap) {
+                const int e = atomicAdd(&st->ncomp, 1);
+                cand[e] = CandEntry{j, i, d2, 0.0, -1, 0};
+            }
         }
-        const unsigned long long mask = __ballot(hit);
-        if (hit) {
-            const int pos = w + __popcll(mask & ((1ull << lane) - 1ull));
-            if (pos < keep) cand[slot0 + pos] = CandEntry{j, i, d2};
-        }
-        w += __popcll(mask);
     }
-    if (lane == 0) cand_cnt[j] = cnt;
+}
+
+// Steer + collide for the window: tasks [0, W) are (sample j → its snapshot NN), tasks
+// [W, W + ncomp) are candidate entries (sample j → window sample i, with i's yaw under ITS
+// snapshot parent: the speculation the resolve validates).
+__global__ __launch_bounds__(256) void steer_window_kernel(
+    const DevState* __restrict__ st, SceneDev sc, TreeDev tr, const double* __restrict__ wsx,
+    const double* __restrict__ wsy, const int* __restrict__ nn_idx,
+    const double* __restrict__ nn_d2, const double* __restrict__ rs_d2,
+    const int* __restrict__ rs_idx, CandEntry* __restrict__ cand, int* __restrict__ snap_status,
+    double* __restrict__ snap_yaw) {
+    const int lane = threadIdx.x & 63;
+    const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    const int W = st->W;
+    const int total = W + st->ncomp;
+    for (int t = gw; t < total; t += nw) {
+        int j;
+        double px, py, pyaw;
+        if (t < W) {
+            j = t;
+            const int p = final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);
+            px = tr.x[p];
+            py = tr.y[p];
+            pyaw = tr.yaw[p];
+        } else {
+            const CandEntry ce = cand[t - W];
+            j = ce.j;
+            const int ni = final_nn(ce.i, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);
+            px = wsx[ce.i];
+            py = wsy[ce.i];
+            pyaw = atan2(tr.y[ni] - py, tr.x[ni] - px);
+        }
+        const double x = wsx[j], y = wsy[j];
+        const double yaw = atan2(py - y, px - x);  // compute_yaw, rrt.rs:267-271
+        const int s = steer_collide_fast(sc, x, y, yaw, px, py, pyaw);
+        if (lane == 0) {
+            if (t < W) {
+                snap_status[t] = s;
+                snap_yaw[t] = yaw;
+            } else {
+                cand[t - W].status = s;
+                cand[t - W].yaw = yaw;
+            }
+        }
+    }
+}
+
+// Block-wide exclusive prefix sum of one int per thread (kResolveThreads threads, 4 waves).
+__device__ inline int block_exclusive_scan(int v, int* s_wave, int* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[wave] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kResolveThreads / 64; ++w) {
+        const int t = s_wave[w];
+        base += w < wave ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+// The sequential-consistency resolve of one window, on one workgroup, state in LDS: replays the
+// window in order — sample j's parent is the first ACCEPTED entry of its candidate list in
+// (d2, i) order, else its snapshot NN.  Samples without candidates are decided in one parallel
+// pass; the few with candidates go through round-stamped passes (a verdict written in round r
+// is read from round r + 1 on), and (child, parent) pairs nobody speculated on are re-steered
+// by the workgroup's waves.  The accepted samples are then appended to the tree in iteration
+// order (rrt.rs:586-589) and DevState advances.
+__global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
+    DevState* __restrict__ st, SceneDev sc, TreeDev tr, const double* __restrict__ wsx,
+    const double* __restrict__ wsy, const int* __restrict__ nn_idx,
+    const double* __restrict__ nn_d2, const double* __restrict__ rs_d2,
+    const int* __restrict__ rs_idx, const int* __restrict__ cand_cnt,
+    const CandEntry* __restrict__ cand, const int* __restrict__ snap_status,
+    const double* __restrict__ snap_yaw, ResolveScratch rs, double* __restrict__ lit_scratch) {
+    constexpr int NT = kResolveThreads;
+    constexpr int KW = kMaxWindow;
+    constexpr int kTaskCap = 256;
+    constexpr int kUndecided = 0x7fffffff;
+    __shared__ int s_round[KW];   // round the sample was decided in
+    __shared__ int s_par[KW];     // -1: snapshot NN, else window sample index
+    __shared__ double s_yaw[KW];
+    __shared__ int s_off[KW];     // candidate list offset; reused as tree node index at commit
+    __shared__ int s_fill[KW];
+    __shared__ int s_pend[KW];    // samples that need the round passes
+    __shared__ signed char s_verdict[KW];
+    __shared__ int s_task_j[kTaskCap], s_task_p[kTaskCap], s_task_lit[kTaskCap];
+    __shared__ int s_wave[NT / 64];
+    __shared__ int s_weff, s_npend, s_total, s_changed, s_ntask, s_err;
+    const int W = st->W;
+    if (W == 0) return;
+    const int64_t it0 = st->it;
+    const int n0 = st->n;
+    const int ncomp = st->ncomp;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) {
+        s_weff = W;
+        s_npend = 0;
+        s_total = 0;
+        s_err = 0;
+    }
+    __syncthreads();
+
+    // 1. parallel pass: samples with no nearer window sample are decided by their snapshot
+    //    verdict; the rest are queued (and their candidate lists get LDS offsets)
+    for (int j = tid; j < W; j += NT) {
+        const int c = cand_cnt[j];
+        s_round[j] = kUndecided;
+        s_fill[j] = 0;
+        if (c > kCandCap) atomicMin(&s_weff, j);  // list incomplete: the window stops there
+        const int ss = c == 0 ? snap_status[j] : -1;
+        if (c == 0 && (ss == kAccept || ss == kReject)) {
+            s_verdict[j] = ss == kAccept;
+            s_par[j] = -1;
+            s_yaw[j] = snap_yaw[j];
+            s_round[j] = 0;
+        } else {
+            s_pend[atomicAdd(&s_npend, 1)] = j;
+            rs.rep[j] = -1;
+            if (c > 0) s_off[j] = atomicAdd(&s_total, min(c, kCandCap));
+        }
+    }
+    __syncthreads();
+    const int Weff = s_weff;
+    const int npend = s_npend;
+    for (int e = tid; e < ncomp; e += NT) {
+        const int j = cand[e].j;
+        const int pos = atomicAdd(&s_fill[j], 1);
+        rs.order[s_off[j] + pos] = e;
+    }
+    __syncthreads();
+    for (int q = tid; q < npend; q += NT) {  // sort each list by (d2, i)
+        const int j = s_pend[q];
+        const int k = min(cand_cnt[j], kCandCap);
+        if (k < 2) continue;
+        const int o = s_off[j];
+        for (int a2 = 1; a2 < k; ++a2) {
+            const int e = rs.order[o + a2];
+            const double d = cand[e].d2;
+            const int ii = cand[e].i;
+            int b2 = a2 - 1;
+            while (b2 >= 0) {
+                const int eb = rs.order[o + b2];
+                if (cand[eb].d2 < d || (cand[eb].d2 == d && cand[eb].i < ii)) break;
+                rs.order[o + b2 + 1] = eb;
+                --b2;
+            }
+            rs.order[o + b2 + 1] = e;
+        }
+    }
+    __syncthreads();
+
+    // 2. round passes over the queued samples
+    int64_t n_rounds_rep = 0, n_rep = 0, n_lit = 0;
+    for (int round = 1; round < (1 << 20) && npend > 0; ++round) {
+        if (tid == 0) {
+            s_changed = 0;
+            s_ntask = 0;
+        }
+        __syncthreads();
+        for (int q = tid; q < npend; q += NT) {
+            const int j = s_pend[q];
+            if (j >= Weff || s_round[j] != kUndecided) continue;
+            int parent = -1, slot = -1;
+            bool blocked = false;
+            const int k = min(cand_cnt[j], kCandCap);
+            const int o = k > 0 ? s_off[j] : 0;
+            for (int a2 = 0; a2 < k; ++a2) {
+                const int e = rs.order[o + a2];
+                const int i = cand[e].i;
+                if (s_round[i] >= round) {  // undecided as of this round's start
+                    blocked = true;
+                    break;
+                }
+                if (s_verdict[i]) {
+                    parent = i;
+                    slot = e;
+                    break;
+                }
+            }
+            if (blocked) continue;
+            int status = -1, lit_done = 0;
+            double y = 0.0;
+            const int rep = rs.rep[j];
+            if (rep >= 0) {
+                status = rep & 15;
+                lit_done = rep >> 4;
+                y = rs.repyaw[j];
+            } else if (parent < 0) {
+                status = snap_status[j];
+                y = snap_yaw[j];
+            } else if (s_par[parent] < 0) {
+                status = cand[slot].status;
+                y = cand[slot].yaw;
+            }
+            if (status < 0 || (status == kLiteral && !lit_done)) {
+                const int tk = atomicAdd(&s_ntask, 1);
+                if (tk < kTaskCap) {
+                    s_task_j[tk] = j;
+                    s_task_p[tk] = parent;
+                    s_task_lit[tk] = status == kLiteral;
+                }
+                continue;
+            }
+            if (status != kAccept && status != kReject) s_err = 1;  // kError
+            s_verdict[j] = status == kAccept;
+            s_par[j] = parent;
+            s_yaw[j] = y;
+            s_round[j] = round;
+            s_changed = 1;
+        }
+        __syncthreads();
+        const int ntask = min(s_ntask, kTaskCap);
+        if (ntask == 0 && !s_changed) break;
+        if (ntask > 0) {
+            for (int tk = wave; tk < ntask; tk += NT / 64) {
+                const int j = s_task_j[tk], p = s_task_p[tk], lit = s_task_lit[tk];
+                const double x = wsx[j], y = wsy[j];
+                double px, py, pyaw;
+                if (p < 0) {
+                    const int q = final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);
+                    px = tr.x[q];
+                    py = tr.y[q];
+                    pyaw = tr.yaw[q];
+                } else {
+                    px = wsx[p];
+                    py = wsy[p];
+                    pyaw = s_yaw[p];
+                }
+                const double yaw = atan2(py - y, px - x);
+                double* bx = lit_scratch + (size_t)wave * 3 * kLiteralCap;
+                const int sres = lit ? steer_collide_literal(sc, x, y, yaw, px, py, pyaw, bx,
+                                                             bx + kLiteralCap, bx + 2 * kLiteralCap)
+                                     : steer_collide_fast(sc, x, y, yaw, px, py, pyaw);
+                if (lane == 0) {
+                    rs.rep[j] = sres | (lit << 4);
+                    rs.repyaw[j] = yaw;
+                }
+            }
+            if (tid == 0) {
+                n_rounds_rep++;
+                n_rep += ntask;
+                for (int tk = 0; tk < ntask; ++tk) n_lit += s_task_lit[tk];
+            }
+        }
+        __syncthreads();
+    }
+
+    // 3. commit: accepted samples get consecutive node indices in iteration order
+    constexpr int PER = KW / NT;  // contiguous samples per thread
+    const int j0 = tid * PER;
+    int local = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = j0 + q;
+        local += (j < Weff && s_verdict[j]) ? 1 : 0;
+    }
+    int total = 0;
+    int node = n0 + block_exclusive_scan(local, s_wave, &total);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = j0 + q;
+        if (j < Weff && s_verdict[j]) s_off[j] = node++;
+    }
+    __syncthreads();
+    for (int j = tid; j < Weff; j += NT) {
+        if (!s_verdict[j]) continue;
+        const int nd = s_off[j];
+        const int p = s_par[j];
+        const double x = wsx[j], y = wsy[j];
+        tr.x[nd] = x;
+        tr.y[nd] = y;
+        tr.x32[nd] = (float)x;
+        tr.y32[nd] = (float)y;
+        tr.yaw[nd] = s_yaw[j];
+        tr.parent[nd] = p < 0 ? final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, nullptr) : s_off[p];
+    }
+    if (tid == 0) {
+        st->n = n0 + total;
+        st->it = it0 + Weff;
+        if (s_err) st->error = 1;
+        st->iterations += Weff;
+        st->accepted += total;
+        st->windows += 1;
+        st->truncations += Weff < W;
+        st->repair_rounds += n_rounds_rep;
+        st->repairs += n_rep;
+        st->literal_repairs += n_lit;
+        st->nn_flagged += st->flag_count;
+        st->node_evals += (int64_t)W * n0;
+    }
 }
 
 // --------------------------------------------------------------------------- launch wrappers
 
-hipError_t launch_nn(hipStream_t st, const TreeDev& tr, const double* qx, const double* qy,
-                     int nq, int stride, float* pbest, float* psecond, int* pidx, double eps_coord,
-                     int* out_idx, double* out_d2, int* flag_list, int* flag_count,
-                     hipEvent_t ev_scan0, hipEvent_t ev_scan1) {
-    if (nq <= 0) return hipSuccess;
-    const int n = tr.n;
-    int chunk_len = (n + kMaxChunks - 1) / kMaxChunks;
-    if (chunk_len < 512) chunk_len = 512;
-    chunk_len = (chunk_len + 31) & ~31;
-    const int n_chunks = (n + chunk_len - 1) / chunk_len;
-    hipError_t e = hipMemsetAsync(flag_count, 0, sizeof(int), st);
-    if (e != hipSuccess) return e;
-    dim3 g1((nq + kQPB - 1) / kQPB, n_chunks);
-    if (ev_scan0) (void)hipEventRecord(ev_scan0, st);
-    nn_scan_kernel<<<g1, 256, 0, st>>>(tr.x32, tr.y32, n, qx, qy, nq, chunk_len, stride, pbest,
-                                       psecond, pidx);
-    if (ev_scan1) (void)hipEventRecord(ev_scan1, st);
-    nn_finalize_kernel<<<(nq + 255) / 256, 256, 0, st>>>(pbest, psecond, pidx, n_chunks, stride,
-                                                         nq, qx, qy, tr.x, tr.y, eps_coord,
-                                                         out_idx, out_d2, flag_list, flag_count);
-    const int g3 = nq < 256 ? nq : 256;
-    nn_rescan_kernel<<<g3, 256, 0, st>>>(flag_list, flag_count, qx, qy, tr.x, tr.y, n, out_idx,
-                                         out_d2);
+hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev) {
+    const int K = a.K;
+    const int nqb = (K + kQPB - 1) / kQPB;
+    const int Tk = (K + 63) / 64;
+    const int tiles = Tk * (Tk + 1) / 2;
+    window_begin_kernel<<<(K + 255) / 256, 256, 0, s>>>(a.st, K, a.target, a.seed, a.sc.minx, a.sc.maxx,
+                                                         a.sc.miny, a.sc.maxy, a.wsx, a.wsy,
+                                                         a.cand_cnt);
+    if (ev) (void)hipEventRecord(ev[0], s);
+    nn_scan_kernel<<<nqb * kMaxChunks, 256, 0, s>>>(a.st, a.tr.x32, a.tr.y32, a.wsx, a.wsy, nqb, K,
+                                                   a.pbest, a.psecond, a.pidx);
+    if (ev) (void)hipEventRecord(ev[1], s);
+    nn_finalize_kernel<<<(K + 63) / 64, 256, 0, s>>>(a.st, a.pbest, a.psecond, a.pidx, K, a.wsx,
+                                                     a.wsy, a.tr.x, a.tr.y, a.eps_coord, a.nn_idx,
+                                                     a.nn_d2, a.flag_list);
+    nn_rescan_kernel<<<dim3(kMaxChunks, kRescanSlots), 256, 0, s>>>(
+        a.st, a.flag_list, a.wsx, a.wsy, a.tr.x, a.tr.y, a.rs_d2, a.rs_idx);
+    window_pairs_kernel<<<(tiles + 3) / 4, 256, 0, s>>>(a.st, a.wsx, a.wsy, a.nn_idx, a.nn_d2,
+                                                        a.rs_d2, a.rs_idx, a.cand_cnt, a.cand);
+    if (ev) (void)hipEventRecord(ev[2], s);
+    steer_window_kernel<<<(K + 3) / 4, 256, 0, s>>>(a.st, a.sc, a.tr, a.wsx, a.wsy, a.nn_idx,
+                                                    a.nn_d2, a.rs_d2, a.rs_idx, a.cand,
+                                                    a.snap_status, a.snap_yaw);
+    if (ev) (void)hipEventRecord(ev[3], s);
+    resolve_kernel<<<1, kResolveThreads, 0, s>>>(a.st, a.sc, a.tr, a.wsx, a.wsy, a.nn_idx, a.nn_d2,
+                                                 a.rs_d2, a.rs_idx, a.cand_cnt, a.cand,
+                                                 a.snap_status, a.snap_yaw, a.rs, a.lit_scratch);
     return hipGetLastError();
 }
 
-hipError_t launch_pairs(hipStream_t st, const double* wsx, const double* wsy, const double* nn_d2,
-                        int W, int* cand_cnt, CandEntry* cand, int* ncomp) {
-    if (W <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(ncomp, 0, sizeof(int), st);
-    if (e != hipSuccess) return e;
-    window_pairs_kernel<<<(W + 3) / 4, 256, 0, st>>>(wsx, wsy, nn_d2, W, cand_cnt, cand, ncomp);
-    return hipGetLastError();
-}
-
-hipError_t launch_steer_window(hipStream_t st, const SceneDev& sc, const TreeDev& tr,
-                               const double* wsx, const double* wsy, const int* nn_idx,
-                               const CandEntry* cand, const int* ncomp, int W, int* snap_status,
-                               double* snap_yaw, int* spec_status, double* spec_yaw) {
-    if (W <= 0) return hipSuccess;
-    // one wave per snapshot task; the (few) candidate tasks are picked up by the grid-stride loop
-    int waves = W;
-    if (waves > 16384) waves = 16384;
-    steer_window_kernel<<<(waves + 3) / 4, 256, 0, st>>>(sc, tr, wsx, wsy, nn_idx, cand, ncomp, W,
-                                                         snap_status, snap_yaw, spec_status,
-                                                         spec_yaw);
+hipError_t launch_nearest(hipStream_t s, const WindowArgs& a) {
+    const int K = a.K;
+    const int nqb = (K + kQPB - 1) / kQPB;
+    nn_scan_kernel<<<nqb * kMaxChunks, 256, 0, s>>>(a.st, a.tr.x32, a.tr.y32, a.wsx, a.wsy, nqb, K,
+                                                   a.pbest, a.psecond, a.pidx);
+    nn_finalize_kernel<<<(K + 63) / 64, 256, 0, s>>>(a.st, a.pbest, a.psecond, a.pidx, K, a.wsx,
+                                                     a.wsy, a.tr.x, a.tr.y, a.eps_coord, a.nn_idx,
+                                                     a.nn_d2, a.flag_list);
+    nn_rescan_kernel<<<dim3(kMaxChunks, kRescanSlots), 256, 0, s>>>(
+        a.st, a.flag_list, a.wsx, a.wsy, a.tr.x, a.tr.y, a.rs_d2, a.rs_idx);
+    nn_fix_kernel<<<(K + 255) / 256, 256, 0, s>>>(a.st, a.nn_idx, a.nn_d2, a.rs_d2, a.rs_idx);
     return hipGetLastError();
 }
 
@@ -651,22 +989,6 @@ hipError_t launch_steer_tasks(hipStream_t st, const SceneDev& sc, const TreeDev&
     if (waves > 16384) waves = 16384;
     steer_tasks_kernel<<<(waves + 3) / 4, 256, 0, st>>>(sc, tr, tasks, n, out_status, out_yaw,
                                                         scratch);
-    return hipGetLastError();
-}
-
-hipError_t launch_sample(hipStream_t st, uint64_t seed, int64_t it0, int W, double minx,
-                         double maxx, double miny, double maxy, double* wsx, double* wsy) {
-    if (W <= 0) return hipSuccess;
-    sample_kernel<<<(W + 255) / 256, 256, 0, st>>>(seed, it0, W, minx, maxx, miny, maxy, wsx, wsy);
-    return hipGetLastError();
-}
-
-hipError_t launch_append(hipStream_t st, const CommitEntry* ents, int n_new, int n0,
-                         const double* wsx, const double* wsy, const int* nn_idx, float* x32,
-                         float* y32, double* X, double* Y, double* YAW, int* PAR) {
-    if (n_new <= 0) return hipSuccess;
-    append_kernel<<<(n_new + 255) / 256, 256, 0, st>>>(ents, n_new, n0, wsx, wsy, nn_idx, x32, y32,
-                                                       X, Y, YAW, PAR);
     return hipGetLastError();
 }
 

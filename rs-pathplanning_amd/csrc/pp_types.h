@@ -16,12 +16,13 @@ enum : int {
     kError = 3,    // n_point overflow (the reference would panic) or scratch too small
 };
 
-// Window-level constants.
-constexpr int kCandCap = 16;        // in-window nearer-sample list per sample
-constexpr int kSlots = 1 + kCandCap;  // steer slots per sample: snapshot parent + candidates
-constexpr int kMaxChunks = 64;      // node chunks of the NN scan (partials per query)
-constexpr int kLiteralCap = 16384;  // points per literal-path scratch buffer
-constexpr int kLiteralWaves = 256;  // concurrent literal-path waves (scratch buffers)
+constexpr int kCandCap = 16;         // in-window nearer-sample entries kept per sample
+constexpr int kMaxChunks = 64;       // node chunks of the NN screen (partials per sample)
+constexpr int kRescanSlots = 32;     // flagged samples rescanned concurrently (grid y)
+constexpr int kLiteralCap = 16384;   // points per literal-path scratch buffer
+constexpr int kLiteralWaves = 256;   // literal scratch buffers (explicit-task kernel)
+constexpr int kResolveThreads = 256; // one workgroup resolves a window (4 waves: 1 per SIMD)
+constexpr int kMaxWindow = 4096;     // K limit: the resolve keeps the window's state in LDS
 
 // Scene in device memory (Space, rrt.rs:70-78, with Q10 analytic discs).
 struct SceneDev {
@@ -37,12 +38,27 @@ struct SceneDev {
 
 // Tree in device memory: f32 SoA for the NN screen, f64 SoA for everything exact.
 struct TreeDev {
-    const float* x32;
-    const float* y32;
-    const double* x;
-    const double* y;
-    const double* yaw;
-    int n;
+    float* x32;
+    float* y32;
+    double* x;
+    double* y;
+    double* yaw;
+    int* parent;
+};
+
+// Device-resident planner state: the window kernels read it and the resolve kernel advances it,
+// so windows are enqueued back to back without a host round trip.
+struct DevState {
+    int64_t it;      // next iteration (RNG counter base)
+    int n;           // tree nodes
+    int W;           // samples in the current window (0: nothing left to do)
+    int error;       // sticky kError seen (the reference would panic)
+    int flag_count;  // NN samples flagged for the exact rescan (this window)
+    int ncomp;       // candidate entries appended by window_pairs (this window)
+    int pad;
+    // statistics (pp_stats)
+    int64_t iterations, accepted, windows, truncations, repair_rounds, repairs, literal_repairs,
+        nn_flagged, node_evals;
 };
 
 // An explicit steer task: child (x, y) steered toward its parent — tree node `pnode` when
@@ -53,16 +69,21 @@ struct SteerTask {
     int literal;  // 1 = take the literal (single-lane) path
 };
 
-// A window sample i < j that is strictly nearer to sample j than j's snapshot NN.
+// A window sample i < j that is strictly nearer to sample j than j's snapshot NN, with the
+// speculative verdict for (j, parent i) computed by the steer kernel.
 struct CandEntry {
     int j, i;
     double d2;
+    double yaw;
+    int status;
+    int pad;
 };
 
-// An accepted window sample to append: parent = tree node `parent`, or nn_idx[j] when -1.
-struct CommitEntry {
-    int j, parent;
-    double yaw;
+// Resolve scratch (global, one window).
+struct ResolveScratch {
+    int* order;     // [K * kCandCap] entry indices, per sample sorted by (d2, i)
+    int* rep;       // [K] repair verdict (-1: none), | 16 when it came from the literal path
+    double* repyaw; // [K]
 };
 
 }  // namespace ppamd
