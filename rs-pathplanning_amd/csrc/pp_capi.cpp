@@ -91,6 +91,8 @@ constexpr int kMaxBatch = 64;  // windows enqueued between two host synchronisat
 struct pp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;               // window_pairs + candidate steers
+    hipEvent_t ev_nn = nullptr, ev_pairs = nullptr;  // cross-stream ordering (no timing)
 
     // ---- scene (Space)
     bool has_scene = false;
@@ -98,6 +100,10 @@ struct pp_ctx {
     double width = 0, height = 0, max_steer = 0;
     int m = 0;
     DBuf<double> d_cx, d_cy, d_r2, d_rcull;
+    DBuf<int> d_goff, d_gitems;
+    double gx0 = 0, gy0 = 0, ginv = 1;
+    int gnx = 1, gny = 1;
+    int lds_bytes = 0, lds_goff = 0, lds_items = 0, lds_cx = 0, lds_cy = 0, lds_r2 = 0;
 
     // ---- planner (RRT)
     bool has_rrt = false;
@@ -118,10 +124,11 @@ struct pp_ctx {
     // ---- window buffers (sized for Kcap)
     int K = 4096;
     int Kcap = 0;
-    DBuf<double> wsx, wsy, nn_d2, rs_d2, snap_yaw;
+    DBuf<double> wsx, wsy, nn_d2, rs_d2, snap_yaw, snap_pose;
     DBuf<float> pbest, psecond;
     DBuf<int> pidx, nn_idx, flag_list, rs_idx, cand_cnt, snap_status;
     DBuf<CandEntry> cand;
+    DBuf<char> prep;  // SteerPrep records (opaque here)
     DBuf<int> r_order, r_rep;
     DBuf<double> r_repyaw;
     DBuf<double> lit_scratch;  // resolve: one literal buffer per wave
@@ -141,6 +148,9 @@ struct pp_ctx {
     ~pp_ctx() {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
+        if (ev_nn) (void)hipEventDestroy(ev_nn);
+        if (ev_pairs) (void)hipEventDestroy(ev_pairs);
+        if (stream2) (void)hipStreamDestroy(stream2);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -157,6 +167,19 @@ struct pp_ctx {
         s.cy = d_cy.p;
         s.r2 = d_r2.p;
         s.rcull = d_rcull.p;
+        s.gx0 = gx0;
+        s.gy0 = gy0;
+        s.ginv = ginv;
+        s.gnx = gnx;
+        s.gny = gny;
+        s.goff = d_goff.p;
+        s.gitems = d_gitems.p;
+        s.lds_bytes = lds_bytes;
+        s.lds_goff = lds_goff;
+        s.lds_items = lds_items;
+        s.lds_cx = lds_cx;
+        s.lds_cy = lds_cy;
+        s.lds_r2 = lds_r2;
         return s;
     }
     TreeDev tree_dev() const {
@@ -191,6 +214,8 @@ struct pp_ctx {
         a.cand = cand.p;
         a.snap_status = snap_status.p;
         a.snap_yaw = snap_yaw.p;
+        a.snap_pose = snap_pose.p;
+        a.prep = reinterpret_cast<SteerPrep*>(prep.p);
         a.rs.order = r_order.p;
         a.rs.rep = r_rep.p;
         a.rs.repyaw = r_repyaw.p;
@@ -227,8 +252,10 @@ int ensure_window(pp_ctx* c, int K) {
     PP_HIP(c->rs_idx.reserve(k * kMaxChunks));
     PP_HIP(c->cand_cnt.reserve(k));
     PP_HIP(c->cand.reserve(k * kCandCap));
+    PP_HIP(c->prep.reserve((k + k * kCandCap) * kSteerPrepBytes));
     PP_HIP(c->snap_status.reserve(k));
     PP_HIP(c->snap_yaw.reserve(k));
+    PP_HIP(c->snap_pose.reserve(3 * k));
     PP_HIP(c->r_order.reserve(k * kCandCap));
     PP_HIP(c->r_rep.reserve(k));
     PP_HIP(c->r_repyaw.reserve(k));
@@ -311,6 +338,9 @@ int pp_create(int device, pp_ctx** out) {
     pp_ctx* c = new pp_ctx();
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_nn, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_pairs, hipEventDisableTiming);
     if (e == hipSuccess) e = c->d_state.reserve(1);
     if (e == hipSuccess) e = c->d_api_state.reserve(1);
     if (e == hipSuccess) e = c->h_state.reserve(2);
@@ -326,6 +356,7 @@ int pp_destroy(pp_ctx* ctx) {
     if (!ctx) return PP_OK;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamSynchronize(ctx->stream2);
     delete ctx;
     return PP_OK;
 }
@@ -420,6 +451,58 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
         r2[k] = reff * reff;
         rc_[k] = reff * (1.0 + 1e-9) + 1e-9;
     }
+    // uniform grid over the discs (square cells, about one cell per disc)
+    const double spanx = maxx - minx, spany = maxy - miny;
+    const double span = std::max(spanx, spany);
+    const int per_axis = std::max(1, std::min(256, (int)std::ceil(std::sqrt((double)std::max(m, 1)))));
+    const double cell = span / per_axis;
+    const int gnx = std::max(1, std::min(256, (int)std::ceil(spanx / cell)));
+    const int gny = std::max(1, std::min(256, (int)std::ceil(spany / cell)));
+    const double ginv = 1.0 / cell;
+    auto cell_of = [&](double v, double v0, int n) {
+        const double f = std::floor((v - v0) * ginv);
+        return f < 0.0 ? 0 : (f >= (double)(n - 1) ? n - 1 : (int)f);
+    };
+    std::vector<int> goff((size_t)gnx * gny + 1, 0), gitems;
+    {
+        std::vector<std::vector<int>> lists((size_t)gnx * gny);
+        for (int k = 0; k < m; ++k) {
+            const int x0c = cell_of(cx[k] - rc_[k], minx, gnx), x1c = cell_of(cx[k] + rc_[k], minx, gnx);
+            const int y0c = cell_of(cy[k] - rc_[k], miny, gny), y1c = cell_of(cy[k] + rc_[k], miny, gny);
+            for (int gy = y0c; gy <= y1c; ++gy)
+                for (int gx = x0c; gx <= x1c; ++gx) lists[(size_t)gy * gnx + gx].push_back(k);
+        }
+        for (size_t q = 0; q < lists.size(); ++q) {
+            goff[q + 1] = goff[q] + (int)lists[q].size();
+            gitems.insert(gitems.end(), lists[q].begin(), lists[q].end());
+        }
+    }
+    PP_HIP(ctx->d_goff.reserve(goff.size()));
+    PP_HIP(ctx->d_gitems.reserve(std::max<size_t>(gitems.size(), 1)));
+    PP_HIP(hipMemcpy(ctx->d_goff.p, goff.data(), goff.size() * sizeof(int), hipMemcpyHostToDevice));
+    if (!gitems.empty())
+        PP_HIP(hipMemcpy(ctx->d_gitems.p, gitems.data(), gitems.size() * sizeof(int), hipMemcpyHostToDevice));
+    {  // LDS image for the steer kernels: [goff | items | cx | cy | r2], 16-byte aligned parts
+        auto al = [](size_t b) { return (int)((b + 15) & ~(size_t)15); };
+        const int o_goff = 0;
+        const int o_items = o_goff + al(goff.size() * sizeof(int));
+        const int o_cx = o_items + al(gitems.size() * sizeof(int));
+        const int o_cy = o_cx + al((size_t)m * sizeof(double));
+        const int o_r2 = o_cy + al((size_t)m * sizeof(double));
+        const int total = o_r2 + al((size_t)m * sizeof(double));
+        const bool fits = total <= 64 * 1024;  // 2 workgroups per CU fit in 160 KB
+        ctx->lds_bytes = fits ? total : 0;
+        ctx->lds_goff = o_goff;
+        ctx->lds_items = o_items;
+        ctx->lds_cx = o_cx;
+        ctx->lds_cy = o_cy;
+        ctx->lds_r2 = o_r2;
+    }
+    ctx->gx0 = minx;
+    ctx->gy0 = miny;
+    ctx->ginv = ginv;
+    ctx->gnx = gnx;
+    ctx->gny = gny;
     const size_t mm = (size_t)std::max(m, 1);
     PP_HIP(ctx->d_cx.reserve(mm));
     PP_HIP(ctx->d_cy.reserve(mm));
@@ -528,7 +611,8 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
         if (ctx->prof && (r = ensure_events(ctx, 4 * (size_t)nw))) return r;
         const int64_t windows_before = ctx->h_state.p[0].windows;
         for (int w = 0; w < nw; ++w)
-            PP_HIP(launch_window(st, a, ctx->prof ? &ctx->ev[4 * w] : nullptr));
+            PP_HIP(launch_window(st, ctx->stream2, ctx->ev_nn, ctx->ev_pairs, a,
+                                 ctx->prof ? &ctx->ev[4 * w] : nullptr));
         PP_HIP(hipMemcpyAsync(ctx->h_state.p, ctx->d_state.p, sizeof(DevState), hipMemcpyDeviceToHost, st));
         PP_HIP(hipStreamSynchronize(st));
         const DevState& s = ctx->h_state.p[0];
@@ -690,6 +774,7 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out) {
         s.literal_repairs = d.literal_repairs;
         s.nn_flagged = d.nn_flagged;
         s.node_evals = d.node_evals;
+        for (int k = 0; k < 8; ++k) s.stamps[k] = d.stamps[k];
     }
     s.nn_scan_ms = ctx->nn_scan_ms;
     s.nn_scan_launches = ctx->nn_scan_launches;
@@ -708,6 +793,7 @@ int pp_rrt_reset_stats(pp_ctx* ctx) {
         DevState d = ctx->h_state.p[0];
         d.iterations = d.accepted = d.windows = d.truncations = d.repair_rounds = d.repairs =
             d.literal_repairs = d.nn_flagged = d.node_evals = 0;
+        for (auto& t : d.stamps) t = 0;
         ctx->h_state.p[0] = d;
         PP_HIP(hipMemcpyAsync(ctx->d_state.p, ctx->h_state.p, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));

@@ -15,22 +15,63 @@
 // No MFMA anywhere: there is no dense contraction on this path.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "pp_device.h"
 #include "pp_kernels.h"
 
 namespace ppamd {
 
+#ifdef PP_STAMPS
+#define PP_STAMP(var) const int64_t var = (int64_t)__builtin_amdgcn_s_memrealtime()
+#else
+#define PP_STAMP(var)
+#endif
+
 // ------------------------------------------------------------------------------ collision
 
 // One 64-point chunk of a polyline, one point per lane: bounds for the lanes flagged
 // `check_bounds`, then the segment (lane-1 → lane) of every lane flagged `seg_valid` against the
-// discs that overlap the chunk's bounding box (Space::verify, rrt.rs:124-137, Q10).
-// Must be called by all 64 lanes.  Returns true when the chunk rejects the line.
-__device__ bool chunk_rejects(const SceneDev& sc, bool has, bool check_bounds, bool seg_valid,
-                              double qx, double qy) {
+// discs listed in the grid cells the chunk's bounding box touches (Space::verify,
+// rrt.rs:124-137, Q10).  A disc whose cull box meets the chunk's box shares a cell with it (the
+// cell index is monotone in the coordinate), so the cull is exact.  Must be called by all 64
+// lanes.  Returns true when the chunk rejects the line.
+__device__ inline int grid_cell(double v, double v0, double inv, int n) {
+    const double f = floor((v - v0) * inv);
+    return f < 0.0 ? 0 : (f >= (double)(n - 1) ? n - 1 : (int)f);
+}
+
+// Dynamic LDS of the steer kernels: the scene image (SceneDev::lds_*) when kLds.
+extern __shared__ __attribute__((aligned(16))) char pp_smem[];
+
+// Copy the scene's grid and discs into this workgroup's LDS image (all threads call it).
+__device__ inline void stage_scene(const SceneDev& sc) {
+    const int ncell = sc.gnx * sc.gny + 1;
+    const int nitem = sc.goff[ncell - 1];
+    int* goff = reinterpret_cast<int*>(pp_smem + sc.lds_goff);
+    int* items = reinterpret_cast<int*>(pp_smem + sc.lds_items);
+    double* cx = reinterpret_cast<double*>(pp_smem + sc.lds_cx);
+    double* cy = reinterpret_cast<double*>(pp_smem + sc.lds_cy);
+    double* r2 = reinterpret_cast<double*>(pp_smem + sc.lds_r2);
+    for (int k = threadIdx.x; k < ncell; k += blockDim.x) goff[k] = sc.goff[k];
+    for (int k = threadIdx.x; k < nitem; k += blockDim.x) items[k] = sc.gitems[k];
+    for (int k = threadIdx.x; k < sc.m; k += blockDim.x) {
+        cx[k] = sc.cx[k];
+        cy[k] = sc.cy[k];
+        r2[k] = sc.r2[k];
+    }
+    __syncthreads();
+}
+
+template <bool kLds>
+__device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool check_bounds,
+                                              bool seg_valid, double qx, double qy,
+                                              int64_t* ph = nullptr) {
+    PP_STAMP(tq0);
     const bool oob =
         check_bounds && !(qx >= sc.minx && qx <= sc.maxx && qy >= sc.miny && qy <= sc.maxy);
     if (__any(oob)) return true;
+    if (sc.m == 0) return false;
     const double ax = __shfl_up(qx, 1);
     const double ay = __shfl_up(qy, 1);
     const double inf = __builtin_inf();
@@ -38,36 +79,65 @@ __device__ bool chunk_rejects(const SceneDev& sc, bool has, bool check_bounds, b
     const double bx1 = wave_max(has ? qx : -inf);
     const double by0 = wave_min(has ? qy : inf);
     const double by1 = wave_max(has ? qy : -inf);
-    const int lane = threadIdx.x & 63;
-    for (int base = 0; base < sc.m; base += 64) {
-        const int k = base + lane;
-        bool ov = false;
-        if (k < sc.m) {
-            const double cx = sc.cx[k], cy = sc.cy[k], rc = sc.rcull[k];
-            ov = (cx + rc >= bx0) && (cx - rc <= bx1) && (cy + rc >= by0) && (cy - rc <= by1);
-        }
-        unsigned long long mask = __ballot(ov);
-        while (mask) {
-            const int b = __ffsll((unsigned long long)mask) - 1;
-            mask &= mask - 1;
-            const int kk = base + b;
-            const double cx = sc.cx[kk], cy = sc.cy[kk], r2 = sc.r2[kk];
-            const bool hit = seg_valid && seg_hits_disc(ax, ay, qx, qy, cx, cy, r2);
-            if (__any(hit)) return true;
+    PP_STAMP(tq1);
+#ifdef PP_STAMPS
+    if (ph) ph[0] += tq1 - tq0;
+#endif
+    const int cx0 = __builtin_amdgcn_readfirstlane(grid_cell(bx0, sc.gx0, sc.ginv, sc.gnx));
+    const int cx1 = __builtin_amdgcn_readfirstlane(grid_cell(bx1, sc.gx0, sc.ginv, sc.gnx));
+    const int cy0 = __builtin_amdgcn_readfirstlane(grid_cell(by0, sc.gy0, sc.ginv, sc.gny));
+    const int cy1 = __builtin_amdgcn_readfirstlane(grid_cell(by1, sc.gy0, sc.ginv, sc.gny));
+    const int* goff = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_goff) : sc.goff;
+    const int* items = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_items) : sc.gitems;
+    const double* dcx = kLds ? reinterpret_cast<const double*>(pp_smem + sc.lds_cx) : sc.cx;
+    const double* dcy = kLds ? reinterpret_cast<const double*>(pp_smem + sc.lds_cy) : sc.cy;
+    const double* dr2 = kLds ? reinterpret_cast<const double*>(pp_smem + sc.lds_r2) : sc.r2;
+    for (int gy = cy0; gy <= cy1; ++gy) {
+        for (int gx = cx0; gx <= cx1; ++gx) {
+            const int cell = gy * sc.gnx + gx;
+            const int k0 = goff[cell], k1 = goff[cell + 1];
+            for (int k = k0; k < k1; ++k) {
+#ifdef PP_STAMPS
+                if (ph) ph[1] += 1;
+#endif
+                const int d = items[k];
+                const bool hit = seg_valid && seg_hits_disc(ax, ay, qx, qy, dcx[d], dcy[d], dr2[d]);
+                if (__any(hit)) return true;
+            }
         }
     }
     return false;
 }
 
-// Fast path of verify_node for the edge child (x, y, yaw) → parent (px, py, pyaw):
-// the Dubins polyline of line_to_origin (rrt.rs:295-315) plus the junction to the parent, whose
-// own line was verified when it was inserted.  The word choice and the segment
-// origins are wave-uniform; the pd accumulation of generate_local_course (dubins.rs:239-255) is
-// replayed uniformly and each lane captures one grid point, so every point carries exactly the
-// reference's `pd += d` value; interpolation and the collision test then run lane-parallel.
-__device__ int steer_collide_fast(const SceneDev& sc, double x, double y, double yaw, double px,
-                                  double py, double pyaw) {
-    const int lane = threadIdx.x & 63;
+// Fast path of verify_node for the edge child (x, y, yaw) → parent (px, py, pyaw): the Dubins
+// polyline of line_to_origin (rrt.rs:295-315) plus the junction to the parent, whose own line
+// was verified when it was inserted.  Split in two:
+//   steer_prep  per lane (one task per lane): word choice, lengths, segment origins, the trim
+//               checks — all the per-task scalar math;
+//   steer_walk  per wave (one task per wave): the `pd += d` walk of generate_local_course
+//               (dubins.rs:239-255) replayed uniformly, each lane capturing one grid point so
+//               every point carries exactly the reference's accumulated value; interpolation
+//               and the collision test then run lane-parallel, 63 points per chunk.
+struct SteerPrep {
+    double x, y, px, py;      // child (point 0 of the edge) and parent (the junction)
+    double c, cw, sw;         // curvature, cos/sin(-yaw) of the world transform
+    double L0, L1, L2;        // segment lengths
+    double o1x, o1y, o1yaw;   // origin of segment 1 (endpoint of segment 0)
+    double o2x, o2y, o2yaw;   // origin of segment 2
+    long long n_point;        // dubins.rs:369
+    int m0, m1, m2;           // segment modes
+    int state;                // -1: walk; kReject/kAccept: decided; kLiteral; kError; 4: None
+};
+enum : int { kPrepWalk = -1, kPrepNone = 4 };
+static_assert(sizeof(SteerPrep) == kSteerPrepBytes, "SteerPrep layout");
+
+__device__ __forceinline__ SteerPrep steer_prep(const SceneDev& sc, double x, double y,
+                                                double yaw, double px, double py, double pyaw) {
+    SteerPrep r;
+    r.x = x;
+    r.y = y;
+    r.px = px;
+    r.py = py;
     const double step = sc.step_size;
     // dubins_path_planning, dubins.rs:401-408 (s = child, e = parent)
     const double ex = px - x, ey = py - y;
@@ -76,36 +146,100 @@ __device__ int steer_collide_fast(const SceneDev& sc, double x, double y, double
     const double ley = -(sin(yaw)) * ex + cos(yaw) * ey;
     const double leyaw = pyaw - yaw;
     const Steer s = select_word(lex, ley, leyaw, c);
-    if (s.word < 0) {
-        // steer failed: line_to_origin contributes [(sx, sy)] (rrt.rs:313)
-        const bool has = lane < 2;
-        const double qx = lane == 0 ? x : px, qy = lane == 0 ? y : py;
-        return chunk_rejects(sc, has, lane == 0, lane == 1, qx, qy) ? kReject : kAccept;
+    r.c = c;
+    r.cw = cos(-yaw);
+    r.sw = sin(-yaw);
+    if (s.word < 0) {  // steer failed: line_to_origin contributes [(sx, sy)] (rrt.rs:313)
+        r.state = kPrepNone;
+        return r;
     }
-    const double L0 = s.t, L1 = s.p, L2 = s.q;
-    const int m0 = word_mode(s.word, 0), m1 = word_mode(s.word, 1), m2 = word_mode(s.word, 2);
+    r.L0 = s.t;
+    r.L1 = s.p;
+    r.L2 = s.q;
+    r.m0 = word_mode(s.word, 0);
+    r.m1 = word_mode(s.word, 1);
+    r.m2 = word_mode(s.word, 2);
     double total = 0.0;
-    total += L0;
-    total += L1;
-    total += L2;
+    total += s.t;
+    total += s.p;
+    total += s.q;
     const double nq = trunc(total / step);
-    if (!(nq >= 0.0) || nq > 1.0e8) return kError;
-    const long n_point = (long)nq + 3 + 4;
+    if (!(nq >= 0.0) || nq > 1.0e8) {
+        r.state = kError;
+        return r;
+    }
+    r.n_point = (long long)nq + 3 + 4;
     // segment origins = previous segment's endpoint (dubins.rs:230, 258-271)
     const Pose O0{0.0, 0.0, 0.0};
-    const Pose O1 = interp_local(m0, L0, c, O0);
-    const Pose O2 = interp_local(m1, L1, c, O1);
-    const Pose E = interp_local(m2, L2, c, O2);
+    const Pose O1 = interp_local(r.m0, r.L0, c, O0);
+    const Pose O2 = interp_local(r.m1, r.L1, c, O1);
+    const Pose E = interp_local(r.m2, r.L2, c, O2);
+    r.o1x = O1.x;
+    r.o1y = O1.y;
+    r.o1yaw = O1.yaw;
+    r.o2x = O2.x;
+    r.o2y = O2.y;
+    r.o2yaw = O2.yaw;
     // The trim (dubins.rs:281-288) drops exactly the final endpoint unless its local x is 0.0
     // (then it keeps popping) or the array has no trailing zero: both go to the literal path.
-    if (E.x == 0.0) return kLiteral;
-    const double cw = cos(-yaw), sw = sin(-yaw);
+    r.state = E.x == 0.0 ? kLiteral : kPrepWalk;
+    return r;
+}
 
+// The record's fields travel as scalars (a struct passed by reference ends up on the private
+// stack once the per-lane segment select turns into an indexed load).
+struct WalkIn {
+    double x, y, px, py, c, cw, sw, L0, L1, L2, o1x, o1y, o1yaw, o2x, o2y, o2yaw;
+    long long n_point;
+    int m0, m1, m2, state;
+};
+__device__ __forceinline__ WalkIn walk_in(const SteerPrep* __restrict__ p) {
+    WalkIn w;
+    w.x = p->x;
+    w.y = p->y;
+    w.px = p->px;
+    w.py = p->py;
+    w.c = p->c;
+    w.cw = p->cw;
+    w.sw = p->sw;
+    w.L0 = p->L0;
+    w.L1 = p->L1;
+    w.L2 = p->L2;
+    w.o1x = p->o1x;
+    w.o1y = p->o1y;
+    w.o1yaw = p->o1yaw;
+    w.o2x = p->o2x;
+    w.o2y = p->o2y;
+    w.o2yaw = p->o2yaw;
+    w.n_point = p->n_point;
+    w.m0 = p->m0;
+    w.m1 = p->m1;
+    w.m2 = p->m2;
+    w.state = p->state;
+    return w;
+}
+__device__ __forceinline__ WalkIn walk_in(const SteerPrep& p) { return walk_in(&p); }
+
+template <bool kLds>
+__device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
+                                          int64_t* ph = nullptr) {
+    const int lane = threadIdx.x & 63;
+    if (r.state == kPrepNone) {  // polyline [(x, y), (px, py)]
+        const bool has = lane < 2;
+        const double qx = lane == 0 ? r.x : r.px, qy = lane == 0 ? r.y : r.py;
+        return chunk_rejects<kLds>(sc, has, has, lane == 1, qx, qy) ? kReject : kAccept;
+    }
+    if (r.state != kPrepWalk) return r.state;
+    const double step = sc.step_size;
+    const double L0 = r.L0, L1 = r.L1, L2 = r.L2;
+    const int m0 = r.m0, m1 = r.m1, m2 = r.m2;
+    const double o1x = r.o1x, o1y = r.o1y, o1yaw = r.o1yaw;
+    const double o2x = r.o2x, o2y = r.o2y, o2yaw = r.o2yaw;
     int seg = 0;
     double dd = (L0 > 0.0) ? step : -step;
     double pd = dd - 0.0;
-    long grid = 0;
-    double carry_x = x, carry_y = y;  // point 0 of the edge is the child itself
+    long long grid = 0;
+    double carry_x = r.x, carry_y = r.y;  // point 0 of the edge is the child itself
     bool first = true;
     for (;;) {
         int my_seg = 0;
@@ -133,29 +267,57 @@ __device__ int steer_collide_fast(const SceneDev& sc, double x, double y, double
         grid += cnt;
         const bool junction_here = (seg >= 3) && cnt < 63;
         double qx = carry_x, qy = carry_y;
-        bool has = (lane == 0), isgrid = false;
+        bool has = (lane == 0), isgrid = false, isjunction = false;
         if (lane >= 1 && lane <= cnt) {
-            const Pose o = my_seg == 0 ? O0 : (my_seg == 1 ? O1 : O2);
+            Pose o;
+            o.x = my_seg == 0 ? 0.0 : (my_seg == 1 ? o1x : o2x);
+            o.y = my_seg == 0 ? 0.0 : (my_seg == 1 ? o1y : o2y);
+            o.yaw = my_seg == 0 ? 0.0 : (my_seg == 1 ? o1yaw : o2yaw);
             const int mm = my_seg == 0 ? m0 : (my_seg == 1 ? m1 : m2);
-            const Pose r = interp_local(mm, my_pd, c, o);
-            qx = cw * r.x + sw * r.y + x;   // dubins.rs:415
-            qy = -sw * r.x + cw * r.y + y;  // dubins.rs:420
+            const Pose p = interp_local(mm, my_pd, r.c, o);
+            qx = r.cw * p.x + r.sw * p.y + r.x;   // dubins.rs:415
+            qy = -r.sw * p.x + r.cw * p.y + r.y;  // dubins.rs:420
             has = true;
             isgrid = true;
         } else if (junction_here && lane == cnt + 1) {
-            qx = px;
-            qy = py;
+            qx = r.px;
+            qy = r.py;
             has = true;
+            isjunction = true;  // the parent: already checked unless it is the root
         }
-        const bool check_bounds = isgrid || (first && lane == 0);
-        if (chunk_rejects(sc, has, check_bounds, has && lane >= 1, qx, qy)) return kReject;
+        const bool check_bounds = isgrid || isjunction || (first && lane == 0);
+        PP_STAMP(tc0);
+#ifdef PP_STAMPS
+        int64_t cph[2] = {0, 0};
+        const bool rej = chunk_rejects<kLds>(sc, has, check_bounds, has && lane >= 1, qx, qy, cph);
+#else
+        const bool rej = chunk_rejects<kLds>(sc, has, check_bounds, has && lane >= 1, qx, qy);
+#endif
+        PP_STAMP(tc1);
+#ifdef PP_STAMPS
+        if (ph) {
+            ph[2] += tc1 - tc0;
+            ph[3] += 1;
+            ph[4] += cph[0];
+            ph[5] += cph[1];
+        }
+#endif
+        if (rej) return kReject;
         if (junction_here) break;
         carry_x = __shfl(qx, cnt);
         carry_y = __shfl(qy, cnt);
         first = false;
     }
-    if (1 + grid > n_point - 2) return kLiteral;
+    if (1 + grid > r.n_point - 2) return kLiteral;
     return kAccept;
+}
+
+// Both halves on one wave (uniform prep): the repair and verify_node paths.
+template <bool kLds>
+__device__ int steer_collide_fast(const SceneDev& sc, double x, double y, double yaw, double px,
+                                  double py, double pyaw) {
+    const SteerPrep r = steer_prep(sc, x, y, yaw, px, py, pyaw);
+    return steer_walk<kLds>(sc, walk_in(r));
 }
 
 // Literal path (measure-zero trim cases): lane 0 runs dubins_literal into its scratch buffer and
@@ -231,7 +393,7 @@ __global__ __launch_bounds__(256) void steer_tasks_kernel(SceneDev sc, TreeDev t
         else if (tk.literal)
             s = kError;
         else
-            s = steer_collide_fast(sc, tk.x, tk.y, yaw, px, py, pyaw);
+            s = steer_collide_fast<false>(sc, tk.x, tk.y, yaw, px, py, pyaw);
         if (lane == 0) {
             out_status[t] = s;
             out_yaw[t] = yaw;
@@ -434,8 +596,8 @@ __global__ __launch_bounds__(256) void nn_finalize_kernel(
     DevState* __restrict__ st, const float* __restrict__ pbest, const float* __restrict__ psecond,
     const int* __restrict__ pidx, int stride, const double* __restrict__ qx,
     const double* __restrict__ qy, const double* __restrict__ X, const double* __restrict__ Y,
-    double eps_coord, int* __restrict__ out_idx, double* __restrict__ out_d2,
-    int* __restrict__ flag_list) {
+    const double* __restrict__ YAW, double eps_coord, int* __restrict__ out_idx,
+    double* __restrict__ out_d2, double* __restrict__ out_pose, int* __restrict__ flag_list) {
     __shared__ float s_b[4][64];
     __shared__ float s_s[4][64];
     __shared__ int s_i[4][64];
@@ -479,9 +641,15 @@ __global__ __launch_bounds__(256) void nn_finalize_kernel(
         flag_list[f] = q;
         out_idx[q] = -(f + 1);
     } else {
-        const double dx = qx[q] - X[t.i], dy = qy[q] - Y[t.i];
+        const double nxp = X[t.i], nyp = Y[t.i];
+        const double dx = qx[q] - nxp, dy = qy[q] - nyp;
         out_idx[q] = t.i;
         out_d2[q] = dx * dx + dy * dy;
+        if (out_pose) {
+            out_pose[3 * q] = nxp;
+            out_pose[3 * q + 1] = nyp;
+            out_pose[3 * q + 2] = YAW[t.i];
+        }
     }
 }
 
@@ -607,15 +775,14 @@ __global__ __launch_bounds__(256) void window_pairs_kernel(DevState* __restrict_
     const int j = jt * 64 + lane;
     const int i0 = it * 64;
     const bool valid = j < W;
-    double xj = 0.0, yj = 0.0, D2 = -1.0;
-    if (valid) {
-        xj = wsx[j];
-        yj = wsy[j];
-        (void)final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, &D2);
-    }
     const int il = i0 + lane;
+    // every load issued before any is used
+    const double xj = valid ? wsx[j] : 0.0, yj = valid ? wsy[j] : 0.0;
+    const int nj = valid ? nn_idx[j] : 0;
+    double D2 = valid ? nn_d2[j] : -1.0;
     const double xi = il < W ? wsx[il] : 0.0;
     const double yi = il < W ? wsy[il] : 0.0;
+    if (valid && nj < 0) (void)final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, &D2);  // flagged
 #pragma unroll 16
     for (int k = 0; k < 64; ++k) {
         const double xk = readlane_f64(xi, k), yk = readlane_f64(yi, k);
@@ -635,45 +802,103 @@ __global__ __launch_bounds__(256) void window_pairs_kernel(DevState* __restrict_
 // Steer + collide for the window: tasks [0, W) are (sample j → its snapshot NN), tasks
 // [W, W + ncomp) are candidate entries (sample j → window sample i, with i's yaw under ITS
 // snapshot parent: the speculation the resolve validates).
-__global__ __launch_bounds__(256) void steer_window_kernel(
+// Task t of a window: t < W is (sample t → its snapshot NN); t >= W is candidate entry t - W
+// (sample E.j → window sample E.i, with E.i's yaw under ITS snapshot parent: the speculation the
+// resolve validates).  spec = 0 runs the snapshot tasks (independent of window_pairs, so on the
+// first stream concurrently with it), spec = 1 the candidate tasks.
+__device__ inline void window_task(int t, int W, const TreeDev& tr, const double* wsx,
+                                   const double* wsy, const int* nn_idx, const double* nn_d2,
+                                   const double* rs_d2, const int* rs_idx,
+                                   const double* snap_pose, const CandEntry* cand, int* j_out,
+                                   double* px, double* py, double* pyaw) {
+    if (t < W) {
+        const int j = t;
+        *j_out = j;
+        if (nn_idx[j] >= 0) {  // parent pose written by nn_finalize (one memory hop)
+            *px = snap_pose[3 * j];
+            *py = snap_pose[3 * j + 1];
+            *pyaw = snap_pose[3 * j + 2];
+        } else {
+            const int p = final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);
+            *px = tr.x[p];
+            *py = tr.y[p];
+            *pyaw = tr.yaw[p];
+        }
+    } else {
+        const CandEntry ce = cand[t - W];
+        *j_out = ce.j;
+        const int ni = final_nn(ce.i, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);
+        *px = wsx[ce.i];
+        *py = wsy[ce.i];
+        *pyaw = atan2(tr.y[ni] - *py, tr.x[ni] - *px);
+    }
+}
+
+// steer_prep, one task per lane: record + the task's yaw (compute_yaw, rrt.rs:267-271).
+__global__ __launch_bounds__(256) void steer_prep_kernel(
     const DevState* __restrict__ st, SceneDev sc, TreeDev tr, const double* __restrict__ wsx,
     const double* __restrict__ wsy, const int* __restrict__ nn_idx,
     const double* __restrict__ nn_d2, const double* __restrict__ rs_d2,
-    const int* __restrict__ rs_idx, CandEntry* __restrict__ cand, int* __restrict__ snap_status,
-    double* __restrict__ snap_yaw) {
+    const int* __restrict__ rs_idx, const double* __restrict__ snap_pose,
+    CandEntry* __restrict__ cand, SteerPrep* __restrict__ prep, double* __restrict__ snap_yaw,
+    int spec) {
+    const int W = st->W;
+    const int first = spec ? W : 0;
+    const int total = spec ? W + st->ncomp : W;
+    const int t = first + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t >= total) return;
+    int j;
+    double px, py, pyaw;
+    window_task(t, W, tr, wsx, wsy, nn_idx, nn_d2, rs_d2, rs_idx, snap_pose, cand, &j, &px, &py,
+                &pyaw);
+    const double x = wsx[j], y = wsy[j];
+    const double yaw = atan2(py - y, px - x);
+    prep[t] = steer_prep(sc, x, y, yaw, px, py, pyaw);
+    if (t < W)
+        snap_yaw[t] = yaw;
+    else
+        cand[t - W].yaw = yaw;
+}
+
+// steer_walk, one task per wave (persistent grid, grid-stride); kLds: the scene's disc grid is
+// staged into this workgroup's LDS first.
+template <bool kLds>
+__global__ __launch_bounds__(256, 4) void steer_walk_kernel(const DevState* __restrict__ st,
+                                                         SceneDev sc,
+                                                         const SteerPrep* __restrict__ prep,
+                                                         CandEntry* __restrict__ cand,
+                                                         int* __restrict__ snap_status, int spec) {
     const int lane = threadIdx.x & 63;
+    const int W = st->W;
+    const int first = spec ? W : 0;
+    const int total = spec ? W + st->ncomp : W;
+    if (first + (int)blockIdx.x * 4 >= total) return;  // whole workgroup idle
+    if (kLds) stage_scene(sc);
     const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    const int W = st->W;
-    const int total = W + st->ncomp;
-    for (int t = gw; t < total; t += nw) {
-        int j;
-        double px, py, pyaw;
-        if (t < W) {
-            j = t;
-            const int p = final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);
-            px = tr.x[p];
-            py = tr.y[p];
-            pyaw = tr.yaw[p];
-        } else {
-            const CandEntry ce = cand[t - W];
-            j = ce.j;
-            const int ni = final_nn(ce.i, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);
-            px = wsx[ce.i];
-            py = wsy[ce.i];
-            pyaw = atan2(tr.y[ni] - py, tr.x[ni] - px);
+    for (int t = first + gw; t < total; t += nw) {
+        const WalkIn r = walk_in(prep + t);
+#ifdef PP_STAMPS
+        int64_t ph[6] = {0, 0, 0, 0, 0, 0};
+        PP_STAMP(tt0);
+        const int s = steer_walk<kLds>(sc, r, ph);
+        PP_STAMP(tt1);
+        if (lane == 0 && !spec) {
+            DevState* sw = const_cast<DevState*>(st);
+            atomicAdd((unsigned long long*)&sw->stamps[0], (unsigned long long)(tt1 - tt0));
+            atomicAdd((unsigned long long*)&sw->stamps[2], (unsigned long long)ph[2]);
+            atomicAdd((unsigned long long*)&sw->stamps[3], (unsigned long long)ph[3]);
+            atomicAdd((unsigned long long*)&sw->stamps[4], (unsigned long long)ph[4]);
+            atomicAdd((unsigned long long*)&sw->stamps[5], (unsigned long long)ph[5]);
         }
-        const double x = wsx[j], y = wsy[j];
-        const double yaw = atan2(py - y, px - x);  // compute_yaw, rrt.rs:267-271
-        const int s = steer_collide_fast(sc, x, y, yaw, px, py, pyaw);
+#else
+        const int s = steer_walk<kLds>(sc, r);
+#endif
         if (lane == 0) {
-            if (t < W) {
+            if (t < W)
                 snap_status[t] = s;
-                snap_yaw[t] = yaw;
-            } else {
+            else
                 cand[t - W].status = s;
-                cand[t - W].yaw = yaw;
-            }
         }
     }
 }
@@ -731,6 +956,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
     __shared__ int s_weff, s_npend, s_total, s_changed, s_ntask, s_err;
     const int W = st->W;
     if (W == 0) return;
+    PP_STAMP(t_0);
     const int64_t it0 = st->it;
     const int n0 = st->n;
     const int ncomp = st->ncomp;
@@ -745,17 +971,31 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
     __syncthreads();
 
     // 1. parallel pass: samples with no nearer window sample are decided by their snapshot
-    //    verdict; the rest are queued (and their candidate lists get LDS offsets)
-    for (int j = tid; j < W; j += NT) {
-        const int c = cand_cnt[j];
+    //    verdict; the rest are queued (and their candidate lists get LDS offsets).  Every load
+    //    of the pass is issued before any of them is used (one memory round trip, not 16).
+    constexpr int PER = KW / NT;  // samples per thread (strided: j = tid + NT * q)
+    int v_c[PER], v_s[PER];
+    double v_y[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = tid + NT * q;
+        const bool in = j < W;
+        v_c[q] = in ? cand_cnt[j] : 0;
+        v_s[q] = in ? snap_status[j] : kReject;
+        v_y[q] = in ? snap_yaw[j] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = tid + NT * q;
+        if (j >= W) break;
+        const int c = v_c[q], ss = v_s[q];
         s_round[j] = kUndecided;
         s_fill[j] = 0;
         if (c > kCandCap) atomicMin(&s_weff, j);  // list incomplete: the window stops there
-        const int ss = c == 0 ? snap_status[j] : -1;
         if (c == 0 && (ss == kAccept || ss == kReject)) {
             s_verdict[j] = ss == kAccept;
             s_par[j] = -1;
-            s_yaw[j] = snap_yaw[j];
+            s_yaw[j] = v_y[q];
             s_round[j] = 0;
         } else {
             s_pend[atomicAdd(&s_npend, 1)] = j;
@@ -764,6 +1004,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
         }
     }
     __syncthreads();
+    PP_STAMP(t_1);
     const int Weff = s_weff;
     const int npend = s_npend;
     for (int e = tid; e < ncomp; e += NT) {
@@ -793,6 +1034,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
     }
     __syncthreads();
 
+    PP_STAMP(t_2);
     // 2. round passes over the queued samples
     int64_t n_rounds_rep = 0, n_rep = 0, n_lit = 0;
     for (int round = 1; round < (1 << 20) && npend > 0; ++round) {
@@ -874,7 +1116,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
                 double* bx = lit_scratch + (size_t)wave * 3 * kLiteralCap;
                 const int sres = lit ? steer_collide_literal(sc, x, y, yaw, px, py, pyaw, bx,
                                                              bx + kLiteralCap, bx + 2 * kLiteralCap)
-                                     : steer_collide_fast(sc, x, y, yaw, px, py, pyaw);
+                                     : steer_collide_fast<false>(sc, x, y, yaw, px, py, pyaw);
                 if (lane == 0) {
                     rs.rep[j] = sres | (lit << 4);
                     rs.repyaw[j] = yaw;
@@ -889,9 +1131,9 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
         __syncthreads();
     }
 
+    PP_STAMP(t_3);
     // 3. commit: accepted samples get consecutive node indices in iteration order
-    constexpr int PER = KW / NT;  // contiguous samples per thread
-    const int j0 = tid * PER;
+    const int j0 = tid * PER;  // contiguous samples per thread for the scan
     int local = 0;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -906,18 +1148,47 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
         if (j < Weff && s_verdict[j]) s_off[j] = node++;
     }
     __syncthreads();
-    for (int j = tid; j < Weff; j += NT) {
+    double v_x[PER], v_yy[PER];
+    int v_p[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {  // loads first, then the (scattered) tree stores
+        const int j = tid + NT * q;
+        const bool in = j < Weff;
+        v_x[q] = in ? wsx[j] : 0.0;
+        v_yy[q] = in ? wsy[j] : 0.0;
+        v_p[q] = in ? nn_idx[j] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = tid + NT * q;
+        if (j >= Weff) break;
         if (!s_verdict[j]) continue;
         const int nd = s_off[j];
         const int p = s_par[j];
-        const double x = wsx[j], y = wsy[j];
-        tr.x[nd] = x;
-        tr.y[nd] = y;
-        tr.x32[nd] = (float)x;
-        tr.y32[nd] = (float)y;
+        int par;
+        if (p >= 0)
+            par = s_off[p];
+        else if (v_p[q] >= 0)
+            par = v_p[q];
+        else
+            par = final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);  // flagged sample
+        tr.x[nd] = v_x[q];
+        tr.y[nd] = v_yy[q];
+        tr.x32[nd] = (float)v_x[q];
+        tr.y32[nd] = (float)v_yy[q];
         tr.yaw[nd] = s_yaw[j];
-        tr.parent[nd] = p < 0 ? final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, nullptr) : s_off[p];
+        tr.parent[nd] = par;
     }
+    __syncthreads();
+    PP_STAMP(t_4);
+#ifdef PP_STAMPS_RESOLVE
+    if (tid == 0) {
+        st->stamps[0] += t_1 - t_0;
+        st->stamps[1] += t_2 - t_1;
+        st->stamps[2] += t_3 - t_2;
+        st->stamps[3] += t_4 - t_3;
+    }
+#endif
     if (tid == 0) {
         st->n = n0 + total;
         st->it = it0 + Weff;
@@ -936,30 +1207,55 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
 
 // --------------------------------------------------------------------------- launch wrappers
 
-hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev) {
+hipError_t launch_window(hipStream_t s, hipStream_t s2, hipEvent_t ev_nn, hipEvent_t ev_pairs,
+                         const WindowArgs& a, hipEvent_t* ev) {
     const int K = a.K;
     const int nqb = (K + kQPB - 1) / kQPB;
     const int Tk = (K + 63) / 64;
     const int tiles = Tk * (Tk + 1) / 2;
-    window_begin_kernel<<<(K + 255) / 256, 256, 0, s>>>(a.st, K, a.target, a.seed, a.sc.minx, a.sc.maxx,
-                                                         a.sc.miny, a.sc.maxy, a.wsx, a.wsy,
-                                                         a.cand_cnt);
+    window_begin_kernel<<<(K + 255) / 256, 256, 0, s>>>(a.st, K, a.target, a.seed, a.sc.minx,
+                                                         a.sc.maxx, a.sc.miny, a.sc.maxy, a.wsx,
+                                                         a.wsy, a.cand_cnt);
     if (ev) (void)hipEventRecord(ev[0], s);
     nn_scan_kernel<<<nqb * kMaxChunks, 256, 0, s>>>(a.st, a.tr.x32, a.tr.y32, a.wsx, a.wsy, nqb, K,
                                                    a.pbest, a.psecond, a.pidx);
     if (ev) (void)hipEventRecord(ev[1], s);
     nn_finalize_kernel<<<(K + 63) / 64, 256, 0, s>>>(a.st, a.pbest, a.psecond, a.pidx, K, a.wsx,
-                                                     a.wsy, a.tr.x, a.tr.y, a.eps_coord, a.nn_idx,
-                                                     a.nn_d2, a.flag_list);
+                                                     a.wsy, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord,
+                                                     a.nn_idx, a.nn_d2, a.snap_pose, a.flag_list);
     nn_rescan_kernel<<<dim3(kMaxChunks, kRescanSlots), 256, 0, s>>>(
         a.st, a.flag_list, a.wsx, a.wsy, a.tr.x, a.tr.y, a.rs_d2, a.rs_idx);
-    window_pairs_kernel<<<(tiles + 3) / 4, 256, 0, s>>>(a.st, a.wsx, a.wsy, a.nn_idx, a.nn_d2,
-                                                        a.rs_d2, a.rs_idx, a.cand_cnt, a.cand);
+    hipError_t e = hipEventRecord(ev_nn, s);
+    if (e != hipSuccess) return e;
+    // second stream: candidate lists, then the candidate steers
+    e = hipStreamWaitEvent(s2, ev_nn, 0);
+    if (e != hipSuccess) return e;
+    window_pairs_kernel<<<(tiles + 3) / 4, 256, 0, s2>>>(a.st, a.wsx, a.wsy, a.nn_idx, a.nn_d2,
+                                                         a.rs_d2, a.rs_idx, a.cand_cnt, a.cand);
+    const int lds = a.sc.lds_bytes;
+    const int spec_cap = K * kCandCap;
+    steer_prep_kernel<<<(spec_cap + 255) / 256, 256, 0, s2>>>(
+        a.st, a.sc, a.tr, a.wsx, a.wsy, a.nn_idx, a.nn_d2, a.rs_d2, a.rs_idx, a.snap_pose, a.cand,
+        a.prep, a.snap_yaw, 1);
+    if (lds > 0)
+        steer_walk_kernel<true><<<64, 256, lds, s2>>>(a.st, a.sc, a.prep, a.cand, a.snap_status, 1);
+    else
+        steer_walk_kernel<false><<<64, 256, 0, s2>>>(a.st, a.sc, a.prep, a.cand, a.snap_status, 1);
+    e = hipEventRecord(ev_pairs, s2);
+    if (e != hipSuccess) return e;
+    // first stream: the snapshot steers meanwhile
     if (ev) (void)hipEventRecord(ev[2], s);
-    steer_window_kernel<<<(K + 3) / 4, 256, 0, s>>>(a.st, a.sc, a.tr, a.wsx, a.wsy, a.nn_idx,
-                                                    a.nn_d2, a.rs_d2, a.rs_idx, a.cand,
-                                                    a.snap_status, a.snap_yaw);
+    steer_prep_kernel<<<(K + 255) / 256, 256, 0, s>>>(a.st, a.sc, a.tr, a.wsx, a.wsy, a.nn_idx,
+                                                      a.nn_d2, a.rs_d2, a.rs_idx, a.snap_pose,
+                                                      a.cand, a.prep, a.snap_yaw, 0);
+    const int nwg = std::min((K + 3) / 4, 1024);  // persistent walk grid
+    if (lds > 0)
+        steer_walk_kernel<true><<<nwg, 256, lds, s>>>(a.st, a.sc, a.prep, a.cand, a.snap_status, 0);
+    else
+        steer_walk_kernel<false><<<nwg, 256, 0, s>>>(a.st, a.sc, a.prep, a.cand, a.snap_status, 0);
     if (ev) (void)hipEventRecord(ev[3], s);
+    e = hipStreamWaitEvent(s, ev_pairs, 0);
+    if (e != hipSuccess) return e;
     resolve_kernel<<<1, kResolveThreads, 0, s>>>(a.st, a.sc, a.tr, a.wsx, a.wsy, a.nn_idx, a.nn_d2,
                                                  a.rs_d2, a.rs_idx, a.cand_cnt, a.cand,
                                                  a.snap_status, a.snap_yaw, a.rs, a.lit_scratch);
@@ -972,8 +1268,8 @@ hipError_t launch_nearest(hipStream_t s, const WindowArgs& a) {
     nn_scan_kernel<<<nqb * kMaxChunks, 256, 0, s>>>(a.st, a.tr.x32, a.tr.y32, a.wsx, a.wsy, nqb, K,
                                                    a.pbest, a.psecond, a.pidx);
     nn_finalize_kernel<<<(K + 63) / 64, 256, 0, s>>>(a.st, a.pbest, a.psecond, a.pidx, K, a.wsx,
-                                                     a.wsy, a.tr.x, a.tr.y, a.eps_coord, a.nn_idx,
-                                                     a.nn_d2, a.flag_list);
+                                                     a.wsy, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord,
+                                                     a.nn_idx, a.nn_d2, nullptr, a.flag_list);
     nn_rescan_kernel<<<dim3(kMaxChunks, kRescanSlots), 256, 0, s>>>(
         a.st, a.flag_list, a.wsx, a.wsy, a.tr.x, a.tr.y, a.rs_d2, a.rs_idx);
     nn_fix_kernel<<<(K + 255) / 256, 256, 0, s>>>(a.st, a.nn_idx, a.nn_d2, a.rs_d2, a.rs_idx);

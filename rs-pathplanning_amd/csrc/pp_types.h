@@ -23,6 +23,7 @@ constexpr int kLiteralCap = 16384;   // points per literal-path scratch buffer
 constexpr int kLiteralWaves = 256;   // literal scratch buffers (explicit-task kernel)
 constexpr int kResolveThreads = 256; // one workgroup resolves a window (4 waves: 1 per SIMD)
 constexpr int kMaxWindow = 4096;     // K limit: the resolve keeps the window's state in LDS
+constexpr int kSteerPrepBytes = 152; // sizeof(SteerPrep) (checked in pp_kernels.hip)
 
 // Scene in device memory (Space, rrt.rs:70-78, with Q10 analytic discs).
 struct SceneDev {
@@ -34,6 +35,15 @@ struct SceneDev {
     const double* cy;
     const double* r2;     // (r + width/2)^2
     const double* rcull;  // (r + width/2) * (1 + 1e-9) + 1e-9: conservative bbox cull radius
+    // uniform grid over the discs: cell (gx, gy) = floor((v - g0) * ginv), clamped; a disc is
+    // listed in every cell its cull box [c - rcull, c + rcull] touches (CSR: off, items)
+    double gx0, gy0, ginv;
+    int gnx, gny;
+    const int* goff;    // [gnx * gny + 1]
+    const int* gitems;  // disc indices
+    // LDS image of (goff, gitems, cx, cy, r2) staged by the steer kernels when it fits
+    int lds_bytes;  // 0: read the scene from global memory
+    int lds_goff, lds_items, lds_cx, lds_cy, lds_r2;  // byte offsets inside the image
 };
 
 // Tree in device memory: f32 SoA for the NN screen, f64 SoA for everything exact.
@@ -59,6 +69,7 @@ struct DevState {
     // statistics (pp_stats)
     int64_t iterations, accepted, windows, truncations, repair_rounds, repairs, literal_repairs,
         nn_flagged, node_evals;
+    int64_t stamps[8];  // diagnostic build only (PP_STAMPS): accumulated phase times, 100 MHz ticks
 };
 
 // An explicit steer task: child (x, y) steered toward its parent — tree node `pnode` when

@@ -55,10 +55,13 @@ class StatsC(C.Structure):
         ("literal_repairs", C.c_int64), ("nn_flagged", C.c_int64), ("node_evals", C.c_int64),
         ("nn_scan_ms", C.c_double), ("nn_scan_launches", C.c_int64),
         ("steer_ms", C.c_double), ("steer_launches", C.c_int64),
+        ("stamps", C.c_int64 * 8),
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["stamps"] = list(self.stamps)
+        return d
 
 
 _lock = threading.Lock()
