@@ -91,8 +91,6 @@ constexpr int kMaxBatch = 64;  // windows enqueued between two host synchronisat
 struct pp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;               // window_pairs + candidate steers
-    hipEvent_t ev_nn = nullptr, ev_pairs = nullptr;  // cross-stream ordering (no timing)
 
     // ---- scene (Space)
     bool has_scene = false;
@@ -126,9 +124,10 @@ struct pp_ctx {
     int Kcap = 0;
     DBuf<double> wsx, wsy, nn_d2, rs_d2, snap_yaw, snap_pose;
     DBuf<float> pbest, psecond;
-    DBuf<int> pidx, nn_idx, flag_list, rs_idx, cand_cnt, snap_status;
+    DBuf<int> pidx, nn_idx, flag_list, rs_idx, rs_done, cand_cnt, snap_status;
     DBuf<CandEntry> cand;
-    DBuf<char> prep;  // SteerPrep records (opaque here)
+    DBuf<PrepRec> rec;   // per-task steer records
+    DBuf<double> pdbuf;  // per-task grid-point distances (kPdCap per task)
     DBuf<int> r_order, r_rep;
     DBuf<double> r_repyaw;
     DBuf<double> lit_scratch;  // resolve: one literal buffer per wave
@@ -148,9 +147,6 @@ struct pp_ctx {
     ~pp_ctx() {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
-        if (ev_nn) (void)hipEventDestroy(ev_nn);
-        if (ev_pairs) (void)hipEventDestroy(ev_pairs);
-        if (stream2) (void)hipStreamDestroy(stream2);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -210,12 +206,14 @@ struct pp_ctx {
         a.flag_list = flag_list.p;
         a.rs_d2 = rs_d2.p;
         a.rs_idx = rs_idx.p;
+        a.rs_done = rs_done.p;
         a.cand_cnt = cand_cnt.p;
         a.cand = cand.p;
         a.snap_status = snap_status.p;
         a.snap_yaw = snap_yaw.p;
         a.snap_pose = snap_pose.p;
-        a.prep = reinterpret_cast<SteerPrep*>(prep.p);
+        a.rec = rec.p;
+        a.pdbuf = pdbuf.p;
         a.rs.order = r_order.p;
         a.rs.rep = r_rep.p;
         a.rs.repyaw = r_repyaw.p;
@@ -250,9 +248,12 @@ int ensure_window(pp_ctx* c, int K) {
     PP_HIP(c->flag_list.reserve(k));
     PP_HIP(c->rs_d2.reserve(k * kMaxChunks));
     PP_HIP(c->rs_idx.reserve(k * kMaxChunks));
+    PP_HIP(c->rs_done.reserve(k));
+    PP_HIP(hipMemsetAsync(c->rs_done.p, 0, k * sizeof(int), c->stream));
     PP_HIP(c->cand_cnt.reserve(k));
     PP_HIP(c->cand.reserve(k * kCandCap));
-    PP_HIP(c->prep.reserve((k + k * kCandCap) * kSteerPrepBytes));
+    PP_HIP(c->rec.reserve(k + k * kCandCap));
+    PP_HIP(c->pdbuf.reserve((k + k * kCandCap) * kPdCap));
     PP_HIP(c->snap_status.reserve(k));
     PP_HIP(c->snap_yaw.reserve(k));
     PP_HIP(c->snap_pose.reserve(3 * k));
@@ -338,9 +339,6 @@ int pp_create(int device, pp_ctx** out) {
     pp_ctx* c = new pp_ctx();
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_nn, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_pairs, hipEventDisableTiming);
     if (e == hipSuccess) e = c->d_state.reserve(1);
     if (e == hipSuccess) e = c->d_api_state.reserve(1);
     if (e == hipSuccess) e = c->h_state.reserve(2);
@@ -356,7 +354,6 @@ int pp_destroy(pp_ctx* ctx) {
     if (!ctx) return PP_OK;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    (void)hipStreamSynchronize(ctx->stream2);
     delete ctx;
     return PP_OK;
 }
@@ -611,8 +608,7 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
         if (ctx->prof && (r = ensure_events(ctx, 4 * (size_t)nw))) return r;
         const int64_t windows_before = ctx->h_state.p[0].windows;
         for (int w = 0; w < nw; ++w)
-            PP_HIP(launch_window(st, ctx->stream2, ctx->ev_nn, ctx->ev_pairs, a,
-                                 ctx->prof ? &ctx->ev[4 * w] : nullptr));
+            PP_HIP(launch_window(st, a, ctx->prof ? &ctx->ev[4 * w] : nullptr));
         PP_HIP(hipMemcpyAsync(ctx->h_state.p, ctx->d_state.p, sizeof(DevState), hipMemcpyDeviceToHost, st));
         PP_HIP(hipStreamSynchronize(st));
         const DevState& s = ctx->h_state.p[0];

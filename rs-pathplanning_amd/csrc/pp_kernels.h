@@ -7,8 +7,6 @@
 
 namespace ppamd {
 
-struct SteerPrep;
-
 // Everything one window (or one nearest-neighbour batch) touches.  Buffers are sized for K.
 struct WindowArgs {
     int K = 0;
@@ -28,21 +26,21 @@ struct WindowArgs {
     int* flag_list = nullptr;
     double* rs_d2 = nullptr;
     int* rs_idx = nullptr;
+    int* rs_done = nullptr;       // [K] per-flag partial counters (zero between windows)
     int* cand_cnt = nullptr;
     CandEntry* cand = nullptr;
     int* snap_status = nullptr;
     double* snap_yaw = nullptr;
     double* snap_pose = nullptr;  // [3K] parent pose of each unflagged sample (nn_finalize)
-    struct SteerPrep* prep = nullptr;  // [K + K * kCandCap] per-task steer records
+    PrepRec* rec = nullptr;       // [K + K * kCandCap] per-task steer records
+    double* pdbuf = nullptr;      // [(K + K * kCandCap) * kPdCap] grid-point distances
     ResolveScratch rs{};
     double* lit_scratch = nullptr;
 };
 
-// Enqueue one window.  The candidate lists and candidate steers run on s2 (ordered through the
-// sync events ev_nn / ev_pairs) while the snapshot steers run on s.  ev (optional) = 4 timing
-// events: around nn_scan and around the snapshot steer_window.
-hipError_t launch_window(hipStream_t s, hipStream_t s2, hipEvent_t ev_nn, hipEvent_t ev_pairs,
-                         const WindowArgs& a, hipEvent_t* ev);
+// Enqueue one window on stream s.  ev (optional) = 4 timing events: around nn_scan and around
+// the steer (prep + walk) of all the window's tasks.
+hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev);
 
 // Exact nearest tree node of st->W samples (wsx, wsy): nn_scan + finalize + rescan + fix.
 hipError_t launch_nearest(hipStream_t s, const WindowArgs& a);

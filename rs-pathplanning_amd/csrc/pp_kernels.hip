@@ -128,7 +128,6 @@ struct SteerPrep {
     int m0, m1, m2;           // segment modes
     int state;                // -1: walk; kReject/kAccept: decided; kLiteral; kError; 4: None
 };
-enum : int { kPrepWalk = -1, kPrepNone = 4 };
 static_assert(sizeof(SteerPrep) == kSteerPrepBytes, "SteerPrep layout");
 
 __device__ __forceinline__ SteerPrep steer_prep(const SceneDev& sc, double x, double y,
@@ -655,17 +654,25 @@ __global__ __launch_bounds__(256) void nn_finalize_kernel(
 
 // Exact f64 brute force for the flagged samples: grid (kMaxChunks node chunks, kRescanSlots);
 // workgroup (c, s) scans chunk c for flagged samples s, s + kRescanSlots, ... and writes the
-// chunk's (d2, lowest index) partial; final_nn merges the partials.
-__global__ __launch_bounds__(256) void nn_rescan_kernel(const DevState* __restrict__ st,
-                                                        const int* __restrict__ flag_list,
-                                                        const double* __restrict__ qx,
-                                                        const double* __restrict__ qy,
-                                                        const double* __restrict__ X,
-                                                        const double* __restrict__ Y,
-                                                        double* __restrict__ rs_d2,
-                                                        int* __restrict__ rs_idx) {
+// chunk's (d2, lowest index) partial.  The workgroup that completes a sample's last partial
+// merges all kMaxChunks of them and writes the exact nn_idx / nn_d2 / parent pose, so every later
+// kernel reads plain indices.
+__device__ inline void argmin_pair(double& d, int& i, double od, int oi) {
+    if (od < d || (od == d && oi < i)) {
+        d = od;
+        i = oi;
+    }
+}
+
+__global__ __launch_bounds__(256) void nn_rescan_kernel(
+    const DevState* __restrict__ st, const int* __restrict__ flag_list,
+    const double* __restrict__ qx, const double* __restrict__ qy, const double* __restrict__ X,
+    const double* __restrict__ Y, const double* __restrict__ YAW, double* __restrict__ rs_d2,
+    int* __restrict__ rs_idx, int* __restrict__ rs_done, int* __restrict__ nn_idx,
+    double* __restrict__ nn_d2, double* __restrict__ out_pose) {
     __shared__ double s_d[256];
     __shared__ int s_i[256];
+    __shared__ int s_last;
     const int cnt = st->flag_count, n = st->n;
     const int c = blockIdx.x;
     const int cl = (n + kMaxChunks - 1) / kMaxChunks;
@@ -688,212 +695,503 @@ __global__ __launch_bounds__(256) void nn_rescan_kernel(const DevState* __restri
         __syncthreads();
         for (int h = 128; h > 0; h >>= 1) {
             if ((int)threadIdx.x < h) {
-                const double od = s_d[threadIdx.x + h];
-                const int oi = s_i[threadIdx.x + h];
-                if (od < s_d[threadIdx.x] || (od == s_d[threadIdx.x] && oi < s_i[threadIdx.x])) {
-                    s_d[threadIdx.x] = od;
-                    s_i[threadIdx.x] = oi;
-                }
+                double d = s_d[threadIdx.x];
+                int i = s_i[threadIdx.x];
+                argmin_pair(d, i, s_d[threadIdx.x + h], s_i[threadIdx.x + h]);
+                s_d[threadIdx.x] = d;
+                s_i[threadIdx.x] = i;
             }
             __syncthreads();
         }
         if (threadIdx.x == 0) {
             rs_d2[(size_t)f * kMaxChunks + c] = s_d[0];
             rs_idx[(size_t)f * kMaxChunks + c] = s_i[0] == 0x7fffffff ? -1 : s_i[0];
+            __threadfence();
+            s_last = atomicAdd(&rs_done[f], 1) == kMaxChunks - 1;
+        }
+        __syncthreads();
+        if (s_last && threadIdx.x < 64) {  // one wave merges the kMaxChunks partials
+            __threadfence();
+            const size_t o = (size_t)f * kMaxChunks + threadIdx.x;
+            const int ci = __hip_atomic_load(&rs_idx[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const double cd =
+                __hip_atomic_load(&rs_d2[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            double d = ci >= 0 ? cd : __builtin_inf();
+            int i = ci >= 0 ? ci : 0x7fffffff;
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) argmin_pair(d, i, __shfl_xor(d, m), __shfl_xor(i, m));
+            if (threadIdx.x == 0) {
+                nn_idx[q] = i;
+                nn_d2[q] = d;
+                if (out_pose) {
+                    out_pose[3 * q] = X[i];
+                    out_pose[3 * q + 1] = Y[i];
+                    out_pose[3 * q + 2] = YAW[i];
+                }
+                rs_done[f] = 0;
+            }
         }
         __syncthreads();
     }
 }
 
-// The snapshot nearest node of window sample j (exact), merging the rescan partials if flagged.
-__device__ inline int final_nn(int j, const int* __restrict__ nn_idx,
-                               const double* __restrict__ nn_d2, const double* __restrict__ rs_d2,
-                               const int* __restrict__ rs_idx, double* d2_out) {
-    const int i = nn_idx[j];
-    if (i >= 0) {
-        if (d2_out) *d2_out = nn_d2[j];
-        return i;
-    }
-    const size_t f = (size_t)(-i - 1);
-    double bd = __builtin_inf();
-    int bi = 0x7fffffff;
-    for (int c = 0; c < kMaxChunks; ++c) {
-        const int ci = rs_idx[f * kMaxChunks + c];
-        const double cd = rs_d2[f * kMaxChunks + c];
-        if (ci >= 0 && (cd < bd || (cd == bd && ci < bi))) {
-            bd = cd;
-            bi = ci;
-        }
-    }
-    if (d2_out) *d2_out = bd;
-    return bi;
-}
-
-// API path (pp_rrt_get_nearest_node_batch): write the merged result of the flagged samples.
-__global__ __launch_bounds__(256) void nn_fix_kernel(const DevState* __restrict__ st,
-                                                     int* __restrict__ nn_idx,
-                                                     double* __restrict__ nn_d2,
-                                                     const double* __restrict__ rs_d2,
-                                                     const int* __restrict__ rs_idx) {
-    const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (q >= st->W || nn_idx[q] >= 0) return;
-    double d2;
-    const int i = final_nn(q, nn_idx, nn_d2, rs_d2, rs_idx, &d2);
-    nn_idx[q] = i;
-    nn_d2[q] = d2;
-}
-
 // Window pairs: for every sample j, the earlier samples i < j of the same window that are
 // strictly nearer than j's snapshot NN (the candidates of the sequential-consistency resolve).
-// One wave per (j-tile, i-tile) of the lower triangle: lane l owns sample j = 64*jt + l and the
-// i-tile's coordinates sit one per lane, broadcast step by step with v_readlane.  Hits are rare
-// and appended with atomics (cand_cnt[j] is the exact count, at most kCandCap entries of each j
-// are stored).
-__device__ inline double readlane_f64(double v, int k) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), k);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), k);
-    return __hiloint2double(hi, lo);
-}
+// One workgroup per (j-tile, i-tile) of the lower triangle (kPairTile x kPairTile): the i-tile's
+// coordinates are staged in LDS and read as broadcasts; thread l owns sample j = jt*kPairTile + l.
+// Hits are rare and appended with atomics (cand_cnt[j] is the exact count, at most kCandCap
+// entries of each j are stored).
+constexpr int kPairTile = 128;
 
-__global__ __launch_bounds__(256) void window_pairs_kernel(DevState* __restrict__ st,
-                                                           const double* __restrict__ wsx,
-                                                           const double* __restrict__ wsy,
-                                                           const int* __restrict__ nn_idx,
-                                                           const double* __restrict__ nn_d2,
-                                                           const double* __restrict__ rs_d2,
-                                                           const int* __restrict__ rs_idx,
-                                                           int* __restrict__ cand_cnt,
-                                                           CandEntry* __restrict__ cand) {
+__global__ __launch_bounds__(kPairTile) void window_pairs_kernel(DevState* __restrict__ st,
+                                                                 const double* __restrict__ wsx,
+                                                                 const double* __restrict__ wsy,
+                                                                 const double* __restrict__ nn_d2,
+                                                                 int* __restrict__ cand_cnt,
+                                                                 CandEntry* __restrict__ cand) {
+    __shared__ double s_x[kPairTile], s_y[kPairTile];
     const int W = st->W;
-    const int g = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    int jt = (int)((sqrt(8.0 * g + 1.0) - 1.0) * 0.5);
-    while ((jt + 1) * (jt + 2) / 2 <= g) ++jt;
-    while (jt * (jt + 1) / 2 > g) --jt;
-    const int it = g - jt * (jt + 1) / 2;
-    if (jt * 64 >= W) return;
-    const int lane = threadIdx.x & 63;
-    const int j = jt * 64 + lane;
-    const int i0 = it * 64;
+    const int b = blockIdx.x;
+    int jt = (int)((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+    while ((jt + 1) * (jt + 2) / 2 <= b) ++jt;
+    while (jt * (jt + 1) / 2 > b) --jt;
+    const int it = b - jt * (jt + 1) / 2;
+    if (jt * kPairTile >= W) return;
+    const int tid = threadIdx.x;
+    const int j = jt * kPairTile + tid;
+    const int i0 = it * kPairTile;
+    const int il = i0 + tid;
+    s_x[tid] = il < W ? wsx[il] : 0.0;
+    s_y[tid] = il < W ? wsy[il] : 0.0;
     const bool valid = j < W;
-    const int il = i0 + lane;
-    // every load issued before any is used
     const double xj = valid ? wsx[j] : 0.0, yj = valid ? wsy[j] : 0.0;
-    const int nj = valid ? nn_idx[j] : 0;
-    double D2 = valid ? nn_d2[j] : -1.0;
-    const double xi = il < W ? wsx[il] : 0.0;
-    const double yi = il < W ? wsy[il] : 0.0;
-    if (valid && nj < 0) (void)final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, &D2);  // flagged
-#pragma unroll 16
-    for (int k = 0; k < 64; ++k) {
-        const double xk = readlane_f64(xi, k), yk = readlane_f64(yi, k);
-        const double dx = xj - xk, dy = yj - yk;
+    const double D2 = valid ? nn_d2[j] : -1.0;
+    __syncthreads();
+    const int kend = valid ? min(kPairTile, j - i0) : 0;  // i < j (< W)
+#pragma unroll 8
+    for (int k = 0; k < kend; ++k) {
+        const double dx = xj - s_x[k], dy = yj - s_y[k];
         const double d2 = dx * dx + dy * dy;
-        const int i = i0 + k;
-        if (valid && i < j && d2 < D2) {
+        if (d2 < D2) {
             const int cpos = atomicAdd(&cand_cnt[j], 1);
             if (cpos < kCandCap) {
                 const int e = atomicAdd(&st->ncomp, 1);
-                cand[e] = CandEntry{j, i, d2, 0.0, -1, 0};
+                cand[e] = CandEntry{j, i0 + k, d2, 0.0, -1, 0};
             }
         }
     }
 }
 
-// Steer + collide for the window: tasks [0, W) are (sample j → its snapshot NN), tasks
-// [W, W + ncomp) are candidate entries (sample j → window sample i, with i's yaw under ITS
-// snapshot parent: the speculation the resolve validates).
 // Task t of a window: t < W is (sample t → its snapshot NN); t >= W is candidate entry t - W
 // (sample E.j → window sample E.i, with E.i's yaw under ITS snapshot parent: the speculation the
-// resolve validates).  spec = 0 runs the snapshot tasks (independent of window_pairs, so on the
-// first stream concurrently with it), spec = 1 the candidate tasks.
-__device__ inline void window_task(int t, int W, const TreeDev& tr, const double* wsx,
-                                   const double* wsy, const int* nn_idx, const double* nn_d2,
-                                   const double* rs_d2, const int* rs_idx,
+// resolve validates).
+__device__ inline void window_task(int t, int W, const double* wsx, const double* wsy,
                                    const double* snap_pose, const CandEntry* cand, int* j_out,
                                    double* px, double* py, double* pyaw) {
-    if (t < W) {
-        const int j = t;
-        *j_out = j;
-        if (nn_idx[j] >= 0) {  // parent pose written by nn_finalize (one memory hop)
-            *px = snap_pose[3 * j];
-            *py = snap_pose[3 * j + 1];
-            *pyaw = snap_pose[3 * j + 2];
-        } else {
-            const int p = final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);
-            *px = tr.x[p];
-            *py = tr.y[p];
-            *pyaw = tr.yaw[p];
-        }
-    } else {
+    if (t < W) {  // parent = the snapshot NN, whose pose nn_finalize / nn_rescan wrote
+        *j_out = t;
+        *px = snap_pose[3 * t];
+        *py = snap_pose[3 * t + 1];
+        *pyaw = snap_pose[3 * t + 2];
+    } else {  // parent = window sample i, heading toward ITS snapshot NN (compute_yaw)
         const CandEntry ce = cand[t - W];
         *j_out = ce.j;
-        const int ni = final_nn(ce.i, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);
         *px = wsx[ce.i];
         *py = wsy[ce.i];
-        *pyaw = atan2(tr.y[ni] - *py, tr.x[ni] - *px);
+        *pyaw = atan2(snap_pose[3 * ce.i + 1] - *py, snap_pose[3 * ce.i] - *px);
     }
 }
 
-// steer_prep, one task per lane: record + the task's yaw (compute_yaw, rrt.rs:267-271).
-__global__ __launch_bounds__(256) void steer_prep_kernel(
-    const DevState* __restrict__ st, SceneDev sc, TreeDev tr, const double* __restrict__ wsx,
-    const double* __restrict__ wsy, const int* __restrict__ nn_idx,
-    const double* __restrict__ nn_d2, const double* __restrict__ rs_d2,
-    const int* __restrict__ rs_idx, const double* __restrict__ snap_pose,
-    CandEntry* __restrict__ cand, SteerPrep* __restrict__ prep, double* __restrict__ snap_yaw,
-    int spec) {
-    const int W = st->W;
-    const int first = spec ? W : 0;
-    const int total = spec ? W + st->ncomp : W;
-    const int t = first + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (t >= total) return;
-    int j;
-    double px, py, pyaw;
-    window_task(t, W, tr, wsx, wsy, nn_idx, nn_d2, rs_d2, rs_idx, snap_pose, cand, &j, &px, &py,
-                &pyaw);
-    const double x = wsx[j], y = wsy[j];
-    const double yaw = atan2(py - y, px - x);
-    prep[t] = steer_prep(sc, x, y, yaw, px, py, pyaw);
-    if (t < W)
-        snap_yaw[t] = yaw;
-    else
-        cand[t - W].yaw = yaw;
+// One segment's endpoint from its origin (interpolate at the full length, dubins.rs:155-198)
+// with the transcendental values supplied: ca/sa as in PrepRec, sl/cl = sin/cos(length).
+struct Pt {
+    double x, y;
+};
+__device__ inline Pt seg_end(int mode, double len, double c, double ox, double oy, double ca,
+                             double sa, double sl, double cl) {
+    Pt r;
+    if (mode == kModeS) {
+        r.x = ox + len / c * ca;
+        r.y = oy + len / c * sa;
+    } else {
+        const double ldx = sl / c;
+        const double ldy = mode == kModeL ? (1.0 - cl) / c : (1.0 - cl) / -c;
+        const double gdx = ca * ldx + sa * ldy;
+        const double gdy = -sa * ldx + ca * ldy;
+        r.x = ox + gdx;
+        r.y = oy + gdy;
+    }
+    return r;
 }
 
-// steer_walk, one task per wave (persistent grid, grid-stride); kLds: the scene's disc grid is
-// staged into this workgroup's LDS first.
+// steer_prep: kPrepLanes lanes per task (persistent grid over the window's W + ncomp tasks).
+// compute_yaw (rrt.rs:267-271), dubins_path_planning's frame change and word choice
+// (dubins.rs:333-363, 401-408), the segment origins and the `pd += d` walk of
+// generate_local_course (dubins.rs:200-272).  Every transcendental sits at a call site all lanes
+// reach with per-lane arguments (lane r evaluates word r; one sin and one cos call give all the
+// segment trig), so a task's chain is ~9 calls deep instead of ~32.  The walk itself is serial
+// (each pd is the previous one plus d, rounded); all 8 lanes replay it and lane r stores the
+// points g with g % 8 == r.
+__global__ __launch_bounds__(256) void steer_prep_kernel(
+    const DevState* __restrict__ st, SceneDev sc, const double* __restrict__ wsx,
+    const double* __restrict__ wsy, const double* __restrict__ snap_pose,
+    CandEntry* __restrict__ cand, PrepRec* __restrict__ rec, double* __restrict__ pdbuf,
+    double* __restrict__ snap_yaw) {
+    const int W = st->W;
+    const int total = W + st->ncomp;
+    const int lane = threadIdx.x & 63;
+    const int r = lane & (kPrepLanes - 1), g0 = lane & ~(kPrepLanes - 1);
+    const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    constexpr int TPW = 64 / kPrepLanes;  // tasks per wave
+    const double step = sc.step_size;
+    const double c = 1.0 / sc.turn_radius;
+    for (int base = gw * TPW; base < total; base += nw * TPW) {
+        const int t = base + lane / kPrepLanes;
+        const bool act = t < total;
+        int j = 0;
+        double px = 1.0, py = 0.0, pyaw = 0.0;
+        if (act)
+            window_task(t, W, wsx, wsy, snap_pose, cand, &j, &px, &py, &pyaw);
+        const double x = act ? wsx[j] : 0.0, y = act ? wsy[j] : 0.0;
+        const double yaw = atan2(py - y, px - x);
+        // dubins_path_planning, dubins.rs:401-408 (s = child, e = parent)
+        const double ex = px - x, ey = py - y;
+        const double cyw = cos(yaw), syw = sin(yaw);
+        const double lex = cyw * ex + syw * ey;
+        const double ley = -(syw)*ex + cyw * ey;
+        const double leyaw = pyaw - yaw;
+        // dubins_path_planning_from_origin, dubins.rs:333-348
+        const double hyp = hypot(lex, ley);
+        const double d = hyp * c;
+        const double theta = mod2pi(atan2(ley, lex));
+        const double alpha = mod2pi(-theta);
+        const double beta = mod2pi(leyaw - theta);
+        // lanes 0/1: sin(alpha), sin(beta); lanes 0/1/2: cos(alpha), cos(beta), cos(alpha - beta)
+        const double s_in = sin(r == 0 ? alpha : beta);
+        const double c_in = cos(r == 0 ? alpha : (r == 1 ? beta : alpha - beta));
+        const double sa = __shfl(s_in, g0), sb = __shfl(s_in, g0 + 1);
+        const double ca = __shfl(c_in, g0), cb = __shfl(c_in, g0 + 1), c_ab = __shfl(c_in, g0 + 2);
+        // lane r < 6 evaluates word r of ALL_PLANNERS (dubins.rs:27-153, 291)
+        const double dd2 = d * d;
+        double ya = 0.0, xa = 1.0, psq = -1.0, tmpc = 2.0;
+        if (r == 0) {
+            psq = 2.0 + dd2 - (2.0 * c_ab) + (2.0 * d * (sa - sb));
+            ya = cb - ca;
+            xa = d + sa - sb;
+        } else if (r == 1) {
+            psq = 2.0 + dd2 - (2.0 * c_ab) + (2.0 * d * (sb - sa));
+            ya = ca - cb;
+            xa = d - sa + sb;
+        } else if (r == 2) {
+            psq = -2.0 + dd2 + (2.0 * c_ab) + (2.0 * d * (sa + sb));
+            ya = -ca - cb;
+            xa = d + sa + sb;
+        } else if (r == 3) {
+            psq = -2.0 + dd2 + (2.0 * c_ab) - (2.0 * d * (sa + sb));
+            ya = ca + cb;
+            xa = d - sa - sb;
+        } else if (r == 4) {
+            tmpc = (6.0 - dd2 + 2.0 * c_ab + 2.0 * d * (sa - sb)) / 8.0;
+            ya = ca - cb;
+            xa = d - sa + sb;
+        } else if (r == 5) {
+            tmpc = (6.0 - dd2 + 2.0 * c_ab + 2.0 * d * (-sa + sb)) / 8.0;
+            ya = ca - cb;
+            xa = d + sa - sb;
+        }
+        const bool wok = r < 4 ? !(psq < 0.0) : (r < 6 ? !(fabs(tmpc) > 1.0) : false);
+        const double A1 = atan2(ya, xa);
+        const double pp = sqrt(r < 4 && wok ? psq : 0.0);
+        const double A2 = atan2(r == 2 ? -2.0 : 2.0, pp);
+        const double Cc = acos(r >= 4 && wok ? tmpc : 0.0);
+        double wt = 0.0, wp = 0.0, wq = 0.0;
+        if (r == 0) {
+            wt = mod2pi(-alpha + A1);
+            wp = pp;
+            wq = mod2pi(beta - A1);
+        } else if (r == 1) {
+            wt = mod2pi(alpha - A1);
+            wp = pp;
+            wq = mod2pi(-beta + A1);
+        } else if (r == 2) {
+            const double tm = A1 - A2;
+            wt = mod2pi(-alpha + tm);
+            wp = pp;
+            wq = mod2pi(-mod2pi(beta) + tm);
+        } else if (r == 3) {
+            const double tm = A1 - A2;
+            wt = mod2pi(alpha - tm);
+            wp = pp;
+            wq = mod2pi(beta - tm);
+        } else if (r == 4) {
+            wp = mod2pi(2.0 * kPi - Cc);
+            wt = mod2pi(alpha - A1 + mod2pi(wp / 2.0));
+            wq = mod2pi(alpha - beta - wt + mod2pi(wp));
+        } else if (r == 5) {
+            wp = mod2pi(2.0 * kPi - Cc);
+            wt = mod2pi(-alpha - A1 + wp / 2.0);
+            wq = mod2pi(mod2pi(beta) - alpha - wt + mod2pi(wp));
+        }
+        const double wcost = fabs(wt) + fabs(wp) + fabs(wq);
+        // first strict minimum in ALL_PLANNERS order (dubins.rs:351-360)
+        double bc = __builtin_inf();
+        int bw = -1;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const double ck = __shfl(wcost, g0 + k);
+            const int okk = __shfl((int)wok, g0 + k);
+            if (okk && bc > ck) {
+                bc = ck;
+                bw = k;
+            }
+        }
+        const int src = g0 + (bw < 0 ? 0 : bw);
+        const double L0 = __shfl(wt, src), L1 = __shfl(wp, src), L2 = __shfl(wq, src);
+        const int m0 = word_mode(bw, 0), m1 = word_mode(bw, 1), m2 = word_mode(bw, 2);
+        int state = !act ? kReject : (bw < 0 ? kPrepNone : kPrepWalk);
+        double tot = 0.0;
+        tot += L0;
+        tot += L1;
+        tot += L2;
+        const double nq = trunc(tot / step);
+        if (state == kPrepWalk && (!(nq >= 0.0) || nq > 1.0e8)) state = kError;
+        // segment origin headings (interpolate's yaw, dubins.rs:191-196)
+        const double oy0 = 0.0;
+        const double oy1 = m0 == kModeL ? oy0 + L0 : (m0 == kModeR ? oy0 - L0 : oy0);
+        const double oy2 = m1 == kModeL ? oy1 + L1 : (m1 == kModeR ? oy1 - L1 : oy1);
+        // lanes 0..2: segment trig, 3..5: sin/cos of the lengths, 6: the world transform
+        double arg = 0.0;
+        if (r < 3) {
+            const int ms = r == 0 ? m0 : (r == 1 ? m1 : m2);
+            const double oys = r == 0 ? oy0 : (r == 1 ? oy1 : oy2);
+            arg = ms == kModeS ? oys : -oys;
+        } else if (r < 6) {
+            arg = r == 3 ? L0 : (r == 4 ? L1 : L2);
+        } else if (r == 6) {
+            arg = -yaw;
+        }
+        const double sv = sin(arg), cv = cos(arg);
+        const double ca0 = __shfl(cv, g0), ca1 = __shfl(cv, g0 + 1), ca2 = __shfl(cv, g0 + 2);
+        const double sa0 = __shfl(sv, g0), sa1 = __shfl(sv, g0 + 1), sa2 = __shfl(sv, g0 + 2);
+        const double sl0 = __shfl(sv, g0 + 3), sl1 = __shfl(sv, g0 + 4), sl2 = __shfl(sv, g0 + 5);
+        const double cl0 = __shfl(cv, g0 + 3), cl1 = __shfl(cv, g0 + 4), cl2 = __shfl(cv, g0 + 5);
+        const double cw = __shfl(cv, g0 + 6), sw = __shfl(sv, g0 + 6);
+        const Pt O1 = seg_end(m0, L0, c, 0.0, 0.0, ca0, sa0, sl0, cl0);
+        const Pt O2 = seg_end(m1, L1, c, O1.x, O1.y, ca1, sa1, sl1, cl1);
+        const Pt E = seg_end(m2, L2, c, O2.x, O2.y, ca2, sa2, sl2, cl2);
+        // the trim (dubins.rs:281-288) drops exactly the endpoint unless its local x is 0.0
+        if (state == kPrepWalk && E.x == 0.0) state = kLiteral;
+        int cnt0 = 0, cnt1 = 0, cnt2 = 0;
+        if (state == kPrepWalk) {
+            double* pdv = pdbuf + (size_t)t * kPdCap;
+            int g = 0, seg = 0;
+            double Ls = L0;
+            double dd = (L0 > 0.0) ? step : -step;
+            double pd = dd - 0.0;
+            bool over = false;
+            for (;;) {  // every iteration stores a point (g < kPdCap) or ends a segment
+                if (fabs(pd) <= fabs(Ls)) {
+                    if (g >= kPdCap) {
+                        over = true;
+                        break;
+                    }
+                    if ((g & (kPrepLanes - 1)) == r) pdv[g] = pd;
+                    ++g;
+                    pd += dd;
+                } else {
+                    if (seg == 0)
+                        cnt0 = g;
+                    else if (seg == 1)
+                        cnt1 = g - cnt0;
+                    else
+                        cnt2 = g - cnt0 - cnt1;
+                    const double ll = Ls - pd - dd;
+                    if (++seg == 3) break;
+                    const double Ln = seg == 1 ? L1 : L2;
+                    const double dn = (Ln > 0.0) ? step : -step;
+                    pd = ((Ls * Ln) > 0.0) ? (-dn - ll) : (dn - ll);
+                    dd = dn;
+                    Ls = Ln;
+                }
+            }
+            // no trailing zero left for the trim (or the reference's index panic): literal path
+            if (over)
+                state = kPrepFallback;
+            else if (1 + (long long)g > (long long)nq + 7 - 2)
+                state = kLiteral;
+        }
+        if (act && r == 0) {
+            PrepRec o;
+            o.x = x;
+            o.y = y;
+            o.px = px;
+            o.py = py;
+            o.yaw = yaw;
+            o.pyaw = pyaw;
+            o.c = c;
+            o.cw = cw;
+            o.sw = sw;
+            o.ox[0] = 0.0;
+            o.oy[0] = 0.0;
+            o.ox[1] = O1.x;
+            o.oy[1] = O1.y;
+            o.ox[2] = O2.x;
+            o.oy[2] = O2.y;
+            o.ca[0] = ca0;
+            o.ca[1] = ca1;
+            o.ca[2] = ca2;
+            o.sa[0] = sa0;
+            o.sa[1] = sa1;
+            o.sa[2] = sa2;
+            o.L[0] = L0;
+            o.L[1] = L1;
+            o.L[2] = L2;
+            o.n_point = (long long)nq + 3 + 4;
+            o.m[0] = m0;
+            o.m[1] = m1;
+            o.m[2] = m2;
+            o.cnt[0] = cnt0;
+            o.cnt[1] = cnt1;
+            o.cnt[2] = cnt2;
+            o.state = state;
+            o.pad = 0;
+            rec[t] = o;
+            if (t < W)
+                snap_yaw[t] = yaw;
+            else
+                cand[t - W].yaw = yaw;
+        }
+    }
+}
+
+// steer_walk for one PrepRec (called by all 64 lanes; the record is wave-uniform).  Chunks of 63
+// grid points: lane k >= 1 interpolates grid point base + k - 1 (interpolate, dubins.rs:155-198,
+// then the world transform dubins.rs:412-422), lane 0 carries the previous chunk's last point,
+// and the junction to the parent follows the last grid point.  A kPrepWalk task reads its pd
+// values from pdbuf; a kPrepFallback task (more than kPdCap points) regenerates them with the
+// uniform serial `pd += d` walk, each lane capturing its own point.
+template <bool kLds>
+__device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
+                                        const double* __restrict__ pdv) {
+    const int lane = threadIdx.x & 63;
+    const int state = p->state;
+    const double x = p->x, y = p->y, px = p->px, py = p->py;
+    if (state == kPrepNone) {  // steer failed: polyline [(x, y), (px, py)] (rrt.rs:313)
+        const bool has = lane < 2;
+        const double qx = lane == 0 ? x : px, qy = lane == 0 ? y : py;
+        return chunk_rejects<kLds>(sc, has, has, lane == 1, qx, qy) ? kReject : kAccept;
+    }
+    if (state != kPrepWalk && state != kPrepFallback) return state;
+    const bool gen = state == kPrepFallback;
+    const double step = sc.step_size;
+    const double c = p->c, cw = p->cw, sw = p->sw;
+    const double ox1 = p->ox[1], oy1 = p->oy[1], ox2 = p->ox[2], oy2 = p->oy[2];
+    const double ca0 = p->ca[0], ca1 = p->ca[1], ca2 = p->ca[2];
+    const double sa0 = p->sa[0], sa1 = p->sa[1], sa2 = p->sa[2];
+    const double L0 = p->L[0], L1 = p->L[1], L2 = p->L[2];
+    const int m0 = p->m[0], m1 = p->m[1], m2 = p->m[2];
+    const int n0 = p->cnt[0], n01 = n0 + p->cnt[1], ng = n01 + p->cnt[2];
+    // serial generator state (kPrepFallback only)
+    int gseg = 0;
+    double gdd = (L0 > 0.0) ? step : -step;
+    double gpd = gdd - 0.0;
+    long long grid = 0;
+    double carry_x = x, carry_y = y;
+    for (int base = 0;; base += 63) {
+        int cnt = 0, my_seg = 0;
+        double my_pd = 0.0;
+        bool done;
+        if (gen) {
+            while (cnt < 63 && gseg < 3) {
+                const double Ls = gseg == 0 ? L0 : (gseg == 1 ? L1 : L2);
+                if (fabs(gpd) <= fabs(Ls)) {
+                    if (lane == cnt + 1) {
+                        my_seg = gseg;
+                        my_pd = gpd;
+                    }
+                    ++cnt;
+                    gpd += gdd;
+                } else {
+                    const double ll = Ls - gpd - gdd;
+                    if (++gseg < 3) {
+                        const double Ln = gseg == 1 ? L1 : L2;
+                        gdd = (Ln > 0.0) ? step : -step;
+                        gpd = ((Ls * Ln) > 0.0) ? (-gdd - ll) : (gdd - ll);
+                    }
+                }
+            }
+            grid += cnt;
+            done = gseg >= 3;
+        } else {
+            const int rem = ng - base;
+            cnt = rem < 63 ? rem : 63;
+            done = rem < 63;
+            const int g = base + lane - 1;
+            if (lane >= 1 && lane <= cnt) {
+                my_pd = pdv[g];
+                my_seg = g < n0 ? 0 : (g < n01 ? 1 : 2);
+            }
+        }
+        const bool junction_here = done && cnt < 63;
+        const bool isgrid = lane >= 1 && lane <= cnt;
+        const bool isj = junction_here && lane == cnt + 1;
+        double qx = carry_x, qy = carry_y;
+        if (isgrid) {
+            const int mm = my_seg == 0 ? m0 : (my_seg == 1 ? m1 : m2);
+            const double ox = my_seg == 0 ? 0.0 : (my_seg == 1 ? ox1 : ox2);
+            const double oy = my_seg == 0 ? 0.0 : (my_seg == 1 ? oy1 : oy2);
+            const double ca = my_seg == 0 ? ca0 : (my_seg == 1 ? ca1 : ca2);
+            const double sa = my_seg == 0 ? sa0 : (my_seg == 1 ? sa1 : sa2);
+            const double pd = my_pd;
+            double lx, ly;
+            if (mm == kModeS) {
+                lx = ox + pd / c * ca;
+                ly = oy + pd / c * sa;
+            } else {
+                const double ldx = sin(pd) / c;
+                const double ldy = (1.0 - cos(pd)) / (mm == kModeL ? c : -c);
+                const double gdx = ca * ldx + sa * ldy;
+                const double gdy = -sa * ldx + ca * ldy;
+                lx = ox + gdx;
+                ly = oy + gdy;
+            }
+            qx = cw * lx + sw * ly + x;   // dubins.rs:415
+            qy = -sw * lx + cw * ly + y;  // dubins.rs:420
+        } else if (isj) {
+            qx = px;
+            qy = py;
+        }
+        const bool has = lane == 0 || isgrid || isj;
+        const bool chk = isgrid || isj || (base == 0 && lane == 0);
+        if (chunk_rejects<kLds>(sc, has, chk, has && lane >= 1, qx, qy)) return kReject;
+        if (junction_here) break;
+        carry_x = __shfl(qx, 63);
+        carry_y = __shfl(qy, 63);
+    }
+    // no trailing zero left for the trim (dubins.rs:281-288): the literal path decides
+    if (gen && 1 + grid > p->n_point - 2) return kLiteral;
+    return kAccept;
+}
+
+// steer_walk, one task per wave (persistent grid, grid-stride over the W + ncomp tasks); kLds:
+// the scene's disc grid is staged into this workgroup's LDS first.
 template <bool kLds>
 __global__ __launch_bounds__(256, 4) void steer_walk_kernel(const DevState* __restrict__ st,
                                                          SceneDev sc,
-                                                         const SteerPrep* __restrict__ prep,
+                                                         const PrepRec* __restrict__ rec,
+                                                         const double* __restrict__ pdbuf,
                                                          CandEntry* __restrict__ cand,
-                                                         int* __restrict__ snap_status, int spec) {
+                                                         int* __restrict__ snap_status) {
     const int lane = threadIdx.x & 63;
     const int W = st->W;
-    const int first = spec ? W : 0;
-    const int total = spec ? W + st->ncomp : W;
-    if (first + (int)blockIdx.x * 4 >= total) return;  // whole workgroup idle
+    const int total = W + st->ncomp;
+    if ((int)blockIdx.x * 4 >= total) return;  // whole workgroup idle
     if (kLds) stage_scene(sc);
-    const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    for (int t = first + gw; t < total; t += nw) {
-        const WalkIn r = walk_in(prep + t);
-#ifdef PP_STAMPS
-        int64_t ph[6] = {0, 0, 0, 0, 0, 0};
-        PP_STAMP(tt0);
-        const int s = steer_walk<kLds>(sc, r, ph);
-        PP_STAMP(tt1);
-        if (lane == 0 && !spec) {
-            DevState* sw = const_cast<DevState*>(st);
-            atomicAdd((unsigned long long*)&sw->stamps[0], (unsigned long long)(tt1 - tt0));
-            atomicAdd((unsigned long long*)&sw->stamps[2], (unsigned long long)ph[2]);
-            atomicAdd((unsigned long long*)&sw->stamps[3], (unsigned long long)ph[3]);
-            atomicAdd((unsigned long long*)&sw->stamps[4], (unsigned long long)ph[4]);
-            atomicAdd((unsigned long long*)&sw->stamps[5], (unsigned long long)ph[5]);
-        }
-#else
-        const int s = steer_walk<kLds>(sc, r);
-#endif
+    for (int t = gw; t < total; t += nw) {
+        const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap);
         if (lane == 0) {
             if (t < W)
                 snap_status[t] = s;
@@ -936,8 +1234,7 @@ __device__ inline int block_exclusive_scan(int v, int* s_wave, int* total) {
 __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
     DevState* __restrict__ st, SceneDev sc, TreeDev tr, const double* __restrict__ wsx,
     const double* __restrict__ wsy, const int* __restrict__ nn_idx,
-    const double* __restrict__ nn_d2, const double* __restrict__ rs_d2,
-    const int* __restrict__ rs_idx, const int* __restrict__ cand_cnt,
+    const int* __restrict__ cand_cnt,
     const CandEntry* __restrict__ cand, const int* __restrict__ snap_status,
     const double* __restrict__ snap_yaw, ResolveScratch rs, double* __restrict__ lit_scratch) {
     constexpr int NT = kResolveThreads;
@@ -1103,7 +1400,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
                 const double x = wsx[j], y = wsy[j];
                 double px, py, pyaw;
                 if (p < 0) {
-                    const int q = final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);
+                    const int q = nn_idx[j];
                     px = tr.x[q];
                     py = tr.y[q];
                     pyaw = tr.yaw[q];
@@ -1165,13 +1462,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
         if (!s_verdict[j]) continue;
         const int nd = s_off[j];
         const int p = s_par[j];
-        int par;
-        if (p >= 0)
-            par = s_off[p];
-        else if (v_p[q] >= 0)
-            par = v_p[q];
-        else
-            par = final_nn(j, nn_idx, nn_d2, rs_d2, rs_idx, nullptr);  // flagged sample
+        const int par = p >= 0 ? s_off[p] : v_p[q];
         tr.x[nd] = v_x[q];
         tr.y[nd] = v_yy[q];
         tr.x32[nd] = (float)v_x[q];
@@ -1207,12 +1498,10 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
 
 // --------------------------------------------------------------------------- launch wrappers
 
-hipError_t launch_window(hipStream_t s, hipStream_t s2, hipEvent_t ev_nn, hipEvent_t ev_pairs,
-                         const WindowArgs& a, hipEvent_t* ev) {
+hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev) {
     const int K = a.K;
     const int nqb = (K + kQPB - 1) / kQPB;
-    const int Tk = (K + 63) / 64;
-    const int tiles = Tk * (Tk + 1) / 2;
+    const int Tp = (K + kPairTile - 1) / kPairTile;
     window_begin_kernel<<<(K + 255) / 256, 256, 0, s>>>(a.st, K, a.target, a.seed, a.sc.minx,
                                                          a.sc.maxx, a.sc.miny, a.sc.maxy, a.wsx,
                                                          a.wsy, a.cand_cnt);
@@ -1224,40 +1513,26 @@ hipError_t launch_window(hipStream_t s, hipStream_t s2, hipEvent_t ev_nn, hipEve
                                                      a.wsy, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord,
                                                      a.nn_idx, a.nn_d2, a.snap_pose, a.flag_list);
     nn_rescan_kernel<<<dim3(kMaxChunks, kRescanSlots), 256, 0, s>>>(
-        a.st, a.flag_list, a.wsx, a.wsy, a.tr.x, a.tr.y, a.rs_d2, a.rs_idx);
-    hipError_t e = hipEventRecord(ev_nn, s);
-    if (e != hipSuccess) return e;
-    // second stream: candidate lists, then the candidate steers
-    e = hipStreamWaitEvent(s2, ev_nn, 0);
-    if (e != hipSuccess) return e;
-    window_pairs_kernel<<<(tiles + 3) / 4, 256, 0, s2>>>(a.st, a.wsx, a.wsy, a.nn_idx, a.nn_d2,
-                                                         a.rs_d2, a.rs_idx, a.cand_cnt, a.cand);
-    const int lds = a.sc.lds_bytes;
-    const int spec_cap = K * kCandCap;
-    steer_prep_kernel<<<(spec_cap + 255) / 256, 256, 0, s2>>>(
-        a.st, a.sc, a.tr, a.wsx, a.wsy, a.nn_idx, a.nn_d2, a.rs_d2, a.rs_idx, a.snap_pose, a.cand,
-        a.prep, a.snap_yaw, 1);
-    if (lds > 0)
-        steer_walk_kernel<true><<<64, 256, lds, s2>>>(a.st, a.sc, a.prep, a.cand, a.snap_status, 1);
-    else
-        steer_walk_kernel<false><<<64, 256, 0, s2>>>(a.st, a.sc, a.prep, a.cand, a.snap_status, 1);
-    e = hipEventRecord(ev_pairs, s2);
-    if (e != hipSuccess) return e;
-    // first stream: the snapshot steers meanwhile
+        a.st, a.flag_list, a.wsx, a.wsy, a.tr.x, a.tr.y, a.tr.yaw, a.rs_d2, a.rs_idx, a.rs_done,
+        a.nn_idx, a.nn_d2, a.snap_pose);
+    window_pairs_kernel<<<Tp * (Tp + 1) / 2, kPairTile, 0, s>>>(a.st, a.wsx, a.wsy, a.nn_d2,
+                                                                a.cand_cnt, a.cand);
     if (ev) (void)hipEventRecord(ev[2], s);
-    steer_prep_kernel<<<(K + 255) / 256, 256, 0, s>>>(a.st, a.sc, a.tr, a.wsx, a.wsy, a.nn_idx,
-                                                      a.nn_d2, a.rs_d2, a.rs_idx, a.snap_pose,
-                                                      a.cand, a.prep, a.snap_yaw, 0);
-    const int nwg = std::min((K + 3) / 4, 1024);  // persistent walk grid
+    // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
+    const int prep_blocks = (2 * K * kPrepLanes + 255) / 256;
+    steer_prep_kernel<<<prep_blocks, 256, 0, s>>>(a.st, a.sc, a.wsx, a.wsy, a.snap_pose, a.cand,
+                                                  a.rec, a.pdbuf, a.snap_yaw);
+    const int lds = a.sc.lds_bytes;
+    const int nwg = std::min((K + 3) / 4, 1024);
     if (lds > 0)
-        steer_walk_kernel<true><<<nwg, 256, lds, s>>>(a.st, a.sc, a.prep, a.cand, a.snap_status, 0);
+        steer_walk_kernel<true><<<nwg, 256, lds, s>>>(a.st, a.sc, a.rec, a.pdbuf, a.cand,
+                                                      a.snap_status);
     else
-        steer_walk_kernel<false><<<nwg, 256, 0, s>>>(a.st, a.sc, a.prep, a.cand, a.snap_status, 0);
+        steer_walk_kernel<false><<<nwg, 256, 0, s>>>(a.st, a.sc, a.rec, a.pdbuf, a.cand,
+                                                     a.snap_status);
     if (ev) (void)hipEventRecord(ev[3], s);
-    e = hipStreamWaitEvent(s, ev_pairs, 0);
-    if (e != hipSuccess) return e;
-    resolve_kernel<<<1, kResolveThreads, 0, s>>>(a.st, a.sc, a.tr, a.wsx, a.wsy, a.nn_idx, a.nn_d2,
-                                                 a.rs_d2, a.rs_idx, a.cand_cnt, a.cand,
+    resolve_kernel<<<1, kResolveThreads, 0, s>>>(a.st, a.sc, a.tr, a.wsx, a.wsy, a.nn_idx,
+                                                 a.cand_cnt, a.cand,
                                                  a.snap_status, a.snap_yaw, a.rs, a.lit_scratch);
     return hipGetLastError();
 }
@@ -1271,8 +1546,8 @@ hipError_t launch_nearest(hipStream_t s, const WindowArgs& a) {
                                                      a.wsy, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord,
                                                      a.nn_idx, a.nn_d2, nullptr, a.flag_list);
     nn_rescan_kernel<<<dim3(kMaxChunks, kRescanSlots), 256, 0, s>>>(
-        a.st, a.flag_list, a.wsx, a.wsy, a.tr.x, a.tr.y, a.rs_d2, a.rs_idx);
-    nn_fix_kernel<<<(K + 255) / 256, 256, 0, s>>>(a.st, a.nn_idx, a.nn_d2, a.rs_d2, a.rs_idx);
+        a.st, a.flag_list, a.wsx, a.wsy, a.tr.x, a.tr.y, a.tr.yaw, a.rs_d2, a.rs_idx, a.rs_done,
+        a.nn_idx, a.nn_d2, nullptr);
     return hipGetLastError();
 }
 

@@ -24,6 +24,8 @@ constexpr int kLiteralWaves = 256;   // literal scratch buffers (explicit-task k
 constexpr int kResolveThreads = 256; // one workgroup resolves a window (4 waves: 1 per SIMD)
 constexpr int kMaxWindow = 4096;     // K limit: the resolve keeps the window's state in LDS
 constexpr int kSteerPrepBytes = 152; // sizeof(SteerPrep) (checked in pp_kernels.hip)
+constexpr int kPdCap = 256;          // grid points per task stored by steer_prep (more: fallback)
+constexpr int kPrepLanes = 8;        // lanes per task in steer_prep
 
 // Scene in device memory (Space, rrt.rs:70-78, with Q10 analytic discs).
 struct SceneDev {
@@ -89,6 +91,22 @@ struct CandEntry {
     int status;
     int pad;
 };
+
+// Per-task steer record of the window pipeline, written by steer_prep (8 lanes per task) and read
+// by steer_walk (one wave per task) with scalar loads.  The task's grid-point distances (the
+// `pd` values of generate_local_course, dubins.rs:239-255) sit in pdbuf[t * kPdCap + g]; a task
+// with more than kPdCap grid points (kPrepFallback) is walked serially by steer_walk instead.
+struct PrepRec {
+    double x, y, px, py, yaw, pyaw;  // child (point 0), parent (the junction) and their headings
+    double c, cw, sw;                // curvature, cos/sin(-yaw) of the world transform
+    double ox[3], oy[3];             // segment origins in the local frame
+    double ca[3], sa[3];             // segment trig: S cos/sin(o.yaw), L/R cos/sin(-o.yaw)
+    double L[3];                     // segment lengths (the serial walk of kPrepFallback)
+    long long n_point;               // dubins.rs:369
+    int m[3], cnt[3];                // segment modes and grid points per segment
+    int state, pad;                  // kPrepWalk / kPrepNone / kPrepFallback or a verdict
+};
+enum : int { kPrepWalk = -1, kPrepNone = 4, kPrepFallback = 5 };
 
 // Resolve scratch (global, one window).
 struct ResolveScratch {
