@@ -490,9 +490,22 @@ __device__ inline Top2 merge_top2(Top2 a, Top2 c) {
 
 // RRT::get_nearest_node screen (rrt.rs:378-391): f32 SoA nodes x W samples.  Grid = nqb * 64
 // blocks (nqb sample blocks x 64 node chunks), mapped XCD-aware so the nqb blocks that stream the
-// same node chunk share one XCD's L2.  Each wave scans a quarter of the chunk; node coordinates
-// are wave-uniform scalar loads used as SGPR operands; every lane holds 4 samples and keeps an
-// exact per-lane top-2 (best, second, index of best).
+// same node chunk share one XCD's L2.  Each wave scans a quarter of the chunk with node
+// coordinates as wave-uniform scalar loads (double-buffered one block ahead); every lane holds 4
+// samples as two packed pairs, so a node costs 2 packed VALU ops per sample for the distance
+// (v_pk_add / v_pk_mul / v_pk_fma on f32x2).  Per block of kScanBlk nodes each sample keeps only
+// the block minimum (v_min3), then merges it into (best, second) with med3 and records the block
+// that first attained the best.  The winning block is re-evaluated afterwards with the same
+// arithmetic (bit-identical distances) for the lowest index and the in-block second best, so the
+// result is the exact per-chunk top-2 of the f32 distances, as before.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr int kScanBlk = 16;
+
+__device__ __forceinline__ float scan_d2(float qx, float qy, float nx, float ny) {
+    const float dx = qx - nx, dy = qy - ny;
+    return __builtin_fmaf(dy, dy, dx * dx);
+}
+
 __global__ __launch_bounds__(256) void nn_scan_kernel(const DevState* __restrict__ st,
                                                       const float* __restrict__ nx,
                                                       const float* __restrict__ ny,
@@ -501,6 +514,7 @@ __global__ __launch_bounds__(256) void nn_scan_kernel(const DevState* __restrict
                                                       int stride, float* __restrict__ pbest,
                                                       float* __restrict__ psecond,
                                                       int* __restrict__ pidx) {
+    static_assert(kQPL == 4, "two packed sample pairs per lane");
     __shared__ float s_b[4][kQPB];
     __shared__ float s_s[4][kQPB];
     __shared__ int s_i[4][kQPB];
@@ -516,7 +530,7 @@ __global__ __launch_bounds__(256) void nn_scan_kernel(const DevState* __restrict
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int qbase = qb * kQPB;
     float qxr[kQPL], qyr[kQPL], best[kQPL], second[kQPL];
-    int bi[kQPL];
+    int blk[kQPL], bi[kQPL];
 #pragma unroll
     for (int r = 0; r < kQPL; ++r) {
         const int q = qbase + r * 64 + lane;
@@ -524,42 +538,104 @@ __global__ __launch_bounds__(256) void nn_scan_kernel(const DevState* __restrict
         qyr[r] = q < W ? (float)qy[q] : 0.0f;
         best[r] = __builtin_inff();
         second[r] = __builtin_inff();
+        blk[r] = -1;
         bi[r] = -1;
     }
-    const int per = (((c1 - c0) + 3) / 4 + 7) & ~7;
-    // wave-uniform range: readfirstlane lets the compiler use scalar loads for the nodes
+    const f32x2 qxa = {qxr[0], qxr[1]}, qya = {qyr[0], qyr[1]};
+    const f32x2 qxb = {qxr[2], qxr[3]}, qyb = {qyr[2], qyr[3]};
+    // wave-uniform range (kScanBlk-aligned start): readfirstlane lets the compiler use scalar loads
+    const int per = (((c1 - c0) + 3) / 4 + kScanBlk - 1) & ~(kScanBlk - 1);
     const int w0 = __builtin_amdgcn_readfirstlane(min(c0 + wave * per, c1));
     const int w1 = __builtin_amdgcn_readfirstlane(min(w0 + per, c1));
-    int k = w0;
-    for (; k + 8 <= w1; k += 8) {
-        float px[8], py[8];
+    const int wb = w0 + ((w1 - w0) / kScanBlk) * kScanBlk;  // end of the whole blocks
+    if (w0 < wb) {
+        float cx[kScanBlk], cy[kScanBlk];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            px[u] = nx[k + u];
-            py[u] = ny[k + u];
+        for (int u = 0; u < kScanBlk; ++u) {
+            cx[u] = nx[w0 + u];
+            cy[u] = ny[w0 + u];
         }
+        for (int k = w0; k < wb; k += kScanBlk) {
+            float px[kScanBlk], py[kScanBlk];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < kScanBlk; ++u) {
+                px[u] = cx[u];
+                py[u] = cy[u];
+            }
+            const int kn = k + kScanBlk < wb ? k + kScanBlk : k;  // prefetch the next block
+#pragma unroll
+            for (int u = 0; u < kScanBlk; ++u) {
+                cx[u] = nx[kn + u];
+                cy[u] = ny[kn + u];
+            }
+            float bm[kQPL];
+#pragma unroll
+            for (int u = 0; u < kScanBlk; ++u) {
+                const f32x2 sx = {px[u], px[u]}, sy = {py[u], py[u]};
+                const f32x2 dxa = qxa - sx, dya = qya - sy;
+                const f32x2 dxb = qxb - sx, dyb = qyb - sy;
+                const f32x2 da = __builtin_elementwise_fma(dya, dya, dxa * dxa);
+                const f32x2 db = __builtin_elementwise_fma(dyb, dyb, dxb * dxb);
+                if (u == 0) {
+                    bm[0] = da.x;
+                    bm[1] = da.y;
+                    bm[2] = db.x;
+                    bm[3] = db.y;
+                } else {
+                    bm[0] = __builtin_fminf(bm[0], da.x);
+                    bm[1] = __builtin_fminf(bm[1], da.y);
+                    bm[2] = __builtin_fminf(bm[2], db.x);
+                    bm[3] = __builtin_fminf(bm[3], db.y);
+                }
+            }
 #pragma unroll
             for (int r = 0; r < kQPL; ++r) {
-                const float dx = qxr[r] - px[u];
-                const float dy = qyr[r] - py[u];
-                const float d = __builtin_fmaf(dy, dy, dx * dx);
-                second[r] = __builtin_amdgcn_fmed3f(best[r], d, second[r]);
-                if (d < best[r]) {
-                    best[r] = d;
-                    bi[r] = k + u;
+                second[r] = __builtin_amdgcn_fmed3f(best[r], bm[r], second[r]);
+                if (bm[r] < best[r]) {
+                    best[r] = bm[r];
+                    blk[r] = k;
                 }
             }
         }
+        // the winning block again, scalar and bit-identical: lowest index of the best distance
+        // and the best of the block's other nodes (the block minima only carried one each)
+#pragma unroll
+        for (int r = 0; r < kQPL; ++r) {
+            if (blk[r] < 0) continue;
+            const float4* bx = reinterpret_cast<const float4*>(nx + blk[r]);
+            const float4* by = reinterpret_cast<const float4*>(ny + blk[r]);
+            float vx[kScanBlk], vy[kScanBlk];
+#pragma unroll
+            for (int v = 0; v < kScanBlk / 4; ++v) {
+                const float4 a4 = bx[v], b4 = by[v];
+                vx[4 * v] = a4.x;
+                vx[4 * v + 1] = a4.y;
+                vx[4 * v + 2] = a4.z;
+                vx[4 * v + 3] = a4.w;
+                vy[4 * v] = b4.x;
+                vy[4 * v + 1] = b4.y;
+                vy[4 * v + 2] = b4.z;
+                vy[4 * v + 3] = b4.w;
+            }
+            int ui = -1;
+            float other = __builtin_inff();
+#pragma unroll
+            for (int u = 0; u < kScanBlk; ++u) {
+                const float d = scan_d2(qxr[r], qyr[r], vx[u], vy[u]);
+                if (ui < 0 && d == best[r])
+                    ui = u;
+                else
+                    other = __builtin_fminf(other, d);
+            }
+            bi[r] = blk[r] + ui;
+            second[r] = __builtin_fminf(second[r], other);
+        }
     }
-    for (; k < w1; ++k) {
+    for (int k = wb; k < w1; ++k) {  // tail (< kScanBlk nodes): exact top-2 per node
         const float px = nx[k], py = ny[k];
 #pragma unroll
         for (int r = 0; r < kQPL; ++r) {
-            const float dx = qxr[r] - px;
-            const float dy = qyr[r] - py;
-            const float d = __builtin_fmaf(dy, dy, dx * dx);
+            const float d = scan_d2(qxr[r], qyr[r], px, py);
             second[r] = __builtin_amdgcn_fmed3f(best[r], d, second[r]);
             if (d < best[r]) {
                 best[r] = d;
