@@ -33,6 +33,7 @@ extern "C" {
 #define PP_ERR_CAPACITY (-4)
 #define PP_ERR_STATE (-5)          /* no scene / no planner configured yet */
 #define PP_ERR_STEER_OVERFLOW (-6) /* generate_local_course would index past n_point (panic) */
+#define PP_ERR_REFERENCE_PANIC (-7) /* finalize: an edge with no feasible Dubins word (panic) */
 
 typedef struct pp_ctx pp_ctx;
 
@@ -125,6 +126,25 @@ int pp_rrt_get_nearest_node_batch(pp_ctx* ctx, const double* qx, const double* q
  * ok[i] = 1 when the line to the root verifies; yaw[i] = the new node's yaw (may be NULL) */
 int pp_rrt_verify_node_batch(pp_ctx* ctx, const double* x, const double* y,
                              const int32_t* parent, int k, uint8_t* ok, double* yaw);
+
+/* --------------------------------------------------- goal connection (src/rrt.rs:428-619) */
+/* RRT::check_finish (rrt.rs:428-438) for k tree nodes: optimize_from_goal's shortcut search
+ * (rrt.rs:463-501, RECURSION_LIMIT 16), finalize's line (rrt.rs:503-540) and its verify.
+ * ok[i] = 1 when the line verifies (Some); length[i] = its euclidean_length, n_points[i] its
+ * points (both may be NULL; computed for verified lines only).  chain (may be NULL) receives k
+ * rows of PP_CF_CHAIN ints: [levels, edges, optimize's chosen ancestor per level...]. */
+#define PP_CF_CHAIN 18
+int pp_rrt_check_finish_batch(pp_ctx* ctx, const int32_t* nodes, int k, uint8_t* ok,
+                              double* length, int32_t* n_points, int32_t* chain);
+/* check_finish for one node with the line itself (root side first, as finalize returns it);
+ * *n = 0 when *ok = 0.  PP_ERR_CAPACITY when cap is too small. */
+int pp_rrt_check_finish(pp_ctx* ctx, int32_t node, uint8_t* ok, double* x, double* y,
+                        int64_t cap, int64_t* n, double* length);
+/* RRT::plan (rrt.rs:599-619), sequential spec: n_iter plan_one iterations (extend + check_finish
+ * on every accepted node); *best_node = the node whose finish has the minimum euclidean_length
+ * (first on ties, -1 when none verified); the line via pp_rrt_check_finish(best_node). */
+int pp_rrt_plan(pp_ctx* ctx, int64_t n_iter, int32_t* best_node, double* best_length,
+                int64_t* n_finishes);
 
 int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out);
 int pp_rrt_reset_stats(pp_ctx* ctx);

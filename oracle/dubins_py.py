@@ -304,3 +304,97 @@ def rrt_extend(scene, tree, seed, it0, n_iter):
             tree["parent"].append(p)
         log.append((p, int(ok)))
     return log
+
+
+# ------------------------------------------- check_finish / optimize / finalize (small cases)
+class PNode:
+    """rrt.rs:161-214: a point, an optional parent and the yaw toward it (or the given yaw)."""
+    __slots__ = ("x", "y", "yaw", "parent")
+
+    def __init__(self, x, y, yaw, parent):
+        self.x, self.y, self.yaw, self.parent = x, y, yaw, parent
+
+    @staticmethod
+    def new(x, y, parent):  # Node::new, compute_yaw (rrt.rs:169-175, 267-271)
+        return PNode(x, y, math.atan2(parent.y - y, parent.x - x), parent)
+
+    def iter_to_root(self):  # NodeIter (rrt.rs:253-265)
+        n = self
+        while n is not None:
+            yield n
+            n = n.parent
+
+
+def tree_nodes(tree):
+    """PNode objects for a tree dict (x, y, yaw, parent lists, root first)."""
+    nodes = []
+    for i in range(len(tree["x"])):
+        p = tree["parent"][i]
+        nodes.append(PNode(tree["x"][i], tree["y"][i], tree["yaw"][i], nodes[p] if p >= 0 else None))
+    return nodes
+
+
+def line_to_origin(node, R, step):  # rrt.rs:291-321, sequential order
+    xs, ys = [], []
+    for n in node.iter_to_root():
+        if n.parent is None:
+            xs.append(n.x)
+            ys.append(n.y)
+            continue
+        r = dubins_path_planning(n.x, n.y, n.yaw, n.parent.x, n.parent.y, n.parent.yaw, R, step)
+        if r is None:
+            xs.append(n.x)
+            ys.append(n.y)
+        else:
+            xs.extend(r[0])
+            ys.extend(r[1])
+    return xs, ys
+
+
+def optimize(scene, node, i, chain):  # rrt.rs:463-487, full line_to_origin verify
+    if i >= 16:
+        return None
+    R, step = scene["turn_radius"], scene["step_size"]
+    for to in reversed(list(node.iter_to_root())):
+        new = PNode.new(node.x, node.y, to)
+        if verify_line(scene, *line_to_origin(new, R, step)):
+            chain.append(to)
+            t = optimize(scene, to, i + 1, chain)
+            return PNode.new(node.x, node.y, t) if t is not None else new
+    return None
+
+
+def finalize(scene, goal):  # rrt.rs:489-540
+    R, step = scene["turn_radius"], scene["step_size"]
+    chain = []
+    if goal.parent is not None:
+        n = optimize(scene, goal.parent, 0, chain)
+        if n is not None:
+            goal = PNode(goal.x, goal.y, goal.yaw, n)
+    xs, ys = [], []
+    for n in goal.iter_to_root():
+        if n.parent is None:
+            continue
+        r = dubins_path_planning(n.x, n.y, n.yaw, n.parent.x, n.parent.y, n.parent.yaw, R, step)
+        if r is None:
+            raise RuntimeError("Should plan dubins curve")  # rrt.rs:529
+        xs.extend(r[0])
+        ys.extend(r[1])
+    xs.reverse()
+    ys.reverse()
+    return xs, ys, chain
+
+
+def line_length(xs, ys):  # geo EuclideanLength: sum of hypot over consecutive points
+    s = 0.0
+    for i in range(len(xs) - 1):
+        s += libm_hypot(xs[i + 1] - xs[i], ys[i + 1] - ys[i])
+    return s
+
+
+def check_finish(scene, node, goal, goal_yaw):  # rrt.rs:428-438
+    """(ok, xs, ys, length, chain) — chain = optimize's chosen ancestors (PNode objects)."""
+    g = PNode(goal[0], goal[1], goal_yaw, node)  # Node::new_goal
+    xs, ys, chain = finalize(scene, g)
+    ok = verify_line(scene, xs, ys)
+    return ok, xs, ys, line_length(xs, ys), chain

@@ -77,6 +77,17 @@ def lib():
             L.orc_verify_candidate.argtypes = [C.POINTER(Scene), C.POINTER(Tree), C.c_double,
                                                C.c_double, C.c_int, C.c_int, dp]
             L.orc_verify_candidate.restype = C.c_int
+            ip = C.POINTER(C.c_int)
+            L.orc_check_finish.argtypes = [C.POINTER(Scene), C.POINTER(Tree), C.c_int, C.c_double,
+                                           C.c_double, C.c_double, C.c_int, dp, dp, C.c_int, ip,
+                                           dp, ip, ip]
+            L.orc_check_finish.restype = C.c_int
+            L.orc_line_length.argtypes = [dp, dp, C.c_int]
+            L.orc_line_length.restype = C.c_double
+            L.orc_plan.argtypes = [C.POINTER(Scene), C.POINTER(Tree), C.c_uint64, C.c_int64,
+                                   C.c_int64, C.c_double, C.c_double, C.c_double, C.c_int, ip, dp,
+                                   C.POINTER(C.c_int32)]
+            L.orc_plan.restype = C.c_int64
             _lib = L
     return _lib
 
@@ -203,3 +214,50 @@ def verify_candidate(scene: OracleScene, tree: OracleTree, x, y, parent, full_re
     if ok < 0:
         raise RuntimeError("orc_verify_candidate failed")
     return bool(ok), yaw.value
+
+
+def check_finish(scene: OracleScene, tree: OracleTree, node: int, goal, goal_yaw,
+                 full_reverify=False):
+    """RRT::check_finish (rrt.rs:428-438) for tree node `node`: None, or a dict with the finalized
+    line (rrt.rs:503-540), its euclidean_length and optimize's chosen ancestors per level."""
+    L = lib()
+    gx, gy = goal
+    n, ln, nch = C.c_int(0), C.c_double(0), C.c_int(0)
+    chain = np.full(16, -1, dtype=np.int32)
+    ip = C.POINTER(C.c_int)
+    r = L.orc_check_finish(C.byref(scene._c), C.byref(tree._c), node, gx, gy, goal_yaw,
+                           int(full_reverify), None, None, 0, C.byref(n), C.byref(ln),
+                           chain.ctypes.data_as(ip), C.byref(nch))
+    if r < 0:
+        raise RuntimeError(f"orc_check_finish failed ({r})")
+    out = {"ok": bool(r), "n": n.value, "length": ln.value, "chain": chain[:nch.value].tolist()}
+    if r == 1:
+        cap = max(n.value, 1)
+        x, y = np.zeros(cap), np.zeros(cap)
+        r2 = L.orc_check_finish(C.byref(scene._c), C.byref(tree._c), node, gx, gy, goal_yaw,
+                                int(full_reverify), _dp(x), _dp(y), cap, C.byref(n), C.byref(ln),
+                                None, None)
+        assert r2 == 1
+        out["x"], out["y"] = x[:n.value], y[:n.value]
+    return out
+
+
+def line_length(xs, ys):
+    xs = np.ascontiguousarray(xs, dtype=np.float64)
+    ys = np.ascontiguousarray(ys, dtype=np.float64)
+    return lib().orc_line_length(_dp(xs), _dp(ys), len(xs))
+
+
+def plan(scene: OracleScene, tree: OracleTree, seed: int, it0: int, n_iter: int, goal, goal_yaw,
+         full_reverify=False):
+    """RRT::plan (rrt.rs:599-619), sequential spec: extend + check_finish on every accepted node.
+    Returns (accepted, best_node (-1: no finish), best_length, finish log per iteration
+    (-1 not accepted, 0 None, 1 Some))."""
+    bn, bl = C.c_int(-1), C.c_double(0)
+    log = np.zeros(n_iter, dtype=np.int32)
+    acc = lib().orc_plan(C.byref(scene._c), C.byref(tree._c), seed, it0, n_iter, goal[0], goal[1],
+                         goal_yaw, int(full_reverify), C.byref(bn), C.byref(bl),
+                         log.ctypes.data_as(C.POINTER(C.c_int32)))
+    if acc < 0:
+        raise RuntimeError(f"orc_plan failed ({acc})")
+    return acc, bn.value, bl.value, log

@@ -520,3 +520,182 @@ int orc_verify_candidate(const orc_scene* sc, const orc_tree* tr, double x, doub
     free(s.px); free(s.py); free(s.pyaw);
     return ok;
 }
+
+/* ---------------------------------------- check_finish / optimize / finalize / plan (§8f) */
+/* Node pool: ids [0, tr->n) are tree nodes, ids >= tr->n are the nodes optimize and
+ * check_finish create (Node::new / Node::new_goal, rrt.rs:169-187), never inserted in the tree. */
+typedef struct { double x, y, yaw; int parent; } orc_pnode;
+typedef struct {
+    const orc_scene* sc;
+    const orc_tree* tr;
+    int full_reverify;
+    orc_pnode* v;
+    int n, cap;
+    pbuf b;
+    dscratch s;
+    int* chain;     /* optimize's chosen `to` per level (diagnostics) */
+    int n_chain;
+} orc_cf;
+
+static double P_x(const orc_cf* C, int i) { return i < C->tr->n ? C->tr->x[i] : C->v[i - C->tr->n].x; }
+static double P_y(const orc_cf* C, int i) { return i < C->tr->n ? C->tr->y[i] : C->v[i - C->tr->n].y; }
+static double P_yaw(const orc_cf* C, int i) { return i < C->tr->n ? C->tr->yaw[i] : C->v[i - C->tr->n].yaw; }
+static int P_par(const orc_cf* C, int i) { return i < C->tr->n ? C->tr->parent[i] : C->v[i - C->tr->n].parent; }
+
+static int pool_new(orc_cf* C, double x, double y, double yaw, int parent) {
+    if (C->n == C->cap) {
+        int nc = C->cap ? 2 * C->cap : 64;
+        orc_pnode* nv = (orc_pnode*)realloc(C->v, sizeof(orc_pnode) * nc);
+        if (!nv) return -1;
+        C->v = nv;
+        C->cap = nc;
+    }
+    C->v[C->n] = (orc_pnode){x, y, yaw, parent};
+    return C->tr->n + C->n++;
+}
+
+enum { ORC_NONE = -1, ORC_FAIL = -2, ORC_PANIC = -3 };
+
+/* RRT::optimize, rrt.rs:463-487.  `node` is always a tree node here (optimize_from_goal passes the
+ * goal's parent; the recursion passes ancestors from NodeIter).  The candidate line is
+ * line_to_origin(Node::new(node, to)) (rrt.rs:476-477) — verified in full or as edge ++ [to]
+ * (`to` is a tree node whose own line passed verify at its insert). */
+static int optimize(orc_cf* C, int node, int i) {
+    if (i >= 16) return ORC_NONE; /* RECURSION_LIMIT, rrt.rs:14 */
+    int len = 0;
+    for (int c = node; c >= 0; c = C->tr->parent[c]) len++;
+    int* nodes = (int*)malloc(sizeof(int) * (size_t)len);
+    if (!nodes) return ORC_FAIL;
+    len = 0;
+    for (int c = node; c >= 0; c = C->tr->parent[c]) nodes[len++] = c;
+    int res = ORC_NONE;
+    const double nx = C->tr->x[node], ny = C->tr->y[node];
+    for (int k = len - 1; k >= 0; --k) { /* nodes_vec.into_iter().rev(): root first */
+        const int to = nodes[k];
+        const double yaw = compute_yaw(nx, ny, C->tr->x[to], C->tr->y[to]);
+        int ok = verify_candidate(C->sc, C->tr, nx, ny, yaw, to, C->full_reverify, &C->b, &C->s);
+        if (ok < 0) { res = ORC_FAIL; break; }
+        if (!ok) continue;
+        if (C->chain) C->chain[i] = to;
+        if (C->n_chain < i + 1) C->n_chain = i + 1;
+        int r = optimize(C, to, i + 1);
+        if (r == ORC_FAIL) { res = ORC_FAIL; break; }
+        if (r >= 0) /* Node::new(node, to') — yaw toward to' (at to's coordinates) */
+            res = pool_new(C, nx, ny, compute_yaw(nx, ny, P_x(C, r), P_y(C, r)), r);
+        else
+            res = pool_new(C, nx, ny, yaw, to);
+        if (res < 0) res = ORC_FAIL;
+        break;
+    }
+    free(nodes);
+    return res;
+}
+
+/* RRT::finalize, rrt.rs:503-540: NodeIter from the (optimised) goal, each node with a parent
+ * contributes its Dubins points node→parent (None panics, rrt.rs:529), the root nothing; the
+ * concatenation is reversed.  Writes into C->b. */
+static int finalize_line(orc_cf* C, int goal) {
+    pbuf tmp = {0};
+    const double R = C->sc->turn_radius, step = C->sc->step_size;
+    int rc = 0;
+    for (int cur = goal; cur >= 0; cur = P_par(C, cur)) {
+        const int par = P_par(C, cur);
+        if (par < 0) break;
+        double conf[8] = {P_x(C, cur), P_y(C, cur), P_yaw(C, cur), P_x(C, par), P_y(C, par),
+                          P_yaw(C, par), R, step};
+        int need = orc_dubins_n_point(conf);
+        if (need <= 0) { rc = ORC_PANIC; break; }
+        if (dscratch_fit(&C->s, need)) { rc = ORC_FAIL; break; }
+        int n = 0, word = -1;
+        double cost = 0;
+        int r = orc_dubins(conf, C->s.px, C->s.py, C->s.pyaw, C->s.cap, &n, &word, &cost);
+        if (r < 0) { rc = ORC_FAIL; break; }
+        if (r == 0) { rc = ORC_PANIC; break; }
+        for (int i = 0; i < n; ++i)
+            if (pbuf_push(&tmp, C->s.px[i], C->s.py[i])) { rc = ORC_FAIL; break; }
+        if (rc) break;
+    }
+    C->b.n = 0;
+    if (!rc)
+        for (int i = tmp.n - 1; i >= 0; --i) /* l.reverse(), rrt.rs:538 */
+            if (pbuf_push(&C->b, tmp.x[i], tmp.y[i])) { rc = ORC_FAIL; break; }
+    free(tmp.x);
+    free(tmp.y);
+    return rc;
+}
+
+/* geo 0.12 EuclideanLength for LineString: sum over consecutive points of hypot(dx, dy), in
+ * line order (third-party arithmetic: parity unpinned). */
+double orc_line_length(const double* x, const double* y, int n) {
+    double s = 0.0;
+    for (int i = 0; i + 1 < n; ++i) s += hypot(x[i + 1] - x[i], y[i + 1] - y[i]);
+    return s;
+}
+
+/* RRT::check_finish, rrt.rs:428-438, for tree node `node`.  Returns 1 (Some: the line in
+ * out_x/out_y, *n_out points, *len_out its euclidean_length), 0 (None), -1 (allocation or
+ * capacity failure), -3 (finalize would panic).  chain_out (optional, 16 entries) receives
+ * optimize's chosen `to` for each successful level, *n_chain their count. */
+int orc_check_finish(const orc_scene* sc, const orc_tree* tr, int node, double gx, double gy,
+                     double gyaw, int full_reverify, double* out_x, double* out_y, int cap,
+                     int* n_out, double* len_out, int* chain_out, int* n_chain) {
+    orc_cf C = {0};
+    C.sc = sc;
+    C.tr = tr;
+    C.full_reverify = full_reverify;
+    C.chain = chain_out;
+    int rc;
+    /* optimize_from_goal, rrt.rs:489-501 */
+    int goal;
+    int opt = optimize(&C, node, 0);
+    if (opt == ORC_FAIL) { rc = -1; goto done; }
+    goal = pool_new(&C, gx, gy, gyaw, opt >= 0 ? opt : node);
+    if (goal < 0) { rc = -1; goto done; }
+    rc = finalize_line(&C, goal);
+    if (rc == ORC_FAIL) { rc = -1; goto done; }
+    if (rc == ORC_PANIC) { rc = -3; goto done; }
+    rc = orc_verify_line(sc, C.b.x, C.b.y, C.b.n) ? 1 : 0;
+    if (n_out) *n_out = C.b.n;
+    if (len_out) *len_out = orc_line_length(C.b.x, C.b.y, C.b.n);
+    if (out_x && out_y) {
+        if (C.b.n > cap) { rc = -1; goto done; }
+        memcpy(out_x, C.b.x, sizeof(double) * (size_t)C.b.n);
+        memcpy(out_y, C.b.y, sizeof(double) * (size_t)C.b.n);
+    }
+done:
+    if (n_chain) *n_chain = C.n_chain;
+    free(C.v);
+    free(C.b.x); free(C.b.y);
+    free(C.s.px); free(C.s.py); free(C.s.pyaw);
+    return rc;
+}
+
+/* RRT::plan, rrt.rs:599-619, sequential spec: iterations [it0, it0+n_iter) of
+ * plan_one (extend + check_finish on every accepted node); the answer is the first finish with
+ * the minimum euclidean_length.  *best_node = -1 when no finish verified.  Returns accepted
+ * nodes, or -1 / -3 like orc_check_finish. */
+int64_t orc_plan(const orc_scene* sc, orc_tree* tr, uint64_t seed, int64_t it0, int64_t n_iter,
+                 double gx, double gy, double gyaw, int full_reverify, int* best_node,
+                 double* best_len, int32_t* finish_ok) {
+    int64_t acc = 0;
+    *best_node = -1;
+    *best_len = INFINITY;
+    for (int64_t k = 0; k < n_iter; ++k) {
+        int n0 = tr->n;
+        int64_t a = orc_rrt_extend(sc, tr, seed, it0 + k, 1, full_reverify, NULL, NULL);
+        if (a < 0) return -1;
+        if (finish_ok) finish_ok[k] = -1;
+        if (a == 0) continue;
+        acc += a;
+        double len = 0;
+        int r = orc_check_finish(sc, tr, n0, gx, gy, gyaw, full_reverify, NULL, NULL, 0, NULL, &len,
+                                 NULL, NULL);
+        if (r < 0) return r;
+        if (finish_ok) finish_ok[k] = r;
+        if (r == 1 && len < *best_len) { /* min_by keeps the first of equal minima */
+            *best_len = len;
+            *best_node = n0;
+        }
+    }
+    return acc;
+}

@@ -137,6 +137,9 @@ struct pp_ctx {
     DBuf<double> task_yaw;
     DBuf<double> api_lit_scratch;
     HBuf<SteerTask> h_tasks;
+    // check_finish
+    DBuf<int> cf_nodes, cf_ok, cf_npts, cf_chain, cf_etab, cf_err;
+    DBuf<double> cf_len, cf_pts;
 
     // ---- profiling
     bool prof = false;
@@ -303,6 +306,35 @@ int ensure_events(pp_ctx* c, size_t count) {
         PP_HIP(hipEventCreate(&e));
         c->ev.push_back(e);
     }
+    return PP_OK;
+}
+
+static_assert(PP_CF_CHAIN == kCfLevels + 2, "chain row layout");
+constexpr int kCfBatch = 16384;     // nodes per check_finish launch
+constexpr int kCfPtsCap = 1 << 16;  // line points per check_finish workgroup
+
+// check_finish for nodes[0, k) (device pointer already filled); results on the device
+int cf_launch(pp_ctx* c, int k, int want_line, int grid) {
+    PP_HIP(c->cf_ok.reserve(kCfBatch));
+    PP_HIP(c->cf_len.reserve(kCfBatch));
+    PP_HIP(c->cf_npts.reserve(kCfBatch));
+    PP_HIP(c->cf_chain.reserve((size_t)kCfBatch * (kCfLevels + 2)));
+    PP_HIP(c->cf_err.reserve(1));
+    PP_HIP(c->cf_pts.reserve((size_t)kCfGrid * 3 * kCfPtsCap));
+    PP_HIP(c->cf_etab.reserve((size_t)kCfGrid * 2 * kCfMaxEdges));
+    PP_HIP(c->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
+    PP_HIP(hipMemsetAsync(c->cf_err.p, 0, sizeof(int), c->stream));
+    PP_HIP(launch_check_finish(c->stream, c->scene_dev(), c->tree_dev(), c->cf_nodes.p, k,
+                               c->goal[0], c->goal[1], c->goal[2], want_line, c->cf_ok.p,
+                               c->cf_len.p, c->cf_npts.p, c->cf_chain.p, c->api_lit_scratch.p,
+                               c->cf_pts.p, kCfPtsCap, c->cf_etab.p, c->cf_err.p, grid));
+    int err = 0;
+    PP_HIP(hipMemcpyAsync(&err, c->cf_err.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    PP_HIP(hipStreamSynchronize(c->stream));
+    if (err & 2) return set_err(PP_ERR_REFERENCE_PANIC, "finalize: a Dubins edge has no feasible word (rrt.rs:529 panics)");
+    if (err & 4) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
+    if (err & 1) return set_err(PP_ERR_CAPACITY, "tree deeper than the check_finish path capacity");
+    if (err & 8) return set_err(PP_ERR_CAPACITY, "finalized line longer than the point capacity");
     return PP_OK;
 }
 
@@ -749,6 +781,105 @@ int pp_rrt_verify_node_batch(pp_ctx* ctx, const double* x, const double* y,
             }
         }
     }
+    return PP_OK;
+}
+
+int pp_rrt_check_finish_batch(pp_ctx* ctx, const int32_t* nodes, int k, uint8_t* ok,
+                              double* length, int32_t* n_points, int32_t* chain) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (k < 0 || (k > 0 && (!nodes || !ok))) return set_err(PP_ERR_INVALID_ARGUMENT, "bad arguments");
+    for (int i = 0; i < k; ++i)
+        if (nodes[i] < 0 || nodes[i] >= ctx->n)
+            return set_err(PP_ERR_INVALID_ARGUMENT, "node index outside the tree");
+    const int want_line = (length || n_points) ? 1 : 0;
+    std::vector<int> okv, npv;
+    PP_HIP(ctx->cf_nodes.reserve(kCfBatch));
+    for (int b = 0; b < k; b += kCfBatch) {
+        const int nb = std::min(kCfBatch, k - b);
+        PP_HIP(hipMemcpyAsync(ctx->cf_nodes.p, nodes + b, nb * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+        if ((r = cf_launch(ctx, nb, want_line, kCfGrid))) return r;
+        okv.resize(nb);
+        PP_HIP(hipMemcpy(okv.data(), ctx->cf_ok.p, nb * sizeof(int), hipMemcpyDeviceToHost));
+        for (int i = 0; i < nb; ++i) ok[b + i] = (uint8_t)okv[i];
+        if (length) PP_HIP(hipMemcpy(length + b, ctx->cf_len.p, nb * sizeof(double), hipMemcpyDeviceToHost));
+        if (n_points) PP_HIP(hipMemcpy(n_points + b, ctx->cf_npts.p, nb * sizeof(int), hipMemcpyDeviceToHost));
+        if (chain)
+            PP_HIP(hipMemcpy(chain + (size_t)b * (kCfLevels + 2), ctx->cf_chain.p,
+                             (size_t)nb * (kCfLevels + 2) * sizeof(int), hipMemcpyDeviceToHost));
+    }
+    return PP_OK;
+}
+
+int pp_rrt_check_finish(pp_ctx* ctx, int32_t node, uint8_t* ok, double* x, double* y,
+                        int64_t cap, int64_t* n, double* length) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (!ok || node < 0 || node >= ctx->n) return set_err(PP_ERR_INVALID_ARGUMENT, "bad arguments");
+    PP_HIP(ctx->cf_nodes.reserve(kCfBatch));
+    PP_HIP(hipMemcpyAsync(ctx->cf_nodes.p, &node, sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+    if ((r = cf_launch(ctx, 1, 1, 1))) return r;
+    int okv = 0, np = 0, row[kCfLevels + 2];
+    double len = 0.0;
+    PP_HIP(hipMemcpy(&okv, ctx->cf_ok.p, sizeof(int), hipMemcpyDeviceToHost));
+    PP_HIP(hipMemcpy(&np, ctx->cf_npts.p, sizeof(int), hipMemcpyDeviceToHost));
+    PP_HIP(hipMemcpy(&len, ctx->cf_len.p, sizeof(double), hipMemcpyDeviceToHost));
+    PP_HIP(hipMemcpy(row, ctx->cf_chain.p, sizeof(row), hipMemcpyDeviceToHost));
+    *ok = (uint8_t)okv;
+    if (length) *length = len;
+    if (n) *n = okv ? np : 0;
+    if (!okv || !(x && y)) return PP_OK;
+    if (cap < np) return set_err(PP_ERR_CAPACITY, "line buffer smaller than the finalized line");
+    const int E = row[1];
+    std::vector<int> et(2 * (size_t)E);
+    std::vector<double> hx(kCfPtsCap), hy(kCfPtsCap);
+    PP_HIP(hipMemcpy(et.data(), ctx->cf_etab.p, et.size() * sizeof(int), hipMemcpyDeviceToHost));
+    PP_HIP(hipMemcpy(hx.data(), ctx->cf_pts.p, kCfPtsCap * sizeof(double), hipMemcpyDeviceToHost));
+    PP_HIP(hipMemcpy(hy.data(), ctx->cf_pts.p + kCfPtsCap, kCfPtsCap * sizeof(double), hipMemcpyDeviceToHost));
+    int64_t w = 0;  // l.reverse() (rrt.rs:538)
+    for (int e = E - 1; e >= 0; --e)
+        for (int i = et[2 * e + 1] - 1; i >= 0; --i) {
+            x[w] = hx[et[2 * e] + i];
+            y[w] = hy[et[2 * e] + i];
+            ++w;
+        }
+    if (n) *n = w;
+    return PP_OK;
+}
+
+int pp_rrt_plan(pp_ctx* ctx, int64_t n_iter, int32_t* best_node, double* best_length,
+                int64_t* n_finishes) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (n_iter < 0 || !best_node) return set_err(PP_ERR_INVALID_ARGUMENT, "bad arguments");
+    const int64_t n0 = ctx->n;
+    int64_t acc = 0;
+    if ((r = pp_rrt_extend(ctx, n_iter, &acc))) return r;
+    const int64_t n1 = ctx->n;
+    std::vector<int32_t> nodes;
+    nodes.reserve((size_t)(n1 - n0));
+    for (int64_t i = n0; i < n1; ++i) nodes.push_back((int32_t)i);
+    std::vector<uint8_t> okv(nodes.size());
+    std::vector<double> lens(nodes.size());
+    if (!nodes.empty() &&
+        (r = pp_rrt_check_finish_batch(ctx, nodes.data(), (int)nodes.size(), okv.data(),
+                                       lens.data(), nullptr, nullptr)))
+        return r;
+    // min_by(euclidean_length) over the finishes in iteration order: the first minimum wins
+    int32_t bn = -1;
+    double bl = __builtin_inf();
+    int64_t nf = 0;
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        if (!okv[i]) continue;
+        ++nf;
+        if (lens[i] < bl) {
+            bl = lens[i];
+            bn = nodes[i];
+        }
+    }
+    *best_node = bn;
+    if (best_length) *best_length = bl;
+    if (n_finishes) *n_finishes = nf;
     return PP_OK;
 }
 

@@ -49,6 +49,17 @@ hipError_t launch_steer_tasks(hipStream_t st, const SceneDev& sc, const TreeDev&
                               const SteerTask* tasks, int n, int* out_status, double* out_yaw,
                               double* scratch);
 
+// RRT::check_finish for k tree nodes (one workgroup per node, `grid` workgroups).  ok/len/npts
+// per node; chain (optional) = k rows of [levels, edges, optimize's chosen ancestors...] with
+// kCfLevels + 2 ints per row; want_line: materialise verified lines (length, points of the last
+// node each workgroup handled in pts/etab).  err |= 1 depth > kCfMaxDepth, 2 finalize panic,
+// 4 steer overflow, 8 point capacity.
+hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev& tr,
+                               const int* nodes, int k, double gx, double gy, double gyaw,
+                               int want_line, int* ok, double* len, int* npts, int* chain,
+                               double* lit_scratch, double* pts, int pts_cap, int* etab, int* err,
+                               int grid);
+
 hipError_t launch_dubins_batch(hipStream_t st, const double* conf, int n, int cap, double* px,
                                double* py, double* pyaw, int* n_out, int* word_out,
                                double* cost_out, int* status_out);

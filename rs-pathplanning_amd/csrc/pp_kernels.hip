@@ -221,7 +221,7 @@ __device__ __forceinline__ WalkIn walk_in(const SteerPrep& p) { return walk_in(&
 
 template <bool kLds>
 __device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
-                                          int64_t* ph = nullptr) {
+                                          int64_t* ph = nullptr, bool junction = true) {
     const int lane = threadIdx.x & 63;
     if (r.state == kPrepNone) {  // polyline [(x, y), (px, py)]
         const bool has = lane < 2;
@@ -264,7 +264,8 @@ __device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
             }
         }
         grid += cnt;
-        const bool junction_here = (seg >= 3) && cnt < 63;
+        const bool end_here = (seg >= 3) && cnt < 63;
+        const bool junction_here = end_here && junction;
         double qx = carry_x, qy = carry_y;
         bool has = (lane == 0), isgrid = false, isjunction = false;
         if (lane >= 1 && lane <= cnt) {
@@ -302,7 +303,7 @@ __device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
         }
 #endif
         if (rej) return kReject;
-        if (junction_here) break;
+        if (end_here) break;
         carry_x = __shfl(qx, cnt);
         carry_y = __shfl(qy, cnt);
         first = false;
@@ -312,17 +313,20 @@ __device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
 }
 
 // Both halves on one wave (uniform prep): the repair and verify_node paths.
+// junction = false: the polyline ends at the edge's last point (finalize's edge into the root,
+// rrt.rs:532, contributes no root point).
 template <bool kLds>
 __device__ int steer_collide_fast(const SceneDev& sc, double x, double y, double yaw, double px,
-                                  double py, double pyaw) {
+                                  double py, double pyaw, bool junction = true) {
     const SteerPrep r = steer_prep(sc, x, y, yaw, px, py, pyaw);
-    return steer_walk<kLds>(sc, walk_in(r));
+    return steer_walk<kLds>(sc, walk_in(r), nullptr, junction);
 }
 
 // Literal path (measure-zero trim cases): lane 0 runs dubins_literal into its scratch buffer and
 // verifies the polyline alone.  Slow, exact, essentially never taken.
 __device__ int steer_collide_literal(const SceneDev& sc, double x, double y, double yaw, double px,
-                                     double py, double pyaw, double* bx, double* by, double* byaw) {
+                                     double py, double pyaw, double* bx, double* by, double* byaw,
+                                     bool junction = true) {
     const int lane = threadIdx.x & 63;
     int st = kReject;
     if (lane == 0) {
@@ -339,11 +343,11 @@ __device__ int steer_collide_literal(const SceneDev& sc, double x, double y, dou
                 n = 1;
             }
             bool ok = true;
-            for (int i = 0; i < n && ok; ++i)
-                ok = bx[i] >= sc.minx && bx[i] <= sc.maxx && by[i] >= sc.miny && by[i] <= sc.maxy;
             bx[n] = px;
             by[n] = py;
-            const int np = n + 1;
+            const int np = junction ? n + 1 : n;  // the junction point is bounds-checked too
+            for (int i = 0; i < np && ok; ++i)
+                ok = bx[i] >= sc.minx && bx[i] <= sc.maxx && by[i] >= sc.miny && by[i] <= sc.maxy;
             double x0 = bx[0], x1 = bx[0], y0 = by[0], y1 = by[0];
             for (int i = 1; i < np; ++i) {
                 x0 = fmin(x0, bx[i]);
@@ -492,13 +496,12 @@ __device__ inline Top2 merge_top2(Top2 a, Top2 c) {
 // blocks (nqb sample blocks x 64 node chunks), mapped XCD-aware so the nqb blocks that stream the
 // same node chunk share one XCD's L2.  Each wave scans a quarter of the chunk with node
 // coordinates as wave-uniform scalar loads (double-buffered one block ahead); every lane holds 4
-// samples as two packed pairs, so a node costs 2 packed VALU ops per sample for the distance
-// (v_pk_add / v_pk_mul / v_pk_fma on f32x2).  Per block of kScanBlk nodes each sample keeps only
-// the block minimum (v_min3), then merges it into (best, second) with med3 and records the block
+// samples.  Per block of kScanBlk nodes each sample keeps only the block minimum (v_min3: half an
+// op per eval on top of sub, sub, mul, fma), then merges it into (best, second) with med3 and
+// records the block
 // that first attained the best.  The winning block is re-evaluated afterwards with the same
 // arithmetic (bit-identical distances) for the lowest index and the in-block second best, so the
 // result is the exact per-chunk top-2 of the f32 distances, as before.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int kScanBlk = 16;
 
 __device__ __forceinline__ float scan_d2(float qx, float qy, float nx, float ny) {
@@ -514,7 +517,6 @@ __global__ __launch_bounds__(256) void nn_scan_kernel(const DevState* __restrict
                                                       int stride, float* __restrict__ pbest,
                                                       float* __restrict__ psecond,
                                                       int* __restrict__ pidx) {
-    static_assert(kQPL == 4, "two packed sample pairs per lane");
     __shared__ float s_b[4][kQPB];
     __shared__ float s_s[4][kQPB];
     __shared__ int s_i[4][kQPB];
@@ -541,8 +543,6 @@ __global__ __launch_bounds__(256) void nn_scan_kernel(const DevState* __restrict
         blk[r] = -1;
         bi[r] = -1;
     }
-    const f32x2 qxa = {qxr[0], qxr[1]}, qya = {qyr[0], qyr[1]};
-    const f32x2 qxb = {qxr[2], qxr[3]}, qyb = {qyr[2], qyr[3]};
     // wave-uniform range (kScanBlk-aligned start): readfirstlane lets the compiler use scalar loads
     const int per = (((c1 - c0) + 3) / 4 + kScanBlk - 1) & ~(kScanBlk - 1);
     const int w0 = __builtin_amdgcn_readfirstlane(min(c0 + wave * per, c1));
@@ -571,21 +571,10 @@ __global__ __launch_bounds__(256) void nn_scan_kernel(const DevState* __restrict
             float bm[kQPL];
 #pragma unroll
             for (int u = 0; u < kScanBlk; ++u) {
-                const f32x2 sx = {px[u], px[u]}, sy = {py[u], py[u]};
-                const f32x2 dxa = qxa - sx, dya = qya - sy;
-                const f32x2 dxb = qxb - sx, dyb = qyb - sy;
-                const f32x2 da = __builtin_elementwise_fma(dya, dya, dxa * dxa);
-                const f32x2 db = __builtin_elementwise_fma(dyb, dyb, dxb * dxb);
-                if (u == 0) {
-                    bm[0] = da.x;
-                    bm[1] = da.y;
-                    bm[2] = db.x;
-                    bm[3] = db.y;
-                } else {
-                    bm[0] = __builtin_fminf(bm[0], da.x);
-                    bm[1] = __builtin_fminf(bm[1], da.y);
-                    bm[2] = __builtin_fminf(bm[2], db.x);
-                    bm[3] = __builtin_fminf(bm[3], db.y);
+#pragma unroll
+                for (int r = 0; r < kQPL; ++r) {
+                    const float d = scan_d2(qxr[r], qyr[r], px[u], py[u]);
+                    bm[r] = u == 0 ? d : __builtin_fminf(bm[r], d);
                 }
             }
 #pragma unroll
@@ -1570,6 +1559,278 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
         st->nn_flagged += st->flag_count;
         st->node_evals += (int64_t)W * n0;
     }
+}
+
+// ---------------------------------------------------------------- check_finish
+//
+// RRT::check_finish (rrt.rs:428-438) for a batch of tree nodes, one workgroup per node
+// (persistent over the batch), the node's ancestor path root..node staged in LDS:
+//   optimize (rrt.rs:463-487)   level i: candidates path[0..L] root first, 4 waves steer+collide
+//                               4 candidates at a time, the first accepted one wins; recursion
+//                               = the next level on that ancestor; RECURSION_LIMIT 16.  Every
+//                               candidate parent is a tree node, so verifying edge ++ [to] is
+//                               verify(line_to_origin(new)).
+//   finalize (rrt.rs:503-540)   the chain goal → optimised copies → tree path → root; every edge
+//                               is verified with its junction chord, the edge into the root
+//                               without one (the root contributes no point); a None steer is the
+//                               reference's panic (rrt.rs:529).
+//   length                      verified finishes: the edges' literal Dubins points, then
+//                               euclidean_length of the reversed line summed in line order.
+struct CfPose {
+    double x, y, yaw;
+};
+
+// pose j of the finalize chain: 0 = goal, 1..s = optimised copies, then path[ps], ..., path[0]
+__device__ inline CfPose cf_pose(int j, int s, int ps, int D, const int* s_path, const int* s_pos,
+                                 const TreeDev& tr, double gx, double gy, double gyaw) {
+    if (j == 0) return CfPose{gx, gy, gyaw};
+    if (j <= s) {
+        const int i = j - 1;
+        const int here = s_path[i == 0 ? D - 1 : s_pos[i - 1]];
+        const int to = s_path[s_pos[i]];
+        const double x = tr.x[here], y = tr.y[here];
+        return CfPose{x, y, atan2(tr.y[to] - y, tr.x[to] - x)};  // Node::new (compute_yaw)
+    }
+    const int node = s_path[ps - (j - s - 1)];
+    return CfPose{tr.x[node], tr.y[node], tr.yaw[node]};
+}
+
+// verify one edge a → b (+ junction chord to b unless junction is false) on one wave; kCfPanic
+// when the steer is None (finalize's panic; verify_node's callers never pass such an edge here).
+enum : int { kCfPanic = 6 };
+template <bool kAllowNone>
+__device__ __attribute__((noinline)) int cf_edge_check(const SceneDev& sc, CfPose a, CfPose b,
+                                                       bool junction, double* bx) {
+    const SteerPrep r = steer_prep(sc, a.x, a.y, a.yaw, b.x, b.y, b.yaw);
+    if (!kAllowNone && r.state == kPrepNone) return kCfPanic;
+    int st = steer_walk<false>(sc, walk_in(r), nullptr, junction);
+    if (st == kLiteral)
+        st = steer_collide_literal(sc, a.x, a.y, a.yaw, b.x, b.y, b.yaw, bx, bx + kLiteralCap,
+                                   bx + 2 * kLiteralCap, junction);
+    return st;
+}
+
+// n_point of dubins_path_planning(a → b) (dubins.rs:369), 0 when the steer is None
+__device__ inline int cf_npoint(const SceneDev& sc, CfPose a, CfPose b) {
+    const double ex = b.x - a.x, ey = b.y - a.y;
+    const double c = 1.0 / sc.turn_radius;
+    const double lex = cos(a.yaw) * ex + sin(a.yaw) * ey;
+    const double ley = -(sin(a.yaw)) * ex + cos(a.yaw) * ey;
+    const Steer st = select_word(lex, ley, b.yaw - a.yaw, c);
+    if (st.word < 0) return 0;
+    double tot = 0.0;
+    tot += st.t;
+    tot += st.p;
+    tot += st.q;
+    const double nq = trunc(tot / sc.step_size);
+    if (!(nq >= 0.0) || nq > 1.0e8) return -1;
+    return (int)nq + 7;
+}
+
+__global__ __launch_bounds__(256) void check_finish_kernel(
+    SceneDev sc, TreeDev tr, const int* __restrict__ nodes, int k, double gx, double gy,
+    double gyaw, int want_line, int* __restrict__ ok_out, double* __restrict__ len_out,
+    int* __restrict__ npts_out, int* __restrict__ chain_out, double* __restrict__ lit_scratch,
+    double* __restrict__ pts, int pts_cap, int* __restrict__ etab, int* __restrict__ err) {
+    __shared__ int s_path[kCfMaxDepth];
+    __shared__ int s_pos[kCfLevels];
+    __shared__ int s_st[4];
+    __shared__ int s_D, s_bad;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double* bx = lit_scratch + (size_t)(blockIdx.x * 4 + wave) * 3 * kLiteralCap;
+    double* px = pts + (size_t)blockIdx.x * 3 * pts_cap;
+    double* py = px + pts_cap;
+    double* pyw = py + pts_cap;
+    int* et = etab + (size_t)blockIdx.x * 2 * kCfMaxEdges;
+    for (int b = blockIdx.x; b < k; b += gridDim.x) {
+        // ancestor path, node first (NodeIter, rrt.rs:253-265), then reversed: root first
+        if (tid == 0) {
+            int d = 0, c = nodes[b];
+            while (c >= 0 && d < kCfMaxDepth) {
+                s_path[d++] = c;
+                c = tr.parent[c];
+            }
+            s_D = c >= 0 ? -1 : d;
+            s_bad = 0;
+        }
+        __syncthreads();
+        const int D = s_D;
+        if (D < 0) {
+            if (tid == 0) {
+                ok_out[b] = 0;
+                atomicOr(err, 1);
+            }
+            __syncthreads();
+            continue;
+        }
+        for (int i = tid; i < D / 2; i += 256) {
+            const int t = s_path[i];
+            s_path[i] = s_path[D - 1 - i];
+            s_path[D - 1 - i] = t;
+        }
+        __syncthreads();
+        // optimize, level by level
+        int L = D - 1, s_lv = 0;
+        for (int level = 0; level < kCfLevels; ++level) {
+            const int c = s_path[L];
+            const CfPose a0{tr.x[c], tr.y[c], 0.0};
+            int found = -1;
+            for (int base = 0; base <= L; base += 4) {
+                const int m = base + wave;
+                int st = kReject;
+                if (m <= L) {
+                    const int to = s_path[m];
+                    const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
+                    const CfPose a{a0.x, a0.y, atan2(bt.y - a0.y, bt.x - a0.x)};
+                    st = cf_edge_check<true>(sc, a, bt, true, bx);
+                }
+                if (lane == 0) s_st[wave] = st;
+                __syncthreads();
+                for (int w = 0; w < 4 && found == -1; ++w) {
+                    const int sw = s_st[w];
+                    if (base + w > L || sw == kReject) continue;
+                    if (sw == kAccept)
+                        found = base + w;
+                    else
+                        found = -2;  // kError before any accept: the reference would panic
+                }
+                __syncthreads();
+                if (found != -1) break;
+            }
+            if (found == -2) {
+                if (tid == 0) s_bad = 4;
+                break;
+            }
+            if (found < 0) break;
+            if (tid == 0) s_pos[level] = found;
+            L = found;
+            s_lv = level + 1;
+        }
+        __syncthreads();
+        // finalize: verify the chain's edges
+        const int s = s_lv;
+        const int ps = s > 0 ? s_pos[s - 1] : D - 1;
+        const int E = 1 + s + ps;
+        bool vok = s_bad == 0;
+        for (int base = 0; base < E && vok; base += 4) {
+            const int e = base + wave;
+            int st = kAccept;
+            if (e < E) {
+                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                st = cf_edge_check<false>(sc, a, bp, e < E - 1, bx);
+            }
+            if (lane == 0) s_st[wave] = st;
+            __syncthreads();
+            for (int w = 0; w < 4; ++w) {
+                const int sw = s_st[w];
+                if (sw == kCfPanic || sw == kError) {
+                    if (tid == 0) s_bad = sw == kCfPanic ? 2 : 4;
+                    vok = false;
+                } else if (sw != kAccept) {
+                    vok = false;
+                }
+            }
+            __syncthreads();
+        }
+        // a panic anywhere in finalize wins over a rejection (the reference panics first): scan
+        // the remaining edges for None steers
+        if (s_bad == 0 && !vok) {
+            for (int e = tid; e < E; e += 256) {
+                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                if (cf_npoint(sc, a, bp) == 0) atomicOr(&s_bad, 2);
+            }
+            __syncthreads();
+        }
+        const int bad = s_bad;
+        double len = 0.0;
+        int npts = 0;
+        if (vok && bad == 0 && want_line) {
+            // edge capacities, offsets, literal points
+            for (int e = tid; e < E; e += 256) {
+                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                et[2 * e] = cf_npoint(sc, a, bp);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int off = 0;
+                bool neg = false;
+                for (int e = 0; e < E; ++e) {
+                    const int c = et[2 * e];
+                    neg |= c <= 0;
+                    et[2 * e] = off;
+                    off += c > 0 ? c : 0;
+                }
+                s_D = (off <= pts_cap && !neg) ? off : -1;
+            }
+            __syncthreads();
+            if (s_D < 0) {
+                if (tid == 0) s_bad = 8;  // (a None / overflowing edge was rejected above)
+            } else {
+                for (int e = tid; e < E; e += 256) {
+                    const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                    const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                    const int o = et[2 * e];
+                    const int cap = (e + 1 < E ? et[2 * e + 2] : s_D) - o;
+                    int n = 0, word = -1;
+                    double cost = 0.0;
+                    const int r = dubins_literal(a.x, a.y, a.yaw, bp.x, bp.y, bp.yaw,
+                                                 sc.turn_radius, sc.step_size, px + o, py + o,
+                                                 pyw + o, cap, &n, &word, &cost);
+                    et[2 * e + 1] = r == kSteerSome ? n : 0;
+                    if (r != kSteerSome) atomicOr(&s_bad, 2);
+                }
+            }
+            __syncthreads();
+            if (tid == 0 && s_bad == 0) {
+                // l.reverse() (rrt.rs:538), then euclidean_length in that order
+                bool have = false;
+                double qx = 0.0, qy = 0.0;
+                for (int e = E - 1; e >= 0; --e) {
+                    const int o = et[2 * e], n = et[2 * e + 1];
+                    for (int i = n - 1; i >= 0; --i) {
+                        const double x = px[o + i], y = py[o + i];
+                        if (have) len += hypot(x - qx, y - qy);
+                        qx = x;
+                        qy = y;
+                        have = true;
+                    }
+                    npts += n;
+                }
+                s_D = npts;
+            }
+            __syncthreads();
+            npts = s_D;
+        }
+        if (tid == 0) {
+            const int bad2 = s_bad;
+            ok_out[b] = (vok && bad2 == 0) ? 1 : 0;
+            len_out[b] = len;
+            npts_out[b] = npts;
+            if (bad2) atomicOr(err, bad2);
+            if (chain_out) {
+                chain_out[(size_t)b * (kCfLevels + 2)] = s;
+                chain_out[(size_t)b * (kCfLevels + 2) + 1] = E;
+                for (int i = 0; i < s; ++i)
+                    chain_out[(size_t)b * (kCfLevels + 2) + 2 + i] = s_path[s_pos[i]];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev& tr,
+                               const int* nodes, int k, double gx, double gy, double gyaw,
+                               int want_line, int* ok, double* len, int* npts, int* chain,
+                               double* lit_scratch, double* pts, int pts_cap, int* etab, int* err,
+                               int grid) {
+    if (k <= 0) return hipSuccess;
+    check_finish_kernel<<<std::min(grid, k), 256, 0, st>>>(sc, tr, nodes, k, gx, gy, gyaw,
+                                                           want_line, ok, len, npts, chain,
+                                                           lit_scratch, pts, pts_cap, etab, err);
+    return hipGetLastError();
 }
 
 // --------------------------------------------------------------------------- launch wrappers

@@ -26,6 +26,10 @@ constexpr int kMaxWindow = 4096;     // K limit: the resolve keeps the window's 
 constexpr int kSteerPrepBytes = 152; // sizeof(SteerPrep) (checked in pp_kernels.hip)
 constexpr int kPdCap = 256;          // grid points per task stored by steer_prep (more: fallback)
 constexpr int kPrepLanes = 8;        // lanes per task in steer_prep
+constexpr int kCfMaxDepth = 8192;    // check_finish: ancestor path staged in LDS (32 KB)
+constexpr int kCfLevels = 16;        // RECURSION_LIMIT, rrt.rs:14
+constexpr int kCfMaxEdges = kCfLevels + 1 + kCfMaxDepth;
+constexpr int kCfGrid = 64;          // check_finish workgroups (4 literal scratch buffers each)
 
 // Scene in device memory (Space, rrt.rs:70-78, with Q10 analytic discs).
 struct SceneDev {

@@ -19,11 +19,14 @@ PP_ERR_NO_DEVICE = -3
 PP_ERR_CAPACITY = -4
 PP_ERR_STATE = -5
 PP_ERR_STEER_OVERFLOW = -6
+PP_ERR_REFERENCE_PANIC = -7
+PP_CF_CHAIN = 18
 
 _ERR_NAMES = {
     PP_ERR_INVALID_ARGUMENT: "PP_ERR_INVALID_ARGUMENT", PP_ERR_HIP: "PP_ERR_HIP",
     PP_ERR_NO_DEVICE: "PP_ERR_NO_DEVICE", PP_ERR_CAPACITY: "PP_ERR_CAPACITY",
     PP_ERR_STATE: "PP_ERR_STATE", PP_ERR_STEER_OVERFLOW: "PP_ERR_STEER_OVERFLOW",
+    PP_ERR_REFERENCE_PANIC: "PP_ERR_REFERENCE_PANIC",
 }
 
 # every symbol include/pathplanning_amd.h declares (checked by tests/test_capi_symbols.py)
@@ -33,7 +36,8 @@ EXPORTED = [
     "pp_dubins_path_planning_batch", "pp_space_new", "pp_space_get_bounds", "pp_rrt_new",
     "pp_rrt_set_window", "pp_rrt_extend", "pp_rrt_plan_one", "pp_rrt_tree_size",
     "pp_rrt_iteration", "pp_rrt_tree_export", "pp_rrt_get_nearest_node_batch",
-    "pp_rrt_verify_node_batch", "pp_rrt_get_stats", "pp_rrt_reset_stats", "pp_set_profiling",
+    "pp_rrt_verify_node_batch", "pp_rrt_check_finish_batch", "pp_rrt_check_finish",
+    "pp_rrt_plan", "pp_rrt_get_stats", "pp_rrt_reset_stats", "pp_set_profiling",
 ]
 
 
@@ -105,6 +109,11 @@ def lib():
             "pp_rrt_get_nearest_node_batch": ([vp, dp, dp, C.c_int, ip, dp], C.c_int),
             "pp_rrt_verify_node_batch": ([vp, dp, dp, ip, C.c_int, C.POINTER(C.c_uint8), dp],
                                          C.c_int),
+            "pp_rrt_check_finish_batch": ([vp, ip, C.c_int, C.POINTER(C.c_uint8), dp, ip, ip],
+                                          C.c_int),
+            "pp_rrt_check_finish": ([vp, C.c_int32, C.POINTER(C.c_uint8), dp, dp, C.c_int64, i64p,
+                                     dp], C.c_int),
+            "pp_rrt_plan": ([vp, C.c_int64, ip, dp, i64p], C.c_int),
             "pp_rrt_get_stats": ([vp, C.POINTER(StatsC)], C.c_int),
             "pp_rrt_reset_stats": ([vp], C.c_int),
             "pp_set_profiling": ([vp, C.c_int], C.c_int),

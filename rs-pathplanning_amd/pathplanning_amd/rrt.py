@@ -223,6 +223,55 @@ class RRT:  # rrt.rs:325-620
         ok, _ = self.verify_node_batch([x], [y], [parent])
         return bool(ok[0])
 
+    # ---------------------------------------------------------------- goal connection
+    def check_finish_batch(self, nodes, with_length: bool = True):
+        """RRT::check_finish (rrt.rs:428-438) for many tree nodes: dict of arrays ``ok``,
+        ``length`` / ``n_points`` (verified lines only) and ``chain`` (rows of
+        [levels, edges, optimize's chosen ancestor per level...])."""
+        nodes = np.ascontiguousarray(nodes, dtype=np.int32)
+        k = len(nodes)
+        ok = np.zeros(k, dtype=np.uint8)
+        length = np.zeros(k)
+        npts = np.zeros(k, dtype=np.int32)
+        chain = np.zeros((k, _ffi.PP_CF_CHAIN), dtype=np.int32)
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        _ffi.check(_ffi.lib().pp_rrt_check_finish_batch(
+            self.ctx.handle, nodes.ctypes.data_as(ip), k, ok.ctypes.data_as(C.POINTER(C.c_uint8)),
+            length.ctypes.data_as(dp) if with_length else None,
+            npts.ctypes.data_as(ip) if with_length else None, chain.ctypes.data_as(ip)))
+        return {"ok": ok.astype(bool), "length": length, "n_points": npts, "chain": chain}
+
+    def check_finish(self, node: int):
+        """RRT::check_finish for one tree node: the finalized line as an (n, 2) array (root side
+        first, rrt.rs:538), or None when it does not verify."""
+        ok = C.c_uint8(0)
+        n, ln = C.c_int64(0), C.c_double(0)
+        _ffi.check(_ffi.lib().pp_rrt_check_finish(self.ctx.handle, int(node), C.byref(ok), None,
+                                                  None, 0, C.byref(n), C.byref(ln)))
+        if not ok.value:
+            return None
+        cap = n.value
+        x, y = np.zeros(max(cap, 1)), np.zeros(max(cap, 1))
+        dp = C.POINTER(C.c_double)
+        _ffi.check(_ffi.lib().pp_rrt_check_finish(
+            self.ctx.handle, int(node), C.byref(ok), x.ctypes.data_as(dp), y.ctypes.data_as(dp),
+            cap, C.byref(n), C.byref(ln)))
+        return np.stack([x[:n.value], y[:n.value]], axis=1)
+
+    def plan(self, n_iter: int | None = None):
+        """RRT::plan (rrt.rs:599-619), sequential spec: ``n_iter`` (default max_iter) plan_one
+        iterations, check_finish on every accepted node; the line with the minimum
+        euclidean_length (first on ties) or None.  ``self.last_plan`` keeps (node, length,
+        finishes)."""
+        bn, bl, nf = C.c_int32(-1), C.c_double(0), C.c_int64(0)
+        n_iter = self.max_iter if n_iter is None else int(n_iter)
+        _ffi.check(_ffi.lib().pp_rrt_plan(self.ctx.handle, n_iter, C.byref(bn), C.byref(bl),
+                                          C.byref(nf)))
+        self.last_plan = (bn.value, bl.value, nf.value)
+        if bn.value < 0:
+            return None
+        return self.check_finish(bn.value)
+
     # ---------------------------------------------------------------- instrumentation
     def stats(self) -> dict:
         s = _ffi.StatsC()

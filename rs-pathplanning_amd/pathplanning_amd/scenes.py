@@ -62,6 +62,17 @@ def bench6() -> dict:
     }
 
 
+def bench6_open(start_yaw: float = math.pi / 4.0) -> dict:
+    """bench6 with the start moved into open space, (-3, -3, start_yaw): the goal-connection
+    scene.  At bench6's own start (-5, -5, -45 deg) every check_finish fails — optimize's chain
+    of root copies (yaw atan2(0,0) = 0, rrt.rs:463-487) ends in a Dubins loop into the root that
+    leaves the shrunken bounds — so plan() has nothing to return there."""
+    raw = bench6()
+    raw["name"] = "bench6_open"
+    raw["start"] = (-3.0, -3.0, float(start_yaw))
+    return raw
+
+
 def field512(n_obstacles: int = 1024, seed: int = 1234, size: float = 512.0,
              r_lo: float = 2.0, r_hi: float = 8.0, robot_width: float = 1.0,
              turn_radius: float = 4.0, step_size: float = 0.1,

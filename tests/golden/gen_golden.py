@@ -81,6 +81,34 @@ def rrt_record(raw, seed, n_iter):
             "log_acc": [b for _, b in log]}
 
 
+def finish_record(raw, seed, n_iter):
+    """RRT::plan's pieces on the goal-connection scene: the tree, check_finish of every node
+    (rrt.rs:428-540, full line_to_origin verifies) and plan's answer (rrt.rs:599-619)."""
+    from oracle import OracleScene  # noqa: E402  (scene arithmetic only)
+
+    sc = OracleScene.from_raw(raw).as_dict()
+    rec = rrt_record(raw, seed, n_iter)
+    tree = {k: rec[k] for k in ("x", "y", "yaw", "parent")}
+    nodes = P.tree_nodes(tree)
+    index = {id(n): i for i, n in enumerate(nodes)}
+    goal, gyaw = raw["goal"][:2], raw["goal"][2]
+    fin = []
+    best = (-1, math.inf)
+    for i in range(1, len(nodes)):  # in insertion (= iteration) order
+        ok, xs, ys, ln, chain = P.check_finish(sc, nodes[i], goal, gyaw)
+        fin.append({"node": i, "ok": bool(ok), "chain": [index[id(n)] for n in chain],
+                    "n": len(xs), "length": ln if ok else None})
+        if ok and ln < best[1]:
+            best = (i, ln)
+    out = {"scene": raw["name"], "start": list(raw["start"]), "seed": seed, "n_iter": n_iter,
+           "n_nodes": len(nodes), "finish": fin, "best_node": best[0],
+           "best_length": best[1] if best[0] >= 0 else None}
+    if best[0] >= 0:
+        ok, xs, ys, ln, _ = P.check_finish(sc, nodes[best[0]], goal, gyaw)
+        out["best_x"], out["best_y"] = xs, ys
+    return out
+
+
 def main():
     known = {k: dubins_record(v) for k, v in KNOWN.items()}
     with open(os.path.join(HERE, "dubins_known.json"), "w") as f:
@@ -94,6 +122,12 @@ def main():
     field = scenes.field512()
     with open(os.path.join(HERE, "rrt_field512.json"), "w") as f:
         json.dump([rrt_record(field, 42, 1200)], f)
+    fin = [finish_record(scenes.bench6_open(), s, 600) for s in (0, 1)]
+    with open(os.path.join(HERE, "finish_bench6_open.json"), "w") as f:
+        json.dump(fin, f)
+    print("finish: nodes", [r["n_nodes"] for r in fin], "ok",
+          [sum(x["ok"] for x in r["finish"]) for r in fin], "best",
+          [(r["best_node"], r["best_length"]) for r in fin])
     for k, v in known.items():
         print(k, P.WORD_NAMES[v["word"]], v["cost"], v["n"])
     print("bench6 nodes:", [len(r["x"]) for r in recs])

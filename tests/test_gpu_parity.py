@@ -344,3 +344,53 @@ def test_errors_are_codes(pkg, ctx):
     with pytest.raises(pkg.PPError) as e:
         rrt.RRT((5.0, 5.0), 0.0, (8.0, 8.0), 0.0, 10, 0.0, space, ctx=ctx)  # step 0
     assert e.value.code == pkg._ffi.PP_ERR_INVALID_ARGUMENT
+
+
+# ------------------------------------------------------------- goal connection (§8f rows 1-2)
+@pytest.mark.parametrize("k", [0, 1])
+def test_check_finish_batch_golden(pkg, ctx, k):
+    from pathplanning_amd import scenes
+
+    rec = load_golden("finish_bench6_open.json")[k]
+    raw = scenes.bench6_open(rec["start"][2])
+    p = _planner(pkg, raw, rec["seed"], 64, ctx)
+    p.extend(rec["n_iter"])
+    assert p.tree_size() == rec["n_nodes"]
+    nodes = np.arange(1, rec["n_nodes"], dtype=np.int32)
+    r = p.check_finish_batch(nodes)
+    fin = rec["finish"]
+    assert [bool(v) for v in r["ok"]] == [f["ok"] for f in fin]
+    for i, f in enumerate(fin):
+        levels = int(r["chain"][i, 0])
+        assert r["chain"][i, 2:2 + levels].tolist() == f["chain"], f["node"]
+        if f["ok"]:
+            assert r["n_points"][i] == f["n"]
+            assert abs(r["length"][i] - f["length"]) <= 1e-9 * f["length"]
+
+
+@pytest.mark.parametrize("k", [0, 1])
+def test_plan_golden(pkg, ctx, k):
+    from pathplanning_amd import scenes
+
+    rec = load_golden("finish_bench6_open.json")[k]
+    raw = scenes.bench6_open(rec["start"][2])
+    p = _planner(pkg, raw, rec["seed"], 4096, ctx)
+    line = p.plan(rec["n_iter"])
+    bn, bl, nf = p.last_plan
+    assert bn == rec["best_node"] and nf == sum(f["ok"] for f in rec["finish"])
+    assert abs(bl - rec["best_length"]) <= 1e-9 * rec["best_length"]
+    assert line.shape == (len(rec["best_x"]), 2)
+    assert np.max(np.abs(line[:, 0] - rec["best_x"])) <= PT_TOL
+    assert np.max(np.abs(line[:, 1] - rec["best_y"])) <= PT_TOL
+
+
+def test_check_finish_bench6_none_and_errors(pkg, ctx):
+    from pathplanning_amd import _ffi, scenes
+
+    raw = scenes.bench6()
+    p = _planner(pkg, raw, 0, 256, ctx)
+    assert p.plan(400) is None and p.last_plan[0] == -1
+    r = p.check_finish_batch(np.arange(1, p.tree_size(), dtype=np.int32))
+    assert not r["ok"].any() and (r["chain"][:, 0] == 16).all()
+    with pytest.raises(_ffi.PPError):
+        p.check_finish_batch(np.array([p.tree_size()], dtype=np.int32))
