@@ -17,6 +17,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "rs-pathplanning_amd"))
 
@@ -29,8 +31,15 @@ BYTES_PER_EVAL = 8            # f32 x + f32 y of one SoA node
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--workload", choices=("config2", "config3"), default="config2",
+                    help="config2: one tree, K-candidate windows (default); config3: a batch of "
+                         "independent queries sharded over the ranks")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (config2: windows, default 20; config3: lockstep "
+                         "iterations, default max_iter)")
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--queries", type=int, default=8192, help="config3: queries over all ranks")
+    ap.add_argument("--max-iter", type=int, default=2000, help="config3: RRT.max_iter per query")
     ap.add_argument("--window", type=int, default=4096)
     ap.add_argument("--nodes", type=int, default=100_000, help="tree size before timing")
     ap.add_argument("--seed", type=int, default=42)
@@ -41,16 +50,27 @@ def parse():
     return ap.parse_args()
 
 
-def dist_setup(args):
+def shard(total, world, rank):
+    """Queries [a, b) of `rank`: contiguous, sizes differ by at most one."""
+    base, extra = divmod(total, world)
+    a = rank * base + min(rank, extra)
+    return a, a + base + (1 if rank < extra else 0)
+
+
+def dist_setup(args, backend="gloo"):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch.distributed as dist  # control plane only: barrier + max-time reduce
+        import torch.distributed as dist  # control plane: barrier, max-time reduce, gather
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend="gloo", rank=rank, world_size=world)
+        if backend == "nccl":  # RCCL over xGMI on the GPU box
+            import torch
+
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return dist, world, rank, local
 
 
@@ -133,8 +153,32 @@ def load_traffic():
         return json.load(f).get("hbm_bytes_per_launch")
 
 
+def gather_records(dist, rec, backend):
+    """The config-3 result gather: every rank's per-query records to every rank (one
+    all_gather; RCCL over xGMI when the backend is nccl).  rec: int64 [q_rank, 3]."""
+    import torch
+
+    if dist is None:
+        return torch.from_numpy(rec)
+    world = dist.get_world_size()
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else None
+    n = torch.tensor([rec.shape[0]], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    mx = int(max(int(v.item()) for v in sizes))
+    pad = torch.zeros((mx, 3), dtype=torch.int64, device=dev)
+    pad[: rec.shape[0]] = torch.from_numpy(rec).to(pad.device)
+    outs = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad)
+    return torch.cat([o[: int(sz.item())].cpu() for o, sz in zip(outs, sizes)])
+
+
 def main():
     args = parse()
+    if args.workload == "config3":
+        return main_config3(args)
+    if args.steps is None:
+        args.steps = 20
     dist, world, rank, local = dist_setup(args)
     from pathplanning_amd import scenes
 
@@ -249,6 +293,99 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     p.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def main_config3(args):
+    """BASELINE config 3: `queries` independent planners on the config-2 field (query q: seed
+    42 + q, start/goal from stream q), max_iter each, sharded contiguously over the ranks; a step
+    = one lockstep extend iteration of every query of the rank.  Strong scaling: the total work is
+    fixed, each rank runs queries/world of it; one all_gather of per-query records at the end."""
+    import torch
+
+    backend = "nccl" if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and
+                         torch.cuda.is_available()) else "gloo"
+    dist, world, rank, local = dist_setup(args, backend)
+    from pathplanning_amd import rrt, scenes
+
+    raw = scenes.field512()
+    space = rrt.Space.from_raw(raw)
+    a, b = shard(args.queries, world, rank)
+    starts, goals, seeds = scenes.config3_queries(raw, a, b - a)
+    steps = args.max_iter if args.steps is None else args.steps
+    batch = rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
+                         device=local)
+    batch.extend(args.warmup)  # untimed warmup on a throwaway run
+    batch.close()
+    batch = rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
+                         device=local)
+    barrier(dist)
+    t0 = time.perf_counter()
+    it_local, acc_local = batch.extend(steps)
+    t_local = time.perf_counter() - t0
+    barrier(dist)
+    n, its, evals = batch.state(with_evals=True)
+    rec = np.stack([np.arange(a, b, dtype=np.int64), its.astype(np.int64), n.astype(np.int64)], 1)
+    allrec = gather_records(dist, rec, backend)
+    t_max = allreduce_max(dist, t_local)
+    iters_total = int(allrec[:, 1].sum())
+    value = iters_total / t_max
+    # profiled pass (same workload): HIP events around the batch NN kernel of every step
+    batch.close()
+    batch = rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
+                         device=local)
+    batch.set_profiling(True)
+    batch.extend(steps)
+    sp = batch.stats()
+    _, _, evals_p = batch.state(with_evals=True)
+    nn_ms = sp["nn_scan_ms"] / max(sp["nn_scan_launches"], 1)
+    evals_per_launch = float(evals_p.sum()) / max(sp["nn_scan_launches"], 1)
+    bytes_per_eval = 16  # f64 x + f64 y of one SoA row (exact NN, no f32 screen here)
+    achieved = evals_per_launch * bytes_per_eval / (nn_ms * 1e-3) / 1e9
+    line = {
+        "metric": "RRT extend iterations/sec (2D Dubins, 1k obstacles)",
+        "value": round(value, 1),
+        "unit": "iterations/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * t_max / steps, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"config3: {args.queries} independent queries on the config-2 field "
+                        f"(query q: seed 42+q, start/goal from stream q), max_iter "
+                        f"{args.max_iter}, sharded contiguously over {world} rank(s)",
+            "queries": args.queries,
+            "queries_per_rank": b - a,
+            "parallelism": f"query-shard{world}",
+            "gather": f"all_gather of per-query records ({backend})",
+        },
+        "iterations_total": iters_total,
+        "nodes_total": int(allrec[:, 2].sum()),
+        "roofline": {
+            "kernel": "mq_sample_nn",
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "avg_launch_ms": round(nn_ms, 5),
+            "evals_per_launch": int(evals_per_launch),
+            "bytes_per_eval": bytes_per_eval,
+            "measured": f"HIP events around mq_sample_nn, {sp['nn_scan_launches']} launches of "
+                        "the profiled pass that follows the timed region (same workload)",
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    batch.close()
     if dist is not None:
         dist.destroy_process_group()
 

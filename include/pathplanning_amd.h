@@ -56,7 +56,7 @@ typedef struct pp_stats {
     int64_t literal_repairs;  /* candidates re-run on the literal single-lane path */
     int64_t nn_flagged;       /* samples whose f32 NN screen needed the exact f64 rescan */
     int64_t node_evals;       /* sample-node distance evaluations of the NN screen */
-    double nn_scan_ms;        /* device time of nn_scan (HIP events; only when profiling is on) */
+    double nn_scan_ms;        /* device time of nn_scan, or of the batch NN (HIP events; profiling on) */
     int64_t nn_scan_launches;
     double steer_ms;          /* device time of steer_window (HIP events; profiling on) */
     int64_t steer_launches;
@@ -145,6 +145,23 @@ int pp_rrt_check_finish(pp_ctx* ctx, int32_t node, uint8_t* ok, double* x, doubl
  * (first on ties, -1 when none verified); the line via pp_rrt_check_finish(best_node). */
 int pp_rrt_plan(pp_ctx* ctx, int64_t n_iter, int32_t* best_node, double* best_length,
                 int64_t* n_finishes);
+
+/* ------------------------------------------------ independent query batch (BASELINE config 3) */
+/* q independent planners on the context's scene — RRT::new (rrt.rs:335-355) per query with
+ * start starts[3i..3i+2] (x, y, yaw), goal goals[3i..] (may be NULL), sampling stream seeds[i],
+ * the shared max_iter and step_size.  Replaces any previous batch of the context. */
+int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
+                 const uint64_t* seeds, int64_t max_iter, double step_size);
+/* n_steps lockstep steps: every query runs one plan_one extend iteration (rrt.rs:583-589) per
+ * step until it reaches max_iter.  Totals over the batch are returned (may be NULL). */
+int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted);
+/* per-query tree sizes (q int32), consumed iterations and NN node-distance evaluations (q int64
+ * each); any may be NULL.  With pp_set_profiling on, pp_batch_extend times its NN kernel with
+ * HIP events into pp_stats.nn_scan_ms / nn_scan_launches. */
+int pp_batch_state(pp_ctx* ctx, int32_t* n_nodes, int64_t* iterations, int64_t* node_evals);
+/* one query's tree (root first), like pp_rrt_tree_export */
+int pp_batch_tree_export(pp_ctx* ctx, int query, double* x, double* y, double* yaw,
+                         int32_t* parent, int64_t cap, int64_t* n);
 
 int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out);
 int pp_rrt_reset_stats(pp_ctx* ctx);

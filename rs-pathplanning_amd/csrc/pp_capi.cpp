@@ -140,6 +140,19 @@ struct pp_ctx {
     // check_finish
     DBuf<int> cf_nodes, cf_ok, cf_npts, cf_chain, cf_etab, cf_err;
     DBuf<double> cf_len, cf_pts;
+    // ---- multi-query batch (config 3)
+    bool has_batch = false;
+    int mq_Q = 0, mq_cap = 0;
+    int64_t mq_max_iter = 0;
+    double mq_step = 0.1;
+    DBuf<double> mq_x, mq_y, mq_yaw, mq_yawbuf, mq_pdbuf;
+    DBuf<int> mq_par, mq_n, mq_status, mq_err;
+    DBuf<int64_t> mq_it, mq_evals;
+    DBuf<uint64_t> mq_seed;
+    DBuf<SteerTask> mq_tasks;
+    DBuf<PrepRec> mq_rec;
+    DBuf<DevState> mq_state;
+    std::vector<double> mq_goal;  // 3 per query (kept for the host; the batch path is extend only)
 
     // ---- profiling
     bool prof = false;
@@ -338,6 +351,47 @@ int cf_launch(pp_ctx* c, int k, int want_line, int grid) {
     return PP_OK;
 }
 
+MqArgs mq_args(pp_ctx* c) {
+    MqArgs a;
+    a.mq.Q = c->mq_Q;
+    a.mq.cap = c->mq_cap;
+    a.mq.max_iter = c->mq_max_iter;
+    a.mq.x = c->mq_x.p;
+    a.mq.y = c->mq_y.p;
+    a.mq.yaw = c->mq_yaw.p;
+    a.mq.parent = c->mq_par.p;
+    a.mq.n = c->mq_n.p;
+    a.mq.it = c->mq_it.p;
+    a.mq.evals = c->mq_evals.p;
+    a.mq.seed = c->mq_seed.p;
+    a.sc = c->scene_dev();
+    a.sc.step_size = c->mq_step;
+    a.st = c->mq_state.p;
+    a.tasks = c->mq_tasks.p;
+    a.rec = c->mq_rec.p;
+    a.pdbuf = c->mq_pdbuf.p;
+    a.status = c->mq_status.p;
+    a.yaw = c->mq_yawbuf.p;
+    a.lit_scratch = c->api_lit_scratch.p;
+    a.err = c->mq_err.p;
+    return a;
+}
+
+int mq_totals(pp_ctx* c, int64_t* it_sum, int64_t* n_sum) {
+    std::vector<int> hn(c->mq_Q);
+    std::vector<int64_t> hit(c->mq_Q);
+    PP_HIP(hipMemcpyAsync(hn.data(), c->mq_n.p, c->mq_Q * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    PP_HIP(hipMemcpyAsync(hit.data(), c->mq_it.p, c->mq_Q * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    PP_HIP(hipStreamSynchronize(c->stream));
+    int64_t a = 0, b = 0;
+    for (int i = 0; i < c->mq_Q; ++i) {
+        a += hit[i];
+        b += hn[i];
+    }
+    *it_sum = a;
+    *n_sum = b;
+    return PP_OK;
+}
 }  // namespace
 
 // ===================================================================================== C ABI
@@ -880,6 +934,133 @@ int pp_rrt_plan(pp_ctx* ctx, int64_t n_iter, int32_t* best_node, double* best_le
     *best_node = bn;
     if (best_length) *best_length = bl;
     if (n_finishes) *n_finishes = nf;
+    return PP_OK;
+}
+
+int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
+                 const uint64_t* seeds, int64_t max_iter, double step_size) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (q <= 0 || !starts || !seeds || max_iter < 0 || max_iter > 0x7ffffff0 || !(step_size > 0.0))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad batch arguments");
+    const int64_t cap64 = max_iter + 1;
+    if ((int64_t)q * cap64 > ((int64_t)1 << 34)) return set_err(PP_ERR_CAPACITY, "batch too large");
+    const size_t rows = (size_t)q * (size_t)cap64;
+    ctx->has_batch = false;
+    PP_HIP(ctx->mq_x.reserve(rows));
+    PP_HIP(ctx->mq_y.reserve(rows));
+    PP_HIP(ctx->mq_yaw.reserve(rows));
+    PP_HIP(ctx->mq_par.reserve(rows));
+    PP_HIP(ctx->mq_n.reserve(q));
+    PP_HIP(ctx->mq_it.reserve(q));
+    PP_HIP(ctx->mq_evals.reserve(q));
+    PP_HIP(ctx->mq_seed.reserve(q));
+    PP_HIP(ctx->mq_tasks.reserve(q));
+    PP_HIP(ctx->mq_status.reserve(q));
+    PP_HIP(ctx->mq_yawbuf.reserve(q));
+    PP_HIP(ctx->mq_rec.reserve(q));
+    PP_HIP(ctx->mq_pdbuf.reserve((size_t)q * kPdCap));
+    PP_HIP(ctx->mq_state.reserve(1));
+    PP_HIP(ctx->mq_err.reserve(1));
+    PP_HIP(ctx->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
+    ctx->mq_Q = q;
+    ctx->mq_cap = (int)cap64;
+    ctx->mq_max_iter = max_iter;
+    ctx->mq_step = step_size;
+    ctx->mq_goal.assign(goals ? goals : starts, (goals ? goals : starts) + 3 * (size_t)q);
+    // RRT::new per query: the root (rrt.rs:344-346) in row 0 of each tree
+    std::vector<double> hx(q), hy(q), hyaw(q);
+    std::vector<int> hpar(q, -1), hn(q, 1);
+    std::vector<int64_t> hit(q, 0);
+    hipStream_t st = ctx->stream;
+    for (int i = 0; i < q; ++i) {
+        const size_t o = (size_t)i * cap64;
+        PP_HIP(hipMemcpyAsync(ctx->mq_x.p + o, starts + 3 * i, sizeof(double), hipMemcpyHostToDevice, st));
+        PP_HIP(hipMemcpyAsync(ctx->mq_y.p + o, starts + 3 * i + 1, sizeof(double), hipMemcpyHostToDevice, st));
+        PP_HIP(hipMemcpyAsync(ctx->mq_yaw.p + o, starts + 3 * i + 2, sizeof(double), hipMemcpyHostToDevice, st));
+        PP_HIP(hipMemcpyAsync(ctx->mq_par.p + o, &hpar[i], sizeof(int), hipMemcpyHostToDevice, st));
+        PP_HIP(hipStreamSynchronize(st));
+    }
+    PP_HIP(hipMemcpyAsync(ctx->mq_n.p, hn.data(), q * sizeof(int), hipMemcpyHostToDevice, st));
+    PP_HIP(hipMemcpyAsync(ctx->mq_it.p, hit.data(), q * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    PP_HIP(hipMemcpyAsync(ctx->mq_evals.p, hit.data(), q * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    ctx->nn_scan_ms = 0.0;
+    ctx->nn_scan_launches = 0;
+    PP_HIP(hipMemcpyAsync(ctx->mq_seed.p, seeds, q * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    DevState ds{};
+    ds.W = q;
+    PP_HIP(hipMemcpyAsync(ctx->mq_state.p, &ds, sizeof(DevState), hipMemcpyHostToDevice, st));
+    PP_HIP(hipMemsetAsync(ctx->mq_err.p, 0, sizeof(int), st));
+    PP_HIP(hipStreamSynchronize(st));
+    ctx->has_batch = true;
+    return PP_OK;
+}
+
+
+int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (!ctx->has_batch) return set_err(PP_ERR_STATE, "pp_batch_new has not been called");
+    if (n_steps < 0) return set_err(PP_ERR_INVALID_ARGUMENT, "n_steps < 0");
+    int64_t it0 = 0, n0 = 0, it1 = 0, n1 = 0;
+    if ((n_iterations || n_accepted) && (r = mq_totals(ctx, &it0, &n0))) return r;
+    MqArgs a = mq_args(ctx);
+    for (int64_t done = 0; done < n_steps;) {
+        const int chunk = (int)std::min<int64_t>(n_steps - done, 256);
+        if (ctx->prof) {
+            if ((r = ensure_events(ctx, 2 * (size_t)chunk))) return r;
+            a.ev = ctx->ev.data();
+        }
+        PP_HIP(launch_mq_steps(ctx->stream, a, chunk));
+        if (ctx->prof) {
+            PP_HIP(hipStreamSynchronize(ctx->stream));
+            for (int k = 0; k < chunk; ++k) {
+                float ms = 0.f;
+                PP_HIP(hipEventElapsedTime(&ms, ctx->ev[2 * k], ctx->ev[2 * k + 1]));
+                ctx->nn_scan_ms += ms;
+            }
+            ctx->nn_scan_launches += chunk;
+        }
+        done += chunk;
+    }
+    int err = 0;
+    PP_HIP(hipMemcpyAsync(&err, ctx->mq_err.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    PP_HIP(hipStreamSynchronize(ctx->stream));
+    if (err) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
+    if ((n_iterations || n_accepted) && (r = mq_totals(ctx, &it1, &n1))) return r;
+    if (n_iterations) *n_iterations = it1 - it0;
+    if (n_accepted) *n_accepted = n1 - n0;
+    return PP_OK;
+}
+
+int pp_batch_state(pp_ctx* ctx, int32_t* n_nodes, int64_t* iterations, int64_t* node_evals) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (!ctx->has_batch) return set_err(PP_ERR_STATE, "pp_batch_new has not been called");
+    if (node_evals) PP_HIP(hipMemcpyAsync(node_evals, ctx->mq_evals.p, ctx->mq_Q * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    if (n_nodes) PP_HIP(hipMemcpyAsync(n_nodes, ctx->mq_n.p, ctx->mq_Q * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    if (iterations) PP_HIP(hipMemcpyAsync(iterations, ctx->mq_it.p, ctx->mq_Q * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    PP_HIP(hipStreamSynchronize(ctx->stream));
+    return PP_OK;
+}
+
+int pp_batch_tree_export(pp_ctx* ctx, int query, double* x, double* y, double* yaw,
+                         int32_t* parent, int64_t cap, int64_t* n) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (!ctx->has_batch) return set_err(PP_ERR_STATE, "pp_batch_new has not been called");
+    if (query < 0 || query >= ctx->mq_Q) return set_err(PP_ERR_INVALID_ARGUMENT, "query out of range");
+    int nn = 0;
+    PP_HIP(hipMemcpy(&nn, ctx->mq_n.p + query, sizeof(int), hipMemcpyDeviceToHost));
+    if (n) *n = nn;
+    if (cap < nn) return set_err(PP_ERR_CAPACITY, "export buffer smaller than the tree");
+    const size_t o = (size_t)query * ctx->mq_cap;
+    hipStream_t st = ctx->stream;
+    if (x) PP_HIP(hipMemcpyAsync(x, ctx->mq_x.p + o, nn * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (y) PP_HIP(hipMemcpyAsync(y, ctx->mq_y.p + o, nn * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (yaw) PP_HIP(hipMemcpyAsync(yaw, ctx->mq_yaw.p + o, nn * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (parent) PP_HIP(hipMemcpyAsync(parent, ctx->mq_par.p + o, nn * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
     return PP_OK;
 }
 

@@ -60,6 +60,22 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
                                double* lit_scratch, double* pts, int pts_cap, int* etab, int* err,
                                int grid);
 
+// Multi-query batch: `steps` lockstep extend iterations of every query (config 3).
+struct MqArgs {
+    MqDev mq{};
+    SceneDev sc{};
+    DevState* st = nullptr;  // W = Q, ncomp = 0 (the steer kernels' task count)
+    SteerTask* tasks = nullptr;
+    PrepRec* rec = nullptr;
+    double* pdbuf = nullptr;
+    int* status = nullptr;
+    double* yaw = nullptr;
+    double* lit_scratch = nullptr;  // kLiteralWaves buffers
+    int* err = nullptr;
+    hipEvent_t* ev = nullptr;  // optional: 2 per step, around mq_sample_nn
+};
+hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps);
+
 hipError_t launch_dubins_batch(hipStream_t st, const double* conf, int n, int cap, double* px,
                                double* py, double* pyaw, int* n_out, int* word_out,
                                double* cost_out, int* status_out);

@@ -901,7 +901,9 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
     const DevState* __restrict__ st, SceneDev sc, const double* __restrict__ wsx,
     const double* __restrict__ wsy, const double* __restrict__ snap_pose,
     CandEntry* __restrict__ cand, PrepRec* __restrict__ rec, double* __restrict__ pdbuf,
-    double* __restrict__ snap_yaw) {
+    double* __restrict__ snap_yaw, const SteerTask* __restrict__ tasks) {
+    // tasks != nullptr: explicit (child, parent pose) tasks [0, W) (multi-query batch); a task
+    // with pnode < 0 is idle
     const int W = st->W;
     const int total = W + st->ncomp;
     const int lane = threadIdx.x & 63;
@@ -913,12 +915,22 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
     const double c = 1.0 / sc.turn_radius;
     for (int base = gw * TPW; base < total; base += nw * TPW) {
         const int t = base + lane / kPrepLanes;
-        const bool act = t < total;
+        bool act = t < total;
         int j = 0;
-        double px = 1.0, py = 0.0, pyaw = 0.0;
-        if (act)
+        double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0;
+        if (act && tasks) {
+            const SteerTask tk = tasks[t];
+            act = tk.pnode >= 0;
+            x = tk.x;
+            y = tk.y;
+            px = act ? tk.px : 1.0;
+            py = act ? tk.py : 0.0;
+            pyaw = act ? tk.pyaw : 0.0;
+        } else if (act) {
             window_task(t, W, wsx, wsy, snap_pose, cand, &j, &px, &py, &pyaw);
-        const double x = act ? wsx[j] : 0.0, y = act ? wsy[j] : 0.0;
+            x = wsx[j];
+            y = wsy[j];
+        }
         const double yaw = atan2(py - y, px - x);
         // dubins_path_planning, dubins.rs:401-408 (s = child, e = parent)
         const double ex = px - x, ey = py - y;
@@ -1086,7 +1098,7 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
             else if (1 + (long long)g > (long long)nq + 7 - 2)
                 state = kLiteral;
         }
-        if (act && r == 0) {
+        if (t < total && r == 0) {  // idle batch tasks get a kReject record (act == false)
             PrepRec o;
             o.x = x;
             o.y = y;
@@ -1122,7 +1134,7 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
             o.state = state;
             o.pad = 0;
             rec[t] = o;
-            if (t < W)
+            if (t < W || tasks)
                 snap_yaw[t] = yaw;
             else
                 cand[t - W].yaw = yaw;
@@ -1833,6 +1845,117 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
     return hipGetLastError();
 }
 
+// ------------------------------------------------- multi-query batch (config 3)
+//
+// One lockstep step advances every query by one plan_one extend iteration (rrt.rs:583-589):
+//   mq_sample_nn   one wave per query: rand_point (the query's own seeded stream) and the exact
+//                  f64 brute-force nearest node of its tree (lanes stride the SoA rows, lowest
+//                  index on ties) — each step streams every tree once: the HBM-read-bound NN of
+//                  SURVEY §8d
+//   steer_prep / steer_walk   the window pipeline's kernels on the Q explicit tasks
+//   mq_insert      the verdict (literal path for the measure-zero trim cases), append, it += 1
+// Queries are independent, so there is no speculation and no resolve.
+__global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx, double maxx,
+                                                           double miny, double maxy,
+                                                           SteerTask* __restrict__ tasks) {
+    const int lane = threadIdx.x & 63;
+    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    for (int q = gw; q < mq.Q; q += nw) {
+        const int64_t it = mq.it[q];
+        if (it >= mq.max_iter) {
+            if (lane == 0) tasks[q].pnode = -1;
+            continue;
+        }
+        const uint64_t seed = mq.seed[q];
+        const double x = gen_range(seed, 2 * (uint64_t)it, minx, maxx);
+        const double y = gen_range(seed, 2 * (uint64_t)it + 1, miny, maxy);
+        const int n = mq.n[q];
+        const size_t row = (size_t)q * mq.cap;
+        const double* __restrict__ X = mq.x + row;
+        const double* __restrict__ Y = mq.y + row;
+        double bd = __builtin_inf();
+        int bi = 0x7fffffff;
+#pragma unroll 4
+        for (int k = lane; k < n; k += 64) {
+            const double dx = x - X[k], dy = y - Y[k];
+            const double d2 = dx * dx + dy * dy;
+            if (d2 < bd) {
+                bd = d2;
+                bi = k;
+            }
+        }
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+        if (lane == 0)
+            tasks[q] = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, 0};
+    }
+}
+
+__global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
+                                                        const SteerTask* __restrict__ tasks,
+                                                        const int* __restrict__ status,
+                                                        const double* __restrict__ yaw,
+                                                        double* __restrict__ lit_scratch,
+                                                        int* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);  // <= kLiteralWaves
+    double* bx = lit_scratch + (size_t)gw * 3 * kLiteralCap;
+    for (int q = gw; q < mq.Q; q += nw) {
+        const SteerTask tk = tasks[q];
+        if (tk.pnode < 0) continue;
+        int st = status[q];
+        const double yw = yaw[q];
+        if (st == kLiteral)
+            st = steer_collide_literal(sc, tk.x, tk.y, yw, tk.px, tk.py, tk.pyaw, bx,
+                                       bx + kLiteralCap, bx + 2 * kLiteralCap);
+        if (lane == 0) {
+            if (st == kError) {
+                atomicOr(err, 1);
+                continue;
+            }
+            const int n = mq.n[q];
+            mq.evals[q] += n;  // the NN of this iteration scanned n nodes
+            if (st == kAccept) {
+                const size_t o = (size_t)q * mq.cap + n;
+                mq.x[o] = tk.x;
+                mq.y[o] = tk.y;
+                mq.yaw[o] = yw;
+                mq.parent[o] = tk.pnode;
+                mq.n[q] = n + 1;
+            }
+            mq.it[q] += 1;
+        }
+    }
+}
+
+hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
+    const int Q = a.mq.Q;
+    const int nn_blocks = std::min((Q + 3) / 4, 4096);
+    const int prep_blocks = std::min((Q * kPrepLanes + 255) / 256, 2048);
+    const int walk_blocks = std::min((Q + 3) / 4, 1024);
+    const int ins_blocks = std::min((Q + 3) / 4, kLiteralWaves / 4);
+    const int lds = a.sc.lds_bytes;
+    for (int k = 0; k < steps; ++k) {
+        if (a.ev) (void)hipEventRecord(a.ev[2 * k], s);
+        mq_sample_nn_kernel<<<nn_blocks, 256, 0, s>>>(a.mq, a.sc.minx, a.sc.maxx, a.sc.miny,
+                                                      a.sc.maxy, a.tasks);
+        if (a.ev) (void)hipEventRecord(a.ev[2 * k + 1], s);
+        steer_prep_kernel<<<prep_blocks, 256, 0, s>>>(a.st, a.sc, nullptr, nullptr, nullptr,
+                                                      nullptr, a.rec, a.pdbuf, a.yaw, a.tasks);
+        if (lds > 0)
+            steer_walk_kernel<true><<<walk_blocks, 256, lds, s>>>(a.st, a.sc, a.rec, a.pdbuf,
+                                                                  nullptr, a.status);
+        else
+            steer_walk_kernel<false><<<walk_blocks, 256, 0, s>>>(a.st, a.sc, a.rec, a.pdbuf,
+                                                                 nullptr, a.status);
+        mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
+                                                    a.lit_scratch, a.err);
+    }
+    return hipGetLastError();
+}
+
 // --------------------------------------------------------------------------- launch wrappers
 
 hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev) {
@@ -1858,7 +1981,7 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev) {
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K * kPrepLanes + 255) / 256;
     steer_prep_kernel<<<prep_blocks, 256, 0, s>>>(a.st, a.sc, a.wsx, a.wsy, a.snap_pose, a.cand,
-                                                  a.rec, a.pdbuf, a.snap_yaw);
+                                                  a.rec, a.pdbuf, a.snap_yaw, nullptr);
     const int lds = a.sc.lds_bytes;
     const int nwg = std::min((K + 3) / 4, 1024);
     if (lds > 0)

@@ -112,6 +112,22 @@ struct PrepRec {
 };
 enum : int { kPrepWalk = -1, kPrepNone = 4, kPrepFallback = 5 };
 
+// Multi-query batch (BASELINE config 3): Q independent trees, tree q in rows [q * cap, q * cap +
+// n[q]) of the SoA arrays, all advanced one extend iteration per lockstep step.
+struct MqDev {
+    int Q;             // queries
+    int cap;           // node rows per query (max_iter + 1: at most one insert per iteration)
+    int64_t max_iter;  // RRT.max_iter of every query
+    double* x;
+    double* y;
+    double* yaw;
+    int* parent;
+    int* n;                 // [Q] tree nodes
+    int64_t* it;            // [Q] next iteration
+    int64_t* evals;         // [Q] node-distance evaluations of the NN so far
+    const uint64_t* seed;   // [Q] sampling stream
+};
+
 // Resolve scratch (global, one window).
 struct ResolveScratch {
     int* order;     // [K * kCandCap] entry indices, per sample sorted by (d2, i)

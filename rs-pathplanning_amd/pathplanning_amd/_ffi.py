@@ -37,7 +37,8 @@ EXPORTED = [
     "pp_rrt_set_window", "pp_rrt_extend", "pp_rrt_plan_one", "pp_rrt_tree_size",
     "pp_rrt_iteration", "pp_rrt_tree_export", "pp_rrt_get_nearest_node_batch",
     "pp_rrt_verify_node_batch", "pp_rrt_check_finish_batch", "pp_rrt_check_finish",
-    "pp_rrt_plan", "pp_rrt_get_stats", "pp_rrt_reset_stats", "pp_set_profiling",
+    "pp_rrt_plan", "pp_batch_new", "pp_batch_extend", "pp_batch_state", "pp_batch_tree_export",
+    "pp_rrt_get_stats", "pp_rrt_reset_stats", "pp_set_profiling",
 ]
 
 
@@ -114,6 +115,11 @@ def lib():
             "pp_rrt_check_finish": ([vp, C.c_int32, C.POINTER(C.c_uint8), dp, dp, C.c_int64, i64p,
                                      dp], C.c_int),
             "pp_rrt_plan": ([vp, C.c_int64, ip, dp, i64p], C.c_int),
+            "pp_batch_new": ([vp, C.c_int, dp, dp, C.POINTER(C.c_uint64), C.c_int64, C.c_double],
+                             C.c_int),
+            "pp_batch_extend": ([vp, C.c_int64, i64p, i64p], C.c_int),
+            "pp_batch_state": ([vp, ip, i64p, i64p], C.c_int),
+            "pp_batch_tree_export": ([vp, C.c_int, dp, dp, dp, ip, C.c_int64, i64p], C.c_int),
             "pp_rrt_get_stats": ([vp, C.POINTER(StatsC)], C.c_int),
             "pp_rrt_reset_stats": ([vp], C.c_int),
             "pp_set_profiling": ([vp, C.c_int], C.c_int),

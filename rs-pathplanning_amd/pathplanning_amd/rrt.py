@@ -289,3 +289,66 @@ class RRT:  # rrt.rs:325-620
 
     def close(self):
         self.ctx.close()
+
+
+class RRTBatch:
+    """Many independent planners on one scene (BASELINE config 3): ``RRT::new`` per query
+    (rrt.rs:335-355) with its own start, goal and sampling stream, advanced in lockstep — one
+    plan_one extend iteration (rrt.rs:583-589) of every query per step — on one GPU."""
+
+    def __init__(self, starts, goals, max_iter, step_size, space: Space, seeds, device: int = 0,
+                 ctx: _ffi.Context | None = None):
+        self.ctx = ctx or _ffi.Context(device)
+        self.space = space
+        starts = np.ascontiguousarray(starts, dtype=np.float64).reshape(-1, 3)
+        goals = np.ascontiguousarray(goals, dtype=np.float64).reshape(-1, 3)
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+        self.q = len(starts)
+        self.max_iter = int(max_iter)
+        space._upload(self.ctx)
+        dp = C.POINTER(C.c_double)
+        _ffi.check(_ffi.lib().pp_batch_new(
+            self.ctx.handle, self.q, starts.ctypes.data_as(dp), goals.ctypes.data_as(dp),
+            seeds.ctypes.data_as(C.POINTER(C.c_uint64)), self.max_iter, float(step_size)))
+
+    def extend(self, n_steps: int):
+        """n_steps lockstep steps; returns (iterations consumed, nodes inserted) over the batch."""
+        it, acc = C.c_int64(0), C.c_int64(0)
+        _ffi.check(_ffi.lib().pp_batch_extend(self.ctx.handle, int(n_steps), C.byref(it),
+                                              C.byref(acc)))
+        return it.value, acc.value
+
+    def state(self, with_evals: bool = False):
+        """(tree sizes int32[q], iterations int64[q]) [+ NN node-distance evals int64[q]]."""
+        n = np.zeros(self.q, dtype=np.int32)
+        it = np.zeros(self.q, dtype=np.int64)
+        ev = np.zeros(self.q, dtype=np.int64)
+        i64 = C.POINTER(C.c_int64)
+        _ffi.check(_ffi.lib().pp_batch_state(self.ctx.handle,
+                                             n.ctypes.data_as(C.POINTER(C.c_int32)),
+                                             it.ctypes.data_as(i64), ev.ctypes.data_as(i64)))
+        return (n, it, ev) if with_evals else (n, it)
+
+    def stats(self) -> dict:
+        s = _ffi.StatsC()
+        _ffi.check(_ffi.lib().pp_rrt_get_stats(self.ctx.handle, C.byref(s)))
+        return s.as_dict()
+
+    def set_profiling(self, on: bool):
+        _ffi.check(_ffi.lib().pp_set_profiling(self.ctx.handle, int(bool(on))))
+
+    def tree(self, query: int):
+        """(x, y, yaw, parent) of one query's tree, root first."""
+        n_all, _ = self.state()
+        n = int(n_all[query])
+        x, y, yaw = np.zeros(n), np.zeros(n), np.zeros(n)
+        par = np.zeros(n, dtype=np.int32)
+        out = C.c_int64(0)
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        _ffi.check(_ffi.lib().pp_batch_tree_export(
+            self.ctx.handle, int(query), x.ctypes.data_as(dp), y.ctypes.data_as(dp),
+            yaw.ctypes.data_as(dp), par.ctypes.data_as(ip), n, C.byref(out)))
+        return x, y, yaw, par
+
+    def close(self):
+        self.ctx.close()

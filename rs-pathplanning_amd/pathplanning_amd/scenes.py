@@ -132,3 +132,32 @@ def query_endpoints(raw: dict, q: int, seed_base: int = 0):
         if free(x, y):
             out.append((x, y, yaw))
     return out[0], out[1]
+
+
+def config3_queries(raw: dict, first: int, count: int, seed_base: int = 42):
+    """BASELINE config 3: query q (q in [first, first + count)) samples with stream seed_base + q;
+    its start and goal are the first two free poses of stream q — attempt a draws x, y, yaw from
+    counters 3a, 3a+1, 3a+2 over the shrunken bounds; a pose is free when it is at least 1.0
+    outside every inflated disc.  Returns (starts[count, 3], goals[count, 3], seeds[count])."""
+    half = raw["robot"][0] / 2.0
+    x0, y0, x1, y1 = raw["bounds"]
+    minx, miny, maxx, maxy = x0 + half, y0 + half, x1 - half, y1 - half
+    circ = np.asarray(raw["circles"], dtype=np.float64).reshape(-1, 3)
+    cx, cy = circ[:, 0], circ[:, 1]
+    lim2 = (circ[:, 2] + half + 1.0) ** 2
+    starts = np.zeros((count, 3))
+    goals = np.zeros((count, 3))
+    for i in range(count):
+        q = first + i
+        poses = []
+        a = 0
+        while len(poses) < 2:
+            x = gen_range(q, 3 * a, minx, maxx)
+            y = gen_range(q, 3 * a + 1, miny, maxy)
+            yaw = gen_range(q, 3 * a + 2, -math.pi, math.pi)
+            a += 1
+            if len(cx) == 0 or np.all((cx - x) ** 2 + (cy - y) ** 2 > lim2):
+                poses.append((x, y, yaw))
+        starts[i], goals[i] = poses
+    seeds = np.arange(first, first + count, dtype=np.uint64) + np.uint64(seed_base)
+    return starts, goals, seeds

@@ -394,3 +394,42 @@ def test_check_finish_bench6_none_and_errors(pkg, ctx):
     assert not r["ok"].any() and (r["chain"][:, 0] == 16).all()
     with pytest.raises(_ffi.PPError):
         p.check_finish_batch(np.array([p.tree_size()], dtype=np.int32))
+
+
+# ----------------------------------------------------- independent query batch (config 3)
+def _oracle_query(oracle_mod, raw, start, seed, n_iter, max_iter):
+    sc = oracle_mod.OracleScene.from_raw(raw)
+    tr = oracle_mod.OracleTree(tuple(start), n_iter + 8)
+    oracle_mod.rrt_extend(sc, tr, int(seed), 0, min(n_iter, max_iter))
+    return tr.arrays()
+
+
+def test_batch_field512_matches_independent_oracle_runs(pkg, ctx, oracle_mod):
+    from pathplanning_amd import rrt, scenes
+
+    raw = scenes.field512()
+    starts, goals, seeds = scenes.config3_queries(raw, 0, 37)  # Q not a multiple of 4 or 8
+    b = rrt.RRTBatch(starts, goals, 2000, raw["step_size"], rrt.Space.from_raw(raw), seeds,
+                     ctx=ctx)
+    it, acc = b.extend(250)
+    n, its = b.state()
+    assert it == 37 * 250 and (its == 250).all() and acc == int(n.sum()) - 37
+    for q in range(37):
+        exp = _oracle_query(oracle_mod, raw, starts[q], seeds[q], 250, 2000)
+        _assert_same_tree(b.tree(q), exp)
+
+
+def test_batch_stops_at_max_iter_and_matches_bench6(pkg, ctx, oracle_mod):
+    from pathplanning_amd import rrt, scenes
+
+    raw = scenes.bench6_open()
+    starts, goals, seeds = scenes.config3_queries(raw, 100, 24)
+    b = rrt.RRTBatch(starts, goals, 150, raw["step_size"], rrt.Space.from_raw(raw), seeds,
+                     ctx=ctx)
+    b.extend(100)
+    it, acc = b.extend(100)  # only 50 more iterations per query remain
+    n, its = b.state()
+    assert it == 24 * 50 and (its == 150).all()
+    for q in range(24):
+        exp = _oracle_query(oracle_mod, raw, starts[q], seeds[q], 150, 150)
+        _assert_same_tree(b.tree(q), exp)
