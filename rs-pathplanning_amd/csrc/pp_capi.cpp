@@ -969,23 +969,11 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
     ctx->mq_step = step_size;
     ctx->mq_goal.assign(goals ? goals : starts, (goals ? goals : starts) + 3 * (size_t)q);
     // RRT::new per query: the root (rrt.rs:344-346) in row 0 of each tree
-    std::vector<double> hx(q), hy(q), hyaw(q);
-    std::vector<int> hpar(q, -1), hn(q, 1);
-    std::vector<int64_t> hit(q, 0);
     hipStream_t st = ctx->stream;
-    for (int i = 0; i < q; ++i) {
-        const size_t o = (size_t)i * cap64;
-        PP_HIP(hipMemcpyAsync(ctx->mq_x.p + o, starts + 3 * i, sizeof(double), hipMemcpyHostToDevice, st));
-        PP_HIP(hipMemcpyAsync(ctx->mq_y.p + o, starts + 3 * i + 1, sizeof(double), hipMemcpyHostToDevice, st));
-        PP_HIP(hipMemcpyAsync(ctx->mq_yaw.p + o, starts + 3 * i + 2, sizeof(double), hipMemcpyHostToDevice, st));
-        PP_HIP(hipMemcpyAsync(ctx->mq_par.p + o, &hpar[i], sizeof(int), hipMemcpyHostToDevice, st));
-        PP_HIP(hipStreamSynchronize(st));
-    }
-    PP_HIP(hipMemcpyAsync(ctx->mq_n.p, hn.data(), q * sizeof(int), hipMemcpyHostToDevice, st));
-    PP_HIP(hipMemcpyAsync(ctx->mq_it.p, hit.data(), q * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    PP_HIP(hipMemcpyAsync(ctx->mq_evals.p, hit.data(), q * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    ctx->nn_scan_ms = 0.0;
-    ctx->nn_scan_launches = 0;
+    DBuf<double> d_starts;
+    PP_HIP(d_starts.reserve(3 * (size_t)q));
+    PP_HIP(hipMemcpyAsync(d_starts.p, starts, 3 * (size_t)q * sizeof(double), hipMemcpyHostToDevice, st));
+    PP_HIP(launch_mq_init(st, mq_args(ctx).mq, d_starts.p));
     PP_HIP(hipMemcpyAsync(ctx->mq_seed.p, seeds, q * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     DevState ds{};
     ds.W = q;

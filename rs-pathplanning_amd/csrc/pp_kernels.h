@@ -75,6 +75,7 @@ struct MqArgs {
     hipEvent_t* ev = nullptr;  // optional: 2 per step, around mq_sample_nn
 };
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps);
+hipError_t launch_mq_init(hipStream_t s, const MqDev& mq, const double* starts);
 
 hipError_t launch_dubins_batch(hipStream_t st, const double* conf, int n, int cap, double* px,
                                double* py, double* pyaw, int* n_out, int* word_out,

@@ -1059,7 +1059,8 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
         const Pt E = seg_end(m2, L2, c, O2.x, O2.y, ca2, sa2, sl2, cl2);
         // the trim (dubins.rs:281-288) drops exactly the endpoint unless its local x is 0.0
         if (state == kPrepWalk && E.x == 0.0) state = kLiteral;
-        int cnt0 = 0, cnt1 = 0, cnt2 = 0;
+        int cnt0 = 0, cnt1 = 0, cnt2 = 0, fb_seg = 0;
+        double fb_pd = 0.0, fb_dd = 0.0;
         if (state == kPrepWalk) {
             double* pdv = pdbuf + (size_t)t * kPdCap;
             int g = 0, seg = 0;
@@ -1069,8 +1070,17 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
             bool over = false;
             for (;;) {  // every iteration stores a point (g < kPdCap) or ends a segment
                 if (fabs(pd) <= fabs(Ls)) {
-                    if (g >= kPdCap) {
+                    if (g >= kPdCap) {  // keep the walk's state for steer_walk
                         over = true;
+                        fb_seg = seg;
+                        fb_pd = pd;
+                        fb_dd = dd;
+                        if (seg == 0)
+                            cnt0 = g;
+                        else if (seg == 1)
+                            cnt1 = g - cnt0;
+                        else
+                            cnt2 = g - cnt0 - cnt1;
                         break;
                     }
                     if ((g & (kPrepLanes - 1)) == r) pdv[g] = pd;
@@ -1125,6 +1135,9 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
             o.L[1] = L1;
             o.L[2] = L2;
             o.n_point = (long long)nq + 3 + 4;
+            o.fb_pd = fb_pd;
+            o.fb_dd = fb_dd;
+            o.fb_seg = fb_seg;
             o.m[0] = m0;
             o.m[1] = m1;
             o.m[2] = m2;
@@ -1132,7 +1145,6 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
             o.cnt[1] = cnt1;
             o.cnt[2] = cnt2;
             o.state = state;
-            o.pad = 0;
             rec[t] = o;
             if (t < W || tasks)
                 snap_yaw[t] = yaw;
@@ -1146,8 +1158,9 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
 // grid points: lane k >= 1 interpolates grid point base + k - 1 (interpolate, dubins.rs:155-198,
 // then the world transform dubins.rs:412-422), lane 0 carries the previous chunk's last point,
 // and the junction to the parent follows the last grid point.  A kPrepWalk task reads its pd
-// values from pdbuf; a kPrepFallback task (more than kPdCap points) regenerates them with the
-// uniform serial `pd += d` walk, each lane capturing its own point.
+// values from pdbuf; a kPrepFallback task (more than kPdCap points) reads its first kPdCap there
+// and continues with the uniform serial `pd += d` walk from the state steer_prep kept, each lane
+// capturing its own point.
 template <bool kLds>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
                                         const double* __restrict__ pdv) {
@@ -1160,7 +1173,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         return chunk_rejects<kLds>(sc, has, has, lane == 1, qx, qy) ? kReject : kAccept;
     }
     if (state != kPrepWalk && state != kPrepFallback) return state;
-    const bool gen = state == kPrepFallback;
+    const bool partial = state == kPrepFallback;  // pdbuf holds the first kPdCap points only
     const double step = sc.step_size;
     const double c = p->c, cw = p->cw, sw = p->sw;
     const double ox1 = p->ox[1], oy1 = p->oy[1], ox2 = p->ox[2], oy2 = p->oy[2];
@@ -1169,39 +1182,55 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     const double L0 = p->L[0], L1 = p->L[1], L2 = p->L[2];
     const int m0 = p->m[0], m1 = p->m[1], m2 = p->m[2];
     const int n0 = p->cnt[0], n01 = n0 + p->cnt[1], ng = n01 + p->cnt[2];
-    // serial generator state (kPrepFallback only)
-    int gseg = 0;
-    double gdd = (L0 > 0.0) ? step : -step;
-    double gpd = gdd - 0.0;
-    long long grid = 0;
+    // serial generator (kPrepFallback past the stored points), resumed where steer_prep stopped
+    int gseg = p->fb_seg;
+    double gdd = p->fb_dd;
+    double gpd = p->fb_pd;
+    long long grid = kPdCap;
+    static_assert(kPdCap % 63 == 0, "stored points end on a chunk boundary");
     double carry_x = x, carry_y = y;
     for (int base = 0;; base += 63) {
         int cnt = 0, my_seg = 0;
         double my_pd = 0.0;
         bool done;
+        const bool gen = partial && base >= kPdCap;
         if (gen) {
-            while (cnt < 63 && gseg < 3) {
+            // lane-parallel `pd += d` (dubins.rs:239-255): lane l >= pos replays l - pos
+            // additions from the uniform start value — the serial walk's exact rounding
+            // sequence — and the first lane whose |pd| exceeds |L| ends the segment (its value
+            // gives ll and the next segment's start, dubins.rs:256-259)
+            int pos = 1;
+            while (pos <= 63 && gseg < 3) {
                 const double Ls = gseg == 0 ? L0 : (gseg == 1 ? L1 : L2);
-                if (fabs(gpd) <= fabs(Ls)) {
-                    if (lane == cnt + 1) {
-                        my_seg = gseg;
-                        my_pd = gpd;
-                    }
-                    ++cnt;
-                    gpd += gdd;
-                } else {
-                    const double ll = Ls - gpd - gdd;
+                const int kk = lane - pos;
+                double v = gpd;
+                for (int u = 0; u < 63 - pos; ++u) v = (u < kk) ? v + gdd : v;
+                const uint64_t bad = __ballot(lane >= pos && !(fabs(v) <= fabs(Ls)));
+                const int m = bad ? (int)__builtin_ctzll(bad) : 64;
+                if (lane >= pos && lane < m) {
+                    my_seg = gseg;
+                    my_pd = v;
+                }
+                if (m <= 63) {
+                    const double pend = readlane_f64(v, m);
+                    const double ll = Ls - pend - gdd;
                     if (++gseg < 3) {
                         const double Ln = gseg == 1 ? L1 : L2;
                         gdd = (Ln > 0.0) ? step : -step;
                         gpd = ((Ls * Ln) > 0.0) ? (-gdd - ll) : (gdd - ll);
                     }
+                    cnt += m - pos;
+                    pos = m;
+                } else {
+                    gpd = readlane_f64(v, 63) + gdd;
+                    cnt += 64 - pos;
+                    pos = 64;
                 }
             }
             grid += cnt;
             done = gseg >= 3;
         } else {
-            const int rem = ng - base;
+            const int rem = partial ? 63 : ng - base;
             cnt = rem < 63 ? rem : 63;
             done = rem < 63;
             const int g = base + lane - 1;
@@ -1247,7 +1276,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         carry_y = __shfl(qy, 63);
     }
     // no trailing zero left for the trim (dubins.rs:281-288): the literal path decides
-    if (gen && 1 + grid > p->n_point - 2) return kLiteral;
+    if (partial && 1 + grid > p->n_point - 2) return kLiteral;
     return kAccept;
 }
 
@@ -1898,36 +1927,70 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
                                                         const double* __restrict__ yaw,
                                                         double* __restrict__ lit_scratch,
                                                         int* __restrict__ err) {
+    // lane per query; a wave (<= kLiteralWaves of them, one literal scratch each) re-runs its
+    // lanes' literal-path tasks together, one at a time
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);  // <= kLiteralWaves
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     double* bx = lit_scratch + (size_t)gw * 3 * kLiteralCap;
-    for (int q = gw; q < mq.Q; q += nw) {
-        const SteerTask tk = tasks[q];
-        if (tk.pnode < 0) continue;
-        int st = status[q];
-        const double yw = yaw[q];
-        if (st == kLiteral)
-            st = steer_collide_literal(sc, tk.x, tk.y, yw, tk.px, tk.py, tk.pyaw, bx,
-                                       bx + kLiteralCap, bx + 2 * kLiteralCap);
-        if (lane == 0) {
-            if (st == kError) {
-                atomicOr(err, 1);
-                continue;
-            }
-            const int n = mq.n[q];
-            mq.evals[q] += n;  // the NN of this iteration scanned n nodes
-            if (st == kAccept) {
-                const size_t o = (size_t)q * mq.cap + n;
-                mq.x[o] = tk.x;
-                mq.y[o] = tk.y;
-                mq.yaw[o] = yw;
-                mq.parent[o] = tk.pnode;
-                mq.n[q] = n + 1;
-            }
-            mq.it[q] += 1;
+    for (int base = gw * 64; base < mq.Q; base += nw * 64) {
+        const int q = base + lane;
+        const bool in = q < mq.Q;
+        SteerTask tk{};
+        int st = kReject;
+        double yw = 0.0;
+        if (in) {
+            tk = tasks[q];
+            st = status[q];
+            yw = yaw[q];
         }
+        const bool act = in && tk.pnode >= 0;
+        uint64_t lit = __ballot(act && st == kLiteral);
+        while (lit) {
+            const int l = __builtin_ctzll(lit);
+            lit &= lit - 1;
+            const double x = __shfl(tk.x, l), y = __shfl(tk.y, l), w = __shfl(yw, l);
+            const double px = __shfl(tk.px, l), py = __shfl(tk.py, l), pw = __shfl(tk.pyaw, l);
+            const int r = steer_collide_literal(sc, x, y, w, px, py, pw, bx, bx + kLiteralCap,
+                                                bx + 2 * kLiteralCap);
+            if (lane == l) st = r;
+        }
+        if (!act) continue;
+        if (st == kError) {
+            atomicOr(err, 1);
+            continue;
+        }
+        const int n = mq.n[q];
+        mq.evals[q] += n;  // the NN of this iteration scanned n nodes
+        if (st == kAccept) {
+            const size_t o = (size_t)q * mq.cap + n;
+            mq.x[o] = tk.x;
+            mq.y[o] = tk.y;
+            mq.yaw[o] = yw;
+            mq.parent[o] = tk.pnode;
+            mq.n[q] = n + 1;
+        }
+        mq.it[q] += 1;
     }
+}
+
+// roots of a new batch (RRT::new, rrt.rs:344-346): row 0 of every tree
+__global__ __launch_bounds__(256) void mq_init_kernel(MqDev mq, const double* __restrict__ starts) {
+    const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= mq.Q) return;
+    const size_t o = (size_t)q * mq.cap;
+    mq.x[o] = starts[3 * q];
+    mq.y[o] = starts[3 * q + 1];
+    mq.yaw[o] = starts[3 * q + 2];
+    mq.parent[o] = -1;
+    mq.n[q] = 1;
+    mq.it[q] = 0;
+    mq.evals[q] = 0;
+}
+
+hipError_t launch_mq_init(hipStream_t s, const MqDev& mq, const double* starts) {
+    mq_init_kernel<<<(mq.Q + 255) / 256, 256, 0, s>>>(mq, starts);
+    return hipGetLastError();
 }
 
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
@@ -1935,7 +1998,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int nn_blocks = std::min((Q + 3) / 4, 4096);
     const int prep_blocks = std::min((Q * kPrepLanes + 255) / 256, 2048);
     const int walk_blocks = std::min((Q + 3) / 4, 1024);
-    const int ins_blocks = std::min((Q + 3) / 4, kLiteralWaves / 4);
+    const int ins_blocks = std::min((Q + 255) / 256, kLiteralWaves / 4);
     const int lds = a.sc.lds_bytes;
     for (int k = 0; k < steps; ++k) {
         if (a.ev) (void)hipEventRecord(a.ev[2 * k], s);

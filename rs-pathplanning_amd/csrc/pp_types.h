@@ -24,7 +24,7 @@ constexpr int kLiteralWaves = 256;   // literal scratch buffers (explicit-task k
 constexpr int kResolveThreads = 256; // one workgroup resolves a window (4 waves: 1 per SIMD)
 constexpr int kMaxWindow = 4096;     // K limit: the resolve keeps the window's state in LDS
 constexpr int kSteerPrepBytes = 152; // sizeof(SteerPrep) (checked in pp_kernels.hip)
-constexpr int kPdCap = 256;          // grid points per task stored by steer_prep (more: fallback)
+constexpr int kPdCap = 63;           // grid points per task stored by steer_prep (one walk chunk)
 constexpr int kPrepLanes = 8;        // lanes per task in steer_prep
 constexpr int kCfMaxDepth = 8192;    // check_finish: ancestor path staged in LDS (32 KB)
 constexpr int kCfLevels = 16;        // RECURSION_LIMIT, rrt.rs:14
@@ -99,16 +99,19 @@ struct CandEntry {
 // Per-task steer record of the window pipeline, written by steer_prep (8 lanes per task) and read
 // by steer_walk (one wave per task) with scalar loads.  The task's grid-point distances (the
 // `pd` values of generate_local_course, dubins.rs:239-255) sit in pdbuf[t * kPdCap + g]; a task
-// with more than kPdCap grid points (kPrepFallback) is walked serially by steer_walk instead.
+// with more than kPdCap grid points (kPrepFallback) stores its first kPdCap and the walk's state
+// there, and steer_walk generates the rest lane-parallel (only if the first chunk did not reject).
 struct PrepRec {
     double x, y, px, py, yaw, pyaw;  // child (point 0), parent (the junction) and their headings
     double c, cw, sw;                // curvature, cos/sin(-yaw) of the world transform
     double ox[3], oy[3];             // segment origins in the local frame
     double ca[3], sa[3];             // segment trig: S cos/sin(o.yaw), L/R cos/sin(-o.yaw)
     double L[3];                     // segment lengths (the serial walk of kPrepFallback)
+    double fb_pd, fb_dd;             // kPrepFallback: the walk's state at point kPdCap (pd, d)
     long long n_point;               // dubins.rs:369
-    int m[3], cnt[3];                // segment modes and grid points per segment
-    int state, pad;                  // kPrepWalk / kPrepNone / kPrepFallback or a verdict
+    int m[3], cnt[3];                // segment modes, grid points per segment (of the stored ones)
+    int state, fb_seg;               // kPrepWalk / kPrepNone / kPrepFallback or a verdict; the
+                                     // kPrepFallback walk's segment at point kPdCap
 };
 enum : int { kPrepWalk = -1, kPrepNone = 4, kPrepFallback = 5 };
 
