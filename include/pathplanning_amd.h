@@ -98,6 +98,15 @@ int pp_dubins_path_planning_batch(pp_ctx* ctx, const pp_dubins_config* confs, in
 int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double robot_width,
                  double robot_height, double max_steer, const double* cx, const double* cy,
                  const double* r, int m);
+/* BASELINE config 4: replace the obstacles of the current Space by a bit-packed occupancy grid
+ * of w x h cells of size `cell` whose corner is (x0, y0): cell (i, j) is bit i % 32 of word
+ * j * ceil(w / 32) + i / 32.  Verify then requires every point of the line inside the bounds and
+ * in a free cell, with cell = (floor((x - x0) / cell), floor((y - y0) / cell)) and points outside
+ * the grid counting as occupied; segments are not rasterised.  (The reference has no grid mode;
+ * this is the build-defined semantics of SURVEY.md §8d config 4.)  A later pp_space_new clears
+ * it; a planner must be created after it (pp_rrt_new / pp_batch_new). */
+int pp_space_set_grid(pp_ctx* ctx, const uint32_t* bits, int w, int h, double x0, double y0,
+                      double cell);
 /* the shrunken bounds bbox (minx, maxx, miny, maxy) sampled by Space::rand_point (rrt.rs:84-106) */
 int pp_space_get_bounds(pp_ctx* ctx, double out_minx_maxx_miny_maxy[4]);
 

@@ -260,6 +260,16 @@ def verify_line(scene, xs, ys):  # rrt.rs:124-137 (Q10)
         return False
     if np.any(ys < scene["miny"]) or np.any(ys > scene["maxy"]):
         return False
+    if scene.get("grid") is not None:  # config 4: every point in a free cell
+        bits, w, gx0, gy0, cell = scene["grid"]
+        inv = 1.0 / cell
+        for x, y in zip(xs, ys):
+            fx, fy = math.floor((x - gx0) * inv), math.floor((y - gy0) * inv)
+            if not (0 <= fx < w and 0 <= fy < bits.shape[0]):
+                return False
+            if (int(bits[fy, fx >> 5]) >> (fx & 31)) & 1:
+                return False
+        return True
     cx, cy, r2 = scene["cx"], scene["cy"], scene["r2"]
     if len(cx) == 0:
         return True

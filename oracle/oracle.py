@@ -37,6 +37,8 @@ class Scene(C.Structure):
         ("m", C.c_int),
         ("cx", C.POINTER(C.c_double)), ("cy", C.POINTER(C.c_double)), ("r2", C.POINTER(C.c_double)),
         ("turn_radius", C.c_double), ("step_size", C.c_double),
+        ("bits", C.POINTER(C.c_uint32)), ("bw", C.c_int), ("bh", C.c_int), ("bwords", C.c_int),
+        ("bx0", C.c_double), ("by0", C.c_double), ("binv", C.c_double),
     ]
 
 
@@ -136,7 +138,7 @@ class OracleScene:
     """Space::new (rrt.rs:81-122) restated for the oracle: bounds rectangle shrunk by width/2,
     discs inflated by width/2 (Q10)."""
 
-    def __init__(self, bounds, width, circles, turn_radius, step_size):
+    def __init__(self, bounds, width, circles, turn_radius, step_size, grid=None):
         half = width / 2.0
         x0, y0, x1, y1 = bounds
         self.minx, self.miny, self.maxx, self.maxy = x0 + half, y0 + half, x1 - half, y1 - half
@@ -149,15 +151,24 @@ class OracleScene:
         self.step_size = float(step_size)
         self._c = Scene(self.minx, self.maxx, self.miny, self.maxy, len(self.cx), _dp(self.cx),
                         _dp(self.cy), _dp(self.r2), self.turn_radius, self.step_size)
+        self.grid = None
+        if grid is not None:
+            bits, w, gx0, gy0, cell = grid
+            self.bits = np.ascontiguousarray(bits, dtype=np.uint32)
+            self.grid = (self.bits, int(w), float(gx0), float(gy0), float(cell))
+            self._c.bits = self.bits.ctypes.data_as(C.POINTER(C.c_uint32))
+            self._c.bw, self._c.bh, self._c.bwords = int(w), self.bits.shape[0], self.bits.shape[1]
+            self._c.bx0, self._c.by0, self._c.binv = float(gx0), float(gy0), 1.0 / float(cell)
 
     @classmethod
     def from_raw(cls, raw):
-        return cls(raw["bounds"], raw["robot"][0], raw["circles"], raw["robot"][2], raw["step_size"])
+        return cls(raw["bounds"], raw["robot"][0], raw["circles"], raw["robot"][2], raw["step_size"],
+                   grid=raw.get("grid"))
 
     def as_dict(self):
         return {"minx": self.minx, "maxx": self.maxx, "miny": self.miny, "maxy": self.maxy,
                 "cx": self.cx, "cy": self.cy, "r2": self.r2, "turn_radius": self.turn_radius,
-                "step_size": self.step_size}
+                "step_size": self.step_size, "grid": self.grid}
 
     def verify_line(self, xs, ys):
         xs = np.ascontiguousarray(xs, dtype=np.float64)

@@ -336,6 +336,11 @@ typedef struct {
     const double* r2; /* (r + width/2)^2 */
     double turn_radius;  /* Robot.max_steer (rrt.rs:37-39 → 424) */
     double step_size;
+    /* config 4 occupancy grid (build-defined): when bits != NULL the discs are
+     * ignored and every point of a line must lie in a free cell */
+    const uint32_t* bits;
+    int bw, bh, bwords;
+    double bx0, by0, binv;
 } orc_scene;
 
 typedef struct {
@@ -367,12 +372,26 @@ static int in_bounds(const orc_scene* sc, double x, double y) {
     return x >= sc->minx && x <= sc->maxx && y >= sc->miny && y <= sc->maxy;
 }
 
+/* config 4 probe: cell (floor((x - x0) * inv), floor((y - y0) * inv)); outside = occupied */
+static int grid_occupied(const orc_scene* sc, double x, double y) {
+    double fx = floor((x - sc->bx0) * sc->binv), fy = floor((y - sc->by0) * sc->binv);
+    if (!(fx >= 0.0) || !(fy >= 0.0) || fx >= (double)sc->bw || fy >= (double)sc->bh) return 1;
+    int i = (int)fx, j = (int)fy;
+    return (int)((sc->bits[(size_t)j * sc->bwords + (i >> 5)] >> (i & 31)) & 1u);
+}
+
 /* Space::verify, rrt.rs:124-137: bounds.contains(line) && no obstacle intersects the line.
- * A one-point line is tested as a point (degenerate segment). */
+ * A one-point line is tested as a point (degenerate segment).  With an occupancy grid: every
+ * point in bounds and in a free cell. */
 int orc_verify_line(const orc_scene* sc, const double* x, const double* y, int n) {
     if (n <= 0) return 1;
     for (int i = 0; i < n; ++i)
         if (!in_bounds(sc, x[i], y[i])) return 0;
+    if (sc->bits) {
+        for (int i = 0; i < n; ++i)
+            if (grid_occupied(sc, x[i], y[i])) return 0;
+        return 1;
+    }
     if (n == 1) {
         for (int k = 0; k < sc->m; ++k)
             if (seg_hits_disc(x[0], y[0], x[0], y[0], sc->cx[k], sc->cy[k], sc->r2[k])) return 0;

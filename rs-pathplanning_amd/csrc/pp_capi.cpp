@@ -102,6 +102,11 @@ struct pp_ctx {
     double gx0 = 0, gy0 = 0, ginv = 1;
     int gnx = 1, gny = 1;
     int lds_bytes = 0, lds_goff = 0, lds_items = 0, lds_cx = 0, lds_cy = 0, lds_r2 = 0;
+    // occupancy grid (config 4)
+    bool has_grid = false;
+    DBuf<uint32_t> d_bits;
+    int bw = 0, bh = 0, bwords = 0, lds_bits_bytes = 0;
+    double bx0 = 0, by0 = 0, binv = 1;
 
     // ---- planner (RRT)
     bool has_rrt = false;
@@ -192,6 +197,14 @@ struct pp_ctx {
         s.lds_cx = lds_cx;
         s.lds_cy = lds_cy;
         s.lds_r2 = lds_r2;
+        s.bits = has_grid ? d_bits.p : nullptr;
+        s.bw = bw;
+        s.bh = bh;
+        s.bwords = bwords;
+        s.bx0 = bx0;
+        s.by0 = by0;
+        s.binv = binv;
+        if (has_grid) s.lds_bytes = lds_bits_bytes;
         return s;
     }
     TreeDev tree_dev() const {
@@ -605,8 +618,31 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
     ctx->height = robot_height;
     ctx->max_steer = max_steer;
     ctx->m = m;
+    ctx->has_grid = false;
     ctx->has_scene = true;
     ctx->has_rrt = false;  // a planner belongs to one Space (RRT::new moves it in, rrt.rs:342)
+    return PP_OK;
+}
+
+int pp_space_set_grid(pp_ctx* ctx, const uint32_t* bits, int w, int h, double x0, double y0,
+                      double cell) {
+    int rc = check_ctx(ctx, true, false);
+    if (rc) return rc;
+    if (!bits || w <= 0 || h <= 0 || w > (1 << 16) || h > (1 << 16) || !(cell > 0.0))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad occupancy grid");
+    const int words = (w + 31) / 32;
+    const size_t n = (size_t)words * h;
+    PP_HIP(ctx->d_bits.reserve(n));
+    PP_HIP(hipMemcpy(ctx->d_bits.p, bits, n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    ctx->bw = w;
+    ctx->bh = h;
+    ctx->bwords = words;
+    ctx->bx0 = x0;
+    ctx->by0 = y0;
+    ctx->binv = 1.0 / cell;
+    ctx->lds_bits_bytes = n * sizeof(uint32_t) <= 64 * 1024 ? (int)(n * sizeof(uint32_t)) : 0;
+    ctx->has_grid = true;
+    ctx->has_rrt = false;  // the planner's Space changed (rrt.rs:342)
     return PP_OK;
 }
 

@@ -320,6 +320,16 @@ __host__ __device__ inline double gen_range(uint64_t seed, uint64_t ctr, double 
     }
 }
 
+// occupancy probe of config 4 (SceneDev::bits): true when the point's cell is occupied or the
+// point lies outside the grid
+__device__ inline bool grid_occupied(const uint32_t* B, int bw, int bh, int bwords, double bx0,
+                                     double by0, double binv, double x, double y) {
+    const double fx = floor((x - bx0) * binv), fy = floor((y - by0) * binv);
+    if (!(fx >= 0.0) || !(fy >= 0.0) || fx >= (double)bw || fy >= (double)bh) return true;
+    const int i = (int)fx, j = (int)fy;
+    return (B[j * bwords + (i >> 5)] >> (i & 31)) & 1u;
+}
+
 // ------------------------------------------------------------------------- wave helpers
 __device__ inline double wave_min(double v) {
 #pragma unroll

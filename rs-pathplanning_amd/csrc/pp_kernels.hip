@@ -46,6 +46,13 @@ extern __shared__ __attribute__((aligned(16))) char pp_smem[];
 
 // Copy the scene's grid and discs into this workgroup's LDS image (all threads call it).
 __device__ inline void stage_scene(const SceneDev& sc) {
+    if (sc.bits) {  // occupancy grid: the bit words only
+        uint32_t* B = reinterpret_cast<uint32_t*>(pp_smem);
+        const int nw = sc.bh * sc.bwords;
+        for (int k = threadIdx.x; k < nw; k += blockDim.x) B[k] = sc.bits[k];
+        __syncthreads();
+        return;
+    }
     const int ncell = sc.gnx * sc.gny + 1;
     const int nitem = sc.goff[ncell - 1];
     int* goff = reinterpret_cast<int*>(pp_smem + sc.lds_goff);
@@ -71,6 +78,12 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const bool oob =
         check_bounds && !(qx >= sc.minx && qx <= sc.maxx && qy >= sc.miny && qy <= sc.maxy);
     if (__any(oob)) return true;
+    if (sc.bits) {  // config 4: every point of the line probes its cell (1 bit), no segments
+        const uint32_t* B = kLds ? reinterpret_cast<const uint32_t*>(pp_smem) : sc.bits;
+        const bool hit = check_bounds && grid_occupied(B, sc.bw, sc.bh, sc.bwords, sc.bx0, sc.by0,
+                                                       sc.binv, qx, qy);
+        return __any(hit);
+    }
     if (sc.m == 0) return false;
     const double ax = __shfl_up(qx, 1);
     const double ay = __shfl_up(qy, 1);
@@ -348,20 +361,26 @@ __device__ int steer_collide_literal(const SceneDev& sc, double x, double y, dou
             const int np = junction ? n + 1 : n;  // the junction point is bounds-checked too
             for (int i = 0; i < np && ok; ++i)
                 ok = bx[i] >= sc.minx && bx[i] <= sc.maxx && by[i] >= sc.miny && by[i] <= sc.maxy;
-            double x0 = bx[0], x1 = bx[0], y0 = by[0], y1 = by[0];
-            for (int i = 1; i < np; ++i) {
-                x0 = fmin(x0, bx[i]);
-                x1 = fmax(x1, bx[i]);
-                y0 = fmin(y0, by[i]);
-                y1 = fmax(y1, by[i]);
-            }
-            for (int k = 0; k < sc.m && ok; ++k) {
-                const double cx = sc.cx[k], cy = sc.cy[k], rc = sc.rcull[k];
-                if (!((cx + rc >= x0) && (cx - rc <= x1) && (cy + rc >= y0) && (cy - rc <= y1)))
-                    continue;
-                for (int i = 0; i + 1 < np && ok; ++i)
-                    if (seg_hits_disc(bx[i], by[i], bx[i + 1], by[i + 1], cx, cy, sc.r2[k]))
-                        ok = false;
+            if (sc.bits) {  // config 4: point probes only
+                for (int i = 0; i < np && ok; ++i)
+                    ok = !grid_occupied(sc.bits, sc.bw, sc.bh, sc.bwords, sc.bx0, sc.by0, sc.binv,
+                                        bx[i], by[i]);
+            } else {
+                double x0 = bx[0], x1 = bx[0], y0 = by[0], y1 = by[0];
+                for (int i = 1; i < np; ++i) {
+                    x0 = fmin(x0, bx[i]);
+                    x1 = fmax(x1, bx[i]);
+                    y0 = fmin(y0, by[i]);
+                    y1 = fmax(y1, by[i]);
+                }
+                for (int k = 0; k < sc.m && ok; ++k) {
+                    const double cx = sc.cx[k], cy = sc.cy[k], rc = sc.rcull[k];
+                    if (!((cx + rc >= x0) && (cx - rc <= x1) && (cy + rc >= y0) && (cy - rc <= y1)))
+                        continue;
+                    for (int i = 0; i + 1 < np && ok; ++i)
+                        if (seg_hits_disc(bx[i], by[i], bx[i + 1], by[i + 1], cx, cy, sc.r2[k]))
+                            ok = false;
+                }
             }
             st = ok ? kAccept : kReject;
         }

@@ -47,9 +47,16 @@ struct SceneDev {
     int gnx, gny;
     const int* goff;    // [gnx * gny + 1]
     const int* gitems;  // disc indices
-    // LDS image of (goff, gitems, cx, cy, r2) staged by the steer kernels when it fits
+    // LDS image of (goff, gitems, cx, cy, r2) — or of the occupancy bits — staged by the steer
+    // kernels when it fits
     int lds_bytes;  // 0: read the scene from global memory
     int lds_goff, lds_items, lds_cx, lds_cy, lds_r2;  // byte offsets inside the image
+    // occupancy grid (BASELINE config 4): when bits != nullptr the discs are ignored and every
+    // polyline point probes its cell: (i, j) = (floor((x - bx0) * binv), floor((y - by0) * binv)),
+    // bit i % 32 of word j * bwords + i / 32; a point outside the grid counts as occupied
+    const uint32_t* bits;
+    int bw, bh, bwords;
+    double bx0, by0, binv;
 };
 
 // Tree in device memory: f32 SoA for the NN screen, f64 SoA for everything exact.

@@ -33,7 +33,8 @@ _ERR_NAMES = {
 EXPORTED = [
     "pp_abi_version", "pp_last_error", "pp_device_count", "pp_create", "pp_destroy",
     "pp_synchronize", "pp_rng_u64", "pp_gen_range", "pp_mod2pi", "pp_pi_2_pi",
-    "pp_dubins_path_planning_batch", "pp_space_new", "pp_space_get_bounds", "pp_rrt_new",
+    "pp_dubins_path_planning_batch", "pp_space_new", "pp_space_set_grid", "pp_space_get_bounds",
+    "pp_rrt_new",
     "pp_rrt_set_window", "pp_rrt_extend", "pp_rrt_plan_one", "pp_rrt_tree_size",
     "pp_rrt_iteration", "pp_rrt_tree_export", "pp_rrt_get_nearest_node_batch",
     "pp_rrt_verify_node_batch", "pp_rrt_check_finish_batch", "pp_rrt_check_finish",
@@ -98,6 +99,8 @@ def lib():
             "pp_dubins_path_planning_batch": (
                 [vp, C.POINTER(DubinsConfigC), C.c_int, C.c_int, dp, dp, dp, ip, ip, dp], C.c_int),
             "pp_space_new": ([vp] + [C.c_double] * 7 + [dp, dp, dp, C.c_int], C.c_int),
+            "pp_space_set_grid": ([vp, C.POINTER(C.c_uint32), C.c_int, C.c_int, C.c_double,
+                                   C.c_double, C.c_double], C.c_int),
             "pp_space_get_bounds": ([vp, dp], C.c_int),
             "pp_rrt_new": ([vp] + [C.c_double] * 6 + [C.c_int64, C.c_double, C.c_uint64, C.c_int64],
                            C.c_int),

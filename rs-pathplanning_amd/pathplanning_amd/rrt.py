@@ -56,9 +56,14 @@ def _rect_of(bounds):
 
 
 class Space:  # rrt.rs:70-159
-    def __init__(self, bounds, robot: Robot, obstacle_list):
+    """``Space::new(bounds, robot, obstacles)``.  ``grid`` (config 4, build-defined): an occupancy
+    grid ``(bits uint32[h, ceil(w/32)], w, x0, y0, cell)`` that replaces the discs — every point
+    of a line must lie in a free cell (pp_space_set_grid)."""
+
+    def __init__(self, bounds, robot: Robot, obstacle_list, grid=None):
         self.raw_bounds = _rect_of(bounds)
         self.robot = robot
+        self.grid = grid
         obs = list(obstacle_list)
         self.circles = np.array([[o.cx, o.cy, o.r] for o in obs], dtype=np.float64).reshape(-1, 3)
         half = robot.get_width() / 2.0  # rrt.rs:82
@@ -68,7 +73,8 @@ class Space:  # rrt.rs:70-159
     @classmethod
     def from_raw(cls, raw: dict) -> "Space":
         return cls(raw["bounds"], Robot(*raw["robot"]),
-                   [create_circle((c[0], c[1]), c[2]) for c in raw["circles"]])
+                   [create_circle((c[0], c[1]), c[2]) for c in raw["circles"]],
+                   grid=raw.get("grid"))
 
     def get_steer(self) -> float:
         return self.robot.get_steer()
@@ -93,6 +99,12 @@ class Space:  # rrt.rs:70-159
             ctx.handle, x0, y0, x1, y1, self.robot.width, self.robot.height,
             self.robot.max_steer, cx.ctypes.data_as(dp), cy.ctypes.data_as(dp),
             r.ctypes.data_as(dp), len(cx)))
+        if self.grid is not None:
+            bits, w, gx0, gy0, cell = self.grid
+            bits = np.ascontiguousarray(bits, dtype=np.uint32)
+            _ffi.check(_ffi.lib().pp_space_set_grid(
+                ctx.handle, bits.ctypes.data_as(C.POINTER(C.c_uint32)), int(w), bits.shape[0],
+                float(gx0), float(gy0), float(cell)))
 
 
 @dataclass

@@ -161,3 +161,38 @@ def config3_queries(raw: dict, first: int, count: int, seed_base: int = 42):
         starts[i], goals[i] = poses
     seeds = np.arange(first, first + count, dtype=np.uint64) + np.uint64(seed_base)
     return starts, goals, seeds
+
+
+def rasterize(raw: dict, w: int = 512, h: int = 512, x0: float = 0.0, y0: float = 0.0,
+              cell: float = 1.0):
+    """BASELINE config 4: the scene's discs rasterised into a w x h grid — cell (i, j) occupied
+    when its centre (x0 + (i + 0.5) cell, y0 + (j + 0.5) cell) lies inside an inflated disc
+    (dx*dx + dy*dy <= (r + width/2)^2) — bit-packed as uint32[h, ceil(w/32)], bit i % 32 of word
+    i // 32.  Returns (bits, w, x0, y0, cell)."""
+    half = raw["robot"][0] / 2.0
+    circ = np.asarray(raw["circles"], dtype=np.float64).reshape(-1, 3)
+    xs = x0 + (np.arange(w) + 0.5) * cell
+    ys = y0 + (np.arange(h) + 0.5) * cell
+    occ = np.zeros((h, w), dtype=bool)
+    for cx, cy, r in circ:
+        reff = r + half
+        ix = np.nonzero(np.abs(xs - cx) <= reff + cell)[0]
+        iy = np.nonzero(np.abs(ys - cy) <= reff + cell)[0]
+        if len(ix) == 0 or len(iy) == 0:
+            continue
+        dx = xs[ix][None, :] - cx
+        dy = ys[iy][:, None] - cy
+        occ[np.ix_(iy, ix)] |= dx * dx + dy * dy <= reff * reff
+    words = (w + 31) // 32
+    padded = np.zeros((h, words * 32), dtype=bool)
+    padded[:, :w] = occ
+    bits = np.packbits(padded.reshape(h, words, 32)[:, :, ::-1], axis=2).view(">u4")
+    return bits.reshape(h, words).astype(np.uint32), w, x0, y0, cell
+
+
+def field512_grid() -> dict:
+    """BASELINE config 4: field512 with its discs replaced by the 512 x 512 unit-cell raster."""
+    raw = field512()
+    raw["name"] = "field512_grid"
+    raw["grid"] = rasterize(raw)
+    return raw

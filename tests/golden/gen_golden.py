@@ -122,6 +122,11 @@ def main():
     field = scenes.field512()
     with open(os.path.join(HERE, "rrt_field512.json"), "w") as f:
         json.dump([rrt_record(field, 42, 1200)], f)
+    grid = scenes.field512_grid()
+    g = rrt_record(grid, 42, 6000)
+    with open(os.path.join(HERE, "rrt_field512_grid.json"), "w") as f:
+        json.dump([g], f)
+    print("field512_grid nodes:", len(g["x"]))
     fin = [finish_record(scenes.bench6_open(), s, 600) for s in (0, 1)]
     with open(os.path.join(HERE, "finish_bench6_open.json"), "w") as f:
         json.dump(fin, f)
