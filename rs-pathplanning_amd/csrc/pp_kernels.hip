@@ -22,7 +22,7 @@
 
 namespace ppamd {
 
-#ifdef PP_STAMPS
+#if defined(PP_STAMPS) || defined(PP_STAMPS_RESOLVE)
 #define PP_STAMP(var) const int64_t var = (int64_t)__builtin_amdgcn_s_memrealtime()
 #else
 #define PP_STAMP(var)
