@@ -145,6 +145,27 @@ def cpu_baseline(raw, p, args):
     return out
 
 
+def cpu_baseline_queries(raw, starts, seeds, max_iter, seconds):
+    """config 3's CPU baseline: the oracle (C, one core) runs whole queries of the same batch —
+    query q from its own start with its own seed, max_iter iterations each, the reference's full
+    re-verify of the line to the root (rrt.rs:414-426) — until `seconds` of CPU time are used."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (cpu_baseline leg: the oracle is the timed CPU port here)
+
+    sc = oracle.OracleScene.from_raw(raw)
+    done, t_used, nq = 0, 0.0, 0
+    for q in range(len(seeds)):
+        tr = oracle.OracleTree(tuple(starts[q]), max_iter + 1)
+        t0 = time.perf_counter()
+        oracle.rrt_extend(sc, tr, int(seeds[q]), 0, max_iter, full_reverify=True)
+        t_used += time.perf_counter() - t0
+        done += max_iter
+        nq += 1
+        if t_used >= seconds:
+            break
+    return done / t_used, done, nq, t_used
+
+
 def load_traffic():
     """HBM bytes per nn_scan launch from the committed rocprofv3 PMC summary (or None)."""
     path = os.path.join(ROOT, "profiles", "nn_scan_traffic.json")
@@ -387,6 +408,14 @@ def main_config3(args):
         },
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        v, n, nq, t = cpu_baseline_queries(raw, starts, seeds, args.max_iter, args.cpu_seconds)
+        line["cpu_baseline"] = {
+            "value": round(v, 2), "unit": "iterations/s", "cores": 1, "kind": "port",
+            "sample": f"{nq} whole queries of the same batch ({n} iterations, max_iter "
+                      f"{args.max_iter} each, full re-verify like rrt.rs:414-426), {t:.1f} s on "
+                      "1 host core",
+        }
     if rank == 0:
         print(json.dumps(line), flush=True)
     batch.close()

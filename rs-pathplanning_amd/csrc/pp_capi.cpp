@@ -115,6 +115,7 @@ struct pp_ctx {
     double step = 0.1;
     uint64_t seed = 0;
     int64_t it = 0;   // mirror of DevState.it (exact after every synchronisation)
+    int64_t seq = 0;  // windows enqueued so far (their sequence numbers)
     int64_t n = 0;    // mirror of DevState.n
     int64_t cap = 0;  // tree capacity
     double eps_coord = 0.0;
@@ -133,7 +134,7 @@ struct pp_ctx {
     DBuf<CandEntry> cand;
     DBuf<PrepRec> rec;   // per-task steer records
     DBuf<double> pdbuf;  // per-task grid-point distances (kPdCap per task)
-    DBuf<int> r_order, r_rep;
+    DBuf<int> r_order, r_rep, pend, fin_par;
     DBuf<double> r_repyaw;
     DBuf<double> lit_scratch;  // resolve: one literal buffer per wave
     // verify_node API
@@ -220,6 +221,7 @@ struct pp_ctx {
     WindowArgs window_args(DevState* st) const {
         WindowArgs a;
         a.K = Kcap;
+        a.Kcap = Kcap;
         a.seed = seed;
         a.eps_coord = eps_coord;
         a.st = st;
@@ -243,6 +245,8 @@ struct pp_ctx {
         a.snap_pose = snap_pose.p;
         a.rec = rec.p;
         a.pdbuf = pdbuf.p;
+        a.pend = pend.p;
+        a.fin_par = fin_par.p;
         a.rs.order = r_order.p;
         a.rs.rep = r_rep.p;
         a.rs.repyaw = r_repyaw.p;
@@ -267,8 +271,8 @@ int ensure_window(pp_ctx* c, int K) {
     K = (K + 255) & ~255;
     if (K <= c->Kcap) return PP_OK;
     const size_t k = (size_t)K;
-    PP_HIP(c->wsx.reserve(k));
-    PP_HIP(c->wsy.reserve(k));
+    PP_HIP(c->wsx.reserve(2 * k));  // double-buffered by window parity
+    PP_HIP(c->wsy.reserve(2 * k));
     PP_HIP(c->pbest.reserve(k * kMaxChunks));
     PP_HIP(c->psecond.reserve(k * kMaxChunks));
     PP_HIP(c->pidx.reserve(k * kMaxChunks));
@@ -288,6 +292,9 @@ int ensure_window(pp_ctx* c, int K) {
     PP_HIP(c->snap_pose.reserve(3 * k));
     PP_HIP(c->r_order.reserve(k * kCandCap));
     PP_HIP(c->r_rep.reserve(k));
+    PP_HIP(c->pend.reserve(k));
+    PP_HIP(c->fin_par.reserve(k));
+    PP_HIP(hipMemsetAsync(c->cand_cnt.p, 0, k * sizeof(int), c->stream));
     PP_HIP(c->r_repyaw.reserve(k));
     PP_HIP(c->tasks.reserve(k));
     PP_HIP(c->task_status.reserve(k));
@@ -696,6 +703,9 @@ int pp_rrt_new(pp_ctx* ctx, double sx, double sy, double syaw, double gx, double
     DevState s{};
     s.it = 0;
     s.n = 1;
+    s.n_scan = 1;
+    s.it_spec = 0;
+    s.void_seq = -1;
     PP_HIP(hipMemcpy(ctx->d_state.p, &s, sizeof(DevState), hipMemcpyHostToDevice));
     ctx->h_state.p[0] = s;
     ctx->n = 1;
@@ -729,8 +739,11 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
         a.target = target;
         if (ctx->prof && (r = ensure_events(ctx, 4 * (size_t)nw))) return r;
         const int64_t windows_before = ctx->h_state.p[0].windows;
+        // windows are pipelined: window w's kernel resolves and commits w - 1; the drain launch
+        // commits the batch's last window before the host reads the state
         for (int w = 0; w < nw; ++w)
-            PP_HIP(launch_window(st, a, ctx->prof ? &ctx->ev[4 * w] : nullptr));
+            PP_HIP(launch_window(st, a, ctx->prof ? &ctx->ev[4 * w] : nullptr, ctx->seq++, w > 0));
+        PP_HIP(launch_drain(st, a, ctx->seq));
         PP_HIP(hipMemcpyAsync(ctx->h_state.p, ctx->d_state.p, sizeof(DevState), hipMemcpyDeviceToHost, st));
         PP_HIP(hipStreamSynchronize(st));
         const DevState& s = ctx->h_state.p[0];
@@ -810,7 +823,11 @@ int pp_rrt_get_nearest_node_batch(pp_ctx* ctx, const double* qx, const double* q
         DevState* hs = &ctx->h_state.p[1];
         *hs = DevState{};
         hs->W = nb;
+        hs->Wp[0] = nb;
         hs->n = (int)ctx->n;
+        hs->nsp[0] = (int)ctx->n;
+        hs->n_scan = (int)ctx->n;
+        hs->void_seq = -1;
         PP_HIP(hipMemcpyAsync(ctx->d_api_state.p, hs, sizeof(DevState), hipMemcpyHostToDevice, st));
         PP_HIP(hipMemcpyAsync(ctx->wsx.p, qx + b, nb * sizeof(double), hipMemcpyHostToDevice, st));
         PP_HIP(hipMemcpyAsync(ctx->wsy.p, qy + b, nb * sizeof(double), hipMemcpyHostToDevice, st));

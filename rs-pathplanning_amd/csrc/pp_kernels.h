@@ -9,14 +9,15 @@ namespace ppamd {
 
 // Everything one window (or one nearest-neighbour batch) touches.  Buffers are sized for K.
 struct WindowArgs {
-    int K = 0;
+    int K = 0;           // samples per window
+    int Kcap = 0;        // buffer capacity per window (parity stride of wsx / wsy)
     int64_t target = 0;  // iteration the enqueued windows stop at
     uint64_t seed = 0;
     double eps_coord = 0.0;
     DevState* st = nullptr;
     SceneDev sc{};
     TreeDev tr{};
-    double* wsx = nullptr;
+    double* wsx = nullptr;        // [2 * Kcap] samples, double-buffered by window parity
     double* wsy = nullptr;
     float* pbest = nullptr;
     float* psecond = nullptr;
@@ -34,15 +35,22 @@ struct WindowArgs {
     double* snap_pose = nullptr;  // [3K] parent pose of each unflagged sample (nn_finalize)
     PrepRec* rec = nullptr;       // [K + K * kCandCap] per-task steer records
     double* pdbuf = nullptr;      // [(K + K * kCandCap) * kPdCap] grid-point distances
+    int* pend = nullptr;          // [K] samples queued for the resolve's round passes
+    int* fin_par = nullptr;       // [K] window parent of a resolved sample (kWinParent)
     ResolveScratch rs{};
     double* lit_scratch = nullptr;
 };
 
-// Enqueue one window on stream s.  ev (optional) = 4 timing events: around nn_scan and around
-// the steer (prep + walk) of all the window's tasks.
-hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev);
+// Enqueue window number `seq` on stream s: its window kernel also resolves and commits window
+// seq - 1 when resolve_prev (the previous window of the same batch).  ev (optional) = 4 timing
+// events: around the window kernel (the NN screen) and around the steer (prep + walk).
+hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int64_t seq,
+                         int resolve_prev);
+// Resolve and commit the last enqueued window (seq_next - 1): ends a batch.
+hipError_t launch_drain(hipStream_t s, const WindowArgs& a, int64_t seq_next);
 
-// Exact nearest tree node of st->W samples (wsx, wsy): nn_scan + finalize + rescan + fix.
+// Exact nearest tree node of Wp[0] samples (wsx, wsy parity 0; nsp[0] = n): screen + finalize +
+// rescan.
 hipError_t launch_nearest(hipStream_t s, const WindowArgs& a);
 
 hipError_t launch_steer_tasks(hipStream_t st, const SceneDev& sc, const TreeDev& tr,

@@ -449,46 +449,36 @@ __global__ __launch_bounds__(64) void dubins_batch_kernel(const double* __restri
 
 // ------------------------------------------------------------------------- window pipeline
 //
-// One speculative window = window_begin → nn_scan → nn_finalize → nn_rescan → window_pairs →
-// steer_window → resolve, all reading the device-resident DevState, so the host enqueues windows
-// back to back and synchronises once per batch.
+// One speculative window w = window_kernel (w's NN screen ‖ resolve + commit of w - 1) →
+// nn_finalize → nn_rescan → window_pairs → steer_prep → steer_walk; window w's resolve and commit
+// run inside window w + 1's window_kernel (or the batch's drain launch).  Everything reads the
+// device-resident DevState, so the host enqueues windows back to back and synchronises once per
+// batch.
 
-constexpr int kQPL = 4;          // samples per lane in nn_scan
-constexpr int kQPB = 64 * kQPL;  // samples per nn_scan workgroup (all 4 waves share them)
+constexpr int kQPL = 4;                          // samples per lane in the screen
+constexpr int kQPB = 64 * kQPL;                  // samples per screen workgroup (its waves share them)
+constexpr int kScanThreads = 1024;               // window_kernel workgroup (16 waves)
+constexpr int kScanWaves = kScanThreads / 64;
+constexpr int kScanBlk = 16;                     // nodes per scalar-load block
+constexpr int kScanGrid = 240;                   // screen workgroups per window (one per CU, with
+                                                 // the resolve workgroup: 241 <= 256 CUs)
 
-__host__ __device__ inline int nn_chunk_len(int n) {
-    int cl = (n + kMaxChunks - 1) / kMaxChunks;
-    if (cl < 512) cl = 512;
-    return (cl + 31) & ~31;
+// node chunks of the screen for a window of K samples: the nqb sample blocks x chunks workgroups
+// fill kScanGrid; every chunk is a whole number of kScanBlk blocks
+__host__ __device__ inline int scan_chunks(int K) {
+    const int nqb = (K + kQPB - 1) / kQPB;
+    int c = kScanGrid / nqb;
+    if (c > kMaxChunks) c = kMaxChunks;
+    return c < 1 ? 1 : c;
 }
-__host__ __device__ inline int nn_chunks(int n) {
-    const int cl = nn_chunk_len(n);
+__host__ __device__ inline int scan_chunk_len(int n, int chunks) {
+    int cl = (n + chunks - 1) / chunks;
+    if (cl < kScanWaves * kScanBlk) cl = kScanWaves * kScanBlk;
+    return (cl + kScanBlk - 1) & ~(kScanBlk - 1);
+}
+__host__ __device__ inline int scan_chunks_used(int n, int chunks) {
+    const int cl = scan_chunk_len(n, chunks);
     return (n + cl - 1) / cl;
-}
-
-// Space::rand_point for iterations [it, it + W) of the window (rrt.rs:139-146, seeded: Q7):
-// x = draw 2*it, y = draw 2*it + 1.  Also opens the window: W = min(K, target - it).
-__global__ __launch_bounds__(256) void window_begin_kernel(DevState* st, int K, int64_t target,
-                                                           uint64_t seed,
-                                                           double minx, double maxx, double miny,
-                                                           double maxy, double* __restrict__ wsx,
-                                                           double* __restrict__ wsy,
-                                                           int* __restrict__ cand_cnt) {
-    const int64_t it = st->it;
-    const int64_t rem = target - it;
-    const int W = (rem <= 0 || st->error) ? 0 : (rem < K ? (int)rem : K);
-    const int j = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (j == 0) {
-        st->W = W;
-        st->flag_count = 0;
-        st->ncomp = 0;
-    }
-    if (j < W) {
-        const uint64_t itj = (uint64_t)(it + j);
-        wsx[j] = gen_range(seed, 2 * itj, minx, maxx);
-        wsy[j] = gen_range(seed, 2 * itj + 1, miny, maxy);
-        cand_cnt[j] = 0;
-    }
 }
 
 struct Top2 {
@@ -511,59 +501,119 @@ __device__ inline Top2 merge_top2(Top2 a, Top2 c) {
     return r;
 }
 
-// RRT::get_nearest_node screen (rrt.rs:378-391): f32 SoA nodes x W samples.  Grid = nqb * 64
-// blocks (nqb sample blocks x 64 node chunks), mapped XCD-aware so the nqb blocks that stream the
-// same node chunk share one XCD's L2.  Each wave scans a quarter of the chunk with node
-// coordinates as wave-uniform scalar loads (double-buffered one block ahead); every lane holds 4
-// samples.  Per block of kScanBlk nodes each sample keeps only the block minimum (v_min3: half an
-// op per eval on top of sub, sub, mul, fma), then merges it into (best, second) with med3 and
-// records the block
-// that first attained the best.  The winning block is re-evaluated afterwards with the same
-// arithmetic (bit-identical distances) for the lowest index and the in-block second best, so the
-// result is the exact per-chunk top-2 of the f32 distances, as before.
-constexpr int kScanBlk = 16;
-
 __device__ __forceinline__ float scan_d2(float qx, float qy, float nx, float ny) {
     const float dx = qx - nx, dy = qy - ny;
     return __builtin_fmaf(dy, dy, dx * dx);
 }
 
-__global__ __launch_bounds__(256) void nn_scan_kernel(const DevState* __restrict__ st,
-                                                      const float* __restrict__ nx,
-                                                      const float* __restrict__ ny,
-                                                      const double* __restrict__ qx,
-                                                      const double* __restrict__ qy, int nqb,
-                                                      int stride, float* __restrict__ pbest,
-                                                      float* __restrict__ psecond,
-                                                      int* __restrict__ pidx) {
-    __shared__ float s_b[4][kQPB];
-    __shared__ float s_s[4][kQPB];
-    __shared__ int s_i[4][kQPB];
-    const int W = st->W, n = st->n;
-    const int G = gridDim.x;  // multiple of 8 (kMaxChunks chunks per sample block)
-    const int b = blockIdx.x;
-    const int t = (b & 7) * (G >> 3) + (b >> 3);
-    const int qb = t % nqb, c = t / nqb;
-    const int chunk_len = nn_chunk_len(n);
-    const int c0 = c * chunk_len;
-    if (c0 >= n || qb * kQPB >= W) return;
-    const int c1 = min(c0 + chunk_len, n);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// Arguments of the window kernel.  Sample buffers are double-buffered by window parity: the
+// screen of window w writes wsx/wsy[p], the resolve of w - 1 reads [1 - p].
+struct WinKArgs {
+    DevState* st;
+    SceneDev sc;
+    TreeDev tr;
+    int K;              // samples per window
+    int Kcap;           // buffer capacity per window (stride of the partials)
+    int nqb, chunks;    // screen geometry (scan_chunks)
+    int p;              // parity of the screened window
+    int gen;            // 1: generate the window's samples (RNG); 0: screen the given wsx/wsy[p]
+    int resolve;        // 1: workgroup 0 resolves + commits the previous window
+    int scan;           // 0: the drain launch (resolve only)
+    int64_t seq;        // sequence number of the screened window
+    int64_t target;     // iteration the enqueued windows stop at
+    uint64_t seed;
+    double* wsx[2];
+    double* wsy[2];
+    float* pbest;
+    float* psecond;
+    int* pidx;
+    // resolve + commit of the previous window (parity 1 - p)
+    const int* nn_idx;
+    int* cand_cnt;
+    const CandEntry* cand;
+    const int* pend;
+    int* snap_status;
+    double* snap_yaw;
+    int* fin_par;
+    ResolveScratch rs;
+    double* lit_scratch;
+};
+
+// RRT::get_nearest_node screen (rrt.rs:378-391): f32 SoA nodes x the window's samples.  The
+// screen workgroup b of kScanGrid (mapped XCD-aware, so the sample blocks that stream one node
+// chunk share an XCD's L2) takes sample block qb and node chunk c.  Its 16 waves split the
+// chunk; every lane holds 4 samples; node coordinates are wave-uniform scalar loads (double-
+// buffered one block ahead) used directly as SGPR operands.  Per block of kScanBlk nodes each
+// sample keeps only the block minimum (v_min3: half an op per eval on top of sub, sub, mul, fma),
+// merges it into (best, second) with med3 and records the block that first attained the best;
+// the winning block is re-evaluated afterwards with the same arithmetic (bit-identical) for the
+// lowest index and the in-block second best.  Result: the exact per-chunk top-2 of the f32
+// distances.  In generating mode the samples come from the counter RNG (Space::rand_point,
+// rrt.rs:139-146, seeded: Q7: x = draw 2*it, y = draw 2*it + 1) for iterations
+// [it_spec, it_spec + W), W = min(K, target - it_spec), and the chunk-0 workgroups store them.
+__device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& a, int b,
+                                                               char* smem) {
+    DevState* st = a.st;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int W, ns;
+    int64_t start = 0;
+    if (a.gen) {
+        start = st->it_spec;
+        const int64_t rem = a.target - start;
+        W = (rem <= 0 || st->error) ? 0 : (rem < a.K ? (int)rem : a.K);
+        ns = st->n_scan;
+        if (b == 0 && tid == 0) {
+            st->Wp[a.p] = W;
+            st->wsp[a.p] = start;
+            st->nsp[a.p] = ns;
+        }
+    } else {
+        W = st->Wp[a.p];
+        ns = st->nsp[a.p];
+    }
+    const int G = a.nqb * a.chunks;
+    if (b >= G) return;
+    const int t = (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b;
+    const int qb = t % a.nqb, c = t / a.nqb;
     const int qbase = qb * kQPB;
+    if (qbase >= W) return;
+    const int cl = scan_chunk_len(ns, a.chunks);
+    const int c0 = c * cl;
+    if (c0 >= ns) return;
+    const int c1 = min(c0 + cl, ns);
+    double* qxo = a.wsx[a.p];
+    double* qyo = a.wsy[a.p];
     float qxr[kQPL], qyr[kQPL], best[kQPL], second[kQPL];
     int blk[kQPL], bi[kQPL];
 #pragma unroll
     for (int r = 0; r < kQPL; ++r) {
         const int q = qbase + r * 64 + lane;
-        qxr[r] = q < W ? (float)qx[q] : 0.0f;
-        qyr[r] = q < W ? (float)qy[q] : 0.0f;
+        double x = 0.0, y = 0.0;
+        if (q < W) {
+            if (a.gen) {
+                const uint64_t itq = (uint64_t)(start + q);
+                x = gen_range(a.seed, 2 * itq, a.sc.minx, a.sc.maxx);
+                y = gen_range(a.seed, 2 * itq + 1, a.sc.miny, a.sc.maxy);
+                if (c == 0 && wave == 0) {
+                    qxo[q] = x;
+                    qyo[q] = y;
+                }
+            } else {
+                x = qxo[q];
+                y = qyo[q];
+            }
+        }
+        qxr[r] = (float)x;
+        qyr[r] = (float)y;
         best[r] = __builtin_inff();
         second[r] = __builtin_inff();
         blk[r] = -1;
         bi[r] = -1;
     }
+    const float* nx = a.tr.x32;
+    const float* ny = a.tr.y32;
     // wave-uniform range (kScanBlk-aligned start): readfirstlane lets the compiler use scalar loads
-    const int per = (((c1 - c0) + 3) / 4 + kScanBlk - 1) & ~(kScanBlk - 1);
+    const int per = (((c1 - c0) + kScanWaves - 1) / kScanWaves + kScanBlk - 1) & ~(kScanBlk - 1);
     const int w0 = __builtin_amdgcn_readfirstlane(min(c0 + wave * per, c1));
     const int w1 = __builtin_amdgcn_readfirstlane(min(w0 + per, c1));
     const int wb = w0 + ((w1 - w0) / kScanBlk) * kScanBlk;  // end of the whole blocks
@@ -605,8 +655,8 @@ __global__ __launch_bounds__(256) void nn_scan_kernel(const DevState* __restrict
                 }
             }
         }
-        // the winning block again, scalar and bit-identical: lowest index of the best distance
-        // and the best of the block's other nodes (the block minima only carried one each)
+        // the winning block again, bit-identical: lowest index of the best distance and the best
+        // of the block's other nodes (the block minima only carried one each)
 #pragma unroll
         for (int r = 0; r < kQPL; ++r) {
             if (blk[r] < 0) continue;
@@ -651,54 +701,76 @@ __global__ __launch_bounds__(256) void nn_scan_kernel(const DevState* __restrict
             }
         }
     }
+    float* s_b = reinterpret_cast<float*>(smem);              // [kScanWaves][kQPB]
+    float* s_s = s_b + kScanWaves * kQPB;
+    int* s_i = reinterpret_cast<int*>(s_s + kScanWaves * kQPB);
 #pragma unroll
     for (int r = 0; r < kQPL; ++r) {
-        s_b[wave][r * 64 + lane] = best[r];
-        s_s[wave][r * 64 + lane] = second[r];
-        s_i[wave][r * 64 + lane] = bi[r];
+        s_b[wave * kQPB + r * 64 + lane] = best[r];
+        s_s[wave * kQPB + r * 64 + lane] = second[r];
+        s_i[wave * kQPB + r * 64 + lane] = bi[r];
     }
     __syncthreads();
-    const int slot = wave * 64 + lane;  // wave w merges sample group r = w across the 4 waves
-    Top2 tt{s_b[0][slot], s_s[0][slot], s_i[0][slot]};
+    if (tid < kQPB) {  // one thread per sample merges the waves' partials
+        Top2 tt{s_b[tid], s_s[tid], s_i[tid]};
 #pragma unroll
-    for (int w = 1; w < 4; ++w) tt = merge_top2(tt, Top2{s_b[w][slot], s_s[w][slot], s_i[w][slot]});
-    const int q = qbase + slot;
-    if (q < W) {
-        const size_t o = (size_t)c * stride + q;
-        pbest[o] = tt.b;
-        psecond[o] = tt.s;
-        pidx[o] = tt.i;
+        for (int w = 1; w < kScanWaves; ++w)
+            tt = merge_top2(tt, Top2{s_b[w * kQPB + tid], s_s[w * kQPB + tid], s_i[w * kQPB + tid]});
+        const int q = qbase + tid;
+        if (q < W) {
+            const size_t o = (size_t)c * a.Kcap + q;
+            a.pbest[o] = tt.b;
+            a.psecond[o] = tt.s;
+            a.pidx[o] = tt.i;
+        }
     }
 }
 
-// 64 samples per workgroup: wave w merges chunks w, w+4, ... for its lane's sample, then wave 0
-// merges the 4 and decides whether the f32 winner is certainly the exact f64 winner (margin test
-// against the f32 rounding bound).  Certain: exact f64 d2 of the winner.  Else: queue for the
-// exact rescan, nn_idx = -(slot + 1).
-__global__ __launch_bounds__(256) void nn_finalize_kernel(
-    DevState* __restrict__ st, const float* __restrict__ pbest, const float* __restrict__ psecond,
-    const int* __restrict__ pidx, int stride, const double* __restrict__ qx,
-    const double* __restrict__ qy, const double* __restrict__ X, const double* __restrict__ Y,
+// 64 samples per workgroup of 16 waves: wave w merges the screen chunks w, w+16, ... for its
+// lane's sample and screens its share of the nodes the window's screen did not cover — the ones
+// appended since (the previous window's commit) — with the same f32 arithmetic and scalar node
+// loads; then wave 0 merges the 16 and decides whether the f32 winner is certainly the exact f64
+// winner (margin test against the f32 rounding bound).  Certain: exact f64 d2 of the winner.
+// Else: queue for the exact rescan, nn_idx = -(slot + 1).  Workgroup 0 also publishes the window
+// (W, or 0 when a truncated predecessor voided it) for the later kernels and advances the next
+// window's screen position.
+constexpr int kFinThreads = 1024;
+constexpr int kFinWaves = kFinThreads / 64;
+__global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
+    DevState* __restrict__ st, int p, int64_t seq, int chunks, const float* __restrict__ pbest,
+    const float* __restrict__ psecond, const int* __restrict__ pidx, int stride,
+    const double* __restrict__ qx, const double* __restrict__ qy, const float* __restrict__ x32,
+    const float* __restrict__ y32, const double* __restrict__ X, const double* __restrict__ Y,
     const double* __restrict__ YAW, double eps_coord, int* __restrict__ out_idx,
     double* __restrict__ out_d2, double* __restrict__ out_pose, int* __restrict__ flag_list) {
-    __shared__ float s_b[4][64];
-    __shared__ float s_s[4][64];
-    __shared__ int s_i[4][64];
-    const int W = st->W, n = st->n;
+    __shared__ float s_b[kFinWaves][64];
+    __shared__ float s_s[kFinWaves][64];
+    __shared__ int s_i[kFinWaves][64];
+    const bool voided = st->void_seq == seq || st->error;
+    const int W = voided ? 0 : st->Wp[p];
+    const int ns = st->nsp[p], n = st->n;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->W = W;
+        st->weff = W;
+        st->n_scan = n;
+        if (!voided) st->it_spec = st->wsp[p] + W;
+    }
     if ((int)blockIdx.x * 64 >= W) return;
-    const int n_chunks = nn_chunks(n);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n_chunks = scan_chunks_used(ns, chunks);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int q = blockIdx.x * 64 + lane;
+    const bool in = q < W;
     Top2 t{__builtin_inff(), __builtin_inff(), -1};
-    if (q < W) {
-        constexpr int kPer = kMaxChunks / 4;
+    {
+        constexpr int kPer = (kMaxChunks + kFinWaves - 1) / kFinWaves;
         float vb[kPer], vs[kPer];
         int vi[kPer];
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {  // all loads in flight before the merge
-            const int c = wave + 4 * u;
+            const int c = wave + kFinWaves * u;
             const size_t o = (size_t)c * stride + q;
-            const bool ok = c < n_chunks;
+            const bool ok = in && c < n_chunks;
             vb[u] = ok ? pbest[o] : __builtin_inff();
             vs[u] = ok ? psecond[o] : __builtin_inff();
             vi[u] = ok ? pidx[o] : -1;
@@ -706,13 +778,48 @@ __global__ __launch_bounds__(256) void nn_finalize_kernel(
 #pragma unroll
         for (int u = 0; u < kPer; ++u) t = merge_top2(t, Top2{vb[u], vs[u], vi[u]});
     }
+    // nodes appended after the screen's snapshot: wave w takes a contiguous share, scalar loads
+    // in blocks of kScanBlk, exact top-2 per node (same f32 arithmetic as the screen)
+    const float fx = in ? (float)qx[q] : 0.0f, fy = in ? (float)qy[q] : 0.0f;
+    const int D = n - ns;
+    if (D > 0) {
+        const int per = ((D + kFinWaves - 1) / kFinWaves + kScanBlk - 1) & ~(kScanBlk - 1);
+        const int k0 = min(ns + wave * per, n), k1 = min(k0 + per, n);
+        int k = k0;
+        for (; k + kScanBlk <= k1; k += kScanBlk) {
+            float cx[kScanBlk], cy[kScanBlk];
+#pragma unroll
+            for (int u = 0; u < kScanBlk; ++u) {
+                cx[u] = x32[k + u];
+                cy[u] = y32[k + u];
+            }
+#pragma unroll
+            for (int u = 0; u < kScanBlk; ++u) {
+                const float d = scan_d2(fx, fy, cx[u], cy[u]);
+                t.s = __builtin_amdgcn_fmed3f(t.b, d, t.s);
+                if (d < t.b) {
+                    t.b = d;
+                    t.i = k + u;
+                }
+            }
+        }
+        for (; k < k1; ++k) {
+            const float d = scan_d2(fx, fy, x32[k], y32[k]);
+            t.s = __builtin_amdgcn_fmed3f(t.b, d, t.s);
+            if (d < t.b) {
+                t.b = d;
+                t.i = k;
+            }
+        }
+    }
     s_b[wave][lane] = t.b;
     s_s[wave][lane] = t.s;
     s_i[wave][lane] = t.i;
     __syncthreads();
-    if (wave != 0 || q >= W) return;
+    if (wave != 0 || !in) return;
 #pragma unroll
-    for (int w = 1; w < 4; ++w) t = merge_top2(t, Top2{s_b[w][lane], s_s[w][lane], s_i[w][lane]});
+    for (int w = 1; w < kFinWaves; ++w)
+        t = merge_top2(t, Top2{s_b[w][lane], s_s[w][lane], s_i[w][lane]});
     bool flag = t.i < 0 || !(t.b < __builtin_inff());
     if (!flag && t.s < __builtin_inff()) {
         const double D1 = sqrt((double)t.b), D2 = sqrt((double)t.s);
@@ -824,7 +931,8 @@ __global__ __launch_bounds__(256) void nn_rescan_kernel(
 // One workgroup per (j-tile, i-tile) of the lower triangle (kPairTile x kPairTile): the i-tile's
 // coordinates are staged in LDS and read as broadcasts; thread l owns sample j = jt*kPairTile + l.
 // Hits are rare and appended with atomics (cand_cnt[j] is the exact count, at most kCandCap
-// entries of each j are stored).
+// entries of each j are stored).  A sample's first hit queues it for the resolve's round passes
+// (pend); a list that overflows cuts the window before its sample (weff).
 constexpr int kPairTile = 128;
 
 __global__ __launch_bounds__(kPairTile) void window_pairs_kernel(DevState* __restrict__ st,
@@ -832,7 +940,8 @@ __global__ __launch_bounds__(kPairTile) void window_pairs_kernel(DevState* __res
                                                                  const double* __restrict__ wsy,
                                                                  const double* __restrict__ nn_d2,
                                                                  int* __restrict__ cand_cnt,
-                                                                 CandEntry* __restrict__ cand) {
+                                                                 CandEntry* __restrict__ cand,
+                                                                 int* __restrict__ pend) {
     __shared__ double s_x[kPairTile], s_y[kPairTile];
     const int W = st->W;
     const int b = blockIdx.x;
@@ -852,6 +961,7 @@ __global__ __launch_bounds__(kPairTile) void window_pairs_kernel(DevState* __res
     const double D2 = valid ? nn_d2[j] : -1.0;
     __syncthreads();
     const int kend = valid ? min(kPairTile, j - i0) : 0;  // i < j (< W)
+    bool first = false, over = false;
 #pragma unroll 8
     for (int k = 0; k < kend; ++k) {
         const double dx = xj - s_x[k], dy = yj - s_y[k];
@@ -862,8 +972,12 @@ __global__ __launch_bounds__(kPairTile) void window_pairs_kernel(DevState* __res
                 const int e = atomicAdd(&st->ncomp, 1);
                 cand[e] = CandEntry{j, i0 + k, d2, 0.0, -1, 0};
             }
+            first |= cpos == 0;
+            over |= cpos == kCandCap;
         }
     }
+    if (first) pend[atomicAdd(&st->npend, 1)] = j;
+    if (over) atomicMin(&st->weff, j);
 }
 
 // Task t of a window: t < W is (sample t → its snapshot NN); t >= W is candidate entry t - W
@@ -1301,13 +1415,18 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
 
 // steer_walk, one task per wave (persistent grid, grid-stride over the W + ncomp tasks); kLds:
 // the scene's disc grid is staged into this workgroup's LDS first.
+// Window mode (pend != nullptr): a snapshot task whose verdict is not final (literal path,
+// error) and that has no nearer window sample is queued for the resolve (the others were queued
+// by window_pairs).
 template <bool kLds>
-__global__ __launch_bounds__(256, 4) void steer_walk_kernel(const DevState* __restrict__ st,
+__global__ __launch_bounds__(256, 4) void steer_walk_kernel(DevState* __restrict__ st,
                                                          SceneDev sc,
                                                          const PrepRec* __restrict__ rec,
                                                          const double* __restrict__ pdbuf,
                                                          CandEntry* __restrict__ cand,
-                                                         int* __restrict__ snap_status) {
+                                                         int* __restrict__ snap_status,
+                                                         const int* __restrict__ cand_cnt,
+                                                         int* __restrict__ pend) {
     const int lane = threadIdx.x & 63;
     const int W = st->W;
     const int total = W + st->ncomp;
@@ -1318,128 +1437,172 @@ __global__ __launch_bounds__(256, 4) void steer_walk_kernel(const DevState* __re
     for (int t = gw; t < total; t += nw) {
         const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap);
         if (lane == 0) {
-            if (t < W)
+            if (t < W) {
                 snap_status[t] = s;
-            else
+                if (pend && s != kAccept && s != kReject && cand_cnt[t] == 0)
+                    pend[atomicAdd(&st->npend, 1)] = t;
+            } else {
                 cand[t - W].status = s;
+            }
         }
     }
 }
 
-// Block-wide exclusive prefix sum of one int per thread (kResolveThreads threads, 4 waves).
-__device__ inline int block_exclusive_scan(int v, int* s_wave, int* total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) s_wave[wave] = x;
-    __syncthreads();
-    int base = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kResolveThreads / 64; ++w) {
-        const int t = s_wave[w];
-        base += w < wave ? t : 0;
-        tot += t;
-    }
-    __syncthreads();
-    *total = tot;
-    return base + x - v;
+// A resolve repair (one wave): the (child, parent pose) pair steered and collision-checked anew.
+// Out of line, so the resolve's round loop stays a few KB of code (it is cold in the instruction
+// cache at every window: the other window kernels run in between).
+__device__ __attribute__((noinline)) int resolve_repair(const SceneDev& sc, double x, double y,
+                                                        double yaw, double px, double py,
+                                                        double pyaw, int lit, double* bx) {
+    return lit ? steer_collide_literal(sc, x, y, yaw, px, py, pyaw, bx, bx + kLiteralCap,
+                                       bx + 2 * kLiteralCap)
+               : steer_collide_fast<false>(sc, x, y, yaw, px, py, pyaw);
 }
 
-// The sequential-consistency resolve of one window, on one workgroup, state in LDS: replays the
-// window in order — sample j's parent is the first ACCEPTED entry of its candidate list in
-// (d2, i) order, else its snapshot NN.  Samples without candidates are decided in one parallel
-// pass; the few with candidates go through round-stamped passes (a verdict written in round r
-// is read from round r + 1 on), and (child, parent) pairs nobody speculated on are re-steered
-// by the workgroup's waves.  The accepted samples are then appended to the tree in iteration
-// order (rrt.rs:586-589) and DevState advances.
-__global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
-    DevState* __restrict__ st, SceneDev sc, TreeDev tr, const double* __restrict__ wsx,
-    const double* __restrict__ wsy, const int* __restrict__ nn_idx,
-    const int* __restrict__ cand_cnt,
-    const CandEntry* __restrict__ cand, const int* __restrict__ snap_status,
-    const double* __restrict__ snap_yaw, ResolveScratch rs, double* __restrict__ lit_scratch) {
-    constexpr int NT = kResolveThreads;
+// The sequential-consistency resolve of one window's PENDING samples, on one workgroup with its
+// state in LDS.  A sample is pending when window_pairs found an earlier window sample strictly
+// nearer than its snapshot NN, or when its snapshot verdict is not final (literal path, error);
+// every other sample is decided by its snapshot verdict and never touches the resolve.  The
+// replay: sample j's parent is the first ACCEPTED entry of its candidate list in (d2, i) order,
+// else its snapshot NN.  Output per pending j < weff: snap_status[j] = verdict | kWinParent
+// (parent = window sample fin_par[j]), snap_yaw[j] = its final yaw.  commit_role then appends
+// the window.
+constexpr int kResolveEnt = 1024;  // candidate-list positions staged in LDS (the rest: rs.order)
+struct ResolveLds {
+    double yaw[kMaxWindow];          // slot: snapshot yaw, then a repair's, then the final one
+    double ed[kResolveEnt];          // list position: d2 (the sort key), then the entry's yaw
+    int j[kMaxWindow];               // slot -> sample
+    int round[kMaxWindow];           // slot: decided flag (published last)
+    int par[kMaxWindow];             // slot: -1 snapshot NN, else window sample index
+    int off[kMaxWindow];             // slot: first list position
+    int cnt[kMaxWindow];             // slot: list length (<= kCandCap); first the fill counter
+    int ei[kResolveEnt];             // list position: candidate sample i
+    int ee[kResolveEnt];             // list position: entry index into cand[]
+    int ec[kResolveEnt];             // list position: i's slot, or -1 / -2 (rejected / accepted by
+                                     // its snapshot verdict)
+    short slot[kMaxWindow];          // sample -> pending slot, -1: decided by its snapshot
+    signed char verdict[kMaxWindow]; // slot: snapshot status until decided, then 0/1
+    signed char rep[kMaxWindow];     // slot: repair verdict (-1: none) | 16 if literal
+    signed char es[kResolveEnt];     // list position: the entry's speculative status
+    int total, err, bail;
+    int stat[4];                     // repair passes, repairs, literal repairs, max passes of a wave
+};
+
+// kRepair = false (the window kernel): no repair code is compiled in (it would spill at the
+// window kernel's 128-VGPR budget); a window that needs a repair returns false without
+// publishing anything and resolve_tail_kernel redoes it with repairs.
+template <bool kRepair, int NT>
+__device__ __attribute__((always_inline)) inline bool resolve_role(
+    DevState* __restrict__ st, const SceneDev& sc, const TreeDev& tr,
+    const double* __restrict__ wsx, const double* __restrict__ wsy,
+    const int* __restrict__ nn_idx, const int* __restrict__ cand_cnt,
+    const CandEntry* __restrict__ cand, const int* __restrict__ pend,
+    int* __restrict__ snap_status, double* __restrict__ snap_yaw, int* __restrict__ fin_par,
+    ResolveScratch rs, double* __restrict__ lit_scratch, int W, char* smem) {
     constexpr int KW = kMaxWindow;
-    constexpr int kTaskCap = 256;
-    constexpr int kUndecided = 0x7fffffff;
-    __shared__ int s_round[KW];   // round the sample was decided in
-    __shared__ int s_par[KW];     // -1: snapshot NN, else window sample index
-    __shared__ double s_yaw[KW];
-    __shared__ int s_off[KW];     // candidate list offset; reused as tree node index at commit
-    __shared__ int s_fill[KW];
-    __shared__ int s_pend[KW];    // samples that need the round passes
-    __shared__ signed char s_verdict[KW];
-    __shared__ int s_task_j[kTaskCap], s_task_p[kTaskCap], s_task_lit[kTaskCap];
-    __shared__ int s_wave[NT / 64];
-    __shared__ int s_weff, s_npend, s_total, s_changed, s_ntask, s_err;
-    const int W = st->W;
-    if (W == 0) return;
+    constexpr int kEntLds = kResolveEnt;
+    ResolveLds& L = *reinterpret_cast<ResolveLds*>(smem);
+    auto& s_slot = L.slot;
+    auto& s_j = L.j;
+    auto& s_round = L.round;
+    auto& s_par = L.par;
+    auto& s_yaw = L.yaw;
+    auto& s_off = L.off;
+    auto& s_cnt = L.cnt;
+    auto& s_verdict = L.verdict;
+    auto& s_rep = L.rep;
+    auto& s_ei = L.ei;
+    auto& s_ee = L.ee;
+    auto& s_ec = L.ec;
+    auto& s_ed = L.ed;
+    auto& s_es = L.es;
+    auto& s_total = L.total;
+    auto& s_err = L.err;
+    auto& s_stat = L.stat;
+    auto& s_bail = L.bail;
     PP_STAMP(t_0);
-    const int64_t it0 = st->it;
-    const int n0 = st->n;
+    const int Weff = min(W, st->weff);
+    const int npend = min(st->npend, KW);
     const int ncomp = st->ncomp;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
+    if (tid < 4) s_stat[tid] = 0;
     if (tid == 0) {
-        s_weff = W;
-        s_npend = 0;
         s_total = 0;
         s_err = 0;
+        s_bail = 0;
     }
+    for (int j = tid; j < W; j += NT) s_slot[j] = -1;
     __syncthreads();
-
-    // 1. parallel pass: samples with no nearer window sample are decided by their snapshot
-    //    verdict; the rest are queued (and their candidate lists get LDS offsets).  Every load
-    //    of the pass is issued before any of them is used (one memory round trip, not 16).
-    constexpr int PER = KW / NT;  // samples per thread (strided: j = tid + NT * q)
-    int v_c[PER], v_s[PER];
-    double v_y[PER];
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int j = tid + NT * q;
-        const bool in = j < W;
-        v_c[q] = in ? cand_cnt[j] : 0;
-        v_s[q] = in ? snap_status[j] : kReject;
-        v_y[q] = in ? snap_yaw[j] : 0.0;
-    }
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int j = tid + NT * q;
-        if (j >= W) break;
-        const int c = v_c[q], ss = v_s[q];
-        s_round[j] = kUndecided;
-        s_fill[j] = 0;
-        if (c > kCandCap) atomicMin(&s_weff, j);  // list incomplete: the window stops there
-        if (c == 0 && (ss == kAccept || ss == kReject)) {
-            s_verdict[j] = ss == kAccept;
-            s_par[j] = -1;
-            s_yaw[j] = v_y[q];
-            s_round[j] = 0;
-        } else {
-            s_pend[atomicAdd(&s_npend, 1)] = j;
-            rs.rep[j] = -1;
-            if (c > 0) s_off[j] = atomicAdd(&s_total, min(c, kCandCap));
-        }
+    // 1. slots: every load of the pass is issued before any of them is used
+    for (int q = tid; q < npend; q += NT) {
+        const int j = pend[q];
+        const int c = cand_cnt[j];
+        const int ss = snap_status[j];
+        const double sy = snap_yaw[j];
+        s_slot[j] = (short)q;
+        s_j[q] = j;
+        s_round[q] = 0;
+        const int k = min(c, kCandCap);
+        s_off[q] = atomicAdd(&s_total, k);
+        s_cnt[q] = 0;
+        s_verdict[q] = (signed char)ss;
+        s_yaw[q] = sy;
+        s_rep[q] = -1;
     }
     __syncthreads();
     PP_STAMP(t_1);
-    const int Weff = s_weff;
-    const int npend = s_npend;
+    // 2. lists: each entry goes to its sample's segment (then sorted by (d2, i))
     for (int e = tid; e < ncomp; e += NT) {
-        const int j = cand[e].j;
-        const int pos = atomicAdd(&s_fill[j], 1);
-        rs.order[s_off[j] + pos] = e;
+        const CandEntry ce = cand[e];
+        const int q = s_slot[ce.j];
+        const int k = s_off[q] + atomicAdd(&s_cnt[q], 1);
+        const int qi = s_slot[ce.i];
+        const int code = qi >= 0 ? qi : (snap_status[ce.i] == kAccept ? -2 : -1);
+        if (k < kEntLds) {
+            s_ei[k] = ce.i;
+            s_ee[k] = e;
+            s_ec[k] = code;
+            s_ed[k] = ce.d2;
+        } else {
+            rs.order[k] = e;
+        }
     }
     __syncthreads();
-    for (int q = tid; q < npend; q += NT) {  // sort each list by (d2, i)
-        const int j = s_pend[q];
-        const int k = min(cand_cnt[j], kCandCap);
-        if (k < 2) continue;
-        const int o = s_off[j];
+    auto ent_e = [&](int k) { return k < kEntLds ? s_ee[k] : rs.order[k]; };
+    auto ent_i = [&](int k) { return k < kEntLds ? s_ei[k] : cand[rs.order[k]].i; };
+    auto ent_c = [&](int k) {
+        if (k < kEntLds) return s_ec[k];
+        const int i = cand[rs.order[k]].i;
+        const int qi = s_slot[i];
+        return qi >= 0 ? qi : (snap_status[i] == kAccept ? -2 : -1);
+    };
+    for (int q = tid; q < npend; q += NT) {  // insertion sort of each list by (d2, i)
+        const int o = s_off[q], k = s_cnt[q];
+        if (o + k > kEntLds) continue;  // lists past the LDS part: sorted below (global)
+        for (int a2 = 1; a2 < k; ++a2) {
+            const double d = s_ed[o + a2];
+            const int ii = s_ei[o + a2], ee = s_ee[o + a2], cc = s_ec[o + a2];
+            int b2 = a2 - 1;
+            while (b2 >= 0 && (s_ed[o + b2] > d || (s_ed[o + b2] == d && s_ei[o + b2] > ii))) {
+                s_ed[o + b2 + 1] = s_ed[o + b2];
+                s_ei[o + b2 + 1] = s_ei[o + b2];
+                s_ee[o + b2 + 1] = s_ee[o + b2];
+                s_ec[o + b2 + 1] = s_ec[o + b2];
+                --b2;
+            }
+            s_ed[o + b2 + 1] = d;
+            s_ei[o + b2 + 1] = ii;
+            s_ee[o + b2 + 1] = ee;
+            s_ec[o + b2 + 1] = cc;
+        }
+    }
+    for (int q = tid; q < npend; q += NT) {  // the rare lists that straddle or pass kEntLds
+        const int o = s_off[q], k = s_cnt[q];
+        if (o + k <= kEntLds) continue;
+        // materialise the whole list in rs.order, then sort it there
+        for (int a2 = 0; a2 < k; ++a2)
+            if (o + a2 < kEntLds) rs.order[o + a2] = s_ee[o + a2];
         for (int a2 = 1; a2 < k; ++a2) {
             const int e = rs.order[o + a2];
             const double d = cand[e].d2;
@@ -1453,149 +1616,158 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
             }
             rs.order[o + b2 + 1] = e;
         }
+        for (int a2 = 0; a2 < k && o + a2 < kEntLds; ++a2) {  // refresh the LDS part
+            const int e = rs.order[o + a2];
+            const int i = cand[e].i;
+            const int qi = s_slot[i];
+            s_ee[o + a2] = e;
+            s_ei[o + a2] = i;
+            s_ed[o + a2] = cand[e].d2;
+            s_ec[o + a2] = qi >= 0 ? qi : (snap_status[i] == kAccept ? -2 : -1);
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < min(s_total, kEntLds); k += NT) {  // the entries' speculative verdicts
+        const int e = s_ee[k];
+        const int es = cand[e].status;
+        const double ey = cand[e].yaw;
+        s_es[k] = (signed char)es;
+        s_ed[k] = ey;
     }
     __syncthreads();
 
     PP_STAMP(t_2);
-    // 2. round passes over the queued samples
-    int64_t n_rounds_rep = 0, n_rep = 0, n_lit = 0;
-    for (int round = 1; round < (1 << 20) && npend > 0; ++round) {
-        if (tid == 0) {
-            s_changed = 0;
-            s_ntask = 0;
-        }
-        __syncthreads();
+    // 3. decisions, without workgroup barriers: every wave passes over its own slots until all of
+    //    them are decided, reading the other slots' decisions from LDS as they appear.  A decision
+    //    is final once published (its flag is stored last, with release order), and every
+    //    dependency points to an earlier sample, so the earliest undecided slot can always be
+    //    decided: the passes terminate.  A pair nobody speculated on is re-steered by the wave
+    //    that owns the slot, between its passes.
+    int64_t n_rounds_rep = 0, n_rep = 0, n_lit = 0, n_rounds = 0;
+    for (int pass = 0; pass < (1 << 20); ++pass) {
+        ++n_rounds;
+        bool left = false;
+        int rq = -1, rpar = -1, rlit = 0;  // this lane's repair request (one per pass)
         for (int q = tid; q < npend; q += NT) {
-            const int j = s_pend[q];
-            if (j >= Weff || s_round[j] != kUndecided) continue;
-            int parent = -1, slot = -1;
+            if (__hip_atomic_load(&s_round[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                continue;
+            const int j = s_j[q];
+            if (j >= Weff) continue;
+            int parent = -1, pos = -1, pq = -1;
             bool blocked = false;
-            const int k = min(cand_cnt[j], kCandCap);
-            const int o = k > 0 ? s_off[j] : 0;
+            const int k = s_cnt[q], o = s_off[q];
             for (int a2 = 0; a2 < k; ++a2) {
-                const int e = rs.order[o + a2];
-                const int i = cand[e].i;
-                if (s_round[i] >= round) {  // undecided as of this round's start
-                    blocked = true;
-                    break;
+                const int code = ent_c(o + a2);
+                if (code >= 0) {
+                    if (!__hip_atomic_load(&s_round[code], __ATOMIC_ACQUIRE,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                        blocked = true;  // an earlier candidate is still undecided
+                        break;
+                    }
+                    if (!s_verdict[code]) continue;
+                } else if (code == -1) {
+                    continue;
                 }
-                if (s_verdict[i]) {
-                    parent = i;
-                    slot = e;
-                    break;
-                }
+                parent = ent_i(o + a2);
+                pos = o + a2;
+                pq = code;
+                break;
             }
-            if (blocked) continue;
+            if (blocked) {
+                left = true;
+                continue;
+            }
             int status = -1, lit_done = 0;
             double y = 0.0;
-            const int rep = rs.rep[j];
-            if (rep >= 0) {
-                status = rep & 15;
-                lit_done = rep >> 4;
-                y = rs.repyaw[j];
+            const int rp = s_rep[q];
+            if (rp >= 0) {
+                status = rp & 15;
+                lit_done = rp >> 4;
+                y = s_yaw[q];
             } else if (parent < 0) {
-                status = snap_status[j];
-                y = snap_yaw[j];
-            } else if (s_par[parent] < 0) {
-                status = cand[slot].status;
-                y = cand[slot].yaw;
+                status = s_verdict[q];
+                y = s_yaw[q];
+            } else if (pq < 0 || s_par[pq] < 0) {  // parent kept its snapshot parent: speculated
+                if (pos < kEntLds) {
+                    status = s_es[pos];
+                    y = s_ed[pos];
+                } else {
+                    const int e = ent_e(pos);
+                    status = cand[e].status;
+                    y = cand[e].yaw;
+                }
             }
             if (status < 0 || (status == kLiteral && !lit_done)) {
-                const int tk = atomicAdd(&s_ntask, 1);
-                if (tk < kTaskCap) {
-                    s_task_j[tk] = j;
-                    s_task_p[tk] = parent;
-                    s_task_lit[tk] = status == kLiteral;
+                left = true;
+                if (rq < 0) {
+                    rq = q;
+                    rpar = parent;
+                    rlit = status == kLiteral;
                 }
                 continue;
             }
             if (status != kAccept && status != kReject) s_err = 1;  // kError
-            s_verdict[j] = status == kAccept;
-            s_par[j] = parent;
-            s_yaw[j] = y;
-            s_round[j] = round;
-            s_changed = 1;
+            s_verdict[q] = status == kAccept;
+            s_par[q] = parent;
+            s_yaw[q] = y;
+            __hip_atomic_store(&s_round[q], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        __syncthreads();
-        const int ntask = min(s_ntask, kTaskCap);
-        if (ntask == 0 && !s_changed) break;
-        if (ntask > 0) {
-            for (int tk = wave; tk < ntask; tk += NT / 64) {
-                const int j = s_task_j[tk], p = s_task_p[tk], lit = s_task_lit[tk];
+        // repairs requested by this wave's lanes, one wave-wide steer each
+        uint64_t m = __ballot(rq >= 0);
+        if constexpr (!kRepair) {
+            if (m && lane == 0) s_bail = 1;
+            if (__hip_atomic_load(&s_bail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+        } else {
+            if (m) ++n_rounds_rep;
+            while (m) {
+                const int l = (int)__builtin_ctzll(m);
+                m &= m - 1;
+                const int q = __shfl(rq, l), p = __shfl(rpar, l), lit = __shfl(rlit, l);
+                const int j = s_j[q];
                 const double x = wsx[j], y = wsy[j];
                 double px, py, pyaw;
                 if (p < 0) {
-                    const int q = nn_idx[j];
-                    px = tr.x[q];
-                    py = tr.y[q];
-                    pyaw = tr.yaw[q];
+                    const int nq = nn_idx[j];
+                    px = tr.x[nq];
+                    py = tr.y[nq];
+                    pyaw = tr.yaw[nq];
                 } else {
                     px = wsx[p];
                     py = wsy[p];
-                    pyaw = s_yaw[p];
+                    const int pq = s_slot[p];
+                    pyaw = pq >= 0 ? s_yaw[pq] : snap_yaw[p];
                 }
                 const double yaw = atan2(py - y, px - x);
                 double* bx = lit_scratch + (size_t)wave * 3 * kLiteralCap;
-                const int sres = lit ? steer_collide_literal(sc, x, y, yaw, px, py, pyaw, bx,
-                                                             bx + kLiteralCap, bx + 2 * kLiteralCap)
-                                     : steer_collide_fast<false>(sc, x, y, yaw, px, py, pyaw);
+                const int sres = resolve_repair(sc, x, y, yaw, px, py, pyaw, lit, bx);
                 if (lane == 0) {
-                    rs.rep[j] = sres | (lit << 4);
-                    rs.repyaw[j] = yaw;
+                    s_rep[q] = (signed char)(sres | (lit << 4));
+                    s_yaw[q] = yaw;
                 }
-            }
-            if (tid == 0) {
-                n_rounds_rep++;
-                n_rep += ntask;
-                for (int tk = 0; tk < ntask; ++tk) n_lit += s_task_lit[tk];
+                ++n_rep;
+                n_lit += lit;
             }
         }
-        __syncthreads();
+        if (!__any(left)) break;
     }
-
+    if (lane == 0) {  // per-wave statistics (wave-uniform values)
+        atomicAdd(&s_stat[0], (int)n_rounds_rep);
+        atomicAdd(&s_stat[1], (int)n_rep);
+        atomicAdd(&s_stat[2], (int)n_lit);
+        atomicMax(&s_stat[3], (int)n_rounds);
+    }
+    __syncthreads();
+    if (!kRepair && s_bail) return false;
     PP_STAMP(t_3);
-    // 3. commit: accepted samples get consecutive node indices in iteration order
-    const int j0 = tid * PER;  // contiguous samples per thread for the scan
-    int local = 0;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int j = j0 + q;
-        local += (j < Weff && s_verdict[j]) ? 1 : 0;
+    // 4. publish the pending verdicts for window_commit
+    for (int q = tid; q < npend; q += NT) {
+        const int j = s_j[q];
+        if (j >= Weff) continue;
+        const int p = s_par[q];
+        snap_status[j] = (s_verdict[q] ? kAccept : kReject) | (p >= 0 ? kWinParent : 0);
+        snap_yaw[j] = s_yaw[q];
+        fin_par[j] = p;
     }
-    int total = 0;
-    int node = n0 + block_exclusive_scan(local, s_wave, &total);
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int j = j0 + q;
-        if (j < Weff && s_verdict[j]) s_off[j] = node++;
-    }
-    __syncthreads();
-    double v_x[PER], v_yy[PER];
-    int v_p[PER];
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {  // loads first, then the (scattered) tree stores
-        const int j = tid + NT * q;
-        const bool in = j < Weff;
-        v_x[q] = in ? wsx[j] : 0.0;
-        v_yy[q] = in ? wsy[j] : 0.0;
-        v_p[q] = in ? nn_idx[j] : 0;
-    }
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int j = tid + NT * q;
-        if (j >= Weff) break;
-        if (!s_verdict[j]) continue;
-        const int nd = s_off[j];
-        const int p = s_par[j];
-        const int par = p >= 0 ? s_off[p] : v_p[q];
-        tr.x[nd] = v_x[q];
-        tr.y[nd] = v_yy[q];
-        tr.x32[nd] = (float)v_x[q];
-        tr.y32[nd] = (float)v_yy[q];
-        tr.yaw[nd] = s_yaw[j];
-        tr.parent[nd] = par;
-    }
-    __syncthreads();
     PP_STAMP(t_4);
 #ifdef PP_STAMPS_RESOLVE
     if (tid == 0) {
@@ -1603,21 +1775,170 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(
         st->stamps[1] += t_2 - t_1;
         st->stamps[2] += t_3 - t_2;
         st->stamps[3] += t_4 - t_3;
+        st->stamps[4] += s_stat[3];
+        st->stamps[5] += npend;
+        st->stamps[6] += ncomp;
     }
 #endif
     if (tid == 0) {
+        if (s_err) st->error = 1;
+        st->repair_rounds += s_stat[0];
+        st->repairs += s_stat[1];
+        st->literal_repairs += s_stat[2];
+    }
+    return true;
+}
+
+// Append the window (rrt.rs:586-589): the accepted samples j < weff get consecutive node indices
+// in iteration order (a prefix sum of the verdict words in LDS, so a window parent's node index is
+// known), then DevState advances.  A truncated window (weff < W) restarts the next window at
+// sample weff: the window screened concurrently (seq) is void.
+template <int NT>
+__device__ __attribute__((always_inline)) inline void commit_role(
+    DevState* __restrict__ st, const TreeDev& tr, const double* __restrict__ wsx,
+    const double* __restrict__ wsy, const int* __restrict__ nn_idx,
+    const int* __restrict__ snap_status, const double* __restrict__ snap_yaw,
+    const int* __restrict__ fin_par, int* __restrict__ cand_cnt, int W, int64_t void_next,
+    char* smem) {
+    constexpr int PER = kMaxWindow / NT;
+    static_assert(PER % 4 == 0, "commit: whole int4 loads per thread");
+    int* s_node = reinterpret_cast<int*>(smem);
+    int* s_wave = s_node + kMaxWindow;
+    const int Weff = min(W, st->weff);
+    const int n0 = st->n;
+    const int64_t it0 = st->it;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int j0 = tid * PER;
+    int v[PER];
+    if (j0 + PER <= Weff) {
+#pragma unroll
+        for (int u = 0; u < PER; u += 4) {
+            const int4 w4 = *reinterpret_cast<const int4*>(snap_status + j0 + u);
+            v[u] = w4.x;
+            v[u + 1] = w4.y;
+            v[u + 2] = w4.z;
+            v[u + 3] = w4.w;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) v[u] = j0 + u < Weff ? snap_status[j0 + u] : 0;
+    }
+    int local = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) local += v[u] & 1;
+    int x = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[wave] = x;
+    __syncthreads();
+    int base = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        base += w < wave ? s_wave[w] : 0;
+        total += s_wave[w];
+    }
+    int node = n0 + base + x - local;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        s_node[j0 + u] = node;
+        node += v[u] & 1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int j = j0 + u;
+        if (j < Weff && (v[u] & 1)) {
+            const int nd = s_node[j];
+            const double xx = wsx[j], yy = wsy[j];
+            tr.x[nd] = xx;
+            tr.y[nd] = yy;
+            tr.x32[nd] = (float)xx;
+            tr.y32[nd] = (float)yy;
+            tr.yaw[nd] = snap_yaw[j];
+            tr.parent[nd] = (v[u] & kWinParent) ? s_node[fin_par[j]] : nn_idx[j];
+        }
+        if (j < W) cand_cnt[j] = 0;  // the next window's pair counts start at zero
+    }
+    if (tid == 0) {
         st->n = n0 + total;
         st->it = it0 + Weff;
-        if (s_err) st->error = 1;
         st->iterations += Weff;
         st->accepted += total;
         st->windows += 1;
         st->truncations += Weff < W;
-        st->repair_rounds += n_rounds_rep;
-        st->repairs += n_rep;
-        st->literal_repairs += n_lit;
         st->nn_flagged += st->flag_count;
         st->node_evals += (int64_t)W * n0;
+        if (Weff < W) {
+            st->it_spec = it0 + Weff;
+            if (void_next >= 0) st->void_seq = void_next;
+        }
+    }
+}
+
+// The window kernel: workgroup 0 resolves and commits the previous window (or, in the drain
+// launch, the batch's last one) while workgroups 1.. screen this window's samples.  One LDS image
+// serves the role of each workgroup (ResolveLds / the commit prefix / the screen's wave merge).
+constexpr int kWinLds = (int)sizeof(ResolveLds);
+static_assert(kWinLds <= 160 * 1024, "window kernel LDS");
+static_assert((int)(3 * kScanWaves * kQPB * 4) <= kWinLds, "screen merge fits the LDS image");
+
+__global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[kWinLds];
+    if (blockIdx.x == 0) {
+        DevState* st = a.st;
+        if (a.resolve) {
+            const int W = st->W;
+            if (W > 0) {
+                const int q = 1 - a.p;
+                if (!resolve_role<false, kScanThreads>(st, a.sc, a.tr, a.wsx[q], a.wsy[q], a.nn_idx,
+                                                       a.cand_cnt, a.cand, a.pend, a.snap_status,
+                                                       a.snap_yaw, a.fin_par, a.rs, a.lit_scratch,
+                                                       W, smem)) {
+                    if (threadIdx.x == 0) st->resolve_bail = 1;  // resolve_tail_kernel redoes it
+                    return;
+                }
+                __threadfence();
+                __syncthreads();
+                commit_role<kScanThreads>(st, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.snap_status,
+                                          a.snap_yaw, a.fin_par, a.cand_cnt, W,
+                                          a.scan ? a.seq : -1, smem);
+            }
+        }
+        if (threadIdx.x == 0) {  // the screened window's counters start at zero
+            st->flag_count = 0;
+            st->ncomp = 0;
+            st->npend = 0;
+        }
+        return;
+    }
+    if (a.scan) scan_role(a, (int)blockIdx.x - 1, smem);
+}
+
+// The resolve + commit of a window whose resolve in the window kernel needed a repair (a pair
+// nobody speculated on, or the literal path): redone here with the repairs, at kResolveThreads
+// (256 VGPRs each, no spill).  A no-op launch otherwise.
+__global__ __launch_bounds__(kResolveThreads) void resolve_tail_kernel(WinKArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[kWinLds];
+    DevState* st = a.st;
+    if (!st->resolve_bail) return;
+    const int q = 1 - a.p;
+    const int W = st->W;
+    resolve_role<true, kResolveThreads>(st, a.sc, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.cand_cnt,
+                                         a.cand, a.pend, a.snap_status, a.snap_yaw, a.fin_par,
+                                         a.rs, a.lit_scratch, W, smem);
+    __threadfence();
+    __syncthreads();
+    commit_role<kResolveThreads>(st, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.snap_status,
+                                 a.snap_yaw, a.fin_par, a.cand_cnt, W, a.scan ? a.seq : -1, smem);
+    if (threadIdx.x == 0) {
+        st->resolve_bail = 0;
+        st->flag_count = 0;
+        st->ncomp = 0;
+        st->npend = 0;
     }
 }
 
@@ -2028,10 +2349,12 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
                                                       nullptr, a.rec, a.pdbuf, a.yaw, a.tasks);
         if (lds > 0)
             steer_walk_kernel<true><<<walk_blocks, 256, lds, s>>>(a.st, a.sc, a.rec, a.pdbuf,
-                                                                  nullptr, a.status);
+                                                                  nullptr, a.status, nullptr,
+                                                                  nullptr);
         else
             steer_walk_kernel<false><<<walk_blocks, 256, 0, s>>>(a.st, a.sc, a.rec, a.pdbuf,
-                                                                 nullptr, a.status);
+                                                                 nullptr, a.status, nullptr,
+                                                                 nullptr);
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
                                                     a.lit_scratch, a.err);
     }
@@ -2040,53 +2363,94 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
 
 // --------------------------------------------------------------------------- launch wrappers
 
-hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev) {
+namespace {
+WinKArgs win_args(const WindowArgs& a, int p, int gen, int resolve, int scan, int64_t seq) {
+    WinKArgs k;
+    k.st = a.st;
+    k.sc = a.sc;
+    k.tr = a.tr;
+    k.K = a.K;
+    k.Kcap = a.Kcap;
+    k.nqb = (a.K + kQPB - 1) / kQPB;
+    k.chunks = scan_chunks(a.K);
+    k.p = p;
+    k.gen = gen;
+    k.resolve = resolve;
+    k.scan = scan;
+    k.seq = seq;
+    k.target = a.target;
+    k.seed = a.seed;
+    k.wsx[0] = a.wsx;
+    k.wsx[1] = a.wsx + a.Kcap;
+    k.wsy[0] = a.wsy;
+    k.wsy[1] = a.wsy + a.Kcap;
+    k.pbest = a.pbest;
+    k.psecond = a.psecond;
+    k.pidx = a.pidx;
+    k.nn_idx = a.nn_idx;
+    k.cand_cnt = a.cand_cnt;
+    k.cand = a.cand;
+    k.pend = a.pend;
+    k.snap_status = a.snap_status;
+    k.snap_yaw = a.snap_yaw;
+    k.fin_par = a.fin_par;
+    k.rs = a.rs;
+    k.lit_scratch = a.lit_scratch;
+    return k;
+}
+}  // namespace
+
+hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int64_t seq,
+                         int resolve_prev) {
     const int K = a.K;
-    const int nqb = (K + kQPB - 1) / kQPB;
+    const int p = (int)(seq & 1);
+    const WinKArgs wk = win_args(a, p, 1, resolve_prev, 1, seq);
     const int Tp = (K + kPairTile - 1) / kPairTile;
-    window_begin_kernel<<<(K + 255) / 256, 256, 0, s>>>(a.st, K, a.target, a.seed, a.sc.minx,
-                                                         a.sc.maxx, a.sc.miny, a.sc.maxy, a.wsx,
-                                                         a.wsy, a.cand_cnt);
+    double* wsx = a.wsx + (size_t)p * a.Kcap;
+    double* wsy = a.wsy + (size_t)p * a.Kcap;
     if (ev) (void)hipEventRecord(ev[0], s);
-    nn_scan_kernel<<<nqb * kMaxChunks, 256, 0, s>>>(a.st, a.tr.x32, a.tr.y32, a.wsx, a.wsy, nqb, K,
-                                                   a.pbest, a.psecond, a.pidx);
+    window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
     if (ev) (void)hipEventRecord(ev[1], s);
-    nn_finalize_kernel<<<(K + 63) / 64, 256, 0, s>>>(a.st, a.pbest, a.psecond, a.pidx, K, a.wsx,
-                                                     a.wsy, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord,
-                                                     a.nn_idx, a.nn_d2, a.snap_pose, a.flag_list);
+    if (resolve_prev) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
+    nn_finalize_kernel<<<(K + 63) / 64, kFinThreads, 0, s>>>(
+        a.st, p, seq, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, wsx, wsy, a.tr.x32, a.tr.y32,
+        a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose, a.flag_list);
     nn_rescan_kernel<<<dim3(kMaxChunks, kRescanSlots), 256, 0, s>>>(
-        a.st, a.flag_list, a.wsx, a.wsy, a.tr.x, a.tr.y, a.tr.yaw, a.rs_d2, a.rs_idx, a.rs_done,
+        a.st, a.flag_list, wsx, wsy, a.tr.x, a.tr.y, a.tr.yaw, a.rs_d2, a.rs_idx, a.rs_done,
         a.nn_idx, a.nn_d2, a.snap_pose);
-    window_pairs_kernel<<<Tp * (Tp + 1) / 2, kPairTile, 0, s>>>(a.st, a.wsx, a.wsy, a.nn_d2,
-                                                                a.cand_cnt, a.cand);
+    window_pairs_kernel<<<Tp * (Tp + 1) / 2, kPairTile, 0, s>>>(a.st, wsx, wsy, a.nn_d2,
+                                                                a.cand_cnt, a.cand, a.pend);
     if (ev) (void)hipEventRecord(ev[2], s);
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K * kPrepLanes + 255) / 256;
-    steer_prep_kernel<<<prep_blocks, 256, 0, s>>>(a.st, a.sc, a.wsx, a.wsy, a.snap_pose, a.cand,
+    steer_prep_kernel<<<prep_blocks, 256, 0, s>>>(a.st, a.sc, wsx, wsy, a.snap_pose, a.cand,
                                                   a.rec, a.pdbuf, a.snap_yaw, nullptr);
     const int lds = a.sc.lds_bytes;
     const int nwg = std::min((K + 3) / 4, 1024);
     if (lds > 0)
         steer_walk_kernel<true><<<nwg, 256, lds, s>>>(a.st, a.sc, a.rec, a.pdbuf, a.cand,
-                                                      a.snap_status);
+                                                      a.snap_status, a.cand_cnt, a.pend);
     else
         steer_walk_kernel<false><<<nwg, 256, 0, s>>>(a.st, a.sc, a.rec, a.pdbuf, a.cand,
-                                                     a.snap_status);
+                                                     a.snap_status, a.cand_cnt, a.pend);
     if (ev) (void)hipEventRecord(ev[3], s);
-    resolve_kernel<<<1, kResolveThreads, 0, s>>>(a.st, a.sc, a.tr, a.wsx, a.wsy, a.nn_idx,
-                                                 a.cand_cnt, a.cand,
-                                                 a.snap_status, a.snap_yaw, a.rs, a.lit_scratch);
+    return hipGetLastError();
+}
+
+hipError_t launch_drain(hipStream_t s, const WindowArgs& a, int64_t seq_next) {
+    const WinKArgs wk = win_args(a, (int)(seq_next & 1), 1, 1, 0, seq_next);
+    window_kernel<<<1, kScanThreads, 0, s>>>(wk);
+    resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
     return hipGetLastError();
 }
 
 hipError_t launch_nearest(hipStream_t s, const WindowArgs& a) {
     const int K = a.K;
-    const int nqb = (K + kQPB - 1) / kQPB;
-    nn_scan_kernel<<<nqb * kMaxChunks, 256, 0, s>>>(a.st, a.tr.x32, a.tr.y32, a.wsx, a.wsy, nqb, K,
-                                                   a.pbest, a.psecond, a.pidx);
-    nn_finalize_kernel<<<(K + 63) / 64, 256, 0, s>>>(a.st, a.pbest, a.psecond, a.pidx, K, a.wsx,
-                                                     a.wsy, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord,
-                                                     a.nn_idx, a.nn_d2, nullptr, a.flag_list);
+    const WinKArgs wk = win_args(a, 0, 0, 0, 1, 0);
+    window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
+    nn_finalize_kernel<<<(K + 63) / 64, kFinThreads, 0, s>>>(
+        a.st, 0, 0, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, a.wsx, a.wsy, a.tr.x32,
+        a.tr.y32, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, nullptr, a.flag_list);
     nn_rescan_kernel<<<dim3(kMaxChunks, kRescanSlots), 256, 0, s>>>(
         a.st, a.flag_list, a.wsx, a.wsy, a.tr.x, a.tr.y, a.tr.yaw, a.rs_d2, a.rs_idx, a.rs_done,
         a.nn_idx, a.nn_d2, nullptr);

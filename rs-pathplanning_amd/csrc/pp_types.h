@@ -21,7 +21,7 @@ constexpr int kMaxChunks = 64;       // node chunks of the NN screen (partials p
 constexpr int kRescanSlots = 32;     // flagged samples rescanned concurrently (grid y)
 constexpr int kLiteralCap = 16384;   // points per literal-path scratch buffer
 constexpr int kLiteralWaves = 256;   // literal scratch buffers (explicit-task kernel)
-constexpr int kResolveThreads = 256; // one workgroup resolves a window (4 waves: 1 per SIMD)
+constexpr int kResolveThreads = 512;  // resolve_tail_kernel (8 waves, 256 VGPRs: the repair path)
 constexpr int kMaxWindow = 4096;     // K limit: the resolve keeps the window's state in LDS
 constexpr int kSteerPrepBytes = 152; // sizeof(SteerPrep) (checked in pp_kernels.hip)
 constexpr int kPdCap = 63;           // grid points per task stored by steer_prep (one walk chunk)
@@ -70,15 +70,26 @@ struct TreeDev {
 };
 
 // Device-resident planner state: the window kernels read it and the resolve kernel advances it,
-// so windows are enqueued back to back without a host round trip.
+// so windows are enqueued back to back without a host round trip.  Windows are pipelined: the
+// window kernel of window w scans w's samples while its workgroup 0 resolves and commits window
+// w - 1, so the scan-side fields are kept per window parity (p = w & 1).
 struct DevState {
-    int64_t it;      // next iteration (RNG counter base)
-    int n;           // tree nodes
-    int W;           // samples in the current window (0: nothing left to do)
+    int64_t it;      // next iteration (RNG counter base) = committed iterations
+    int n;           // tree nodes (committed)
+    int W;           // samples in the current window (0: nothing left to do / void window)
     int error;       // sticky kError seen (the reference would panic)
     int flag_count;  // NN samples flagged for the exact rescan (this window)
     int ncomp;       // candidate entries appended by window_pairs (this window)
-    int pad;
+    int npend;       // samples queued for the resolve's round passes (this window)
+    int weff;        // the window stops before this sample (a candidate list overflowed)
+    int n_scan;      // tree nodes the next window's scan covers (nodes past it: nn_finalize)
+    int64_t it_spec; // first iteration of the next window to scan
+    int64_t wsp[2];  // per parity: first iteration of the window the scan generated
+    int Wp[2];       // per parity: its sample count
+    int nsp[2];      // per parity: tree nodes its scan covered
+    int64_t void_seq;  // window sequence number voided by a truncated predecessor (-1: none)
+    int resolve_bail;  // the window kernel's resolve needed a repair: resolve_tail_kernel redoes it
+    int pad2;
     // statistics (pp_stats)
     int64_t iterations, accepted, windows, truncations, repair_rounds, repairs, literal_repairs,
         nn_flagged, node_evals;
@@ -138,11 +149,15 @@ struct MqDev {
     const uint64_t* seed;   // [Q] sampling stream
 };
 
-// Resolve scratch (global, one window).
+// Resolve scratch (global, one window; indexed by pending slot / list position).
 struct ResolveScratch {
-    int* order;     // [K * kCandCap] entry indices, per sample sorted by (d2, i)
+    int* order;     // [K * kCandCap] entry indices of list positions past the LDS-staged ones
     int* rep;       // [K] repair verdict (-1: none), | 16 when it came from the literal path
     double* repyaw; // [K]
 };
+
+// window status word after the resolve (snap_status of a pending sample is overwritten with it):
+// bit 0 = accepted, bit 2 = its parent is the window sample fin_par[j] (else its snapshot NN)
+constexpr int kWinParent = 4;
 
 }  // namespace ppamd

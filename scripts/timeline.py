@@ -5,7 +5,7 @@ import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/iter/trace/run_kernel_trace.csv"
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-wb = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("window_begin")]
+wb = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(("window_begin", "window_kernel"))]
 a, b = wb[-8], wb[-7]
 t0 = int(rows[a]["Start_Timestamp"])
 for r in rows[a:b + 1]:
