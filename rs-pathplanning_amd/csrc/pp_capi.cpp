@@ -128,9 +128,9 @@ struct pp_ctx {
     // ---- window buffers (sized for Kcap)
     int K = 4096;
     int Kcap = 0;
-    DBuf<double> wsx, wsy, nn_d2, rs_d2, snap_yaw, snap_pose;
+    DBuf<double> wsx, wsy, nn_d2, snap_yaw, snap_pose;
     DBuf<float> pbest, psecond;
-    DBuf<int> pidx, nn_idx, flag_list, rs_idx, rs_done, cand_cnt, snap_status;
+    DBuf<int> pidx, nn_idx, cand_cnt, snap_status;
     DBuf<CandEntry> cand;
     DBuf<PrepRec> rec;   // per-task steer records
     DBuf<double> pdbuf;  // per-task grid-point distances (kPdCap per task)
@@ -234,10 +234,6 @@ struct pp_ctx {
         a.pidx = pidx.p;
         a.nn_idx = nn_idx.p;
         a.nn_d2 = nn_d2.p;
-        a.flag_list = flag_list.p;
-        a.rs_d2 = rs_d2.p;
-        a.rs_idx = rs_idx.p;
-        a.rs_done = rs_done.p;
         a.cand_cnt = cand_cnt.p;
         a.cand = cand.p;
         a.snap_status = snap_status.p;
@@ -278,11 +274,6 @@ int ensure_window(pp_ctx* c, int K) {
     PP_HIP(c->pidx.reserve(k * kMaxChunks));
     PP_HIP(c->nn_idx.reserve(k));
     PP_HIP(c->nn_d2.reserve(k));
-    PP_HIP(c->flag_list.reserve(k));
-    PP_HIP(c->rs_d2.reserve(k * kMaxChunks));
-    PP_HIP(c->rs_idx.reserve(k * kMaxChunks));
-    PP_HIP(c->rs_done.reserve(k));
-    PP_HIP(hipMemsetAsync(c->rs_done.p, 0, k * sizeof(int), c->stream));
     PP_HIP(c->cand_cnt.reserve(k));
     PP_HIP(c->cand.reserve(k * kCandCap));
     PP_HIP(c->rec.reserve(k + k * kCandCap));

@@ -24,10 +24,6 @@ struct WindowArgs {
     int* pidx = nullptr;
     int* nn_idx = nullptr;
     double* nn_d2 = nullptr;
-    int* flag_list = nullptr;
-    double* rs_d2 = nullptr;
-    int* rs_idx = nullptr;
-    int* rs_done = nullptr;       // [K] per-flag partial counters (zero between windows)
     int* cand_cnt = nullptr;
     CandEntry* cand = nullptr;
     int* snap_status = nullptr;

@@ -22,7 +22,7 @@
 
 namespace ppamd {
 
-#if defined(PP_STAMPS) || defined(PP_STAMPS_RESOLVE)
+#if defined(PP_STAMPS) || defined(PP_STAMPS_RESOLVE) || defined(PP_STAMPS_WALK)
 #define PP_STAMP(var) const int64_t var = (int64_t)__builtin_amdgcn_s_memrealtime()
 #else
 #define PP_STAMP(var)
@@ -455,11 +455,23 @@ __global__ __launch_bounds__(64) void dubins_batch_kernel(const double* __restri
 // device-resident DevState, so the host enqueues windows back to back and synchronises once per
 // batch.
 
-constexpr int kQPL = 4;                          // samples per lane in the screen
+#ifndef PP_QPL
+#define PP_QPL 4
+#endif
+#ifndef PP_SCANBLK
+#define PP_SCANBLK 16
+#endif
+constexpr int kQPL = PP_QPL;                     // samples per lane in the screen
 constexpr int kQPB = 64 * kQPL;                  // samples per screen workgroup (its waves share them)
+#ifdef PP_WIN1024
 constexpr int kScanThreads = 1024;               // window_kernel workgroup (16 waves)
+constexpr bool kWinRepair = false;               // repairs in resolve_tail_kernel
+#else
+constexpr int kScanThreads = 512;                // window_kernel workgroup (8 waves, 256 VGPRs)
+constexpr bool kWinRepair = true;                // repairs inside the window kernel (no spill)
+#endif
 constexpr int kScanWaves = kScanThreads / 64;
-constexpr int kScanBlk = 16;                     // nodes per scalar-load block
+constexpr int kScanBlk = PP_SCANBLK;             // nodes per scalar-load block
 constexpr int kScanGrid = 240;                   // screen workgroups per window (one per CU, with
                                                  // the resolve workgroup: 241 <= 256 CUs)
 
@@ -479,6 +491,13 @@ __host__ __device__ inline int scan_chunk_len(int n, int chunks) {
 __host__ __device__ inline int scan_chunks_used(int n, int chunks) {
     const int cl = scan_chunk_len(n, chunks);
     return (n + cl - 1) / cl;
+}
+
+__device__ inline void argmin_pair(double& d, int& i, double od, int oi) {
+    if (od < d || (od == d && oi < i)) {
+        d = od;
+        i = oi;
+    }
 }
 
 struct Top2 {
@@ -742,10 +761,14 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     const double* __restrict__ qx, const double* __restrict__ qy, const float* __restrict__ x32,
     const float* __restrict__ y32, const double* __restrict__ X, const double* __restrict__ Y,
     const double* __restrict__ YAW, double eps_coord, int* __restrict__ out_idx,
-    double* __restrict__ out_d2, double* __restrict__ out_pose, int* __restrict__ flag_list) {
+    double* __restrict__ out_d2, double* __restrict__ out_pose) {
     __shared__ float s_b[kFinWaves][64];
     __shared__ float s_s[kFinWaves][64];
     __shared__ int s_i[kFinWaves][64];
+    __shared__ double s_fd[64];  // f32 winner's distance of each sample
+    __shared__ double s_rd[kFinWaves];
+    __shared__ int s_ri[kFinWaves];
+    __shared__ uint64_t s_fmask, s_cmask;
     const bool voided = st->void_seq == seq || st->error;
     const int W = voided ? 0 : st->Wp[p];
     const int ns = st->nsp[p], n = st->n;
@@ -816,110 +839,93 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     s_s[wave][lane] = t.s;
     s_i[wave][lane] = t.i;
     __syncthreads();
-    if (wave != 0 || !in) return;
+    if (wave == 0) {
 #pragma unroll
-    for (int w = 1; w < kFinWaves; ++w)
-        t = merge_top2(t, Top2{s_b[w][lane], s_s[w][lane], s_i[w][lane]});
-    bool flag = t.i < 0 || !(t.b < __builtin_inff());
-    if (!flag && t.s < __builtin_inff()) {
-        const double D1 = sqrt((double)t.b), D2 = sqrt((double)t.s);
-        const double tau = 8.0 * eps_coord + 1.0e-6 * D2;
-        flag = !(D2 - D1 > tau);
-    }
-    if (flag) {
-        const int f = atomicAdd(&st->flag_count, 1);
-        flag_list[f] = q;
-        out_idx[q] = -(f + 1);
-    } else {
-        const double nxp = X[t.i], nyp = Y[t.i];
-        const double dx = qx[q] - nxp, dy = qy[q] - nyp;
-        out_idx[q] = t.i;
-        out_d2[q] = dx * dx + dy * dy;
-        if (out_pose) {
-            out_pose[3 * q] = nxp;
-            out_pose[3 * q + 1] = nyp;
-            out_pose[3 * q + 2] = YAW[t.i];
+        for (int w = 1; w < kFinWaves; ++w)
+            t = merge_top2(t, Top2{s_b[w][lane], s_s[w][lane], s_i[w][lane]});
+        bool flag = t.i < 0 || !(t.b < __builtin_inff());
+        double D1 = __builtin_inf();
+        if (!flag) {
+            D1 = sqrt((double)t.b);
+            if (t.s < __builtin_inff()) {
+                const double D2 = sqrt((double)t.s);
+                const double tau = 8.0 * eps_coord + 1.0e-6 * D2;
+                flag = !(D2 - D1 > tau);
+            }
+        }
+        flag = flag && in;
+        s_fd[lane] = D1;
+        const uint64_t fm = __ballot(flag);
+        if (lane == 0) s_fmask = fm;
+        if (flag) {
+            atomicAdd(&st->flag_count, 1);  // statistics (nn_flagged)
+        } else if (in) {
+            const double nxp = X[t.i], nyp = Y[t.i];
+            const double dx = qx[q] - nxp, dy = qy[q] - nyp;
+            out_idx[q] = t.i;
+            out_d2[q] = dx * dx + dy * dy;
+            if (out_pose) {
+                out_pose[3 * q] = nxp;
+                out_pose[3 * q + 1] = nyp;
+                out_pose[3 * q + 2] = YAW[t.i];
+            }
         }
     }
-}
-
-// Exact f64 brute force for the flagged samples: grid (kMaxChunks node chunks, kRescanSlots);
-// workgroup (c, s) scans chunk c for flagged samples s, s + kRescanSlots, ... and writes the
-// chunk's (d2, lowest index) partial.  The workgroup that completes a sample's last partial
-// merges all kMaxChunks of them and writes the exact nn_idx / nn_d2 / parent pose, so every later
-// kernel reads plain indices.
-__device__ inline void argmin_pair(double& d, int& i, double od, int oi) {
-    if (od < d || (od == d && oi < i)) {
-        d = od;
-        i = oi;
-    }
-}
-
-__global__ __launch_bounds__(256) void nn_rescan_kernel(
-    const DevState* __restrict__ st, const int* __restrict__ flag_list,
-    const double* __restrict__ qx, const double* __restrict__ qy, const double* __restrict__ X,
-    const double* __restrict__ Y, const double* __restrict__ YAW, double* __restrict__ rs_d2,
-    int* __restrict__ rs_idx, int* __restrict__ rs_done, int* __restrict__ nn_idx,
-    double* __restrict__ nn_d2, double* __restrict__ out_pose) {
-    __shared__ double s_d[256];
-    __shared__ int s_i[256];
-    __shared__ int s_last;
-    const int cnt = st->flag_count, n = st->n;
-    const int c = blockIdx.x;
-    const int cl = (n + kMaxChunks - 1) / kMaxChunks;
-    const int c0 = min(c * cl, n), c1 = min(c0 + cl, n);
-    for (int f = blockIdx.y; f < cnt; f += gridDim.y) {
-        const int q = flag_list[f];
-        const double x = qx[q], y = qy[q];
-        double best = __builtin_inf();
-        int bi = 0x7fffffff;
-        for (int k = c0 + (int)threadIdx.x; k < c1; k += 256) {
+    __syncthreads();
+    // near-ties: the exact f64 brute force, over the screen chunks whose f32 minimum could hide
+    // the exact nearest (f32 distance within the rounding bound of the f32 winner) and over the
+    // nodes appended after the screen; lowest index on exact ties (rrt.rs:378-391, Q9)
+    uint64_t fm = s_fmask;
+    const int tid = threadIdx.x;
+    while (fm) {
+        const int l = (int)__builtin_ctzll(fm);
+        fm &= fm - 1;
+        const int qf = blockIdx.x * 64 + l;
+        const double D1 = s_fd[l];
+        const double tc = 16.0 * eps_coord + 4.0e-6 * (D1 + 1.0);
+        if (tid < 64) {
+            const bool cand = tid < n_chunks &&
+                              !(sqrt((double)pbest[(size_t)tid * stride + qf]) > D1 + tc);
+            const uint64_t cm = __ballot(cand);
+            if (tid == 0) s_cmask = cm;
+        }
+        __syncthreads();
+        const uint64_t cm = s_cmask;
+        const int cl = scan_chunk_len(ns, chunks);
+        const double x = qx[qf], y = qy[qf];
+        double bd = __builtin_inf();
+        int bk = 0x7fffffff;
+        uint64_t mm = cm;
+        while (mm) {
+            const int c = (int)__builtin_ctzll(mm);
+            mm &= mm - 1;
+            const int c0 = c * cl, c1 = min(c0 + cl, ns);
+            for (int k = c0 + tid; k < c1; k += kFinThreads) {
+                const double dx = x - X[k], dy = y - Y[k];
+                argmin_pair(bd, bk, dx * dx + dy * dy, k);
+            }
+        }
+        for (int k = ns + tid; k < n; k += kFinThreads) {
             const double dx = x - X[k], dy = y - Y[k];
-            const double d2 = dx * dx + dy * dy;
-            if (d2 < best) {
-                best = d2;
-                bi = k;
-            }
+            argmin_pair(bd, bk, dx * dx + dy * dy, k);
         }
-        s_d[threadIdx.x] = best;
-        s_i[threadIdx.x] = bi;
-        __syncthreads();
-        for (int h = 128; h > 0; h >>= 1) {
-            if ((int)threadIdx.x < h) {
-                double d = s_d[threadIdx.x];
-                int i = s_i[threadIdx.x];
-                argmin_pair(d, i, s_d[threadIdx.x + h], s_i[threadIdx.x + h]);
-                s_d[threadIdx.x] = d;
-                s_i[threadIdx.x] = i;
-            }
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) {
-            rs_d2[(size_t)f * kMaxChunks + c] = s_d[0];
-            rs_idx[(size_t)f * kMaxChunks + c] = s_i[0] == 0x7fffffff ? -1 : s_i[0];
-            __threadfence();
-            s_last = atomicAdd(&rs_done[f], 1) == kMaxChunks - 1;
-        }
-        __syncthreads();
-        if (s_last && threadIdx.x < 64) {  // one wave merges the kMaxChunks partials
-            __threadfence();
-            const size_t o = (size_t)f * kMaxChunks + threadIdx.x;
-            const int ci = __hip_atomic_load(&rs_idx[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const double cd =
-                __hip_atomic_load(&rs_d2[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            double d = ci >= 0 ? cd : __builtin_inf();
-            int i = ci >= 0 ? ci : 0x7fffffff;
 #pragma unroll
-            for (int m = 32; m > 0; m >>= 1) argmin_pair(d, i, __shfl_xor(d, m), __shfl_xor(i, m));
-            if (threadIdx.x == 0) {
-                nn_idx[q] = i;
-                nn_d2[q] = d;
-                if (out_pose) {
-                    out_pose[3 * q] = X[i];
-                    out_pose[3 * q + 1] = Y[i];
-                    out_pose[3 * q + 2] = YAW[i];
-                }
-                rs_done[f] = 0;
+        for (int m = 32; m > 0; m >>= 1) argmin_pair(bd, bk, __shfl_xor(bd, m), __shfl_xor(bk, m));
+        if (lane == 0) {
+            s_rd[wave] = bd;
+            s_ri[wave] = bk;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double d = s_rd[0];
+            int i = s_ri[0];
+            for (int w = 1; w < kFinWaves; ++w) argmin_pair(d, i, s_rd[w], s_ri[w]);
+            out_idx[qf] = i;
+            out_d2[qf] = d;
+            if (out_pose) {
+                out_pose[3 * qf] = X[i];
+                out_pose[3 * qf + 1] = Y[i];
+                out_pose[3 * qf + 2] = YAW[i];
             }
         }
         __syncthreads();
@@ -1022,15 +1028,14 @@ __device__ inline Pt seg_end(int mode, double len, double c, double ox, double o
     return r;
 }
 
-// steer_prep: kPrepLanes lanes per task (persistent grid over the window's W + ncomp tasks).
-// compute_yaw (rrt.rs:267-271), dubins_path_planning's frame change and word choice
-// (dubins.rs:333-363, 401-408), the segment origins and the `pd += d` walk of
-// generate_local_course (dubins.rs:200-272).  Every transcendental sits at a call site all lanes
-// reach with per-lane arguments (lane r evaluates word r; one sin and one cos call give all the
-// segment trig), so a task's chain is ~9 calls deep instead of ~32.  The walk itself is serial
-// (each pd is the previous one plus d, rounded); all 8 lanes replay it and lane r stores the
-// points g with g % 8 == r.
-__global__ __launch_bounds__(256) void steer_prep_kernel(
+// steer_prep: kPrepLanes lanes per task, 8 tasks per wave (persistent grid over the
+// window's W + ncomp tasks): compute_yaw (rrt.rs:267-271),
+// dubins_path_planning's frame change and word choice (dubins.rs:333-363, 401-408) and the
+// segment origins.  Every transcendental sits at a call site all lanes reach with per-lane
+// arguments (lane r evaluates word r; one sin and one cos call give all the segment trig), so a
+// task's chain is ~9 calls deep instead of ~32.  The `pd += d` walk of generate_local_course
+// (dubins.rs:200-272) is left to steer_walk (lane-parallel, exact).
+__global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     const DevState* __restrict__ st, SceneDev sc, const double* __restrict__ wsx,
     const double* __restrict__ wsy, const double* __restrict__ snap_pose,
     CandEntry* __restrict__ cand, PrepRec* __restrict__ rec, double* __restrict__ pdbuf,
@@ -1039,15 +1044,14 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
     // with pnode < 0 is idle
     const int W = st->W;
     const int total = W + st->ncomp;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & (kPrepLanes - 1), g0 = lane & ~(kPrepLanes - 1);
-    const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    constexpr int TPW = 64 / kPrepLanes;  // tasks per wave
+    constexpr int TPW = 64 / kPrepLanes;  // tasks per wave in phase A
     const double step = sc.step_size;
     const double c = 1.0 / sc.turn_radius;
-    for (int base = gw * TPW; base < total; base += nw * TPW) {
-        const int t = base + lane / kPrepLanes;
+    constexpr int TPB = kPrepThreads / 64 * TPW;  // tasks per workgroup
+    for (int blk = blockIdx.x; blk * TPB < total; blk += gridDim.x) {
+        const int t = blk * TPB + wave * TPW + lane / kPrepLanes;
         bool act = t < total;
         int j = 0;
         double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0;
@@ -1194,52 +1198,13 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
         if (state == kPrepWalk && E.x == 0.0) state = kLiteral;
         int cnt0 = 0, cnt1 = 0, cnt2 = 0, fb_seg = 0;
         double fb_pd = 0.0, fb_dd = 0.0;
+        // no grid points are stored: steer_walk generates them all, lane-parallel and bit-exact,
+        // from the walk's initial state (segment 0, pd = d - 0.0, dubins.rs:239-241), and runs
+        // the trailing-zero check itself
         if (state == kPrepWalk) {
-            double* pdv = pdbuf + (size_t)t * kPdCap;
-            int g = 0, seg = 0;
-            double Ls = L0;
-            double dd = (L0 > 0.0) ? step : -step;
-            double pd = dd - 0.0;
-            bool over = false;
-            for (;;) {  // every iteration stores a point (g < kPdCap) or ends a segment
-                if (fabs(pd) <= fabs(Ls)) {
-                    if (g >= kPdCap) {  // keep the walk's state for steer_walk
-                        over = true;
-                        fb_seg = seg;
-                        fb_pd = pd;
-                        fb_dd = dd;
-                        if (seg == 0)
-                            cnt0 = g;
-                        else if (seg == 1)
-                            cnt1 = g - cnt0;
-                        else
-                            cnt2 = g - cnt0 - cnt1;
-                        break;
-                    }
-                    if ((g & (kPrepLanes - 1)) == r) pdv[g] = pd;
-                    ++g;
-                    pd += dd;
-                } else {
-                    if (seg == 0)
-                        cnt0 = g;
-                    else if (seg == 1)
-                        cnt1 = g - cnt0;
-                    else
-                        cnt2 = g - cnt0 - cnt1;
-                    const double ll = Ls - pd - dd;
-                    if (++seg == 3) break;
-                    const double Ln = seg == 1 ? L1 : L2;
-                    const double dn = (Ln > 0.0) ? step : -step;
-                    pd = ((Ls * Ln) > 0.0) ? (-dn - ll) : (dn - ll);
-                    dd = dn;
-                    Ls = Ln;
-                }
-            }
-            // no trailing zero left for the trim (or the reference's index panic): literal path
-            if (over)
-                state = kPrepFallback;
-            else if (1 + (long long)g > (long long)nq + 7 - 2)
-                state = kLiteral;
+            state = kPrepFallback;
+            fb_dd = (L0 > 0.0) ? step : -step;
+            fb_pd = fb_dd - 0.0;
         }
         if (t < total && r == 0) {  // idle batch tasks get a kReject record (act == false)
             PrepRec o;
@@ -1296,7 +1261,11 @@ __global__ __launch_bounds__(256) void steer_prep_kernel(
 // capturing its own point.
 template <bool kLds>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
-                                        const double* __restrict__ pdv) {
+                                        const double* __restrict__ pdv,
+                                        unsigned long long* stw = nullptr) {
+#ifndef PP_STAMPS_WALK
+    (void)stw;
+#endif
     const int lane = threadIdx.x & 63;
     const int state = p->state;
     const double x = p->x, y = p->y, px = p->px, py = p->py;
@@ -1306,7 +1275,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         return chunk_rejects<kLds>(sc, has, has, lane == 1, qx, qy) ? kReject : kAccept;
     }
     if (state != kPrepWalk && state != kPrepFallback) return state;
-    const bool partial = state == kPrepFallback;  // pdbuf holds the first kPdCap points only
+    const bool partial = state == kPrepFallback;  // pdbuf holds the first ng points only (0 or kPdCap)
     const double step = sc.step_size;
     const double c = p->c, cw = p->cw, sw = p->sw;
     const double ox1 = p->ox[1], oy1 = p->oy[1], ox2 = p->ox[2], oy2 = p->oy[2];
@@ -1319,14 +1288,20 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     int gseg = p->fb_seg;
     double gdd = p->fb_dd;
     double gpd = p->fb_pd;
-    long long grid = kPdCap;
+    long long grid = ng;  // grid points stored by steer_prep (0 or kPdCap for kPrepFallback)
     static_assert(kPdCap % 63 == 0, "stored points end on a chunk boundary");
     double carry_x = x, carry_y = y;
+#ifdef PP_STAMPS_WALK
+    int64_t sw_gen = 0, sw_pt = 0, sw_col = 0, sw_chunks = 0;
+#endif
     for (int base = 0;; base += 63) {
+#ifdef PP_STAMPS_WALK
+        const int64_t w0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+#endif
         int cnt = 0, my_seg = 0;
         double my_pd = 0.0;
         bool done;
-        const bool gen = partial && base >= kPdCap;
+        const bool gen = partial && base >= ng;
         if (gen) {
             // lane-parallel `pd += d` (dubins.rs:239-255): lane l >= pos replays l - pos
             // additions from the uniform start value — the serial walk's exact rounding
@@ -1335,10 +1310,29 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
             int pos = 1;
             while (pos <= 63 && gseg < 3) {
                 const double Ls = gseg == 0 ? L0 : (gseg == 1 ? L1 : L2);
+                // the serial chain w_u = gpd (+ gdd) x u is the same in every lane; lane pos + u
+                // captures w_u (the select is off the chain, so a step costs one f64 add
+                // latency).  Within a segment the passing values form a prefix (|pd| can only
+                // shrink before it grows), so the chain stops, 4 steps at a time, once its latest
+                // value fails; lanes past the last generated value count as failed
                 const int kk = lane - pos;
-                double v = gpd;
-                for (int u = 0; u < 63 - pos; ++u) v = (u < kk) ? v + gdd : v;
-                const uint64_t bad = __ballot(lane >= pos && !(fabs(v) <= fabs(Ls)));
+                const double aL = fabs(Ls);
+                const int umax = 63 - pos;
+                double v = gpd, w = gpd;
+                int u = 0;
+                bool ended = !(fabs(w) <= aL);
+                while (!ended && u < umax) {
+#pragma unroll
+                    for (int z = 0; z < 4; ++z) {
+                        if (u < umax) {
+                            w += gdd;
+                            ++u;
+                            if (u == kk) v = w;
+                        }
+                    }
+                    ended = !(fabs(w) <= aL);
+                }
+                const uint64_t bad = __ballot(lane >= pos && (kk > u || !(fabs(v) <= aL)));
                 const int m = bad ? (int)__builtin_ctzll(bad) : 64;
                 if (lane >= pos && lane < m) {
                     my_seg = gseg;
@@ -1372,6 +1366,9 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                 my_seg = g < n0 ? 0 : (g < n01 ? 1 : 2);
             }
         }
+#ifdef PP_STAMPS_WALK
+        const int64_t w1 = (int64_t)__builtin_amdgcn_s_memrealtime() + (int64_t)(my_pd * 0.0);
+#endif
         const bool junction_here = done && cnt < 63;
         const bool isgrid = lane >= 1 && lane <= cnt;
         const bool isj = junction_here && lane == cnt + 1;
@@ -1401,9 +1398,31 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
             qx = px;
             qy = py;
         }
+#ifdef PP_STAMPS_WALK
+        const int64_t w2 = (int64_t)__builtin_amdgcn_s_memrealtime() + (int64_t)(qx * 0.0);
+#endif
         const bool has = lane == 0 || isgrid || isj;
         const bool chk = isgrid || isj || (base == 0 && lane == 0);
+#ifdef PP_STAMPS_WALK
+        const bool rj_ = chunk_rejects<kLds>(sc, has, chk, has && lane >= 1, qx, qy);
+        const int64_t w3 = (int64_t)__builtin_amdgcn_s_memrealtime();
+        sw_gen += w1 - w0;
+        sw_pt += w2 - w1;
+        sw_col += w3 - w2;
+        sw_chunks += 1;
+        if (rj_ || junction_here) {
+            if (lane == 0) {
+                atomicAdd((unsigned long long*)&stw[0], (unsigned long long)sw_gen);
+                atomicAdd((unsigned long long*)&stw[1], (unsigned long long)sw_pt);
+                atomicAdd((unsigned long long*)&stw[2], (unsigned long long)sw_col);
+                atomicAdd((unsigned long long*)&stw[3], (unsigned long long)sw_chunks);
+                atomicAdd((unsigned long long*)&stw[4], 1ull);
+            }
+        }
+        if (rj_) return kReject;
+#else
         if (chunk_rejects<kLds>(sc, has, chk, has && lane >= 1, qx, qy)) return kReject;
+#endif
         if (junction_here) break;
         carry_x = __shfl(qx, 63);
         carry_y = __shfl(qy, 63);
@@ -1431,11 +1450,22 @@ __global__ __launch_bounds__(256, 4) void steer_walk_kernel(DevState* __restrict
     const int W = st->W;
     const int total = W + st->ncomp;
     if ((int)blockIdx.x * 4 >= total) return;  // whole workgroup idle
+#ifdef PP_STAMPS_WALK
+    const int64_t ws0 = (int64_t)__builtin_amdgcn_s_memrealtime();
     if (kLds) stage_scene(sc);
+    if (threadIdx.x == 0) {
+        atomicAdd((unsigned long long*)&st->stamps[5], (unsigned long long)((int64_t)__builtin_amdgcn_s_memrealtime() - ws0));
+        atomicAdd((unsigned long long*)&st->stamps[6], 1ull);
+    }
+    unsigned long long* stw = (unsigned long long*)st->stamps;
+#else
+    if (kLds) stage_scene(sc);
+    unsigned long long* stw = nullptr;
+#endif
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     for (int t = gw; t < total; t += nw) {
-        const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap);
+        const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, stw);
         if (lane == 0) {
             if (t < W) {
                 snap_status[t] = s;
@@ -1448,10 +1478,9 @@ __global__ __launch_bounds__(256, 4) void steer_walk_kernel(DevState* __restrict
     }
 }
 
-// A resolve repair (one wave): the (child, parent pose) pair steered and collision-checked anew.
-// Out of line, so the resolve's round loop stays a few KB of code (it is cold in the instruction
-// cache at every window: the other window kernels run in between).
-__device__ __attribute__((noinline)) int resolve_repair(const SceneDev& sc, double x, double y,
+// A resolve repair (one wave): the (child, parent pose) pair steered and collision-checked anew
+// (only resolve_tail_kernel compiles it: inlined there it needs no scratch).
+__device__ __forceinline__ int resolve_repair(const SceneDev& sc, double x, double y,
                                                         double yaw, double px, double py,
                                                         double pyaw, int lit, double* bx) {
     return lit ? steer_collide_literal(sc, x, y, yaw, px, py, pyaw, bx, bx + kLiteralCap,
@@ -1894,14 +1923,14 @@ __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
             const int W = st->W;
             if (W > 0) {
                 const int q = 1 - a.p;
-                if (!resolve_role<false, kScanThreads>(st, a.sc, a.tr, a.wsx[q], a.wsy[q], a.nn_idx,
+                if (!resolve_role<kWinRepair, kScanThreads>(st, a.sc, a.tr, a.wsx[q], a.wsy[q], a.nn_idx,
                                                        a.cand_cnt, a.cand, a.pend, a.snap_status,
                                                        a.snap_yaw, a.fin_par, a.rs, a.lit_scratch,
                                                        W, smem)) {
                     if (threadIdx.x == 0) st->resolve_bail = 1;  // resolve_tail_kernel redoes it
                     return;
                 }
-                __threadfence();
+                // (same workgroup: the barrier's workgroup-scope fence orders these stores)
                 __syncthreads();
                 commit_role<kScanThreads>(st, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.snap_status,
                                           a.snap_yaw, a.fin_par, a.cand_cnt, W,
@@ -1930,7 +1959,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_tail_kernel(WinKArgs 
     resolve_role<true, kResolveThreads>(st, a.sc, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.cand_cnt,
                                          a.cand, a.pend, a.snap_status, a.snap_yaw, a.fin_par,
                                          a.rs, a.lit_scratch, W, smem);
-    __threadfence();
+    // (same workgroup: the barrier's workgroup-scope fence orders these stores)
     __syncthreads();
     commit_role<kResolveThreads>(st, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.snap_status,
                                  a.snap_yaw, a.fin_par, a.cand_cnt, W, a.scan ? a.seq : -1, smem);
@@ -2336,7 +2365,7 @@ hipError_t launch_mq_init(hipStream_t s, const MqDev& mq, const double* starts) 
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int Q = a.mq.Q;
     const int nn_blocks = std::min((Q + 3) / 4, 4096);
-    const int prep_blocks = std::min((Q * kPrepLanes + 255) / 256, 2048);
+    const int prep_blocks = std::min((Q + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walk_blocks = std::min((Q + 3) / 4, 1024);
     const int ins_blocks = std::min((Q + 255) / 256, kLiteralWaves / 4);
     const int lds = a.sc.lds_bytes;
@@ -2345,7 +2374,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
         mq_sample_nn_kernel<<<nn_blocks, 256, 0, s>>>(a.mq, a.sc.minx, a.sc.maxx, a.sc.miny,
                                                       a.sc.maxy, a.tasks);
         if (a.ev) (void)hipEventRecord(a.ev[2 * k + 1], s);
-        steer_prep_kernel<<<prep_blocks, 256, 0, s>>>(a.st, a.sc, nullptr, nullptr, nullptr,
+        steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, nullptr, nullptr, nullptr,
                                                       nullptr, a.rec, a.pdbuf, a.yaw, a.tasks);
         if (lds > 0)
             steer_walk_kernel<true><<<walk_blocks, 256, lds, s>>>(a.st, a.sc, a.rec, a.pdbuf,
@@ -2411,19 +2440,16 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     if (ev) (void)hipEventRecord(ev[0], s);
     window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
     if (ev) (void)hipEventRecord(ev[1], s);
-    if (resolve_prev) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
+    if (resolve_prev && !kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
     nn_finalize_kernel<<<(K + 63) / 64, kFinThreads, 0, s>>>(
         a.st, p, seq, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, wsx, wsy, a.tr.x32, a.tr.y32,
-        a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose, a.flag_list);
-    nn_rescan_kernel<<<dim3(kMaxChunks, kRescanSlots), 256, 0, s>>>(
-        a.st, a.flag_list, wsx, wsy, a.tr.x, a.tr.y, a.tr.yaw, a.rs_d2, a.rs_idx, a.rs_done,
-        a.nn_idx, a.nn_d2, a.snap_pose);
+        a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose);
     window_pairs_kernel<<<Tp * (Tp + 1) / 2, kPairTile, 0, s>>>(a.st, wsx, wsy, a.nn_d2,
                                                                 a.cand_cnt, a.cand, a.pend);
     if (ev) (void)hipEventRecord(ev[2], s);
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
-    const int prep_blocks = (2 * K * kPrepLanes + 255) / 256;
-    steer_prep_kernel<<<prep_blocks, 256, 0, s>>>(a.st, a.sc, wsx, wsy, a.snap_pose, a.cand,
+    const int prep_blocks = (2 * K + kPrepThreads / 8 - 1) / (kPrepThreads / 8);
+    steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, wsx, wsy, a.snap_pose, a.cand,
                                                   a.rec, a.pdbuf, a.snap_yaw, nullptr);
     const int lds = a.sc.lds_bytes;
     const int nwg = std::min((K + 3) / 4, 1024);
@@ -2440,7 +2466,7 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
 hipError_t launch_drain(hipStream_t s, const WindowArgs& a, int64_t seq_next) {
     const WinKArgs wk = win_args(a, (int)(seq_next & 1), 1, 1, 0, seq_next);
     window_kernel<<<1, kScanThreads, 0, s>>>(wk);
-    resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
+    if (!kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
     return hipGetLastError();
 }
 
@@ -2450,10 +2476,7 @@ hipError_t launch_nearest(hipStream_t s, const WindowArgs& a) {
     window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
     nn_finalize_kernel<<<(K + 63) / 64, kFinThreads, 0, s>>>(
         a.st, 0, 0, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, a.wsx, a.wsy, a.tr.x32,
-        a.tr.y32, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, nullptr, a.flag_list);
-    nn_rescan_kernel<<<dim3(kMaxChunks, kRescanSlots), 256, 0, s>>>(
-        a.st, a.flag_list, a.wsx, a.wsy, a.tr.x, a.tr.y, a.tr.yaw, a.rs_d2, a.rs_idx, a.rs_done,
-        a.nn_idx, a.nn_d2, nullptr);
+        a.tr.y32, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, nullptr);
     return hipGetLastError();
 }
 

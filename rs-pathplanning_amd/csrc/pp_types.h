@@ -18,14 +18,14 @@ enum : int {
 
 constexpr int kCandCap = 16;         // in-window nearer-sample entries kept per sample
 constexpr int kMaxChunks = 64;       // node chunks of the NN screen (partials per sample)
-constexpr int kRescanSlots = 32;     // flagged samples rescanned concurrently (grid y)
 constexpr int kLiteralCap = 16384;   // points per literal-path scratch buffer
 constexpr int kLiteralWaves = 256;   // literal scratch buffers (explicit-task kernel)
 constexpr int kResolveThreads = 512;  // resolve_tail_kernel (8 waves, 256 VGPRs: the repair path)
 constexpr int kMaxWindow = 4096;     // K limit: the resolve keeps the window's state in LDS
 constexpr int kSteerPrepBytes = 152; // sizeof(SteerPrep) (checked in pp_kernels.hip)
 constexpr int kPdCap = 63;           // grid points per task stored by steer_prep (one walk chunk)
-constexpr int kPrepLanes = 8;        // lanes per task in steer_prep
+constexpr int kPrepLanes = 8;        // lanes per task in steer_prep's phase A
+constexpr int kPrepThreads = 256;    // steer_prep workgroup: 32 tasks (8 per wave)
 constexpr int kCfMaxDepth = 8192;    // check_finish: ancestor path staged in LDS (32 KB)
 constexpr int kCfLevels = 16;        // RECURSION_LIMIT, rrt.rs:14
 constexpr int kCfMaxEdges = kCfLevels + 1 + kCfMaxDepth;
