@@ -99,9 +99,11 @@ struct pp_ctx {
     int m = 0;
     DBuf<double> d_cx, d_cy, d_r2, d_rcull;
     DBuf<int> d_goff, d_gitems;
+    DBuf<uint4> d_img, d_gimg;  // LDS images (discs / occupancy bits), contiguous
     double gx0 = 0, gy0 = 0, ginv = 1;
     int gnx = 1, gny = 1;
-    int lds_bytes = 0, lds_goff = 0, lds_items = 0, lds_cx = 0, lds_cy = 0, lds_r2 = 0;
+    int lds_bytes = 0, lds_goff = 0, lds_items = 0, lds_cx = 0, lds_cy = 0, lds_r2 = 0, lds_d4 = 0;
+    DBuf<float4> d_d4;
     // occupancy grid (config 4)
     bool has_grid = false;
     DBuf<uint32_t> d_bits;
@@ -198,6 +200,8 @@ struct pp_ctx {
         s.lds_cx = lds_cx;
         s.lds_cy = lds_cy;
         s.lds_r2 = lds_r2;
+        s.d4 = d_d4.p;
+        s.lds_d4 = lds_d4;
         s.bits = has_grid ? d_bits.p : nullptr;
         s.bw = bw;
         s.bh = bh;
@@ -205,7 +209,11 @@ struct pp_ctx {
         s.bx0 = bx0;
         s.by0 = by0;
         s.binv = binv;
-        if (has_grid) s.lds_bytes = lds_bits_bytes;
+        s.img = d_img.p;
+        if (has_grid) {
+            s.lds_bytes = lds_bits_bytes;
+            s.img = d_gimg.p;
+        }
         return s;
     }
     TreeDev tree_dev() const {
@@ -540,10 +548,13 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
     if (!(minx < maxx) || !(miny < maxy))  // gen_range asserts low < high (rrt.rs:142-143)
         return set_err(PP_ERR_INVALID_ARGUMENT, "shrunken bounds are empty");
     std::vector<double> r2(m), rc_(m);
+    std::vector<float4> d4(m);
     for (int k = 0; k < m; ++k) {
         const double reff = r[k] + half;
         r2[k] = reff * reff;
         rc_[k] = reff * (1.0 + 1e-9) + 1e-9;
+        // f32 cull copy: the radius rounded up (the cull only ever over-includes)
+        d4[k] = make_float4((float)cx[k], (float)cy[k], std::nextafter((float)rc_[k], 1e30f), 0.0f);
     }
     // uniform grid over the discs (square cells, about one cell per disc)
     const double spanx = maxx - minx, spany = maxy - miny;
@@ -576,21 +587,31 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
     PP_HIP(hipMemcpy(ctx->d_goff.p, goff.data(), goff.size() * sizeof(int), hipMemcpyHostToDevice));
     if (!gitems.empty())
         PP_HIP(hipMemcpy(ctx->d_gitems.p, gitems.data(), gitems.size() * sizeof(int), hipMemcpyHostToDevice));
-    {  // LDS image for the steer kernels: [goff | items | cx | cy | r2], 16-byte aligned parts
+    {  // LDS image for the steer kernels: [goff | items | d4], 16-byte aligned parts (the f64
+       // discs of the exact test stay in global memory: the f32 cull leaves few exact tests)
         auto al = [](size_t b) { return (int)((b + 15) & ~(size_t)15); };
         const int o_goff = 0;
         const int o_items = o_goff + al(goff.size() * sizeof(int));
-        const int o_cx = o_items + al(gitems.size() * sizeof(int));
-        const int o_cy = o_cx + al((size_t)m * sizeof(double));
-        const int o_r2 = o_cy + al((size_t)m * sizeof(double));
-        const int total = o_r2 + al((size_t)m * sizeof(double));
+        const int o_d4 = o_items + al(gitems.size() * sizeof(int));
+        const int o_cx = -1, o_cy = -1, o_r2 = -1;
+        const int total = o_d4 + al((size_t)m * sizeof(float4));
         const bool fits = total <= 64 * 1024;  // 2 workgroups per CU fit in 160 KB
         ctx->lds_bytes = fits ? total : 0;
+        if (fits) {  // the same image, contiguous in global memory (stage_scene copies it whole)
+            std::vector<char> img((size_t)total, 0);
+            std::memcpy(img.data() + o_goff, goff.data(), goff.size() * sizeof(int));
+            if (!gitems.empty())
+                std::memcpy(img.data() + o_items, gitems.data(), gitems.size() * sizeof(int));
+            for (int k = 0; k < m; ++k) std::memcpy(img.data() + o_d4 + 16 * k, &d4[k], 16);
+            PP_HIP(ctx->d_img.reserve((size_t)total / 16));
+            PP_HIP(hipMemcpy(ctx->d_img.p, img.data(), (size_t)total, hipMemcpyHostToDevice));
+        }
         ctx->lds_goff = o_goff;
         ctx->lds_items = o_items;
         ctx->lds_cx = o_cx;
         ctx->lds_cy = o_cy;
         ctx->lds_r2 = o_r2;
+        ctx->lds_d4 = o_d4;
     }
     ctx->gx0 = minx;
     ctx->gy0 = miny;
@@ -602,11 +623,13 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
     PP_HIP(ctx->d_cy.reserve(mm));
     PP_HIP(ctx->d_r2.reserve(mm));
     PP_HIP(ctx->d_rcull.reserve(mm));
+    PP_HIP(ctx->d_d4.reserve(mm));
     if (m > 0) {
         PP_HIP(hipMemcpy(ctx->d_cx.p, cx, m * sizeof(double), hipMemcpyHostToDevice));
         PP_HIP(hipMemcpy(ctx->d_cy.p, cy, m * sizeof(double), hipMemcpyHostToDevice));
         PP_HIP(hipMemcpy(ctx->d_r2.p, r2.data(), m * sizeof(double), hipMemcpyHostToDevice));
         PP_HIP(hipMemcpy(ctx->d_rcull.p, rc_.data(), m * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_d4.p, d4.data(), m * sizeof(float4), hipMemcpyHostToDevice));
     }
     ctx->minx = minx;
     ctx->maxx = maxx;
@@ -638,7 +661,14 @@ int pp_space_set_grid(pp_ctx* ctx, const uint32_t* bits, int w, int h, double x0
     ctx->bx0 = x0;
     ctx->by0 = y0;
     ctx->binv = 1.0 / cell;
-    ctx->lds_bits_bytes = n * sizeof(uint32_t) <= 64 * 1024 ? (int)(n * sizeof(uint32_t)) : 0;
+    const size_t img_bytes = (n * sizeof(uint32_t) + 15) & ~(size_t)15;
+    ctx->lds_bits_bytes = img_bytes <= 64 * 1024 ? (int)img_bytes : 0;
+    if (ctx->lds_bits_bytes) {
+        std::vector<uint32_t> img(img_bytes / 4, 0u);
+        std::memcpy(img.data(), bits, n * sizeof(uint32_t));
+        PP_HIP(ctx->d_gimg.reserve(img_bytes / 16));
+        PP_HIP(hipMemcpy(ctx->d_gimg.p, img.data(), img_bytes, hipMemcpyHostToDevice));
+    }
     ctx->has_grid = true;
     ctx->has_rrt = false;  // the planner's Space changed (rrt.rs:342)
     return PP_OK;

@@ -44,28 +44,25 @@ __device__ inline int grid_cell(double v, double v0, double inv, int n) {
 // Dynamic LDS of the steer kernels: the scene image (SceneDev::lds_*) when kLds.
 extern __shared__ __attribute__((aligned(16))) char pp_smem[];
 
-// Copy the scene's grid and discs into this workgroup's LDS image (all threads call it).
+// Copy the scene's LDS image (disc grid + discs, or the occupancy bits) into this workgroup's LDS
+// (all threads call it): 16-byte words, 8 loads in flight per thread before their stores.
 __device__ inline void stage_scene(const SceneDev& sc) {
-    if (sc.bits) {  // occupancy grid: the bit words only
-        uint32_t* B = reinterpret_cast<uint32_t*>(pp_smem);
-        const int nw = sc.bh * sc.bwords;
-        for (int k = threadIdx.x; k < nw; k += blockDim.x) B[k] = sc.bits[k];
-        __syncthreads();
-        return;
-    }
-    const int ncell = sc.gnx * sc.gny + 1;
-    const int nitem = sc.goff[ncell - 1];
-    int* goff = reinterpret_cast<int*>(pp_smem + sc.lds_goff);
-    int* items = reinterpret_cast<int*>(pp_smem + sc.lds_items);
-    double* cx = reinterpret_cast<double*>(pp_smem + sc.lds_cx);
-    double* cy = reinterpret_cast<double*>(pp_smem + sc.lds_cy);
-    double* r2 = reinterpret_cast<double*>(pp_smem + sc.lds_r2);
-    for (int k = threadIdx.x; k < ncell; k += blockDim.x) goff[k] = sc.goff[k];
-    for (int k = threadIdx.x; k < nitem; k += blockDim.x) items[k] = sc.gitems[k];
-    for (int k = threadIdx.x; k < sc.m; k += blockDim.x) {
-        cx[k] = sc.cx[k];
-        cy[k] = sc.cy[k];
-        r2[k] = sc.r2[k];
+    constexpr int U = 8;
+    const int n16 = sc.lds_bytes >> 4;
+    uint4* dst = reinterpret_cast<uint4*>(pp_smem);
+    const int nt = blockDim.x;
+    for (int base = threadIdx.x; base < n16; base += nt * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: all U stay in flight
+            const int k = min(base + u * nt, n16 - 1);
+            v[u] = sc.img[k];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = base + u * nt;
+            if (k < n16) dst[k] = v[u];
+        }
     }
     __syncthreads();
 }
@@ -102,9 +99,15 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const int cy1 = __builtin_amdgcn_readfirstlane(grid_cell(by1, sc.gy0, sc.ginv, sc.gny));
     const int* goff = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_goff) : sc.goff;
     const int* items = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_items) : sc.gitems;
-    const double* dcx = kLds ? reinterpret_cast<const double*>(pp_smem + sc.lds_cx) : sc.cx;
-    const double* dcy = kLds ? reinterpret_cast<const double*>(pp_smem + sc.lds_cy) : sc.cy;
-    const double* dr2 = kLds ? reinterpret_cast<const double*>(pp_smem + sc.lds_r2) : sc.r2;
+    const double* dcx = sc.cx;  // exact test: f64 discs from global memory (L2)
+    const double* dcy = sc.cy;
+    const double* dr2 = sc.r2;
+    const float4* d4 = kLds ? reinterpret_cast<const float4*>(pp_smem + sc.lds_d4) : sc.d4;
+    // per-lane f32 cull: a segment a-b can only touch a disc (exact test below) if
+    // |a - c| <= rcull + |b - a|; 1e-3 of slack covers the f32 rounding of coordinates <= 2^10
+    const float axf = (float)ax, ayf = (float)ay;
+    const float vxf = (float)(qx - ax), vyf = (float)(qy - ay);
+    const float Lf = __builtin_sqrtf(vxf * vxf + vyf * vyf) * 1.000001f + 1.0e-3f;
     for (int gy = cy0; gy <= cy1; ++gy) {
         for (int gx = cx0; gx <= cx1; ++gx) {
             const int cell = gy * sc.gnx + gx;
@@ -114,7 +117,11 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
                 if (ph) ph[1] += 1;
 #endif
                 const int d = items[k];
-                const bool hit = seg_valid && seg_hits_disc(ax, ay, qx, qy, dcx[d], dcy[d], dr2[d]);
+                const float4 D = d4[d];
+                const float dxf = D.x - axf, dyf = D.y - ayf, thr = D.z + Lf;
+                const bool near = seg_valid && dxf * dxf + dyf * dyf <= thr * thr;
+                if (!__any(near)) continue;
+                const bool hit = near && seg_hits_disc(ax, ay, qx, qy, dcx[d], dcy[d], dr2[d]);
                 if (__any(hit)) return true;
             }
         }
@@ -1261,7 +1268,7 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
 // capturing its own point.
 template <bool kLds>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
-                                        const double* __restrict__ pdv,
+                                        const double* __restrict__ pdv, double* __restrict__ gs,
                                         unsigned long long* stw = nullptr) {
 #ifndef PP_STAMPS_WALK
     (void)stw;
@@ -1310,28 +1317,40 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
             int pos = 1;
             while (pos <= 63 && gseg < 3) {
                 const double Ls = gseg == 0 ? L0 : (gseg == 1 ? L1 : L2);
-                // the serial chain w_u = gpd (+ gdd) x u is the same in every lane; lane pos + u
-                // captures w_u (the select is off the chain, so a step costs one f64 add
-                // latency).  Within a segment the passing values form a prefix (|pd| can only
-                // shrink before it grows), so the chain stops, 4 steps at a time, once its latest
-                // value fails; lanes past the last generated value count as failed
+                // the serial chain w_u = gpd (+ gdd) x u is the same in every lane: one f64 add
+                // per step, lane 0 parks the values in the wave's LDS slots (gs) and lane pos + u
+                // picks w_u up afterwards.  Within a segment the passing values form a prefix
+                // (|pd| can only shrink before it grows), so the chain stops, 4 steps at a time,
+                // once its latest value fails; lanes past the last generated value count as failed
                 const int kk = lane - pos;
                 const double aL = fabs(Ls);
                 const int umax = 63 - pos;
-                double v = gpd, w = gpd;
+                double w = gpd;
+                if (lane == 0) gs[0] = w;
                 int u = 0;
                 bool ended = !(fabs(w) <= aL);
+#ifdef PP_T_NOGEN
+                if (lane <= umax) gs[lane] = gpd + lane * gdd;  // timing experiment only
+                u = umax;
+                ended = true;
+#endif
                 while (!ended && u < umax) {
+                    double t4[4];
 #pragma unroll
                     for (int z = 0; z < 4; ++z) {
-                        if (u < umax) {
-                            w += gdd;
-                            ++u;
-                            if (u == kk) v = w;
-                        }
+                        w += gdd;
+                        t4[z] = w;
                     }
+                    if (lane == 0) {
+#pragma unroll
+                        for (int z = 0; z < 4; ++z) gs[u + 1 + z] = t4[z];
+                    }
+                    u += 4;
                     ended = !(fabs(w) <= aL);
                 }
+                u = min(u, umax);
+                __builtin_amdgcn_wave_barrier();
+                const double v = (kk >= 0 && kk <= u) ? gs[kk] : gpd;
                 const uint64_t bad = __ballot(lane >= pos && (kk > u || !(fabs(v) <= aL)));
                 const int m = bad ? (int)__builtin_ctzll(bad) : 64;
                 if (lane >= pos && lane < m) {
@@ -1402,7 +1421,15 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         const int64_t w2 = (int64_t)__builtin_amdgcn_s_memrealtime() + (int64_t)(qx * 0.0);
 #endif
         const bool has = lane == 0 || isgrid || isj;
+#ifdef PP_T_NOCOL
+        const bool chk = false;  // timing experiment only
+        if (junction_here) break;
+        carry_x = __shfl(qx, 63);
+        carry_y = __shfl(qy, 63);
+        continue;
+#else
         const bool chk = isgrid || isj || (base == 0 && lane == 0);
+#endif
 #ifdef PP_STAMPS_WALK
         const bool rj_ = chunk_rejects<kLds>(sc, has, chk, has && lane >= 1, qx, qy);
         const int64_t w3 = (int64_t)__builtin_amdgcn_s_memrealtime();
@@ -1434,11 +1461,17 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
 
 // steer_walk, one task per wave (persistent grid, grid-stride over the W + ncomp tasks); kLds:
 // the scene's disc grid is staged into this workgroup's LDS first.
+constexpr int kGenSlots = 68;  // per-wave LDS slots of the point generator (63 + 4 overshoot + 1)
+constexpr int kWalkMaxWG = 768;  // 3 resident workgroups per CU
+__host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
+    return scene_bytes + kWalkThreads / 64 * kGenSlots * 8;
+}
+
 // Window mode (pend != nullptr): a snapshot task whose verdict is not final (literal path,
 // error) and that has no nearer window sample is queued for the resolve (the others were queued
 // by window_pairs).
 template <bool kLds>
-__global__ __launch_bounds__(256, 4) void steer_walk_kernel(DevState* __restrict__ st,
+__global__ __launch_bounds__(kWalkThreads) void steer_walk_kernel(DevState* __restrict__ st,
                                                          SceneDev sc,
                                                          const PrepRec* __restrict__ rec,
                                                          const double* __restrict__ pdbuf,
@@ -1449,7 +1482,7 @@ __global__ __launch_bounds__(256, 4) void steer_walk_kernel(DevState* __restrict
     const int lane = threadIdx.x & 63;
     const int W = st->W;
     const int total = W + st->ncomp;
-    if ((int)blockIdx.x * 4 >= total) return;  // whole workgroup idle
+    if ((int)blockIdx.x * (kWalkThreads / 64) >= total) return;  // whole workgroup idle
 #ifdef PP_STAMPS_WALK
     const int64_t ws0 = (int64_t)__builtin_amdgcn_s_memrealtime();
     if (kLds) stage_scene(sc);
@@ -1464,8 +1497,10 @@ __global__ __launch_bounds__(256, 4) void steer_walk_kernel(DevState* __restrict
 #endif
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) +
+                 (threadIdx.x >> 6) * kGenSlots;  // this wave's generator slots
     for (int t = gw; t < total; t += nw) {
-        const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, stw);
+        const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, stw);
         if (lane == 0) {
             if (t < W) {
                 snap_status[t] = s;
@@ -2366,7 +2401,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int Q = a.mq.Q;
     const int nn_blocks = std::min((Q + 3) / 4, 4096);
     const int prep_blocks = std::min((Q + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
-    const int walk_blocks = std::min((Q + 3) / 4, 1024);
+    const int walk_blocks = std::min((Q + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
     const int ins_blocks = std::min((Q + 255) / 256, kLiteralWaves / 4);
     const int lds = a.sc.lds_bytes;
     for (int k = 0; k < steps; ++k) {
@@ -2377,11 +2412,11 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
         steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, nullptr, nullptr, nullptr,
                                                       nullptr, a.rec, a.pdbuf, a.yaw, a.tasks);
         if (lds > 0)
-            steer_walk_kernel<true><<<walk_blocks, 256, lds, s>>>(a.st, a.sc, a.rec, a.pdbuf,
+            steer_walk_kernel<true><<<walk_blocks, kWalkThreads, walk_lds_bytes(lds), s>>>(a.st, a.sc, a.rec, a.pdbuf,
                                                                   nullptr, a.status, nullptr,
                                                                   nullptr);
         else
-            steer_walk_kernel<false><<<walk_blocks, 256, 0, s>>>(a.st, a.sc, a.rec, a.pdbuf,
+            steer_walk_kernel<false><<<walk_blocks, kWalkThreads, walk_lds_bytes(0), s>>>(a.st, a.sc, a.rec, a.pdbuf,
                                                                  nullptr, a.status, nullptr,
                                                                  nullptr);
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
@@ -2452,12 +2487,13 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, wsx, wsy, a.snap_pose, a.cand,
                                                   a.rec, a.pdbuf, a.snap_yaw, nullptr);
     const int lds = a.sc.lds_bytes;
-    const int nwg = std::min((K + 3) / 4, 1024);
+    // snapshot tasks plus the usual few candidate tasks in one round of waves
+    const int nwg = std::min((K + K / 4 + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
     if (lds > 0)
-        steer_walk_kernel<true><<<nwg, 256, lds, s>>>(a.st, a.sc, a.rec, a.pdbuf, a.cand,
+        steer_walk_kernel<true><<<nwg, kWalkThreads, walk_lds_bytes(lds), s>>>(a.st, a.sc, a.rec, a.pdbuf, a.cand,
                                                       a.snap_status, a.cand_cnt, a.pend);
     else
-        steer_walk_kernel<false><<<nwg, 256, 0, s>>>(a.st, a.sc, a.rec, a.pdbuf, a.cand,
+        steer_walk_kernel<false><<<nwg, kWalkThreads, walk_lds_bytes(0), s>>>(a.st, a.sc, a.rec, a.pdbuf, a.cand,
                                                      a.snap_status, a.cand_cnt, a.pend);
     if (ev) (void)hipEventRecord(ev[3], s);
     return hipGetLastError();

@@ -3,6 +3,8 @@
 
 #include <stdint.h>
 
+#include <hip/hip_runtime.h>  // uint4
+
 namespace ppamd {
 
 // dubins_literal return codes
@@ -26,6 +28,7 @@ constexpr int kSteerPrepBytes = 152; // sizeof(SteerPrep) (checked in pp_kernels
 constexpr int kPdCap = 63;           // grid points per task stored by steer_prep (one walk chunk)
 constexpr int kPrepLanes = 8;        // lanes per task in steer_prep's phase A
 constexpr int kPrepThreads = 256;    // steer_prep workgroup: 32 tasks (8 per wave)
+constexpr int kWalkThreads = 512;    // steer_walk workgroup: 8 tasks at a time (3 workgroups per CU)
 constexpr int kCfMaxDepth = 8192;    // check_finish: ancestor path staged in LDS (32 KB)
 constexpr int kCfLevels = 16;        // RECURSION_LIMIT, rrt.rs:14
 constexpr int kCfMaxEdges = kCfLevels + 1 + kCfMaxDepth;
@@ -50,7 +53,11 @@ struct SceneDev {
     // LDS image of (goff, gitems, cx, cy, r2) — or of the occupancy bits — staged by the steer
     // kernels when it fits
     int lds_bytes;  // 0: read the scene from global memory
+    const uint4* img;  // the LDS image, contiguous in global memory (lds_bytes / 16 words)
     int lds_goff, lds_items, lds_cx, lds_cy, lds_r2;  // byte offsets inside the image
+    // the discs in f32 for the per-lane cull: (cx, cy, rcull rounded up, 0)
+    const float4* d4;
+    int lds_d4;
     // occupancy grid (BASELINE config 4): when bits != nullptr the discs are ignored and every
     // polyline point probes its cell: (i, j) = (floor((x - bx0) * binv), floor((y - by0) * binv)),
     // bit i % 32 of word j * bwords + i / 32; a point outside the grid counts as occupied

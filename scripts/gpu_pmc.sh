@@ -9,7 +9,9 @@ cd /tmp && export TMPDIR=/tmp
 A="--steps 20 --warmup 3 --no-cpu-baseline --no-size-sweep ${BENCH_ARGS:-}"
 K="${KERNEL:-window_kernel}"
 i=0
-for grp in "GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES" "SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU" "SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_SMEM" "SQ_WAIT_ANY SQ_INSTS_LDS SQ_INST_CYCLES_VMEM" "FETCH_SIZE" "WRITE_SIZE"; do
+GROUPS=${GROUPS:-"GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES|SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU|SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_SMEM|SQ_WAIT_ANY SQ_INSTS_LDS SQ_INST_CYCLES_VMEM|FETCH_SIZE|WRITE_SIZE"}
+IFS='|' read -ra GRPS <<< "$GROUPS"
+for grp in "${GRPS[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp -T -f csv --kernel-include-regex "$K" -d "$OUT/p$i" -o run -- python3 "$R/bench.py" $A > "$OUT/p$i.log" 2>&1 || { tail -5 "$OUT/p$i.log"; exit 1; }
 done
