@@ -131,7 +131,7 @@ struct pp_ctx {
     int K = 4096;
     int Kcap = 0;
     DBuf<double> wsx, wsy, nn_d2, snap_yaw, snap_pose;
-    DBuf<float> pbest, psecond;
+    DBuf<float> pbest, psecond, wsx32, wsy32;
     DBuf<int> pidx, nn_idx, cand_cnt, snap_status;
     DBuf<CandEntry> cand;
     DBuf<PrepRec> rec;   // per-task steer records
@@ -237,6 +237,8 @@ struct pp_ctx {
         a.tr = tree_dev();
         a.wsx = wsx.p;
         a.wsy = wsy.p;
+        a.wsx32 = wsx32.p;
+        a.wsy32 = wsy32.p;
         a.pbest = pbest.p;
         a.psecond = psecond.p;
         a.pidx = pidx.p;
@@ -277,6 +279,8 @@ int ensure_window(pp_ctx* c, int K) {
     const size_t k = (size_t)K;
     PP_HIP(c->wsx.reserve(2 * k));  // double-buffered by window parity
     PP_HIP(c->wsy.reserve(2 * k));
+    PP_HIP(c->wsx32.reserve(2 * k));
+    PP_HIP(c->wsy32.reserve(2 * k));
     PP_HIP(c->pbest.reserve(k * kMaxChunks));
     PP_HIP(c->psecond.reserve(k * kMaxChunks));
     PP_HIP(c->pidx.reserve(k * kMaxChunks));

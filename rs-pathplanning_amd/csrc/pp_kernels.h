@@ -19,6 +19,8 @@ struct WindowArgs {
     TreeDev tr{};
     double* wsx = nullptr;        // [2 * Kcap] samples, double-buffered by window parity
     double* wsy = nullptr;
+    float* wsx32 = nullptr;       // [2 * Kcap] their f32 copies
+    float* wsy32 = nullptr;
     float* pbest = nullptr;
     float* psecond = nullptr;
     int* pidx = nullptr;

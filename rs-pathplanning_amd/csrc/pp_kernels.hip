@@ -550,6 +550,8 @@ struct WinKArgs {
     uint64_t seed;
     double* wsx[2];
     double* wsy[2];
+    float* wsx32[2];    // f32 copies (the pair search's prefilter)
+    float* wsy32[2];
     float* pbest;
     float* psecond;
     int* pidx;
@@ -623,6 +625,8 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
                 if (c == 0 && wave == 0) {
                     qxo[q] = x;
                     qyo[q] = y;
+                    a.wsx32[a.p][q] = (float)x;
+                    a.wsy32[a.p][q] = (float)y;
                 }
             } else {
                 x = qxo[q];
@@ -752,30 +756,52 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
     }
 }
 
-// 64 samples per workgroup of 16 waves: wave w merges the screen chunks w, w+16, ... for its
-// lane's sample and screens its share of the nodes the window's screen did not cover — the ones
-// appended since (the previous window's commit) — with the same f32 arithmetic and scalar node
-// loads; then wave 0 merges the 16 and decides whether the f32 winner is certainly the exact f64
-// winner (margin test against the f32 rounding bound).  Certain: exact f64 d2 of the winner.
-// Else: queue for the exact rescan, nn_idx = -(slot + 1).  Workgroup 0 also publishes the window
-// (W, or 0 when a truncated predecessor voided it) for the later kernels and advances the next
-// window's screen position.
+// nn_finalize: kFinSamples samples per workgroup, one wave per sample.
+//  1. The wave merges the sample's screen partials (lane c: chunk c) and screens the nodes the
+//     window's screen did not cover — the ones appended since (the previous window's commit) —
+//     with the same f32 arithmetic (lanes stride them), then reduces the top-2 across the wave.
+//     Margin test against the f32 rounding bound: certain → exact f64 d2 of the winner; else the
+//     wave's exact f64 brute force over the screen chunks whose f32 minimum could hide the exact
+//     nearest and over the appended nodes (rrt.rs:378-391; lowest index on exact ties, Q9).
+//  2. Window pairs (window mode): for each of the workgroup's samples j, the earlier window
+//     samples i < j strictly nearer than j's snapshot NN — the candidates of the sequential-
+//     consistency resolve.  The window's samples are staged in LDS (f32); lane (s, r) tests
+//     sample s against i = r (mod 4) of its wave's slice; an f32 distance within 5e-4 of the NN
+//     distance goes to the exact f64 test (dx*dx + dy*dy < nn_d2, the oracle's arithmetic).  Hits
+//     stay in LDS (at most kCandCap per sample, the count exact) and are appended with one global
+//     atomic per workgroup.
+// Workgroup 0 also publishes the window (W, or 0 when a truncated predecessor voided it) for the
+// later kernels and advances the next window's screen position.
 constexpr int kFinThreads = 1024;
 constexpr int kFinWaves = kFinThreads / 64;
+constexpr int kFinSamples = kFinWaves;  // one wave per sample
+constexpr int kFinDelta = 4096;         // appended nodes staged in LDS (beyond: global loads)
+
+__device__ inline Top2 shfl_xor_top2(Top2 t, int m) {
+    return Top2{__shfl_xor(t.b, m), __shfl_xor(t.s, m), __shfl_xor(t.i, m)};
+}
+
 __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     DevState* __restrict__ st, int p, int64_t seq, int chunks, const float* __restrict__ pbest,
     const float* __restrict__ psecond, const int* __restrict__ pidx, int stride,
     const double* __restrict__ qx, const double* __restrict__ qy, const float* __restrict__ x32,
     const float* __restrict__ y32, const double* __restrict__ X, const double* __restrict__ Y,
     const double* __restrict__ YAW, double eps_coord, int* __restrict__ out_idx,
-    double* __restrict__ out_d2, double* __restrict__ out_pose) {
-    __shared__ float s_b[kFinWaves][64];
-    __shared__ float s_s[kFinWaves][64];
-    __shared__ int s_i[kFinWaves][64];
-    __shared__ double s_fd[64];  // f32 winner's distance of each sample
+    double* __restrict__ out_d2, double* __restrict__ out_pose, const float* __restrict__ qx32,
+    const float* __restrict__ qy32, int* __restrict__ cand_cnt, CandEntry* __restrict__ cand,
+    int* __restrict__ pend) {
+    __shared__ double s_nd2[kFinSamples];  // exact snapshot NN d2 of each sample
+    __shared__ int s_pc[kFinSamples];      // pair search: nearer window samples found
+    __shared__ int s_pi[kFinSamples][kCandCap];
+    __shared__ double s_pd[kFinSamples][kCandCap];
+    __shared__ int s_pbase, s_pnb;
+    __shared__ uint32_t s_fmask;         // samples (waves) that need the exact brute force
+    __shared__ double s_fd[kFinSamples];
+    __shared__ uint64_t s_cmask;
     __shared__ double s_rd[kFinWaves];
     __shared__ int s_ri[kFinWaves];
-    __shared__ uint64_t s_fmask, s_cmask;
+    __shared__ float2 s_xy[kMaxWindow];  // the window's samples (f32) for the pair search
+    __shared__ float2 s_dn[kFinDelta];   // nodes appended after the screen's snapshot (f32)
     const bool voided = st->void_seq == seq || st->error;
     const int W = voided ? 0 : st->Wp[p];
     const int ns = st->nsp[p], n = st->n;
@@ -785,71 +811,39 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
         st->n_scan = n;
         if (!voided) st->it_spec = st->wsp[p] + W;
     }
-    if ((int)blockIdx.x * 64 >= W) return;
-    const int n_chunks = scan_chunks_used(ns, chunks);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int q = blockIdx.x * 64 + lane;
+    const int q0 = (int)blockIdx.x * kFinSamples;
+    if (q0 >= W) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int q = q0 + wave;
     const bool in = q < W;
-    Top2 t{__builtin_inff(), __builtin_inff(), -1};
-    {
-        constexpr int kPer = (kMaxChunks + kFinWaves - 1) / kFinWaves;
-        float vb[kPer], vs[kPer];
-        int vi[kPer];
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) {  // all loads in flight before the merge
-            const int c = wave + kFinWaves * u;
-            const size_t o = (size_t)c * stride + q;
-            const bool ok = in && c < n_chunks;
-            vb[u] = ok ? pbest[o] : __builtin_inff();
-            vs[u] = ok ? psecond[o] : __builtin_inff();
-            vi[u] = ok ? pidx[o] : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) t = merge_top2(t, Top2{vb[u], vs[u], vi[u]});
+    if (cand) {  // stage the window's earlier samples for the pair search
+        const int jmax = min(q0 + kFinSamples - 1, W - 1);
+        for (int i = tid; i < jmax; i += kFinThreads) s_xy[i] = make_float2(qx32[i], qy32[i]);
     }
-    // nodes appended after the screen's snapshot: wave w takes a contiguous share, scalar loads
-    // in blocks of kScanBlk, exact top-2 per node (same f32 arithmetic as the screen)
-    const float fx = in ? (float)qx[q] : 0.0f, fy = in ? (float)qy[q] : 0.0f;
-    const int D = n - ns;
-    if (D > 0) {
-        const int per = ((D + kFinWaves - 1) / kFinWaves + kScanBlk - 1) & ~(kScanBlk - 1);
-        const int k0 = min(ns + wave * per, n), k1 = min(k0 + per, n);
-        int k = k0;
-        for (; k + kScanBlk <= k1; k += kScanBlk) {
-            float cx[kScanBlk], cy[kScanBlk];
-#pragma unroll
-            for (int u = 0; u < kScanBlk; ++u) {
-                cx[u] = x32[k + u];
-                cy[u] = y32[k + u];
-            }
-#pragma unroll
-            for (int u = 0; u < kScanBlk; ++u) {
-                const float d = scan_d2(fx, fy, cx[u], cy[u]);
-                t.s = __builtin_amdgcn_fmed3f(t.b, d, t.s);
-                if (d < t.b) {
-                    t.b = d;
-                    t.i = k + u;
-                }
-            }
-        }
-        for (; k < k1; ++k) {
-            const float d = scan_d2(fx, fy, x32[k], y32[k]);
-            t.s = __builtin_amdgcn_fmed3f(t.b, d, t.s);
-            if (d < t.b) {
-                t.b = d;
-                t.i = k;
-            }
-        }
-    }
-    s_b[wave][lane] = t.b;
-    s_s[wave][lane] = t.s;
-    s_i[wave][lane] = t.i;
+    const int D = n - ns, Dl = min(D, kFinDelta);  // appended nodes (staged: the first kFinDelta)
+    for (int k = tid; k < Dl; k += kFinThreads) s_dn[k] = make_float2(x32[ns + k], y32[ns + k]);
+    if (tid < kFinSamples) s_pc[tid] = 0;
+    if (tid == 0) s_fmask = 0;
     __syncthreads();
-    if (wave == 0) {
+    // ---- 1. the sample's nearest node
+    if (in) {
+        const int n_chunks = scan_chunks_used(ns, chunks);
+        Top2 t{__builtin_inff(), __builtin_inff(), -1};
+        if (lane < n_chunks) {
+            const size_t o = (size_t)lane * stride + q;
+            t = Top2{pbest[o], psecond[o], pidx[o]};
+        }
+        const double xq = qx[q], yq = qy[q];
+        const float fx = (float)xq, fy = (float)yq;
+        for (int k = lane; k < D; k += 64) {  // appended nodes: exact top-2 per lane
+            const float2 v = k < Dl ? s_dn[k] : make_float2(x32[ns + k], y32[ns + k]);
+            const float d = scan_d2(fx, fy, v.x, v.y);
+            const Top2 c{d, __builtin_inff(), ns + k};
+            t = merge_top2(t, c);
+        }
 #pragma unroll
-        for (int w = 1; w < kFinWaves; ++w)
-            t = merge_top2(t, Top2{s_b[w][lane], s_s[w][lane], s_i[w][lane]});
+        for (int m = 1; m < 64; m <<= 1) t = merge_top2(t, shfl_xor_top2(t, m));
         bool flag = t.i < 0 || !(t.b < __builtin_inff());
         double D1 = __builtin_inf();
         if (!flag) {
@@ -860,75 +854,73 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
                 flag = !(D2 - D1 > tau);
             }
         }
-        flag = flag && in;
-        s_fd[lane] = D1;
-        const uint64_t fm = __ballot(flag);
-        if (lane == 0) s_fmask = fm;
-        if (flag) {
-            atomicAdd(&st->flag_count, 1);  // statistics (nn_flagged)
-        } else if (in) {
-            const double nxp = X[t.i], nyp = Y[t.i];
-            const double dx = qx[q] - nxp, dy = qy[q] - nyp;
-            out_idx[q] = t.i;
-            out_d2[q] = dx * dx + dy * dy;
-            if (out_pose) {
-                out_pose[3 * q] = nxp;
-                out_pose[3 * q + 1] = nyp;
-                out_pose[3 * q + 2] = YAW[t.i];
+        if (!flag) {
+            const int bi = t.i;
+            const double dx = xq - X[bi], dy = yq - Y[bi];
+            const double bd = dx * dx + dy * dy;
+            if (lane == 0) {
+                out_idx[q] = bi;
+                out_d2[q] = bd;
+                s_nd2[wave] = bd;
+                if (out_pose) {
+                    out_pose[3 * q] = X[bi];
+                    out_pose[3 * q + 1] = Y[bi];
+                    out_pose[3 * q + 2] = YAW[bi];
+                }
             }
+        } else if (lane == 0) {
+            atomicAdd(&st->flag_count, 1);  // statistics (nn_flagged)
+            atomicOr(&s_fmask, 1u << wave);
+            s_fd[wave] = D1;
         }
     }
     __syncthreads();
-    // near-ties: the exact f64 brute force, over the screen chunks whose f32 minimum could hide
-    // the exact nearest (f32 distance within the rounding bound of the f32 winner) and over the
-    // nodes appended after the screen; lowest index on exact ties (rrt.rs:378-391, Q9)
-    uint64_t fm = s_fmask;
-    const int tid = threadIdx.x;
-    while (fm) {
-        const int l = (int)__builtin_ctzll(fm);
-        fm &= fm - 1;
-        const int qf = blockIdx.x * 64 + l;
-        const double D1 = s_fd[l];
+    // near-ties: the workgroup's exact f64 brute force, over the screen chunks whose f32 minimum
+    // could hide the exact nearest (f32 distance within the rounding bound of the f32 winner)
+    // and over the appended nodes; lowest index on exact ties (rrt.rs:378-391, Q9)
+    for (uint32_t fm = s_fmask; fm; fm &= fm - 1) {
+        const int w = (int)__builtin_ctz(fm);
+        const int qf = q0 + w;
+        const double D1 = s_fd[w];
         const double tc = 16.0 * eps_coord + 4.0e-6 * (D1 + 1.0);
-        if (tid < 64) {
-            const bool cand = tid < n_chunks &&
-                              !(sqrt((double)pbest[(size_t)tid * stride + qf]) > D1 + tc);
-            const uint64_t cm = __ballot(cand);
-            if (tid == 0) s_cmask = cm;
+        const int n_chunks = scan_chunks_used(ns, chunks);
+        if (wave == 0) {
+            const bool cc = lane < n_chunks &&
+                            !(sqrt((double)pbest[(size_t)lane * stride + qf]) > D1 + tc);
+            const uint64_t cm = __ballot(cc);
+            if (lane == 0) s_cmask = cm;
         }
         __syncthreads();
-        const uint64_t cm = s_cmask;
         const int cl = scan_chunk_len(ns, chunks);
-        const double x = qx[qf], y = qy[qf];
+        const double xq = qx[qf], yq = qy[qf];
         double bd = __builtin_inf();
-        int bk = 0x7fffffff;
-        uint64_t mm = cm;
-        while (mm) {
-            const int c = (int)__builtin_ctzll(mm);
-            mm &= mm - 1;
-            const int c0 = c * cl, c1 = min(c0 + cl, ns);
-            for (int k = c0 + tid; k < c1; k += kFinThreads) {
-                const double dx = x - X[k], dy = y - Y[k];
-                argmin_pair(bd, bk, dx * dx + dy * dy, k);
+        int bi = 0x7fffffff;
+        for (uint64_t cm = s_cmask; cm; cm &= cm - 1) {
+            const int c = (int)__builtin_ctzll(cm);
+            const int c1 = min(c * cl + cl, ns);
+            for (int k = c * cl + tid; k < c1; k += kFinThreads) {
+                const double dx = xq - X[k], dy = yq - Y[k];
+                argmin_pair(bd, bi, dx * dx + dy * dy, k);
             }
         }
         for (int k = ns + tid; k < n; k += kFinThreads) {
-            const double dx = x - X[k], dy = y - Y[k];
-            argmin_pair(bd, bk, dx * dx + dy * dy, k);
+            const double dx = xq - X[k], dy = yq - Y[k];
+            argmin_pair(bd, bi, dx * dx + dy * dy, k);
         }
 #pragma unroll
-        for (int m = 32; m > 0; m >>= 1) argmin_pair(bd, bk, __shfl_xor(bd, m), __shfl_xor(bk, m));
+        for (int m = 32; m > 0; m >>= 1) argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
         if (lane == 0) {
             s_rd[wave] = bd;
-            s_ri[wave] = bk;
+            s_ri[wave] = bi;
         }
         __syncthreads();
         if (tid == 0) {
             double d = s_rd[0];
             int i = s_ri[0];
-            for (int w = 1; w < kFinWaves; ++w) argmin_pair(d, i, s_rd[w], s_ri[w]);
+            for (int v = 1; v < kFinWaves; ++v) argmin_pair(d, i, s_rd[v], s_ri[v]);
             out_idx[qf] = i;
             out_d2[qf] = d;
+            s_nd2[w] = d;
             if (out_pose) {
                 out_pose[3 * qf] = X[i];
                 out_pose[3 * qf + 1] = Y[i];
@@ -937,60 +929,80 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
         }
         __syncthreads();
     }
-}
-
-// Window pairs: for every sample j, the earlier samples i < j of the same window that are
-// strictly nearer than j's snapshot NN (the candidates of the sequential-consistency resolve).
-// One workgroup per (j-tile, i-tile) of the lower triangle (kPairTile x kPairTile): the i-tile's
-// coordinates are staged in LDS and read as broadcasts; thread l owns sample j = jt*kPairTile + l.
-// Hits are rare and appended with atomics (cand_cnt[j] is the exact count, at most kCandCap
-// entries of each j are stored).  A sample's first hit queues it for the resolve's round passes
-// (pend); a list that overflows cuts the window before its sample (weff).
-constexpr int kPairTile = 128;
-
-__global__ __launch_bounds__(kPairTile) void window_pairs_kernel(DevState* __restrict__ st,
-                                                                 const double* __restrict__ wsx,
-                                                                 const double* __restrict__ wsy,
-                                                                 const double* __restrict__ nn_d2,
-                                                                 int* __restrict__ cand_cnt,
-                                                                 CandEntry* __restrict__ cand,
-                                                                 int* __restrict__ pend) {
-    __shared__ double s_x[kPairTile], s_y[kPairTile];
-    const int W = st->W;
-    const int b = blockIdx.x;
-    int jt = (int)((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
-    while ((jt + 1) * (jt + 2) / 2 <= b) ++jt;
-    while (jt * (jt + 1) / 2 > b) --jt;
-    const int it = b - jt * (jt + 1) / 2;
-    if (jt * kPairTile >= W) return;
-    const int tid = threadIdx.x;
-    const int j = jt * kPairTile + tid;
-    const int i0 = it * kPairTile;
-    const int il = i0 + tid;
-    s_x[tid] = il < W ? wsx[il] : 0.0;
-    s_y[tid] = il < W ? wsy[il] : 0.0;
-    const bool valid = j < W;
-    const double xj = valid ? wsx[j] : 0.0, yj = valid ? wsy[j] : 0.0;
-    const double D2 = valid ? nn_d2[j] : -1.0;
-    __syncthreads();
-    const int kend = valid ? min(kPairTile, j - i0) : 0;  // i < j (< W)
-    bool first = false, over = false;
-#pragma unroll 8
-    for (int k = 0; k < kend; ++k) {
-        const double dx = xj - s_x[k], dy = yj - s_y[k];
-        const double d2 = dx * dx + dy * dy;
-        if (d2 < D2) {
-            const int cpos = atomicAdd(&cand_cnt[j], 1);
-            if (cpos < kCandCap) {
-                const int e = atomicAdd(&st->ncomp, 1);
-                cand[e] = CandEntry{j, i0 + k, d2, 0.0, -1, 0};
+    if (!cand) return;  // nearest-only launch (no window)
+    // ---- 2. window pairs
+    {
+        const int s = lane & (kFinSamples - 1), r = lane >> 4;  // 4 lane groups of 16 samples
+        const int j = q0 + s;
+        const bool jin = j < W;
+        const double xj = jin ? qx[j] : 0.0, yj = jin ? qy[j] : 0.0;
+        const float xjf = (float)xj, yjf = (float)yj;
+        const double D2 = jin ? s_nd2[s] : -1.0;
+        const float df = jin ? __builtin_sqrtf((float)D2) + 5.0e-4f : -1.0f;
+        const float thr = jin ? df * df : -1.0f;
+        const int jmax = min(q0 + kFinSamples - 1, W - 1);  // pairs i < j <= jmax
+        const int per = ((jmax + kFinWaves - 1) / kFinWaves + 3) & ~3;
+        const int i0 = min(wave * per, jmax), i1 = min(i0 + per, jmax);
+        for (int ib = i0; ib < i1; ib += 32) {  // 8 pairs per lane per step
+            float2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = s_xy[min(ib + 4 * u + r, i1 - 1)];
+            float dmin = __builtin_inff();
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int ii = ib + 4 * u + r;
+                const float d = scan_d2(xjf, yjf, v[u].x, v[u].y) - thr;
+                dmin = (ii < i1 && ii < j) ? fminf(dmin, d) : dmin;
             }
-            first |= cpos == 0;
-            over |= cpos == kCandCap;
+            if (__any(dmin <= 0.0f)) {  // rare: the exact tests of this step's candidates
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int ii = ib + 4 * u + r;
+                    if (ii < i1 && ii < j && scan_d2(xjf, yjf, v[u].x, v[u].y) <= thr) {
+                        const double dx = xj - qx[ii], dy = yj - qy[ii];
+                        const double d2 = dx * dx + dy * dy;
+                        if (d2 < D2) {
+                            const int pos = atomicAdd(&s_pc[s], 1);
+                            if (pos < kCandCap) {
+                                s_pi[s][pos] = ii;
+                                s_pd[s][pos] = d2;
+                            }
+                        }
+                    }
+                }
+            }
         }
     }
-    if (first) pend[atomicAdd(&st->npend, 1)] = j;
-    if (over) atomicMin(&st->weff, j);
+    __syncthreads();
+    if (wave == 0) {
+        const int j = q0 + lane;
+        const bool jin = lane < kFinSamples && j < W;
+        const int cnt = jin ? s_pc[lane] : 0;
+        const int keep = min(cnt, kCandCap);
+        if (jin) cand_cnt[j] = cnt;
+        // one reservation per workgroup for the entries and for the queue of pending samples
+        int ex = keep, pc = cnt > 0 ? 1 : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int ye = __shfl_up(ex, o), yp = __shfl_up(pc, o);
+            if (lane >= o) {
+                ex += ye;
+                pc += yp;
+            }
+        }
+        const int eo = ex - keep, po = pc - (cnt > 0 ? 1 : 0);
+        if (lane == 63) {
+            s_pbase = ex > 0 ? atomicAdd(&st->ncomp, ex) : 0;
+            s_pnb = pc > 0 ? atomicAdd(&st->npend, pc) : 0;
+        }
+        const uint64_t ov = __ballot(cnt > kCandCap);  // a list overflowed: the window stops there
+        __builtin_amdgcn_wave_barrier();
+        const int eb = s_pbase + eo, pb = s_pnb + po;
+        for (int k = 0; k < keep; ++k)
+            cand[eb + k] = CandEntry{j, s_pi[lane][k], s_pd[lane][k], 0.0, -1, 0};
+        if (cnt > 0) pend[pb] = j;
+        if (lane == 0 && ov) atomicMin(&st->weff, q0 + (int)__builtin_ctzll(ov));
+    }
 }
 
 // Task t of a window: t < W is (sample t → its snapshot NN); t >= W is candidate entry t - W
@@ -2448,6 +2460,10 @@ WinKArgs win_args(const WindowArgs& a, int p, int gen, int resolve, int scan, in
     k.wsx[1] = a.wsx + a.Kcap;
     k.wsy[0] = a.wsy;
     k.wsy[1] = a.wsy + a.Kcap;
+    k.wsx32[0] = a.wsx32;
+    k.wsx32[1] = a.wsx32 + a.Kcap;
+    k.wsy32[0] = a.wsy32;
+    k.wsy32[1] = a.wsy32 + a.Kcap;
     k.pbest = a.pbest;
     k.psecond = a.psecond;
     k.pidx = a.pidx;
@@ -2469,18 +2485,16 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     const int K = a.K;
     const int p = (int)(seq & 1);
     const WinKArgs wk = win_args(a, p, 1, resolve_prev, 1, seq);
-    const int Tp = (K + kPairTile - 1) / kPairTile;
     double* wsx = a.wsx + (size_t)p * a.Kcap;
     double* wsy = a.wsy + (size_t)p * a.Kcap;
     if (ev) (void)hipEventRecord(ev[0], s);
     window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
     if (ev) (void)hipEventRecord(ev[1], s);
     if (resolve_prev && !kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
-    nn_finalize_kernel<<<(K + 63) / 64, kFinThreads, 0, s>>>(
+    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples, kFinThreads, 0, s>>>(
         a.st, p, seq, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, wsx, wsy, a.tr.x32, a.tr.y32,
-        a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose);
-    window_pairs_kernel<<<Tp * (Tp + 1) / 2, kPairTile, 0, s>>>(a.st, wsx, wsy, a.nn_d2,
-                                                                a.cand_cnt, a.cand, a.pend);
+        a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose, wk.wsx32[p],
+        wk.wsy32[p], a.cand_cnt, a.cand, a.pend);
     if (ev) (void)hipEventRecord(ev[2], s);
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K + kPrepThreads / 8 - 1) / (kPrepThreads / 8);
@@ -2510,9 +2524,10 @@ hipError_t launch_nearest(hipStream_t s, const WindowArgs& a) {
     const int K = a.K;
     const WinKArgs wk = win_args(a, 0, 0, 0, 1, 0);
     window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
-    nn_finalize_kernel<<<(K + 63) / 64, kFinThreads, 0, s>>>(
+    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples, kFinThreads, 0, s>>>(
         a.st, 0, 0, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, a.wsx, a.wsy, a.tr.x32,
-        a.tr.y32, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, nullptr);
+        a.tr.y32, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, nullptr, nullptr,
+        nullptr, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 
