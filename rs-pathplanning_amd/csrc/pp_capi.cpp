@@ -6,7 +6,7 @@
 // Dubins, verifies, inserts.  The GPU evaluates a window of K iterations against the tree
 // snapshot at the window start, and a one-workgroup resolve kernel replays the window in order:
 //   * sample j's true parent is the nearest of {snapshot NN} ∪ {accepted window samples i < j};
-//     window_pairs lists the i that are strictly nearer than the snapshot NN, so the parent is
+//     nn_finalize's pair search lists the i that are strictly nearer than the snapshot NN, so the parent is
 //     the first accepted entry of that list in (d2, i) order, or the snapshot NN;
 //   * the verdict for (j, parent) was precomputed for the snapshot NN and for every listed i
 //     under i's own snapshot parent; only a parent that itself changed needs a repair steer.
@@ -132,6 +132,8 @@ struct pp_ctx {
     int Kcap = 0;
     DBuf<double> wsx, wsy, nn_d2, snap_yaw, snap_pose;
     DBuf<float> pbest, psecond, wsx32, wsy32;
+    DBuf<int> perm;
+    DBuf<double> sqb;
     DBuf<int> pidx, nn_idx, cand_cnt, snap_status;
     DBuf<CandEntry> cand;
     DBuf<PrepRec> rec;   // per-task steer records
@@ -239,6 +241,8 @@ struct pp_ctx {
         a.wsy = wsy.p;
         a.wsx32 = wsx32.p;
         a.wsy32 = wsy32.p;
+        a.perm = perm.p;
+        a.sq = sqb.p;
         a.pbest = pbest.p;
         a.psecond = psecond.p;
         a.pidx = pidx.p;
@@ -281,6 +285,8 @@ int ensure_window(pp_ctx* c, int K) {
     PP_HIP(c->wsy.reserve(2 * k));
     PP_HIP(c->wsx32.reserve(2 * k));
     PP_HIP(c->wsy32.reserve(2 * k));
+    PP_HIP(c->perm.reserve(2 * k));
+    PP_HIP(c->sqb.reserve(2 * k));
     PP_HIP(c->pbest.reserve(k * kMaxChunks));
     PP_HIP(c->psecond.reserve(k * kMaxChunks));
     PP_HIP(c->pidx.reserve(k * kMaxChunks));

@@ -21,6 +21,8 @@ struct WindowArgs {
     double* wsy = nullptr;
     float* wsx32 = nullptr;       // [2 * Kcap] their f32 copies
     float* wsy32 = nullptr;
+    int* perm = nullptr;          // [2 * Kcap] spatially sorted sample order (window_samples)
+    double* sq = nullptr;         // [2 * Kcap] |q - o|^2 about the screen block's centre
     float* pbest = nullptr;
     float* psecond = nullptr;
     int* pidx = nullptr;

@@ -1,15 +1,19 @@
 // pp_kernels.hip — hand-written CDNA4 (gfx950) kernels of the RRT extend hot path.
 //
 // Window pipeline (one speculative window of K iterations, device-resident state):
-//   window_begin   Space::rand_point for the window's iterations (seeded stream)   rrt.rs:139-146
-//   nn_scan        K samples x N tree nodes, f32 SoA screen: scalar-broadcast nodes, 4 samples
-//                  per lane, exact per-lane top-2, XCD-aware chunk mapping         rrt.rs:378-391
-//   nn_finalize    merge the 64 chunk partials, flag near-ties, exact f64 d2 of the winner
-//   nn_rescan      exact f64 brute force of the flagged samples, chunk-parallel
-//   window_pairs   earlier samples of the same window strictly nearer than the snapshot NN
-//   steer_window   one wave per (sample, parent): compute_yaw + Dubins steer + sampled-arc
-//                  collision, fused, f64                        rrt.rs:169-175,414-426, dubins.rs
-//   resolve        one workgroup: sequential-consistency replay, repairs, in-order insert
+//   window_samples Space::rand_point for the window's iterations (seeded stream), Morton-sorted
+//                  (the first window of a batch; later ones come from nn_finalize) rrt.rs:139-146
+//   window_kernel  workgroups 1..: the NN screen, K samples x N tree nodes, f32 SoA, expanded form
+//                  about each sample block's centre, scalar-broadcast nodes, 4 samples per lane,
+//                  exact per-chunk top-2, XCD-aware mapping                          rrt.rs:378-391
+//                  workgroup 0: resolve + commit of the previous window (sequential-consistency
+//                  replay, repairs inline, in-order insert)                          rrt.rs:414-426
+//   nn_finalize    merge the chunk partials and the appended nodes, exact f64 d2 of the winner,
+//                  near-ties decided exactly (wave, or workgroup brute force), window pairs
+//                  (earlier samples nearer than the snapshot NN), next window's samples
+//   steer_prep     8 lanes per (sample, parent): compute_yaw + Dubins word + grid-point distances
+//   steer_walk     one wave per task: sampled-arc polyline, bounds + disc collision, f64
+//                                                               rrt.rs:169-175,414-426, dubins.rs
 // API kernels: steer_tasks (verify_node batch), nn_fix (nearest batch), dubins_batch.
 //
 // No MFMA anywhere: there is no dense contraction on this path.
@@ -457,7 +461,7 @@ __global__ __launch_bounds__(64) void dubins_batch_kernel(const double* __restri
 // ------------------------------------------------------------------------- window pipeline
 //
 // One speculative window w = window_kernel (w's NN screen ‖ resolve + commit of w - 1) →
-// nn_finalize → nn_rescan → window_pairs → steer_prep → steer_walk; window w's resolve and commit
+// nn_finalize (+ window pairs, + w + 1's samples) → steer_prep → steer_walk; window w's resolve and commit
 // run inside window w + 1's window_kernel (or the batch's drain launch).  Everything reads the
 // device-resident DevState, so the host enqueues windows back to back and synchronises once per
 // batch.
@@ -542,7 +546,7 @@ struct WinKArgs {
     int Kcap;           // buffer capacity per window (stride of the partials)
     int nqb, chunks;    // screen geometry (scan_chunks)
     int p;              // parity of the screened window
-    int gen;            // 1: generate the window's samples (RNG); 0: screen the given wsx/wsy[p]
+    int gen;            // 1: window mode (sorted samples, expanded screen); 0: given wsx/wsy[p]
     int resolve;        // 1: workgroup 0 resolves + commits the previous window
     int scan;           // 0: the drain launch (resolve only)
     int64_t seq;        // sequence number of the screened window
@@ -552,6 +556,8 @@ struct WinKArgs {
     double* wsy[2];
     float* wsx32[2];    // f32 copies (the pair search's prefilter)
     float* wsy32[2];
+    int* perm[2];       // window mode: sorted position -> sample (window_samples)
+    double* sq[2];      // window mode: |q - o|^2 of every sample (the screen's block origin)
     float* pbest;
     float* psecond;
     int* pidx;
@@ -568,37 +574,29 @@ struct WinKArgs {
 };
 
 // RRT::get_nearest_node screen (rrt.rs:378-391): f32 SoA nodes x the window's samples.  The
-// screen workgroup b of kScanGrid (mapped XCD-aware, so the sample blocks that stream one node
-// chunk share an XCD's L2) takes sample block qb and node chunk c.  Its 16 waves split the
-// chunk; every lane holds 4 samples; node coordinates are wave-uniform scalar loads (double-
-// buffered one block ahead) used directly as SGPR operands.  Per block of kScanBlk nodes each
-// sample keeps only the block minimum (v_min3: half an op per eval on top of sub, sub, mul, fma),
-// merges it into (best, second) with med3 and records the block that first attained the best;
-// the winning block is re-evaluated afterwards with the same arithmetic (bit-identical) for the
-// lowest index and the in-block second best.  Result: the exact per-chunk top-2 of the f32
-// distances.  In generating mode the samples come from the counter RNG (Space::rand_point,
-// rrt.rs:139-146, seeded: Q7: x = draw 2*it, y = draw 2*it + 1) for iterations
-// [it_spec, it_spec + W), W = min(K, target - it_spec), and the chunk-0 workgroups store them.
+// screen workgroup b (mapped XCD-aware, so the sample blocks that stream one node chunk share an
+// XCD's L2) takes sample block qb and node chunk c.  Its waves split the chunk; every lane holds 4
+// samples; node coordinates are wave-uniform scalar loads (the next block in flight) used directly
+// as SGPR operands.  Per block of kScanBlk nodes each sample keeps only the block minimum (v_min3),
+// merges it into (best, second) with med3 and records the block that first attained the best; the
+// winning block is re-evaluated afterwards with the same arithmetic (bit-identical) for the lowest
+// index and the in-block second best.  Result: the exact per-chunk top-2 of the screen values.
+//
+// kExp (window mode): the samples come spatially sorted (window_samples: perm), so a block of 256
+// is compact and the screen runs in the expanded form about the block's centre o:
+//     e(n) = |n - o|^2 - 2 (q - o).(n - o)  =  |q - n|^2 - |q - o|^2
+// two FMAs per (node, sample) after a per-node prologue (n - o, |n - o|^2: four ops per wave,
+// shared by the lane's 4 samples) — 3.5 VALU per evaluation instead of 4.5.  nn_finalize adds
+// |q - o|^2 back (sq) and widens the near-tie margin by the expanded form's rounding bound.
+// !kExp (nearest API): the given samples, direct form (sub, sub, mul, fma).
+template <bool kExp>
 __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& a, int b,
                                                                char* smem) {
     DevState* st = a.st;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int W, ns;
-    int64_t start = 0;
-    if (a.gen) {
-        start = st->it_spec;
-        const int64_t rem = a.target - start;
-        W = (rem <= 0 || st->error) ? 0 : (rem < a.K ? (int)rem : a.K);
-        ns = st->n_scan;
-        if (b == 0 && tid == 0) {
-            st->Wp[a.p] = W;
-            st->wsp[a.p] = start;
-            st->nsp[a.p] = ns;
-        }
-    } else {
-        W = st->Wp[a.p];
-        ns = st->nsp[a.p];
-    }
+    const int W = st->Wp[a.p];
+    const int ns = st->n_scan;
+    if (b == 0 && tid == 0) st->nsp[a.p] = ns;
     const int G = a.nqb * a.chunks;
     if (b >= G) return;
     const int t = (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b;
@@ -609,37 +607,67 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
     const int c0 = c * cl;
     if (c0 >= ns) return;
     const int c1 = min(c0 + cl, ns);
-    double* qxo = a.wsx[a.p];
-    double* qyo = a.wsy[a.p];
+    const double* qxs = a.wsx[a.p];
+    const double* qys = a.wsy[a.p];
     float qxr[kQPL], qyr[kQPL], best[kQPL], second[kQPL];
-    int blk[kQPL], bi[kQPL];
+    int sid[kQPL], blk[kQPL], bi[kQPL];
+    double xs[kQPL], ys[kQPL];
 #pragma unroll
     for (int r = 0; r < kQPL; ++r) {
-        const int q = qbase + r * 64 + lane;
-        double x = 0.0, y = 0.0;
-        if (q < W) {
-            if (a.gen) {
-                const uint64_t itq = (uint64_t)(start + q);
-                x = gen_range(a.seed, 2 * itq, a.sc.minx, a.sc.maxx);
-                y = gen_range(a.seed, 2 * itq + 1, a.sc.miny, a.sc.maxy);
-                if (c == 0 && wave == 0) {
-                    qxo[q] = x;
-                    qyo[q] = y;
-                    a.wsx32[a.p][q] = (float)x;
-                    a.wsy32[a.p][q] = (float)y;
-                }
-            } else {
-                x = qxo[q];
-                y = qyo[q];
-            }
-        }
-        qxr[r] = (float)x;
-        qyr[r] = (float)y;
+        const int pos = qbase + r * 64 + lane;
+        sid[r] = pos < W ? (kExp ? a.perm[a.p][pos] : pos) : -1;
+        xs[r] = sid[r] >= 0 ? qxs[sid[r]] : 0.0;
+        ys[r] = sid[r] >= 0 ? qys[sid[r]] : 0.0;
         best[r] = __builtin_inff();
         second[r] = __builtin_inff();
         blk[r] = -1;
         bi[r] = -1;
     }
+    float oxf = 0.0f, oyf = 0.0f;
+    if (kExp) {  // the block's centre (every wave reduces the same 256 samples)
+        double x0 = __builtin_inf(), x1 = -__builtin_inf(), y0 = __builtin_inf(), y1 = -__builtin_inf();
+#pragma unroll
+        for (int r = 0; r < kQPL; ++r) {
+            if (sid[r] < 0) continue;
+            x0 = fmin(x0, xs[r]);
+            x1 = fmax(x1, xs[r]);
+            y0 = fmin(y0, ys[r]);
+            y1 = fmax(y1, ys[r]);
+        }
+        x0 = wave_min(x0);
+        x1 = wave_max(x1);
+        y0 = wave_min(y0);
+        y1 = wave_max(y1);
+        oxf = (float)(0.5 * (x0 + x1));
+        oyf = (float)(0.5 * (y0 + y1));
+    }
+#pragma unroll
+    for (int r = 0; r < kQPL; ++r) {
+        if (kExp) {
+            const float qpx = (float)(xs[r] - (double)oxf), qpy = (float)(ys[r] - (double)oyf);
+            qxr[r] = -2.0f * qpx;  // exact scaling
+            qyr[r] = -2.0f * qpy;
+            if (c == 0 && wave == 0 && sid[r] >= 0)  // |q - o|^2 for nn_finalize (exact in f64)
+                a.sq[a.p][sid[r]] = (double)qpx * (double)qpx + (double)qpy * (double)qpy;
+        } else {
+            qxr[r] = (float)xs[r];
+            qyr[r] = (float)ys[r];
+        }
+    }
+    // screen value of (sample r, node (nx, ny)); expanded: the node's (x - ox, y - oy, |.|^2)
+    auto val = [&](int r, float px, float py, float pw) {
+        if (kExp) return __builtin_fmaf(qxr[r], px, __builtin_fmaf(qyr[r], py, pw));
+        return scan_d2(qxr[r], qyr[r], px, py);
+    };
+    auto prep = [&](float& px, float& py, float& pw) {
+        if (kExp) {
+            px = px - oxf;
+            py = py - oyf;
+            pw = __builtin_fmaf(py, py, px * px);
+        } else {
+            pw = 0.0f;
+        }
+    };
     const float* nx = a.tr.x32;
     const float* ny = a.tr.y32;
     // wave-uniform range (kScanBlk-aligned start): readfirstlane lets the compiler use scalar loads
@@ -655,11 +683,12 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
             cy[u] = ny[w0 + u];
         }
         for (int k = w0; k < wb; k += kScanBlk) {
-            float px[kScanBlk], py[kScanBlk];
+            float px[kScanBlk], py[kScanBlk], pw[kScanBlk];
 #pragma unroll
             for (int u = 0; u < kScanBlk; ++u) {
                 px[u] = cx[u];
                 py[u] = cy[u];
+                prep(px[u], py[u], pw[u]);
             }
             const int kn = k + kScanBlk < wb ? k + kScanBlk : k;  // prefetch the next block
 #pragma unroll
@@ -672,7 +701,7 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
             for (int u = 0; u < kScanBlk; ++u) {
 #pragma unroll
                 for (int r = 0; r < kQPL; ++r) {
-                    const float d = scan_d2(qxr[r], qyr[r], px[u], py[u]);
+                    const float d = val(r, px[u], py[u], pw[u]);
                     bm[r] = u == 0 ? d : __builtin_fminf(bm[r], d);
                 }
             }
@@ -685,14 +714,14 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
                 }
             }
         }
-        // the winning block again, bit-identical: lowest index of the best distance and the best
-        // of the block's other nodes (the block minima only carried one each)
+        // the winning block again, bit-identical: lowest index of the best value and the best of
+        // the block's other nodes (the block minima only carried one each)
 #pragma unroll
         for (int r = 0; r < kQPL; ++r) {
             if (blk[r] < 0) continue;
             const float4* bx = reinterpret_cast<const float4*>(nx + blk[r]);
             const float4* by = reinterpret_cast<const float4*>(ny + blk[r]);
-            float vx[kScanBlk], vy[kScanBlk];
+            float vx[kScanBlk], vy[kScanBlk], vw[kScanBlk];
 #pragma unroll
             for (int v = 0; v < kScanBlk / 4; ++v) {
                 const float4 a4 = bx[v], b4 = by[v];
@@ -709,7 +738,8 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
             float other = __builtin_inff();
 #pragma unroll
             for (int u = 0; u < kScanBlk; ++u) {
-                const float d = scan_d2(qxr[r], qyr[r], vx[u], vy[u]);
+                prep(vx[u], vy[u], vw[u]);
+                const float d = val(r, vx[u], vy[u], vw[u]);
                 if (ui < 0 && d == best[r])
                     ui = u;
                 else
@@ -720,10 +750,11 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
         }
     }
     for (int k = wb; k < w1; ++k) {  // tail (< kScanBlk nodes): exact top-2 per node
-        const float px = nx[k], py = ny[k];
+        float px = nx[k], py = ny[k], pw;
+        prep(px, py, pw);
 #pragma unroll
         for (int r = 0; r < kQPL; ++r) {
-            const float d = scan_d2(qxr[r], qyr[r], px, py);
+            const float d = val(r, px, py, pw);
             second[r] = __builtin_amdgcn_fmed3f(best[r], d, second[r]);
             if (d < best[r]) {
                 best[r] = d;
@@ -734,11 +765,13 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
     float* s_b = reinterpret_cast<float*>(smem);              // [kScanWaves][kQPB]
     float* s_s = s_b + kScanWaves * kQPB;
     int* s_i = reinterpret_cast<int*>(s_s + kScanWaves * kQPB);
+    int* s_sid = s_i + kScanWaves * kQPB;                      // [kQPB]
 #pragma unroll
     for (int r = 0; r < kQPL; ++r) {
         s_b[wave * kQPB + r * 64 + lane] = best[r];
         s_s[wave * kQPB + r * 64 + lane] = second[r];
         s_i[wave * kQPB + r * 64 + lane] = bi[r];
+        if (wave == 0) s_sid[r * 64 + lane] = sid[r];
     }
     __syncthreads();
     if (tid < kQPB) {  // one thread per sample merges the waves' partials
@@ -746,14 +779,99 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
 #pragma unroll
         for (int w = 1; w < kScanWaves; ++w)
             tt = merge_top2(tt, Top2{s_b[w * kQPB + tid], s_s[w * kQPB + tid], s_i[w * kQPB + tid]});
-        const int q = qbase + tid;
-        if (q < W) {
+        const int q = s_sid[tid];
+        if (q >= 0) {
             const size_t o = (size_t)c * a.Kcap + q;
             a.pbest[o] = tt.b;
             a.psecond[o] = tt.s;
             a.pidx[o] = tt.i;
         }
     }
+}
+
+// window_samples: Space::rand_point for the iterations [start, start + W) of a window
+// (rrt.rs:139-146, seeded: Q7 — x = draw 2*it, y = draw 2*it + 1), W = min(K, target - start),
+// and a counting sort of the samples by the Morton index of their cell in a 16 x 16 grid over the
+// sampling box: perm[pos] = sample, so a screen block of 256 consecutive sorted samples is
+// spatially compact (the expanded screen's precision).  Within a cell the order is arbitrary —
+// the results never depend on it (only which samples meet the exact rescan).
+struct SamplesArgs {
+    int K;
+    int64_t target;
+    uint64_t seed;
+    double minx, maxx, miny, maxy;
+    double* wsx[2];
+    double* wsy[2];
+    float* wsx32[2];
+    float* wsy32[2];
+    int* perm[2];
+};
+
+__device__ inline int morton16(int x, int y) {
+    int m = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) m |= (((x >> b) & 1) << (2 * b)) | (((y >> b) & 1) << (2 * b + 1));
+    return m;
+}
+
+__device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t start,
+                             char* smem) {
+    int* s_hist = reinterpret_cast<int*>(smem);                  // [256]
+    unsigned char* s_cell = reinterpret_cast<unsigned char*>(s_hist + 256);  // [K]
+    const int tid = threadIdx.x, NT = blockDim.x;
+    const int64_t rem = g.target - start;
+    const int W = (rem <= 0 || st->error) ? 0 : (rem < g.K ? (int)rem : g.K);
+    if (tid == 0) {
+        st->Wp[np] = W;
+        st->wsp[np] = start;
+    }
+    for (int i = tid; i < 256; i += NT) s_hist[i] = 0;
+    __syncthreads();
+    const double fx = 16.0 / (g.maxx - g.minx), fy = 16.0 / (g.maxy - g.miny);
+    for (int j = tid; j < W; j += NT) {
+        const uint64_t itj = (uint64_t)(start + j);
+        const double x = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
+        const double y = gen_range(g.seed, 2 * itj + 1, g.miny, g.maxy);
+        g.wsx[np][j] = x;
+        g.wsy[np][j] = y;
+        g.wsx32[np][j] = (float)x;
+        g.wsy32[np][j] = (float)y;
+        const int cx = min(max((int)((x - g.minx) * fx), 0), 15);
+        const int cy = min(max((int)((y - g.miny) * fy), 0), 15);
+        const int cell = morton16(cx, cy);
+        s_cell[j] = (unsigned char)cell;
+        atomicAdd(&s_hist[cell], 1);
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive prefix of the 256 cell counts, 4 per lane
+        int v[4], sum = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            v[u] = s_hist[4 * tid + u];
+            sum += v[u];
+        }
+        int x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (tid >= o) x += y;
+        }
+        int base = x - sum;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            s_hist[4 * tid + u] = base;
+            base += v[u];
+        }
+    }
+    __syncthreads();
+    for (int j = tid; j < W; j += NT) g.perm[np][atomicAdd(&s_hist[s_cell[j]], 1)] = j;
+}
+
+// The first window of a batch: its samples (the later ones come from the previous window's
+// nn_finalize, which knows where the next window starts).
+__global__ __launch_bounds__(1024) void window_samples_kernel(DevState* st, SamplesArgs g, int np) {
+    __shared__ __attribute__((aligned(16))) char smem[256 * 4 + kMaxWindow];
+    samples_role(st, g, np, st->it_spec, smem);
 }
 
 // nn_finalize: kFinSamples samples per workgroup, one wave per sample.
@@ -789,14 +907,14 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     const double* __restrict__ YAW, double eps_coord, int* __restrict__ out_idx,
     double* __restrict__ out_d2, double* __restrict__ out_pose, const float* __restrict__ qx32,
     const float* __restrict__ qy32, int* __restrict__ cand_cnt, CandEntry* __restrict__ cand,
-    int* __restrict__ pend) {
+    int* __restrict__ pend, const double* __restrict__ sq, SamplesArgs g) {
     __shared__ double s_nd2[kFinSamples];  // exact snapshot NN d2 of each sample
     __shared__ int s_pc[kFinSamples];      // pair search: nearer window samples found
     __shared__ int s_pi[kFinSamples][kCandCap];
     __shared__ double s_pd[kFinSamples][kCandCap];
     __shared__ int s_pbase, s_pnb;
     __shared__ uint32_t s_fmask;         // samples (waves) that need the exact brute force
-    __shared__ double s_fd[kFinSamples];
+    __shared__ double s_fd[kFinSamples];  // candidate-chunk bound on pbest of a near-tie
     __shared__ uint64_t s_cmask;
     __shared__ double s_rd[kFinWaves];
     __shared__ int s_ri[kFinWaves];
@@ -805,6 +923,11 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     const bool voided = st->void_seq == seq || st->error;
     const int W = voided ? 0 : st->Wp[p];
     const int ns = st->nsp[p], n = st->n;
+    if (sq && blockIdx.x == gridDim.x - 1) {  // the next window's samples (window mode)
+        samples_role(st, g, 1 - p, voided ? st->it_spec : st->wsp[p] + W,
+                     reinterpret_cast<char*>(s_xy));
+        return;
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->W = W;
         st->weff = W;
@@ -830,9 +953,15 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     if (in) {
         const int n_chunks = scan_chunks_used(ns, chunks);
         Top2 t{__builtin_inff(), __builtin_inff(), -1};
+        const double qq = sq ? sq[q] : 0.0;  // window mode: screen values are d2 - |q - o|^2
+        float cb = __builtin_inff(), cs = __builtin_inff();  // this lane's chunk: raw screen top-2
+        int ci = -1;
         if (lane < n_chunks) {
             const size_t o = (size_t)lane * stride + q;
-            t = Top2{pbest[o], psecond[o], pidx[o]};
+            cb = pbest[o];
+            cs = psecond[o];
+            ci = pidx[o];
+            t = Top2{(float)((double)cb + qq), (float)((double)cs + qq), ci};
         }
         const double xq = qx[q], yq = qy[q];
         const float fx = (float)xq, fy = (float)yq;
@@ -845,13 +974,26 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
 #pragma unroll
         for (int m = 1; m < 64; m <<= 1) t = merge_top2(t, shfl_xor_top2(t, m));
         bool flag = t.i < 0 || !(t.b < __builtin_inff());
-        double D1 = __builtin_inf();
+        double cthr = __builtin_inf();  // near-tie: the chunks with pbest <= cthr are rescanned
         if (!flag) {
-            D1 = sqrt((double)t.b);
-            if (t.s < __builtin_inff()) {
-                const double D2 = sqrt((double)t.s);
-                const double tau = 8.0 * eps_coord + 1.0e-6 * D2;
-                flag = !(D2 - D1 > tau);
+            const double D1 = sqrt((double)t.b);
+            if (!sq) {  // direct screen: f32 rounding of the coordinates and the arithmetic
+                const double tc = 16.0 * eps_coord + 4.0e-6 * (D1 + 1.0);
+                cthr = (D1 + tc) * (D1 + tc);
+                if (t.s < __builtin_inff()) {
+                    const double D2 = sqrt((double)t.s);
+                    flag = !(D2 - D1 > 8.0 * eps_coord + 1.0e-6 * D2);
+                }
+            } else {  // expanded screen: rounding of |n-o|^2 - 2(q-o).(n-o) about the block centre
+                const double qn = sqrt(qq);
+                const double D = (t.s < __builtin_inff() ? sqrt((double)t.s) : D1) + 1.0;
+                // |dE| <= 5u (|n-o|^2 + 2|q-o||n-o|) for the f32 inputs and arithmetic
+                // (u = 2^-24, |n-o| <= |q-o| + D for the winner and the runner-up), plus the f32
+                // rounding of the node coordinates (|dn| <= eps_coord / 2 per axis)
+                const double E = 4.0e-7 * ((qn + D) * (qn + D) + 2.0 * qn * (qn + D)) +
+                                 8.0 * eps_coord * (D + 1.0);
+                cthr = (double)t.b + 2.0 * E - qq;
+                if (t.s < __builtin_inff()) flag = !((double)t.s - (double)t.b > 2.0 * E);
             }
         }
         if (!flag) {
@@ -868,10 +1010,62 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
                     out_pose[3 * q + 2] = YAW[bi];
                 }
             }
-        } else if (lane == 0) {
-            atomicAdd(&st->flag_count, 1);  // statistics (nn_flagged)
-            atomicOr(&s_fmask, 1u << wave);
-            s_fd[wave] = D1;
+        } else {
+            // a near-tie: the nodes that can still be the exact nearest are those whose screen
+            // value is <= cthr.  When every candidate chunk holds one of them (its second > cthr),
+            // they are the chunks' known winners: the wave decides exactly on those and the
+            // appended nodes.  A chunk with two (or more) falls to the workgroup's brute force.
+            // The appended nodes are screened again in the direct form against the exact
+            // distance U of a known node: only those within its f32 rounding bound load f64.
+            bool need = false;
+            double bd = __builtin_inf();
+            int bi = 0x7fffffff;
+            if (t.i >= 0) {  // the screen's winner (a chunk's or an appended node)
+                const double dx = xq - X[t.i], dy = yq - Y[t.i];
+                bd = dx * dx + dy * dy;
+                bi = t.i;
+            }
+            if (!((double)cb > cthr)) {
+                if (!((double)cs > cthr) || ci < 0) {
+                    need = true;
+                } else {
+                    const double dx = xq - X[ci], dy = yq - Y[ci];
+                    argmin_pair(bd, bi, dx * dx + dy * dy, ci);
+                }
+            }
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1)
+                argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+            if (D > 0 && !__any(need)) {
+                const double U = sqrt(bd), tu = 16.0 * eps_coord + 4.0e-6 * (U + 1.0);
+                const double lim = (U + tu) * (U + tu);
+                for (int k = lane; k < D; k += 64) {
+                    const float2 v = k < Dl ? s_dn[k] : make_float2(x32[ns + k], y32[ns + k]);
+                    if (!((double)scan_d2(fx, fy, v.x, v.y) > lim)) {
+                        const double dx = xq - X[ns + k], dy = yq - Y[ns + k];
+                        argmin_pair(bd, bi, dx * dx + dy * dy, ns + k);
+                    }
+                }
+#pragma unroll
+                for (int m = 32; m > 0; m >>= 1)
+                    argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+            }
+            if (lane == 0) atomicAdd(&st->flag_count, 1);  // statistics (nn_flagged)
+            if (__any(need) || bi == 0x7fffffff) {
+                if (lane == 0) {
+                    atomicOr(&s_fmask, 1u << wave);
+                    s_fd[wave] = cthr;
+                }
+            } else if (lane == 0) {
+                out_idx[q] = bi;
+                out_d2[q] = bd;
+                s_nd2[wave] = bd;
+                if (out_pose) {
+                    out_pose[3 * q] = X[bi];
+                    out_pose[3 * q + 1] = Y[bi];
+                    out_pose[3 * q + 2] = YAW[bi];
+                }
+            }
         }
     }
     __syncthreads();
@@ -881,12 +1075,10 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     for (uint32_t fm = s_fmask; fm; fm &= fm - 1) {
         const int w = (int)__builtin_ctz(fm);
         const int qf = q0 + w;
-        const double D1 = s_fd[w];
-        const double tc = 16.0 * eps_coord + 4.0e-6 * (D1 + 1.0);
+        const double cthr = s_fd[w];
         const int n_chunks = scan_chunks_used(ns, chunks);
         if (wave == 0) {
-            const bool cc = lane < n_chunks &&
-                            !(sqrt((double)pbest[(size_t)lane * stride + qf]) > D1 + tc);
+            const bool cc = lane < n_chunks && !((double)pbest[(size_t)lane * stride + qf] > cthr);
             const uint64_t cm = __ballot(cc);
             if (lane == 0) s_cmask = cm;
         }
@@ -1011,7 +1203,7 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
 __device__ inline void window_task(int t, int W, const double* wsx, const double* wsy,
                                    const double* snap_pose, const CandEntry* cand, int* j_out,
                                    double* px, double* py, double* pyaw) {
-    if (t < W) {  // parent = the snapshot NN, whose pose nn_finalize / nn_rescan wrote
+    if (t < W) {  // parent = the snapshot NN, whose pose nn_finalize wrote
         *j_out = t;
         *px = snap_pose[3 * t];
         *py = snap_pose[3 * t + 1];
@@ -1481,7 +1673,7 @@ __host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
 
 // Window mode (pend != nullptr): a snapshot task whose verdict is not final (literal path,
 // error) and that has no nearer window sample is queued for the resolve (the others were queued
-// by window_pairs).
+// by nn_finalize's pair search).
 template <bool kLds>
 __global__ __launch_bounds__(kWalkThreads) void steer_walk_kernel(DevState* __restrict__ st,
                                                          SceneDev sc,
@@ -1536,7 +1728,7 @@ __device__ __forceinline__ int resolve_repair(const SceneDev& sc, double x, doub
 }
 
 // The sequential-consistency resolve of one window's PENDING samples, on one workgroup with its
-// state in LDS.  A sample is pending when window_pairs found an earlier window sample strictly
+// state in LDS.  A sample is pending when nn_finalize's pair search found an earlier window sample strictly
 // nearer than its snapshot NN, or when its snapshot verdict is not final (literal path, error);
 // every other sample is decided by its snapshot verdict and never touches the resolve.  The
 // replay: sample j's parent is the first ACCEPTED entry of its candidate list in (d2, i) order,
@@ -1960,7 +2152,7 @@ __device__ __attribute__((always_inline)) inline void commit_role(
 // serves the role of each workgroup (ResolveLds / the commit prefix / the screen's wave merge).
 constexpr int kWinLds = (int)sizeof(ResolveLds);
 static_assert(kWinLds <= 160 * 1024, "window kernel LDS");
-static_assert((int)(3 * kScanWaves * kQPB * 4) <= kWinLds, "screen merge fits the LDS image");
+static_assert((int)((3 * kScanWaves + 1) * kQPB * 4) <= kWinLds, "screen merge fits the LDS image");
 
 __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
     __shared__ __attribute__((aligned(16))) char smem[kWinLds];
@@ -1991,7 +2183,12 @@ __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
         }
         return;
     }
-    if (a.scan) scan_role(a, (int)blockIdx.x - 1, smem);
+    if (a.scan) {
+        if (a.gen)
+            scan_role<true>(a, (int)blockIdx.x - 1, smem);
+        else
+            scan_role<false>(a, (int)blockIdx.x - 1, smem);
+    }
 }
 
 // The resolve + commit of a window whose resolve in the window kernel needed a repair (a pair
@@ -2464,6 +2661,10 @@ WinKArgs win_args(const WindowArgs& a, int p, int gen, int resolve, int scan, in
     k.wsx32[1] = a.wsx32 + a.Kcap;
     k.wsy32[0] = a.wsy32;
     k.wsy32[1] = a.wsy32 + a.Kcap;
+    k.perm[0] = a.perm;
+    k.perm[1] = a.perm + a.Kcap;
+    k.sq[0] = a.sq;
+    k.sq[1] = a.sq + a.Kcap;
     k.pbest = a.pbest;
     k.psecond = a.psecond;
     k.pidx = a.pidx;
@@ -2480,21 +2681,43 @@ WinKArgs win_args(const WindowArgs& a, int p, int gen, int resolve, int scan, in
 }
 }  // namespace
 
+SamplesArgs samples_args(const WindowArgs& a) {
+    SamplesArgs g;
+    g.K = a.K;
+    g.target = a.target;
+    g.seed = a.seed;
+    g.minx = a.sc.minx;
+    g.maxx = a.sc.maxx;
+    g.miny = a.sc.miny;
+    g.maxy = a.sc.maxy;
+    for (int q = 0; q < 2; ++q) {
+        g.wsx[q] = a.wsx + (size_t)q * a.Kcap;
+        g.wsy[q] = a.wsy + (size_t)q * a.Kcap;
+        g.wsx32[q] = a.wsx32 + (size_t)q * a.Kcap;
+        g.wsy32[q] = a.wsy32 + (size_t)q * a.Kcap;
+        g.perm[q] = a.perm + (size_t)q * a.Kcap;
+    }
+    return g;
+}
+
 hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int64_t seq,
                          int resolve_prev) {
     const int K = a.K;
     const int p = (int)(seq & 1);
     const WinKArgs wk = win_args(a, p, 1, resolve_prev, 1, seq);
+    const SamplesArgs g = samples_args(a);
+    if (!resolve_prev)  // the batch's first window: its samples (later: the previous finalize)
+        window_samples_kernel<<<1, 1024, 0, s>>>(a.st, g, p);
     double* wsx = a.wsx + (size_t)p * a.Kcap;
     double* wsy = a.wsy + (size_t)p * a.Kcap;
     if (ev) (void)hipEventRecord(ev[0], s);
     window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
     if (ev) (void)hipEventRecord(ev[1], s);
     if (resolve_prev && !kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
-    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples, kFinThreads, 0, s>>>(
+    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples + 1, kFinThreads, 0, s>>>(
         a.st, p, seq, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, wsx, wsy, a.tr.x32, a.tr.y32,
         a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose, wk.wsx32[p],
-        wk.wsy32[p], a.cand_cnt, a.cand, a.pend);
+        wk.wsy32[p], a.cand_cnt, a.cand, a.pend, wk.sq[p], g);
     if (ev) (void)hipEventRecord(ev[2], s);
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K + kPrepThreads / 8 - 1) / (kPrepThreads / 8);
@@ -2527,7 +2750,7 @@ hipError_t launch_nearest(hipStream_t s, const WindowArgs& a) {
     nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples, kFinThreads, 0, s>>>(
         a.st, 0, 0, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, a.wsx, a.wsy, a.tr.x32,
         a.tr.y32, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, nullptr, nullptr,
-        nullptr, nullptr, nullptr, nullptr);
+        nullptr, nullptr, nullptr, nullptr, nullptr, SamplesArgs{});
     return hipGetLastError();
 }
 

@@ -86,7 +86,7 @@ struct DevState {
     int W;           // samples in the current window (0: nothing left to do / void window)
     int error;       // sticky kError seen (the reference would panic)
     int flag_count;  // NN samples flagged for the exact rescan (this window)
-    int ncomp;       // candidate entries appended by window_pairs (this window)
+    int ncomp;       // candidate entries appended by nn_finalize's pair search (this window)
     int npend;       // samples queued for the resolve's round passes (this window)
     int weff;        // the window stops before this sample (a candidate list overflowed)
     int n_scan;      // tree nodes the next window's scan covers (nodes past it: nn_finalize)
