@@ -250,7 +250,7 @@ def main():
     evals_per_launch = sp["node_evals"] / launches
     achieved_tflops = evals_per_launch * FLOP_PER_EVAL / (avg_ms * 1e-3) / 1e12
     roofline = {
-        "kernel": "nn_scan",
+        "kernel": "window_kernel (NN screen; workgroup 0 resolves the previous window)",
         "bound": "valu",
         "achieved": round(achieved_tflops, 3),
         "peak": F32_VALU_PEAK_TFLOPS,

@@ -12,7 +12,7 @@ OUT="$R/gpurun_out/prof"
 mkdir -p "$OUT"
 ARGS="--steps 20 --warmup 3 --no-cpu-baseline --no-size-sweep"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/trace.log" 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -f csv --kernel-include-regex nn_scan -d "$OUT/fetch" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/fetch.log" 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -f csv --kernel-include-regex nn_scan -d "$OUT/write" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/write.log" 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -f csv --kernel-include-regex window_kernel -d "$OUT/fetch" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/fetch.log" 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -f csv --kernel-include-regex window_kernel -d "$OUT/write" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/write.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$OUT/trace3" -o run -- python3 "$R/bench.py" --workload config3 --steps 400 > "$OUT/trace3.log" 2>&1 || exit $?
 echo profile-done
