@@ -107,6 +107,23 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
  * it; a planner must be created after it (pp_rrt_new / pp_batch_new). */
 int pp_space_set_grid(pp_ctx* ctx, const uint32_t* bits, int w, int h, double x0, double y0,
                       double cell);
+/* Space::new(bounds, Robot::new(width, height, max_steer), obstacles) (rrt.rs:25,81-122) with
+ * polygon bounds and polygon obstacles, as examples/rrt/src/main.rs:30-45 builds them from its
+ * JSON scene.  bounds_xy: nb vertices (x, y interleaved) of the bounds ring; obstacle o is the
+ * ring obs_xy[2*obs_off[o] .. 2*obs_off[o+1]); a closing repeat of the first vertex is dropped.
+ * Build-defined: geo-offset's buffers are the exact Minkowski buffers — an
+ * obstacle grows by the closed disc of radius width/2 (a segment hits it when it crosses an edge
+ * or comes within width/2 of one), the bounds shrink to the points at distance >= width/2 from
+ * the ring inside it (tested on the line's points, like geo's Contains<LineString>).
+ * rand_point samples the bounds' bbox shrunk by width/2.  Replaces the previous scene. */
+int pp_space_new_polygons(pp_ctx* ctx, const double* bounds_xy, int nb, const double* obs_xy,
+                          const int32_t* obs_off, int n_obs, double robot_width,
+                          double robot_height, double max_steer);
+/* Space::verify (rrt.rs:124-137) of k polylines on the GPU: line i is the points
+ * [off[i], off[i+1]) of x / y; ok[i] = 1 when the line is inside the bounds and meets no
+ * obstacle (a one-point line is tested as a point). */
+int pp_space_verify_batch(pp_ctx* ctx, const double* x, const double* y, const int64_t* off,
+                          int k, uint8_t* ok);
 /* the shrunken bounds bbox (minx, maxx, miny, maxy) sampled by Space::rand_point (rrt.rs:84-106) */
 int pp_space_get_bounds(pp_ctx* ctx, double out_minx_maxx_miny_maxy[4]);
 

@@ -10,7 +10,7 @@ methods do (``hypot`` goes through libm via ctypes, see below), and CPython eval
 the C oracle are expected to agree bit for bit.  Parity against the Rust crate itself is
 **unpinned** (no toolchain, no reference goldens: SURVEY.md K3/K7).
 
-Build-defined deviations are the same as the C oracle's header lists (Q7-Q10).
+Build-defined deviations are the same as the C oracle's header lists (Q7-Q10, Q10p).
 """
 from __future__ import annotations
 
@@ -251,6 +251,64 @@ def _seg_hits_any(xs, ys, cx, cy, r2):
     return bool(np.any(ex * ex + ey * ey <= r2[None, :]))
 
 
+def _seg_point_d2(ax, ay, bx, by, cx, cy):
+    """squared distance from c to the closed segment a-b (broadcasting; same op order as C)"""
+    vx, vy = bx - ax, by - ay
+    wx, wy = cx - ax, cy - ay
+    l2 = vx * vx + vy * vy
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t = (wx * vx + wy * vy) / l2
+    t = np.where(l2 > 0.0, t, 0.0)
+    t = np.where(t < 0.0, 0.0, np.where(t > 1.0, 1.0, t))
+    ex, ey = wx - t * vx, wy - t * vy
+    return ex * ex + ey * ey
+
+
+def _ray_crosses(px, py, xi, yi, xj, yj):
+    """even-odd step: edge (xi, yi)-(xj, yj) crosses the ray from (px, py) toward +x"""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        xc = (xj - xi) * (py - yi) / (yj - yi) + xi
+    return ((yi > py) != (yj > py)) & (px < xc)
+
+
+def _polygon_verify(scene, xs, ys):
+    """Q10p (polygon scenes): points in the eroded bounds ring, segments clear of the obstacle
+    edge buffers (cross or within h), point 0 outside every obstacle polygon."""
+    h2 = scene["h2"]
+    bvx, bvy = scene["bvx"], scene["bvy"]
+    bjx, bjy = np.roll(bvx, -1), np.roll(bvy, -1)
+    px, py = xs[:, None], ys[:, None]
+    inside = np.sum(_ray_crosses(px, py, bvx[None, :], bvy[None, :], bjx[None, :], bjy[None, :]),
+                    axis=1) % 2 == 1
+    near = np.any(_seg_point_d2(bvx[None, :], bvy[None, :], bjx[None, :], bjy[None, :], px, py) < h2,
+                  axis=1)
+    if not np.all(inside & ~near):
+        return False
+    ex0, ey0, ex1, ey1 = scene["ex0"], scene["ey0"], scene["ex1"], scene["ey1"]
+    if len(ex0) == 0:
+        return True
+    if len(xs) == 1:
+        ax, ay, bx, by = xs[:, None], ys[:, None], xs[:, None], ys[:, None]
+    else:
+        ax, ay, bx, by = xs[:-1, None], ys[:-1, None], xs[1:, None], ys[1:, None]
+    e0x, e0y, e1x, e1y = ex0[None, :], ey0[None, :], ex1[None, :], ey1[None, :]
+    d1 = (e1x - e0x) * (ay - e0y) - (e1y - e0y) * (ax - e0x)
+    d2 = (e1x - e0x) * (by - e0y) - (e1y - e0y) * (bx - e0x)
+    d3 = (bx - ax) * (e0y - ay) - (by - ay) * (e0x - ax)
+    d4 = (bx - ax) * (e1y - ay) - (by - ay) * (e1x - ax)
+    cross = (((d1 > 0.0) & (d2 < 0.0)) | ((d1 < 0.0) & (d2 > 0.0))) & \
+            (((d3 > 0.0) & (d4 < 0.0)) | ((d3 < 0.0) & (d4 > 0.0)))
+    hit = cross | (_seg_point_d2(e0x, e0y, e1x, e1y, ax, ay) <= h2) | \
+        (_seg_point_d2(e0x, e0y, e1x, e1y, bx, by) <= h2) | \
+        (_seg_point_d2(ax, ay, bx, by, e0x, e0y) <= h2) | \
+        (_seg_point_d2(ax, ay, bx, by, e1x, e1y) <= h2)
+    if np.any(hit):
+        return False
+    c = _ray_crosses(xs[0], ys[0], ex0, ey0, ex1, ey1).astype(np.int64)
+    per_poly = np.bincount(scene["epoly"], weights=c)
+    return not np.any(per_poly.astype(np.int64) % 2 == 1)
+
+
 def verify_line(scene, xs, ys):  # rrt.rs:124-137 (Q10)
     xs = np.asarray(xs, dtype=np.float64)
     ys = np.asarray(ys, dtype=np.float64)
@@ -260,6 +318,8 @@ def verify_line(scene, xs, ys):  # rrt.rs:124-137 (Q10)
         return False
     if np.any(ys < scene["miny"]) or np.any(ys > scene["maxy"]):
         return False
+    if scene.get("bvx") is not None:  # polygon scene (Q10p)
+        return _polygon_verify(scene, xs, ys)
     if scene.get("grid") is not None:  # config 4: every point in a free cell
         bits, w, gx0, gy0, cell = scene["grid"]
         inv = 1.0 / cell

@@ -39,6 +39,10 @@ class Scene(C.Structure):
         ("turn_radius", C.c_double), ("step_size", C.c_double),
         ("bits", C.POINTER(C.c_uint32)), ("bw", C.c_int), ("bh", C.c_int), ("bwords", C.c_int),
         ("bx0", C.c_double), ("by0", C.c_double), ("binv", C.c_double),
+        ("nbv", C.c_int), ("bvx", C.POINTER(C.c_double)), ("bvy", C.POINTER(C.c_double)),
+        ("ne", C.c_int), ("ex0", C.POINTER(C.c_double)), ("ey0", C.POINTER(C.c_double)),
+        ("ex1", C.POINTER(C.c_double)), ("ey1", C.POINTER(C.c_double)),
+        ("epoly", C.POINTER(C.c_int)), ("h2", C.c_double),
     ]
 
 
@@ -134,12 +138,25 @@ def pi_2_pi(x):
 
 
 # ------------------------------------------------------------------------------- scene
+def _ring(points):
+    """polygon ring (N, 2) without an exact closing repeat of the first vertex"""
+    r = np.asarray(points, dtype=np.float64).reshape(-1, 2)
+    if len(r) > 1 and r[0, 0] == r[-1, 0] and r[0, 1] == r[-1, 1]:
+        r = r[:-1]
+    return np.ascontiguousarray(r)
+
+
 class OracleScene:
     """Space::new (rrt.rs:81-122) restated for the oracle: bounds rectangle shrunk by width/2,
-    discs inflated by width/2 (Q10)."""
+    discs inflated by width/2 (Q10).  Polygon mode (Q10p): ``polygons=(bounds_ring,
+    [obstacle rings])`` — the sampling box is the ring's bbox shrunk by width/2, the obstacles
+    are edge lists with exact Minkowski buffers."""
 
-    def __init__(self, bounds, width, circles, turn_radius, step_size, grid=None):
+    def __init__(self, bounds, width, circles, turn_radius, step_size, grid=None, polygons=None):
         half = width / 2.0
+        if polygons is not None:
+            bring = _ring(polygons[0])
+            bounds = (bring[:, 0].min(), bring[:, 1].min(), bring[:, 0].max(), bring[:, 1].max())
         x0, y0, x1, y1 = bounds
         self.minx, self.miny, self.maxx, self.maxy = x0 + half, y0 + half, x1 - half, y1 - half
         circ = np.asarray(circles, dtype=np.float64).reshape(-1, 3)
@@ -159,16 +176,48 @@ class OracleScene:
             self._c.bits = self.bits.ctypes.data_as(C.POINTER(C.c_uint32))
             self._c.bw, self._c.bh, self._c.bwords = int(w), self.bits.shape[0], self.bits.shape[1]
             self._c.bx0, self._c.by0, self._c.binv = float(gx0), float(gy0), 1.0 / float(cell)
+        self.polygons = None
+        if polygons is not None:
+            self.bvx = np.ascontiguousarray(bring[:, 0])
+            self.bvy = np.ascontiguousarray(bring[:, 1])
+            e0, e1, ep = [], [], []
+            for k, o in enumerate(polygons[1]):
+                r = _ring(o)
+                if len(r) == 0:
+                    continue
+                e0.append(r)
+                e1.append(np.roll(r, -1, axis=0))
+                ep.append(np.full(len(r), k, dtype=np.int32))
+            E0 = np.concatenate(e0) if e0 else np.zeros((0, 2))
+            E1 = np.concatenate(e1) if e1 else np.zeros((0, 2))
+            self.ex0, self.ey0 = np.ascontiguousarray(E0[:, 0]), np.ascontiguousarray(E0[:, 1])
+            self.ex1, self.ey1 = np.ascontiguousarray(E1[:, 0]), np.ascontiguousarray(E1[:, 1])
+            self.epoly = np.ascontiguousarray(np.concatenate(ep) if ep else np.zeros(0, np.int32))
+            self.h2 = half * half
+            self.polygons = (bring, [_ring(o) for o in polygons[1]])
+            c = self._c
+            c.nbv, c.bvx, c.bvy = len(self.bvx), _dp(self.bvx), _dp(self.bvy)
+            c.ne = len(self.ex0)
+            c.ex0, c.ey0, c.ex1, c.ey1 = _dp(self.ex0), _dp(self.ey0), _dp(self.ex1), _dp(self.ey1)
+            c.epoly = self.epoly.ctypes.data_as(C.POINTER(C.c_int))
+            c.h2 = self.h2
 
     @classmethod
     def from_raw(cls, raw):
+        polys = None
+        if "bounds_polygon" in raw:
+            polys = (raw["bounds_polygon"], raw["obstacle_polygons"])
         return cls(raw["bounds"], raw["robot"][0], raw["circles"], raw["robot"][2], raw["step_size"],
-                   grid=raw.get("grid"))
+                   grid=raw.get("grid"), polygons=polys)
 
     def as_dict(self):
-        return {"minx": self.minx, "maxx": self.maxx, "miny": self.miny, "maxy": self.maxy,
-                "cx": self.cx, "cy": self.cy, "r2": self.r2, "turn_radius": self.turn_radius,
-                "step_size": self.step_size, "grid": self.grid}
+        d = {"minx": self.minx, "maxx": self.maxx, "miny": self.miny, "maxy": self.maxy,
+             "cx": self.cx, "cy": self.cy, "r2": self.r2, "turn_radius": self.turn_radius,
+             "step_size": self.step_size, "grid": self.grid}
+        if self.polygons is not None:
+            d.update(bvx=self.bvx, bvy=self.bvy, ex0=self.ex0, ey0=self.ey0, ex1=self.ex1,
+                     ey1=self.ey1, epoly=self.epoly, h2=self.h2)
+        return d
 
     def verify_line(self, xs, ys):
         xs = np.ascontiguousarray(xs, dtype=np.float64)

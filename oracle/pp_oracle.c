@@ -23,7 +23,10 @@
  *   Q8  sequential spec (one rayon thread) in place of the 4-thread pool;
  *   Q9  exact brute-force NN on dx*dx+dy*dy, lowest index wins ties (rstar's pruning is inexact);
  *   Q10 obstacles are analytic discs of radius r + robot.width/2 and the bounds an axis-aligned
- *       rectangle shrunk by robot.width/2; polyline-vs-disc uses exact segment distance.
+ *       rectangle shrunk by robot.width/2; polyline-vs-disc uses exact segment distance;
+ *   Q10p polygon scenes (examples/rrt/src/main.rs:30-45): the geo-offset buffers are the exact
+ *       Minkowski buffers (obstacle polygon + closed disc of radius width/2; bounds polygon eroded
+ *       by it), tested on the line's segments and points (see orc_verify_line).
  */
 #include <math.h>
 #include <stdint.h>
@@ -341,6 +344,20 @@ typedef struct {
     const uint32_t* bits;
     int bw, bh, bwords;
     double bx0, by0, binv;
+    /* polygon mode (pp_space_new_polygons; build-defined Q10p, see orc_verify_line): the bounds
+     * polygon ring (nbv vertices, no closing repeat; 0 = the rectangle above only) and the
+     * obstacle polygons as ne edges (ex0, ey0)-(ex1, ey1), the edges of one polygon consecutive
+     * with their polygon id in epoly; h2 = (width/2)^2.  ne > 0 replaces the discs. */
+    int nbv;
+    const double* bvx;
+    const double* bvy;
+    int ne;
+    const double* ex0;
+    const double* ey0;
+    const double* ex1;
+    const double* ey1;
+    const int* epoly;
+    double h2;
 } orc_scene;
 
 typedef struct {
@@ -352,9 +369,8 @@ typedef struct {
     int n;
 } orc_tree;
 
-/* polyline segment vs closed disc: exact closest point on the segment */
-static int seg_hits_disc(double ax, double ay, double bx, double by, double cx, double cy,
-                         double r2) {
+/* squared distance from (cx, cy) to the closed segment a-b: exact closest point on the segment */
+static double seg_point_d2(double ax, double ay, double bx, double by, double cx, double cy) {
     double vx = bx - ax, vy = by - ay;
     double wx = cx - ax, wy = cy - ay;
     double l2 = vx * vx + vy * vy;
@@ -365,11 +381,73 @@ static int seg_hits_disc(double ax, double ay, double bx, double by, double cx, 
         else if (t > 1.0) t = 1.0;
     }
     double ex = wx - t * vx, ey = wy - t * vy;
-    return ex * ex + ey * ey <= r2;
+    return ex * ex + ey * ey;
+}
+
+/* polyline segment vs closed disc */
+static int seg_hits_disc(double ax, double ay, double bx, double by, double cx, double cy,
+                         double r2) {
+    return seg_point_d2(ax, ay, bx, by, cx, cy) <= r2;
+}
+
+/* ---- polygon mode (Q10p): geo's Contains / Intersects on geo-offset buffers (rrt.rs:62-68,
+ * 82, 108-111, 124-137) restated as the exact Minkowski buffers of the polygons: an obstacle
+ * grows by the closed disc of radius h = width/2, the bounds shrink to the points whose disc of
+ * radius h stays inside.  geo-offset's arc approximation is not reproduced (parity unpinned,
+ * SURVEY.md §8c). */
+
+/* crossing-number step: the edge (xi, yi)-(xj, yj) crosses the ray from (px, py) toward +x
+ * (half-open in y, the classic even-odd rule) */
+static int ray_crosses(double px, double py, double xi, double yi, double xj, double yj) {
+    return ((yi > py) != (yj > py)) && (px < (xj - xi) * (py - yi) / (yj - yi) + xi);
+}
+
+/* the point lies in the shrunken bounds polygon: inside the ring (even-odd) and at distance >= h
+ * from every bounds edge */
+static int in_poly_bounds(const orc_scene* sc, double x, double y) {
+    int inside = 0;
+    for (int i = 0; i < sc->nbv; ++i) {
+        const int j = i + 1 == sc->nbv ? 0 : i + 1;
+        const double xi = sc->bvx[i], yi = sc->bvy[i], xj = sc->bvx[j], yj = sc->bvy[j];
+        if (ray_crosses(x, y, xi, yi, xj, yj)) inside ^= 1;
+        if (seg_point_d2(xi, yi, xj, yj, x, y) < sc->h2) return 0;
+    }
+    return inside;
+}
+
+/* polyline segment a-b vs the buffer of one obstacle edge e0-e1: the segments cross properly,
+ * or an endpoint of one lies within h of the other (touching counts: <= h^2) */
+static int seg_hits_edge(double ax, double ay, double bx, double by, double e0x, double e0y,
+                         double e1x, double e1y, double h2) {
+    const double d1 = (e1x - e0x) * (ay - e0y) - (e1y - e0y) * (ax - e0x);
+    const double d2 = (e1x - e0x) * (by - e0y) - (e1y - e0y) * (bx - e0x);
+    const double d3 = (bx - ax) * (e0y - ay) - (by - ay) * (e0x - ax);
+    const double d4 = (bx - ax) * (e1y - ay) - (by - ay) * (e1x - ax);
+    if (((d1 > 0.0 && d2 < 0.0) || (d1 < 0.0 && d2 > 0.0)) &&
+        ((d3 > 0.0 && d4 < 0.0) || (d3 < 0.0 && d4 > 0.0)))
+        return 1;
+    return seg_point_d2(e0x, e0y, e1x, e1y, ax, ay) <= h2 ||
+           seg_point_d2(e0x, e0y, e1x, e1y, bx, by) <= h2 ||
+           seg_point_d2(ax, ay, bx, by, e0x, e0y) <= h2 ||
+           seg_point_d2(ax, ay, bx, by, e1x, e1y) <= h2;
+}
+
+/* the point lies inside some obstacle polygon (even-odd over each polygon's edges) */
+static int in_obstacle(const orc_scene* sc, double x, double y) {
+    int inside = 0;
+    for (int k = 0; k < sc->ne; ++k) {
+        if (k > 0 && sc->epoly[k] != sc->epoly[k - 1]) {
+            if (inside) return 1;
+            inside = 0;
+        }
+        if (ray_crosses(x, y, sc->ex0[k], sc->ey0[k], sc->ex1[k], sc->ey1[k])) inside ^= 1;
+    }
+    return inside;
 }
 
 static int in_bounds(const orc_scene* sc, double x, double y) {
-    return x >= sc->minx && x <= sc->maxx && y >= sc->miny && y <= sc->maxy;
+    if (!(x >= sc->minx && x <= sc->maxx && y >= sc->miny && y <= sc->maxy)) return 0;
+    return sc->nbv == 0 || in_poly_bounds(sc, x, y);
 }
 
 /* config 4 probe: cell (floor((x - x0) * inv), floor((y - y0) * inv)); outside = occupied */
@@ -382,7 +460,10 @@ static int grid_occupied(const orc_scene* sc, double x, double y) {
 
 /* Space::verify, rrt.rs:124-137: bounds.contains(line) && no obstacle intersects the line.
  * A one-point line is tested as a point (degenerate segment).  With an occupancy grid: every
- * point in bounds and in a free cell. */
+ * point in bounds and in a free cell.  Polygon mode (Q10p): every point in the bounds rectangle
+ * and in the eroded bounds polygon (geo's Contains<LineString> tests the points against the
+ * exterior), no segment within h of an obstacle edge or crossing it, and point 0 outside every
+ * obstacle polygon (with no segment meeting an edge buffer the whole line is on one side). */
 int orc_verify_line(const orc_scene* sc, const double* x, const double* y, int n) {
     if (n <= 0) return 1;
     for (int i = 0; i < n; ++i)
@@ -391,6 +472,18 @@ int orc_verify_line(const orc_scene* sc, const double* x, const double* y, int n
         for (int i = 0; i < n; ++i)
             if (grid_occupied(sc, x[i], y[i])) return 0;
         return 1;
+    }
+    if (sc->ne > 0) { /* polygon obstacles: every segment vs every edge buffer, then one point
+                       * inside test (no segment meets a buffer: the line is on one side) */
+        for (int k = 0; k < sc->ne; ++k) {
+            const double e0x = sc->ex0[k], e0y = sc->ey0[k], e1x = sc->ex1[k], e1y = sc->ey1[k];
+            if (n == 1 && seg_hits_edge(x[0], y[0], x[0], y[0], e0x, e0y, e1x, e1y, sc->h2))
+                return 0;
+            for (int i = 0; i + 1 < n; ++i)
+                if (seg_hits_edge(x[i], y[i], x[i + 1], y[i + 1], e0x, e0y, e1x, e1y, sc->h2))
+                    return 0;
+        }
+        return !in_obstacle(sc, x[0], y[0]);
     }
     if (n == 1) {
         for (int k = 0; k < sc->m; ++k)

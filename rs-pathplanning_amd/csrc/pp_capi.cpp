@@ -109,6 +109,15 @@ struct pp_ctx {
     DBuf<uint32_t> d_bits;
     int bw = 0, bh = 0, bwords = 0, lds_bits_bytes = 0;
     double bx0 = 0, by0 = 0, binv = 1;
+    // polygon mode (pp_space_new_polygons, Q10p): obstacle edges, bounds ring; host copies for
+    // the point checks (root / query starts)
+    int ne = 0, nbv = 0;
+    double h2 = 0.0;
+    float cull_slack = 1.0e-3f;
+    DBuf<double> d_ex0, d_ey0, d_ex1, d_ey1, d_bvx, d_bvy;
+    DBuf<int> d_epoly;
+    std::vector<double> h_ex0, h_ey0, h_ex1, h_ey1, h_bvx, h_bvy;
+    std::vector<int> h_epoly;
 
     // ---- planner (RRT)
     bool has_rrt = false;
@@ -121,6 +130,7 @@ struct pp_ctx {
     int64_t n = 0;    // mirror of DevState.n
     int64_t cap = 0;  // tree capacity
     double eps_coord = 0.0;
+    bool root_blocked = false;  // polygon mode: the root fails verify (nothing is ever inserted)
     DBuf<float> x32, y32;
     DBuf<double> X, Y, YAW;
     DBuf<int> PAR;
@@ -159,6 +169,8 @@ struct pp_ctx {
     DBuf<int> mq_par, mq_n, mq_status, mq_err;
     DBuf<int64_t> mq_it, mq_evals;
     DBuf<uint64_t> mq_seed;
+    DBuf<uint8_t> mq_blocked;
+    bool mq_any_blocked = false;
     DBuf<SteerTask> mq_tasks;
     DBuf<PrepRec> mq_rec;
     DBuf<DevState> mq_state;
@@ -216,7 +228,37 @@ struct pp_ctx {
             s.lds_bytes = lds_bits_bytes;
             s.img = d_gimg.p;
         }
+        s.ne = ne;
+        s.ex0 = d_ex0.p;
+        s.ey0 = d_ey0.p;
+        s.ex1 = d_ex1.p;
+        s.ey1 = d_ey1.p;
+        s.epoly = d_epoly.p;
+        s.h2 = h2;
+        s.nbv = nbv;
+        s.bvx = d_bvx.p;
+        s.bvy = d_bvy.p;
+        s.cull_slack = cull_slack;
+        s.root_blocked = root_blocked ? 1 : 0;
         return s;
+    }
+    // Space::verify of the one-point line [(x, y)] on the host, polygon mode (Q10p; the same
+    // arithmetic as the kernels and the oracle): bounds, edge buffers, inside an obstacle
+    bool point_ok(double x, double y) const {
+        SceneDev s{};
+        s.minx = minx;
+        s.maxx = maxx;
+        s.miny = miny;
+        s.maxy = maxy;
+        s.nbv = nbv;
+        s.bvx = h_bvx.data();
+        s.bvy = h_bvy.data();
+        s.h2 = h2;
+        if (!point_in_bounds(s, x, y)) return false;
+        for (int k = 0; k < ne; ++k)
+            if (seg_hits_edge(x, y, x, y, h_ex0[k], h_ey0[k], h_ex1[k], h_ey1[k], h2)) return false;
+        return !in_obstacle(ne, h_ex0.data(), h_ey0.data(), h_ex1.data(), h_ey1.data(),
+                            h_epoly.data(), x, y);
     }
     TreeDev tree_dev() const {
         TreeDev t;
@@ -393,6 +435,7 @@ MqArgs mq_args(pp_ctx* c) {
     a.mq.it = c->mq_it.p;
     a.mq.evals = c->mq_evals.p;
     a.mq.seed = c->mq_seed.p;
+    a.mq.blocked = c->mq_any_blocked ? c->mq_blocked.p : nullptr;
     a.sc = c->scene_dev();
     a.sc.step_size = c->mq_step;
     a.st = c->mq_state.p;
@@ -543,30 +586,17 @@ int pp_dubins_path_planning_batch(pp_ctx* ctx, const pp_dubins_config* confs, in
     return PP_OK;
 }
 
-int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double robot_width,
-                 double robot_height, double max_steer, const double* cx, const double* cy,
-                 const double* r, int m) {
-    int rc = check_ctx(ctx, false, false);
-    if (rc) return rc;
-    if (m < 0 || (m > 0 && (!cx || !cy || !r)))
-        return set_err(PP_ERR_INVALID_ARGUMENT, "bad obstacle arrays");
-    if (!(robot_width >= 0.0) || !(max_steer > 0.0))
-        return set_err(PP_ERR_INVALID_ARGUMENT, "robot width must be >= 0 and max_steer > 0");
-    // Space::new, rrt.rs:82-111: bounds offset by -width/2, obstacles by +width/2
-    const double half = robot_width / 2.0;
-    const double minx = x0 + half, maxx = x1 - half, miny = y0 + half, maxy = y1 - half;
-    if (!(minx < maxx) || !(miny < maxy))  // gen_range asserts low < high (rrt.rs:142-143)
-        return set_err(PP_ERR_INVALID_ARGUMENT, "shrunken bounds are empty");
-    std::vector<double> r2(m), rc_(m);
-    std::vector<float4> d4(m);
-    for (int k = 0; k < m; ++k) {
-        const double reff = r[k] + half;
-        r2[k] = reff * reff;
-        rc_[k] = reff * (1.0 + 1e-9) + 1e-9;
-        // f32 cull copy: the radius rounded up (the cull only ever over-includes)
-        d4[k] = make_float4((float)cx[k], (float)cy[k], std::nextafter((float)rc_[k], 1e30f), 0.0f);
-    }
-    // uniform grid over the discs (square cells, about one cell per disc)
+namespace {
+// Uniform grid over the scene's collision items (discs, or polygon edges in Q10p) for the steer
+// kernels' exact cull: item k is listed in every cell its cull box [bx0, bx1] x [by0, by1]
+// touches (CSR: goff, gitems), cells clamped to the sampling box; f32 cull discs d4 (centre,
+// radius rounded up).  Uploads everything and the LDS image [goff | items | d4] when it fits.
+int build_item_grid(pp_ctx* ctx, double minx, double maxx, double miny, double maxy,
+                    const std::vector<double>& bx0, const std::vector<double>& bx1,
+                    const std::vector<double>& by0, const std::vector<double>& by1,
+                    const std::vector<float4>& d4) {
+    const int m = (int)d4.size();
+    // square cells, about one cell per item
     const double spanx = maxx - minx, spany = maxy - miny;
     const double span = std::max(spanx, spany);
     const int per_axis = std::max(1, std::min(256, (int)std::ceil(std::sqrt((double)std::max(m, 1)))));
@@ -582,8 +612,8 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
     {
         std::vector<std::vector<int>> lists((size_t)gnx * gny);
         for (int k = 0; k < m; ++k) {
-            const int x0c = cell_of(cx[k] - rc_[k], minx, gnx), x1c = cell_of(cx[k] + rc_[k], minx, gnx);
-            const int y0c = cell_of(cy[k] - rc_[k], miny, gny), y1c = cell_of(cy[k] + rc_[k], miny, gny);
+            const int x0c = cell_of(bx0[k], minx, gnx), x1c = cell_of(bx1[k], minx, gnx);
+            const int y0c = cell_of(by0[k], miny, gny), y1c = cell_of(by1[k], miny, gny);
             for (int gy = y0c; gy <= y1c; ++gy)
                 for (int gx = x0c; gx <= x1c; ++gx) lists[(size_t)gy * gnx + gx].push_back(k);
         }
@@ -598,12 +628,11 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
     if (!gitems.empty())
         PP_HIP(hipMemcpy(ctx->d_gitems.p, gitems.data(), gitems.size() * sizeof(int), hipMemcpyHostToDevice));
     {  // LDS image for the steer kernels: [goff | items | d4], 16-byte aligned parts (the f64
-       // discs of the exact test stay in global memory: the f32 cull leaves few exact tests)
+       // items of the exact test stay in global memory: the f32 cull leaves few exact tests)
         auto al = [](size_t b) { return (int)((b + 15) & ~(size_t)15); };
         const int o_goff = 0;
         const int o_items = o_goff + al(goff.size() * sizeof(int));
         const int o_d4 = o_items + al(gitems.size() * sizeof(int));
-        const int o_cx = -1, o_cy = -1, o_r2 = -1;
         const int total = o_d4 + al((size_t)m * sizeof(float4));
         const bool fits = total <= 64 * 1024;  // 2 workgroups per CU fit in 160 KB
         ctx->lds_bytes = fits ? total : 0;
@@ -618,9 +647,7 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
         }
         ctx->lds_goff = o_goff;
         ctx->lds_items = o_items;
-        ctx->lds_cx = o_cx;
-        ctx->lds_cy = o_cy;
-        ctx->lds_r2 = o_r2;
+        ctx->lds_cx = ctx->lds_cy = ctx->lds_r2 = -1;
         ctx->lds_d4 = o_d4;
     }
     ctx->gx0 = minx;
@@ -628,19 +655,75 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
     ctx->ginv = ginv;
     ctx->gnx = gnx;
     ctx->gny = gny;
+    PP_HIP(ctx->d_d4.reserve((size_t)std::max(m, 1)));
+    if (m > 0) PP_HIP(hipMemcpy(ctx->d_d4.p, d4.data(), m * sizeof(float4), hipMemcpyHostToDevice));
+    return PP_OK;
+}
+
+// f32 cull slack: the rounding of coordinates of magnitude <= mx to f32 (both ends of a
+// difference, both axes) with a wide margin; never below the 1e-3 that covers |c| <= 2^10
+float cull_slack_for(double mx) {
+    return (float)std::max(1.0e-3, 16.0 * mx * std::ldexp(1.0, -24));
+}
+
+// reset the polygon-mode part of the scene (pp_space_new / pp_space_new_polygons)
+void clear_polygons(pp_ctx* ctx) {
+    ctx->ne = 0;
+    ctx->nbv = 0;
+    ctx->h_ex0.clear();
+    ctx->h_ey0.clear();
+    ctx->h_ex1.clear();
+    ctx->h_ey1.clear();
+    ctx->h_epoly.clear();
+    ctx->h_bvx.clear();
+    ctx->h_bvy.clear();
+}
+}  // namespace
+
+int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double robot_width,
+                 double robot_height, double max_steer, const double* cx, const double* cy,
+                 const double* r, int m) {
+    int rc = check_ctx(ctx, false, false);
+    if (rc) return rc;
+    if (m < 0 || (m > 0 && (!cx || !cy || !r)))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad obstacle arrays");
+    if (!(robot_width >= 0.0) || !(max_steer > 0.0))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "robot width must be >= 0 and max_steer > 0");
+    // Space::new, rrt.rs:82-111: bounds offset by -width/2, obstacles by +width/2
+    const double half = robot_width / 2.0;
+    const double minx = x0 + half, maxx = x1 - half, miny = y0 + half, maxy = y1 - half;
+    if (!(minx < maxx) || !(miny < maxy))  // gen_range asserts low < high (rrt.rs:142-143)
+        return set_err(PP_ERR_INVALID_ARGUMENT, "shrunken bounds are empty");
+    std::vector<double> r2(m), rc_(m), bx0(m), bx1(m), by0(m), by1(m);
+    std::vector<float4> d4(m);
+    double mx = std::max({std::fabs(minx), std::fabs(maxx), std::fabs(miny), std::fabs(maxy)});
+    for (int k = 0; k < m; ++k) {
+        const double reff = r[k] + half;
+        r2[k] = reff * reff;
+        rc_[k] = reff * (1.0 + 1e-9) + 1e-9;
+        // f32 cull copy: the radius rounded up (the cull only ever over-includes)
+        d4[k] = make_float4((float)cx[k], (float)cy[k], std::nextafter((float)rc_[k], 1e30f), 0.0f);
+        bx0[k] = cx[k] - rc_[k];
+        bx1[k] = cx[k] + rc_[k];
+        by0[k] = cy[k] - rc_[k];
+        by1[k] = cy[k] + rc_[k];
+        mx = std::max({mx, std::fabs(cx[k]) + rc_[k], std::fabs(cy[k]) + rc_[k]});
+    }
+    if ((rc = build_item_grid(ctx, minx, maxx, miny, maxy, bx0, bx1, by0, by1, d4))) return rc;
     const size_t mm = (size_t)std::max(m, 1);
     PP_HIP(ctx->d_cx.reserve(mm));
     PP_HIP(ctx->d_cy.reserve(mm));
     PP_HIP(ctx->d_r2.reserve(mm));
     PP_HIP(ctx->d_rcull.reserve(mm));
-    PP_HIP(ctx->d_d4.reserve(mm));
     if (m > 0) {
         PP_HIP(hipMemcpy(ctx->d_cx.p, cx, m * sizeof(double), hipMemcpyHostToDevice));
         PP_HIP(hipMemcpy(ctx->d_cy.p, cy, m * sizeof(double), hipMemcpyHostToDevice));
         PP_HIP(hipMemcpy(ctx->d_r2.p, r2.data(), m * sizeof(double), hipMemcpyHostToDevice));
         PP_HIP(hipMemcpy(ctx->d_rcull.p, rc_.data(), m * sizeof(double), hipMemcpyHostToDevice));
-        PP_HIP(hipMemcpy(ctx->d_d4.p, d4.data(), m * sizeof(float4), hipMemcpyHostToDevice));
     }
+    clear_polygons(ctx);
+    ctx->h2 = half * half;
+    ctx->cull_slack = cull_slack_for(mx);
     ctx->minx = minx;
     ctx->maxx = maxx;
     ctx->miny = miny;
@@ -652,6 +735,121 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
     ctx->has_grid = false;
     ctx->has_scene = true;
     ctx->has_rrt = false;  // a planner belongs to one Space (RRT::new moves it in, rrt.rs:342)
+    ctx->has_batch = false;
+    return PP_OK;
+}
+
+int pp_space_new_polygons(pp_ctx* ctx, const double* bounds_xy, int nb, const double* obs_xy,
+                          const int32_t* obs_off, int n_obs, double robot_width,
+                          double robot_height, double max_steer) {
+    int rc = check_ctx(ctx, false, false);
+    if (rc) return rc;
+    if (!bounds_xy || nb < 3 || n_obs < 0 || (n_obs > 0 && (!obs_xy || !obs_off)))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad polygon arrays (bounds need >= 3 vertices)");
+    if (!(robot_width >= 0.0) || !(max_steer > 0.0))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "robot width must be >= 0 and max_steer > 0");
+    // rings: a closing repeat of the first vertex is dropped (geo closes rings itself)
+    auto ring = [](const double* xy, int n, std::vector<double>& vx, std::vector<double>& vy) {
+        if (n > 1 && xy[0] == xy[2 * (n - 1)] && xy[1] == xy[2 * (n - 1) + 1]) --n;
+        vx.resize(n);
+        vy.resize(n);
+        for (int i = 0; i < n; ++i) {
+            vx[i] = xy[2 * i];
+            vy[i] = xy[2 * i + 1];
+        }
+    };
+    std::vector<double> bvx, bvy;
+    ring(bounds_xy, nb, bvx, bvy);
+    if (bvx.size() < 3) return set_err(PP_ERR_INVALID_ARGUMENT, "bounds ring has < 3 vertices");
+    for (size_t i = 0; i < bvx.size(); ++i)
+        if (!std::isfinite(bvx[i]) || !std::isfinite(bvy[i]))
+            return set_err(PP_ERR_INVALID_ARGUMENT, "non-finite bounds vertex");
+    // Space::new, rrt.rs:82-106: rand_point samples the bbox of the shrunken bounds — here the
+    // bounds' bbox shrunk by width/2, which contains the eroded polygon (Q10p)
+    const double half = robot_width / 2.0;
+    const double minx = *std::min_element(bvx.begin(), bvx.end()) + half;
+    const double maxx = *std::max_element(bvx.begin(), bvx.end()) - half;
+    const double miny = *std::min_element(bvy.begin(), bvy.end()) + half;
+    const double maxy = *std::max_element(bvy.begin(), bvy.end()) - half;
+    if (!(minx < maxx) || !(miny < maxy))  // gen_range asserts low < high (rrt.rs:142-143)
+        return set_err(PP_ERR_INVALID_ARGUMENT, "shrunken bounds are empty");
+    double mx = 0.0;
+    for (size_t i = 0; i < bvx.size(); ++i) mx = std::max({mx, std::fabs(bvx[i]), std::fabs(bvy[i])});
+    // obstacle edges (rrt.rs:108-111: every obstacle buffered by width/2)
+    std::vector<double> ex0, ey0, ex1, ey1, bx0, bx1, by0, by1;
+    std::vector<int> epoly;
+    std::vector<float4> d4;
+    const double rcull = half * (1.0 + 1e-9) + 1e-9;
+    for (int o = 0; o < n_obs; ++o) {
+        const int a = obs_off[o], b = obs_off[o + 1];
+        if (a < 0 || b < a) return set_err(PP_ERR_INVALID_ARGUMENT, "bad obstacle offsets");
+        std::vector<double> vx, vy;
+        ring(obs_xy + 2 * (size_t)a, b - a, vx, vy);
+        const int n = (int)vx.size();
+        if (n == 0) continue;
+        for (int i = 0; i < n; ++i) {
+            if (!std::isfinite(vx[i]) || !std::isfinite(vy[i]))
+                return set_err(PP_ERR_INVALID_ARGUMENT, "non-finite obstacle vertex");
+            const int j = i + 1 == n ? 0 : i + 1;
+            ex0.push_back(vx[i]);
+            ey0.push_back(vy[i]);
+            ex1.push_back(vx[j]);
+            ey1.push_back(vy[j]);
+            epoly.push_back(o);
+            bx0.push_back(std::min(vx[i], vx[j]) - rcull);
+            bx1.push_back(std::max(vx[i], vx[j]) + rcull);
+            by0.push_back(std::min(vy[i], vy[j]) - rcull);
+            by1.push_back(std::max(vy[i], vy[j]) + rcull);
+            // f32 cull disc: the midpoint, half the length + h, rounded up generously
+            const double hl = 0.5 * std::hypot(vx[j] - vx[i], vy[j] - vy[i]);
+            const double rr = (hl + rcull) * (1.0 + 1e-7) + 1e-9;
+            d4.push_back(make_float4((float)(0.5 * (vx[i] + vx[j])), (float)(0.5 * (vy[i] + vy[j])),
+                                     std::nextafter((float)rr, 1e30f), 0.0f));
+            mx = std::max({mx, std::fabs(vx[i]), std::fabs(vy[i])});
+        }
+    }
+    const int ne = (int)ex0.size();
+    if ((rc = build_item_grid(ctx, minx, maxx, miny, maxy, bx0, bx1, by0, by1, d4))) return rc;
+    const size_t nn = (size_t)std::max(ne, 1);
+    PP_HIP(ctx->d_ex0.reserve(nn));
+    PP_HIP(ctx->d_ey0.reserve(nn));
+    PP_HIP(ctx->d_ex1.reserve(nn));
+    PP_HIP(ctx->d_ey1.reserve(nn));
+    PP_HIP(ctx->d_epoly.reserve(nn));
+    PP_HIP(ctx->d_bvx.reserve(bvx.size()));
+    PP_HIP(ctx->d_bvy.reserve(bvy.size()));
+    if (ne > 0) {
+        PP_HIP(hipMemcpy(ctx->d_ex0.p, ex0.data(), ne * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_ey0.p, ey0.data(), ne * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_ex1.p, ex1.data(), ne * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_ey1.p, ey1.data(), ne * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_epoly.p, epoly.data(), ne * sizeof(int), hipMemcpyHostToDevice));
+    }
+    PP_HIP(hipMemcpy(ctx->d_bvx.p, bvx.data(), bvx.size() * sizeof(double), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->d_bvy.p, bvy.data(), bvy.size() * sizeof(double), hipMemcpyHostToDevice));
+    ctx->h_ex0 = ex0;
+    ctx->h_ey0 = ey0;
+    ctx->h_ex1 = ex1;
+    ctx->h_ey1 = ey1;
+    ctx->h_epoly = epoly;
+    ctx->h_bvx = bvx;
+    ctx->h_bvy = bvy;
+    ctx->ne = ne;
+    ctx->nbv = (int)bvx.size();
+    ctx->h2 = half * half;
+    ctx->cull_slack = cull_slack_for(mx + half);
+    ctx->minx = minx;
+    ctx->maxx = maxx;
+    ctx->miny = miny;
+    ctx->maxy = maxy;
+    ctx->width = robot_width;
+    ctx->height = robot_height;
+    ctx->max_steer = max_steer;
+    ctx->m = 0;
+    ctx->has_grid = false;
+    ctx->has_scene = true;
+    ctx->has_rrt = false;
+    ctx->has_batch = false;
     return PP_OK;
 }
 
@@ -681,6 +879,36 @@ int pp_space_set_grid(pp_ctx* ctx, const uint32_t* bits, int w, int h, double x0
     }
     ctx->has_grid = true;
     ctx->has_rrt = false;  // the planner's Space changed (rrt.rs:342)
+    return PP_OK;
+}
+
+int pp_space_verify_batch(pp_ctx* ctx, const double* x, const double* y, const int64_t* off,
+                          int k, uint8_t* ok) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (k < 0 || (k > 0 && (!off || !ok))) return set_err(PP_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (k == 0) return PP_OK;
+    if (off[0] != 0) return set_err(PP_ERR_INVALID_ARGUMENT, "off[0] must be 0");
+    for (int i = 0; i < k; ++i)
+        if (off[i + 1] < off[i]) return set_err(PP_ERR_INVALID_ARGUMENT, "off must be non-decreasing");
+    const int64_t np = off[k];
+    if (np > 0 && (!x || !y)) return set_err(PP_ERR_INVALID_ARGUMENT, "null points");
+    hipStream_t st = ctx->stream;
+    DBuf<double> dx, dy;
+    DBuf<int64_t> doff;
+    DBuf<uint8_t> dok;
+    PP_HIP(dx.reserve((size_t)std::max<int64_t>(np, 1)));
+    PP_HIP(dy.reserve((size_t)std::max<int64_t>(np, 1)));
+    PP_HIP(doff.reserve((size_t)k + 1));
+    PP_HIP(dok.reserve((size_t)k));
+    if (np > 0) {
+        PP_HIP(hipMemcpyAsync(dx.p, x, np * sizeof(double), hipMemcpyHostToDevice, st));
+        PP_HIP(hipMemcpyAsync(dy.p, y, np * sizeof(double), hipMemcpyHostToDevice, st));
+    }
+    PP_HIP(hipMemcpyAsync(doff.p, off, ((size_t)k + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    PP_HIP(launch_verify_lines(st, ctx->scene_dev(), dx.p, dy.p, doff.p, k, dok.p));
+    PP_HIP(hipMemcpyAsync(ok, dok.p, (size_t)k, hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
     return PP_OK;
 }
 
@@ -722,6 +950,9 @@ int pp_rrt_new(pp_ctx* ctx, double sx, double sy, double syaw, double gx, double
     double mx = std::max({std::fabs(ctx->minx), std::fabs(ctx->maxx), std::fabs(ctx->miny),
                           std::fabs(ctx->maxy), std::fabs(sx), std::fabs(sy)});
     ctx->eps_coord = mx * std::ldexp(1.0, -23);
+    // polygon mode: a root that fails verify fails every line_to_origin (it ends the line), so
+    // nothing is ever inserted; the kernels' incremental verify assumes a free root (Q10p)
+    ctx->root_blocked = (ctx->ne > 0 || ctx->nbv > 0) && !ctx->point_ok(sx, sy);
     // RRT::new inserts the root (rrt.rs:344-346)
     const float fx = (float)sx, fy = (float)sy;
     const int par = -1;
@@ -757,6 +988,18 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
     if (r) return r;
     if (n_iter < 0) return set_err(PP_ERR_INVALID_ARGUMENT, "n_iter < 0");
     if ((r = ensure_window(ctx, ctx->K))) return r;
+    if (ctx->root_blocked) {  // every iteration rejects: only the iteration counters advance
+        DevState& s = ctx->h_state.p[0];
+        PP_HIP(hipMemcpy(&s, ctx->d_state.p, sizeof(DevState), hipMemcpyDeviceToHost));
+        s.it += n_iter;
+        s.it_spec = s.it;
+        s.iterations += n_iter;
+        s.node_evals += n_iter;  // the NN of every iteration scans the root
+        PP_HIP(hipMemcpy(ctx->d_state.p, &s, sizeof(DevState), hipMemcpyHostToDevice));
+        ctx->it = s.it;
+        if (n_accepted) *n_accepted = 0;
+        return PP_OK;
+    }
     const int64_t target = ctx->it + n_iter;
     const int64_t n_before = ctx->n;
     hipStream_t st = ctx->stream;
@@ -914,7 +1157,7 @@ int pp_rrt_verify_node_batch(pp_ctx* ctx, const double* x, const double* y,
                 if (stv[t] == kError)
                     return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
                 status[i] = stv[t];
-                ok[b + i] = stv[t] == kAccept ? 1 : 0;
+                ok[b + i] = stv[t] == kAccept && !ctx->root_blocked ? 1 : 0;
                 if (yaw) yaw[b + i] = yv[t];
             }
         }
@@ -1059,6 +1302,17 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
     PP_HIP(hipMemcpyAsync(d_starts.p, starts, 3 * (size_t)q * sizeof(double), hipMemcpyHostToDevice, st));
     PP_HIP(launch_mq_init(st, mq_args(ctx).mq, d_starts.p));
     PP_HIP(hipMemcpyAsync(ctx->mq_seed.p, seeds, q * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    // polygon mode: queries whose root fails verify never insert (see pp_rrt_new)
+    ctx->mq_any_blocked = false;
+    if (ctx->ne > 0 || ctx->nbv > 0) {
+        std::vector<uint8_t> blk(q);
+        for (int i = 0; i < q; ++i) {
+            blk[i] = ctx->point_ok(starts[3 * i], starts[3 * i + 1]) ? 0 : 1;
+            ctx->mq_any_blocked |= blk[i] != 0;
+        }
+        PP_HIP(ctx->mq_blocked.reserve(q));
+        PP_HIP(hipMemcpy(ctx->mq_blocked.p, blk.data(), q, hipMemcpyHostToDevice));
+    }
     DevState ds{};
     ds.W = q;
     PP_HIP(hipMemcpyAsync(ctx->mq_state.p, &ds, sizeof(DevState), hipMemcpyHostToDevice, st));

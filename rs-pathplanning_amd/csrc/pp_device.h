@@ -281,9 +281,9 @@ __device__ inline int dubins_literal(double sx, double sy, double syaw, double e
     return kSteerSome;
 }
 
-// Polyline segment vs closed disc: exact closest point of the segment.
-__device__ inline bool seg_hits_disc(double ax, double ay, double bx, double by, double cx,
-                                     double cy, double r2) {
+// Squared distance from (cx, cy) to the closed segment a-b: exact closest point of the segment.
+__host__ __device__ inline double seg_point_d2(double ax, double ay, double bx, double by,
+                                               double cx, double cy) {
     const double vx = bx - ax, vy = by - ay;
     const double wx = cx - ax, wy = cy - ay;
     const double l2 = vx * vx + vy * vy;
@@ -296,7 +296,77 @@ __device__ inline bool seg_hits_disc(double ax, double ay, double bx, double by,
             t = 1.0;
     }
     const double ex = wx - t * vx, ey = wy - t * vy;
-    return ex * ex + ey * ey <= r2;
+    return ex * ex + ey * ey;
+}
+
+// Polyline segment vs closed disc.
+__device__ inline bool seg_hits_disc(double ax, double ay, double bx, double by, double cx,
+                                     double cy, double r2) {
+    return seg_point_d2(ax, ay, bx, by, cx, cy) <= r2;
+}
+
+// ---- polygon mode (Q10p): geo's Contains / Intersects on the geo-offset buffers (rrt.rs:62-68,
+// 82, 108-111, 124-137) as exact Minkowski buffers — an obstacle polygon grows by the closed disc
+// of radius h = width/2, the bounds polygon shrinks to the points whose disc stays inside.  The
+// same arithmetic as the oracle (oracle/pp_oracle.c), so verdicts agree bit for bit.
+
+// crossing-number step: edge (xi, yi)-(xj, yj) crosses the ray from (px, py) toward +x
+__host__ __device__ inline bool ray_crosses(double px, double py, double xi, double yi, double xj,
+                                            double yj) {
+    return ((yi > py) != (yj > py)) && (px < (xj - xi) * (py - yi) / (yj - yi) + xi);
+}
+
+// the point lies in the bounds polygon eroded by h: inside the ring (even-odd) and at distance
+// >= h from every bounds edge
+__host__ __device__ inline bool in_poly_bounds(int nbv, const double* bvx, const double* bvy,
+                                               double h2, double x, double y) {
+    bool inside = false;
+    for (int i = 0; i < nbv; ++i) {
+        const int j = i + 1 == nbv ? 0 : i + 1;
+        const double xi = bvx[i], yi = bvy[i], xj = bvx[j], yj = bvy[j];
+        if (ray_crosses(x, y, xi, yi, xj, yj)) inside = !inside;
+        if (seg_point_d2(xi, yi, xj, yj, x, y) < h2) return false;
+    }
+    return inside;
+}
+
+// polyline segment a-b vs the buffer of the obstacle edge e0-e1: a proper crossing, or an
+// endpoint of one segment within h of the other (touching counts)
+__host__ __device__ inline bool seg_hits_edge(double ax, double ay, double bx, double by,
+                                              double e0x, double e0y, double e1x, double e1y,
+                                              double h2) {
+    const double d1 = (e1x - e0x) * (ay - e0y) - (e1y - e0y) * (ax - e0x);
+    const double d2 = (e1x - e0x) * (by - e0y) - (e1y - e0y) * (bx - e0x);
+    const double d3 = (bx - ax) * (e0y - ay) - (by - ay) * (e0x - ax);
+    const double d4 = (bx - ax) * (e1y - ay) - (by - ay) * (e1x - ax);
+    if (((d1 > 0.0 && d2 < 0.0) || (d1 < 0.0 && d2 > 0.0)) &&
+        ((d3 > 0.0 && d4 < 0.0) || (d3 < 0.0 && d4 > 0.0)))
+        return true;
+    return seg_point_d2(e0x, e0y, e1x, e1y, ax, ay) <= h2 ||
+           seg_point_d2(e0x, e0y, e1x, e1y, bx, by) <= h2 ||
+           seg_point_d2(ax, ay, bx, by, e0x, e0y) <= h2 ||
+           seg_point_d2(ax, ay, bx, by, e1x, e1y) <= h2;
+}
+
+// the point lies inside some obstacle polygon (even-odd over each polygon's consecutive edges)
+__host__ __device__ inline bool in_obstacle(int ne, const double* ex0, const double* ey0,
+                                            const double* ex1, const double* ey1,
+                                            const int* epoly, double x, double y) {
+    bool inside = false;
+    for (int k = 0; k < ne; ++k) {
+        if (k > 0 && epoly[k] != epoly[k - 1]) {
+            if (inside) return true;
+            inside = false;
+        }
+        if (ray_crosses(x, y, ex0[k], ey0[k], ex1[k], ey1[k])) inside = !inside;
+    }
+    return inside;
+}
+
+// a point in bounds: the (shrunken) rectangle, and the eroded bounds polygon when there is one
+__host__ __device__ inline bool point_in_bounds(const SceneDev& sc, double x, double y) {
+    if (!(x >= sc.minx && x <= sc.maxx && y >= sc.miny && y <= sc.maxy)) return false;
+    return sc.nbv == 0 || in_poly_bounds(sc.nbv, sc.bvx, sc.bvy, sc.h2, x, y);
 }
 
 // --------------------------------------------------------- seeded sampling

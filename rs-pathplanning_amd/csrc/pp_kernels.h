@@ -53,6 +53,11 @@ hipError_t launch_drain(hipStream_t s, const WindowArgs& a, int64_t seq_next);
 // rescan.
 hipError_t launch_nearest(hipStream_t s, const WindowArgs& a);
 
+// Space::verify (rrt.rs:124-137) of k polylines, line i = points [off[i], off[i + 1]) of X/Y;
+// ok[i] = 1 when it verifies.
+hipError_t launch_verify_lines(hipStream_t st, const SceneDev& sc, const double* X,
+                               const double* Y, const int64_t* off, int k, uint8_t* ok);
+
 hipError_t launch_steer_tasks(hipStream_t st, const SceneDev& sc, const TreeDev& tr,
                               const SteerTask* tasks, int n, int* out_status, double* out_yaw,
                               double* scratch);

@@ -76,16 +76,21 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
                                               bool seg_valid, double qx, double qy,
                                               int64_t* ph = nullptr) {
     PP_STAMP(tq0);
-    const bool oob =
+    bool oob =
         check_bounds && !(qx >= sc.minx && qx <= sc.maxx && qy >= sc.miny && qy <= sc.maxy);
     if (__any(oob)) return true;
+    if (sc.nbv > 0) {  // polygon bounds (Q10p): the eroded ring, per lane over every bounds edge
+        oob = check_bounds && !in_poly_bounds(sc.nbv, sc.bvx, sc.bvy, sc.h2, qx, qy);
+        if (__any(oob)) return true;
+    }
     if (sc.bits) {  // config 4: every point of the line probes its cell (1 bit), no segments
         const uint32_t* B = kLds ? reinterpret_cast<const uint32_t*>(pp_smem) : sc.bits;
         const bool hit = check_bounds && grid_occupied(B, sc.bw, sc.bh, sc.bwords, sc.bx0, sc.by0,
                                                        sc.binv, qx, qy);
         return __any(hit);
     }
-    if (sc.m == 0) return false;
+    if (sc.m == 0 && sc.ne == 0) return false;
+    const bool poly = sc.ne > 0;  // grid items are polygon edges (Q10p), else discs
     const double ax = __shfl_up(qx, 1);
     const double ay = __shfl_up(qy, 1);
     const double inf = __builtin_inf();
@@ -107,11 +112,12 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const double* dcy = sc.cy;
     const double* dr2 = sc.r2;
     const float4* d4 = kLds ? reinterpret_cast<const float4*>(pp_smem + sc.lds_d4) : sc.d4;
-    // per-lane f32 cull: a segment a-b can only touch a disc (exact test below) if
-    // |a - c| <= rcull + |b - a|; 1e-3 of slack covers the f32 rounding of coordinates <= 2^10
+    // per-lane f32 cull: a segment a-b can only touch a disc / an edge buffer (exact test below)
+    // if |a - c| <= rcull + |b - a| (c: the disc centre / the edge midpoint, rcull: the radius /
+    // half length + h); cull_slack covers the f32 rounding of the scene's coordinates
     const float axf = (float)ax, ayf = (float)ay;
     const float vxf = (float)(qx - ax), vyf = (float)(qy - ay);
-    const float Lf = __builtin_sqrtf(vxf * vxf + vyf * vyf) * 1.000001f + 1.0e-3f;
+    const float Lf = __builtin_sqrtf(vxf * vxf + vyf * vyf) * 1.000001f + sc.cull_slack;
     for (int gy = cy0; gy <= cy1; ++gy) {
         for (int gx = cx0; gx <= cx1; ++gx) {
             const int cell = gy * sc.gnx + gx;
@@ -125,7 +131,10 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
                 const float dxf = D.x - axf, dyf = D.y - ayf, thr = D.z + Lf;
                 const bool near = seg_valid && dxf * dxf + dyf * dyf <= thr * thr;
                 if (!__any(near)) continue;
-                const bool hit = near && seg_hits_disc(ax, ay, qx, qy, dcx[d], dcy[d], dr2[d]);
+                const bool hit =
+                    near && (poly ? seg_hits_edge(ax, ay, qx, qy, sc.ex0[d], sc.ey0[d], sc.ex1[d],
+                                                  sc.ey1[d], sc.h2)
+                                  : seg_hits_disc(ax, ay, qx, qy, dcx[d], dcy[d], dr2[d]));
                 if (__any(hit)) return true;
             }
         }
@@ -370,8 +379,7 @@ __device__ int steer_collide_literal(const SceneDev& sc, double x, double y, dou
             bx[n] = px;
             by[n] = py;
             const int np = junction ? n + 1 : n;  // the junction point is bounds-checked too
-            for (int i = 0; i < np && ok; ++i)
-                ok = bx[i] >= sc.minx && bx[i] <= sc.maxx && by[i] >= sc.miny && by[i] <= sc.maxy;
+            for (int i = 0; i < np && ok; ++i) ok = point_in_bounds(sc, bx[i], by[i]);
             if (sc.bits) {  // config 4: point probes only
                 for (int i = 0; i < np && ok; ++i)
                     ok = !grid_occupied(sc.bits, sc.bw, sc.bh, sc.bwords, sc.bx0, sc.by0, sc.binv,
@@ -383,6 +391,17 @@ __device__ int steer_collide_literal(const SceneDev& sc, double x, double y, dou
                     x1 = fmax(x1, bx[i]);
                     y0 = fmin(y0, by[i]);
                     y1 = fmax(y1, by[i]);
+                }
+                for (int k = 0; k < sc.ne && ok; ++k) {  // polygon edges (Q10p)
+                    const double e0x = sc.ex0[k], e0y = sc.ey0[k], e1x = sc.ex1[k], e1y = sc.ey1[k];
+                    const double rc = sqrt(sc.h2) * (1.0 + 1e-9) + 1e-9;
+                    if (!((fmax(e0x, e1x) + rc >= x0) && (fmin(e0x, e1x) - rc <= x1) &&
+                          (fmax(e0y, e1y) + rc >= y0) && (fmin(e0y, e1y) - rc <= y1)))
+                        continue;
+                    for (int i = 0; i + 1 < np && ok; ++i)
+                        if (seg_hits_edge(bx[i], by[i], bx[i + 1], by[i + 1], e0x, e0y, e1x, e1y,
+                                          sc.h2))
+                            ok = false;
                 }
                 for (int k = 0; k < sc.m && ok; ++k) {
                     const double cx = sc.cx[k], cy = sc.cy[k], rc = sc.rcull[k];
@@ -2332,7 +2351,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
             for (int base = 0; base <= L; base += 4) {
                 const int m = base + wave;
                 int st = kReject;
-                if (m <= L) {
+                if (m <= L && !sc.root_blocked) {
                     const int to = s_path[m];
                     const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
                     const CfPose a{a0.x, a0.y, atan2(bt.y - a0.y, bt.x - a0.x)};
@@ -2387,6 +2406,10 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
             }
             __syncthreads();
         }
+        // polygon mode: the chain's line is connected and no segment met an edge buffer, so it
+        // lies on one side of every obstacle boundary — the goal decides (Q10p)
+        if (vok && sc.ne > 0 && in_obstacle(sc.ne, sc.ex0, sc.ey0, sc.ex1, sc.ey1, sc.epoly, gx, gy))
+            vok = false;
         // a panic anywhere in finalize wins over a rejection (the reference panics first): scan
         // the remaining edges for None steers
         if (s_bad == 0 && !vok) {
@@ -2575,7 +2598,7 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
         }
         const int n = mq.n[q];
         mq.evals[q] += n;  // the NN of this iteration scanned n nodes
-        if (st == kAccept) {
+        if (st == kAccept && !(mq.blocked && mq.blocked[q])) {
             const size_t o = (size_t)q * mq.cap + n;
             mq.x[o] = tk.x;
             mq.y[o] = tk.y;
@@ -2751,6 +2774,51 @@ hipError_t launch_nearest(hipStream_t s, const WindowArgs& a) {
         a.st, 0, 0, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, a.wsx, a.wsy, a.tr.x32,
         a.tr.y32, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, nullptr, nullptr,
         nullptr, nullptr, nullptr, nullptr, nullptr, SamplesArgs{});
+    return hipGetLastError();
+}
+
+// Space::verify (rrt.rs:124-137) of whole polylines, one wave per line: chunks of 63 points
+// (lane 0 carries the previous chunk's last point) through the walk's chunk test — every point
+// in bounds (and in a free cell, config 4), every segment clear of the discs / edge buffers; a
+// one-point line is its degenerate segment.  Polygon mode: point 0 outside every obstacle
+// polygon (Q10p: with no segment meeting an edge buffer the line is on one side).
+__global__ __launch_bounds__(256) void verify_lines_kernel(SceneDev sc, const double* __restrict__ X,
+                                                          const double* __restrict__ Y,
+                                                          const int64_t* __restrict__ off, int k,
+                                                          uint8_t* __restrict__ ok) {
+    const int lane = threadIdx.x & 63;
+    const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    for (int i = gw; i < k; i += nw) {
+        const int64_t a = off[i], n = off[i + 1] - a;
+        bool good = true;
+        if (n > 0) {
+            if (n == 1) {
+                const bool has = lane == 0;
+                good = !chunk_rejects<false>(sc, has, has, has, X[a], Y[a]);
+            } else {
+                // lane l holds point c0 + l; lane 0 is the previous chunk's last point (checked)
+                for (int64_t c0 = 0; c0 + 1 < n && good; c0 += 63) {
+                    const int64_t j = c0 + lane;
+                    const bool has = j < n;
+                    const double qx = has ? X[a + j] : 0.0, qy = has ? Y[a + j] : 0.0;
+                    good = !chunk_rejects<false>(sc, has, has && (lane >= 1 || c0 == 0),
+                                                 has && lane >= 1, qx, qy);
+                }
+            }
+            if (good && sc.ne > 0 &&
+                in_obstacle(sc.ne, sc.ex0, sc.ey0, sc.ex1, sc.ey1, sc.epoly, X[a], Y[a]))
+                good = false;
+        }
+        if (lane == 0) ok[i] = good ? 1 : 0;
+    }
+}
+
+hipError_t launch_verify_lines(hipStream_t st, const SceneDev& sc, const double* X,
+                               const double* Y, const int64_t* off, int k, uint8_t* ok) {
+    if (k <= 0) return hipSuccess;
+    const int waves = std::min(k, 16384);
+    verify_lines_kernel<<<(waves + 3) / 4, 256, 0, st>>>(sc, X, Y, off, k, ok);
     return hipGetLastError();
 }
 

@@ -64,6 +64,25 @@ struct SceneDev {
     const uint32_t* bits;
     int bw, bh, bwords;
     double bx0, by0, binv;
+    // polygon mode (pp_space_new_polygons, build-defined Q10p): when ne > 0 the grid items are
+    // obstacle polygon edges (ex0, ey0)-(ex1, ey1) instead of discs (d4 = their f32 cull discs:
+    // midpoint, half length + h rounded up); a segment hits an edge when they cross or an
+    // endpoint of one lies within h of the other (h2 = (width/2)^2).  epoly: polygon id per edge
+    // (a polygon's edges are consecutive) for the point-inside test.  nbv > 0: the bounds are the
+    // polygon ring (bvx, bvy) eroded by h, on top of the rectangle test (its shrunken bbox).
+    int ne;
+    const double* ex0;
+    const double* ey0;
+    const double* ex1;
+    const double* ey1;
+    const int* epoly;
+    double h2;
+    int nbv;
+    const double* bvx;
+    const double* bvy;
+    float cull_slack;  // f32 cull slack for the scene's coordinate magnitude
+    int root_blocked;  // planner (polygon mode): the root itself fails verify, so every
+                       // line_to_origin does (check_finish: optimize accepts no candidate)
 };
 
 // Tree in device memory: f32 SoA for the NN screen, f64 SoA for everything exact.
@@ -154,6 +173,8 @@ struct MqDev {
     int64_t* it;            // [Q] next iteration
     int64_t* evals;         // [Q] node-distance evaluations of the NN so far
     const uint64_t* seed;   // [Q] sampling stream
+    const uint8_t* blocked; // [Q] polygon mode: the root fails verify, so every line_to_origin
+                            // does and nothing is ever inserted (rrt.rs:414-426); may be null
 };
 
 // Resolve scratch (global, one window; indexed by pending slot / list position).

@@ -34,6 +34,7 @@ EXPORTED = [
     "pp_abi_version", "pp_last_error", "pp_device_count", "pp_create", "pp_destroy",
     "pp_synchronize", "pp_rng_u64", "pp_gen_range", "pp_mod2pi", "pp_pi_2_pi",
     "pp_dubins_path_planning_batch", "pp_space_new", "pp_space_set_grid", "pp_space_get_bounds",
+    "pp_space_new_polygons", "pp_space_verify_batch",
     "pp_rrt_new",
     "pp_rrt_set_window", "pp_rrt_extend", "pp_rrt_plan_one", "pp_rrt_tree_size",
     "pp_rrt_iteration", "pp_rrt_tree_export", "pp_rrt_get_nearest_node_batch",
@@ -102,6 +103,10 @@ def lib():
             "pp_space_set_grid": ([vp, C.POINTER(C.c_uint32), C.c_int, C.c_int, C.c_double,
                                    C.c_double, C.c_double], C.c_int),
             "pp_space_get_bounds": ([vp, dp], C.c_int),
+            "pp_space_new_polygons": ([vp, dp, C.c_int, dp, C.POINTER(C.c_int32), C.c_int,
+                                       C.c_double, C.c_double, C.c_double], C.c_int),
+            "pp_space_verify_batch": ([vp, dp, dp, C.POINTER(C.c_int64), C.c_int,
+                                       C.POINTER(C.c_uint8)], C.c_int),
             "pp_rrt_new": ([vp] + [C.c_double] * 6 + [C.c_int64, C.c_double, C.c_uint64, C.c_int64],
                            C.c_int),
             "pp_rrt_set_window": ([vp, C.c_int], C.c_int),

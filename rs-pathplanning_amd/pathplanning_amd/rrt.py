@@ -5,8 +5,8 @@ Same names and argument meaning as the crate: ``Robot``, ``create_circle``, ``Sp
 batched ``extend``.  Build-defined differences: obstacles are analytic discs
 and the bounds an axis-aligned rectangle (Q10), sampling is a seeded stream (Q7), iterations run
 with the sequential semantics of one rayon thread (Q8), the nearest neighbour is exact (Q9).
-``plan()``'s goal-connect / shortcut / path materialisation (``check_finish``, ``optimize``,
-``finalize``) is the next row of the build and is not provided yet.
+Polygon scenes (the example's JSON format) use exact Minkowski buffers in place of geo-offset
+(Q10p).  ``plan()`` runs the goal connection (``check_finish``, ``optimize``, ``finalize``).
 """
 from __future__ import annotations
 
@@ -15,7 +15,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from . import _ffi
+from . import _ffi, scenes
 
 
 class Robot:  # rrt.rs:16-40
@@ -44,34 +44,63 @@ def create_circle(center, radius: float) -> Circle:  # rrt.rs:43
 
 
 def _rect_of(bounds):
+    """(x0, y0, x1, y1) when ``bounds`` is a 4-tuple or an axis-aligned rectangle ring, else None."""
     b = np.asarray(bounds, dtype=np.float64)
     if b.shape == (4,):
         return tuple(b)
-    # polygon ring: accepted when it is an axis-aligned rectangle
+    b = scenes.ring(b)
+    if len(b) != 4:
+        return None
     xs, ys = b[:, 0], b[:, 1]
     x0, x1, y0, y1 = xs.min(), xs.max(), ys.min(), ys.max()
-    if not np.all((np.isclose(xs, x0) | np.isclose(xs, x1)) & (np.isclose(ys, y0) | np.isclose(ys, y1))):
-        raise ValueError("bounds must be an axis-aligned rectangle (polygon bounds: next row)")
+    if not np.all(((xs == x0) | (xs == x1)) & ((ys == y0) | (ys == y1))):
+        return None
     return (x0, y0, x1, y1)
 
 
 class Space:  # rrt.rs:70-159
-    """``Space::new(bounds, robot, obstacles)``.  ``grid`` (config 4, build-defined): an occupancy
-    grid ``(bits uint32[h, ceil(w/32)], w, x0, y0, cell)`` that replaces the discs — every point
-    of a line must lie in a free cell (pp_space_set_grid)."""
+    """``Space::new(bounds, robot, obstacles)``.
+
+    Disc mode (configs 1-4): ``bounds`` an axis-aligned rectangle (4-tuple or ring) and every
+    obstacle a ``Circle`` — analytic discs (Q10).  Polygon mode (§8f row 3, Q10p): any obstacle
+    given as a polygon ring ((M, 2) array-like) or non-rectangular bounds; ``Circle`` obstacles
+    then become the crate's ``create_circle`` polygons.  ``grid`` (config 4, build-defined): an
+    occupancy grid ``(bits uint32[h, ceil(w/32)], w, x0, y0, cell)`` that replaces the discs —
+    every point of a line must lie in a free cell (pp_space_set_grid)."""
 
     def __init__(self, bounds, robot: Robot, obstacle_list, grid=None):
-        self.raw_bounds = _rect_of(bounds)
         self.robot = robot
         self.grid = grid
         obs = list(obstacle_list)
-        self.circles = np.array([[o.cx, o.cy, o.r] for o in obs], dtype=np.float64).reshape(-1, 3)
+        rect = _rect_of(bounds)
+        self.polygon_mode = rect is None or any(not isinstance(o, Circle) for o in obs)
         half = robot.get_width() / 2.0  # rrt.rs:82
+        if self.polygon_mode:
+            if grid is not None:
+                raise ValueError("an occupancy grid replaces disc obstacles, not polygons")
+            b = np.asarray(bounds, dtype=np.float64)
+            if b.shape == (4,):
+                x0, y0, x1, y1 = b
+                b = [(x0, y0), (x1, y0), (x1, y1), (x0, y1)]
+            self.bounds_polygon = scenes.ring(b)
+            self.obstacle_polygons = [
+                scenes.create_circle_polygon((o.cx, o.cy), o.r) if isinstance(o, Circle)
+                else scenes.ring(o) for o in obs]
+            bp = self.bounds_polygon
+            self.raw_bounds = (bp[:, 0].min(), bp[:, 1].min(), bp[:, 0].max(), bp[:, 1].max())
+            self.circles = np.zeros((0, 3))
+        else:
+            self.raw_bounds = rect
+            self.circles = np.array([[o.cx, o.cy, o.r] for o in obs],
+                                    dtype=np.float64).reshape(-1, 3)
         x0, y0, x1, y1 = self.raw_bounds
         self.minx, self.miny, self.maxx, self.maxy = x0 + half, y0 + half, x1 - half, y1 - half
+        self._ctx = None
 
     @classmethod
     def from_raw(cls, raw: dict) -> "Space":
+        if "bounds_polygon" in raw:
+            return cls(raw["bounds_polygon"], Robot(*raw["robot"]), raw["obstacle_polygons"])
         return cls(raw["bounds"], Robot(*raw["robot"]),
                    [create_circle((c[0], c[1]), c[2]) for c in raw["circles"]],
                    grid=raw.get("grid"))
@@ -84,16 +113,58 @@ class Space:  # rrt.rs:70-159
         return (self.minx, self.maxx, self.miny, self.maxy)
 
     def get_obs(self):
-        """inflated discs (cx, cy, r + width/2) (rrt.rs:108-111, 152-154)."""
+        """Disc mode: the inflated discs (cx, cy, r + width/2) (rrt.rs:108-111, 152-154).
+        Polygon mode: the obstacle rings before buffering (the buffer is analytic, Q10p)."""
+        if self.polygon_mode:
+            return [p.copy() for p in self.obstacle_polygons]
         half = self.robot.get_width() / 2.0
         c = self.circles.copy()
         c[:, 2] += half
         return c
 
+    def verify_batch(self, lines, ctx: _ffi.Context | None = None):
+        """``Space::verify`` (rrt.rs:124-137) of many polylines (each (n, 2)) on the GPU: bool
+        array.  Uses ``ctx`` (the scene is uploaded into it) or a context of its own."""
+        if ctx is None:
+            if self._ctx is None:
+                self._ctx = _ffi.Context(0)
+                self._upload(self._ctx)
+            ctx = self._ctx
+        else:
+            self._upload(ctx)
+        pts = [np.asarray(l, dtype=np.float64).reshape(-1, 2) for l in lines]
+        off = np.zeros(len(pts) + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(p) for p in pts])
+        allp = np.concatenate(pts) if pts and off[-1] > 0 else np.zeros((1, 2))
+        x = np.ascontiguousarray(allp[:, 0])
+        y = np.ascontiguousarray(allp[:, 1])
+        ok = np.zeros(len(pts), dtype=np.uint8)
+        dp = C.POINTER(C.c_double)
+        _ffi.check(_ffi.lib().pp_space_verify_batch(
+            ctx.handle, x.ctypes.data_as(dp), y.ctypes.data_as(dp),
+            off.ctypes.data_as(C.POINTER(C.c_int64)), len(pts),
+            ok.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return ok.astype(bool)
+
+    def verify(self, line, ctx: _ffi.Context | None = None) -> bool:
+        """``Space::verify(&LineString) -> bool`` (rrt.rs:124-137)."""
+        return bool(self.verify_batch([line], ctx)[0])
+
     def _upload(self, ctx: _ffi.Context):
+        dp = C.POINTER(C.c_double)
+        if self.polygon_mode:
+            b = np.ascontiguousarray(self.bounds_polygon.reshape(-1))
+            rings = self.obstacle_polygons
+            off = np.zeros(len(rings) + 1, dtype=np.int32)
+            off[1:] = np.cumsum([len(r) for r in rings])
+            o = np.ascontiguousarray(np.concatenate(rings).reshape(-1)) if rings else np.zeros(2)
+            _ffi.check(_ffi.lib().pp_space_new_polygons(
+                ctx.handle, b.ctypes.data_as(dp), len(self.bounds_polygon), o.ctypes.data_as(dp),
+                off.ctypes.data_as(C.POINTER(C.c_int32)), len(rings), self.robot.width,
+                self.robot.height, self.robot.max_steer))
+            return
         c = np.ascontiguousarray(self.circles)
         cx, cy, r = (np.ascontiguousarray(c[:, k]) for k in range(3))
-        dp = C.POINTER(C.c_double)
         x0, y0, x1, y1 = self.raw_bounds
         _ffi.check(_ffi.lib().pp_space_new(
             ctx.handle, x0, y0, x1, y1, self.robot.width, self.robot.height,

@@ -3,10 +3,16 @@
 * ``bench6`` — the reference's only fully specified scene, ``benches/all.rs:8-42`` (config 1).
 * ``field512`` — BASELINE.json config 2/3/4: 1024 random discs on a 512x512 rectangle.
 
+* ``transit`` / ``load_json`` — the example's JSON scene format (examples/rrt/src/main.rs:13-45):
+  polygon bounds and polygon obstacles (§8f row 3, polygon mode).
+* ``bench6_polygons`` — bench6 with its obstacles as ``create_circle`` polygons (rrt.rs:43-60).
+
 A raw scene is a plain dict: ``bounds`` (x0, y0, x1, y1) of the un-shrunk rectangle, ``robot``
 (width, height, max_steer) as in ``Robot::new`` (rrt.rs:25), ``circles`` (M, 3) array of
 (cx, cy, r) as built by ``create_circle`` (rrt.rs:43), ``start``/``goal`` (x, y, yaw),
-``max_iter`` and ``step_size`` as passed to ``RRT::new`` (rrt.rs:335-343).
+``max_iter`` and ``step_size`` as passed to ``RRT::new`` (rrt.rs:335-343).  A polygon scene
+adds ``bounds_polygon`` (the bounds ring, (N, 2)) and ``obstacle_polygons`` (a list of (M_i, 2)
+rings); its ``bounds`` is the ring's bbox and ``circles`` is empty.
 """
 from __future__ import annotations
 
@@ -196,3 +202,102 @@ def field512_grid() -> dict:
     raw["name"] = "field512_grid"
     raw["grid"] = rasterize(raw)
     return raw
+
+
+# ------------------------------------------------------------------ polygon scenes (§8f row 3)
+def ring(points) -> np.ndarray:
+    """A polygon ring as (N, 2) f64 without the closing repeat (geo closes rings itself; the
+    C ABI drops an exact repeat of the first vertex too)."""
+    r = np.asarray(points, dtype=np.float64).reshape(-1, 2)
+    if len(r) > 1 and r[0, 0] == r[-1, 0] and r[0, 1] == r[-1, 1]:
+        r = r[:-1]
+    return np.ascontiguousarray(r)
+
+
+def create_circle_polygon(center, radius: float) -> np.ndarray:
+    """``create_circle`` (rrt.rs:43-60) as the polygon the crate builds: n = ceil(2 pi r / 1.0)
+    chords, vertices i = 0..=n at angle 2 pi / n * i (the last one repeats the first up to
+    rounding).  Same evaluation order as the Rust expression."""
+    cx, cy = float(center[0]), float(center[1])
+    circum = 2.0 * math.pi * radius
+    n = math.ceil(circum / 1.0)
+    pts = [(math.cos(2.0 * math.pi / n * float(i)) * radius + cx,
+            math.sin(2.0 * math.pi / n * float(i)) * radius + cy) for i in range(int(n + 1.0))]
+    return np.array(pts, dtype=np.float64)
+
+
+def polygon_scene(bounds, obstacles, robot, start, goal, max_iter=8000, step_size=0.1,
+                  name="polygons") -> dict:
+    """A raw polygon scene: ``Space::new(Polygon(bounds), robot, obstacles)`` (rrt.rs:81-122)."""
+    b = ring(bounds)
+    obs = [ring(o) for o in obstacles]
+    return {
+        "name": name,
+        "bounds": (float(b[:, 0].min()), float(b[:, 1].min()), float(b[:, 0].max()),
+                   float(b[:, 1].max())),
+        "bounds_polygon": b,
+        "obstacle_polygons": obs,
+        "robot": tuple(float(v) for v in robot),
+        "circles": np.zeros((0, 3)),
+        "start": tuple(float(v) for v in start),
+        "goal": tuple(float(v) for v in goal),
+        "max_iter": int(max_iter),
+        "step_size": float(step_size),
+    }
+
+
+def load_json(src, name: str = "json") -> dict:
+    """The example's scene file (examples/rrt/src/main.rs:13-45): ``{bounds: [[x, y]...],
+    obstacles: [[[x, y]...]...], path, start: [x, y, yaw], goal: [x, y, yaw]}`` with the
+    example's ``Robot::new(1.8, 3.0, 0.8)``, ``max_iter`` 8000 and step 0.1
+    (main.rs:47, 58-66).  ``src``: a path or an already parsed dict."""
+    import json
+
+    conf = src if isinstance(src, dict) else json.load(open(src))
+    return polygon_scene(conf["bounds"], conf["obstacles"], (1.8, 3.0, 0.8), conf["start"],
+                         conf["goal"], 8000, 0.1, name=name)
+
+
+def load_path(path: str) -> np.ndarray:
+    """A ``cac.path`` file as examples/rrt/convert.py reads it: whitespace-separated x y per
+    line, divided by 100.  Returns (N, 2)."""
+    out = []
+    with open(path) as f:
+        for line in f:
+            n = line.split()
+            if len(n) >= 2:
+                out.append((float(n[0]) / 100.0, float(n[1]) / 100.0))
+    return np.array(out, dtype=np.float64).reshape(-1, 2)
+
+
+def bench6_polygons() -> dict:
+    """bench6 (benches/all.rs:8-42) with the obstacles as the crate's own ``create_circle``
+    polygons and the bounds rectangle as a ring: the reference's scene in polygon mode."""
+    raw = bench6()
+    x0, y0, x1, y1 = raw["bounds"]
+    obs = [create_circle_polygon((c[0], c[1]), c[2]) for c in raw["circles"]]
+    # the ring in the bench's own vertex order (benches/all.rs:21-28)
+    out = polygon_scene([(x0, y0), (x0, y1), (x1, y1), (x1, y0), (x0, y0)], obs, raw["robot"],
+                        raw["start"], raw["goal"], raw["max_iter"], raw["step_size"],
+                        name="bench6_polygons")
+    return out
+
+
+def bench6_polygons_open(start_yaw: float = math.pi / 4.0) -> dict:
+    """bench6_polygons from bench6_open's start (-3, -3, start_yaw): the polygon-mode
+    goal-connection scene (at bench6's own start nothing ever finishes, see bench6_open)."""
+    raw = bench6_polygons()
+    raw["name"] = "bench6_polygons_open"
+    raw["start"] = (-3.0, -3.0, float(start_yaw))
+    return raw
+
+
+def transit(path: str | None = None) -> dict:
+    """The example's own scene, examples/rrt/transit.debug.json (a copy of the data file lives
+    in tests/golden/ so the GPU box, which has no /root/reference, can load it)."""
+    import os
+
+    if path is None:
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+            os.path.abspath(__file__)))), "tests", "golden", "transit.debug.json")
+    return load_json(path, name="transit")

@@ -5,7 +5,9 @@ The reference ships no golden vectors and cannot be built or run here (SURVEY.md
 expected outputs come from this independent restatement; the inputs are the reference's own
 known configurations (examples/dubins/src/main.rs:131-164, benches/all.rs:8-42,102-111) plus a
 seeded random battery and the build's config-2 field.  The C oracle and the HIP path are checked
-against these files.  Re-run with:  python tests/golden/gen_golden.py
+against these files.  Re-run with:  python tests/golden/gen_golden.py  (--polygons: only the
+polygon-mode fixtures; transit.debug.json is a verbatim copy of the reference's example scene
+data, examples/rrt/transit.debug.json)
 """
 from __future__ import annotations
 
@@ -109,6 +111,24 @@ def finish_record(raw, seed, n_iter):
     return out
 
 
+def polygons_main():
+    """Polygon mode (§8f row 3, Q10p): the example's JSON scene (examples/rrt/transit.debug.json,
+    copied here as data) and bench6 with its create_circle polygons."""
+    tr = scenes.transit()
+    recs = [rrt_record(tr, 42, 2500)]
+    b6 = scenes.bench6_polygons()
+    recs += [rrt_record(b6, s, 600) for s in (0, 1)]
+    with open(os.path.join(HERE, "rrt_polygons.json"), "w") as f:
+        json.dump(recs, f)
+    print("polygon trees:", [(r["scene"], r["seed"], len(r["x"])) for r in recs])
+    fin = [finish_record(scenes.bench6_polygons_open(), 0, 500)]
+    with open(os.path.join(HERE, "finish_polygons.json"), "w") as f:
+        json.dump(fin, f)
+    print("polygon finish: nodes", [r["n_nodes"] for r in fin], "ok",
+          [sum(x["ok"] for x in r["finish"]) for r in fin], "best",
+          [(r["best_node"], r["best_length"]) for r in fin])
+
+
 def main():
     known = {k: dubins_record(v) for k, v in KNOWN.items()}
     with open(os.path.join(HERE, "dubins_known.json"), "w") as f:
@@ -139,4 +159,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--polygons" in sys.argv:
+        polygons_main()
+    else:
+        main()
+        polygons_main()
