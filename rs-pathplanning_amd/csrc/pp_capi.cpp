@@ -142,7 +142,8 @@ struct pp_ctx {
     int Kcap = 0;
     DBuf<double> wsx, wsy, nn_d2, snap_yaw, snap_pose;
     DBuf<float> pbest, psecond, wsx32, wsy32;
-    DBuf<int> perm;
+    DBuf<int> perm, cofs;
+    DBuf<float2> sxy;
     DBuf<double> sqb;
     DBuf<int> pidx, nn_idx, cand_cnt, snap_status;
     DBuf<CandEntry> cand;
@@ -284,6 +285,8 @@ struct pp_ctx {
         a.wsx32 = wsx32.p;
         a.wsy32 = wsy32.p;
         a.perm = perm.p;
+        a.cofs = cofs.p;
+        a.sxy = sxy.p;
         a.sq = sqb.p;
         a.pbest = pbest.p;
         a.psecond = psecond.p;
@@ -328,6 +331,8 @@ int ensure_window(pp_ctx* c, int K) {
     PP_HIP(c->wsx32.reserve(2 * k));
     PP_HIP(c->wsy32.reserve(2 * k));
     PP_HIP(c->perm.reserve(2 * k));
+    PP_HIP(c->sxy.reserve(2 * k));
+    PP_HIP(c->cofs.reserve(2 * 257));
     PP_HIP(c->sqb.reserve(2 * k));
     PP_HIP(c->pbest.reserve(k * kMaxChunks));
     PP_HIP(c->psecond.reserve(k * kMaxChunks));
@@ -702,7 +707,8 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
         r2[k] = reff * reff;
         rc_[k] = reff * (1.0 + 1e-9) + 1e-9;
         // f32 cull copy: the radius rounded up (the cull only ever over-includes)
-        d4[k] = make_float4((float)cx[k], (float)cy[k], std::nextafter((float)rc_[k], 1e30f), 0.0f);
+        d4[k] = make_float4((float)cx[k], (float)cy[k], std::nextafter((float)rc_[k], 1e30f),
+                            (float)reff);  // w: the radius for the walk's f32 decision band
         bx0[k] = cx[k] - rc_[k];
         bx1[k] = cx[k] + rc_[k];
         by0[k] = cy[k] - rc_[k];

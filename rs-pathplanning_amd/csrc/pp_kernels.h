@@ -22,6 +22,8 @@ struct WindowArgs {
     float* wsx32 = nullptr;       // [2 * Kcap] their f32 copies
     float* wsy32 = nullptr;
     int* perm = nullptr;          // [2 * Kcap] spatially sorted sample order (window_samples)
+    int* cofs = nullptr;          // [2 * 257] start of each Morton cell in the sorted order
+    float2* sxy = nullptr;        // [2 * Kcap] the samples in sorted order (f32)
     double* sq = nullptr;         // [2 * Kcap] |q - o|^2 about the screen block's centre
     float* pbest = nullptr;
     float* psecond = nullptr;

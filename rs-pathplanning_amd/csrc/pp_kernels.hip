@@ -117,25 +117,66 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     // half length + h); cull_slack covers the f32 rounding of the scene's coordinates
     const float axf = (float)ax, ayf = (float)ay;
     const float vxf = (float)(qx - ax), vyf = (float)(qy - ay);
-    const float Lf = __builtin_sqrtf(vxf * vxf + vyf * vyf) * 1.000001f + sc.cull_slack;
+    const float l2f = vxf * vxf + vyf * vyf;
+    const float Lf = __builtin_sqrtf(l2f) * 1.000001f + sc.cull_slack;
+    // the chunk's bbox in f32, widened by the rounding slack: an item whose cull disc misses it
+    // cannot meet any of the chunk's segments
+    const int lane = threadIdx.x & 63;
+    const float bxl = (float)bx0 - sc.cull_slack, bxh = (float)bx1 + sc.cull_slack;
+    const float byl = (float)by0 - sc.cull_slack, byh = (float)by1 + sc.cull_slack;
     for (int gy = cy0; gy <= cy1; ++gy) {
         for (int gx = cx0; gx <= cx1; ++gx) {
             const int cell = gy * sc.gnx + gx;
             const int k0 = goff[cell], k1 = goff[cell + 1];
-            for (int k = k0; k < k1; ++k) {
+            // the cell's items in parallel, one per lane: the cull disc against the chunk's bbox;
+            // the survivors are then tested against every lane's segment, one at a time
+            for (int kb = k0; kb < k1; kb += 64) {
+                const int kk = kb + lane;
+                int dl = 0;
+                float4 Dl = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                bool ov = false;
+                if (kk < k1) {
+                    dl = items[kk];
+                    Dl = d4[dl];
+                    ov = Dl.x + Dl.z >= bxl && Dl.x - Dl.z <= bxh && Dl.y + Dl.z >= byl &&
+                         Dl.y - Dl.z <= byh;
+                }
+                for (uint64_t m = __ballot(ov); m; m &= m - 1) {
+                    const int src = (int)__builtin_ctzll(m);
+                    const int d = __builtin_amdgcn_readlane(dl, src);
+                    float4 D;
+                    D.x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.x), src));
+                    D.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.y), src));
+                    D.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.z), src));
+                    D.w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.w), src));
 #ifdef PP_STAMPS
-                if (ph) ph[1] += 1;
+                    if (ph) ph[1] += 1;
 #endif
-                const int d = items[k];
-                const float4 D = d4[d];
-                const float dxf = D.x - axf, dyf = D.y - ayf, thr = D.z + Lf;
-                const bool near = seg_valid && dxf * dxf + dyf * dyf <= thr * thr;
-                if (!__any(near)) continue;
-                const bool hit =
-                    near && (poly ? seg_hits_edge(ax, ay, qx, qy, sc.ex0[d], sc.ey0[d], sc.ex1[d],
-                                                  sc.ey1[d], sc.h2)
-                                  : seg_hits_disc(ax, ay, qx, qy, dcx[d], dcy[d], dr2[d]));
-                if (__any(hit)) return true;
+                    const float dxf = D.x - axf, dyf = D.y - ayf, thr = D.z + Lf;
+                    bool near = seg_valid && dxf * dxf + dyf * dyf <= thr * thr;
+                    if (!__any(near)) continue;
+                    if (!poly) {
+                        // f32 closest point of the segment to the disc centre, decisive outside
+                        // a band of +-eps around the radius (eps bounds the f32 rounding of the
+                        // coordinates, the radius and this arithmetic): only the band needs the
+                        // exact f64 test and its global loads
+                        float t = 0.0f;
+                        if (l2f > 0.0f)
+                            t = __builtin_fminf(__builtin_fmaxf((dxf * vxf + dyf * vyf) / l2f, 0.0f), 1.0f);
+                        const float ex = dxf - t * vxf, ey = dyf - t * vyf;
+                        const float e2 = ex * ex + ey * ey;
+                        const float eps = sc.cull_slack + 1.0e-4f * (1.0f + thr);
+                        const float lo = __builtin_fmaxf(D.w - eps, 0.0f), hi = D.w + eps;
+                        if (__any(near && e2 < lo * lo)) return true;  // surely within the disc
+                        near = near && e2 <= hi * hi;                  // else surely clear
+                        if (!__any(near)) continue;
+                    }
+                    const bool hit =
+                        near && (poly ? seg_hits_edge(ax, ay, qx, qy, sc.ex0[d], sc.ey0[d], sc.ex1[d],
+                                                      sc.ey1[d], sc.h2)
+                                      : seg_hits_disc(ax, ay, qx, qy, dcx[d], dcy[d], dr2[d]));
+                    if (__any(hit)) return true;
+                }
             }
         }
     }
@@ -502,8 +543,11 @@ constexpr bool kWinRepair = true;                // repairs inside the window ke
 #endif
 constexpr int kScanWaves = kScanThreads / 64;
 constexpr int kScanBlk = PP_SCANBLK;             // nodes per scalar-load block
-constexpr int kScanGrid = 240;                   // screen workgroups per window (one per CU, with
-                                                 // the resolve workgroup: 241 <= 256 CUs)
+#ifndef PP_SCANGRID
+#define PP_SCANGRID 240
+#endif
+constexpr int kScanGrid = PP_SCANGRID;           // screen workgroups per window (one per CU, with
+                                                 // the resolve workgroup: <= 256 CUs)
 
 // node chunks of the screen for a window of K samples: the nqb sample blocks x chunks workgroups
 // fill kScanGrid; every chunk is a whole number of kScanBlk blocks
@@ -555,6 +599,98 @@ __device__ __forceinline__ float scan_d2(float qx, float qy, float nx, float ny)
     return __builtin_fmaf(dy, dy, dx * dx);
 }
 
+// window_samples: Space::rand_point for the iterations [start, start + W) of a window
+// (rrt.rs:139-146, seeded: Q7 — x = draw 2*it, y = draw 2*it + 1), W = min(K, target - start),
+// and a counting sort of the samples by the Morton index of their cell in a 16 x 16 grid over the
+// sampling box: perm[pos] = sample, so a screen block of 256 consecutive sorted samples is
+// spatially compact (the expanded screen's precision).  Within a cell the order is arbitrary —
+// the results never depend on it (only which samples meet the exact rescan).
+struct SamplesArgs {
+    int K;
+    int64_t target;
+    uint64_t seed;
+    double minx, maxx, miny, maxy;
+    double* wsx[2];
+    double* wsy[2];
+    float* wsx32[2];
+    float* wsy32[2];
+    int* perm[2];
+    int* cofs[2];     // [257] first sorted position of each Morton cell (cell 256: W)
+    float2* sxy[2];   // sorted position -> (x, y) f32 (the pair search's prefilter)
+};
+
+__device__ inline int morton16(int x, int y) {
+    int m = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) m |= (((x >> b) & 1) << (2 * b)) | (((y >> b) & 1) << (2 * b + 1));
+    return m;
+}
+
+__device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t start,
+                             char* smem) {
+    int* s_hist = reinterpret_cast<int*>(smem);                  // [256]
+    unsigned char* s_cell = reinterpret_cast<unsigned char*>(s_hist + 256);  // [K]
+    const int tid = threadIdx.x, NT = blockDim.x;
+    const int64_t rem = g.target - start;
+    const int W = (rem <= 0 || st->error) ? 0 : (rem < g.K ? (int)rem : g.K);
+    if (tid == 0) {
+        st->Wp[np] = W;
+        st->wsp[np] = start;
+    }
+    for (int i = tid; i < 256; i += NT) s_hist[i] = 0;
+    __syncthreads();
+    const double fx = 16.0 / (g.maxx - g.minx), fy = 16.0 / (g.maxy - g.miny);
+    for (int j = tid; j < W; j += NT) {
+        const uint64_t itj = (uint64_t)(start + j);
+        const double x = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
+        const double y = gen_range(g.seed, 2 * itj + 1, g.miny, g.maxy);
+        g.wsx[np][j] = x;
+        g.wsy[np][j] = y;
+        g.wsx32[np][j] = (float)x;
+        g.wsy32[np][j] = (float)y;
+        const int cx = min(max((int)((x - g.minx) * fx), 0), 15);  // == sample_cell
+        const int cy = min(max((int)((y - g.miny) * fy), 0), 15);
+        const int cell = morton16(cx, cy);
+        s_cell[j] = (unsigned char)cell;
+        atomicAdd(&s_hist[cell], 1);
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive prefix of the 256 cell counts, 4 per lane
+        int v[4], sum = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            v[u] = s_hist[4 * tid + u];
+            sum += v[u];
+        }
+        int x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (tid >= o) x += y;
+        }
+        int base = x - sum;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            s_hist[4 * tid + u] = base;
+            base += v[u];
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < 256; i += NT) g.cofs[np][i] = s_hist[i];
+    if (tid == 0) g.cofs[np][256] = W;
+    __syncthreads();  // the cell starts are read before the scatter advances them
+    for (int j = tid; j < W; j += NT) {
+        const int pos = atomicAdd(&s_hist[s_cell[j]], 1);
+        g.perm[np][pos] = j;
+        g.sxy[np][pos] = make_float2(g.wsx32[np][j], g.wsy32[np][j]);
+    }
+}
+
+// the Morton cell coordinate of v along one axis (samples_role's binning, clamped)
+__device__ inline int sample_cell(double v, double v0, double f) {
+    return min(max((int)((v - v0) * f), 0), 15);
+}
+
 // Arguments of the window kernel.  Sample buffers are double-buffered by window parity: the
 // screen of window w writes wsx/wsy[p], the resolve of w - 1 reads [1 - p].
 struct WinKArgs {
@@ -590,6 +726,9 @@ struct WinKArgs {
     int* fin_par;
     ResolveScratch rs;
     double* lit_scratch;
+    // window mode: workgroup 0 draws the next window's samples (parity 1 - p) after its commit
+    int gen_next;
+    SamplesArgs g;
 };
 
 // RRT::get_nearest_node screen (rrt.rs:378-391): f32 SoA nodes x the window's samples.  The
@@ -808,86 +947,8 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
     }
 }
 
-// window_samples: Space::rand_point for the iterations [start, start + W) of a window
-// (rrt.rs:139-146, seeded: Q7 — x = draw 2*it, y = draw 2*it + 1), W = min(K, target - start),
-// and a counting sort of the samples by the Morton index of their cell in a 16 x 16 grid over the
-// sampling box: perm[pos] = sample, so a screen block of 256 consecutive sorted samples is
-// spatially compact (the expanded screen's precision).  Within a cell the order is arbitrary —
-// the results never depend on it (only which samples meet the exact rescan).
-struct SamplesArgs {
-    int K;
-    int64_t target;
-    uint64_t seed;
-    double minx, maxx, miny, maxy;
-    double* wsx[2];
-    double* wsy[2];
-    float* wsx32[2];
-    float* wsy32[2];
-    int* perm[2];
-};
-
-__device__ inline int morton16(int x, int y) {
-    int m = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) m |= (((x >> b) & 1) << (2 * b)) | (((y >> b) & 1) << (2 * b + 1));
-    return m;
-}
-
-__device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t start,
-                             char* smem) {
-    int* s_hist = reinterpret_cast<int*>(smem);                  // [256]
-    unsigned char* s_cell = reinterpret_cast<unsigned char*>(s_hist + 256);  // [K]
-    const int tid = threadIdx.x, NT = blockDim.x;
-    const int64_t rem = g.target - start;
-    const int W = (rem <= 0 || st->error) ? 0 : (rem < g.K ? (int)rem : g.K);
-    if (tid == 0) {
-        st->Wp[np] = W;
-        st->wsp[np] = start;
-    }
-    for (int i = tid; i < 256; i += NT) s_hist[i] = 0;
-    __syncthreads();
-    const double fx = 16.0 / (g.maxx - g.minx), fy = 16.0 / (g.maxy - g.miny);
-    for (int j = tid; j < W; j += NT) {
-        const uint64_t itj = (uint64_t)(start + j);
-        const double x = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
-        const double y = gen_range(g.seed, 2 * itj + 1, g.miny, g.maxy);
-        g.wsx[np][j] = x;
-        g.wsy[np][j] = y;
-        g.wsx32[np][j] = (float)x;
-        g.wsy32[np][j] = (float)y;
-        const int cx = min(max((int)((x - g.minx) * fx), 0), 15);
-        const int cy = min(max((int)((y - g.miny) * fy), 0), 15);
-        const int cell = morton16(cx, cy);
-        s_cell[j] = (unsigned char)cell;
-        atomicAdd(&s_hist[cell], 1);
-    }
-    __syncthreads();
-    if (tid < 64) {  // exclusive prefix of the 256 cell counts, 4 per lane
-        int v[4], sum = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            v[u] = s_hist[4 * tid + u];
-            sum += v[u];
-        }
-        int x = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o);
-            if (tid >= o) x += y;
-        }
-        int base = x - sum;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            s_hist[4 * tid + u] = base;
-            base += v[u];
-        }
-    }
-    __syncthreads();
-    for (int j = tid; j < W; j += NT) g.perm[np][atomicAdd(&s_hist[s_cell[j]], 1)] = j;
-}
-
-// The first window of a batch: its samples (the later ones come from the previous window's
-// nn_finalize, which knows where the next window starts).
+// The first window of a batch: its samples (the later ones come from the previous window kernel
+// workgroup 0, after the commit that decides where the next window starts).
 __global__ __launch_bounds__(1024) void window_samples_kernel(DevState* st, SamplesArgs g, int np) {
     __shared__ __attribute__((aligned(16))) char smem[256 * 4 + kMaxWindow];
     samples_role(st, g, np, st->it_spec, smem);
@@ -900,19 +961,29 @@ __global__ __launch_bounds__(1024) void window_samples_kernel(DevState* st, Samp
 //     Margin test against the f32 rounding bound: certain → exact f64 d2 of the winner; else the
 //     wave's exact f64 brute force over the screen chunks whose f32 minimum could hide the exact
 //     nearest and over the appended nodes (rrt.rs:378-391; lowest index on exact ties, Q9).
-//  2. Window pairs (window mode): for each of the workgroup's samples j, the earlier window
-//     samples i < j strictly nearer than j's snapshot NN — the candidates of the sequential-
-//     consistency resolve.  The window's samples are staged in LDS (f32); lane (s, r) tests
-//     sample s against i = r (mod 4) of its wave's slice; an f32 distance within 5e-4 of the NN
-//     distance goes to the exact f64 test (dx*dx + dy*dy < nn_d2, the oracle's arithmetic).  Hits
-//     stay in LDS (at most kCandCap per sample, the count exact) and are appended with one global
-//     atomic per workgroup.
+//  2. Window pairs (window mode): for each of the workgroup's samples j (one wave each), the
+//     earlier window samples i < j strictly nearer than j's snapshot NN — the candidates of the
+//     sequential-consistency resolve.  The window's samples are binned in a 16 x 16 Morton grid
+//     (samples_role: perm, cofs, sorted f32 copies), so the wave visits only the cells j's disc
+//     of radius sqrt(D2) touches; an f32 distance within the rounding margin of the NN distance
+//     goes to the exact f64 test (dx*dx + dy*dy < nn_d2, the oracle's arithmetic).  Hits stay in
+//     LDS (at most kCandCap per sample, the count exact) and are appended with one global atomic
+//     per workgroup.
 // Workgroup 0 also publishes the window (W, or 0 when a truncated predecessor voided it) for the
 // later kernels and advances the next window's screen position.
 constexpr int kFinThreads = 1024;
 constexpr int kFinWaves = kFinThreads / 64;
 constexpr int kFinSamples = kFinWaves;  // one wave per sample
 constexpr int kFinDelta = 4096;         // appended nodes staged in LDS (beyond: global loads)
+
+// The window's samples binned by Morton cell (samples_role): the pair search's spatial index.
+struct PairGrid {
+    const int* perm;     // sorted position -> sample
+    const int* cofs;     // [257] first sorted position of each cell
+    const float2* sxy;   // sorted position -> (x, y) f32
+    double minx, miny, fx, fy;  // samples_role's binning: cell = (v - v0) * f, clamped to 0..15
+    float slack;         // f32 prefilter margin for the coordinates' magnitude
+};
 
 __device__ inline Top2 shfl_xor_top2(Top2 t, int m) {
     return Top2{__shfl_xor(t.b, m), __shfl_xor(t.s, m), __shfl_xor(t.i, m)};
@@ -924,9 +995,9 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     const double* __restrict__ qx, const double* __restrict__ qy, const float* __restrict__ x32,
     const float* __restrict__ y32, const double* __restrict__ X, const double* __restrict__ Y,
     const double* __restrict__ YAW, double eps_coord, int* __restrict__ out_idx,
-    double* __restrict__ out_d2, double* __restrict__ out_pose, const float* __restrict__ qx32,
-    const float* __restrict__ qy32, int* __restrict__ cand_cnt, CandEntry* __restrict__ cand,
-    int* __restrict__ pend, const double* __restrict__ sq, SamplesArgs g) {
+    double* __restrict__ out_d2, double* __restrict__ out_pose, PairGrid pg,
+    int* __restrict__ cand_cnt, CandEntry* __restrict__ cand,
+    int* __restrict__ pend, const double* __restrict__ sq) {
     __shared__ double s_nd2[kFinSamples];  // exact snapshot NN d2 of each sample
     __shared__ int s_pc[kFinSamples];      // pair search: nearer window samples found
     __shared__ int s_pi[kFinSamples][kCandCap];
@@ -937,19 +1008,18 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     __shared__ uint64_t s_cmask;
     __shared__ double s_rd[kFinWaves];
     __shared__ int s_ri[kFinWaves];
-    __shared__ float2 s_xy[kMaxWindow];  // the window's samples (f32) for the pair search
     __shared__ float2 s_dn[kFinDelta];   // nodes appended after the screen's snapshot (f32)
+#ifdef PP_STAMPS_FIN
+#define FIN_STAMP(v) const int64_t v = (int64_t)__builtin_amdgcn_s_memrealtime()
+#else
+#define FIN_STAMP(v)
+#endif
+    FIN_STAMP(tf0);
     const bool voided = st->void_seq == seq || st->error;
     const int W = voided ? 0 : st->Wp[p];
     const int ns = st->nsp[p], n = st->n;
-    if (sq && blockIdx.x == gridDim.x - 1) {  // the next window's samples (window mode)
-        samples_role(st, g, 1 - p, voided ? st->it_spec : st->wsp[p] + W,
-                     reinterpret_cast<char*>(s_xy));
-        return;
-    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->W = W;
-        st->weff = W;
         st->n_scan = n;
         if (!voided) st->it_spec = st->wsp[p] + W;
     }
@@ -959,15 +1029,12 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int q = q0 + wave;
     const bool in = q < W;
-    if (cand) {  // stage the window's earlier samples for the pair search
-        const int jmax = min(q0 + kFinSamples - 1, W - 1);
-        for (int i = tid; i < jmax; i += kFinThreads) s_xy[i] = make_float2(qx32[i], qy32[i]);
-    }
     const int D = n - ns, Dl = min(D, kFinDelta);  // appended nodes (staged: the first kFinDelta)
     for (int k = tid; k < Dl; k += kFinThreads) s_dn[k] = make_float2(x32[ns + k], y32[ns + k]);
     if (tid < kFinSamples) s_pc[tid] = 0;
     if (tid == 0) s_fmask = 0;
     __syncthreads();
+    FIN_STAMP(tf1);
     // ---- 1. the sample's nearest node
     if (in) {
         const int n_chunks = scan_chunks_used(ns, chunks);
@@ -984,7 +1051,11 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
         }
         const double xq = qx[q], yq = qy[q];
         const float fx = (float)xq, fy = (float)yq;
+#ifdef PP_T_NOAPPEND
+        for (int k = lane; k < 0; k += 64) {
+#else
         for (int k = lane; k < D; k += 64) {  // appended nodes: exact top-2 per lane
+#endif
             const float2 v = k < Dl ? s_dn[k] : make_float2(x32[ns + k], y32[ns + k]);
             const float d = scan_d2(fx, fy, v.x, v.y);
             const Top2 c{d, __builtin_inff(), ns + k};
@@ -1088,6 +1159,7 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
         }
     }
     __syncthreads();
+    FIN_STAMP(tf2);
     // near-ties: the workgroup's exact f64 brute force, over the screen chunks whose f32 minimum
     // could hide the exact nearest (f32 distance within the rounding bound of the f32 winner)
     // and over the appended nodes; lowest index on exact ties (rrt.rs:378-391, Q9)
@@ -1140,51 +1212,68 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
         }
         __syncthreads();
     }
+    FIN_STAMP(tf3);
     if (!cand) return;  // nearest-only launch (no window)
     // ---- 2. window pairs
+#ifndef PP_T_NOPAIRS
     {
-        const int s = lane & (kFinSamples - 1), r = lane >> 4;  // 4 lane groups of 16 samples
-        const int j = q0 + s;
-        const bool jin = j < W;
-        const double xj = jin ? qx[j] : 0.0, yj = jin ? qy[j] : 0.0;
-        const float xjf = (float)xj, yjf = (float)yj;
-        const double D2 = jin ? s_nd2[s] : -1.0;
-        const float df = jin ? __builtin_sqrtf((float)D2) + 5.0e-4f : -1.0f;
-        const float thr = jin ? df * df : -1.0f;
-        const int jmax = min(q0 + kFinSamples - 1, W - 1);  // pairs i < j <= jmax
-        const int per = ((jmax + kFinWaves - 1) / kFinWaves + 3) & ~3;
-        const int i0 = min(wave * per, jmax), i1 = min(i0 + per, jmax);
-        for (int ib = i0; ib < i1; ib += 32) {  // 8 pairs per lane per step
-            float2 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = s_xy[min(ib + 4 * u + r, i1 - 1)];
-            float dmin = __builtin_inff();
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int ii = ib + 4 * u + r;
-                const float d = scan_d2(xjf, yjf, v[u].x, v[u].y) - thr;
-                dmin = (ii < i1 && ii < j) ? fminf(dmin, d) : dmin;
-            }
-            if (__any(dmin <= 0.0f)) {  // rare: the exact tests of this step's candidates
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int ii = ib + 4 * u + r;
-                    if (ii < i1 && ii < j && scan_d2(xjf, yjf, v[u].x, v[u].y) <= thr) {
+        // wave w: sample j = q0 + w against the window samples i < j of the Morton cells its
+        // disc of radius sqrt(D2) touches (the binning is monotone, so the cells are a superset)
+        const int j = q0 + wave;
+        if (j < W) {
+            const double xj = qx[j], yj = qy[j];
+            const float xjf = (float)xj, yjf = (float)yj;
+            const double D2 = s_nd2[wave];
+            const float df = __builtin_sqrtf((float)D2) + pg.slack;
+            const float thr = df * df;
+            const double R = sqrt(D2) * (1.0 + 1e-9) + 1e-9;
+            const int cx0 = sample_cell(xj - R, pg.minx, pg.fx), cx1 = sample_cell(xj + R, pg.minx, pg.fx);
+            const int cy0 = sample_cell(yj - R, pg.miny, pg.fy), cy1 = sample_cell(yj + R, pg.miny, pg.fy);
+            for (int cy = cy0; cy <= cy1; ++cy) {
+                for (int cx = cx0; cx <= cx1; ++cx) {
+                    const int m = morton16(cx, cy);
+                    const int a1 = pg.cofs[m + 1];
+                    for (int pos = pg.cofs[m] + lane; pos < a1; pos += 64) {
+                        const float2 v = pg.sxy[pos];
+                        if (!(scan_d2(xjf, yjf, v.x, v.y) <= thr)) continue;
+                        const int ii = pg.perm[pos];
+                        if (ii >= j) continue;
                         const double dx = xj - qx[ii], dy = yj - qy[ii];
                         const double d2 = dx * dx + dy * dy;
-                        if (d2 < D2) {
-                            const int pos = atomicAdd(&s_pc[s], 1);
-                            if (pos < kCandCap) {
-                                s_pi[s][pos] = ii;
-                                s_pd[s][pos] = d2;
+                        if (d2 < D2) {  // strictly nearer than the snapshot NN (which wins ties)
+                            const int at = atomicAdd(&s_pc[wave], 1);
+                            if (at < kCandCap) {
+                                s_pi[wave][at] = ii;
+                                s_pd[wave][at] = d2;
                             }
                         }
                     }
                 }
             }
+#ifdef PP_PAIR_CHECK
+            int bc = 0, gc = 0;
+            for (int i = lane; i < j; i += 64) {
+                const double dx = xj - qx[i], dy = yj - qy[i];
+                bc += (dx * dx + dy * dy < D2) ? 1 : 0;
+            }
+            for (int o = 32; o > 0; o >>= 1) bc += __shfl_xor(bc, o);
+            gc = s_pc[wave];
+            if (lane == 0 && bc != gc) {
+                atomicAdd((unsigned long long*)&st->stamps[0], 1ull);
+                st->stamps[1] = j;
+                st->stamps[2] = bc;
+                st->stamps[3] = gc;
+                st->stamps[4] = (int64_t)(D2 * 1e6);
+                st->stamps[5] = cx0 * 100 + cx1;
+                st->stamps[6] = cy0 * 100 + cy1;
+                st->stamps[7] = seq;
+            }
+#endif
         }
     }
+#endif
     __syncthreads();
+    FIN_STAMP(tf4);
     if (wave == 0) {
         const int j = q0 + lane;
         const bool jin = lane < kFinSamples && j < W;
@@ -1214,6 +1303,18 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
         if (cnt > 0) pend[pb] = j;
         if (lane == 0 && ov) atomicMin(&st->weff, q0 + (int)__builtin_ctzll(ov));
     }
+#ifdef PP_STAMPS_FIN
+    FIN_STAMP(tf5);
+    if (tid == 0) {  // [0..2] workgroups without a near-tie brute force: sum, count, max;
+                     // [3..5] with one; [6] their brute-force time, [7] all pair-search time
+        const int o = s_fmask ? 3 : 0;
+        atomicAdd((unsigned long long*)&st->stamps[o], (unsigned long long)(tf5 - tf0));
+        atomicAdd((unsigned long long*)&st->stamps[o + 1], 1ull);
+        atomicMax((unsigned long long*)&st->stamps[o + 2], (unsigned long long)(tf5 - tf0));
+        if (s_fmask) atomicAdd((unsigned long long*)&st->stamps[6], (unsigned long long)(tf3 - tf2));
+        atomicAdd((unsigned long long*)&st->stamps[7], (unsigned long long)(tf4 - tf3));
+    }
+#endif
 }
 
 // Task t of a window: t < W is (sample t → its snapshot NN); t >= W is candidate entry t - W
@@ -1667,6 +1768,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                 atomicAdd((unsigned long long*)&stw[2], (unsigned long long)sw_col);
                 atomicAdd((unsigned long long*)&stw[3], (unsigned long long)sw_chunks);
                 atomicAdd((unsigned long long*)&stw[4], 1ull);
+                atomicMax((unsigned long long*)&stw[7], (unsigned long long)(sw_gen + sw_pt + sw_col));
             }
         }
         if (rj_) return kReject;
@@ -1685,7 +1787,10 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
 // steer_walk, one task per wave (persistent grid, grid-stride over the W + ncomp tasks); kLds:
 // the scene's disc grid is staged into this workgroup's LDS first.
 constexpr int kGenSlots = 68;  // per-wave LDS slots of the point generator (63 + 4 overshoot + 1)
-constexpr int kWalkMaxWG = 768;  // 3 resident workgroups per CU
+#ifndef PP_WALKWG
+#define PP_WALKWG 768
+#endif
+constexpr int kWalkMaxWG = PP_WALKWG;  // 3 resident workgroups per CU
 __host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
     return scene_bytes + kWalkThreads / 64 * kGenSlots * 8;
 }
@@ -2199,6 +2304,23 @@ __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
             st->flag_count = 0;
             st->ncomp = 0;
             st->npend = 0;
+            // no cut yet: nn_finalize's workgroups lower it with atomicMin in any order (a plain
+            // store there raced with the early finishers)
+            st->weff = 0x7fffffff;
+        }
+        if (a.gen_next) {
+            // Space::rand_point of the window after the screened one, into the parity the
+            // committed window just freed: it starts where the screened window ends, or — when
+            // the commit above voided the screened window (a truncation) — where the committed
+            // one stopped (it_spec).  Off the critical path: the screen takes longer.
+            __shared__ int64_t s_start;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const bool voided = st->void_seq == a.seq || st->error;
+                s_start = voided ? st->it_spec : st->wsp[a.p] + st->Wp[a.p];
+            }
+            __syncthreads();
+            samples_role(st, a.g, 1 - a.p, s_start, smem);
         }
         return;
     }
@@ -2231,6 +2353,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_tail_kernel(WinKArgs 
         st->flag_count = 0;
         st->ncomp = 0;
         st->npend = 0;
+        st->weff = 0x7fffffff;
     }
 }
 
@@ -2660,6 +2783,40 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
 // --------------------------------------------------------------------------- launch wrappers
 
 namespace {
+SamplesArgs samples_args(const WindowArgs& a) {
+    SamplesArgs g;
+    g.K = a.K;
+    g.target = a.target;
+    g.seed = a.seed;
+    g.minx = a.sc.minx;
+    g.maxx = a.sc.maxx;
+    g.miny = a.sc.miny;
+    g.maxy = a.sc.maxy;
+    for (int q = 0; q < 2; ++q) {
+        g.wsx[q] = a.wsx + (size_t)q * a.Kcap;
+        g.wsy[q] = a.wsy + (size_t)q * a.Kcap;
+        g.wsx32[q] = a.wsx32 + (size_t)q * a.Kcap;
+        g.wsy32[q] = a.wsy32 + (size_t)q * a.Kcap;
+        g.perm[q] = a.perm + (size_t)q * a.Kcap;
+        g.cofs[q] = a.cofs + (size_t)q * 257;
+        g.sxy[q] = a.sxy + (size_t)q * a.Kcap;
+    }
+    return g;
+}
+PairGrid pair_grid(const SamplesArgs& g, int p, double eps_coord) {
+    PairGrid r;
+    r.perm = g.perm[p];
+    r.cofs = g.cofs[p];
+    r.sxy = g.sxy[p];
+    r.minx = g.minx;
+    r.miny = g.miny;
+    r.fx = 16.0 / (g.maxx - g.minx);  // samples_role's factors, bit for bit
+    r.fy = 16.0 / (g.maxy - g.miny);
+    // f32 rounding of both samples' coordinates (and of the distance arithmetic)
+    r.slack = (float)(5.0e-4 + 4.0 * eps_coord);
+    return r;
+}
+
 WinKArgs win_args(const WindowArgs& a, int p, int gen, int resolve, int scan, int64_t seq) {
     WinKArgs k;
     k.st = a.st;
@@ -2700,47 +2857,30 @@ WinKArgs win_args(const WindowArgs& a, int p, int gen, int resolve, int scan, in
     k.fin_par = a.fin_par;
     k.rs = a.rs;
     k.lit_scratch = a.lit_scratch;
+    k.gen_next = gen && scan;
+    k.g = samples_args(a);
     return k;
 }
 }  // namespace
 
-SamplesArgs samples_args(const WindowArgs& a) {
-    SamplesArgs g;
-    g.K = a.K;
-    g.target = a.target;
-    g.seed = a.seed;
-    g.minx = a.sc.minx;
-    g.maxx = a.sc.maxx;
-    g.miny = a.sc.miny;
-    g.maxy = a.sc.maxy;
-    for (int q = 0; q < 2; ++q) {
-        g.wsx[q] = a.wsx + (size_t)q * a.Kcap;
-        g.wsy[q] = a.wsy + (size_t)q * a.Kcap;
-        g.wsx32[q] = a.wsx32 + (size_t)q * a.Kcap;
-        g.wsy32[q] = a.wsy32 + (size_t)q * a.Kcap;
-        g.perm[q] = a.perm + (size_t)q * a.Kcap;
-    }
-    return g;
-}
 
 hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int64_t seq,
                          int resolve_prev) {
     const int K = a.K;
     const int p = (int)(seq & 1);
     const WinKArgs wk = win_args(a, p, 1, resolve_prev, 1, seq);
-    const SamplesArgs g = samples_args(a);
-    if (!resolve_prev)  // the batch's first window: its samples (later: the previous finalize)
-        window_samples_kernel<<<1, 1024, 0, s>>>(a.st, g, p);
+    if (!resolve_prev)  // the batch's first window: its samples (later: the previous window kernel)
+        window_samples_kernel<<<1, 1024, 0, s>>>(a.st, wk.g, p);
     double* wsx = a.wsx + (size_t)p * a.Kcap;
     double* wsy = a.wsy + (size_t)p * a.Kcap;
     if (ev) (void)hipEventRecord(ev[0], s);
     window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
     if (ev) (void)hipEventRecord(ev[1], s);
     if (resolve_prev && !kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
-    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples + 1, kFinThreads, 0, s>>>(
+    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples, kFinThreads, 0, s>>>(
         a.st, p, seq, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, wsx, wsy, a.tr.x32, a.tr.y32,
-        a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose, wk.wsx32[p],
-        wk.wsy32[p], a.cand_cnt, a.cand, a.pend, wk.sq[p], g);
+        a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose,
+        pair_grid(wk.g, p, a.eps_coord), a.cand_cnt, a.cand, a.pend, wk.sq[p]);
     if (ev) (void)hipEventRecord(ev[2], s);
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K + kPrepThreads / 8 - 1) / (kPrepThreads / 8);
@@ -2772,8 +2912,8 @@ hipError_t launch_nearest(hipStream_t s, const WindowArgs& a) {
     window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
     nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples, kFinThreads, 0, s>>>(
         a.st, 0, 0, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, a.wsx, a.wsy, a.tr.x32,
-        a.tr.y32, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, nullptr, nullptr,
-        nullptr, nullptr, nullptr, nullptr, nullptr, SamplesArgs{});
+        a.tr.y32, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, nullptr, PairGrid{},
+        nullptr, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 

@@ -55,7 +55,7 @@ struct SceneDev {
     int lds_bytes;  // 0: read the scene from global memory
     const uint4* img;  // the LDS image, contiguous in global memory (lds_bytes / 16 words)
     int lds_goff, lds_items, lds_cx, lds_cy, lds_r2;  // byte offsets inside the image
-    // the discs in f32 for the per-lane cull: (cx, cy, rcull rounded up, 0)
+    // the discs in f32 for the per-lane cull: (cx, cy, rcull rounded up, r + width/2)
     const float4* d4;
     int lds_d4;
     // occupancy grid (BASELINE config 4): when bits != nullptr the discs are ignored and every

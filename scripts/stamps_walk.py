@@ -14,5 +14,5 @@ p.reset_stats()
 p.extend(20 * 4096)
 s = p.stats()["stamps"]
 n = max(s[4], 1)
-print("walk us per task: gen %.2f interp %.2f collide %.2f | chunks/task %.2f tasks %d | staging us/WG %.2f (%d WGs)"
-      % (s[0] / n / 100, s[1] / n / 100, s[2] / n / 100, s[3] / n, n, s[5] / max(s[6], 1) / 100, s[6]))
+print("walk us per task: gen %.2f interp %.2f collide %.2f | chunks/task %.2f tasks %d | staging us/WG %.2f (%d WGs) | slowest task %.2f us"
+      % (s[0] / n / 100, s[1] / n / 100, s[2] / n / 100, s[3] / n, n, s[5] / max(s[6], 1) / 100, s[6], s[7] / 100))
