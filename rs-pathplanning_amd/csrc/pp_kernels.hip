@@ -527,7 +527,7 @@ __global__ __launch_bounds__(64) void dubins_batch_kernel(const double* __restri
 // batch.
 
 #ifndef PP_QPL
-#define PP_QPL 4
+#define PP_QPL 8
 #endif
 #ifndef PP_SCANBLK
 #define PP_SCANBLK 16
@@ -544,7 +544,7 @@ constexpr bool kWinRepair = true;                // repairs inside the window ke
 constexpr int kScanWaves = kScanThreads / 64;
 constexpr int kScanBlk = PP_SCANBLK;             // nodes per scalar-load block
 #ifndef PP_SCANGRID
-#define PP_SCANGRID 240
+#define PP_SCANGRID 255
 #endif
 constexpr int kScanGrid = PP_SCANGRID;           // screen workgroups per window (one per CU, with
                                                  // the resolve workgroup: <= 256 CUs)
