@@ -94,6 +94,13 @@ def lib():
                                    C.c_int64, C.c_double, C.c_double, C.c_double, C.c_int, ip, dp,
                                    C.POINTER(C.c_int32)]
             L.orc_plan.restype = C.c_int64
+            L.orc_extend_replicas.argtypes = [C.POINTER(Scene), C.POINTER(Tree),
+                                              C.POINTER(C.c_uint64), C.c_int, C.c_int64,
+                                              C.c_int64, C.c_int, C.c_int]
+            L.orc_extend_replicas.restype = C.c_int64
+            L.orc_queries.argtypes = [C.POINTER(Scene), dp, C.POINTER(C.c_uint64), C.c_int,
+                                      C.c_int64, C.c_int, C.c_int]
+            L.orc_queries.restype = C.c_int64
             _lib = L
     return _lib
 
@@ -321,3 +328,30 @@ def plan(scene: OracleScene, tree: OracleTree, seed: int, it0: int, n_iter: int,
     if acc < 0:
         raise RuntimeError(f"orc_plan failed ({acc})")
     return acc, bn.value, bl.value, log
+
+
+def extend_replicas(scene: OracleScene, tree: OracleTree, seeds, it0: int, n_iter: int,
+                    threads: int, full_reverify: bool = False) -> int:
+    """len(seeds) independent continuations of ``tree`` (iterations [it0, it0 + n_iter), replica r
+    with seeds[r]) on ``threads`` host threads (the multi-core CPU baseline).  Returns the nodes
+    accepted over all replicas; ``tree`` is not modified."""
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+    r = lib().orc_extend_replicas(C.byref(scene._c), C.byref(tree._c),
+                                  seeds.ctypes.data_as(C.POINTER(C.c_uint64)), len(seeds), it0,
+                                  n_iter, int(full_reverify), int(threads))
+    if r < 0:
+        raise RuntimeError("orc_extend_replicas failed")
+    return r
+
+
+def queries(scene: OracleScene, starts, seeds, max_iter: int, threads: int,
+            full_reverify: bool = False) -> int:
+    """Independent queries (start starts[q], stream seeds[q], max_iter iterations each) on
+    ``threads`` host threads.  Returns the nodes accepted over all queries."""
+    starts = np.ascontiguousarray(starts, dtype=np.float64).reshape(-1, 3)
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+    r = lib().orc_queries(C.byref(scene._c), _dp(starts), seeds.ctypes.data_as(C.POINTER(C.c_uint64)),
+                          len(seeds), max_iter, int(full_reverify), int(threads))
+    if r < 0:
+        raise RuntimeError("orc_queries failed")
+    return r

@@ -29,6 +29,7 @@
  *       by it), tested on the line's segments and points (see orc_verify_line).
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -810,4 +811,98 @@ int64_t orc_plan(const orc_scene* sc, orc_tree* tr, uint64_t seed, int64_t it0, 
         }
     }
     return acc;
+}
+
+/* ------------------------------------------- multi-core CPU baseline (bench.py cpu_baseline) */
+/* Independent sequential planners on T host threads (pthreads): the CPU analogue of the GPU
+ * bench's parallelism.  Every job is one orc_rrt_extend run on its own tree, so results equal the
+ * single-thread runs job by job; only the throughput is measured. */
+typedef struct {
+    const orc_scene* sc;
+    const orc_tree* base;      /* replicas: the tree every job continues (copied) */
+    const double* starts;      /* queries: 3 per job (x, y, yaw) */
+    const uint64_t* seeds;     /* per job */
+    int64_t it0, n_iter;
+    int full_reverify;
+    int n_jobs;
+    int next;                  /* job counter (mutex) */
+    pthread_mutex_t mu;
+    int64_t accepted;
+    int failed;
+} orc_pool;
+
+static void* pool_worker(void* arg) {
+    orc_pool* P = (orc_pool*)arg;
+    for (;;) {
+        pthread_mutex_lock(&P->mu);
+        const int j = P->next < P->n_jobs ? P->next++ : -1;
+        pthread_mutex_unlock(&P->mu);
+        if (j < 0) break;
+        const int n0 = P->base ? P->base->n : 1;
+        const int cap = n0 + (int)P->n_iter + 1;
+        orc_tree t;
+        t.x = (double*)malloc(sizeof(double) * (size_t)cap);
+        t.y = (double*)malloc(sizeof(double) * (size_t)cap);
+        t.yaw = (double*)malloc(sizeof(double) * (size_t)cap);
+        t.parent = (int32_t*)malloc(sizeof(int32_t) * (size_t)cap);
+        t.cap = cap;
+        int64_t a = -1;
+        if (t.x && t.y && t.yaw && t.parent) {
+            if (P->base) {
+                memcpy(t.x, P->base->x, sizeof(double) * (size_t)n0);
+                memcpy(t.y, P->base->y, sizeof(double) * (size_t)n0);
+                memcpy(t.yaw, P->base->yaw, sizeof(double) * (size_t)n0);
+                memcpy(t.parent, P->base->parent, sizeof(int32_t) * (size_t)n0);
+            } else {
+                t.x[0] = P->starts[3 * j];
+                t.y[0] = P->starts[3 * j + 1];
+                t.yaw[0] = P->starts[3 * j + 2];
+                t.parent[0] = -1;
+            }
+            t.n = n0;
+            a = orc_rrt_extend(P->sc, &t, P->seeds[j], P->it0, P->n_iter, P->full_reverify, NULL,
+                               NULL);
+        }
+        free(t.x); free(t.y); free(t.yaw); free(t.parent);
+        pthread_mutex_lock(&P->mu);
+        if (a < 0) P->failed = 1;
+        else P->accepted += a;
+        pthread_mutex_unlock(&P->mu);
+    }
+    return NULL;
+}
+
+static int64_t run_pool(orc_pool* P, int threads) {
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+    if (!th) return -1;
+    pthread_mutex_init(&P->mu, NULL);
+    int started = 0;
+    for (int i = 0; i < threads; ++i)
+        if (pthread_create(&th[i], NULL, pool_worker, P) == 0) started++;
+    if (started == 0) pool_worker(P);
+    for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
+    pthread_mutex_destroy(&P->mu);
+    free(th);
+    return P->failed ? -1 : P->accepted;
+}
+
+/* n_rep replicas of `base`, replica r continuing iterations [it0, it0+n_iter) with seeds[r] */
+int64_t orc_extend_replicas(const orc_scene* sc, const orc_tree* base, const uint64_t* seeds,
+                            int n_rep, int64_t it0, int64_t n_iter, int full_reverify, int threads) {
+    orc_pool P;
+    memset(&P, 0, sizeof P);
+    P.sc = sc; P.base = base; P.seeds = seeds; P.it0 = it0; P.n_iter = n_iter;
+    P.full_reverify = full_reverify; P.n_jobs = n_rep;
+    return run_pool(&P, threads);
+}
+
+/* n_q independent queries (RRT::new at starts[3q..], seeds[q]), max_iter iterations each */
+int64_t orc_queries(const orc_scene* sc, const double* starts, const uint64_t* seeds, int n_q,
+                    int64_t max_iter, int full_reverify, int threads) {
+    orc_pool P;
+    memset(&P, 0, sizeof P);
+    P.sc = sc; P.starts = starts; P.seeds = seeds; P.n_iter = max_iter;
+    P.full_reverify = full_reverify; P.n_jobs = n_q;
+    return run_pool(&P, threads);
 }
