@@ -31,10 +31,12 @@ BYTES_PER_EVAL = 8            # f32 x + f32 y of one SoA node
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=("config2", "config3", "config4"), default="config2",
+    ap.add_argument("--workload", choices=("config2", "config3", "config4", "polygons"),
+                    default="config2",
                     help="config2: one tree, K-candidate windows (default); config3: a batch of "
                          "independent queries sharded over the ranks; config4: config 2 with the "
-                         "512x512 occupancy-grid collision")
+                         "512x512 occupancy-grid collision; polygons: config 2 with its discs as "
+                         "create_circle polygons (polygon mode, SURVEY §8f row 3)")
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (config2: windows, default 20; config3: lockstep "
                          "iterations, default max_iter)")
@@ -232,7 +234,8 @@ def main():
     dist, world, rank, local = dist_setup(args)
     from pathplanning_amd import scenes
 
-    raw = scenes.field512_grid() if args.workload == "config4" else scenes.field512()
+    raw = {"config4": scenes.field512_grid, "polygons": scenes.field512_polygons}.get(
+        args.workload, scenes.field512)()
     p = make_planner(raw, args.seed + rank, args.window, local)
     sweep = {}
     # grow the tree (untimed); on the way time a few windows at 1k and 10k nodes
@@ -313,14 +316,17 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": ("config4: field512 rasterised to a 512x512 bit-packed occupancy grid "
-                         "(32 KB, point probes)" if args.workload == "config4" else
-                         "config2: field512 (1024 discs r~U(2,8), 512x512)")
+            "workload": {"config4": "config4: field512 rasterised to a 512x512 bit-packed "
+                                    "occupancy grid (32 KB, point probes)",
+                         "polygons": "polygons: field512's 1024 discs as create_circle polygons "
+                                     f"({sum(len(o) for o in raw.get('obstacle_polygons', []))} "
+                                     "edges, Minkowski buffers, SURVEY §8f row 3)"}.get(
+                             args.workload, "config2: field512 (1024 discs r~U(2,8), 512x512)")
                         + f", R=4.0, step 0.1, K={args.window} candidates/window, tree grown to "
                         f"{args.nodes} nodes",
             "window": args.window,
             "tree_nodes_at_start": n_start,
-            "obstacles": len(raw["circles"]),
+            "obstacles": len(raw.get("obstacle_polygons", raw["circles"])),
             "parallelism": f"replicas{world}",
             "nn_screen_dtype": "f32 (exact f64 rescan of near-ties)",
         },

@@ -476,8 +476,19 @@ int orc_verify_line(const orc_scene* sc, const double* x, const double* y, int n
     }
     if (sc->ne > 0) { /* polygon obstacles: every segment vs every edge buffer, then one point
                        * inside test (no segment meets a buffer: the line is on one side) */
+        /* exact cull (speed only): an edge whose h-widened bbox misses the line's bbox is beyond
+         * h of every segment (the widening is rounded up) */
+        double lx0 = x[0], lx1 = x[0], ly0 = y[0], ly1 = y[0];
+        for (int i = 1; i < n; ++i) {
+            lx0 = fmin(lx0, x[i]); lx1 = fmax(lx1, x[i]);
+            ly0 = fmin(ly0, y[i]); ly1 = fmax(ly1, y[i]);
+        }
+        const double hm = sqrt(sc->h2) * (1.0 + 1e-9) + 1e-9;
         for (int k = 0; k < sc->ne; ++k) {
             const double e0x = sc->ex0[k], e0y = sc->ey0[k], e1x = sc->ex1[k], e1y = sc->ey1[k];
+            if (fmax(e0x, e1x) + hm < lx0 || fmin(e0x, e1x) - hm > lx1 ||
+                fmax(e0y, e1y) + hm < ly0 || fmin(e0y, e1y) - hm > ly1)
+                continue;
             if (n == 1 && seg_hits_edge(x[0], y[0], x[0], y[0], e0x, e0y, e1x, e1y, sc->h2))
                 return 0;
             for (int i = 0; i + 1 < n; ++i)

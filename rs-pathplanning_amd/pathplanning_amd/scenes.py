@@ -301,3 +301,15 @@ def transit(path: str | None = None) -> dict:
         path = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
             os.path.abspath(__file__)))), "tests", "golden", "transit.debug.json")
     return load_json(path, name="transit")
+
+
+def field512_polygons() -> dict:
+    """config 2's field in polygon mode (§8f row 3 at scale): the same 1024 discs as the crate's
+    own ``create_circle`` polygons (about 31 edges each, ~32k edges) and the 512 x 512 bounds as a
+    ring, so Space::verify runs the polygon-buffer tests (Q10p) instead of the analytic discs."""
+    raw = field512()
+    x0, y0, x1, y1 = raw["bounds"]
+    obs = [create_circle_polygon((c[0], c[1]), c[2]) for c in raw["circles"]]
+    return polygon_scene([(x0, y0), (x1, y0), (x1, y1), (x0, y1)], obs, raw["robot"],
+                         raw["start"], raw["goal"], raw["max_iter"], raw["step_size"],
+                         name="field512_polygons")

@@ -181,3 +181,17 @@ def test_polygon_batch_matches_independent_oracle_runs(pkg, ctx, oracle_mod):
         tr = oracle_mod.OracleTree(tuple(starts[q]), 600)
         oracle_mod.rrt_extend(sc, tr, int(seeds[q]), 0, 500)
         _assert_same_tree(b.tree(q), tr.arrays())
+
+
+def test_field512_polygons_parity(pkg, ctx, oracle_mod):
+    """bench.py --workload polygons at a testable size: config 2's field as ~32k create_circle
+    polygon edges (the scene too big for the LDS image: the walk's global-memory path), K = 4096,
+    15k iterations against the sequential oracle."""
+    from pathplanning_amd import scenes
+
+    raw = scenes.field512_polygons()
+    exp, acc, _, _ = _oracle_tree(oracle_mod, raw, 42, 15000)
+    assert acc > 1000
+    p = _planner(pkg, raw, 42, 4096, ctx)
+    assert p.extend(15000) == acc
+    _assert_same_tree(p.tree(), exp)
