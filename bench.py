@@ -42,6 +42,9 @@ def parse():
                          "iterations, default max_iter)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--queries", type=int, default=8192, help="config3: queries over all ranks")
+    ap.add_argument("--batch-window", type=int, default=0,
+                    help="config3: iterations per query evaluated speculatively per GPU step "
+                         "(power of two <= 64; 0 = automatic: 16 up to 131072 tasks per step)")
     ap.add_argument("--max-iter", type=int, default=2000, help="config3: RRT.max_iter per query")
     ap.add_argument("--window", type=int, default=4096)
     ap.add_argument("--nodes", type=int, default=100_000, help="tree size before timing")
@@ -118,6 +121,14 @@ def timed_windows(p, n_windows, window):
     p.extend(n_windows * window)
     p.synchronize()
     return time.perf_counter() - t0
+
+
+def auto_batch_window(q):
+    """pp_batch_new's automatic window: the largest power of two <= 16 with q * K <= 131072."""
+    k = 1
+    while k < 16 and q * k * 2 <= 131072:
+        k *= 2
+    return k
 
 
 def host_threads():
@@ -377,11 +388,11 @@ def main_config3(args):
     starts, goals, seeds = scenes.config3_queries(raw, a, b - a)
     steps = args.max_iter if args.steps is None else args.steps
     batch = rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
-                         device=local)
+                         device=local, window=args.batch_window)
     batch.extend(args.warmup)  # untimed warmup on a throwaway run
     batch.close()
     batch = rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
-                         device=local)
+                         device=local, window=args.batch_window)
     barrier(dist)
     t0 = time.perf_counter()
     it_local, acc_local = batch.extend(steps)
@@ -396,7 +407,7 @@ def main_config3(args):
     # profiled pass (same workload): HIP events around the batch NN kernel of every step
     batch.close()
     batch = rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
-                         device=local)
+                         device=local, window=args.batch_window)
     batch.set_profiling(True)
     batch.extend(steps)
     sp = batch.stats()
@@ -425,6 +436,7 @@ def main_config3(args):
             "queries": args.queries,
             "queries_per_rank": b - a,
             "parallelism": f"query-shard{world}",
+            "window_per_query": args.batch_window or auto_batch_window(b - a),
             "gather": f"all_gather of per-query records ({backend})",
         },
         "iterations_total": iters_total,

@@ -178,8 +178,13 @@ int pp_rrt_plan(pp_ctx* ctx, int64_t n_iter, int32_t* best_node, double* best_le
  * the shared max_iter and step_size.  Replaces any previous batch of the context. */
 int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
                  const uint64_t* seeds, int64_t max_iter, double step_size);
+/* speculative iterations per query and step (a power of two <= 64; 0 = automatic: 16 while the
+ * step holds at most 131072 tasks).  Results do not depend on it: every query's tree equals its one-at-a-time
+ * sequential run.  Applies to the current batch and the next ones. */
+int pp_batch_set_window(pp_ctx* ctx, int k);
 /* n_steps lockstep steps: every query runs one plan_one extend iteration (rrt.rs:583-589) per
- * step until it reaches max_iter.  Totals over the batch are returned (may be NULL). */
+ * step until it reaches max_iter.  Totals over the batch are returned (may be NULL).  On the
+ * GPU a step evaluates up to the batch window's iterations per query at once. */
 int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted);
 /* per-query tree sizes (q int32), consumed iterations and NN node-distance evaluations (q int64
  * each); any may be NULL.  With pp_set_profiling on, pp_batch_extend times its NN kernel with

@@ -172,6 +172,10 @@ struct pp_ctx {
     DBuf<uint64_t> mq_seed;
     DBuf<uint8_t> mq_blocked;
     bool mq_any_blocked = false;
+    int mq_K = 1;                 // speculative window per query of the current batch
+    int mq_K_user = 0;            // pp_batch_set_window (0: automatic)
+    DBuf<int64_t> mq_target;      // [Q] iteration targets of the running pp_batch_extend
+    DBuf<double> mq_nnd2;         // [Q * kMqMaxK]
     DBuf<SteerTask> mq_tasks;
     DBuf<PrepRec> mq_rec;
     DBuf<DevState> mq_state;
@@ -441,6 +445,9 @@ MqArgs mq_args(pp_ctx* c) {
     a.mq.evals = c->mq_evals.p;
     a.mq.seed = c->mq_seed.p;
     a.mq.blocked = c->mq_any_blocked ? c->mq_blocked.p : nullptr;
+    a.mq.K = c->mq_K;
+    a.mq.target = c->mq_target.p;
+    a.mq.nnd2 = c->mq_nnd2.p;
     a.sc = c->scene_dev();
     a.sc.step_size = c->mq_step;
     a.st = c->mq_state.p;
@@ -452,6 +459,18 @@ MqArgs mq_args(pp_ctx* c) {
     a.lit_scratch = c->api_lit_scratch.p;
     a.err = c->mq_err.p;
     return a;
+}
+
+// per-step task buffers of the batch: K slots per query
+int mq_reserve_tasks(pp_ctx* c, int q, int K) {
+    const size_t tq = (size_t)q * K;
+    PP_HIP(c->mq_tasks.reserve(tq));
+    PP_HIP(c->mq_status.reserve(tq));
+    PP_HIP(c->mq_yawbuf.reserve(tq));
+    PP_HIP(c->mq_rec.reserve(tq));
+    PP_HIP(c->mq_pdbuf.reserve(tq * kPdCap));
+    PP_HIP(c->mq_nnd2.reserve(tq));
+    return PP_OK;
 }
 
 int mq_totals(pp_ctx* c, int64_t* it_sum, int64_t* n_sum) {
@@ -1288,11 +1307,7 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
     PP_HIP(ctx->mq_it.reserve(q));
     PP_HIP(ctx->mq_evals.reserve(q));
     PP_HIP(ctx->mq_seed.reserve(q));
-    PP_HIP(ctx->mq_tasks.reserve(q));
-    PP_HIP(ctx->mq_status.reserve(q));
-    PP_HIP(ctx->mq_yawbuf.reserve(q));
-    PP_HIP(ctx->mq_rec.reserve(q));
-    PP_HIP(ctx->mq_pdbuf.reserve((size_t)q * kPdCap));
+    PP_HIP(ctx->mq_target.reserve(q));
     PP_HIP(ctx->mq_state.reserve(1));
     PP_HIP(ctx->mq_err.reserve(1));
     PP_HIP(ctx->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
@@ -1319,8 +1334,20 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
         PP_HIP(ctx->mq_blocked.reserve(q));
         PP_HIP(hipMemcpy(ctx->mq_blocked.p, blk.data(), q, hipMemcpyHostToDevice));
     }
+    // default window: 16 iterations per query and step while that stays under 131072 tasks (the
+    // throughput saturates there on one GPU; longer windows are cut more often by their own
+    // accepted samples — config 3 measured 219M it/s at K = 16 on the 8192-query batch and on a
+    // 1024-query shard 143M at K = 16 against 111M at K = 64)
+    if (ctx->mq_K_user > 0) {
+        ctx->mq_K = ctx->mq_K_user;
+    } else {
+        int K = 1;
+        while (K < kMqAutoK && (int64_t)q * (K * 2) <= 131072) K *= 2;
+        ctx->mq_K = K;
+    }
+    if ((r = mq_reserve_tasks(ctx, q, ctx->mq_K))) return r;
     DevState ds{};
-    ds.W = q;
+    ds.W = q * ctx->mq_K;
     PP_HIP(hipMemcpyAsync(ctx->mq_state.p, &ds, sizeof(DevState), hipMemcpyHostToDevice, st));
     PP_HIP(hipMemsetAsync(ctx->mq_err.p, 0, sizeof(int), st));
     PP_HIP(hipStreamSynchronize(st));
@@ -1328,6 +1355,23 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
     return PP_OK;
 }
 
+
+int pp_batch_set_window(pp_ctx* ctx, int k) {
+    if (!ctx) return set_err(PP_ERR_INVALID_ARGUMENT, "null context");
+    if (k < 0 || k > kMqMaxK || (k & (k - 1)))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "batch window must be 0 (automatic) or a power of two <= 64");
+    ctx->mq_K_user = k;
+    if (ctx->has_batch && k > 0) {  // applies from the next pp_batch_extend
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+        int r = mq_reserve_tasks(ctx, ctx->mq_Q, k);
+        if (r) return r;
+        ctx->mq_K = k;
+        DevState ds{};
+        ds.W = ctx->mq_Q * k;
+        PP_HIP(hipMemcpy(ctx->mq_state.p, &ds, sizeof(DevState), hipMemcpyHostToDevice));
+    }
+    return PP_OK;
+}
 
 int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted) {
     int r = check_ctx(ctx, true, false);
@@ -1337,28 +1381,42 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
     int64_t it0 = 0, n0 = 0, it1 = 0, n1 = 0;
     if ((n_iterations || n_accepted) && (r = mq_totals(ctx, &it0, &n0))) return r;
     MqArgs a = mq_args(ctx);
-    for (int64_t done = 0; done < n_steps;) {
-        const int chunk = (int)std::min<int64_t>(n_steps - done, 256);
-        if (ctx->prof) {
-            if ((r = ensure_events(ctx, 2 * (size_t)chunk))) return r;
-            a.ev = ctx->ev.data();
-        }
-        PP_HIP(launch_mq_steps(ctx->stream, a, chunk));
-        if (ctx->prof) {
-            PP_HIP(hipStreamSynchronize(ctx->stream));
-            for (int k = 0; k < chunk; ++k) {
-                float ms = 0.f;
-                PP_HIP(hipEventElapsedTime(&ms, ctx->ev[2 * k], ctx->ev[2 * k + 1]));
-                ctx->nn_scan_ms += ms;
+    const int K = ctx->mq_K, Q = ctx->mq_Q;
+    PP_HIP(launch_mq_target(ctx->stream, a.mq, n_steps, ctx->mq_target.p));
+    // every query advances n_steps iterations (to max_iter at most); a window advances up to K
+    // of them, fewer when the in-order replay stops early, so the host tops the steps up until
+    // every query has reached its target
+    int64_t steps = (n_steps + K - 1) / K;
+    std::vector<int64_t> hit(Q), htg(Q);
+    for (int pass = 0; steps > 0; ++pass) {
+        if (pass > 64 + n_steps) return set_err(PP_ERR_HIP, "batch extend made no progress");
+        for (int64_t done = 0; done < steps;) {
+            const int chunk = (int)std::min<int64_t>(steps - done, 256);
+            if (ctx->prof) {
+                if ((r = ensure_events(ctx, 2 * (size_t)chunk))) return r;
+                a.ev = ctx->ev.data();
             }
-            ctx->nn_scan_launches += chunk;
+            PP_HIP(launch_mq_steps(ctx->stream, a, chunk));
+            if (ctx->prof) {
+                PP_HIP(hipStreamSynchronize(ctx->stream));
+                for (int k = 0; k < chunk; ++k) {
+                    float ms = 0.f;
+                    PP_HIP(hipEventElapsedTime(&ms, ctx->ev[2 * k], ctx->ev[2 * k + 1]));
+                    ctx->nn_scan_ms += ms;
+                }
+                ctx->nn_scan_launches += chunk;
+            }
+            done += chunk;
         }
-        done += chunk;
+        PP_HIP(hipMemcpyAsync(hit.data(), ctx->mq_it.p, Q * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+        PP_HIP(hipMemcpyAsync(htg.data(), ctx->mq_target.p, Q * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+        int err = 0;
+        PP_HIP(hipMemcpyAsync(&err, ctx->mq_err.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+        if (err) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
+        steps = 0;
+        for (int q = 0; q < Q; ++q) steps = std::max(steps, (htg[q] - hit[q] + K - 1) / K);
     }
-    int err = 0;
-    PP_HIP(hipMemcpyAsync(&err, ctx->mq_err.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    PP_HIP(hipStreamSynchronize(ctx->stream));
-    if (err) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
     if ((n_iterations || n_accepted) && (r = mq_totals(ctx, &it1, &n1))) return r;
     if (n_iterations) *n_iterations = it1 - it0;
     if (n_accepted) *n_accepted = n1 - n0;

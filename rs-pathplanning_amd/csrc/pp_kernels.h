@@ -91,6 +91,8 @@ struct MqArgs {
 };
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps);
 hipError_t launch_mq_init(hipStream_t s, const MqDev& mq, const double* starts);
+// the per-query iteration targets of a pp_batch_extend(n_steps) call
+hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int64_t* target);
 
 hipError_t launch_dubins_batch(hipStream_t st, const double* conf, int n, int cap, double* px,
                                double* py, double* pyaw, int* n_out, int* word_out,

@@ -2646,13 +2646,18 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
 __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx, double maxx,
                                                            double miny, double maxy,
                                                            SteerTask* __restrict__ tasks) {
+    // one wave per task t = q * K + k: Space::rand_point of iteration it[q] + k on stream q
+    // (rrt.rs:139-146, Q7) and the exact nearest node of tree q as the step found it
+    // (rrt.rs:378-391, Q9: lanes stride the rows, lowest index on ties)
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    for (int q = gw; q < mq.Q; q += nw) {
-        const int64_t it = mq.it[q];
-        if (it >= mq.max_iter) {
-            if (lane == 0) tasks[q].pnode = -1;
+    const int K = mq.K;
+    for (int t = gw; t < mq.Q * K; t += nw) {
+        const int q = t / K, k = t - q * K;
+        const int64_t it = mq.it[q] + k;
+        if (it >= mq.target[q]) {
+            if (lane == 0) tasks[t].pnode = -1;
             continue;
         }
         const uint64_t seed = mq.seed[q];
@@ -2665,19 +2670,30 @@ __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx
         double bd = __builtin_inf();
         int bi = 0x7fffffff;
 #pragma unroll 4
-        for (int k = lane; k < n; k += 64) {
-            const double dx = x - X[k], dy = y - Y[k];
+        for (int i = lane; i < n; i += 64) {
+            const double dx = x - X[i], dy = y - Y[i];
             const double d2 = dx * dx + dy * dy;
             if (d2 < bd) {
                 bd = d2;
-                bi = k;
+                bi = i;
             }
         }
 #pragma unroll
         for (int m = 32; m > 0; m >>= 1) argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
-        if (lane == 0)
-            tasks[q] = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, 0};
+        if (lane == 0) {
+            tasks[t] = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, 0};
+            mq.nnd2[t] = bd;
+        }
     }
+}
+
+// the iteration targets of one pp_batch_extend call: n_steps more iterations, at most max_iter
+__global__ __launch_bounds__(256) void mq_target_kernel(MqDev mq, int64_t n_steps,
+                                                        int64_t* __restrict__ target) {
+    const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= mq.Q) return;
+    const int64_t t = mq.it[q] + n_steps;
+    target[q] = t < mq.max_iter ? t : mq.max_iter;
 }
 
 __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
@@ -2686,50 +2702,78 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
                                                         const double* __restrict__ yaw,
                                                         double* __restrict__ lit_scratch,
                                                         int* __restrict__ err) {
-    // lane per query; a wave (<= kLiteralWaves of them, one literal scratch each) re-runs its
-    // lanes' literal-path tasks together, one at a time
+    // a wave serves 64 / K queries, K lanes each (lane = g * K + k: the window's iteration
+    // it[q] + k of its g-th query; K a power of two <= 16).  Literal-path re-runs first (rare, the
+    // wave's one scratch buffer), then each query's in-order replay: iteration k keeps its
+    // speculative verdict unless an accepted window sample k' < k is strictly nearer than its
+    // snapshot NN (snapshot nodes have lower indices and win ties) — the window stops there and
+    // the next step resumes at it; the accepted samples before it are appended in order
+    // (rrt.rs:586-589).
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    const int K = mq.K, G = 64 / K;
+    const int g = lane / K, k = lane - g * K, g0 = g * K;
+    const uint64_t gmask = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << g0;
     double* bx = lit_scratch + (size_t)gw * 3 * kLiteralCap;
-    for (int base = gw * 64; base < mq.Q; base += nw * 64) {
-        const int q = base + lane;
+    for (int base = gw * G; base < mq.Q; base += nw * G) {
+        const int q = base + g;
         const bool in = q < mq.Q;
+        const int t = q * K + k;
         SteerTask tk{};
         int st = kReject;
-        double yw = 0.0;
+        double yw = 0.0, d2nn = 0.0;
         if (in) {
-            tk = tasks[q];
-            st = status[q];
-            yw = yaw[q];
+            tk = tasks[t];
+            st = status[t];
+            yw = yaw[t];
         }
         const bool act = in && tk.pnode >= 0;
-        uint64_t lit = __ballot(act && st == kLiteral);
-        while (lit) {
+        if (act) d2nn = mq.nnd2[t];
+        for (uint64_t lit = __ballot(act && st == kLiteral); lit; lit &= lit - 1) {
             const int l = __builtin_ctzll(lit);
-            lit &= lit - 1;
             const double x = __shfl(tk.x, l), y = __shfl(tk.y, l), w = __shfl(yw, l);
             const double px = __shfl(tk.px, l), py = __shfl(tk.py, l), pw = __shfl(tk.pyaw, l);
             const int r = steer_collide_literal(sc, x, y, w, px, py, pw, bx, bx + kLiteralCap,
                                                 bx + 2 * kLiteralCap);
             if (lane == l) st = r;
         }
-        if (!act) continue;
-        if (st == kError) {
-            atomicOr(err, 1);
-            continue;
+        const bool blocked = in && mq.blocked && mq.blocked[q];
+        const uint64_t accm = __ballot(act && st == kAccept && !blocked);
+        bool cut = !act;
+        for (int j = 0; j < K; ++j) {  // slot j of every query against its later slots
+            const double xj = __shfl(tk.x, g0 + j), yj = __shfl(tk.y, g0 + j);
+            if (((accm >> (g0 + j)) & 1ull) && k > j && act) {
+                const double dx = tk.x - xj, dy = tk.y - yj;
+                if (dx * dx + dy * dy < d2nn) cut = true;
+            }
         }
-        const int n = mq.n[q];
-        mq.evals[q] += n;  // the NN of this iteration scanned n nodes
-        if (st == kAccept && !(mq.blocked && mq.blocked[q])) {
-            const size_t o = (size_t)q * mq.cap + n;
+        const uint64_t cutm = __ballot(in && cut) & gmask;
+        const int T = cutm ? (int)__builtin_ctzll(cutm) - g0 : K;  // iterations consumed
+        const uint64_t keep = accm & gmask & ((T >= 64 ? ~0ull : ((1ull << T) - 1ull)) << g0);
+        const bool bad = __ballot(k < T && act && st == kError) & gmask;
+        const int n = in ? mq.n[q] : 0;
+        const int before = __popcll(keep & ((1ull << lane) - 1ull));
+        if (!bad && k < T && ((keep >> lane) & 1ull)) {
+            const size_t o = (size_t)q * mq.cap + n + before;
             mq.x[o] = tk.x;
             mq.y[o] = tk.y;
             mq.yaw[o] = yw;
             mq.parent[o] = tk.pnode;
-            mq.n[q] = n + 1;
         }
-        mq.it[q] += 1;
+        // NN node-distance evaluations of the sequential spec: iteration k scans the tree as it
+        // stands then (n + the window samples accepted before it)
+        int64_t ev = (in && k < T) ? (int64_t)(n + before) : 0;
+        for (int o = 1; o < K; o <<= 1) ev += __shfl_xor(ev, o);
+        if (in && k == 0 && T > 0) {
+            if (bad) {
+                atomicOr(err, 1);
+            } else {
+                mq.n[q] = n + __popcll(keep);
+                mq.it[q] += T;
+                mq.evals[q] += ev;
+            }
+        }
     }
 }
 
@@ -2752,12 +2796,18 @@ hipError_t launch_mq_init(hipStream_t s, const MqDev& mq, const double* starts) 
     return hipGetLastError();
 }
 
+hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int64_t* target) {
+    mq_target_kernel<<<(mq.Q + 255) / 256, 256, 0, s>>>(mq, n_steps, target);
+    return hipGetLastError();
+}
+
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int Q = a.mq.Q;
-    const int nn_blocks = std::min((Q + 3) / 4, 4096);
-    const int prep_blocks = std::min((Q + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
-    const int walk_blocks = std::min((Q + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
-    const int ins_blocks = std::min((Q + 255) / 256, kLiteralWaves / 4);
+    const int T = Q * a.mq.K;  // tasks per step
+    const int nn_blocks = std::min((T + 3) / 4, 4096);
+    const int prep_blocks = std::min((T + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
+    const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
+    const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), kLiteralWaves / 4);
     const int lds = a.sc.lds_bytes;
     for (int k = 0; k < steps; ++k) {
         if (a.ev) (void)hipEventRecord(a.ev[2 * k], s);

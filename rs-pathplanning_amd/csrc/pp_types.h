@@ -175,7 +175,17 @@ struct MqDev {
     const uint64_t* seed;   // [Q] sampling stream
     const uint8_t* blocked; // [Q] polygon mode: the root fails verify, so every line_to_origin
                             // does and nothing is ever inserted (rrt.rs:414-426); may be null
+    // speculative windows per query: every step evaluates the next K iterations of each query
+    // against its tree at the step start (task q * K + k = iteration it[q] + k); the insert
+    // replays them in order and stops at the first iteration whose nearest node would be one of
+    // the window's own accepted samples (the next step resumes there), so the result equals
+    // the one-iteration-per-step run for every K
+    int K;
+    const int64_t* target;  // [Q] iteration this pp_batch_extend call stops at
+    double* nnd2;           // [Q * K] exact d2 of each task's snapshot nearest node
 };
+constexpr int kMqMaxK = 64;  // window limit per query (config 3's strong-scaling parallelism)
+constexpr int kMqAutoK = 16; // the automatic window's limit
 
 // Resolve scratch (global, one window; indexed by pending slot / list position).
 struct ResolveScratch {

@@ -39,7 +39,7 @@ EXPORTED = [
     "pp_rrt_set_window", "pp_rrt_extend", "pp_rrt_plan_one", "pp_rrt_tree_size",
     "pp_rrt_iteration", "pp_rrt_tree_export", "pp_rrt_get_nearest_node_batch",
     "pp_rrt_verify_node_batch", "pp_rrt_check_finish_batch", "pp_rrt_check_finish",
-    "pp_rrt_plan", "pp_batch_new", "pp_batch_extend", "pp_batch_state", "pp_batch_tree_export",
+    "pp_rrt_plan", "pp_batch_new", "pp_batch_set_window", "pp_batch_extend", "pp_batch_state", "pp_batch_tree_export",
     "pp_rrt_get_stats", "pp_rrt_reset_stats", "pp_set_profiling",
 ]
 
@@ -125,6 +125,7 @@ def lib():
             "pp_rrt_plan": ([vp, C.c_int64, ip, dp, i64p], C.c_int),
             "pp_batch_new": ([vp, C.c_int, dp, dp, C.POINTER(C.c_uint64), C.c_int64, C.c_double],
                              C.c_int),
+            "pp_batch_set_window": ([vp, C.c_int], C.c_int),
             "pp_batch_extend": ([vp, C.c_int64, i64p, i64p], C.c_int),
             "pp_batch_state": ([vp, ip, i64p, i64p], C.c_int),
             "pp_batch_tree_export": ([vp, C.c_int, dp, dp, dp, ip, C.c_int64, i64p], C.c_int),

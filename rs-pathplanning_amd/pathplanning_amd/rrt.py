@@ -377,10 +377,12 @@ class RRT:  # rrt.rs:325-620
 class RRTBatch:
     """Many independent planners on one scene (BASELINE config 3): ``RRT::new`` per query
     (rrt.rs:335-355) with its own start, goal and sampling stream, advanced in lockstep — one
-    plan_one extend iteration (rrt.rs:583-589) of every query per step — on one GPU."""
+    plan_one extend iteration (rrt.rs:583-589) of every query per step — on one GPU.  ``window``:
+    iterations per query evaluated speculatively per GPU step (a power of two <= 64, 0 =
+    automatic: 16 up to 131072 tasks per step); every query's tree equals its sequential run."""
 
     def __init__(self, starts, goals, max_iter, step_size, space: Space, seeds, device: int = 0,
-                 ctx: _ffi.Context | None = None):
+                 ctx: _ffi.Context | None = None, window: int = 0):
         self.ctx = ctx or _ffi.Context(device)
         self.space = space
         starts = np.ascontiguousarray(starts, dtype=np.float64).reshape(-1, 3)
@@ -389,6 +391,8 @@ class RRTBatch:
         self.q = len(starts)
         self.max_iter = int(max_iter)
         space._upload(self.ctx)
+        # iterations per query evaluated per GPU step (0: automatic); results do not depend on it
+        _ffi.check(_ffi.lib().pp_batch_set_window(self.ctx.handle, int(window)))
         dp = C.POINTER(C.c_double)
         _ffi.check(_ffi.lib().pp_batch_new(
             self.ctx.handle, self.q, starts.ctypes.data_as(dp), goals.ctypes.data_as(dp),

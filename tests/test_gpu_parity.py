@@ -485,3 +485,27 @@ def test_grid_batch_and_verify_api(pkg, ctx, oracle_mod):
     ok, _ = p.verify_node_batch(qx, qy, qp)
     exp = [oracle_mod.verify_candidate(sc, tr, qx[i], qy[i], int(qp[i]))[0] for i in range(300)]
     assert ok.tolist() == exp
+
+
+@pytest.mark.parametrize("window", [1, 2, 8, 16, 64])
+def test_batch_windows_equal_sequential_runs(pkg, ctx, oracle_mod, window):
+    """config 3's per-query speculative windows: every query's tree equals its one-iteration-
+    at-a-time run for any window (bench6_open accepts often, so the in-order replay stops
+    windows early; ragged step counts end mid-window)"""
+    from pathplanning_amd import rrt, scenes
+
+    for raw, q0, nq, steps in ((scenes.bench6_open(), 7, 19, (37, 1, 250)),
+                               (scenes.field512(), 0, 24, (300,))):
+        starts, goals, seeds = scenes.config3_queries(raw, q0, nq)
+        b = rrt.RRTBatch(starts, goals, 2000, raw["step_size"], rrt.Space.from_raw(raw), seeds,
+                         ctx=ctx, window=window)
+        total = 0
+        for s in steps:
+            it, _ = b.extend(s)
+            total += s
+            assert it == nq * s
+        n, its = b.state()
+        assert (its == total).all()
+        for q in range(nq):
+            exp = _oracle_query(oracle_mod, raw, starts[q], seeds[q], total, 2000)
+            _assert_same_tree(b.tree(q), exp)
