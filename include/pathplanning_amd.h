@@ -194,6 +194,32 @@ int pp_batch_state(pp_ctx* ctx, int32_t* n_nodes, int64_t* iterations, int64_t* 
 int pp_batch_tree_export(pp_ctx* ctx, int query, double* x, double* y, double* yaw,
                          int32_t* parent, int64_t cap, int64_t* n);
 
+/* ------------------------------------------------- RRT* query batch (BASELINE config 5) */
+/* Build-defined: the reference has no RRT* (SURVEY.md §8d config 5, §8f row 4).  q independent
+ * k-nearest RRT* planners (Karaman & Frazzoli) in the crate's conventions (DESIGN.md §3.7,
+ * oracle/pp_oracle.c orc_star_extend): rand_point and the exact nearest node as in the extend
+ * (rrt.rs:139-146, 378-391); with eta > 0 a sample farther than eta from its nearest node moves
+ * onto the chord at distance eta (eta = 0: the node sits at the sample, like Node::new); the edge
+ * to the nearest node (verify_node, rrt.rs:414-426) gates the insert; the parent is the first
+ * strict minimum of cost(p) + Dubins cost (dubins.rs:351-361) over the nearest node and the k
+ * nearest nodes of the new point; then every one of those k nodes whose edge to the new node is
+ * feasible and makes it strictly cheaper is rewired (its pose kept), costs of its subtree
+ * recomputed.  k = 0: ceil(2e ln n) (at most 63 and n); 1..63: fixed.  Replaces any previous RRT*
+ * batch of the context. */
+int pp_star_new(pp_ctx* ctx, int q, const double* starts, const uint64_t* seeds,
+                int64_t max_iter, double step_size, int k, double eta);
+/* n_steps lockstep steps: every query runs one RRT* iteration per step until max_iter.  Batch
+ * totals (each may be NULL): iterations, inserted nodes, rewires. */
+int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted,
+                   int64_t* n_rewires);
+/* per-query tree sizes (q int32), iterations, NN node-distance evaluations and rewires (q int64
+ * each); any may be NULL */
+int pp_star_state(pp_ctx* ctx, int32_t* n_nodes, int64_t* iterations, int64_t* node_evals,
+                  int64_t* rewires);
+/* one query's tree (root first): coordinates, yaw, parent (-1 root) and node cost (root 0) */
+int pp_star_tree_export(pp_ctx* ctx, int query, double* x, double* y, double* yaw,
+                        int32_t* parent, double* cost, int64_t cap, int64_t* n);
+
 int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out);
 int pp_rrt_reset_stats(pp_ctx* ctx);
 /* record HIP events around the hot kernels (adds a little host overhead per window) */

@@ -101,6 +101,17 @@ def lib():
             L.orc_queries.argtypes = [C.POINTER(Scene), dp, C.POINTER(C.c_uint64), C.c_int,
                                       C.c_int64, C.c_int, C.c_int]
             L.orc_queries.restype = C.c_int64
+            L.orc_star_k.argtypes = [C.c_int, C.c_int]
+            L.orc_star_k.restype = C.c_int
+            L.orc_star_extend.argtypes = [C.POINTER(Scene), C.POINTER(Tree), dp, dp, C.c_uint64,
+                                          C.c_int64, C.c_int64, C.c_int, C.c_double,
+                                          C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                          C.POINTER(C.c_int8)]
+            L.orc_star_extend.restype = C.c_int64
+            L.orc_star_queries.argtypes = [C.POINTER(Scene), dp, C.POINTER(C.c_uint64), C.c_int,
+                                           C.c_int64, C.c_int, C.c_double, C.c_int,
+                                           C.POINTER(C.c_int64)]
+            L.orc_star_queries.restype = C.c_int64
             _lib = L
     return _lib
 
@@ -355,3 +366,52 @@ def queries(scene: OracleScene, starts, seeds, max_iter: int, threads: int,
     if r < 0:
         raise RuntimeError("orc_queries failed")
     return r
+
+
+# ------------------------------------------------------ RRT* (config 5, build-defined)
+class OracleStarTree(OracleTree):
+    """OracleTree plus the RRT* node costs and edge costs (root cost 0)."""
+
+    def __init__(self, start, cap):
+        super().__init__(start, cap)
+        self.cost = np.zeros(cap)
+        self.elen = np.zeros(cap)
+
+    def star_arrays(self):
+        n = self.n
+        return self.arrays() + (self.cost[:n].copy(), self.elen[:n].copy())
+
+
+def star_k(k_fixed: int, n: int) -> int:
+    return lib().orc_star_k(int(k_fixed), int(n))
+
+
+def star_extend(scene: OracleScene, tree: OracleStarTree, seed: int, it0: int, n_iter: int,
+                k_fixed: int = 0, eta: float = 0.0):
+    """RRT* iterations [it0, it0 + n_iter) (orc_star_extend).  Returns (accepted, rewires,
+    log_nn, log_acc)."""
+    log_nn = np.zeros(n_iter, dtype=np.int32)
+    log_acc = np.zeros(n_iter, dtype=np.int8)
+    rw = C.c_int64(0)
+    acc = lib().orc_star_extend(C.byref(scene._c), C.byref(tree._c), _dp(tree.cost),
+                                _dp(tree.elen), seed, it0, n_iter, int(k_fixed), float(eta),
+                                C.byref(rw),
+                                log_nn.ctypes.data_as(C.POINTER(C.c_int32)),
+                                log_acc.ctypes.data_as(C.POINTER(C.c_int8)))
+    if acc < 0:
+        raise RuntimeError("orc_star_extend failed (capacity?)")
+    return acc, rw.value, log_nn, log_acc
+
+
+def star_queries(scene: OracleScene, starts, seeds, max_iter: int, k_fixed: int, eta: float,
+                 threads: int):
+    """Independent RRT* queries on ``threads`` host threads.  Returns (accepted, rewires)."""
+    starts = np.ascontiguousarray(starts, dtype=np.float64).reshape(-1, 3)
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+    rw = C.c_int64(0)
+    r = lib().orc_star_queries(C.byref(scene._c), _dp(starts),
+                               seeds.ctypes.data_as(C.POINTER(C.c_uint64)), len(seeds), max_iter,
+                               int(k_fixed), float(eta), int(threads), C.byref(rw))
+    if r < 0:
+        raise RuntimeError("orc_star_queries failed")
+    return r, rw.value

@@ -502,10 +502,22 @@ int orc_verify_line(const orc_scene* sc, const double* x, const double* y, int n
             if (seg_hits_disc(x[0], y[0], x[0], y[0], sc->cx[k], sc->cy[k], sc->r2[k])) return 0;
         return 1;
     }
-    for (int k = 0; k < sc->m; ++k)
+    /* exact cull (speed only): a disc whose centre lies farther than its radius (rounded up)
+     * from the line's bbox is farther from every segment */
+    double lx0 = x[0], lx1 = x[0], ly0 = y[0], ly1 = y[0];
+    for (int i = 1; i < n; ++i) {
+        lx0 = fmin(lx0, x[i]); lx1 = fmax(lx1, x[i]);
+        ly0 = fmin(ly0, y[i]); ly1 = fmax(ly1, y[i]);
+    }
+    for (int k = 0; k < sc->m; ++k) {
+        const double cx = sc->cx[k], cy = sc->cy[k];
+        const double dx = fmax(fmax(lx0 - cx, cx - lx1), 0.0);
+        const double dy = fmax(fmax(ly0 - cy, cy - ly1), 0.0);
+        if (dx * dx + dy * dy > sc->r2[k] * (1.0 + 1e-9) + 1e-9) continue;
         for (int i = 0; i + 1 < n; ++i)
-            if (seg_hits_disc(x[i], y[i], x[i + 1], y[i + 1], sc->cx[k], sc->cy[k], sc->r2[k]))
+            if (seg_hits_disc(x[i], y[i], x[i + 1], y[i + 1], cx, cy, sc->r2[k]))
                 return 0;
+    }
     return 1;
 }
 
@@ -916,4 +928,234 @@ int64_t orc_queries(const orc_scene* sc, const double* starts, const uint64_t* s
     P.sc = sc; P.starts = starts; P.seeds = seeds; P.n_iter = max_iter;
     P.full_reverify = full_reverify; P.n_jobs = n_q;
     return run_pool(&P, threads);
+}
+
+/* ------------------------------------------------ RRT* (BASELINE config 5, build-defined) */
+/* The reference has no RRT* (SURVEY.md §8d config 5, §8f row 4): this is the build's own spec,
+ * k-nearest RRT* (Karaman & Frazzoli 2011, Alg. 6) in the crate's conventions, parity
+ * "unpinned" against any reference and pinned against oracle/rrtstar_py.py instead.
+ *   - sample and exact NN exactly as the extend (rrt.rs:139-146, 378-391); with eta > 0 a
+ *     sample farther than eta from its nearest node x_nearest moves to x_nearest + (sample -
+ *     x_nearest) * (eta / |sample - x_nearest|) (Steer; eta = 0 keeps the crate's node-at-the-
+ *     sample, Q5); the edge new → x_nearest (Node::new, verify_node: rrt.rs:169-175, 414-426)
+ *     gates the insert;
+ *   - an edge is feasible when its Dubins steer is Some and verify(edge ++ [parent]) holds (the
+ *     incremental verify of SURVEY.md §3.2; a None steer is infeasible here);
+ *   - edge cost = the crate's Dubins cost (dubins.rs:351-361, |t|+|p|+|q| of the chosen word);
+ *     node cost = cost(parent) + edge cost, accumulated root first in f64;
+ *   - choose parent: X_near = the k nearest nodes of the new point by (d2, index); candidates
+ *     x_nearest first, then X_near in order (x_nearest skipped); the first strict minimum of
+ *     cost(p) + edge cost over the feasible edges new → p (yaw = compute_yaw toward p);
+ *   - rewire: for m in X_near order, m != parent: the edge m → new keeps m's pose (x, y, yaw);
+ *     when feasible and cost(new) + edge cost < cost(m) (current), m's parent becomes new and
+ *     the costs of m's subtree are recomputed top down;
+ *   - k = min(k_fixed, 63, n) when k_fixed > 0, else min(63, n, max(1, ceil(2e ln n))), with n the
+ *     tree size before the insert (orc_star_k). */
+int orc_star_k(int k_fixed, int n) {
+    int k;
+    if (k_fixed > 0) {
+        k = k_fixed;
+    } else {
+        double v = n > 1 ? ceil(2.0 * 2.718281828459045 * log((double)n)) : 1.0;
+        k = v < 1.0 ? 1 : (v > 63.0 ? 63 : (int)v);
+    }
+    if (k > 63) k = 63;
+    return k < n ? k : n;
+}
+
+/* edge child (x, y, yaw) → parent pose: 1 feasible (Some and verify(edge ++ [parent])), 0 not,
+ * -1 error (allocation / the reference's n_point panic); *cost = the Dubins cost */
+static int star_edge(const orc_scene* sc, double x, double y, double yaw, double px, double py,
+                     double pyaw, pbuf* b, dscratch* s, double* cost) {
+    double conf[8] = {x, y, yaw, px, py, pyaw, sc->turn_radius, sc->step_size};
+    *cost = INFINITY;
+    int need = orc_dubins_n_point(conf);
+    if (need <= 0) return 0; /* None */
+    if (dscratch_fit(s, need) != 0) return -1;
+    int n = 0, word = -1;
+    int r = orc_dubins(conf, s->px, s->py, s->pyaw, s->cap, &n, &word, cost);
+    if (r < 0) return -1;
+    if (r == 0) { *cost = INFINITY; return 0; }
+    b->n = 0;
+    for (int i = 0; i < n; ++i)
+        if (pbuf_push(b, s->px[i], s->py[i])) return -1;
+    if (pbuf_push(b, px, py)) return -1;
+    return orc_verify_line(sc, b->x, b->y, b->n);
+}
+
+/* the k nearest nodes by (d2, index), ascending */
+static int star_knn(const orc_tree* tr, double qx, double qy, int k, int32_t* out, double* d2s) {
+    int m = 0;
+    for (int i = 0; i < tr->n; ++i) {
+        double dx = qx - tr->x[i], dy = qy - tr->y[i];
+        double d2 = dx * dx + dy * dy;
+        if (m == k && !(d2 < d2s[m - 1])) continue; /* (d2, i) > the k-th: i is the larger index */
+        int j = m < k ? m++ : m - 1;
+        while (j > 0 && d2 < d2s[j - 1]) { d2s[j] = d2s[j - 1]; out[j] = out[j - 1]; --j; }
+        d2s[j] = d2;
+        out[j] = i;
+    }
+    return m;
+}
+
+/* recompute cost[] over the subtree of m (level by level: each level's parents are final) */
+static int star_propagate(orc_tree* tr, double* cost, const double* elen, int m, uint8_t* fr,
+                          uint8_t* nx) {
+    memset(fr, 0, (size_t)tr->n);
+    fr[m] = 1;
+    for (;;) {
+        int any = 0;
+        memset(nx, 0, (size_t)tr->n);
+        for (int i = 0; i < tr->n; ++i) {
+            int p = tr->parent[i];
+            if (p >= 0 && fr[p]) { cost[i] = cost[p] + elen[i]; nx[i] = 1; any = 1; }
+        }
+        if (!any) break;
+        uint8_t* t = fr; fr = nx; nx = t;
+    }
+    return 0;
+}
+
+/* iterations [it0, it0 + n_iter) of RRT* on tree tr (with cost[], elen[] alongside; root cost
+ * 0).  Logs (optional): nearest index and accepted flag per iteration.  *rewires_out += rewires.
+ * Returns the accepted count, or -1 (allocation / capacity / steer overflow). */
+int64_t orc_star_extend(const orc_scene* sc, orc_tree* tr, double* cost, double* elen,
+                        uint64_t seed, int64_t it0, int64_t n_iter, int k_fixed, double eta,
+                        int64_t* rewires_out, int32_t* log_nn, int8_t* log_acc) {
+    pbuf b = {0};
+    dscratch s = {0};
+    int64_t acc = 0, rew = 0;
+    int32_t near[63];
+    double nd2[63];
+    uint8_t* fr = (uint8_t*)malloc((size_t)tr->cap + 1);
+    uint8_t* nx = (uint8_t*)malloc((size_t)tr->cap + 1);
+    if (!fr || !nx) acc = -1;
+    for (int64_t kk = 0; kk < n_iter && acc >= 0; ++kk) {
+        uint64_t it = (uint64_t)(it0 + kk);
+        double x = orc_gen_range(seed, 2 * it, sc->minx, sc->maxx);
+        double y = orc_gen_range(seed, 2 * it + 1, sc->miny, sc->maxy);
+        double d2;
+        int p = orc_nearest(tr->x, tr->y, tr->n, x, y, &d2);
+        if (log_nn) log_nn[kk] = p;
+        if (log_acc) log_acc[kk] = 0;
+        if (eta > 0.0 && d2 > eta * eta) { /* Steer(x_nearest, x_rand): eta along the chord */
+            double f = eta / sqrt(d2);
+            x = tr->x[p] + (x - tr->x[p]) * f;
+            y = tr->y[p] + (y - tr->y[p]) * f;
+        }
+        double yb = compute_yaw(x, y, tr->x[p], tr->y[p]), eb;
+        int ok = star_edge(sc, x, y, yb, tr->x[p], tr->y[p], tr->yaw[p], &b, &s, &eb);
+        if (ok < 0) { acc = -1; break; }
+        if (!ok) continue;
+        int k = orc_star_k(k_fixed, tr->n);
+        int kn = star_knn(tr, x, y, k, near, nd2);
+        int best = p;
+        double cb = cost[p] + eb;
+        for (int j = 0; j < kn; ++j) {
+            int q = near[j];
+            if (q == p) continue; /* the nearest is the first candidate */
+            double yq = compute_yaw(x, y, tr->x[q], tr->y[q]), eq;
+            int o = star_edge(sc, x, y, yq, tr->x[q], tr->y[q], tr->yaw[q], &b, &s, &eq);
+            if (o < 0) { acc = -1; break; }
+            if (o) {
+                double c = cost[q] + eq;
+                if (c < cb) { cb = c; best = q; yb = yq; eb = eq; }
+            }
+        }
+        if (acc < 0) break;
+        if (tr->n >= tr->cap) { acc = -1; break; }
+        int nw = tr->n;
+        tr->x[nw] = x; tr->y[nw] = y; tr->yaw[nw] = yb; tr->parent[nw] = best;
+        cost[nw] = cb; elen[nw] = eb;
+        tr->n++;
+        acc++;
+        if (log_acc) log_acc[kk] = 1;
+        for (int j = 0; j < kn; ++j) {
+            int m = near[j];
+            if (m == best || !(cb < cost[m])) continue; /* cb + e >= cb: no rewire possible */
+            double em;
+            int o = star_edge(sc, tr->x[m], tr->y[m], tr->yaw[m], x, y, yb, &b, &s, &em);
+            if (o < 0) { acc = -1; break; }
+            if (!o) continue;
+            double cn = cb + em;
+            if (cn < cost[m]) {
+                tr->parent[m] = nw; elen[m] = em; cost[m] = cn;
+                star_propagate(tr, cost, elen, m, fr, nx);
+                rew++;
+            }
+        }
+    }
+    free(fr); free(nx);
+    free(b.x); free(b.y);
+    free(s.px); free(s.py); free(s.pyaw);
+    if (rewires_out) *rewires_out += rew;
+    return acc;
+}
+
+/* n_q independent RRT* queries on T threads (the config-5 CPU baseline) */
+typedef struct {
+    const orc_scene* sc;
+    const double* starts;
+    const uint64_t* seeds;
+    int64_t n_iter;
+    int k_fixed, n_jobs, next, failed;
+    double eta;
+    int64_t accepted, rewires;
+    pthread_mutex_t mu;
+} orc_star_pool;
+
+static void* star_worker(void* arg) {
+    orc_star_pool* P = (orc_star_pool*)arg;
+    for (;;) {
+        pthread_mutex_lock(&P->mu);
+        const int j = P->next < P->n_jobs ? P->next++ : -1;
+        pthread_mutex_unlock(&P->mu);
+        if (j < 0) break;
+        const int cap = (int)P->n_iter + 1;
+        orc_tree t;
+        t.x = (double*)malloc(sizeof(double) * (size_t)cap);
+        t.y = (double*)malloc(sizeof(double) * (size_t)cap);
+        t.yaw = (double*)malloc(sizeof(double) * (size_t)cap);
+        t.parent = (int32_t*)malloc(sizeof(int32_t) * (size_t)cap);
+        double* cost = (double*)malloc(sizeof(double) * (size_t)cap);
+        double* elen = (double*)malloc(sizeof(double) * (size_t)cap);
+        t.cap = cap;
+        int64_t a = -1, rw = 0;
+        if (t.x && t.y && t.yaw && t.parent && cost && elen) {
+            t.x[0] = P->starts[3 * j]; t.y[0] = P->starts[3 * j + 1]; t.yaw[0] = P->starts[3 * j + 2];
+            t.parent[0] = -1; cost[0] = 0.0; elen[0] = 0.0;
+            t.n = 1;
+            a = orc_star_extend(P->sc, &t, cost, elen, P->seeds[j], 0, P->n_iter, P->k_fixed, P->eta, &rw,
+                                NULL, NULL);
+        }
+        free(t.x); free(t.y); free(t.yaw); free(t.parent); free(cost); free(elen);
+        pthread_mutex_lock(&P->mu);
+        if (a < 0) P->failed = 1;
+        else { P->accepted += a; P->rewires += rw; }
+        pthread_mutex_unlock(&P->mu);
+    }
+    return NULL;
+}
+
+int64_t orc_star_queries(const orc_scene* sc, const double* starts, const uint64_t* seeds, int n_q,
+                         int64_t max_iter, int k_fixed, double eta, int threads,
+                         int64_t* rewires_out) {
+    orc_star_pool P;
+    memset(&P, 0, sizeof P);
+    P.sc = sc; P.starts = starts; P.seeds = seeds; P.n_iter = max_iter; P.k_fixed = k_fixed;
+    P.eta = eta;
+    P.n_jobs = n_q;
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+    if (!th) return -1;
+    pthread_mutex_init(&P.mu, NULL);
+    int started = 0;
+    for (int i = 0; i < threads; ++i)
+        if (pthread_create(&th[i], NULL, star_worker, &P) == 0) started++;
+    if (started == 0) star_worker(&P);
+    for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
+    pthread_mutex_destroy(&P.mu);
+    free(th);
+    if (rewires_out) *rewires_out = P.rewires;
+    return P.failed ? -1 : P.accepted;
 }

@@ -181,6 +181,25 @@ struct pp_ctx {
     DBuf<DevState> mq_state;
     std::vector<double> mq_goal;  // 3 per query (kept for the host; the batch path is extend only)
 
+    // ---- RRT* query batch (BASELINE config 5, build-defined: DESIGN.md §3.7)
+    bool has_star = false;
+    int star_Q = 0, star_cap = 0, star_kfix = 0;
+    int64_t star_max_iter = 0;
+    double star_step = 0.1, star_eta = 0.0;
+    DBuf<double> sr_x, sr_y, sr_yaw, sr_cost, sr_elen, sr_px, sr_py, sr_cb;
+    DBuf<int> sr_par, sr_n, sr_mark, sr_stamp, sr_ksched, sr_pn, sr_near, sr_nnear, sr_bslot,
+        sr_cslot, sr_err;
+    DBuf<uint64_t> sr_cmask, sr_seed;
+    DBuf<int64_t> sr_it, sr_evals, sr_target, sr_rew;
+    DBuf<uint8_t> sr_blocked;
+    bool sr_any_blocked = false;
+    DBuf<DevState> sr_state;  // [3]: rounds A, B, C
+    DBuf<SteerTask> sr_tA, sr_tB, sr_tC;
+    DBuf<int> sr_sA, sr_sB, sr_sC;
+    DBuf<double> sr_yA, sr_yB, sr_yC, sr_cA, sr_cB, sr_cC;
+    DBuf<PrepRec> sr_rec;
+    DBuf<double> sr_pdbuf;
+
     // ---- profiling
     bool prof = false;
     std::vector<hipEvent_t> ev;  // 4 per window of a batch
@@ -470,6 +489,97 @@ int mq_reserve_tasks(pp_ctx* c, int q, int K) {
     PP_HIP(c->mq_rec.reserve(tq));
     PP_HIP(c->mq_pdbuf.reserve(tq * kPdCap));
     PP_HIP(c->mq_nnd2.reserve(tq));
+    return PP_OK;
+}
+
+// |X_near| of an insert into an n-node RRT* tree: k_fixed, or the k-nearest RRT* schedule
+// ceil(2e ln n) (Karaman & Frazzoli), capped at kStarKMax and at n (orc_star_k restates it)
+int star_k(int k_fixed, int n) {
+    int k;
+    if (k_fixed > 0) {
+        k = k_fixed;
+    } else {
+        const double v = n > 1 ? std::ceil(2.0 * 2.718281828459045 * std::log((double)n)) : 1.0;
+        k = v < 1.0 ? 1 : (v > kStarKMax ? kStarKMax : (int)v);
+    }
+    if (k > kStarKMax) k = kStarKMax;
+    return k < n ? k : n;
+}
+
+StarArgs star_args(pp_ctx* c) {
+    StarArgs a;
+    StarDev& d = a.sd;
+    d.mq.Q = c->star_Q;
+    d.mq.cap = c->star_cap;
+    d.mq.max_iter = c->star_max_iter;
+    d.mq.x = c->sr_x.p;
+    d.mq.y = c->sr_y.p;
+    d.mq.yaw = c->sr_yaw.p;
+    d.mq.parent = c->sr_par.p;
+    d.mq.n = c->sr_n.p;
+    d.mq.it = c->sr_it.p;
+    d.mq.evals = c->sr_evals.p;
+    d.mq.seed = c->sr_seed.p;
+    d.mq.blocked = c->sr_any_blocked ? c->sr_blocked.p : nullptr;
+    d.mq.K = 1;
+    d.mq.target = c->sr_target.p;
+    d.cost = c->sr_cost.p;
+    d.elen = c->sr_elen.p;
+    d.mark = c->sr_mark.p;
+    d.stamp = c->sr_stamp.p;
+    d.ksched = c->sr_ksched.p;
+    d.eta = c->star_eta;
+    d.px = c->sr_px.p;
+    d.py = c->sr_py.p;
+    d.pn = c->sr_pn.p;
+    d.near = c->sr_near.p;
+    d.nnear = c->sr_nnear.p;
+    d.bslot = c->sr_bslot.p;
+    d.cslot = c->sr_cslot.p;
+    d.cmask = c->sr_cmask.p;
+    d.cb = c->sr_cb.p;
+    d.rewires = c->sr_rew.p;
+    d.stA = c->sr_state.p;
+    d.stB = c->sr_state.p + 1;
+    d.stC = c->sr_state.p + 2;
+    a.sc = c->scene_dev();
+    a.sc.step_size = c->star_step;
+    a.tA = c->sr_tA.p;
+    a.tB = c->sr_tB.p;
+    a.tC = c->sr_tC.p;
+    a.sA = c->sr_sA.p;
+    a.sB = c->sr_sB.p;
+    a.sC = c->sr_sC.p;
+    a.yA = c->sr_yA.p;
+    a.yB = c->sr_yB.p;
+    a.yC = c->sr_yC.p;
+    a.cA = c->sr_cA.p;
+    a.cB = c->sr_cB.p;
+    a.cC = c->sr_cC.p;
+    a.rec = c->sr_rec.p;
+    a.pdbuf = c->sr_pdbuf.p;
+    a.lit_scratch = c->api_lit_scratch.p;
+    a.err = c->sr_err.p;
+    return a;
+}
+
+int star_totals(pp_ctx* c, int64_t* it_sum, int64_t* n_sum, int64_t* rw_sum) {
+    const int Q = c->star_Q;
+    std::vector<int> hn(Q);
+    std::vector<int64_t> hit(Q), hrw(Q);
+    PP_HIP(hipMemcpyAsync(hn.data(), c->sr_n.p, Q * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    PP_HIP(hipMemcpyAsync(hit.data(), c->sr_it.p, Q * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    PP_HIP(hipMemcpyAsync(hrw.data(), c->sr_rew.p, Q * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    PP_HIP(hipStreamSynchronize(c->stream));
+    int64_t a = 0, b = 0, w = 0;
+    for (int i = 0; i < Q; ++i) {
+        a += hit[i];
+        b += hn[i];
+        w += hrw[i];
+    }
+    *it_sum = a;
+    *n_sum = b;
+    *rw_sum = w;
     return PP_OK;
 }
 
@@ -1450,6 +1560,159 @@ int pp_batch_tree_export(pp_ctx* ctx, int query, double* x, double* y, double* y
     if (y) PP_HIP(hipMemcpyAsync(y, ctx->mq_y.p + o, nn * sizeof(double), hipMemcpyDeviceToHost, st));
     if (yaw) PP_HIP(hipMemcpyAsync(yaw, ctx->mq_yaw.p + o, nn * sizeof(double), hipMemcpyDeviceToHost, st));
     if (parent) PP_HIP(hipMemcpyAsync(parent, ctx->mq_par.p + o, nn * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    return PP_OK;
+}
+
+int pp_star_new(pp_ctx* ctx, int q, const double* starts, const uint64_t* seeds,
+                int64_t max_iter, double step_size, int k, double eta) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (q <= 0 || !starts || !seeds || max_iter < 0 || max_iter > 0x7ffffff0 ||
+        !(step_size > 0.0) || k < 0 || k > kStarKMax || !(eta >= 0.0))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad RRT* batch arguments");
+    const int64_t cap64 = max_iter + 1;
+    if ((int64_t)q * cap64 > ((int64_t)1 << 34) || (int64_t)q * kStarKMax > 0x7fffffff)
+        return set_err(PP_ERR_CAPACITY, "RRT* batch too large");
+    const size_t rows = (size_t)q * (size_t)cap64, tb = (size_t)q * kStarKMax;
+    ctx->has_star = false;
+    PP_HIP(ctx->sr_x.reserve(rows));
+    PP_HIP(ctx->sr_y.reserve(rows));
+    PP_HIP(ctx->sr_yaw.reserve(rows));
+    PP_HIP(ctx->sr_par.reserve(rows));
+    PP_HIP(ctx->sr_cost.reserve(rows));
+    PP_HIP(ctx->sr_elen.reserve(rows));
+    PP_HIP(ctx->sr_mark.reserve(rows));
+    PP_HIP(ctx->sr_ksched.reserve((size_t)cap64 + 1));
+    for (auto* b : {&ctx->sr_n, &ctx->sr_stamp, &ctx->sr_pn, &ctx->sr_nnear, &ctx->sr_bslot,
+                    &ctx->sr_cslot, &ctx->sr_sA})
+        PP_HIP(b->reserve(q));
+    for (auto* b : {&ctx->sr_px, &ctx->sr_py, &ctx->sr_cb, &ctx->sr_yA, &ctx->sr_cA})
+        PP_HIP(b->reserve(q));
+    for (auto* b : {&ctx->sr_it, &ctx->sr_evals, &ctx->sr_target, &ctx->sr_rew}) PP_HIP(b->reserve(q));
+    PP_HIP(ctx->sr_seed.reserve(q));
+    PP_HIP(ctx->sr_cmask.reserve(q));
+    PP_HIP(ctx->sr_near.reserve(tb));
+    PP_HIP(ctx->sr_tA.reserve(q));
+    PP_HIP(ctx->sr_tB.reserve(tb));
+    PP_HIP(ctx->sr_tC.reserve(tb));
+    PP_HIP(ctx->sr_sB.reserve(tb));
+    PP_HIP(ctx->sr_sC.reserve(tb));
+    for (auto* b : {&ctx->sr_yB, &ctx->sr_yC, &ctx->sr_cB, &ctx->sr_cC}) PP_HIP(b->reserve(tb));
+    PP_HIP(ctx->sr_rec.reserve(tb));
+    PP_HIP(ctx->sr_pdbuf.reserve(tb * kPdCap));
+    PP_HIP(ctx->sr_state.reserve(3));
+    PP_HIP(ctx->sr_err.reserve(1));
+    PP_HIP(ctx->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
+    ctx->star_Q = q;
+    ctx->star_cap = (int)cap64;
+    ctx->star_max_iter = max_iter;
+    ctx->star_step = step_size;
+    ctx->star_kfix = k;
+    ctx->star_eta = eta;
+    hipStream_t st = ctx->stream;
+    std::vector<int> ks((size_t)cap64 + 1);
+    for (int64_t n = 0; n <= cap64; ++n) ks[n] = star_k(k, (int)n);
+    PP_HIP(hipMemcpy(ctx->sr_ksched.p, ks.data(), ks.size() * sizeof(int), hipMemcpyHostToDevice));
+    PP_HIP(hipMemsetAsync(ctx->sr_mark.p, 0, rows * sizeof(int), st));
+    // polygon mode: queries whose root fails verify never insert (see pp_rrt_new)
+    ctx->sr_any_blocked = false;
+    if (ctx->ne > 0 || ctx->nbv > 0) {
+        std::vector<uint8_t> blk(q);
+        for (int i = 0; i < q; ++i) {
+            blk[i] = ctx->point_ok(starts[3 * i], starts[3 * i + 1]) ? 0 : 1;
+            ctx->sr_any_blocked |= blk[i] != 0;
+        }
+        PP_HIP(ctx->sr_blocked.reserve(q));
+        PP_HIP(hipMemcpy(ctx->sr_blocked.p, blk.data(), q, hipMemcpyHostToDevice));
+    }
+    DBuf<double> d_starts;
+    PP_HIP(d_starts.reserve(3 * (size_t)q));
+    PP_HIP(hipMemcpyAsync(d_starts.p, starts, 3 * (size_t)q * sizeof(double), hipMemcpyHostToDevice, st));
+    PP_HIP(hipMemcpyAsync(ctx->sr_seed.p, seeds, q * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    PP_HIP(launch_star_init(st, star_args(ctx), d_starts.p));
+    DevState ds[3] = {};
+    ds[0].W = q;
+    PP_HIP(hipMemcpyAsync(ctx->sr_state.p, ds, sizeof ds, hipMemcpyHostToDevice, st));
+    PP_HIP(hipMemsetAsync(ctx->sr_err.p, 0, sizeof(int), st));
+    PP_HIP(hipStreamSynchronize(st));
+    ctx->has_star = true;
+    return PP_OK;
+}
+
+int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted,
+                   int64_t* n_rewires) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (!ctx->has_star) return set_err(PP_ERR_STATE, "pp_star_new has not been called");
+    if (n_steps < 0) return set_err(PP_ERR_INVALID_ARGUMENT, "n_steps < 0");
+    const bool tot = n_iterations || n_accepted || n_rewires;
+    int64_t it0 = 0, n0 = 0, w0 = 0, it1 = 0, n1 = 0, w1 = 0;
+    if (tot && (r = star_totals(ctx, &it0, &n0, &w0))) return r;
+    StarArgs a = star_args(ctx);
+    PP_HIP(launch_mq_target(ctx->stream, a.sd.mq, n_steps, ctx->sr_target.p));
+    const int64_t steps = std::min<int64_t>(n_steps, ctx->star_max_iter);  // one iteration a step
+    for (int64_t done = 0; done < steps;) {
+        const int chunk = (int)std::min<int64_t>(steps - done, 256);
+        if (ctx->prof) {
+            if ((r = ensure_events(ctx, 2 * (size_t)chunk))) return r;
+            a.ev = ctx->ev.data();
+        }
+        PP_HIP(launch_star_steps(ctx->stream, a, chunk));
+        if (ctx->prof) {
+            PP_HIP(hipStreamSynchronize(ctx->stream));
+            for (int k = 0; k < chunk; ++k) {
+                float ms = 0.f;
+                PP_HIP(hipEventElapsedTime(&ms, ctx->ev[2 * k], ctx->ev[2 * k + 1]));
+                ctx->nn_scan_ms += ms;
+            }
+            ctx->nn_scan_launches += chunk;
+        }
+        done += chunk;
+    }
+    int err = 0;
+    PP_HIP(hipMemcpyAsync(&err, ctx->sr_err.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    PP_HIP(hipStreamSynchronize(ctx->stream));
+    if (err) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
+    if (tot && (r = star_totals(ctx, &it1, &n1, &w1))) return r;
+    if (n_iterations) *n_iterations = it1 - it0;
+    if (n_accepted) *n_accepted = n1 - n0;
+    if (n_rewires) *n_rewires = w1 - w0;
+    return PP_OK;
+}
+
+int pp_star_state(pp_ctx* ctx, int32_t* n_nodes, int64_t* iterations, int64_t* node_evals,
+                  int64_t* rewires) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (!ctx->has_star) return set_err(PP_ERR_STATE, "pp_star_new has not been called");
+    const int Q = ctx->star_Q;
+    hipStream_t st = ctx->stream;
+    if (n_nodes) PP_HIP(hipMemcpyAsync(n_nodes, ctx->sr_n.p, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+    if (iterations) PP_HIP(hipMemcpyAsync(iterations, ctx->sr_it.p, Q * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    if (node_evals) PP_HIP(hipMemcpyAsync(node_evals, ctx->sr_evals.p, Q * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    if (rewires) PP_HIP(hipMemcpyAsync(rewires, ctx->sr_rew.p, Q * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    return PP_OK;
+}
+
+int pp_star_tree_export(pp_ctx* ctx, int query, double* x, double* y, double* yaw,
+                        int32_t* parent, double* cost, int64_t cap, int64_t* n) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (!ctx->has_star) return set_err(PP_ERR_STATE, "pp_star_new has not been called");
+    if (query < 0 || query >= ctx->star_Q) return set_err(PP_ERR_INVALID_ARGUMENT, "query out of range");
+    int nn = 0;
+    PP_HIP(hipMemcpy(&nn, ctx->sr_n.p + query, sizeof(int), hipMemcpyDeviceToHost));
+    if (n) *n = nn;
+    if (cap < nn) return set_err(PP_ERR_CAPACITY, "export buffer smaller than the tree");
+    const size_t o = (size_t)query * ctx->star_cap;
+    hipStream_t st = ctx->stream;
+    if (x) PP_HIP(hipMemcpyAsync(x, ctx->sr_x.p + o, nn * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (y) PP_HIP(hipMemcpyAsync(y, ctx->sr_y.p + o, nn * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (yaw) PP_HIP(hipMemcpyAsync(yaw, ctx->sr_yaw.p + o, nn * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (parent) PP_HIP(hipMemcpyAsync(parent, ctx->sr_par.p + o, nn * sizeof(int), hipMemcpyDeviceToHost, st));
+    if (cost) PP_HIP(hipMemcpyAsync(cost, ctx->sr_cost.p + o, nn * sizeof(double), hipMemcpyDeviceToHost, st));
     PP_HIP(hipStreamSynchronize(st));
     return PP_OK;
 }

@@ -94,6 +94,24 @@ hipError_t launch_mq_init(hipStream_t s, const MqDev& mq, const double* starts);
 // the per-query iteration targets of a pp_batch_extend(n_steps) call
 hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int64_t* target);
 
+// RRT* query batch (config 5): `steps` lockstep RRT* iterations of every query.  Task arrays of
+// round A hold Q entries, rounds B and C Q * kStarKMax; rec / pdbuf are shared by the rounds.
+struct StarArgs {
+    StarDev sd{};
+    SceneDev sc{};
+    SteerTask *tA = nullptr, *tB = nullptr, *tC = nullptr;
+    int *sA = nullptr, *sB = nullptr, *sC = nullptr;        // verdicts
+    double *yA = nullptr, *yB = nullptr, *yC = nullptr;     // child yaw of each task
+    double *cA = nullptr, *cB = nullptr, *cC = nullptr;     // Dubins cost of each task
+    PrepRec* rec = nullptr;
+    double* pdbuf = nullptr;
+    double* lit_scratch = nullptr;  // kLiteralWaves buffers
+    int* err = nullptr;
+    hipEvent_t* ev = nullptr;  // optional: 2 per step, around star_sample + round A + star_knn
+};
+hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps);
+hipError_t launch_star_init(hipStream_t s, const StarArgs& a, const double* starts);
+
 hipError_t launch_dubins_batch(hipStream_t st, const double* conf, int n, int cap, double* px,
                                double* py, double* pyaw, int* n_out, int* word_out,
                                double* cost_out, int* status_out);

@@ -1370,9 +1370,10 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     const DevState* __restrict__ st, SceneDev sc, const double* __restrict__ wsx,
     const double* __restrict__ wsy, const double* __restrict__ snap_pose,
     CandEntry* __restrict__ cand, PrepRec* __restrict__ rec, double* __restrict__ pdbuf,
-    double* __restrict__ snap_yaw, const SteerTask* __restrict__ tasks) {
+    double* __restrict__ snap_yaw, const SteerTask* __restrict__ tasks,
+    double* __restrict__ cost_out = nullptr) {
     // tasks != nullptr: explicit (child, parent pose) tasks [0, W) (multi-query batch); a task
-    // with pnode < 0 is idle
+    // with pnode < 0 is idle; own_yaw: the child keeps its heading cyaw (RRT* rewire edges)
     const int W = st->W;
     const int total = W + st->ncomp;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1384,8 +1385,8 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     for (int blk = blockIdx.x; blk * TPB < total; blk += gridDim.x) {
         const int t = blk * TPB + wave * TPW + lane / kPrepLanes;
         bool act = t < total;
-        int j = 0;
-        double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0;
+        int j = 0, own = 0;
+        double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0, cyaw = 0.0;
         if (act && tasks) {
             const SteerTask tk = tasks[t];
             act = tk.pnode >= 0;
@@ -1394,12 +1395,15 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
             px = act ? tk.px : 1.0;
             py = act ? tk.py : 0.0;
             pyaw = act ? tk.pyaw : 0.0;
+            own = tk.own_yaw;
+            cyaw = tk.cyaw;
         } else if (act) {
             window_task(t, W, wsx, wsy, snap_pose, cand, &j, &px, &py, &pyaw);
             x = wsx[j];
             y = wsy[j];
         }
-        const double yaw = atan2(py - y, px - x);
+        const double cy_atan = atan2(py - y, px - x);
+        const double yaw = own ? cyaw : cy_atan;
         // dubins_path_planning, dubins.rs:401-408 (s = child, e = parent)
         const double ex = px - x, ey = py - y;
         const double cyw = cos(yaw), syw = sin(yaw);
@@ -1579,6 +1583,8 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
                 snap_yaw[t] = yaw;
             else
                 cand[t - W].yaw = yaw;
+            // the Dubins cost (dubins.rs:351-361; inf on None): the RRT* edge cost
+            if (cost_out) cost_out[t] = bc;
         }
     }
 }
@@ -2827,6 +2833,426 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
                                                     a.lit_scratch, a.err);
     }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------- RRT* query batch (config 5, §3.7)
+//
+// One lockstep step = one RRT* iteration of every query (oracle/pp_oracle.c orc_star_extend):
+//   star_sample    one wave per query: rand_point, the exact nearest node, Steer(eta) and the
+//                  gate task (new → nearest)                                      → round A
+//   star_knn       gated queries: X_near = the k nearest nodes of the new point (exact f64,
+//                  (d2, index) order, distances cached in LDS), one choose-parent task per
+//                  X_near node other than the nearest                               → round B
+//   star_insert    the first strict minimum of cost(p) + edge cost over the feasible candidates
+//                  (nearest first), the append, one rewire task per X_near node that could
+//                  still get cheaper (cost(new) < cost(m))                          → round C
+//   star_rewire    the rewires in X_near order against the costs as they stand, each followed by
+//                  a level-synchronous recomputation of the rewired node's subtree costs
+// Rounds A/B/C are the window pipeline's steer_prep / steer_walk on explicit tasks; their task
+// counts live in DevState W (stA: Q, stB / stC: counted on the device), so a step needs no host
+// round trip.
+constexpr int kKnnWaves = 4;
+constexpr int kKnnCache = 2048;  // d2 values cached per wave (LDS: 4 x 16 KB)
+
+__device__ __forceinline__ bool star_feasible(int status, double e) {
+    return status == kAccept && e <= 1.7976931348623157e308;  // Some and verified (finite cost)
+}
+
+__global__ __launch_bounds__(256) void star_sample_kernel(StarDev sd, double minx, double maxx,
+                                                          double miny, double maxy,
+                                                          SteerTask* __restrict__ tasks) {
+    const int lane = threadIdx.x & 63;
+    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the step's round-B / round-C task counters
+        sd.stB->W = 0;
+        sd.stC->W = 0;
+    }
+    const MqDev& mq = sd.mq;
+    for (int q = gw; q < mq.Q; q += nw) {
+        const int64_t it = mq.it[q];
+        if (it >= mq.target[q]) {
+            if (lane == 0) {
+                tasks[q].pnode = -1;
+                sd.pn[q] = -1;
+            }
+            continue;
+        }
+        const uint64_t seed = mq.seed[q];
+        double x = gen_range(seed, 2 * (uint64_t)it, minx, maxx);      // rrt.rs:139-146 (Q7)
+        double y = gen_range(seed, 2 * (uint64_t)it + 1, miny, maxy);
+        const int n = mq.n[q];
+        const size_t row = (size_t)q * mq.cap;
+        const double* __restrict__ X = mq.x + row;
+        const double* __restrict__ Y = mq.y + row;
+        double bd = __builtin_inf();
+        int bi = 0x7fffffff;
+#pragma unroll 4
+        for (int i = lane; i < n; i += 64) {  // rrt.rs:378-391 (Q9: exact, lowest index on ties)
+            const double dx = x - X[i], dy = y - Y[i];
+            const double d2 = dx * dx + dy * dy;
+            if (d2 < bd) {
+                bd = d2;
+                bi = i;
+            }
+        }
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+        const double nx = X[bi], ny = Y[bi];
+        if (sd.eta > 0.0 && bd > sd.eta * sd.eta) {  // Steer(x_nearest, x_rand)
+            const double f = sd.eta / sqrt(bd);
+            x = nx + (x - nx) * f;
+            y = ny + (y - ny) * f;
+        }
+        if (lane == 0) {
+            SteerTask tk{};
+            tk.x = x;
+            tk.y = y;
+            tk.px = nx;
+            tk.py = ny;
+            tk.pyaw = mq.yaw[row + bi];
+            tk.pnode = bi;
+            tasks[q] = tk;
+            sd.px[q] = x;
+            sd.py[q] = y;
+            sd.pn[q] = bi;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __restrict__ statusA,
+                                                       const double* __restrict__ costA,
+                                                       SteerTask* __restrict__ tasksB,
+                                                       int* __restrict__ err) {
+    __shared__ double s_d2[kKnnWaves][kKnnCache];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    const MqDev& mq = sd.mq;
+    double* cache = s_d2[wave];
+    for (int q = gw; q < mq.Q; q += nw) {
+        const int p = sd.pn[q];
+        if (p < 0) continue;
+        const int n = mq.n[q];
+        const int st = statusA[q];
+        // the gate: the edge new → nearest (a literal-path verdict is settled by star_insert)
+        const bool gate = (st == kLiteral || star_feasible(st, costA[q])) &&
+                          !(mq.blocked && mq.blocked[q]);
+        if (!gate) {
+            if (lane == 0) {
+                if (st == kError) atomicOr(err, 1);  // n_point overflow: the reference panics
+                sd.nnear[q] = -1;
+                mq.it[q] += 1;
+                mq.evals[q] += n;
+            }
+            continue;
+        }
+        const double x = sd.px[q], y = sd.py[q];
+        const size_t row = (size_t)q * mq.cap;
+        const double* __restrict__ X = mq.x + row;
+        const double* __restrict__ Y = mq.y + row;
+        const int k = sd.ksched[n];
+        const bool cached = n <= kKnnCache;
+        if (cached)
+            for (int i = lane; i < n; i += 64) {
+                const double dx = x - X[i], dy = y - Y[i];
+                cache[i] = dx * dx + dy * dy;
+            }
+        // k rounds of the lexicographic (d2, index) successor of the previous winner
+        double pd = -1.0;
+        int pi = -1, mine = -1;
+        for (int r = 0; r < k; ++r) {
+            double bd = __builtin_inf();
+            int bi = 0x7fffffff;
+            for (int i = lane; i < n; i += 64) {
+                double d2;
+                if (cached) {
+                    d2 = cache[i];
+                } else {
+                    const double dx = x - X[i], dy = y - Y[i];
+                    d2 = dx * dx + dy * dy;
+                }
+                if ((d2 > pd || (d2 == pd && i > pi)) && d2 < bd) {
+                    bd = d2;
+                    bi = i;
+                }
+            }
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1)
+                argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+            pd = bd;
+            pi = bi;
+            if (lane == r) mine = bi;
+        }
+        const bool has = lane < k;
+        if (has) sd.near[(size_t)q * kStarKMax + lane] = mine;
+        const uint64_t pm = __ballot(has && mine == p);
+        const int cnt = k - (pm ? 1 : 0);
+        int slot = 0;
+        if (lane == 0) {
+            sd.nnear[q] = k;
+            slot = cnt > 0 ? atomicAdd(&sd.stB->W, cnt) : 0;
+            sd.bslot[q] = slot;
+        }
+        slot = __shfl(slot, 0);
+        if (has && mine != p) {  // X_near order, the nearest skipped
+            const int idx = lane - ((pm & ((1ull << lane) - 1ull)) ? 1 : 0);
+            SteerTask tk{};
+            tk.x = x;
+            tk.y = y;
+            tk.px = X[mine];
+            tk.py = Y[mine];
+            tk.pyaw = mq.yaw[row + mine];
+            tk.pnode = mine;
+            tasksB[slot + idx] = tk;
+        }
+    }
+}
+
+// settle literal-path verdicts of a wave's lanes (the measure-zero trim cases), one at a time
+__device__ __forceinline__ int star_settle(const SceneDev& sc, int st, bool act, double x, double y,
+                                           double yaw, double px, double py, double pyaw,
+                                           double* bx) {
+    const int lane = threadIdx.x & 63;
+    for (uint64_t lit = __ballot(act && st == kLiteral); lit; lit &= lit - 1) {
+        const int l = __builtin_ctzll(lit);
+        const int r = steer_collide_literal(sc, __shfl(x, l), __shfl(y, l), __shfl(yaw, l),
+                                            __shfl(px, l), __shfl(py, l), __shfl(pyaw, l), bx,
+                                            bx + kLiteralCap, bx + 2 * kLiteralCap);
+        if (lane == l) st = r;
+    }
+    return st;
+}
+
+__global__ __launch_bounds__(256) void star_insert_kernel(
+    StarDev sd, SceneDev sc, const int* __restrict__ statusA, const double* __restrict__ yawA,
+    const double* __restrict__ costA, const SteerTask* __restrict__ tasksB,
+    const int* __restrict__ statusB, const double* __restrict__ yawB,
+    const double* __restrict__ costB, SteerTask* __restrict__ tasksC,
+    double* __restrict__ lit_scratch, int* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    const MqDev& mq = sd.mq;
+    double* bx = lit_scratch + (size_t)gw * 3 * kLiteralCap;
+    for (int q = gw; q < mq.Q; q += nw) {
+        if (sd.pn[q] < 0) continue;
+        const int k = sd.nnear[q];
+        if (k < 0) continue;  // no insert this step (settled by star_knn)
+        const int p = sd.pn[q];
+        const int n = mq.n[q];
+        const size_t row = (size_t)q * mq.cap;
+        const double x = sd.px[q], y = sd.py[q];
+        const int mine = lane < k ? sd.near[(size_t)q * kStarKMax + lane] : -1;
+        const bool hasp = __ballot(lane < k && mine == p) != 0;
+        const int ncand = 1 + k - (hasp ? 1 : 0);  // the nearest, then X_near without it
+        const bool act = lane < ncand;
+        int node = p, st = kReject;
+        double yaw = 0.0, e = __builtin_inf();
+        if (lane == 0) {
+            st = statusA[q];
+            yaw = yawA[q];
+            e = costA[q];
+        } else if (act) {
+            const int t = sd.bslot[q] + lane - 1;
+            node = tasksB[t].pnode;
+            st = statusB[t];
+            yaw = yawB[t];
+            e = costB[t];
+        }
+        const double nx = mq.x[row + node], ny = mq.y[row + node], nyaw = mq.yaw[row + node];
+        st = star_settle(sc, st, act, x, y, yaw, nx, ny, nyaw, bx);
+        if (__ballot(act && st == kError)) {
+            if (lane == 0) atomicOr(err, 1);
+            continue;
+        }
+        const bool feas = act && star_feasible(st, e);
+        if (!__shfl((int)feas, 0)) {  // the gate failed on the literal path
+            if (lane == 0) {
+                sd.nnear[q] = -1;
+                mq.it[q] += 1;
+                mq.evals[q] += n;
+            }
+            continue;
+        }
+        // choose parent: the first strict minimum of cost(node) + edge cost in candidate order
+        double c = feas ? sd.cost[row + node] + e : __builtin_inf();
+        int bl = lane;
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) argmin_pair(c, bl, __shfl_xor(c, m), __shfl_xor(bl, m));
+        const int best = __shfl(node, bl);
+        const double yb = __shfl(yaw, bl), eb = __shfl(e, bl), cb = c;
+        if (lane == 0) {
+            const size_t o = row + n;
+            mq.x[o] = x;
+            mq.y[o] = y;
+            mq.yaw[o] = yb;
+            mq.parent[o] = best;
+            sd.cost[o] = cb;
+            sd.elen[o] = eb;
+            mq.n[q] = n + 1;
+            mq.it[q] += 1;
+            mq.evals[q] += n;
+            sd.cb[q] = cb;
+        }
+        // rewire tasks: X_near nodes other than the parent that could still get cheaper
+        // (cost(new) + e >= cost(new) >= cost(m) otherwise; costs only decrease)
+        const bool want = lane < k && mine != best && cb < sd.cost[row + (lane < k ? mine : 0)];
+        const uint64_t wm = __ballot(want);
+        const int cnt = __popcll(wm);
+        int slot = -1;
+        if (lane == 0) {
+            slot = cnt > 0 ? atomicAdd(&sd.stC->W, cnt) : -1;
+            sd.cslot[q] = slot;
+            sd.cmask[q] = wm;
+        }
+        slot = __shfl(slot, 0);
+        if (want) {
+            SteerTask tk{};
+            tk.x = mq.x[row + mine];
+            tk.y = mq.y[row + mine];
+            tk.px = x;
+            tk.py = y;
+            tk.pyaw = yb;
+            tk.pnode = n;  // the new node (the edge's parent)
+            tk.cyaw = mq.yaw[row + mine];
+            tk.own_yaw = 1;
+            tk.pad = mine;
+            tasksC[slot + __popcll(wm & ((1ull << lane) - 1ull))] = tk;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void star_rewire_kernel(
+    StarDev sd, SceneDev sc, const SteerTask* __restrict__ tasksC,
+    const int* __restrict__ statusC, const double* __restrict__ costC,
+    double* __restrict__ lit_scratch, int* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    const MqDev& mq = sd.mq;
+    double* bx = lit_scratch + (size_t)gw * 3 * kLiteralCap;
+    for (int q = gw; q < mq.Q; q += nw) {
+        if (sd.pn[q] < 0 || sd.nnear[q] < 0) continue;
+        const int slot = sd.cslot[q];
+        if (slot < 0) continue;
+        const int cnt = __popcll(sd.cmask[q]);
+        const bool act = lane < cnt;
+        SteerTask tk{};
+        int st = kReject;
+        double e = __builtin_inf();
+        if (act) {
+            tk = tasksC[slot + lane];
+            st = statusC[slot + lane];
+            e = costC[slot + lane];
+        }
+        st = star_settle(sc, st, act, tk.x, tk.y, tk.cyaw, tk.px, tk.py, tk.pyaw, bx);
+        if (__ballot(act && st == kError)) {
+            if (lane == 0) atomicOr(err, 1);
+            continue;
+        }
+        const uint64_t fm = __ballot(act && star_feasible(st, e));
+        const size_t row = (size_t)q * mq.cap;
+        const int n = mq.n[q];
+        const int nwn = n - 1;  // the node star_insert appended
+        const double cb = sd.cb[q];
+        double* __restrict__ cost = sd.cost + row;
+        double* __restrict__ elen = sd.elen + row;
+        int* __restrict__ par = mq.parent + row;
+        int* __restrict__ mark = sd.mark + row;
+        int s = sd.stamp[q];
+        int64_t rw = 0;
+        for (uint64_t f = fm; f; f &= f - 1) {  // X_near order
+            const int i = __builtin_ctzll(f);
+            const int m = __shfl(tk.pad, i);
+            const double em = __shfl(e, i);
+            const double cn = cb + em;
+            if (!(cn < cost[m])) continue;
+            if (lane == 0) {
+                par[m] = nwn;
+                elen[m] = em;
+                cost[m] = cn;
+                mark[m] = s;
+            }
+            ++rw;
+            __threadfence();
+            // the subtree of m, level by level: a node's parent is final one pass earlier
+            for (;;) {
+                bool any = false;
+                for (int j = lane; j < n; j += 64) {
+                    const int pj = par[j];
+                    if (pj >= 0 && mark[pj] == s) {
+                        cost[j] = cost[pj] + elen[j];
+                        mark[j] = s + 1;
+                        any = true;
+                    }
+                }
+                __threadfence();
+                ++s;
+                if (!__ballot(any)) break;
+            }
+        }
+        if (lane == 0) {
+            sd.stamp[q] = s;
+            sd.rewires[q] += rw;
+        }
+    }
+}
+
+hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
+    const int Q = a.sd.mq.Q;
+    const int TB = Q * kStarKMax;  // task capacity of rounds B and C
+    const int qb = std::min((Q + 3) / 4, 4096);
+    const int knn_blocks = std::min((Q + kKnnWaves - 1) / kKnnWaves, 4096);
+    const int lit_blocks = std::min((Q + 3) / 4, kLiteralWaves / 4);
+    const int prepA = std::min((Q + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
+    const int prepB = std::min((TB + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
+    const int walkA = std::min((Q + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
+    const int walkB = std::min((TB + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
+    const int lds = a.sc.lds_bytes;
+    auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, int* status, double* yaw,
+                     double* cost) {
+        steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(st, a.sc, nullptr, nullptr, nullptr, nullptr,
+                                                      a.rec, a.pdbuf, yaw, t, cost);
+        if (lds > 0)
+            steer_walk_kernel<true><<<wb, kWalkThreads, walk_lds_bytes(lds), s>>>(
+                st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr);
+        else
+            steer_walk_kernel<false><<<wb, kWalkThreads, walk_lds_bytes(0), s>>>(
+                st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr);
+    };
+    for (int k = 0; k < steps; ++k) {
+        if (a.ev) (void)hipEventRecord(a.ev[2 * k], s);
+        star_sample_kernel<<<qb, 256, 0, s>>>(a.sd, a.sc.minx, a.sc.maxx, a.sc.miny, a.sc.maxy,
+                                              a.tA);
+        round(a.sd.stA, prepA, walkA, a.tA, a.sA, a.yA, a.cA);
+        star_knn_kernel<<<knn_blocks, 64 * kKnnWaves, 0, s>>>(a.sd, a.sA, a.cA, a.tB, a.err);
+        if (a.ev) (void)hipEventRecord(a.ev[2 * k + 1], s);
+        round(a.sd.stB, prepB, walkB, a.tB, a.sB, a.yB, a.cB);
+        star_insert_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sc, a.sA, a.yA, a.cA, a.tB, a.sB,
+                                                      a.yB, a.cB, a.tC, a.lit_scratch, a.err);
+        round(a.sd.stC, prepB, walkB, a.tC, a.sC, a.yC, a.cC);
+        star_rewire_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sc, a.tC, a.sC, a.cC,
+                                                      a.lit_scratch, a.err);
+    }
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void star_init_kernel(StarDev sd) {
+    const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= sd.mq.Q) return;
+    const size_t o = (size_t)q * sd.mq.cap;
+    sd.cost[o] = 0.0;
+    sd.elen[o] = 0.0;
+    sd.stamp[q] = 1;
+    sd.rewires[q] = 0;
+}
+
+hipError_t launch_star_init(hipStream_t s, const StarArgs& a, const double* starts) {
+    hipError_t e = launch_mq_init(s, a.sd.mq, starts);
+    if (e != hipSuccess) return e;
+    star_init_kernel<<<(a.sd.mq.Q + 255) / 256, 256, 0, s>>>(a.sd);
     return hipGetLastError();
 }
 

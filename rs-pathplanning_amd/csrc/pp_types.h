@@ -128,6 +128,9 @@ struct SteerTask {
     double x, y, px, py, pyaw;
     int pnode;
     int literal;  // 1 = take the literal (single-lane) path
+    double cyaw;  // own_yaw: the child keeps this heading (RRT* rewire: an existing node's pose)
+    int own_yaw;  //          instead of compute_yaw toward the parent (rrt.rs:267-271)
+    int pad;
 };
 
 // A window sample i < j that is strictly nearer to sample j than j's snapshot NN, with the
@@ -184,6 +187,35 @@ struct MqDev {
     const int64_t* target;  // [Q] iteration this pp_batch_extend call stops at
     double* nnd2;           // [Q * K] exact d2 of each task's snapshot nearest node
 };
+// RRT* batch (BASELINE config 5; build-defined, oracle/pp_oracle.c orc_star_extend, DESIGN.md
+// §3.7): Q independent RRT* trees in the MqDev rows (K = 1), one iteration per query and step in
+// three steer rounds — A: the nearest edge (the gate), B: the other choose-parent candidates
+// (X_near), C: the rewire edges X_near → new — each an explicit-task steer_prep / steer_walk pass
+// whose task count the previous kernel sets on the device.
+constexpr int kStarKMax = 63;  // neighbours per insert: with the nearest, <= 64 candidates (lanes)
+struct StarDev {
+    MqDev mq;            // trees, iteration counters, seeds, blocked roots, targets (K = 1)
+    double* cost;        // [Q * cap] node cost, cost(root) = 0, cost = cost(parent) + elen
+    double* elen;        // [Q * cap] Dubins cost of the node's edge to its parent
+    int* mark;           // [Q * cap] subtree propagation: level stamp of the node
+    int* stamp;          // [Q] next free level stamp
+    const int* ksched;   // [cap + 1] |X_near| of an insert into an n-node tree (orc_star_k)
+    double eta;          // Steer distance (0: the new node sits at the sample, Q5)
+    double* px;          // [Q] the new point of the current iteration (after Steer)
+    double* py;
+    int* pn;             // [Q] its nearest node; -1: the query is idle this step
+    int* near;           // [Q * kStarKMax] X_near in (d2, index) order
+    int* nnear;          // [Q] |X_near|; -1: no insert this step (gate rejected, idle)
+    int* bslot;          // [Q] first round-B task of the query (X_near without the nearest)
+    int* cslot;          // [Q] first round-C task; -1 none
+    uint64_t* cmask;     // [Q] X_near positions with a round-C task
+    double* cb;          // [Q] cost of the inserted node
+    int64_t* rewires;    // [Q] rewires so far
+    DevState* stA;       // W = Q (constant)
+    DevState* stB;       // W = round-B task count (reset by star_sample, counted by star_knn)
+    DevState* stC;       // W = round-C task count (counted by star_insert)
+};
+
 constexpr int kMqMaxK = 64;  // window limit per query (config 3's strong-scaling parallelism)
 constexpr int kMqAutoK = 16; // the automatic window's limit
 

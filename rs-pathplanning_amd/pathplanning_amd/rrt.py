@@ -439,3 +439,68 @@ class RRTBatch:
 
     def close(self):
         self.ctx.close()
+
+
+class RRTStarBatch:
+    """Independent k-nearest RRT* planners on one scene (BASELINE config 5), one RRT* iteration
+    of every query per lockstep step on one GPU.  Build-defined — the reference has no RRT*
+    (SURVEY.md §8f row 4): the crate's rand_point / exact NN / Node::new / verify_node / Dubins
+    steer (rrt.rs:139-175, 378-426; dubins.rs:401-428) around Karaman & Frazzoli's choose-parent
+    and rewire, edge cost = the crate's Dubins cost (dubins.rs:351-361).  ``k``: neighbours per
+    insert (0 = ceil(2e ln n), at most 63); ``eta``: Steer distance (0 = the node sits at the
+    sample, like the crate).  DESIGN.md §3.7; oracle: oracle/pp_oracle.c orc_star_extend."""
+
+    def __init__(self, starts, max_iter, step_size, space: Space, seeds, k: int = 0,
+                 eta: float = 0.0, device: int = 0, ctx: _ffi.Context | None = None):
+        self.ctx = ctx or _ffi.Context(device)
+        self.space = space
+        starts = np.ascontiguousarray(starts, dtype=np.float64).reshape(-1, 3)
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+        self.q = len(starts)
+        self.max_iter = int(max_iter)
+        space._upload(self.ctx)
+        _ffi.check(_ffi.lib().pp_star_new(
+            self.ctx.handle, self.q, starts.ctypes.data_as(C.POINTER(C.c_double)),
+            seeds.ctypes.data_as(C.POINTER(C.c_uint64)), self.max_iter, float(step_size), int(k),
+            float(eta)))
+
+    def extend(self, n_steps: int):
+        """n_steps lockstep steps; returns (iterations, nodes inserted, rewires) over the batch."""
+        it, acc, rw = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+        _ffi.check(_ffi.lib().pp_star_extend(self.ctx.handle, int(n_steps), C.byref(it),
+                                             C.byref(acc), C.byref(rw)))
+        return it.value, acc.value, rw.value
+
+    def state(self):
+        """(tree sizes int32[q], iterations, NN node-distance evals, rewires: int64[q] each)"""
+        n = np.zeros(self.q, dtype=np.int32)
+        it, ev, rw = (np.zeros(self.q, dtype=np.int64) for _ in range(3))
+        i64 = C.POINTER(C.c_int64)
+        _ffi.check(_ffi.lib().pp_star_state(self.ctx.handle, n.ctypes.data_as(C.POINTER(C.c_int32)),
+                                            it.ctypes.data_as(i64), ev.ctypes.data_as(i64),
+                                            rw.ctypes.data_as(i64)))
+        return n, it, ev, rw
+
+    def set_profiling(self, on: bool):
+        _ffi.check(_ffi.lib().pp_set_profiling(self.ctx.handle, int(bool(on))))
+
+    def stats(self) -> dict:
+        s = _ffi.StatsC()
+        _ffi.check(_ffi.lib().pp_rrt_get_stats(self.ctx.handle, C.byref(s)))
+        return s.as_dict()
+
+    def tree(self, query: int):
+        """(x, y, yaw, parent, cost) of one query's tree, root first."""
+        n = int(self.state()[0][query])
+        x, y, yaw, cost = np.zeros(n), np.zeros(n), np.zeros(n), np.zeros(n)
+        par = np.zeros(n, dtype=np.int32)
+        out = C.c_int64(0)
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        _ffi.check(_ffi.lib().pp_star_tree_export(
+            self.ctx.handle, int(query), x.ctypes.data_as(dp), y.ctypes.data_as(dp),
+            yaw.ctypes.data_as(dp), par.ctypes.data_as(ip), cost.ctypes.data_as(dp), n,
+            C.byref(out)))
+        return x, y, yaw, par, cost
+
+    def close(self):
+        self.ctx.close()

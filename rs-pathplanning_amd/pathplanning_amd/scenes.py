@@ -115,6 +115,18 @@ def field512(n_obstacles: int = 1024, seed: int = 1234, size: float = 512.0,
     }
 
 
+def config5_field() -> dict:
+    """BASELINE config 5 (RRT*, build-defined): 10240 discs, centres U(0, 2048), r ~ U(1, 4) from
+    stream 1234 (coverage ~7%: the crate's node-at-the-sample RRT accepts ~0.2% of long edges in
+    a denser 10k field, too few for rewiring to matter), R = 4.0, step 0.1; the RRT* queries use
+    Steer eta = 16."""
+    return field512(n_obstacles=10240, size=2048.0, r_lo=1.0, r_hi=4.0,
+                    start=(8.0, 8.0, 0.0), goal=(2040.0, 2040.0, math.pi / 2.0))
+
+
+CONFIG5_ETA = 16.0
+
+
 def query_endpoints(raw: dict, q: int, seed_base: int = 0):
     """Config 3: start/goal of query ``q`` drawn from free space by the seeded stream q.
     Rejection-samples points whose inflated-disc clearance is > 1.0; yaw U(-pi, pi)."""

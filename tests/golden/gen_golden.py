@@ -7,7 +7,7 @@ known configurations (examples/dubins/src/main.rs:131-164, benches/all.rs:8-42,1
 seeded random battery and the build's config-2 field.  The C oracle and the HIP path are checked
 against these files.  Re-run with:  python tests/golden/gen_golden.py  (--polygons: only the
 polygon-mode fixtures; transit.debug.json is a verbatim copy of the reference's example scene
-data, examples/rrt/transit.debug.json)
+data, examples/rrt/transit.debug.json; --star: only the RRT* fixtures, oracle/rrtstar_py.py)
 """
 from __future__ import annotations
 
@@ -129,6 +129,32 @@ def polygons_main():
           [(r["best_node"], r["best_length"]) for r in fin])
 
 
+def star_record(raw, start, seed, n_iter, k, eta):
+    """RRT* (BASELINE config 5, build-defined) by the pure-Python restatement
+    (oracle/rrtstar_py.py)."""
+    import rrtstar_py as S  # noqa: E402
+    from oracle import OracleScene  # noqa: E402  (scene arithmetic only)
+
+    sc = OracleScene.from_raw(raw).as_dict()
+    tree = S.new_tree(start)
+    log, rewires = S.star_extend(sc, tree, seed, 0, n_iter, k, eta)
+    return {"scene": raw["name"], "start": list(start), "seed": seed, "n_iter": n_iter, "k": k,
+            "eta": eta, "rewires": rewires, "log_nn": [a for a, _ in log],
+            "log_acc": [b for _, b in log], **tree}
+
+
+def star_main():
+    b6o = scenes.bench6_open()
+    recs = [star_record(b6o, b6o["start"], 0, 300, 0, 0.0),
+            star_record(scenes.bench6(), scenes.bench6()["start"], 1, 300, 8, 1.5)]
+    f5 = scenes.config5_field()
+    st, _, sd = scenes.config3_queries(f5, 3, 1)
+    recs.append(star_record(f5, tuple(st[0]), int(sd[0]), 250, 0, scenes.CONFIG5_ETA))
+    with open(os.path.join(HERE, "rrtstar.json"), "w") as f:
+        json.dump(recs, f)
+    print("rrt* trees:", [(r["scene"], len(r["x"]), r["rewires"]) for r in recs])
+
+
 def main():
     known = {k: dubins_record(v) for k, v in KNOWN.items()}
     with open(os.path.join(HERE, "dubins_known.json"), "w") as f:
@@ -161,6 +187,9 @@ def main():
 if __name__ == "__main__":
     if "--polygons" in sys.argv:
         polygons_main()
+    elif "--star" in sys.argv:
+        star_main()
     else:
         main()
         polygons_main()
+        star_main()
