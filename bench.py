@@ -31,12 +31,14 @@ BYTES_PER_EVAL = 8            # f32 x + f32 y of one SoA node
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=("config2", "config3", "config4", "polygons"),
+    ap.add_argument("--workload", choices=("config2", "config3", "config4", "polygons",
+                                           "config5"),
                     default="config2",
                     help="config2: one tree, K-candidate windows (default); config3: a batch of "
                          "independent queries sharded over the ranks; config4: config 2 with the "
                          "512x512 occupancy-grid collision; polygons: config 2 with its discs as "
-                         "create_circle polygons (polygon mode, SURVEY §8f row 3)")
+                         "create_circle polygons (polygon mode, SURVEY §8f row 3); config5: a batch of "
+                         "independent RRT* queries (k-nearest rewire) on a 10240-disc field")
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (config2: windows, default 20; config3: lockstep "
                          "iterations, default max_iter)")
@@ -240,6 +242,8 @@ def main():
     args = parse()
     if args.workload == "config3":
         return main_config3(args)
+    if args.workload == "config5":
+        return main_config5(args)
     if args.steps is None:
         args.steps = 20
     dist, world, rank, local = dist_setup(args)
@@ -467,6 +471,137 @@ def main_config3(args):
                       f"threads, {ta:.1f} s wall",
             "one_core": {"value": round(v, 2), "queries": nq, "iterations": n,
                          "seconds": round(t, 2)},
+        }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    batch.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_star(raw, starts, seeds, max_iter, eta, seconds):
+    """config 5's CPU baseline: the RRT* oracle (C, orc_star_extend) on the same queries — query
+    0 on one core in chunks of 100 iterations until seconds/3 (or max_iter), then `threads` whole
+    queries of the batch, each for that many iterations, one per host thread (wall clock)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (cpu_baseline leg: the oracle is the timed CPU port here)
+
+    sc = oracle.OracleScene.from_raw(raw)
+    tr = oracle.OracleStarTree(tuple(starts[0]), max_iter + 1)
+    done, t_used = 0, 0.0
+    while done < max_iter and t_used < seconds / 3.0:
+        n = min(100, max_iter - done)
+        t0 = time.perf_counter()
+        oracle.star_extend(sc, tr, int(seeds[0]), done, n, 0, eta)
+        t_used += time.perf_counter() - t0
+        done += n
+    threads = min(host_threads(), len(seeds))
+    t0 = time.perf_counter()
+    oracle.star_queries(sc, starts[:threads], seeds[:threads], done, 0, eta, threads)
+    t = time.perf_counter() - t0
+    return (done / t_used, done, t_used), (threads * done / t, threads * done, threads, t, done)
+
+
+def main_config5(args):
+    """BASELINE config 5 (stretch; build-defined RRT*): `queries` independent
+    k-nearest RRT* planners on a 10240-disc field (scenes.config5_field, Steer eta = 16, k =
+    ceil(2e ln n)), max_iter each, sharded contiguously over the ranks like config 3; a step = one
+    lockstep RRT* iteration of every query of the rank; one all_gather of records at the end."""
+    import torch
+
+    backend = "nccl" if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and
+                         torch.cuda.is_available()) else "gloo"
+    dist, world, rank, local = dist_setup(args, backend)
+    from pathplanning_amd import rrt, scenes
+
+    raw = scenes.config5_field()
+    eta = scenes.CONFIG5_ETA
+    space = rrt.Space.from_raw(raw)
+    a, b = shard(args.queries, world, rank)
+    starts, _, seeds = scenes.config3_queries(raw, a, b - a)
+    steps = args.max_iter if args.steps is None else args.steps
+
+    def fresh():
+        return rrt.RRTStarBatch(starts, args.max_iter, raw["step_size"], space, seeds, k=0,
+                                eta=eta, device=local)
+
+    batch = fresh()
+    batch.extend(args.warmup)  # untimed warmup on a throwaway run
+    batch.close()
+    batch = fresh()
+    barrier(dist)
+    t0 = time.perf_counter()
+    batch.extend(steps)
+    t_local = time.perf_counter() - t0
+    barrier(dist)
+    n, its, evals, rw = batch.state()
+    rec = np.stack([np.arange(a, b, dtype=np.int64), its.astype(np.int64), n.astype(np.int64)], 1)
+    allrec = gather_records(dist, rec, backend)
+    t_max = allreduce_max(dist, t_local)
+    iters_total = int(allrec[:, 1].sum())
+    rewires_total = int(allreduce_sum(dist, float(rw.sum())))
+    value = iters_total / t_max
+    # profiled pass (same workload): HIP events around star_sample (the exact NN) of every step
+    batch.close()
+    batch = fresh()
+    batch.set_profiling(True)
+    batch.extend(steps)
+    sp = batch.stats()
+    evals_p = batch.state()[2]
+    nn_ms = sp["nn_scan_ms"] / max(sp["nn_scan_launches"], 1)
+    evals_per_launch = float(evals_p.sum()) / max(sp["nn_scan_launches"], 1)
+    bytes_per_eval = 16  # f64 x + f64 y of one SoA row
+    achieved = evals_per_launch * bytes_per_eval / (nn_ms * 1e-3) / 1e9
+    line = {
+        "metric": "RRT* iterations/sec (SE(2) Dubins, k-nearest rewire, 10k obstacles)",
+        "value": round(value, 1),
+        "unit": "iterations/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * t_max / steps, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"config5 (stretch, build-defined RRT*): {args.queries} independent "
+                        f"queries on {raw['name']} (10240 discs r~U(1,4) on 2048^2), Steer eta "
+                        f"{eta}, k = ceil(2e ln n) <= 63, max_iter {args.max_iter}, sharded "
+                        f"contiguously over {world} rank(s)",
+            "queries": args.queries,
+            "queries_per_rank": b - a,
+            "parallelism": f"query-shard{world}",
+            "gather": f"all_gather of per-query records ({backend})",
+        },
+        "iterations_total": iters_total,
+        "nodes_total": int(allrec[:, 2].sum()),
+        "rewires_total": rewires_total,
+        "roofline": {
+            "kernel": "star_sample (exact f64 NN)",
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "avg_launch_ms": round(nn_ms, 5),
+            "evals_per_launch": int(evals_per_launch),
+            "bytes_per_eval": bytes_per_eval,
+            "measured": f"HIP events around star_sample, {sp['nn_scan_launches']} launches of "
+                        "the profiled pass that follows the timed region (same workload)",
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        (v, n1, t1), (va, na, th, ta, m) = cpu_baseline_star(raw, starts, seeds, args.max_iter,
+                                                             eta, args.cpu_seconds)
+        line["cpu_baseline"] = {
+            "value": round(va, 2), "unit": "iterations/s", "cores": th, "kind": "port",
+            "sample": f"the first {th} queries of the same batch, their first {m} RRT* "
+                      f"iterations each ({na} iterations), on {th} host threads, {ta:.1f} s wall",
+            "one_core": {"value": round(v, 2), "iterations": n1, "seconds": round(t1, 2)},
         }
     if rank == 0:
         print(json.dumps(line), flush=True)

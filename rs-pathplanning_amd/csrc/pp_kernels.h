@@ -107,7 +107,7 @@ struct StarArgs {
     double* pdbuf = nullptr;
     double* lit_scratch = nullptr;  // kLiteralWaves buffers
     int* err = nullptr;
-    hipEvent_t* ev = nullptr;  // optional: 2 per step, around star_sample + round A + star_knn
+    hipEvent_t* ev = nullptr;  // optional: 2 per step, around star_sample (the exact NN)
 };
 hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps);
 hipError_t launch_star_init(hipStream_t s, const StarArgs& a, const double* starts);

@@ -3226,9 +3226,9 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
         if (a.ev) (void)hipEventRecord(a.ev[2 * k], s);
         star_sample_kernel<<<qb, 256, 0, s>>>(a.sd, a.sc.minx, a.sc.maxx, a.sc.miny, a.sc.maxy,
                                               a.tA);
+        if (a.ev) (void)hipEventRecord(a.ev[2 * k + 1], s);
         round(a.sd.stA, prepA, walkA, a.tA, a.sA, a.yA, a.cA);
         star_knn_kernel<<<knn_blocks, 64 * kKnnWaves, 0, s>>>(a.sd, a.sA, a.cA, a.tB, a.err);
-        if (a.ev) (void)hipEventRecord(a.ev[2 * k + 1], s);
         round(a.sd.stB, prepB, walkB, a.tB, a.sB, a.yB, a.cB);
         star_insert_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sc, a.sA, a.yA, a.cA, a.tB, a.sB,
                                                       a.yB, a.cB, a.tC, a.lit_scratch, a.err);
