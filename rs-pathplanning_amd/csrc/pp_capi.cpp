@@ -189,7 +189,8 @@ struct pp_ctx {
     DBuf<double> sr_x, sr_y, sr_yaw, sr_cost, sr_elen, sr_px, sr_py, sr_cb;
     DBuf<int> sr_par, sr_n, sr_mark, sr_stamp, sr_ksched, sr_pn, sr_near, sr_nnear, sr_bslot,
         sr_cslot, sr_err;
-    DBuf<uint64_t> sr_cmask, sr_seed;
+    DBuf<uint64_t> sr_cmask, sr_bmask, sr_seed;
+    DBuf<int> lit_locks;  // literal scratch slot locks (api_lit_scratch), zeroed once
     DBuf<int64_t> sr_it, sr_evals, sr_target, sr_rew;
     DBuf<uint8_t> sr_blocked;
     bool sr_any_blocked = false;
@@ -476,6 +477,7 @@ MqArgs mq_args(pp_ctx* c) {
     a.status = c->mq_status.p;
     a.yaw = c->mq_yawbuf.p;
     a.lit_scratch = c->api_lit_scratch.p;
+    a.lit_locks = c->lit_locks.p;
     a.err = c->mq_err.p;
     return a;
 }
@@ -537,6 +539,9 @@ StarArgs star_args(pp_ctx* c) {
     d.bslot = c->sr_bslot.p;
     d.cslot = c->sr_cslot.p;
     d.cmask = c->sr_cmask.p;
+    d.bmask = c->sr_bmask.p;
+    d.curv = 1.0 / c->max_steer;
+    d.lit_locks = c->lit_locks.p;
     d.cb = c->sr_cb.p;
     d.rewires = c->sr_rew.p;
     d.stA = c->sr_state.p;
@@ -1421,6 +1426,10 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
     PP_HIP(ctx->mq_state.reserve(1));
     PP_HIP(ctx->mq_err.reserve(1));
     PP_HIP(ctx->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
+    if (!ctx->lit_locks.p) {
+        PP_HIP(ctx->lit_locks.reserve(kLiteralWaves));
+        PP_HIP(hipMemset(ctx->lit_locks.p, 0, kLiteralWaves * sizeof(int)));
+    }
     ctx->mq_Q = q;
     ctx->mq_cap = (int)cap64;
     ctx->mq_max_iter = max_iter;
@@ -1592,6 +1601,11 @@ int pp_star_new(pp_ctx* ctx, int q, const double* starts, const uint64_t* seeds,
     for (auto* b : {&ctx->sr_it, &ctx->sr_evals, &ctx->sr_target, &ctx->sr_rew}) PP_HIP(b->reserve(q));
     PP_HIP(ctx->sr_seed.reserve(q));
     PP_HIP(ctx->sr_cmask.reserve(q));
+    PP_HIP(ctx->sr_bmask.reserve(q));
+    if (!ctx->lit_locks.p) {
+        PP_HIP(ctx->lit_locks.reserve(kLiteralWaves));
+        PP_HIP(hipMemset(ctx->lit_locks.p, 0, kLiteralWaves * sizeof(int)));
+    }
     PP_HIP(ctx->sr_near.reserve(tb));
     PP_HIP(ctx->sr_tA.reserve(q));
     PP_HIP(ctx->sr_tB.reserve(tb));

@@ -86,6 +86,7 @@ struct MqArgs {
     int* status = nullptr;
     double* yaw = nullptr;
     double* lit_scratch = nullptr;  // kLiteralWaves buffers
+    int* lit_locks = nullptr;       // their slot locks (0 free)
     int* err = nullptr;
     hipEvent_t* ev = nullptr;  // optional: 2 per step, around mq_sample_nn
 };

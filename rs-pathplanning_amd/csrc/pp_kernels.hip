@@ -2639,6 +2639,29 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
     return hipGetLastError();
 }
 
+// A literal-path scratch buffer (3 x kLiteralCap doubles) from a pool of kLiteralWaves slots,
+// so kernels of any width can run the measure-zero literal path: lane 0 takes a free slot with
+// atomicCAS (0 free, 1 taken), spinning over the pool if every slot is held — a holder is a
+// running wave that releases after its bounded literal walk.  Called by all lanes.
+__device__ __forceinline__ int lit_acquire(int* locks, int hint) {
+    int slot = 0;
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0;; ++i) {
+            const int sl = (hint + i) % kLiteralWaves;
+            if (atomicCAS(&locks[sl], 0, 1) == 0) {
+                slot = sl;
+                break;
+            }
+        }
+    slot = __shfl(slot, 0);
+    __threadfence();
+    return slot;
+}
+__device__ __forceinline__ void lit_release(int* locks, int slot) {
+    __threadfence();
+    if ((threadIdx.x & 63) == 0) atomicExch(&locks[slot], 0);
+}
+
 // ------------------------------------------------- multi-query batch (config 3)
 //
 // One lockstep step advances every query by one plan_one extend iteration (rrt.rs:583-589):
@@ -2707,6 +2730,7 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
                                                         const int* __restrict__ status,
                                                         const double* __restrict__ yaw,
                                                         double* __restrict__ lit_scratch,
+                                                        int* __restrict__ lit_locks,
                                                         int* __restrict__ err) {
     // a wave serves 64 / K queries, K lanes each (lane = g * K + k: the window's iteration
     // it[q] + k of its g-th query; K a power of two <= 16).  Literal-path re-runs first (rare, the
@@ -2721,7 +2745,6 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
     const int K = mq.K, G = 64 / K;
     const int g = lane / K, k = lane - g * K, g0 = g * K;
     const uint64_t gmask = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << g0;
-    double* bx = lit_scratch + (size_t)gw * 3 * kLiteralCap;
     for (int base = gw * G; base < mq.Q; base += nw * G) {
         const int q = base + g;
         const bool in = q < mq.Q;
@@ -2736,13 +2759,19 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
         }
         const bool act = in && tk.pnode >= 0;
         if (act) d2nn = mq.nnd2[t];
-        for (uint64_t lit = __ballot(act && st == kLiteral); lit; lit &= lit - 1) {
-            const int l = __builtin_ctzll(lit);
-            const double x = __shfl(tk.x, l), y = __shfl(tk.y, l), w = __shfl(yw, l);
-            const double px = __shfl(tk.px, l), py = __shfl(tk.py, l), pw = __shfl(tk.pyaw, l);
-            const int r = steer_collide_literal(sc, x, y, w, px, py, pw, bx, bx + kLiteralCap,
-                                                bx + 2 * kLiteralCap);
-            if (lane == l) st = r;
+        if (uint64_t lit = __ballot(act && st == kLiteral)) {
+            const int slot = lit_acquire(lit_locks, gw);
+            double* bx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
+            for (; lit; lit &= lit - 1) {
+                const int l = __builtin_ctzll(lit);
+                const double x = __shfl(tk.x, l), y = __shfl(tk.y, l), w = __shfl(yw, l);
+                const double px = __shfl(tk.px, l), py = __shfl(tk.py, l);
+                const double pw = __shfl(tk.pyaw, l);
+                const int r = steer_collide_literal(sc, x, y, w, px, py, pw, bx, bx + kLiteralCap,
+                                                    bx + 2 * kLiteralCap);
+                if (lane == l) st = r;
+            }
+            lit_release(lit_locks, slot);
         }
         const bool blocked = in && mq.blocked && mq.blocked[q];
         const uint64_t accm = __ballot(act && st == kAccept && !blocked);
@@ -2813,7 +2842,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int nn_blocks = std::min((T + 3) / 4, 4096);
     const int prep_blocks = std::min((T + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
-    const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), kLiteralWaves / 4);
+    const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
     const int lds = a.sc.lds_bytes;
     for (int k = 0; k < steps; ++k) {
         if (a.ev) (void)hipEventRecord(a.ev[2 * k], s);
@@ -2831,7 +2860,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
                                                                  nullptr, a.status, nullptr,
                                                                  nullptr);
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
-                                                    a.lit_scratch, a.err);
+                                                    a.lit_scratch, a.lit_locks, a.err);
     }
     return hipGetLastError();
 }
@@ -2857,6 +2886,12 @@ constexpr int kKnnCache = 2048;  // d2 values cached per wave (LDS: 4 x 16 KB)
 
 __device__ __forceinline__ bool star_feasible(int status, double e) {
     return status == kAccept && e <= 1.7976931348623157e308;  // Some and verified (finite cost)
+}
+
+// exact lower bound of an edge's Dubins cost (normalised by the turn radius): the chord, with a
+// slack far above the rounding of both (prunes only what cannot win, so results are unchanged)
+__device__ __forceinline__ double star_chord_lb(double d2, double curv) {
+    return sqrt(d2) * curv * (1.0 - 1e-9) - 1e-9;
 }
 
 __global__ __launch_bounds__(256) void star_sample_kernel(StarDev sd, double minx, double maxx,
@@ -2987,17 +3022,26 @@ __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __
         }
         const bool has = lane < k;
         if (has) sd.near[(size_t)q * kStarKMax + lane] = mine;
-        const uint64_t pm = __ballot(has && mine == p);
-        const int cnt = k - (pm ? 1 : 0);
+        // candidates that could still beat the nearest's cost c0 (chord lower bound): the others
+        // can never be the first strict minimum, so they are not steered
+        const double c0 = sd.cost[row + p] + costA[q];
+        bool want = has && mine != p;
+        if (want) {
+            const double dx = x - X[mine], dy = y - Y[mine];
+            want = sd.cost[row + mine] + star_chord_lb(dx * dx + dy * dy, sd.curv) < c0;
+        }
+        const uint64_t bm = __ballot(want);
+        const int cnt = __popcll(bm);
         int slot = 0;
         if (lane == 0) {
             sd.nnear[q] = k;
+            sd.bmask[q] = bm;
             slot = cnt > 0 ? atomicAdd(&sd.stB->W, cnt) : 0;
             sd.bslot[q] = slot;
         }
         slot = __shfl(slot, 0);
-        if (has && mine != p) {  // X_near order, the nearest skipped
-            const int idx = lane - ((pm & ((1ull << lane) - 1ull)) ? 1 : 0);
+        if (want) {  // X_near order
+            const int idx = __popcll(bm & ((1ull << lane) - 1ull));
             SteerTask tk{};
             tk.x = x;
             tk.y = y;
@@ -3013,15 +3057,20 @@ __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __
 // settle literal-path verdicts of a wave's lanes (the measure-zero trim cases), one at a time
 __device__ __forceinline__ int star_settle(const SceneDev& sc, int st, bool act, double x, double y,
                                            double yaw, double px, double py, double pyaw,
-                                           double* bx) {
+                                           double* lit_scratch, int* locks, int hint) {
     const int lane = threadIdx.x & 63;
-    for (uint64_t lit = __ballot(act && st == kLiteral); lit; lit &= lit - 1) {
+    uint64_t lit = __ballot(act && st == kLiteral);
+    if (!lit) return st;
+    const int slot = lit_acquire(locks, hint);
+    double* bx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
+    for (; lit; lit &= lit - 1) {
         const int l = __builtin_ctzll(lit);
         const int r = steer_collide_literal(sc, __shfl(x, l), __shfl(y, l), __shfl(yaw, l),
                                             __shfl(px, l), __shfl(py, l), __shfl(pyaw, l), bx,
                                             bx + kLiteralCap, bx + 2 * kLiteralCap);
         if (lane == l) st = r;
     }
+    lit_release(locks, slot);
     return st;
 }
 
@@ -3035,7 +3084,6 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     const MqDev& mq = sd.mq;
-    double* bx = lit_scratch + (size_t)gw * 3 * kLiteralCap;
     for (int q = gw; q < mq.Q; q += nw) {
         if (sd.pn[q] < 0) continue;
         const int k = sd.nnear[q];
@@ -3045,8 +3093,8 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
         const size_t row = (size_t)q * mq.cap;
         const double x = sd.px[q], y = sd.py[q];
         const int mine = lane < k ? sd.near[(size_t)q * kStarKMax + lane] : -1;
-        const bool hasp = __ballot(lane < k && mine == p) != 0;
-        const int ncand = 1 + k - (hasp ? 1 : 0);  // the nearest, then X_near without it
+        // the nearest, then the X_near nodes star_knn steered (the pruned ones cannot win)
+        const int ncand = 1 + __popcll(sd.bmask[q]);
         const bool act = lane < ncand;
         int node = p, st = kReject;
         double yaw = 0.0, e = __builtin_inf();
@@ -3062,7 +3110,7 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
             e = costB[t];
         }
         const double nx = mq.x[row + node], ny = mq.y[row + node], nyaw = mq.yaw[row + node];
-        st = star_settle(sc, st, act, x, y, yaw, nx, ny, nyaw, bx);
+        st = star_settle(sc, st, act, x, y, yaw, nx, ny, nyaw, lit_scratch, sd.lit_locks, gw);
         if (__ballot(act && st == kError)) {
             if (lane == 0) atomicOr(err, 1);
             continue;
@@ -3098,7 +3146,11 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
         }
         // rewire tasks: X_near nodes other than the parent that could still get cheaper
         // (cost(new) + e >= cost(new) >= cost(m) otherwise; costs only decrease)
-        const bool want = lane < k && mine != best && cb < sd.cost[row + (lane < k ? mine : 0)];
+        bool want = lane < k && mine != best;
+        if (want) {  // chord lower bound of the rewire edge (prunes only what cannot rewire)
+            const double dx = x - mq.x[row + mine], dy = y - mq.y[row + mine];
+            want = cb + star_chord_lb(dx * dx + dy * dy, sd.curv) < sd.cost[row + mine];
+        }
         const uint64_t wm = __ballot(want);
         const int cnt = __popcll(wm);
         int slot = -1;
@@ -3132,7 +3184,6 @@ __global__ __launch_bounds__(256) void star_rewire_kernel(
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     const MqDev& mq = sd.mq;
-    double* bx = lit_scratch + (size_t)gw * 3 * kLiteralCap;
     for (int q = gw; q < mq.Q; q += nw) {
         if (sd.pn[q] < 0 || sd.nnear[q] < 0) continue;
         const int slot = sd.cslot[q];
@@ -3147,7 +3198,8 @@ __global__ __launch_bounds__(256) void star_rewire_kernel(
             st = statusC[slot + lane];
             e = costC[slot + lane];
         }
-        st = star_settle(sc, st, act, tk.x, tk.y, tk.cyaw, tk.px, tk.py, tk.pyaw, bx);
+        st = star_settle(sc, st, act, tk.x, tk.y, tk.cyaw, tk.px, tk.py, tk.pyaw, lit_scratch,
+                         sd.lit_locks, gw);
         if (__ballot(act && st == kError)) {
             if (lane == 0) atomicOr(err, 1);
             continue;
@@ -3205,7 +3257,7 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
     const int TB = Q * kStarKMax;  // task capacity of rounds B and C
     const int qb = std::min((Q + 3) / 4, 4096);
     const int knn_blocks = std::min((Q + kKnnWaves - 1) / kKnnWaves, 4096);
-    const int lit_blocks = std::min((Q + 3) / 4, kLiteralWaves / 4);
+    const int lit_blocks = std::min((Q + 3) / 4, 4096);  // literal scratch: slot locks
     const int prepA = std::min((Q + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int prepB = std::min((TB + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walkA = std::min((Q + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);

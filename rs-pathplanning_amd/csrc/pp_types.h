@@ -206,7 +206,10 @@ struct StarDev {
     int* pn;             // [Q] its nearest node; -1: the query is idle this step
     int* near;           // [Q * kStarKMax] X_near in (d2, index) order
     int* nnear;          // [Q] |X_near|; -1: no insert this step (gate rejected, idle)
-    int* bslot;          // [Q] first round-B task of the query (X_near without the nearest)
+    int* bslot;          // [Q] first round-B task of the query
+    uint64_t* bmask;     // [Q] X_near positions with a round-B task (not the nearest, not pruned)
+    double curv;         // 1 / turn radius: the chord lower bound of a Dubins cost
+    int* lit_locks;      // [kLiteralWaves] literal scratch slot locks (0 free)
     int* cslot;          // [Q] first round-C task; -1 none
     uint64_t* cmask;     // [Q] X_near positions with a round-C task
     double* cb;          // [Q] cost of the inserted node
