@@ -2888,6 +2888,30 @@ __device__ __forceinline__ bool star_feasible(int status, double e) {
     return status == kAccept && e <= 1.7976931348623157e308;  // Some and verified (finite cost)
 }
 
+// Bitonic sort of one (d, i) pair per lane across the wave, ascending in (d, i) lexicographic
+// order (lane r ends up with the r-th smallest): 21 compare-exchange stages over __shfl_xor.
+struct Kv {
+    double d;
+    int i;
+};
+__device__ __forceinline__ Kv bitonic64(double d, int lane, int i = 0) {
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            const double od = __shfl_xor(d, stride);
+            const int oi = __shfl_xor(i, stride);
+            const bool other_less = od < d || (od == d && oi < i);
+            const bool keep_min = ((lane & stride) == 0) == ((lane & size) == 0 || size == 64);
+            if (keep_min == other_less) {
+                d = od;
+                i = oi;
+            }
+        }
+    }
+    return Kv{d, i};
+}
+
 // exact lower bound of an edge's Dubins cost (normalised by the turn radius): the chord, with a
 // slack far above the rounding of both (prunes only what cannot win, so results are unchanged)
 __device__ __forceinline__ double star_chord_lb(double d2, double curv) {
@@ -2961,7 +2985,11 @@ __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __
                                                        SteerTask* __restrict__ tasksB,
                                                        int* __restrict__ err) {
     __shared__ double s_d2[kKnnWaves][kKnnCache];
+    __shared__ double s_cd[kKnnWaves][64];
+    __shared__ int s_ci[kKnnWaves][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double* cand_d = s_cd[wave];
+    int* cand_i = s_ci[wave];
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     const MqDev& mq = sd.mq;
@@ -2989,36 +3017,75 @@ __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __
         const double* __restrict__ Y = mq.y + row;
         const int k = sd.ksched[n];
         const bool cached = n <= kKnnCache;
-        if (cached)
+        int mine = -1;
+        bool done = false;
+        if (cached) {
+            double lmin = __builtin_inf();
+#pragma unroll 8
             for (int i = lane; i < n; i += 64) {
                 const double dx = x - X[i], dy = y - Y[i];
-                cache[i] = dx * dx + dy * dy;
+                const double d2 = dx * dx + dy * dy;
+                cache[i] = d2;
+                lmin = fmin(lmin, d2);
             }
-        // k rounds of the lexicographic (d2, index) successor of the previous winner
-        double pd = -1.0;
-        int pi = -1, mine = -1;
-        for (int r = 0; r < k; ++r) {
-            double bd = __builtin_inf();
-            int bi = 0x7fffffff;
-            for (int i = lane; i < n; i += 64) {
-                double d2;
-                if (cached) {
-                    d2 = cache[i];
-                } else {
-                    const double dx = x - X[i], dy = y - Y[i];
-                    d2 = dx * dx + dy * dy;
-                }
-                if ((d2 > pd || (d2 == pd && i > pi)) && d2 < bd) {
-                    bd = d2;
-                    bi = i;
-                }
-            }
+            // T = the k-th smallest lane minimum: k distinct nodes lie within it, so the k nearest
+            // are among the nodes with d2 <= T (usually k..2k of them)
+            const double T = readlane_f64(bitonic64(lmin, lane).d, k - 1);
+            int c = 0;
+            for (int i = lane; i < n; i += 64) c += cache[i] <= T;
+            int off = c;  // inclusive prefix over the lanes
 #pragma unroll
-            for (int m = 32; m > 0; m >>= 1)
-                argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
-            pd = bd;
-            pi = bi;
-            if (lane == r) mine = bi;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(off, o);
+                if (lane >= o) off += v;
+            }
+            const int C = __shfl(off, 63);
+            if (C <= 64) {  // gather them into one (d2, index) pair per lane and sort the wave
+                off -= c;
+                for (int i = lane; i < n; i += 64)
+                    if (cache[i] <= T) {
+                        cand_d[off] = cache[i];
+                        cand_i[off] = i;
+                        ++off;
+                    }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                Kv kv{__builtin_inf(), 0x7fffffff};
+                if (lane < C) kv = Kv{cand_d[lane], cand_i[lane]};
+                kv = bitonic64(kv.d, lane, kv.i);
+                mine = lane < k ? kv.i : -1;
+                done = true;
+                __builtin_amdgcn_wave_barrier();  // the list is reused by the next query
+            }
+        }
+        if (!done) {
+            // k rounds of the lexicographic (d2, index) successor of the previous winner
+            double pd = -1.0;
+            int pi = -1;
+            for (int r = 0; r < k; ++r) {
+                double bd = __builtin_inf();
+                int bi = 0x7fffffff;
+                for (int i = lane; i < n; i += 64) {
+                    double d2;
+                    if (cached) {
+                        d2 = cache[i];
+                    } else {
+                        const double dx = x - X[i], dy = y - Y[i];
+                        d2 = dx * dx + dy * dy;
+                    }
+                    if ((d2 > pd || (d2 == pd && i > pi)) && d2 < bd) {
+                        bd = d2;
+                        bi = i;
+                    }
+                }
+#pragma unroll
+                for (int m = 32; m > 0; m >>= 1)
+                    argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+                pd = bd;
+                pi = bi;
+                if (lane == r) mine = bi;
+            }
         }
         const bool has = lane < k;
         if (has) sd.near[(size_t)q * kStarKMax + lane] = mine;
