@@ -1385,8 +1385,9 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     for (int blk = blockIdx.x; blk * TPB < total; blk += gridDim.x) {
         const int t = blk * TPB + wave * TPW + lane / kPrepLanes;
         bool act = t < total;
-        int j = 0, own = 0;
+        int j = 0, own = 0, cull = 0;
         double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0, cyaw = 0.0;
+        double cbase = 0.0, climit = 0.0;
         if (act && tasks) {
             const SteerTask tk = tasks[t];
             act = tk.pnode >= 0;
@@ -1397,6 +1398,9 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
             pyaw = act ? tk.pyaw : 0.0;
             own = tk.own_yaw;
             cyaw = tk.cyaw;
+            cull = tk.cull;
+            cbase = tk.cbase;
+            climit = tk.climit;
         } else if (act) {
             window_task(t, W, wsx, wsy, snap_pose, cand, &j, &px, &py, &pyaw);
             x = wsx[j];
@@ -1541,6 +1545,8 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
             fb_dd = (L0 > 0.0) ? step : -step;
             fb_pd = fb_dd - 0.0;
         }
+        // RRT* cull: an edge whose cost cannot beat the limit is settled without its walk
+        if (act && cull && !(cbase + bc < climit)) state = kReject;
         if (t < total && r == 0) {  // idle batch tasks get a kReject record (act == false)
             PrepRec o;
             o.x = x;
@@ -3116,6 +3122,9 @@ __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __
             tk.py = Y[mine];
             tk.pyaw = mq.yaw[row + mine];
             tk.pnode = mine;
+            tk.cull = 1;  // only a candidate strictly cheaper than the nearest's can win
+            tk.cbase = sd.cost[row + mine];
+            tk.climit = c0;
             tasksB[slot + idx] = tk;
         }
     }
@@ -3237,7 +3246,10 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
             tk.pnode = n;  // the new node (the edge's parent)
             tk.cyaw = mq.yaw[row + mine];
             tk.own_yaw = 1;
-            tk.pad = mine;
+            tk.node = mine;
+            tk.cull = 1;  // only a strictly cheaper path through the new node matters
+            tk.cbase = cb;
+            tk.climit = sd.cost[row + mine];
             tasksC[slot + __popcll(wm & ((1ull << lane) - 1ull))] = tk;
         }
     }
@@ -3284,7 +3296,7 @@ __global__ __launch_bounds__(256) void star_rewire_kernel(
         int64_t rw = 0;
         for (uint64_t f = fm; f; f &= f - 1) {  // X_near order
             const int i = __builtin_ctzll(f);
-            const int m = __shfl(tk.pad, i);
+            const int m = __shfl(tk.node, i);
             const double em = __shfl(e, i);
             const double cn = cb + em;
             if (!(cn < cost[m])) continue;

@@ -129,7 +129,12 @@ struct SteerTask {
     int pnode;
     int literal;  // 1 = take the literal (single-lane) path
     double cyaw;  // own_yaw: the child keeps this heading (RRT* rewire: an existing node's pose)
-    int own_yaw;  //          instead of compute_yaw toward the parent (rrt.rs:267-271)
+                  //          instead of compute_yaw toward the parent (rrt.rs:267-271)
+    double cbase, climit;  // cull (RRT*): steer_prep settles the task as rejected, without a
+                           // walk, unless cbase + its Dubins cost < climit (it cannot matter)
+    int own_yaw;
+    int cull;
+    int node;  // RRT* rewire: the child's tree node
     int pad;
 };
 
