@@ -124,76 +124,59 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const int lane = threadIdx.x & 63;
     const float bxl = (float)bx0 - sc.cull_slack, bxh = (float)bx1 + sc.cull_slack;
     const float byl = (float)by0 - sc.cull_slack, byh = (float)by1 + sc.cull_slack;
-    // the items of all the bbox's cells as one flat list (64 cells at a time): lane l < cells
-    // reads cell l's range, a prefix sum numbers the items, and each lane then loads one item
-    // and its cull disc — three dependent loads per 64 items instead of three per cell
-    const int ncx = cx1 - cx0 + 1;
-    const int ncell = ncx * (cy1 - cy0 + 1);
-    for (int cb = 0; cb < ncell; cb += 64) {
-        const int nc = min(64, ncell - cb);
-        int k0 = 0, cnt = 0;
-        if (lane < nc) {
-            const int ci = cb + lane;
-            const int cell = (cy0 + ci / ncx) * sc.gnx + cx0 + ci % ncx;
-            k0 = goff[cell];
-            cnt = goff[cell + 1] - k0;
-        }
-        int incl = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(incl, o);
-            if (lane >= o) incl += v;
-        }
-        const int total = __shfl(incl, 63);
-        for (int base = 0; base < total; base += 64) {
-            const int j = base + lane;
-            int c = 0;  // the cell of flat item j: the cells whose prefix ends at or before j
-            for (int cc = 0; cc < nc - 1; ++cc) c += __builtin_amdgcn_readlane(incl, cc) <= j;
-            const int kk = __shfl(k0, c) + j - (__shfl(incl, c) - __shfl(cnt, c));
-            int dl = 0;
-            float4 Dl = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            bool ov = false;
-            if (j < total) {
-                dl = items[kk];
-                Dl = d4[dl];
-                ov = Dl.x + Dl.z >= bxl && Dl.x - Dl.z <= bxh && Dl.y + Dl.z >= byl &&
-                     Dl.y - Dl.z <= byh;
-            }
-            for (uint64_t m = __ballot(ov); m; m &= m - 1) {
-                const int src = (int)__builtin_ctzll(m);
-                const int d = __builtin_amdgcn_readlane(dl, src);
-                float4 D;
-                D.x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.x), src));
-                D.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.y), src));
-                D.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.z), src));
-                D.w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.w), src));
-#ifdef PP_STAMPS
-                if (ph) ph[1] += 1;
-#endif
-                const float dxf = D.x - axf, dyf = D.y - ayf, thr = D.z + Lf;
-                bool near = seg_valid && dxf * dxf + dyf * dyf <= thr * thr;
-                if (!__any(near)) continue;
-                if (!poly) {
-                    // f32 closest point of the segment to the disc centre, decisive outside a
-                    // band of +-eps around the radius (eps bounds the f32 rounding of the
-                    // coordinates, the radius and this arithmetic): only the band needs the
-                    // exact f64 test and its global loads
-                    float t = 0.0f;
-                    if (l2f > 0.0f)
-                        t = __builtin_fminf(__builtin_fmaxf((dxf * vxf + dyf * vyf) / l2f, 0.0f), 1.0f);
-                    const float ex = dxf - t * vxf, ey = dyf - t * vyf;
-                    const float e2 = ex * ex + ey * ey;
-                    const float eps = sc.cull_slack + 1.0e-4f * (1.0f + thr);
-                    const float lo = __builtin_fmaxf(D.w - eps, 0.0f), hi = D.w + eps;
-                    if (__any(near && e2 < lo * lo)) return true;  // surely within the disc
-                    near = near && e2 <= hi * hi;                  // else surely clear
-                    if (!__any(near)) continue;
+    for (int gy = cy0; gy <= cy1; ++gy) {
+        for (int gx = cx0; gx <= cx1; ++gx) {
+            const int cell = gy * sc.gnx + gx;
+            const int k0 = goff[cell], k1 = goff[cell + 1];
+            // the cell's items in parallel, one per lane: the cull disc against the chunk's bbox;
+            // the survivors are then tested against every lane's segment, one at a time
+            for (int kb = k0; kb < k1; kb += 64) {
+                const int kk = kb + lane;
+                int dl = 0;
+                float4 Dl = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                bool ov = false;
+                if (kk < k1) {
+                    dl = items[kk];
+                    Dl = d4[dl];
+                    ov = Dl.x + Dl.z >= bxl && Dl.x - Dl.z <= bxh && Dl.y + Dl.z >= byl &&
+                         Dl.y - Dl.z <= byh;
                 }
-                const bool hit =
-                    near && (poly ? seg_hits_edge(ax, ay, qx, qy, sc.ex0[d], sc.ey0[d], sc.ex1[d],
-                                                  sc.ey1[d], sc.h2)
-                                  : seg_hits_disc(ax, ay, qx, qy, dcx[d], dcy[d], dr2[d]));
-                if (__any(hit)) return true;
+                for (uint64_t m = __ballot(ov); m; m &= m - 1) {
+                    const int src = (int)__builtin_ctzll(m);
+                    const int d = __builtin_amdgcn_readlane(dl, src);
+                    float4 D;
+                    D.x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.x), src));
+                    D.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.y), src));
+                    D.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.z), src));
+                    D.w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.w), src));
+#ifdef PP_STAMPS
+                    if (ph) ph[1] += 1;
+#endif
+                    const float dxf = D.x - axf, dyf = D.y - ayf, thr = D.z + Lf;
+                    bool near = seg_valid && dxf * dxf + dyf * dyf <= thr * thr;
+                    if (!__any(near)) continue;
+                    if (!poly) {
+                        // f32 closest point of the segment to the disc centre, decisive outside
+                        // a band of +-eps around the radius (eps bounds the f32 rounding of the
+                        // coordinates, the radius and this arithmetic): only the band needs the
+                        // exact f64 test and its global loads
+                        float t = 0.0f;
+                        if (l2f > 0.0f)
+                            t = __builtin_fminf(__builtin_fmaxf((dxf * vxf + dyf * vyf) / l2f, 0.0f), 1.0f);
+                        const float ex = dxf - t * vxf, ey = dyf - t * vyf;
+                        const float e2 = ex * ex + ey * ey;
+                        const float eps = sc.cull_slack + 1.0e-4f * (1.0f + thr);
+                        const float lo = __builtin_fmaxf(D.w - eps, 0.0f), hi = D.w + eps;
+                        if (__any(near && e2 < lo * lo)) return true;  // surely within the disc
+                        near = near && e2 <= hi * hi;                  // else surely clear
+                        if (!__any(near)) continue;
+                    }
+                    const bool hit =
+                        near && (poly ? seg_hits_edge(ax, ay, qx, qy, sc.ex0[d], sc.ey0[d], sc.ex1[d],
+                                                      sc.ey1[d], sc.h2)
+                                      : seg_hits_disc(ax, ay, qx, qy, dcx[d], dcy[d], dr2[d]));
+                    if (__any(hit)) return true;
+                }
             }
         }
     }
