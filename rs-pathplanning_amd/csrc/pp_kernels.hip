@@ -1605,13 +1605,12 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
 template <bool kLds>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
                                         const double* __restrict__ pdv, double* __restrict__ gs,
-                                        unsigned long long* stw = nullptr,
-                                        int state_override = -1000) {
+                                        unsigned long long* stw = nullptr) {
 #ifndef PP_STAMPS_WALK
     (void)stw;
 #endif
     const int lane = threadIdx.x & 63;
-    const int state = state_override != -1000 ? state_override : p->state;
+    const int state = p->state;
     const double x = p->x, y = p->y, px = p->px, py = p->py;
     if (state == kPrepNone) {  // steer failed: polyline [(x, y), (px, py)] (rrt.rs:313)
         const bool has = lane < 2;
@@ -3151,43 +3150,12 @@ __device__ __forceinline__ int star_settle(const SceneDev& sc, int st, bool act,
     return st;
 }
 
-// Round B's deferral: per gated query, the kStarTopM cheapest choose-parent candidates (by
-// cost(node) + exact Dubins cost, candidate order on ties) are walked; the other candidates that
-// could still win get kDeferOff added to their prep record state, so the walk skips them.
-__global__ __launch_bounds__(256) void star_select_kernel(StarDev sd,
-                                                          const SteerTask* __restrict__ tasksB,
-                                                          const double* __restrict__ costB,
-                                                          PrepRec* __restrict__ rec) {
-    const int lane = threadIdx.x & 63;
-    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    const MqDev& mq = sd.mq;
-    for (int q = gw; q < mq.Q; q += nw) {
-        if (sd.pn[q] < 0 || sd.nnear[q] < 0) continue;
-        const int nb = __popcll(sd.bmask[q]);
-        if (nb <= kStarTopM) continue;
-        const size_t row = (size_t)q * mq.cap;
-        const int t = sd.bslot[q] + lane;
-        double c = __builtin_inf();
-        if (lane < nb && rec[t].state != kReject)  // not settled by the prep's cost cull
-            c = sd.cost[row + tasksB[t].pnode] + costB[t];
-        const Kv kv = bitonic64(c, lane, lane);
-        uint64_t top = (lane < kStarTopM && kv.d < __builtin_inf()) ? 1ull << kv.i : 0ull;
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) top |= __shfl_xor(top, m);
-        if (lane < nb && c < __builtin_inf() && !((top >> lane) & 1ull))
-            rec[t].state += kDeferOff;
-    }
-}
-
 __global__ __launch_bounds__(256) void star_insert_kernel(
     StarDev sd, SceneDev sc, const int* __restrict__ statusA, const double* __restrict__ yawA,
     const double* __restrict__ costA, const SteerTask* __restrict__ tasksB,
     const int* __restrict__ statusB, const double* __restrict__ yawB,
     const double* __restrict__ costB, SteerTask* __restrict__ tasksC,
-    const PrepRec* __restrict__ rec, const double* __restrict__ pdbuf,
     double* __restrict__ lit_scratch, int* __restrict__ err) {
-    __shared__ double s_gs[4][kGenSlots];  // walk_rec's generator slots (deferred candidates)
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
@@ -3204,7 +3172,7 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
         // the nearest, then the X_near nodes star_knn steered (the pruned ones cannot win)
         const int ncand = 1 + __popcll(sd.bmask[q]);
         const bool act = lane < ncand;
-        int node = p, st = kReject, tb = 0;
+        int node = p, st = kReject;
         double yaw = 0.0, e = __builtin_inf();
         if (lane == 0) {
             st = statusA[q];
@@ -3212,7 +3180,6 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
             e = costA[q];
         } else if (act) {
             const int t = sd.bslot[q] + lane - 1;
-            tb = t;
             node = tasksB[t].pnode;
             st = statusB[t];
             yaw = yawB[t];
@@ -3224,7 +3191,7 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
             if (lane == 0) atomicOr(err, 1);
             continue;
         }
-        bool feas = act && star_feasible(st, e);
+        const bool feas = act && star_feasible(st, e);
         if (!__shfl((int)feas, 0)) {  // the gate failed on the literal path
             if (lane == 0) {
                 sd.nnear[q] = -1;
@@ -3233,38 +3200,11 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
             }
             continue;
         }
-        // choose parent: the first strict minimum of cost(node) + edge cost in candidate order =
-        // the first feasible candidate in (cost, order) order; a deferred candidate met on the
-        // way is walked here (the nearest is feasible, so the search ends)
-        const double cand_c = sd.cost[row + node] + e;
-        bool open = act && (feas || st >= kDeferOff);
-        double c;
-        int bl;
-        for (;;) {
-            c = open ? cand_c : __builtin_inf();
-            bl = lane;
+        // choose parent: the first strict minimum of cost(node) + edge cost in candidate order
+        double c = feas ? sd.cost[row + node] + e : __builtin_inf();
+        int bl = lane;
 #pragma unroll
-            for (int m = 32; m > 0; m >>= 1)
-                argmin_pair(c, bl, __shfl_xor(c, m), __shfl_xor(bl, m));
-            const int sbl = __shfl(st, bl);
-            if (sbl < kDeferOff) break;  // a walked, feasible candidate
-            const int t = __shfl(tb, bl);
-            int s2 = walk_rec<false>(sc, rec + t, pdbuf + (size_t)t * kPdCap,
-                                     s_gs[threadIdx.x >> 6], nullptr, sbl - kDeferOff);
-            s2 = star_settle(sc, s2, lane == bl, x, y, yaw, nx, ny, nyaw, lit_scratch,
-                             sd.lit_locks, gw);
-            s2 = __shfl(s2, bl);
-            if (s2 == kError) break;
-            if (lane == bl) {
-                st = s2;
-                feas = star_feasible(st, e);
-                open = feas;
-            }
-        }
-        if (__shfl((int)(st == kError), bl)) {
-            if (lane == 0) atomicOr(err, 1);
-            continue;
-        }
+        for (int m = 32; m > 0; m >>= 1) argmin_pair(c, bl, __shfl_xor(c, m), __shfl_xor(bl, m));
         const int best = __shfl(node, bl);
         const double yb = __shfl(yaw, bl), eb = __shfl(e, bl), cb = c;
         if (lane == 0) {
@@ -3402,19 +3342,16 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
     const int walkA = std::min((Q + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
     const int walkB = std::min((TB + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
     const int lds = a.sc.lds_bytes;
-    auto walk = [&](DevState* st, int wb, int* status) {
+    auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, int* status, double* yaw,
+                     double* cost) {
+        steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(st, a.sc, nullptr, nullptr, nullptr, nullptr,
+                                                      a.rec, a.pdbuf, yaw, t, cost);
         if (lds > 0)
             steer_walk_kernel<true><<<wb, kWalkThreads, walk_lds_bytes(lds), s>>>(
                 st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr);
         else
             steer_walk_kernel<false><<<wb, kWalkThreads, walk_lds_bytes(0), s>>>(
                 st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr);
-    };
-    auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, int* status, double* yaw,
-                     double* cost) {
-        steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(st, a.sc, nullptr, nullptr, nullptr, nullptr,
-                                                      a.rec, a.pdbuf, yaw, t, cost);
-        walk(st, wb, status);
     };
     for (int k = 0; k < steps; ++k) {
         if (a.ev) (void)hipEventRecord(a.ev[2 * k], s);
@@ -3423,14 +3360,9 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
         if (a.ev) (void)hipEventRecord(a.ev[2 * k + 1], s);
         round(a.sd.stA, prepA, walkA, a.tA, a.sA, a.yA, a.cA);
         star_knn_kernel<<<knn_blocks, 64 * kKnnWaves, 0, s>>>(a.sd, a.sA, a.cA, a.tB, a.err);
-        steer_prep_kernel<<<prepB, kPrepThreads, 0, s>>>(a.sd.stB, a.sc, nullptr, nullptr,
-                                                         nullptr, nullptr, a.rec, a.pdbuf, a.yB,
-                                                         a.tB, a.cB);
-        star_select_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.tB, a.cB, a.rec);
-        walk(a.sd.stB, walkB, a.sB);
+        round(a.sd.stB, prepB, walkB, a.tB, a.sB, a.yB, a.cB);
         star_insert_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sc, a.sA, a.yA, a.cA, a.tB, a.sB,
-                                                      a.yB, a.cB, a.tC, a.rec, a.pdbuf,
-                                                      a.lit_scratch, a.err);
+                                                      a.yB, a.cB, a.tC, a.lit_scratch, a.err);
         round(a.sd.stC, prepB, walkB, a.tC, a.sC, a.yC, a.cC);
         star_rewire_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sc, a.tC, a.sC, a.cC,
                                                       a.lit_scratch, a.err);

@@ -165,11 +165,7 @@ struct PrepRec {
     int state, fb_seg;               // kPrepWalk / kPrepNone / kPrepFallback or a verdict; the
                                      // kPrepFallback walk's segment at point kPdCap
 };
-enum : int { kPrepWalk = -1, kPrepNone = 4, kPrepFallback = 5, kDeferOff = 16 };
-// kDeferOff (RRT* choose-parent): a candidate outside the kStarTopM cheapest is not walked by
-// its round (record state + kDeferOff, returned as its status); star_insert walks it, with the
-// original state, only if every cheaper candidate proves infeasible
-constexpr int kStarTopM = 6;
+enum : int { kPrepWalk = -1, kPrepNone = 4, kPrepFallback = 5 };
 
 // Multi-query batch (BASELINE config 3): Q independent trees, tree q in rows [q * cap, q * cap +
 // n[q]) of the SoA arrays, all advanced one extend iteration per lockstep step.
