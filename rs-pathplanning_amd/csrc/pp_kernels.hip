@@ -3340,8 +3340,11 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
     const int prepA = std::min((Q + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int prepB = std::min((TB + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walkA = std::min((Q + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
-    const int walkB = std::min((TB + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
     const int lds = a.sc.lds_bytes;
+    // a scene read from global memory (no LDS image) makes the walk latency-bound: fill every
+    // wave slot the walk's 48 VGPRs allow (4 workgroups of 8 waves per CU)
+    const int walk_cap = lds > 0 ? kWalkMaxWG : 1024;
+    const int walkB = std::min((TB + kWalkThreads / 64 - 1) / (kWalkThreads / 64), walk_cap);
     auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, int* status, double* yaw,
                      double* cost) {
         steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(st, a.sc, nullptr, nullptr, nullptr, nullptr,
