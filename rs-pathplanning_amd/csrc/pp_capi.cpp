@@ -178,7 +178,9 @@ struct pp_ctx {
     DBuf<double> mq_nnd2;         // [Q * kMqMaxK]
     DBuf<SteerTask> mq_tasks;
     DBuf<PrepRec> mq_rec;
-    DBuf<DevState> mq_state;
+    DBuf<DevState> mq_state;      // [2]: one per sub-batch (see mq_sub_args)
+    hipStream_t stream2 = nullptr;  // the second sub-batch's stream (created on first use)
+    hipEvent_t fork_ev = nullptr;
     std::vector<double> mq_goal;  // 3 per query (kept for the host; the batch path is extend only)
 
     // ---- RRT* query batch (BASELINE config 5, build-defined: DESIGN.md §3.7)
@@ -210,6 +212,8 @@ struct pp_ctx {
     ~pp_ctx() {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
+        if (fork_ev) (void)hipEventDestroy(fork_ev);
+        if (stream2) (void)hipStreamDestroy(stream2);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -480,6 +484,46 @@ MqArgs mq_args(pp_ctx* c) {
     a.lit_locks = c->lit_locks.p;
     a.err = c->mq_err.p;
     return a;
+}
+
+// Sub-batch s of 2 (queries [q0, q0 + qs)): a view of the batch with offset per-query pointers
+// and its own DevState, so the two halves run their lockstep steps on two streams and each
+// half's small kernels overlap the other's walk.  Results do not depend on the split: queries
+// are independent.
+int mq_split(int Q) { return Q / 2; }
+MqArgs mq_sub_args(pp_ctx* c, int sub) {
+    MqArgs a = mq_args(c);
+    const int Q = c->mq_Q, K = c->mq_K;
+    const int q0 = sub == 0 ? 0 : mq_split(Q);
+    const int qs = sub == 0 ? mq_split(Q) : Q - mq_split(Q);
+    const size_t r0 = (size_t)q0 * c->mq_cap, t0 = (size_t)q0 * K;
+    a.mq.Q = qs;
+    a.mq.x += r0;
+    a.mq.y += r0;
+    a.mq.yaw += r0;
+    a.mq.parent += r0;
+    a.mq.n += q0;
+    a.mq.it += q0;
+    a.mq.evals += q0;
+    a.mq.seed += q0;
+    if (a.mq.blocked) a.mq.blocked += q0;
+    a.mq.target += q0;
+    a.mq.nnd2 += t0;
+    a.st = c->mq_state.p + sub;
+    a.tasks += t0;
+    a.rec += t0;
+    a.pdbuf += t0 * kPdCap;
+    a.status += t0;
+    a.yaw += t0;
+    return a;
+}
+
+int mq_write_states(pp_ctx* c, hipStream_t st) {
+    DevState ds[2] = {};
+    ds[0].W = mq_split(c->mq_Q) * c->mq_K;
+    ds[1].W = (c->mq_Q - mq_split(c->mq_Q)) * c->mq_K;
+    PP_HIP(hipMemcpyAsync(c->mq_state.p, ds, sizeof ds, hipMemcpyHostToDevice, st));
+    return PP_OK;
 }
 
 // per-step task buffers of the batch: K slots per query
@@ -1423,7 +1467,7 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
     PP_HIP(ctx->mq_evals.reserve(q));
     PP_HIP(ctx->mq_seed.reserve(q));
     PP_HIP(ctx->mq_target.reserve(q));
-    PP_HIP(ctx->mq_state.reserve(1));
+    PP_HIP(ctx->mq_state.reserve(2));
     PP_HIP(ctx->mq_err.reserve(1));
     PP_HIP(ctx->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
     if (!ctx->lit_locks.p) {
@@ -1465,9 +1509,7 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
         ctx->mq_K = K;
     }
     if ((r = mq_reserve_tasks(ctx, q, ctx->mq_K))) return r;
-    DevState ds{};
-    ds.W = q * ctx->mq_K;
-    PP_HIP(hipMemcpyAsync(ctx->mq_state.p, &ds, sizeof(DevState), hipMemcpyHostToDevice, st));
+    if ((r = mq_write_states(ctx, st))) return r;
     PP_HIP(hipMemsetAsync(ctx->mq_err.p, 0, sizeof(int), st));
     PP_HIP(hipStreamSynchronize(st));
     ctx->has_batch = true;
@@ -1485,9 +1527,8 @@ int pp_batch_set_window(pp_ctx* ctx, int k) {
         int r = mq_reserve_tasks(ctx, ctx->mq_Q, k);
         if (r) return r;
         ctx->mq_K = k;
-        DevState ds{};
-        ds.W = ctx->mq_Q * k;
-        PP_HIP(hipMemcpy(ctx->mq_state.p, &ds, sizeof(DevState), hipMemcpyHostToDevice));
+        if ((r = mq_write_states(ctx, ctx->stream))) return r;
+        PP_HIP(hipStreamSynchronize(ctx->stream));
     }
     return PP_OK;
 }
@@ -1502,6 +1543,16 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
     MqArgs a = mq_args(ctx);
     const int K = ctx->mq_K, Q = ctx->mq_Q;
     PP_HIP(launch_mq_target(ctx->stream, a.mq, n_steps, ctx->mq_target.p));
+    // two sub-batches on two streams (not while profiling: the NN events time whole-batch
+    // launches)
+    const bool split = !ctx->prof && Q >= 256;
+    MqArgs sub[2] = {mq_sub_args(ctx, 0), mq_sub_args(ctx, 1)};
+    if (split) {
+        if (!ctx->stream2) PP_HIP(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+        if (!ctx->fork_ev) PP_HIP(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
+        PP_HIP(hipEventRecord(ctx->fork_ev, ctx->stream));
+        PP_HIP(hipStreamWaitEvent(ctx->stream2, ctx->fork_ev, 0));
+    }
     // every query advances n_steps iterations (to max_iter at most); a window advances up to K
     // of them, fewer when the in-order replay stops early, so the host tops the steps up until
     // every query has reached its target
@@ -1515,7 +1566,14 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
                 if ((r = ensure_events(ctx, 2 * (size_t)chunk))) return r;
                 a.ev = ctx->ev.data();
             }
-            PP_HIP(launch_mq_steps(ctx->stream, a, chunk));
+            if (split) {  // interleaved, so both streams always hold work
+                for (int k = 0; k < chunk; ++k) {
+                    PP_HIP(launch_mq_steps(ctx->stream, sub[0], 1));
+                    PP_HIP(launch_mq_steps(ctx->stream2, sub[1], 1));
+                }
+            } else {
+                PP_HIP(launch_mq_steps(ctx->stream, a, chunk));
+            }
             if (ctx->prof) {
                 PP_HIP(hipStreamSynchronize(ctx->stream));
                 for (int k = 0; k < chunk; ++k) {
@@ -1526,6 +1584,10 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
                 ctx->nn_scan_launches += chunk;
             }
             done += chunk;
+        }
+        if (split) {  // join: the host reads the whole batch's counters on the first stream
+            PP_HIP(hipEventRecord(ctx->fork_ev, ctx->stream2));
+            PP_HIP(hipStreamWaitEvent(ctx->stream, ctx->fork_ev, 0));
         }
         PP_HIP(hipMemcpyAsync(hit.data(), ctx->mq_it.p, Q * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
         PP_HIP(hipMemcpyAsync(htg.data(), ctx->mq_target.p, Q * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
