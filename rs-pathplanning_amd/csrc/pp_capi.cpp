@@ -178,7 +178,7 @@ struct pp_ctx {
     DBuf<double> mq_nnd2;         // [Q * kMqMaxK]
     DBuf<SteerTask> mq_tasks;
     DBuf<PrepRec> mq_rec;
-    DBuf<DevState> mq_state;      // [2]: one per sub-batch (see mq_sub_args)
+    DBuf<DevState> mq_state;      // [3]: the whole batch, then one per sub-batch (mq_sub_args)
     hipStream_t stream2 = nullptr;  // the second sub-batch's stream (created on first use)
     hipEvent_t fork_ev = nullptr;
     std::vector<double> mq_goal;  // 3 per query (kept for the host; the batch path is extend only)
@@ -509,7 +509,7 @@ MqArgs mq_sub_args(pp_ctx* c, int sub) {
     if (a.mq.blocked) a.mq.blocked += q0;
     a.mq.target += q0;
     a.mq.nnd2 += t0;
-    a.st = c->mq_state.p + sub;
+    a.st = c->mq_state.p + 1 + sub;
     a.tasks += t0;
     a.rec += t0;
     a.pdbuf += t0 * kPdCap;
@@ -519,9 +519,10 @@ MqArgs mq_sub_args(pp_ctx* c, int sub) {
 }
 
 int mq_write_states(pp_ctx* c, hipStream_t st) {
-    DevState ds[2] = {};
-    ds[0].W = mq_split(c->mq_Q) * c->mq_K;
-    ds[1].W = (c->mq_Q - mq_split(c->mq_Q)) * c->mq_K;
+    DevState ds[3] = {};
+    ds[0].W = c->mq_Q * c->mq_K;
+    ds[1].W = mq_split(c->mq_Q) * c->mq_K;
+    ds[2].W = (c->mq_Q - mq_split(c->mq_Q)) * c->mq_K;
     PP_HIP(hipMemcpyAsync(c->mq_state.p, ds, sizeof ds, hipMemcpyHostToDevice, st));
     return PP_OK;
 }
@@ -1467,7 +1468,7 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
     PP_HIP(ctx->mq_evals.reserve(q));
     PP_HIP(ctx->mq_seed.reserve(q));
     PP_HIP(ctx->mq_target.reserve(q));
-    PP_HIP(ctx->mq_state.reserve(2));
+    PP_HIP(ctx->mq_state.reserve(3));
     PP_HIP(ctx->mq_err.reserve(1));
     PP_HIP(ctx->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
     if (!ctx->lit_locks.p) {
