@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -179,7 +180,7 @@ struct pp_ctx {
     DBuf<SteerTask> mq_tasks;
     DBuf<PrepRec> mq_rec;
     DBuf<DevState> mq_state;      // [3]: the whole batch, then one per sub-batch (mq_sub_args)
-    hipStream_t stream2 = nullptr;  // the second sub-batch's stream (created on first use)
+    hipStream_t sub_stream[4] = {};  // sub-batch streams 1.. (0 is `stream`), created on first use
     hipEvent_t fork_ev = nullptr;
     std::vector<double> mq_goal;  // 3 per query (kept for the host; the batch path is extend only)
 
@@ -213,7 +214,8 @@ struct pp_ctx {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
-        if (stream2) (void)hipStreamDestroy(stream2);
+        for (auto& ss : sub_stream)
+            if (ss) (void)hipStreamDestroy(ss);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -486,18 +488,22 @@ MqArgs mq_args(pp_ctx* c) {
     return a;
 }
 
-// Sub-batch s of 2 (queries [q0, q0 + qs)): a view of the batch with offset per-query pointers
-// and its own DevState, so the two halves run their lockstep steps on two streams and each
-// half's small kernels overlap the other's walk.  Results do not depend on the split: queries
-// are independent.
-int mq_split(int Q) { return Q / 2; }
-MqArgs mq_sub_args(pp_ctx* c, int sub) {
+// Sub-batch s of nsub (queries [Q*s/nsub, Q*(s+1)/nsub)): a view of the batch with offset
+// per-query pointers and its own DevState, so the sub-batches run their lockstep steps on their
+// own streams and one's small kernels overlap another's walk.  Results do not depend on the
+// split: queries are independent.
+constexpr int kMaxSub = 4;
+int mq_nsub(int Q) {
+    int n = Q >= 256 ? 2 : 1;
+    if (const char* e = std::getenv("PP_BATCH_STREAMS")) n = std::max(1, std::min(kMaxSub, std::atoi(e)));
+    return std::min(n, std::max(Q, 1));
+}
+MqArgs mq_sub_args(pp_ctx* c, int sub, int nsub) {
     MqArgs a = mq_args(c);
     const int Q = c->mq_Q, K = c->mq_K;
-    const int q0 = sub == 0 ? 0 : mq_split(Q);
-    const int qs = sub == 0 ? mq_split(Q) : Q - mq_split(Q);
+    const int q0 = (int)((int64_t)Q * sub / nsub), q1 = (int)((int64_t)Q * (sub + 1) / nsub);
     const size_t r0 = (size_t)q0 * c->mq_cap, t0 = (size_t)q0 * K;
-    a.mq.Q = qs;
+    a.mq.Q = q1 - q0;
     a.mq.x += r0;
     a.mq.y += r0;
     a.mq.yaw += r0;
@@ -518,12 +524,15 @@ MqArgs mq_sub_args(pp_ctx* c, int sub) {
     return a;
 }
 
+// DevState 0: the whole batch; 1 + s: sub-batch s of mq_nsub
 int mq_write_states(pp_ctx* c, hipStream_t st) {
-    DevState ds[3] = {};
-    ds[0].W = c->mq_Q * c->mq_K;
-    ds[1].W = mq_split(c->mq_Q) * c->mq_K;
-    ds[2].W = (c->mq_Q - mq_split(c->mq_Q)) * c->mq_K;
+    DevState ds[1 + kMaxSub] = {};
+    const int Q = c->mq_Q, nsub = mq_nsub(Q);
+    ds[0].W = Q * c->mq_K;
+    for (int s = 0; s < nsub; ++s)
+        ds[1 + s].W = (int)((int64_t)Q * (s + 1) / nsub - (int64_t)Q * s / nsub) * c->mq_K;
     PP_HIP(hipMemcpyAsync(c->mq_state.p, ds, sizeof ds, hipMemcpyHostToDevice, st));
+    PP_HIP(hipStreamSynchronize(st));  // ds lives on this stack frame
     return PP_OK;
 }
 
@@ -1468,7 +1477,7 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
     PP_HIP(ctx->mq_evals.reserve(q));
     PP_HIP(ctx->mq_seed.reserve(q));
     PP_HIP(ctx->mq_target.reserve(q));
-    PP_HIP(ctx->mq_state.reserve(3));
+    PP_HIP(ctx->mq_state.reserve(1 + kMaxSub));
     PP_HIP(ctx->mq_err.reserve(1));
     PP_HIP(ctx->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
     if (!ctx->lit_locks.p) {
@@ -1544,15 +1553,23 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
     MqArgs a = mq_args(ctx);
     const int K = ctx->mq_K, Q = ctx->mq_Q;
     PP_HIP(launch_mq_target(ctx->stream, a.mq, n_steps, ctx->mq_target.p));
-    // two sub-batches on two streams (not while profiling: the NN events time whole-batch
+    // sub-batches on their own streams (not while profiling: the NN events time whole-batch
     // launches)
-    const bool split = !ctx->prof && Q >= 256;
-    MqArgs sub[2] = {mq_sub_args(ctx, 0), mq_sub_args(ctx, 1)};
-    if (split) {
-        if (!ctx->stream2) PP_HIP(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+    const int nsub = ctx->prof ? 1 : mq_nsub(Q);
+    MqArgs sub[kMaxSub];
+    hipStream_t sst[kMaxSub] = {ctx->stream};
+    for (int i = 0; i < nsub && nsub > 1; ++i) {
+        sub[i] = mq_sub_args(ctx, i, nsub);
+        if (i > 0) {
+            if (!ctx->sub_stream[i])
+                PP_HIP(hipStreamCreateWithFlags(&ctx->sub_stream[i], hipStreamNonBlocking));
+            sst[i] = ctx->sub_stream[i];
+        }
+    }
+    if (nsub > 1) {  // fork after the target kernel
         if (!ctx->fork_ev) PP_HIP(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
         PP_HIP(hipEventRecord(ctx->fork_ev, ctx->stream));
-        PP_HIP(hipStreamWaitEvent(ctx->stream2, ctx->fork_ev, 0));
+        for (int i = 1; i < nsub; ++i) PP_HIP(hipStreamWaitEvent(sst[i], ctx->fork_ev, 0));
     }
     // every query advances n_steps iterations (to max_iter at most); a window advances up to K
     // of them, fewer when the in-order replay stops early, so the host tops the steps up until
@@ -1567,11 +1584,9 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
                 if ((r = ensure_events(ctx, 2 * (size_t)chunk))) return r;
                 a.ev = ctx->ev.data();
             }
-            if (split) {  // interleaved, so both streams always hold work
-                for (int k = 0; k < chunk; ++k) {
-                    PP_HIP(launch_mq_steps(ctx->stream, sub[0], 1));
-                    PP_HIP(launch_mq_steps(ctx->stream2, sub[1], 1));
-                }
+            if (nsub > 1) {  // interleaved, so every stream always holds work
+                for (int k = 0; k < chunk; ++k)
+                    for (int i = 0; i < nsub; ++i) PP_HIP(launch_mq_steps(sst[i], sub[i], 1));
             } else {
                 PP_HIP(launch_mq_steps(ctx->stream, a, chunk));
             }
@@ -1586,8 +1601,8 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
             }
             done += chunk;
         }
-        if (split) {  // join: the host reads the whole batch's counters on the first stream
-            PP_HIP(hipEventRecord(ctx->fork_ev, ctx->stream2));
+        for (int i = 1; i < nsub; ++i) {  // join: the host reads the counters on `stream`
+            PP_HIP(hipEventRecord(ctx->fork_ev, sst[i]));
             PP_HIP(hipStreamWaitEvent(ctx->stream, ctx->fork_ev, 0));
         }
         PP_HIP(hipMemcpyAsync(hit.data(), ctx->mq_it.p, Q * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
