@@ -126,7 +126,10 @@ def timed_windows(p, n_windows, window):
 
 
 def auto_batch_window(q):
-    """pp_batch_new's automatic window: the largest power of two <= 16 with q * K <= 131072."""
+    """pp_batch_new's automatic window: 32 for at most 2048 queries, else the largest power of
+    two <= 16 with q * K <= 131072."""
+    if q <= 2048:
+        return 32
     k = 1
     while k < 16 and q * k * 2 <= 131072:
         k *= 2

@@ -178,8 +178,8 @@ int pp_rrt_plan(pp_ctx* ctx, int64_t n_iter, int32_t* best_node, double* best_le
  * the shared max_iter and step_size.  Replaces any previous batch of the context. */
 int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
                  const uint64_t* seeds, int64_t max_iter, double step_size);
-/* speculative iterations per query and step (a power of two <= 64; 0 = automatic: 16 while the
- * step holds at most 131072 tasks).  Results do not depend on it: every query's tree equals its one-at-a-time
+/* speculative iterations per query and step (a power of two <= 64; 0 = automatic: 32 for at most
+ * 2048 queries, else 16 while the step holds at most 131072 tasks).  Results do not depend on it: every query's tree equals its one-at-a-time
  * sequential run.  Applies to the current batch and the next ones. */
 int pp_batch_set_window(pp_ctx* ctx, int k);
 /* n_steps lockstep steps: every query runs one plan_one extend iteration (rrt.rs:583-589) per

@@ -197,7 +197,7 @@ struct pp_ctx {
     DBuf<int64_t> sr_it, sr_evals, sr_target, sr_rew;
     DBuf<uint8_t> sr_blocked;
     bool sr_any_blocked = false;
-    DBuf<DevState> sr_state;  // [3]: rounds A, B, C
+    DBuf<DevState> sr_state;  // [3 * (1 + kMaxSub)]: rounds A, B, C of the batch, then per sub-batch
     DBuf<SteerTask> sr_tA, sr_tB, sr_tC;
     DBuf<int> sr_sA, sr_sB, sr_sC;
     DBuf<double> sr_yA, sr_yB, sr_yC, sr_cA, sr_cB, sr_cC;
@@ -619,6 +619,60 @@ StarArgs star_args(pp_ctx* c) {
     a.pdbuf = c->sr_pdbuf.p;
     a.lit_scratch = c->api_lit_scratch.p;
     a.err = c->sr_err.p;
+    return a;
+}
+
+// Sub-batch s of nsub of the RRT* batch (as mq_sub_args): offset per-query pointers, its own
+// round states and task regions (rounds B / C: kStarKMax slots per query)
+StarArgs star_sub_args(pp_ctx* c, int sub, int nsub) {
+    StarArgs a = star_args(c);
+    const int Q = c->star_Q;
+    const int q0 = (int)((int64_t)Q * sub / nsub), q1 = (int)((int64_t)Q * (sub + 1) / nsub);
+    const size_t r0 = (size_t)q0 * c->star_cap, b0 = (size_t)q0 * kStarKMax;
+    StarDev& d = a.sd;
+    d.mq.Q = q1 - q0;
+    d.mq.x += r0;
+    d.mq.y += r0;
+    d.mq.yaw += r0;
+    d.mq.parent += r0;
+    d.mq.n += q0;
+    d.mq.it += q0;
+    d.mq.evals += q0;
+    d.mq.seed += q0;
+    if (d.mq.blocked) d.mq.blocked += q0;
+    d.mq.target += q0;
+    d.cost += r0;
+    d.elen += r0;
+    d.mark += r0;
+    d.stamp += q0;
+    d.px += q0;
+    d.py += q0;
+    d.pn += q0;
+    d.near += b0;
+    d.nnear += q0;
+    d.bslot += q0;
+    d.bmask += q0;
+    d.cslot += q0;
+    d.cmask += q0;
+    d.cb += q0;
+    d.rewires += q0;
+    d.stA = c->sr_state.p + 3 * (1 + sub);
+    d.stB = d.stA + 1;
+    d.stC = d.stA + 2;
+    a.tA += q0;
+    a.sA += q0;
+    a.yA += q0;
+    a.cA += q0;
+    a.tB += b0;
+    a.tC += b0;
+    a.sB += b0;
+    a.sC += b0;
+    a.yB += b0;
+    a.yC += b0;
+    a.cB += b0;
+    a.cC += b0;
+    a.rec += b0;
+    a.pdbuf += b0 * kPdCap;
     return a;
 }
 
@@ -1507,7 +1561,9 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
         PP_HIP(ctx->mq_blocked.reserve(q));
         PP_HIP(hipMemcpy(ctx->mq_blocked.p, blk.data(), q, hipMemcpyHostToDevice));
     }
-    // default window: 16 iterations per query and step while that stays under 131072 tasks (the
+    // default window: 32 for at most 2048 queries (a 1024-query shard: 176M it/s at 32 against
+    // 171M at 16 and 145M at 64, two streams); else 16 iterations per query and step while that
+    // stays under 131072 tasks (the
     // throughput saturates there on one GPU; longer windows are cut more often by their own
     // accepted samples — config 3 measured 219M it/s at K = 16 on the 8192-query batch and on a
     // 1024-query shard 143M at K = 16 against 111M at K = 64)
@@ -1516,6 +1572,7 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
     } else {
         int K = 1;
         while (K < kMqAutoK && (int64_t)q * (K * 2) <= 131072) K *= 2;
+        if (q <= 2048) K = 32;  // a small batch (a rank's shard) needs longer windows to fill the GPU
         ctx->mq_K = K;
     }
     if ((r = mq_reserve_tasks(ctx, q, ctx->mq_K))) return r;
@@ -1693,7 +1750,7 @@ int pp_star_new(pp_ctx* ctx, int q, const double* starts, const uint64_t* seeds,
     for (auto* b : {&ctx->sr_yB, &ctx->sr_yC, &ctx->sr_cB, &ctx->sr_cC}) PP_HIP(b->reserve(tb));
     PP_HIP(ctx->sr_rec.reserve(tb));
     PP_HIP(ctx->sr_pdbuf.reserve(tb * kPdCap));
-    PP_HIP(ctx->sr_state.reserve(3));
+    PP_HIP(ctx->sr_state.reserve(3 * (1 + kMaxSub)));
     PP_HIP(ctx->sr_err.reserve(1));
     PP_HIP(ctx->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
     ctx->star_Q = q;
@@ -1723,8 +1780,11 @@ int pp_star_new(pp_ctx* ctx, int q, const double* starts, const uint64_t* seeds,
     PP_HIP(hipMemcpyAsync(d_starts.p, starts, 3 * (size_t)q * sizeof(double), hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(ctx->sr_seed.p, seeds, q * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     PP_HIP(launch_star_init(st, star_args(ctx), d_starts.p));
-    DevState ds[3] = {};
-    ds[0].W = q;
+    DevState ds[3 * (1 + kMaxSub)] = {};
+    ds[0].W = q;  // round A of the whole batch; sub-batch s: 3 * (1 + s)
+    const int nsub = mq_nsub(q);
+    for (int sb = 0; sb < nsub; ++sb)
+        ds[3 * (1 + sb)].W = (int)((int64_t)q * (sb + 1) / nsub - (int64_t)q * sb / nsub);
     PP_HIP(hipMemcpyAsync(ctx->sr_state.p, ds, sizeof ds, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemsetAsync(ctx->sr_err.p, 0, sizeof(int), st));
     PP_HIP(hipStreamSynchronize(st));
@@ -1744,13 +1804,35 @@ int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t*
     StarArgs a = star_args(ctx);
     PP_HIP(launch_mq_target(ctx->stream, a.sd.mq, n_steps, ctx->sr_target.p));
     const int64_t steps = std::min<int64_t>(n_steps, ctx->star_max_iter);  // one iteration a step
+    // sub-batches on their own streams, as pp_batch_extend (one stream while profiling)
+    const int nsub = ctx->prof ? 1 : mq_nsub(ctx->star_Q);
+    StarArgs sub[kMaxSub];
+    hipStream_t sst[kMaxSub] = {ctx->stream};
+    for (int i = 0; i < nsub && nsub > 1; ++i) {
+        sub[i] = star_sub_args(ctx, i, nsub);
+        if (i > 0) {
+            if (!ctx->sub_stream[i])
+                PP_HIP(hipStreamCreateWithFlags(&ctx->sub_stream[i], hipStreamNonBlocking));
+            sst[i] = ctx->sub_stream[i];
+        }
+    }
+    if (nsub > 1) {  // fork after the target kernel
+        if (!ctx->fork_ev) PP_HIP(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
+        PP_HIP(hipEventRecord(ctx->fork_ev, ctx->stream));
+        for (int i = 1; i < nsub; ++i) PP_HIP(hipStreamWaitEvent(sst[i], ctx->fork_ev, 0));
+    }
     for (int64_t done = 0; done < steps;) {
         const int chunk = (int)std::min<int64_t>(steps - done, 256);
         if (ctx->prof) {
             if ((r = ensure_events(ctx, 2 * (size_t)chunk))) return r;
             a.ev = ctx->ev.data();
         }
-        PP_HIP(launch_star_steps(ctx->stream, a, chunk));
+        if (nsub > 1) {  // interleaved, so every stream always holds work
+            for (int k = 0; k < chunk; ++k)
+                for (int i = 0; i < nsub; ++i) PP_HIP(launch_star_steps(sst[i], sub[i], 1));
+        } else {
+            PP_HIP(launch_star_steps(ctx->stream, a, chunk));
+        }
         if (ctx->prof) {
             PP_HIP(hipStreamSynchronize(ctx->stream));
             for (int k = 0; k < chunk; ++k) {
@@ -1761,6 +1843,10 @@ int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t*
             ctx->nn_scan_launches += chunk;
         }
         done += chunk;
+    }
+    for (int i = 1; i < nsub; ++i) {  // join
+        PP_HIP(hipEventRecord(ctx->fork_ev, sst[i]));
+        PP_HIP(hipStreamWaitEvent(ctx->stream, ctx->fork_ev, 0));
     }
     int err = 0;
     PP_HIP(hipMemcpyAsync(&err, ctx->sr_err.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));

@@ -419,6 +419,24 @@ def test_batch_field512_matches_independent_oracle_runs(pkg, ctx, oracle_mod):
         _assert_same_tree(b.tree(q), exp)
 
 
+def test_batch_sub_batch_streams(pkg, ctx, oracle_mod):
+    """>= 256 queries run as two sub-batches on two streams: spot-checked queries of both halves
+    equal their oracle runs and the batch totals equal the oracle's"""
+    from pathplanning_amd import rrt, scenes
+
+    raw = scenes.bench6_open()
+    starts, goals, seeds = scenes.config3_queries(raw, 0, 300)
+    b = rrt.RRTBatch(starts, goals, 120, raw["step_size"], rrt.Space.from_raw(raw), seeds,
+                     ctx=ctx)
+    it, acc = b.extend(120)
+    n, its = b.state()
+    assert it == 300 * 120 and (its == 120).all()
+    for q in (0, 149, 150, 299):
+        exp = _oracle_query(oracle_mod, raw, starts[q], seeds[q], 120, 120)
+        _assert_same_tree(b.tree(q), exp)
+    assert acc == oracle_mod.queries(oracle_mod.OracleScene.from_raw(raw), starts, seeds, 120, 8)
+
+
 def test_batch_stops_at_max_iter_and_matches_bench6(pkg, ctx, oracle_mod):
     from pathplanning_amd import rrt, scenes
 

@@ -136,3 +136,23 @@ def test_star_errors(pkg, ctx):
         _batch(pkg, raw, [raw["start"]], [0], 10, 64, 0.0, ctx=ctx)  # k > 63
     with pytest.raises(_ffi.PPError):
         _batch(pkg, raw, [raw["start"]], [0], 10, 0, -1.0, ctx=ctx)  # eta < 0
+
+
+def test_star_sub_batch_streams(pkg, oracle_mod, ctx):
+    """>= 256 queries run as two sub-batches on two streams: every query still equals its own
+    oracle run (spot-checked across both halves) and the totals equal the oracle's"""
+    from pathplanning_amd import scenes
+
+    raw = scenes.bench6_open()
+    starts, _, seeds = scenes.config3_queries(raw, 0, 300)
+    b = _batch(pkg, raw, starts, seeds, 80, 0, 0.0, ctx=ctx)
+    b.extend(80)
+    n, it, _, rw = b.state()
+    assert (it == 80).all()
+    for q in (0, 1, 149, 150, 151, 298, 299):
+        exp, erw = _oracle(oracle_mod, raw, tuple(starts[q]), int(seeds[q]), 80, 0, 0.0)
+        _assert_same(b.tree(q), exp)
+        assert rw[q] == erw
+    acc, rws = oracle_mod.star_queries(oracle_mod.OracleScene.from_raw(raw), starts, seeds, 80, 0,
+                                       0.0, 8)
+    assert int(n.sum()) - 300 == acc and int(rw.sum()) == rws
