@@ -493,8 +493,11 @@ MqArgs mq_args(pp_ctx* c) {
 // own streams and one's small kernels overlap another's walk.  Results do not depend on the
 // split: queries are independent.
 constexpr int kMaxSub = 4;
-int mq_nsub(int Q) {
-    int n = Q >= 256 ? 2 : 1;
+// streams: 2 for the extend batch (2: 289M it/s at 8192 queries, 177M on a 1024-query shard; 3:
+// 291M / 160M; 4: 244M / 109M), 3 for RRT* (11 kernels a step: 16.4M / 4.5M against 15.0M / 4.2M
+// with 2; 4 streams collapse to 10.7M / 2.4M, the box runs 4 hardware queues per process)
+int mq_nsub(int Q, int dflt = 2) {
+    int n = Q >= 256 ? dflt : 1;
     if (const char* e = std::getenv("PP_BATCH_STREAMS")) n = std::max(1, std::min(kMaxSub, std::atoi(e)));
     return std::min(n, std::max(Q, 1));
 }
@@ -1782,7 +1785,7 @@ int pp_star_new(pp_ctx* ctx, int q, const double* starts, const uint64_t* seeds,
     PP_HIP(launch_star_init(st, star_args(ctx), d_starts.p));
     DevState ds[3 * (1 + kMaxSub)] = {};
     ds[0].W = q;  // round A of the whole batch; sub-batch s: 3 * (1 + s)
-    const int nsub = mq_nsub(q);
+    const int nsub = mq_nsub(q, 3);
     for (int sb = 0; sb < nsub; ++sb)
         ds[3 * (1 + sb)].W = (int)((int64_t)q * (sb + 1) / nsub - (int64_t)q * sb / nsub);
     PP_HIP(hipMemcpyAsync(ctx->sr_state.p, ds, sizeof ds, hipMemcpyHostToDevice, st));
@@ -1805,7 +1808,7 @@ int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t*
     PP_HIP(launch_mq_target(ctx->stream, a.sd.mq, n_steps, ctx->sr_target.p));
     const int64_t steps = std::min<int64_t>(n_steps, ctx->star_max_iter);  // one iteration a step
     // sub-batches on their own streams, as pp_batch_extend (one stream while profiling)
-    const int nsub = ctx->prof ? 1 : mq_nsub(ctx->star_Q);
+    const int nsub = ctx->prof ? 1 : mq_nsub(ctx->star_Q, 3);
     StarArgs sub[kMaxSub];
     hipStream_t sst[kMaxSub] = {ctx->stream};
     for (int i = 0; i < nsub && nsub > 1; ++i) {
