@@ -221,6 +221,16 @@ def load_traffic():
         return json.load(f).get("hbm_bytes_per_launch")
 
 
+def load_batch_traffic(workload):
+    """HBM bytes per whole-batch NN launch of config 3 / 5 from the committed rocprofv3 PMC
+    summary (scripts/traffic_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", "batch_nn_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get(workload, {}).get("hbm_bytes_per_launch")
+
+
 def gather_records(dist, rec, backend):
     """The config-3 result gather: every rank's per-query records to every rank (one
     all_gather; RCCL over xGMI when the backend is nccl).  rec: int64 [q_rank, 3]."""
@@ -455,7 +465,7 @@ def main_config3(args):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": load_batch_traffic("config3") if args.queries == 8192 else None,
             "avg_launch_ms": round(nn_ms, 5),
             "evals_per_launch": int(evals_per_launch),
             "bytes_per_eval": bytes_per_eval,
@@ -588,7 +598,7 @@ def main_config5(args):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": load_batch_traffic("config5") if args.queries == 8192 else None,
             "avg_launch_ms": round(nn_ms, 5),
             "evals_per_launch": int(evals_per_launch),
             "bytes_per_eval": bytes_per_eval,
