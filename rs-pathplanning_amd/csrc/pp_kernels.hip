@@ -2687,17 +2687,19 @@ __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    const int K = mq.K;
-    for (int t = gw; t < mq.Q * K; t += nw) {
-        const int q = t / K, k = t - q * K;
+    // one wave per query: lane l serves window slot k = l % K over node group g = l / K (nodes
+    // i = g mod 64/K), so every node row is loaded once per wave, not once per slot
+    const int K = mq.K, G = 64 / K;
+    const int k = lane & (K - 1), g = lane / K;
+    for (int q = gw; q < mq.Q; q += nw) {
         const int64_t it = mq.it[q] + k;
-        if (it >= mq.target[q]) {
-            if (lane == 0) tasks[t].pnode = -1;
-            continue;
-        }
+        const bool live = it < mq.target[q];
         const uint64_t seed = mq.seed[q];
-        const double x = gen_range(seed, 2 * (uint64_t)it, minx, maxx);
-        const double y = gen_range(seed, 2 * (uint64_t)it + 1, miny, maxy);
+        double x = 0.0, y = 0.0;
+        if (live) {
+            x = gen_range(seed, 2 * (uint64_t)it, minx, maxx);
+            y = gen_range(seed, 2 * (uint64_t)it + 1, miny, maxy);
+        }
         const int n = mq.n[q];
         const size_t row = (size_t)q * mq.cap;
         const double* __restrict__ X = mq.x + row;
@@ -2705,7 +2707,7 @@ __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx
         double bd = __builtin_inf();
         int bi = 0x7fffffff;
 #pragma unroll 4
-        for (int i = lane; i < n; i += 64) {
+        for (int i = g; i < n; i += G) {
             const double dx = x - X[i], dy = y - Y[i];
             const double d2 = dx * dx + dy * dy;
             if (d2 < bd) {
@@ -2713,11 +2715,16 @@ __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx
                 bi = i;
             }
         }
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
-        if (lane == 0) {
-            tasks[t] = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, 0};
-            mq.nnd2[t] = bd;
+        for (int m = K; m < 64; m <<= 1)  // the G lanes of slot k
+            argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+        if (g == 0) {
+            const int t = q * K + k;
+            if (!live) {
+                tasks[t].pnode = -1;
+            } else {
+                tasks[t] = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, 0};
+                mq.nnd2[t] = bd;
+            }
         }
     }
 }
@@ -2845,7 +2852,7 @@ hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int Q = a.mq.Q;
     const int T = Q * a.mq.K;  // tasks per step
-    const int nn_blocks = std::min((T + 3) / 4, 4096);
+    const int nn_blocks = std::min((Q + 3) / 4, 4096);  // one wave per query
     const int prep_blocks = std::min((T + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
     const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
