@@ -199,6 +199,7 @@ struct pp_ctx {
     bool sr_any_blocked = false;
     DBuf<DevState> sr_state;  // [3 * (1 + kMaxSub)]: rounds A, B, C of the batch, then per sub-batch
     DBuf<SteerTask> sr_tA, sr_tB, sr_tC;
+    DBuf<StarTaskExt> sr_eB, sr_eC;
     DBuf<int> sr_sA, sr_sB, sr_sC;
     DBuf<double> sr_yA, sr_yB, sr_yC, sr_cA, sr_cB, sr_cC;
     DBuf<PrepRec> sr_rec;
@@ -609,6 +610,8 @@ StarArgs star_args(pp_ctx* c) {
     a.tA = c->sr_tA.p;
     a.tB = c->sr_tB.p;
     a.tC = c->sr_tC.p;
+    a.eB = c->sr_eB.p;
+    a.eC = c->sr_eC.p;
     a.sA = c->sr_sA.p;
     a.sB = c->sr_sB.p;
     a.sC = c->sr_sC.p;
@@ -668,6 +671,8 @@ StarArgs star_sub_args(pp_ctx* c, int sub, int nsub) {
     a.cA += q0;
     a.tB += b0;
     a.tC += b0;
+    a.eB += b0;
+    a.eC += b0;
     a.sB += b0;
     a.sC += b0;
     a.yB += b0;
@@ -1748,6 +1753,8 @@ int pp_star_new(pp_ctx* ctx, int q, const double* starts, const uint64_t* seeds,
     PP_HIP(ctx->sr_tA.reserve(q));
     PP_HIP(ctx->sr_tB.reserve(tb));
     PP_HIP(ctx->sr_tC.reserve(tb));
+    PP_HIP(ctx->sr_eB.reserve(tb));
+    PP_HIP(ctx->sr_eC.reserve(tb));
     PP_HIP(ctx->sr_sB.reserve(tb));
     PP_HIP(ctx->sr_sC.reserve(tb));
     for (auto* b : {&ctx->sr_yB, &ctx->sr_yC, &ctx->sr_cB, &ctx->sr_cC}) PP_HIP(b->reserve(tb));

@@ -101,6 +101,7 @@ struct StarArgs {
     StarDev sd{};
     SceneDev sc{};
     SteerTask *tA = nullptr, *tB = nullptr, *tC = nullptr;
+    StarTaskExt *eB = nullptr, *eC = nullptr;  // rounds B / C: cull limits, rewire child poses
     int *sA = nullptr, *sB = nullptr, *sC = nullptr;        // verdicts
     double *yA = nullptr, *yB = nullptr, *yC = nullptr;     // child yaw of each task
     double *cA = nullptr, *cB = nullptr, *cC = nullptr;     // Dubins cost of each task

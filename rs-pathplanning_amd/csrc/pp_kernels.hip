@@ -1371,7 +1371,7 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     const double* __restrict__ wsy, const double* __restrict__ snap_pose,
     CandEntry* __restrict__ cand, PrepRec* __restrict__ rec, double* __restrict__ pdbuf,
     double* __restrict__ snap_yaw, const SteerTask* __restrict__ tasks,
-    double* __restrict__ cost_out = nullptr) {
+    double* __restrict__ cost_out = nullptr, const StarTaskExt* __restrict__ ext = nullptr) {
     // tasks != nullptr: explicit (child, parent pose) tasks [0, W) (multi-query batch); a task
     // with pnode < 0 is idle; own_yaw: the child keeps its heading cyaw (RRT* rewire edges)
     const int W = st->W;
@@ -1396,11 +1396,14 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
             px = act ? tk.px : 1.0;
             py = act ? tk.py : 0.0;
             pyaw = act ? tk.pyaw : 0.0;
-            own = tk.own_yaw;
-            cyaw = tk.cyaw;
-            cull = tk.cull;
-            cbase = tk.cbase;
-            climit = tk.climit;
+            if (ext) {
+                const StarTaskExt ex = ext[t];
+                own = ex.own_yaw;
+                cyaw = ex.cyaw;
+                cull = ex.cull;
+                cbase = ex.cbase;
+                climit = ex.climit;
+            }
         } else if (act) {
             window_task(t, W, wsx, wsy, snap_pose, cand, &j, &px, &py, &pyaw);
             x = wsx[j];
@@ -2996,6 +2999,7 @@ __global__ __launch_bounds__(256) void star_sample_kernel(StarDev sd, double min
 __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __restrict__ statusA,
                                                        const double* __restrict__ costA,
                                                        SteerTask* __restrict__ tasksB,
+                                                       StarTaskExt* __restrict__ extB,
                                                        int* __restrict__ err) {
     __shared__ double s_d2[kKnnWaves][kKnnCache];
     __shared__ double s_cd[kKnnWaves][64];
@@ -3129,10 +3133,12 @@ __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __
             tk.py = Y[mine];
             tk.pyaw = mq.yaw[row + mine];
             tk.pnode = mine;
-            tk.cull = 1;  // only a candidate strictly cheaper than the nearest's can win
-            tk.cbase = sd.cost[row + mine];
-            tk.climit = c0;
             tasksB[slot + idx] = tk;
+            StarTaskExt ex{};
+            ex.cull = 1;  // only a candidate strictly cheaper than the nearest's can win
+            ex.cbase = sd.cost[row + mine];
+            ex.climit = c0;
+            extB[slot + idx] = ex;
         }
     }
 }
@@ -3162,7 +3168,7 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
     const double* __restrict__ costA, const SteerTask* __restrict__ tasksB,
     const int* __restrict__ statusB, const double* __restrict__ yawB,
     const double* __restrict__ costB, SteerTask* __restrict__ tasksC,
-    double* __restrict__ lit_scratch, int* __restrict__ err) {
+    StarTaskExt* __restrict__ extC, double* __restrict__ lit_scratch, int* __restrict__ err) {
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
@@ -3251,21 +3257,24 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
             tk.py = y;
             tk.pyaw = yb;
             tk.pnode = n;  // the new node (the edge's parent)
-            tk.cyaw = mq.yaw[row + mine];
-            tk.own_yaw = 1;
-            tk.node = mine;
-            tk.cull = 1;  // only a strictly cheaper path through the new node matters
-            tk.cbase = cb;
-            tk.climit = sd.cost[row + mine];
-            tasksC[slot + __popcll(wm & ((1ull << lane) - 1ull))] = tk;
+            const int tc = slot + __popcll(wm & ((1ull << lane) - 1ull));
+            tasksC[tc] = tk;
+            StarTaskExt ex{};
+            ex.cyaw = mq.yaw[row + mine];
+            ex.own_yaw = 1;
+            ex.node = mine;
+            ex.cull = 1;  // only a strictly cheaper path through the new node matters
+            ex.cbase = cb;
+            ex.climit = sd.cost[row + mine];
+            extC[tc] = ex;
         }
     }
 }
 
 __global__ __launch_bounds__(256) void star_rewire_kernel(
     StarDev sd, SceneDev sc, const SteerTask* __restrict__ tasksC,
-    const int* __restrict__ statusC, const double* __restrict__ costC,
-    double* __restrict__ lit_scratch, int* __restrict__ err) {
+    const StarTaskExt* __restrict__ extC, const int* __restrict__ statusC,
+    const double* __restrict__ costC, double* __restrict__ lit_scratch, int* __restrict__ err) {
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
@@ -3277,14 +3286,16 @@ __global__ __launch_bounds__(256) void star_rewire_kernel(
         const int cnt = __popcll(sd.cmask[q]);
         const bool act = lane < cnt;
         SteerTask tk{};
+        StarTaskExt ex{};
         int st = kReject;
         double e = __builtin_inf();
         if (act) {
             tk = tasksC[slot + lane];
+            ex = extC[slot + lane];
             st = statusC[slot + lane];
             e = costC[slot + lane];
         }
-        st = star_settle(sc, st, act, tk.x, tk.y, tk.cyaw, tk.px, tk.py, tk.pyaw, lit_scratch,
+        st = star_settle(sc, st, act, tk.x, tk.y, ex.cyaw, tk.px, tk.py, tk.pyaw, lit_scratch,
                          sd.lit_locks, gw);
         if (__ballot(act && st == kError)) {
             if (lane == 0) atomicOr(err, 1);
@@ -3303,7 +3314,7 @@ __global__ __launch_bounds__(256) void star_rewire_kernel(
         int64_t rw = 0;
         for (uint64_t f = fm; f; f &= f - 1) {  // X_near order
             const int i = __builtin_ctzll(f);
-            const int m = __shfl(tk.node, i);
+            const int m = __shfl(ex.node, i);
             const double em = __shfl(e, i);
             const double cn = cb + em;
             if (!(cn < cost[m])) continue;
@@ -3352,10 +3363,10 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
     // wave slot the walk's 48 VGPRs allow (4 workgroups of 8 waves per CU)
     const int walk_cap = lds > 0 ? kWalkMaxWG : 1024;
     const int walkB = std::min((TB + kWalkThreads / 64 - 1) / (kWalkThreads / 64), walk_cap);
-    auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, int* status, double* yaw,
-                     double* cost) {
+    auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, const StarTaskExt* ext,
+                     int* status, double* yaw, double* cost) {
         steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(st, a.sc, nullptr, nullptr, nullptr, nullptr,
-                                                      a.rec, a.pdbuf, yaw, t, cost);
+                                                      a.rec, a.pdbuf, yaw, t, cost, ext);
         if (lds > 0)
             steer_walk_kernel<true><<<wb, kWalkThreads, walk_lds_bytes(lds), s>>>(
                 st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr);
@@ -3368,13 +3379,15 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
         star_sample_kernel<<<qb, 256, 0, s>>>(a.sd, a.sc.minx, a.sc.maxx, a.sc.miny, a.sc.maxy,
                                               a.tA);
         if (a.ev) (void)hipEventRecord(a.ev[2 * k + 1], s);
-        round(a.sd.stA, prepA, walkA, a.tA, a.sA, a.yA, a.cA);
-        star_knn_kernel<<<knn_blocks, 64 * kKnnWaves, 0, s>>>(a.sd, a.sA, a.cA, a.tB, a.err);
-        round(a.sd.stB, prepB, walkB, a.tB, a.sB, a.yB, a.cB);
+        round(a.sd.stA, prepA, walkA, a.tA, nullptr, a.sA, a.yA, a.cA);
+        star_knn_kernel<<<knn_blocks, 64 * kKnnWaves, 0, s>>>(a.sd, a.sA, a.cA, a.tB, a.eB,
+                                                              a.err);
+        round(a.sd.stB, prepB, walkB, a.tB, a.eB, a.sB, a.yB, a.cB);
         star_insert_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sc, a.sA, a.yA, a.cA, a.tB, a.sB,
-                                                      a.yB, a.cB, a.tC, a.lit_scratch, a.err);
-        round(a.sd.stC, prepB, walkB, a.tC, a.sC, a.yC, a.cC);
-        star_rewire_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sc, a.tC, a.sC, a.cC,
+                                                      a.yB, a.cB, a.tC, a.eC, a.lit_scratch,
+                                                      a.err);
+        round(a.sd.stC, prepB, walkB, a.tC, a.eC, a.sC, a.yC, a.cC);
+        star_rewire_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sc, a.tC, a.eC, a.sC, a.cC,
                                                       a.lit_scratch, a.err);
     }
     return hipGetLastError();

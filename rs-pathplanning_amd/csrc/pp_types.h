@@ -128,13 +128,17 @@ struct SteerTask {
     double x, y, px, py, pyaw;
     int pnode;
     int literal;  // 1 = take the literal (single-lane) path
-    double cyaw;  // own_yaw: the child keeps this heading (RRT* rewire: an existing node's pose)
-                  //          instead of compute_yaw toward the parent (rrt.rs:267-271)
-    double cbase, climit;  // cull (RRT*): steer_prep settles the task as rejected, without a
-                           // walk, unless cbase + its Dubins cost < climit (it cannot matter)
+};
+
+// RRT* extension of a SteerTask (a parallel array, so the extend batches keep 48-B tasks)
+struct StarTaskExt {
+    double cyaw;           // own_yaw: the child keeps this heading (rewire: an existing node's
+                           // pose) instead of compute_yaw toward the parent (rrt.rs:267-271)
+    double cbase, climit;  // cull: steer_prep settles the task as rejected, without a walk,
+                           // unless cbase + its Dubins cost < climit (it cannot matter)
     int own_yaw;
     int cull;
-    int node;  // RRT* rewire: the child's tree node
+    int node;  // rewire: the child's tree node
     int pad;
 };
 
