@@ -181,15 +181,6 @@ struct pp_ctx {
     DBuf<PrepRec> mq_rec;
     DBuf<DevState> mq_state;      // [3]: the whole batch, then one per sub-batch (mq_sub_args)
     hipStream_t sub_stream[4] = {};  // sub-batch streams 1.. (0 is `stream`), created on first use
-    // RRT* steps captured as HIP graphs (kStarGraphSteps steps per sub-batch), for the current
-    // RRT* batch and sub-batch split (star_graph_n = its sub-batch count, 0 = none captured)
-    hipGraphExec_t star_graph[4] = {};
-    int star_graph_n = 0;
-    void drop_star_graphs() {
-        for (auto& g : star_graph)
-            if (g) (void)hipGraphExecDestroy(g), g = nullptr;
-        star_graph_n = 0;
-    }
     hipEvent_t fork_ev = nullptr;
     std::vector<double> mq_goal;  // 3 per query (kept for the host; the batch path is extend only)
 
@@ -224,7 +215,6 @@ struct pp_ctx {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
-        drop_star_graphs();
         for (auto& ss : sub_stream)
             if (ss) (void)hipStreamDestroy(ss);
         if (stream) (void)hipStreamDestroy(stream);
@@ -504,7 +494,6 @@ MqArgs mq_args(pp_ctx* c) {
 // own streams and one's small kernels overlap another's walk.  Results do not depend on the
 // split: queries are independent.
 constexpr int kMaxSub = 4;
-constexpr int kStarGraphSteps = 8;  // RRT* steps per captured graph
 // streams: 2 for the extend batch (2: 289M it/s at 8192 queries, 177M on a 1024-query shard; 3:
 // 291M / 160M; 4: 244M / 109M), 3 for RRT* (11 kernels a step: 16.4M / 4.5M against 15.0M / 4.2M
 // with 2; 4 streams collapse to 10.7M / 2.4M, the box runs 4 hardware queues per process)
@@ -1739,7 +1728,6 @@ int pp_star_new(pp_ctx* ctx, int q, const double* starts, const uint64_t* seeds,
         return set_err(PP_ERR_CAPACITY, "RRT* batch too large");
     const size_t rows = (size_t)q * (size_t)cap64, tb = (size_t)q * kStarKMax;
     ctx->has_star = false;
-    ctx->drop_star_graphs();
     PP_HIP(ctx->sr_x.reserve(rows));
     PP_HIP(ctx->sr_y.reserve(rows));
     PP_HIP(ctx->sr_yaw.reserve(rows));
@@ -1828,7 +1816,6 @@ int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t*
     const int64_t steps = std::min<int64_t>(n_steps, ctx->star_max_iter);  // one iteration a step
     // sub-batches on their own streams, as pp_batch_extend (one stream while profiling)
     const int nsub = ctx->prof ? 1 : mq_nsub(ctx->star_Q, 3);
-    const bool use_graphs = !std::getenv("PP_NO_GRAPH");
     StarArgs sub[kMaxSub];
     hipStream_t sst[kMaxSub] = {ctx->stream};
     for (int i = 0; i < nsub && nsub > 1; ++i) {
@@ -1851,28 +1838,7 @@ int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t*
             a.ev = ctx->ev.data();
         }
         if (nsub > 1) {  // interleaved, so every stream always holds work
-            int k = 0;
-            if (use_graphs) {  // whole graphs of kStarGraphSteps steps (one launch each)
-                if (ctx->star_graph_n != nsub) {
-                    ctx->drop_star_graphs();
-                    for (int i = 0; i < nsub; ++i) {
-                        hipGraph_t g = nullptr;
-                        PP_HIP(hipStreamBeginCapture(sst[i], hipStreamCaptureModeRelaxed));
-                        const hipError_t le = launch_star_steps(sst[i], sub[i], kStarGraphSteps);
-                        PP_HIP(hipStreamEndCapture(sst[i], &g));
-                        PP_HIP(le);
-                        const hipError_t ie =
-                            hipGraphInstantiate(&ctx->star_graph[i], g, nullptr, nullptr, 0);
-                        (void)hipGraphDestroy(g);
-                        PP_HIP(ie);
-                    }
-                    ctx->star_graph_n = nsub;
-                }
-                for (; k + kStarGraphSteps <= chunk; k += kStarGraphSteps)
-                    for (int i = 0; i < nsub; ++i)
-                        PP_HIP(hipGraphLaunch(ctx->star_graph[i], sst[i]));
-            }
-            for (; k < chunk; ++k)
+            for (int k = 0; k < chunk; ++k)
                 for (int i = 0; i < nsub; ++i) PP_HIP(launch_star_steps(sst[i], sub[i], 1));
         } else {
             PP_HIP(launch_star_steps(ctx->stream, a, chunk));
