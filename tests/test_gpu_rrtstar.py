@@ -156,3 +156,18 @@ def test_star_sub_batch_streams(pkg, oracle_mod, ctx):
     acc, rws = oracle_mod.star_queries(oracle_mod.OracleScene.from_raw(raw), starts, seeds, 80, 0,
                                        0.0, 8)
     assert int(n.sum()) - 300 == acc and int(rw.sum()) == rws
+
+
+def test_star_large_tree_uncached_knn(pkg, oracle_mod, ctx):
+    """a tree past the kNN's LDS distance cache (n > 2048 nodes): the exclusion rounds over global
+    memory, plus k at its cap region"""
+    from pathplanning_amd import scenes
+
+    raw = scenes.bench6_open()
+    b = _batch(pkg, raw, [raw["start"]], [21], 4000, 0, 0.0, ctx=ctx)
+    b.extend(4000)
+    n = int(b.state()[0][0])
+    assert n > 2100
+    exp, erw = _oracle(oracle_mod, raw, raw["start"], 21, 4000, 0, 0.0)
+    _assert_same(b.tree(0), exp)
+    assert b.state()[3][0] == erw
