@@ -27,3 +27,26 @@ def test_shard_ranges_cover_queries_once():
                 a, b = bench.shard(total, world, r)
                 seen.extend(range(a, b))
             assert seen == list(range(total))
+
+
+def test_config5_field_and_queries():
+    """BASELINE config 5's field (10240 discs on 2048^2) and its query recipe: deterministic,
+    starts clear of every inflated disc, shards concatenate to the whole batch"""
+    import bench
+    from pathplanning_amd import scenes
+
+    raw = scenes.config5_field()
+    circ = np.asarray(raw["circles"])
+    assert circ.shape == (10240, 3) and raw["bounds"] == (0.0, 0.0, 2048.0, 2048.0)
+    assert (circ[:, 2] >= 1.0).all() and (circ[:, 2] < 4.0).all()
+    whole, _, seeds = scenes.config3_queries(raw, 0, 24)
+    parts = []
+    for r in range(4):
+        a, b = bench.shard(24, 4, r)
+        s, _, sd = scenes.config3_queries(raw, a, b - a)
+        assert sd.tolist() == seeds[a:b].tolist()
+        parts.append(s)
+    assert np.array_equal(np.concatenate(parts), whole)
+    for pose in whole:
+        d2 = (circ[:, 0] - pose[0]) ** 2 + (circ[:, 1] - pose[1]) ** 2
+        assert (d2 > (circ[:, 2] + 0.5 + 1.0) ** 2).all()
