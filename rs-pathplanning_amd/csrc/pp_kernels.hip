@@ -3163,82 +3163,6 @@ __device__ __forceinline__ int star_settle(const SceneDev& sc, int st, bool act,
     return st;
 }
 
-// Round B's deferral: per gated query, the kStarTopM cheapest choose-parent candidates (by
-// cost(node) + the prep's exact Dubins cost, candidate order on ties) are walked; the others
-// that could still win get kDeferOff added to their prep record state, so the walk skips them.
-__global__ __launch_bounds__(256) void star_select_kernel(StarDev sd,
-                                                          const SteerTask* __restrict__ tasksB,
-                                                          const double* __restrict__ costB,
-                                                          PrepRec* __restrict__ rec) {
-    const int lane = threadIdx.x & 63;
-    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    const MqDev& mq = sd.mq;
-    for (int q = gw; q < mq.Q; q += nw) {
-        if (sd.pn[q] < 0 || sd.nnear[q] < 0) continue;
-        const int nb = __popcll(sd.bmask[q]);
-        if (nb <= kStarTopM) continue;
-        const size_t row = (size_t)q * mq.cap;
-        const int t = sd.bslot[q] + lane;
-        double c = __builtin_inf();
-        if (lane < nb && rec[t].state != kReject)  // not settled by the prep's cost cull
-            c = sd.cost[row + tasksB[t].pnode] + costB[t];
-        const Kv kv = bitonic64(c, lane, lane);
-        uint64_t top = (lane < kStarTopM && kv.d < __builtin_inf()) ? 1ull << kv.i : 0ull;
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) top |= __shfl_xor(top, m);
-        if (lane < nb && c < __builtin_inf() && !((top >> lane) & 1ull))
-            rec[t].state += kDeferOff;
-    }
-}
-
-// After round B's walk: a query whose first open candidate in (cost, order) order is a walked,
-// feasible one is decided — its deferred candidates can never win and stay deferred; otherwise
-// its deferred candidates get their prep state back for the second walk.  Every walked task's
-// record takes its verdict as state, so the second walk re-emits it without walking.
-__global__ __launch_bounds__(256) void star_defer_kernel(StarDev sd,
-                                                         const int* __restrict__ statusA,
-                                                         const double* __restrict__ costA,
-                                                         const SteerTask* __restrict__ tasksB,
-                                                         const int* __restrict__ statusB,
-                                                         const double* __restrict__ costB,
-                                                         PrepRec* __restrict__ rec) {
-    const int lane = threadIdx.x & 63;
-    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    const MqDev& mq = sd.mq;
-    for (int q = gw; q < mq.Q; q += nw) {
-        if (sd.pn[q] < 0 || sd.nnear[q] < 0) continue;
-        const int nb = __popcll(sd.bmask[q]);
-        if (nb == 0) continue;
-        const size_t row = (size_t)q * mq.cap;
-        const bool act = lane <= nb;
-        int st = kReject, node = sd.pn[q], t = 0;
-        double e = __builtin_inf();
-        if (lane == 0) {
-            st = statusA[q];
-            e = costA[q];
-        } else if (act) {
-            t = sd.bslot[q] + lane - 1;
-            st = statusB[t];
-            e = costB[t];
-            node = tasksB[t].pnode;
-        }
-        const bool open = act && (star_feasible(st, e) || st >= kDeferOff || st == kLiteral);
-        double c = open ? sd.cost[row + node] + e : __builtin_inf();
-        int bl = lane;
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) argmin_pair(c, bl, __shfl_xor(c, m), __shfl_xor(bl, m));
-        const bool decided = __shfl((int)star_feasible(st, e), bl) != 0;
-        if (lane >= 1 && act) {
-            if (st < kDeferOff)
-                rec[t].state = st;  // the verdict, re-emitted by the second walk
-            else if (!decided)
-                rec[t].state = st - kDeferOff;  // walked by the second walk
-        }
-    }
-}
-
 __global__ __launch_bounds__(256) void star_insert_kernel(
     StarDev sd, SceneDev sc, const int* __restrict__ statusA, const double* __restrict__ yawA,
     const double* __restrict__ costA, const SteerTask* __restrict__ tasksB,
@@ -3439,19 +3363,16 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
     // wave slot the walk's 48 VGPRs allow (4 workgroups of 8 waves per CU)
     const int walk_cap = lds > 0 ? kWalkMaxWG : 1024;
     const int walkB = std::min((TB + kWalkThreads / 64 - 1) / (kWalkThreads / 64), walk_cap);
-    auto walk = [&](DevState* st, int wb, int* status) {
+    auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, const StarTaskExt* ext,
+                     int* status, double* yaw, double* cost) {
+        steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(st, a.sc, nullptr, nullptr, nullptr, nullptr,
+                                                      a.rec, a.pdbuf, yaw, t, cost, ext);
         if (lds > 0)
             steer_walk_kernel<true><<<wb, kWalkThreads, walk_lds_bytes(lds), s>>>(
                 st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr);
         else
             steer_walk_kernel<false><<<wb, kWalkThreads, walk_lds_bytes(0), s>>>(
                 st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr);
-    };
-    auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, const StarTaskExt* ext,
-                     int* status, double* yaw, double* cost) {
-        steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(st, a.sc, nullptr, nullptr, nullptr, nullptr,
-                                                      a.rec, a.pdbuf, yaw, t, cost, ext);
-        walk(st, wb, status);
     };
     for (int k = 0; k < steps; ++k) {
         if (a.ev) (void)hipEventRecord(a.ev[2 * k], s);
@@ -3461,13 +3382,7 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
         round(a.sd.stA, prepA, walkA, a.tA, nullptr, a.sA, a.yA, a.cA);
         star_knn_kernel<<<knn_blocks, 64 * kKnnWaves, 0, s>>>(a.sd, a.sA, a.cA, a.tB, a.eB,
                                                               a.err);
-        steer_prep_kernel<<<prepB, kPrepThreads, 0, s>>>(a.sd.stB, a.sc, nullptr, nullptr,
-                                                         nullptr, nullptr, a.rec, a.pdbuf, a.yB,
-                                                         a.tB, a.cB, a.eB);
-        star_select_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.tB, a.cB, a.rec);
-        walk(a.sd.stB, walkB, a.sB);
-        star_defer_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sA, a.cA, a.tB, a.sB, a.cB, a.rec);
-        walk(a.sd.stB, walkB, a.sB);  // the deferred candidates of undecided queries
+        round(a.sd.stB, prepB, walkB, a.tB, a.eB, a.sB, a.yB, a.cB);
         star_insert_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sc, a.sA, a.yA, a.cA, a.tB, a.sB,
                                                       a.yB, a.cB, a.tC, a.eC, a.lit_scratch,
                                                       a.err);

@@ -169,11 +169,7 @@ struct PrepRec {
     int state, fb_seg;               // kPrepWalk / kPrepNone / kPrepFallback or a verdict; the
                                      // kPrepFallback walk's segment at point kPdCap
 };
-enum : int { kPrepWalk = -1, kPrepNone = 4, kPrepFallback = 5, kDeferOff = 16 };
-// kDeferOff (RRT* choose-parent): a candidate outside the kStarTopM cheapest of its query is not
-// walked by round B (record state + kDeferOff, returned as its status); star_defer restores it
-// for a second walk only when every cheaper candidate proved infeasible
-constexpr int kStarTopM = 6;
+enum : int { kPrepWalk = -1, kPrepNone = 4, kPrepFallback = 5 };
 
 // Multi-query batch (BASELINE config 3): Q independent trees, tree q in rows [q * cap, q * cap +
 // n[q]) of the SoA arrays, all advanced one extend iteration per lockstep step.
