@@ -851,20 +851,28 @@ int build_item_grid(pp_ctx* ctx, double minx, double maxx, double miny, double m
                     const std::vector<double>& by0, const std::vector<double>& by1,
                     const std::vector<float4>& d4) {
     const int m = (int)d4.size();
-    // square cells, about one cell per item
     const double spanx = maxx - minx, spany = maxy - miny;
     const double span = std::max(spanx, spany);
-    const int per_axis = std::max(1, std::min(256, (int)std::ceil(std::sqrt((double)std::max(m, 1)))));
-    const double cell = span / per_axis;
-    const int gnx = std::max(1, std::min(256, (int)std::ceil(spanx / cell)));
-    const int gny = std::max(1, std::min(256, (int)std::ceil(spany / cell)));
-    const double ginv = 1.0 / cell;
-    auto cell_of = [&](double v, double v0, int n) {
-        const double f = std::floor((v - v0) * ginv);
-        return f < 0.0 ? 0 : (f >= (double)(n - 1) ? n - 1 : (int)f);
-    };
-    std::vector<int> goff((size_t)gnx * gny + 1, 0), gitems;
-    {
+    auto al = [](size_t b) { return (int)((b + 15) & ~(size_t)15); };
+    constexpr int kLdsImage = 64 * 1024;  // 2 workgroups per CU fit in 160 KB
+    // square cells, about one cell per item; a scene whose LDS image [goff | items | d4] does not
+    // fit gets the image without the cull discs (read from global memory), at a coarser grid if
+    // that is what it takes
+    std::vector<int> goff, gitems;
+    int gnx = 1, gny = 1, lds_total = 0, o_goff = 0, o_items = 0, o_d4 = -1;
+    double ginv = 1.0;
+    const int per0 = std::max(1, std::min(256, (int)std::ceil(std::sqrt((double)std::max(m, 1)))));
+    for (int per_axis = per0;; per_axis = per_axis * 3 / 4) {
+        const double cell = span / per_axis;
+        gnx = std::max(1, std::min(256, (int)std::ceil(spanx / cell)));
+        gny = std::max(1, std::min(256, (int)std::ceil(spany / cell)));
+        ginv = 1.0 / cell;
+        auto cell_of = [&](double v, double v0, int n) {
+            const double f = std::floor((v - v0) * ginv);
+            return f < 0.0 ? 0 : (f >= (double)(n - 1) ? n - 1 : (int)f);
+        };
+        goff.assign((size_t)gnx * gny + 1, 0);
+        gitems.clear();
         std::vector<std::vector<int>> lists((size_t)gnx * gny);
         for (int k = 0; k < m; ++k) {
             const int x0c = cell_of(bx0[k], minx, gnx), x1c = cell_of(bx1[k], minx, gnx);
@@ -876,35 +884,44 @@ int build_item_grid(pp_ctx* ctx, double minx, double maxx, double miny, double m
             goff[q + 1] = goff[q] + (int)lists[q].size();
             gitems.insert(gitems.end(), lists[q].begin(), lists[q].end());
         }
+        o_items = o_goff + al(goff.size() * sizeof(int));
+        const int grid_bytes = o_items + al(gitems.size() * sizeof(int));
+        const int full = grid_bytes + al((size_t)m * sizeof(float4));
+        if (full <= kLdsImage) {  // everything in LDS
+            lds_total = full;
+            o_d4 = grid_bytes;
+            break;
+        }
+        if (grid_bytes <= kLdsImage && m > 4096) {  // the grid in LDS, the cull discs in L2
+            lds_total = grid_bytes;
+            o_d4 = -1;
+            break;
+        }
+        if (per_axis <= 8 || m <= 4096) {  // no LDS image: the walk reads the scene from L2
+            lds_total = 0;
+            break;
+        }
     }
     PP_HIP(ctx->d_goff.reserve(goff.size()));
     PP_HIP(ctx->d_gitems.reserve(std::max<size_t>(gitems.size(), 1)));
     PP_HIP(hipMemcpy(ctx->d_goff.p, goff.data(), goff.size() * sizeof(int), hipMemcpyHostToDevice));
     if (!gitems.empty())
         PP_HIP(hipMemcpy(ctx->d_gitems.p, gitems.data(), gitems.size() * sizeof(int), hipMemcpyHostToDevice));
-    {  // LDS image for the steer kernels: [goff | items | d4], 16-byte aligned parts (the f64
-       // items of the exact test stay in global memory: the f32 cull leaves few exact tests)
-        auto al = [](size_t b) { return (int)((b + 15) & ~(size_t)15); };
-        const int o_goff = 0;
-        const int o_items = o_goff + al(goff.size() * sizeof(int));
-        const int o_d4 = o_items + al(gitems.size() * sizeof(int));
-        const int total = o_d4 + al((size_t)m * sizeof(float4));
-        const bool fits = total <= 64 * 1024;  // 2 workgroups per CU fit in 160 KB
-        ctx->lds_bytes = fits ? total : 0;
-        if (fits) {  // the same image, contiguous in global memory (stage_scene copies it whole)
-            std::vector<char> img((size_t)total, 0);
-            std::memcpy(img.data() + o_goff, goff.data(), goff.size() * sizeof(int));
-            if (!gitems.empty())
-                std::memcpy(img.data() + o_items, gitems.data(), gitems.size() * sizeof(int));
+    ctx->lds_bytes = lds_total;
+    if (lds_total > 0) {  // the image, contiguous in global memory (stage_scene copies it whole)
+        std::vector<char> img((size_t)lds_total, 0);
+        std::memcpy(img.data() + o_goff, goff.data(), goff.size() * sizeof(int));
+        if (!gitems.empty())
+            std::memcpy(img.data() + o_items, gitems.data(), gitems.size() * sizeof(int));
+        if (o_d4 >= 0)
             for (int k = 0; k < m; ++k) std::memcpy(img.data() + o_d4 + 16 * k, &d4[k], 16);
-            PP_HIP(ctx->d_img.reserve((size_t)total / 16));
-            PP_HIP(hipMemcpy(ctx->d_img.p, img.data(), (size_t)total, hipMemcpyHostToDevice));
-        }
-        ctx->lds_goff = o_goff;
-        ctx->lds_items = o_items;
-        ctx->lds_cx = ctx->lds_cy = ctx->lds_r2 = -1;
-        ctx->lds_d4 = o_d4;
+        PP_HIP(ctx->d_img.reserve((size_t)lds_total / 16));
+        PP_HIP(hipMemcpy(ctx->d_img.p, img.data(), (size_t)lds_total, hipMemcpyHostToDevice));
     }
+    ctx->lds_goff = o_goff;
+    ctx->lds_items = o_items;
+    ctx->lds_cx = ctx->lds_cy = ctx->lds_r2 = -1;
+    ctx->lds_d4 = o_d4;
     ctx->gx0 = minx;
     ctx->gy0 = miny;
     ctx->ginv = ginv;

@@ -111,7 +111,10 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const double* dcx = sc.cx;  // exact test: f64 discs from global memory (L2)
     const double* dcy = sc.cy;
     const double* dr2 = sc.r2;
-    const float4* d4 = kLds ? reinterpret_cast<const float4*>(pp_smem + sc.lds_d4) : sc.d4;
+    // the cull discs are in the LDS image too unless the scene only fit without them (lds_d4 < 0)
+    const float4* d4 = (kLds && sc.lds_d4 >= 0)
+                           ? reinterpret_cast<const float4*>(pp_smem + sc.lds_d4)
+                           : sc.d4;
     // per-lane f32 cull: a segment a-b can only touch a disc / an edge buffer (exact test below)
     // if |a - c| <= rcull + |b - a| (c: the disc centre / the edge midpoint, rcull: the radius /
     // half length + h); cull_slack covers the f32 rounding of the scene's coordinates
