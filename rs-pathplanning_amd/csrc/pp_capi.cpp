@@ -855,6 +855,8 @@ int build_item_grid(pp_ctx* ctx, double minx, double maxx, double miny, double m
     const double span = std::max(spanx, spany);
     auto al = [](size_t b) { return (int)((b + 15) & ~(size_t)15); };
     constexpr int kLdsImage = 64 * 1024;  // 2 workgroups per CU fit in 160 KB
+    int part_budget = kLdsImage;  // the grid-only image (PP_LDS_GRID_KB: experiments)
+    if (const char* e = std::getenv("PP_LDS_GRID_KB")) part_budget = std::atoi(e) * 1024;
     // square cells, about one cell per item; a scene whose LDS image [goff | items | d4] does not
     // fit gets the image without the cull discs (read from global memory), at a coarser grid if
     // that is what it takes
@@ -892,7 +894,7 @@ int build_item_grid(pp_ctx* ctx, double minx, double maxx, double miny, double m
             o_d4 = grid_bytes;
             break;
         }
-        if (grid_bytes <= kLdsImage && m > 4096) {  // the grid in LDS, the cull discs in L2
+        if (grid_bytes <= part_budget && m > 4096) {  // the grid in LDS, the cull discs in L2
             lds_total = grid_bytes;
             o_d4 = -1;
             break;
