@@ -1370,14 +1370,13 @@ __device__ inline Pt seg_end(int mode, double len, double c, double ox, double o
 // task's chain is ~9 calls deep instead of ~32.  The `pd += d` walk of generate_local_course
 // (dubins.rs:200-272) is left to steer_walk (lane-parallel, exact).
 __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
-    DevState* __restrict__ st, SceneDev sc, const double* __restrict__ wsx,
+    const DevState* __restrict__ st, SceneDev sc, const double* __restrict__ wsx,
     const double* __restrict__ wsy, const double* __restrict__ snap_pose,
     CandEntry* __restrict__ cand, PrepRec* __restrict__ rec, double* __restrict__ pdbuf,
     double* __restrict__ snap_yaw, const SteerTask* __restrict__ tasks,
     double* __restrict__ cost_out = nullptr, const StarTaskExt* __restrict__ ext = nullptr) {
     // tasks != nullptr: explicit (child, parent pose) tasks [0, W) (multi-query batch); a task
     // with pnode < 0 is idle; own_yaw: the child keeps its heading cyaw (RRT* rewire edges)
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->walk_next = 0;  // the next walk's task counter
     const int W = st->W;
     const int total = W + st->ncomp;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1846,11 +1845,8 @@ __global__ __launch_bounds__(kWalkThreads) void steer_walk_kernel(DevState* __re
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) +
                  (threadIdx.x >> 6) * kGenSlots;  // this wave's generator slots
-    // the first round of tasks by wave index, the rest handed out one at a time (a wave whose
-    // walks run long takes fewer: the kernel ends with the last task, not the unluckiest wave)
-    for (int t = gw; t < total;) {
+    for (int t = gw; t < total; t += nw) {
         const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, stw);
-        int nt = 0;
         if (lane == 0) {
             if (t < W) {
                 snap_status[t] = s;
@@ -1859,9 +1855,7 @@ __global__ __launch_bounds__(kWalkThreads) void steer_walk_kernel(DevState* __re
             } else {
                 cand[t - W].status = s;
             }
-            nt = total > nw ? nw + atomicAdd(&st->walk_next, 1) : total;
         }
-        t = __builtin_amdgcn_readfirstlane(__shfl(nt, 0));
     }
 }
 

@@ -115,7 +115,7 @@ struct DevState {
     int nsp[2];      // per parity: tree nodes its scan covered
     int64_t void_seq;  // window sequence number voided by a truncated predecessor (-1: none)
     int resolve_bail;  // the window kernel's resolve needed a repair: resolve_tail_kernel redoes it
-    int walk_next;     // steer_walk: tasks handed out past the first round (reset by steer_prep)
+    int pad2;
     // statistics (pp_stats)
     int64_t iterations, accepted, windows, truncations, repair_rounds, repairs, literal_repairs,
         nn_flagged, node_evals;
