@@ -2901,7 +2901,10 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
 // counts live in DevState W (stA: Q, stB / stC: counted on the device), so a step needs no host
 // round trip.
 constexpr int kKnnWaves = 4;
-constexpr int kKnnCache = 2048;  // d2 values cached per wave (LDS: 4 x 16 KB)
+#ifndef PP_KNN_CACHE
+#define PP_KNN_CACHE 2048
+#endif
+constexpr int kKnnCache = PP_KNN_CACHE;  // d2 values cached per wave (LDS: 4 x 16 KB)
 
 __device__ __forceinline__ bool star_feasible(int status, double e) {
     return status == kAccept && e <= 1.7976931348623157e308;  // Some and verified (finite cost)
