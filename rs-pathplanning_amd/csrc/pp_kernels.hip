@@ -1812,6 +1812,12 @@ constexpr int kWalkMaxWG = PP_WALKWG;  // 3 resident workgroups per CU
 __host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
     return scene_bytes + kWalkThreads / 64 * kGenSlots * 8;
 }
+// the walk's persistent grid: the workgroups that can be resident at once (the LDS image decides:
+// 160 KB per CU; at most 4 of 8 waves each), so no workgroup starts late with a share of tasks
+inline int walk_grid_cap(int scene_bytes) {
+    const int per_cu = std::max(1, std::min(4, 160 * 1024 / walk_lds_bytes(scene_bytes)));
+    return 256 * per_cu;
+}
 
 // Window mode (pend != nullptr): a snapshot task whose verdict is not final (literal path,
 // error) and that has no nearer window sample is queued for the resolve (the others were queued
@@ -2860,7 +2866,8 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int T = Q * a.mq.K;  // tasks per step
     const int nn_blocks = std::min((Q + 3) / 4, 4096);  // one wave per query
     const int prep_blocks = std::min((T + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
-    const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
+    const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
+                                     std::min(kWalkMaxWG, walk_grid_cap(a.sc.lds_bytes)));
     const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
     const int lds = a.sc.lds_bytes;
     for (int k = 0; k < steps; ++k) {
@@ -3363,11 +3370,12 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
     const int lit_blocks = std::min((Q + 3) / 4, 4096);  // literal scratch: slot locks
     const int prepA = std::min((Q + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int prepB = std::min((TB + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
-    const int walkA = std::min((Q + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
+    const int walkA = std::min((Q + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
+                               std::min(kWalkMaxWG, walk_grid_cap(a.sc.lds_bytes)));
     const int lds = a.sc.lds_bytes;
     // a scene read from global memory (no LDS image) makes the walk latency-bound: fill every
     // wave slot the walk's 48 VGPRs allow (4 workgroups of 8 waves per CU)
-    const int walk_cap = lds > 0 ? kWalkMaxWG : 1024;
+    const int walk_cap = lds > 0 ? std::min(kWalkMaxWG, walk_grid_cap(lds)) : 1024;
     const int walkB = std::min((TB + kWalkThreads / 64 - 1) / (kWalkThreads / 64), walk_cap);
     auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, const StarTaskExt* ext,
                      int* status, double* yaw, double* cost) {
@@ -3524,7 +3532,8 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
                                                   a.rec, a.pdbuf, a.snap_yaw, nullptr);
     const int lds = a.sc.lds_bytes;
     // snapshot tasks plus the usual few candidate tasks in one round of waves
-    const int nwg = std::min((K + K / 4 + kWalkThreads / 64 - 1) / (kWalkThreads / 64), kWalkMaxWG);
+    const int nwg = std::min((K + K / 4 + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
+                             std::min(kWalkMaxWG, walk_grid_cap(a.sc.lds_bytes)));
     if (lds > 0)
         steer_walk_kernel<true><<<nwg, kWalkThreads, walk_lds_bytes(lds), s>>>(a.st, a.sc, a.rec, a.pdbuf, a.cand,
                                                       a.snap_status, a.cand_cnt, a.pend);
