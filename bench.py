@@ -1,19 +1,33 @@
-"""RRT extend iterations/s (2D Dubins, 1k obstacles) — BASELINE.json config 2 on MI355X.
+"""RRT extend iterations/s (2D Dubins, 1k obstacles) — BASELINE.json's metric on MI355X.
 
-A step = one speculative window of K = 4096 extend iterations (sample, exact nearest neighbour,
-Dubins steer, sampled-arc collision check, insert — plan_one minus check_finish) on a tree grown
-beforehand to 100k nodes, with the sequential semantics of the reference (results independent
-of K).  With --gpus N (torchrun), every rank grows its own independent replica tree on its own
-GPU (seed 42 + rank): the path shards by planning query with no data-path collective, so scaling
-is weak and `value` is the iterations of all ranks / the slowest rank's time.
+Headline (`value`): BASELINE config 2 — one tree grown to 100k nodes, a step = one speculative
+window of K = 4096 extend iterations (sample, exact nearest neighbour, Dubins steer, sampled-arc
+collision check, insert: plan_one minus check_finish, rrt.rs:583-589) with the sequential
+semantics of the reference (results independent of K).  With N ranks every rank grows its own
+replica tree on its own GPU (seed 42 + rank): weak scaling, `value` = all ranks' iterations / the
+slowest rank's time.
 
-Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline accounting.
+Sub-results on the same line (the rows of SURVEY.md §8d the driver would not see otherwise):
+  config3  8192 independent queries sharded contiguously over the N ranks (strong scaling), one
+           all_gather of per-query records over RCCL (nccl) when every rank has its own GPU;
+           `records_digest` is the same at every N when the sharded run equals the 1-rank run
+  config5  the RRT* query batch (build-defined, stretch), sharded the same way
+  config4  config 2 on the 512x512 bit-packed occupancy grid (N = 1 only)
+  config1  the reference's own bench scene (benches/all.rs:8-46), 8000 iterations (N = 1 only)
+  plan     RRT::plan on bench6_open: extend + check_finish of every accepted node (N = 1 only)
+
+`python bench.py --gpus N` without WORLD_SIZE starts N rank processes itself (before anything
+touches the GPU); under torchrun it is one of them.  Prints ONE JSON line (rank 0).  See DESIGN.md
+§5 for the roofline accounting.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,38 +38,143 @@ sys.path.insert(0, os.path.join(ROOT, "rs-pathplanning_amd"))
 
 F32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, Peak FP32 (vector), spec
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md, HBM3E peak, spec
+CLOCK_GHZ = 2.4               # MI355X_MICROARCH.md, max clock
+VALU_CYC = 2                  # cycles per wave64 VALU instruction on a SIMD-32 (MICROARCH: v_fma_f32)
 FLOP_PER_EVAL = 5             # dx, dy (2 sub), dx*dx (mul), + dy*dy (fma = 2)
 BYTES_PER_EVAL = 8            # f32 x + f32 y of one SoA node
+METRIC = "RRT extend iterations/sec (2D Dubins, 1k obstacles)"
+WORKLOADS = ("default", "config1", "config2", "config3", "config4", "polygons", "config5", "plan")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=("config2", "config3", "config4", "polygons",
-                                           "config5"),
-                    default="config2",
-                    help="config2: one tree, K-candidate windows (default); config3: a batch of "
-                         "independent queries sharded over the ranks; config4: config 2 with the "
-                         "512x512 occupancy-grid collision; polygons: config 2 with its discs as "
-                         "create_circle polygons (polygon mode, SURVEY §8f row 3); config5: a batch of "
-                         "independent RRT* queries (k-nearest rewire) on a 10240-disc field")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE the bench starts them itself")
+    ap.add_argument("--workload", choices=WORKLOADS, default="default",
+                    help="default: config 2 + the sub-results; config2/config4/polygons: one tree, "
+                         "K-candidate windows (config4: 512x512 occupancy grid; polygons: "
+                         "create_circle polygons, SURVEY §8f row 3); config3: independent queries "
+                         "sharded over the ranks; config5: RRT* query batch; config1: the "
+                         "reference's bench scene; plan: RRT::plan with check_finish")
     ap.add_argument("--steps", type=int, default=None,
-                    help="timed steps (config2: windows, default 20; config3: lockstep "
-                         "iterations, default max_iter)")
+                    help="timed steps (windows for the one-tree workloads, default 20; lockstep "
+                         "iterations for the batches, default max_iter)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--queries", type=int, default=8192, help="config3: queries over all ranks")
+    ap.add_argument("--queries", type=int, default=8192, help="config3/5: queries over all ranks")
     ap.add_argument("--batch-window", type=int, default=0,
                     help="config3: iterations per query evaluated speculatively per GPU step "
-                         "(power of two <= 64; 0 = automatic: 16 up to 131072 tasks per step)")
-    ap.add_argument("--max-iter", type=int, default=2000, help="config3: RRT.max_iter per query")
+                         "(power of two <= 64; 0 = automatic)")
+    ap.add_argument("--max-iter", type=int, default=2000, help="config3/5: RRT.max_iter per query")
     ap.add_argument("--window", type=int, default=4096)
     ap.add_argument("--nodes", type=int, default=100_000, help="tree size before timing")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="bounded CPU-baseline sample per variant (rank 0, N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-size-sweep", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--no-sub", action="store_true", help="default workload: config 2 only")
+    ap.add_argument("--allow-variant-lib", action="store_true",
+                    help="accept PP_AMD_LIB pointing at another build (experiments only)")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------------------ ranks
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: N child processes of this script with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set, started before this process touches the GPU (it never does).
+    Returns the worst exit code; rank 0 prints the JSON line."""
+    env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+                WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = rc or c
+    return rc
+
+
+class Dist:
+    """One process per GPU.  The data path never communicates; the control plane (barrier,
+    max-time / sum reductions) runs over gloo and the per-query record gather over RCCL (nccl)
+    when every local rank has a GPU of its own, else over gloo (ranks sharing one GPU: RCCL
+    refuses two ranks on one device)."""
+
+    def __init__(self, args):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world)))
+        if args.gpus > 1 and self.world != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={self.world}")
+        from pathplanning_amd import _ffi
+
+        ndev = max(1, _ffi.device_count())
+        self.device = self.local % ndev
+        self.dist = None
+        self.gather_backend = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            own_gpu = torch.cuda.is_available() and torch.cuda.device_count() >= local_world
+            if own_gpu:
+                torch.cuda.set_device(self.device)
+                backend = "cpu:gloo,cuda:nccl"
+                self.gather_backend = "nccl"
+            else:
+                backend = "gloo"
+                self.gather_backend = "gloo"
+            dist.init_process_group(backend=backend, rank=self.rank, world_size=self.world)
+            assert dist.get_world_size() == self.world
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            import torch
+
+            self.dist.all_reduce(torch.zeros(1))  # on gloo: a CPU barrier that ignores devices
+
+    def allreduce(self, v, op="max"):
+        if self.dist is None:
+            return v
+        import torch
+
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def gather_records(self, rec):
+        """Every rank's per-query records (int64 [q_rank, C]) to every rank: one all_gather of
+        the padded blocks (RCCL over xGMI when gather_backend is nccl)."""
+        import torch
+
+        if self.dist is None:
+            return torch.from_numpy(rec)
+        dev = torch.device("cuda", self.device) if self.gather_backend == "nccl" else None
+        n = torch.tensor([rec.shape[0]], dtype=torch.int64, device=dev)
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        self.dist.all_gather(sizes, n)
+        mx = int(max(int(v.item()) for v in sizes))
+        pad = torch.zeros((mx, rec.shape[1]), dtype=torch.int64, device=dev)
+        pad[: rec.shape[0]] = torch.from_numpy(rec).to(pad.device)
+        outs = [torch.zeros_like(pad) for _ in range(self.world)]
+        self.dist.all_gather(outs, pad)
+        return torch.cat([o[: int(sz.item())].cpu() for o, sz in zip(outs, sizes)])
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
 
 
 def shard(total, world, rank):
@@ -65,56 +184,71 @@ def shard(total, world, rank):
     return a, a + base + (1 if rank < extra else 0)
 
 
-def dist_setup(args, backend="gloo"):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # control plane: barrier, max-time reduce, gather
+# ------------------------------------------------------------------------------ provenance
+def provenance(args):
+    """The library this run measures: its sha256 and the flags __graft_entry__ builds it with.
+    A PP_AMD_LIB override (a variant build) is refused unless --allow-variant-lib."""
+    from pathplanning_amd import _ffi
+    import __graft_entry__ as g
 
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if backend == "nccl":  # RCCL over xGMI on the GPU box
-            import torch
-
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend, rank=rank, world_size=world)
-    return dist, world, rank, local
-
-
-def barrier(dist):
-    if dist is not None:
-        dist.barrier()
+    if os.environ.get("PP_AMD_LIB") and not args.allow_variant_lib:
+        raise SystemExit("PP_AMD_LIB is set: bench.py measures the in-tree build only "
+                         "(--allow-variant-lib for experiments)")
+    with open(_ffi.LIB_PATH, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    return {"lib": os.path.relpath(_ffi.LIB_PATH, ROOT), "lib_sha256_16": sha,
+            "hipcc_flags": " ".join(g.HIPCC_FLAGS), "variant": bool(os.environ.get("PP_AMD_LIB"))}
 
 
-def allreduce_max(dist, v):
-    if dist is None:
-        return v
-    import torch
-
-    t = torch.tensor([float(v)], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+def load_profile(name):
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return json.load(f)
 
 
-def allreduce_sum(dist, v):
-    if dist is None:
-        return v
-    import torch
-
-    t = torch.tensor([float(v)], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+def host_threads():
+    """The host cores the CPU baseline may use: OMP_NUM_THREADS (16 on the GPU box, its share of
+    the machine), else all visible cores."""
+    return max(1, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1))
 
 
-def make_planner(raw, seed, window, device):
+def host_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc_visible": os.cpu_count(),
+            "reference_crate": "not buildable here (Rust, no cargo/rustc, crates not vendored: "
+                               "SURVEY.md K7); the CPU baseline is the build's C port (oracle/)"}
+
+
+def oracle_mod():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (cpu_baseline leg: the oracle is the timed CPU port here)
+
+    return oracle
+
+
+# ------------------------------------------------------------------------- one tree (config 2/4)
+def make_planner(raw, seed, window, device, capacity=1 << 18):
     from pathplanning_amd import rrt
 
     sx, sy, syaw = raw["start"]
     gx, gy, gyaw = raw["goal"]
     return rrt.RRT((sx, sy), syaw, (gx, gy), gyaw, raw["max_iter"], raw["step_size"],
                    rrt.Space.from_raw(raw), seed=seed, window=window, device=device,
-                   capacity=1 << 18)
+                   capacity=capacity)
+
+
+STAT_KEYS = ("iterations", "accepted", "windows", "truncations", "repair_rounds", "repairs",
+             "literal_repairs", "nn_flagged")
 
 
 def timed_windows(p, n_windows, window):
@@ -125,34 +259,132 @@ def timed_windows(p, n_windows, window):
     return time.perf_counter() - t0
 
 
-def auto_batch_window(q):
-    """pp_batch_new's automatic window: 32 for at most 2048 queries, else the largest power of
-    two <= 16 with q * K <= 131072."""
-    if q <= 2048:
-        return 32
-    k = 1
-    while k < 16 and q * k * 2 <= 131072:
-        k *= 2
-    return k
+def screen_roofline(sp, pmc):
+    """window_kernel (the NN screen, dominant in config 2/4): algorithmic work per launch / the
+    HIP-event average launch duration; plus the VALU instruction-issue bound from the committed
+    PMC pass (VALU instructions per eval, profiles/window_kernel_pmc.json)."""
+    launches = max(sp["nn_scan_launches"], 1)
+    avg_ms = sp["nn_scan_ms"] / launches
+    evals = sp["node_evals"] / launches
+    achieved = evals * FLOP_PER_EVAL / (avg_ms * 1e-3) / 1e12
+    r = {
+        "kernel": "window_kernel (NN screen; workgroup 0 resolves the previous window)",
+        "bound": "valu",
+        "achieved": round(achieved, 3),
+        "peak": F32_VALU_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / F32_VALU_PEAK_TFLOPS, 4),
+        "traffic": pmc.get("hbm_bytes_per_launch"),
+        "avg_launch_ms": round(avg_ms, 5),
+        "evals_per_launch": int(evals),
+        "flop_per_eval": FLOP_PER_EVAL,
+        "measured": f"HIP events on the planner stream, {sp['nn_scan_launches']} launches of the "
+                    "profiled pass that follows the timed region (same workload)",
+    }
+    vpe = pmc.get("valu_insts_per_eval")
+    if vpe:
+        simds = 4 * pmc.get("screen_cus", 248)
+        issue_us = evals * vpe / 64.0 * VALU_CYC / simds / (CLOCK_GHZ * 1e3)
+        r["issue_bound"] = {
+            "valu_insts_per_eval": vpe, "simds": simds,
+            "issue_bound_us": round(issue_us, 2),
+            "issue_frac": round(issue_us / (avg_ms * 1e3), 4),
+            "pmc_valu_busy": pmc.get("valu_busy"),
+            "note": "wave64 VALU instructions x 2 cycles (SIMD-32) / SIMDs / 2.4 GHz; the VALU "
+                    "count per eval is the committed rocprofv3 SQ_INSTS_VALU pass",
+        }
+    return r
 
 
-def host_threads():
-    """The host cores the CPU baseline may use: OMP_NUM_THREADS (16 on the GPU box, its share of
-    the machine), else all visible cores."""
-    return max(1, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1))
+def walk_roofline(sp, pmc, name):
+    """steer_walk (f64 Dubins interpolation + collision): polyline points per second against the
+    walk's VALU instruction-issue bound (VALU instructions per point from the committed PMC pass)."""
+    launches = max(sp["steer_launches"], 1)
+    if not sp["steer_launches"] or not sp.get("walk_points"):
+        return None
+    avg_ms = sp["steer_ms"] / launches
+    pts = sp["walk_points"] / launches
+    achieved = pts / (avg_ms * 1e-3)
+    r = {"kernel": f"steer_walk ({name})", "bound": "valu", "achieved": round(achieved / 1e9, 4),
+         "unit": "Gpoints/s", "avg_launch_ms": round(avg_ms, 5), "points_per_launch": int(pts),
+         "traffic": pmc.get("hbm_bytes_per_launch"),
+         "measured": f"HIP events around steer_walk, {sp['steer_launches']} launches of the "
+                     "profiled pass"}
+    vpp = pmc.get("valu_insts_per_point")
+    if vpp:
+        simds = 4 * pmc.get("cus", 256)
+        peak = simds * CLOCK_GHZ * 1e9 / (vpp / 64.0 * VALU_CYC)
+        r.update(peak=round(peak / 1e9, 4), frac=round(achieved / peak, 4),
+                 valu_insts_per_point=vpp,
+                 note="peak = points/s if every SIMD issued one wave64 VALU instruction per 2 "
+                      "cycles at 2.4 GHz with the measured instruction count per point (f64 and "
+                      "transcendental instructions take longer: the true bound is lower)")
+    return r
 
 
-def cpu_baseline(raw, p, args):
-    """The oracle restatement (oracle/, C) on the SAME workload: continue the GPU's 100k-node tree
-    re-verifying the whole line to the root like the reference's verify_node (rrt.rs:414-426).
-      1. one core, time-capped (a few seconds): the per-core rate, and the incremental-verify
-         rate beside it;
-      2. all host cores: one independent replica per thread (seed + r), each continuing the same
-         tree for the per-core rate x cpu_seconds iterations — the CPU analogue of the GPU's
-         replicas, timed on the wall clock."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle  # noqa: E402  (cpu_baseline leg: the oracle is the timed CPU port here)
+def run_tree(args, D, raw, workload, with_cpu):
+    """Config 2 / 4 / polygons: grow a tree to args.nodes (untimed; windows at ~1k and ~10k nodes
+    timed on the way), W warmup windows, then `steps` windows timed back to back, then a profiled
+    pass of as many windows (HIP events around the screen and the walk)."""
+    steps = args.steps or 20
+    p = make_planner(raw, args.seed + D.rank, args.window, D.device)
+    sweep = {}
+    marks = [] if args.no_size_sweep else [1_000, 10_000]
+    while p.tree_size() < args.nodes:
+        if marks and p.tree_size() >= marks[0]:
+            m = marks.pop(0)
+            n0 = p.tree_size()
+            p.reset_stats()
+            dt = timed_windows(p, 5, args.window)
+            st = p.stats()
+            sweep[str(m)] = {"iterations_per_s": st["iterations"] / dt, "tree_nodes": n0,
+                             "ms_per_window": round(1e3 * dt / max(st["windows"], 1), 4),
+                             "stats": {k: st[k] for k in STAT_KEYS}}
+        p.extend(args.window)
+    p.extend(args.warmup * args.window)
+    p.synchronize()
+    n_start = p.tree_size()
+    p.reset_stats()
+    D.barrier()
+    p.synchronize()
+    t0 = time.perf_counter()
+    p.extend(steps * args.window)  # the K steps back to back (windows enqueued without sync)
+    p.synchronize()
+    t_local = time.perf_counter() - t0
+    D.barrier()
+    st = p.stats()
+    t_max = D.allreduce(t_local, "max")
+    iters_total = D.allreduce(st["iterations"], "sum")
+    sweep[str(args.nodes)] = {"iterations_per_s": st["iterations"] / t_local,
+                              "tree_nodes": n_start,
+                              "ms_per_window": round(1e3 * t_local / max(st["windows"], 1), 4),
+                              "stats": {k: st[k] for k in STAT_KEYS}}
+    p.reset_stats()
+    p.set_profiling(True)
+    p.extend(steps * args.window)
+    p.synchronize()
+    p.set_profiling(False)
+    sp = p.stats()
+    tag = {"config2": "", "config4": "_config4", "polygons": "_polygons"}[workload]
+    res = {
+        "value": iters_total / t_max, "t_max": t_max, "steps": steps, "n_start": n_start,
+        "node_evals_per_s_per_gpu": round(st["node_evals"] / t_local, 1),
+        "sizes": sweep, "stats": {k: st[k] for k in STAT_KEYS},
+        "roofline": screen_roofline(sp, load_profile(f"window_kernel_pmc{tag}.json")),
+        "walk_roofline": walk_roofline(sp, load_profile(f"steer_walk_pmc{tag}.json"), workload),
+    }
+    if with_cpu:
+        res["cpu_baseline"] = cpu_baseline_tree(raw, p, args)
+    p.close()
+    return res
 
+
+def cpu_baseline_tree(raw, p, args):
+    """The oracle restatement (oracle/, C) on the SAME workload: continue the GPU's tree
+    re-verifying the whole line to the root like the reference's verify_node (rrt.rs:414-426):
+    one core time-capped (plus the incremental-verify rate beside it), then one independent
+    replica per host thread (seed + r) for the per-core rate x cpu_seconds iterations each."""
+    oracle = oracle_mod()
     x, y, yaw, par = p.tree()
     it0 = p.iteration()
     sc = oracle.OracleScene.from_raw(raw)
@@ -175,22 +407,159 @@ def cpu_baseline(raw, p, args):
         out[name] = (done / t_used, done, t_used)
     threads = host_threads()
     per = max(16, int(out["full_reverify"][0] * args.cpu_seconds))
-    seeds = [args.seed + 1000 + r for r in range(threads)]
     t0 = time.perf_counter()
-    oracle.extend_replicas(sc, tr, seeds, it0, per, threads, full_reverify=True)
+    oracle.extend_replicas(sc, tr, [args.seed + 1000 + r for r in range(threads)], it0, per,
+                           threads, full_reverify=True)
     t = time.perf_counter() - t0
-    out["all_cores"] = (threads * per / t, threads * per, t, threads, per)
+    v, nn, tt = out["full_reverify"]
+    vi, ni, ti = out["incremental"]
+    return {
+        "value": round(threads * per / t, 2), "unit": "iterations/s", "cores": threads,
+        "kind": "port",
+        "sample": f"{threads} independent replicas on {threads} host threads, each continuing the "
+                  f"same {n}-node tree for {per} iterations (seeds {args.seed + 1000}..), "
+                  f"re-verifying the whole line to the root like rrt.rs:414-426, exact brute-force "
+                  f"NN (the crate's R-tree is rstar, not buildable here); "
+                  f"{threads * per} iterations in {t:.1f} s wall",
+        "one_core": {"value": round(v, 2), "iterations": nn, "seconds": round(tt, 2)},
+        "incremental_verify_one_core": {"value": round(vi, 2), "iterations": ni,
+                                        "seconds": round(ti, 2)},
+        "host": host_info(),
+    }
+
+
+# --------------------------------------------------------------------- query batches (3 / 5)
+def batch_digests(batch, star=False):
+    """Per-query 64-bit digest of the tree (x, y bits and parents, root first): equal digests on
+    every rank count mean the sharded run built exactly the 1-rank run's trees."""
+    n = batch.state()[0]
+    out = np.zeros(len(n), dtype=np.int64)
+    for q in range(len(n)):
+        t = batch.tree(q, int(n[q]))
+        h = hashlib.blake2b(digest_size=8)
+        h.update(np.ascontiguousarray(t[0]).tobytes())
+        h.update(np.ascontiguousarray(t[1]).tobytes())
+        h.update(np.ascontiguousarray(t[3]).tobytes())
+        out[q] = np.frombuffer(h.digest(), dtype=np.int64)[0]
     return out
 
 
-def cpu_baseline_queries(raw, starts, seeds, max_iter, seconds):
-    """config 3's CPU baseline: the oracle (C) runs whole queries of the same batch — query q from
-    its own start with its own seed, max_iter iterations each, the reference's full re-verify of
-    the line to the root (rrt.rs:414-426) — first on one core (a few seconds: the per-query time),
-    then a batch of them on all host cores, one query per thread at a time (wall clock)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle  # noqa: E402  (cpu_baseline leg: the oracle is the timed CPU port here)
+def run_batch(args, D, star, with_cpu):
+    """Config 3 (star=False) / config 5 (star=True): args.queries independent planners, sharded
+    contiguously over the ranks; a step = one lockstep iteration of every query of the rank; the
+    timed region is the whole max_iter-step run of a fresh batch after an untimed warmup batch;
+    then a profiled pass of the same run (HIP events around the NN and the walk)."""
+    from pathplanning_amd import rrt, scenes
 
+    raw = scenes.config5_field() if star else scenes.field512()
+    space = rrt.Space.from_raw(raw)
+    a, b = shard(args.queries, D.world, D.rank)
+    starts, goals, seeds = scenes.config3_queries(raw, a, b - a)
+    steps = args.max_iter if args.steps is None else args.steps
+    eta = scenes.CONFIG5_ETA
+
+    def fresh():
+        if star:
+            return rrt.RRTStarBatch(starts, args.max_iter, raw["step_size"], space, seeds, k=0,
+                                    eta=eta, device=D.device)
+        return rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
+                            device=D.device, window=args.batch_window)
+
+    batch = fresh()
+    batch.extend(args.warmup)  # untimed warmup on a throwaway run
+    batch.close()
+    batch = fresh()
+    D.barrier()
+    t0 = time.perf_counter()
+    batch.extend(steps)
+    t_local = time.perf_counter() - t0
+    D.barrier()
+    stt = batch.state()
+    n, its = stt[0], stt[1]
+    dig = batch_digests(batch, star)
+    rec = np.stack([np.arange(a, b, dtype=np.int64), its.astype(np.int64), n.astype(np.int64),
+                    dig], 1)
+    allrec = D.gather_records(rec).numpy()
+    t_max = D.allreduce(t_local, "max")
+    iters_total = int(allrec[:, 1].sum())
+    extra = {}
+    if star:
+        extra["rewires_total"] = int(D.allreduce(float(stt[3].sum()), "sum"))
+    # profiled pass (same workload): HIP events around the NN and the walks of every step
+    batch.close()
+    batch = fresh()
+    batch.set_profiling(True)
+    batch.extend(steps)
+    sp = batch.stats()
+    evals_p = batch.state()[2] if star else batch.state(with_evals=True)[2]
+    batch.close()
+    nn_ms = sp["nn_scan_ms"] / max(sp["nn_scan_launches"], 1)
+    evals_per_launch = float(evals_p.sum()) / max(sp["nn_scan_launches"], 1)
+    bytes_per_eval = 16  # f64 x + f64 y of one SoA row (exact NN)
+    achieved = evals_per_launch * bytes_per_eval / (nn_ms * 1e-3) / 1e9
+    wl = "config5" if star else "config3"
+    pmc = load_profile("batch_pmc.json").get(wl, {}) if args.queries == 8192 else {}
+    nn_share = sp["nn_scan_ms"] / max(sp["nn_scan_ms"] + sp["steer_ms"], 1e-9)
+    res = {
+        "value": round(iters_total / t_max, 1),
+        "unit": "iterations/s",
+        "n_gpus": D.world,
+        "scaling": "strong",
+        "ms_total": round(1e3 * t_max, 3),
+        "steps": steps,
+        "queries": args.queries,
+        "queries_per_rank": b - a,
+        "max_iter": args.max_iter,
+        "parallelism": f"query-shard{D.world}",
+        "gather": f"all_gather of per-query records ({D.gather_backend or 'none: one rank'})",
+        "iterations_total": iters_total,
+        "nodes_total": int(allrec[:, 2].sum()),
+        "records_digest": hashlib.sha256(allrec.astype(np.int64).tobytes()).hexdigest()[:16],
+        "roofline": walk_roofline(sp, pmc.get("steer_walk", {}), wl),
+        "nn_roofline": {
+            "kernel": "star_sample (exact f64 NN)" if star else "mq_sample_nn (exact f64 NN)",
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": pmc.get("nn", {}).get("hbm_bytes_per_launch"),
+            "avg_launch_ms": round(nn_ms, 5), "evals_per_launch": int(evals_per_launch),
+            "bytes_per_eval": bytes_per_eval,
+            "share_of_nn_plus_walk_time": round(nn_share, 4),
+        },
+        **extra,
+    }
+    if star:
+        res["workload"] = (f"config5 (stretch, build-defined RRT*): {args.queries} queries on "
+                           f"{raw['name']} (10240 discs r~U(1,4) on 2048^2), Steer eta {eta}, "
+                           f"k = ceil(2e ln n) <= 63, max_iter {args.max_iter}")
+    else:
+        res["workload"] = (f"config3: {args.queries} independent queries on the config-2 field "
+                           f"(query q: seed 42+q, start/goal from stream q), max_iter "
+                           f"{args.max_iter}")
+        res["window_per_query"] = args.batch_window or auto_batch_window(b - a)
+    if with_cpu:
+        res["cpu_baseline"] = (cpu_baseline_star(raw, starts, seeds, args.max_iter, eta,
+                                                 args.cpu_seconds) if star else
+                               cpu_baseline_queries(raw, starts, seeds, args.max_iter,
+                                                    args.cpu_seconds))
+    return res
+
+
+def auto_batch_window(q):
+    """pp_batch_new's automatic window: 32 for at most 2048 queries, else the largest power of
+    two <= 16 with q * K <= 131072."""
+    if q <= 2048:
+        return 32
+    k = 1
+    while k < 16 and q * k * 2 <= 131072:
+        k *= 2
+    return k
+
+
+def cpu_baseline_queries(raw, starts, seeds, max_iter, seconds):
+    """config 3's CPU baseline: the oracle (C) runs whole queries of the same batch (full
+    re-verify of the line to the root, rrt.rs:414-426): first on one core (the per-query time),
+    then a batch of them on all host threads, one query per thread at a time (wall clock)."""
+    oracle = oracle_mod()
     sc = oracle.OracleScene.from_raw(raw)
     done, t_used, nq = 0, 0.0, 0
     for q in range(len(seeds)):
@@ -202,303 +571,26 @@ def cpu_baseline_queries(raw, starts, seeds, max_iter, seconds):
         nq += 1
         if t_used >= seconds / 3.0:
             break
-    one = (done / t_used, done, nq, t_used)
     threads = host_threads()
-    per_query = t_used / nq
-    qn = int(min(len(seeds), max(threads, threads * seconds / per_query)))
+    qn = int(min(len(seeds), max(threads, threads * seconds / (t_used / nq))))
     t0 = time.perf_counter()
     oracle.queries(sc, starts[:qn], seeds[:qn], max_iter, threads, full_reverify=True)
     t = time.perf_counter() - t0
-    return one, (qn * max_iter / t, qn * max_iter, qn, t, threads)
-
-
-def load_traffic():
-    """HBM bytes per nn_scan launch from the committed rocprofv3 PMC summary (or None)."""
-    path = os.path.join(ROOT, "profiles", "nn_scan_traffic.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
-
-
-def load_batch_traffic(workload):
-    """HBM bytes per whole-batch NN launch of config 3 / 5 from the committed rocprofv3 PMC
-    summary (scripts/traffic_summary.py), or None."""
-    path = os.path.join(ROOT, "profiles", "batch_nn_traffic.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        return json.load(f).get(workload, {}).get("hbm_bytes_per_launch")
-
-
-def gather_records(dist, rec, backend):
-    """The config-3 result gather: every rank's per-query records to every rank (one
-    all_gather; RCCL over xGMI when the backend is nccl).  rec: int64 [q_rank, 3]."""
-    import torch
-
-    if dist is None:
-        return torch.from_numpy(rec)
-    world = dist.get_world_size()
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else None
-    n = torch.tensor([rec.shape[0]], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    mx = int(max(int(v.item()) for v in sizes))
-    pad = torch.zeros((mx, 3), dtype=torch.int64, device=dev)
-    pad[: rec.shape[0]] = torch.from_numpy(rec).to(pad.device)
-    outs = [torch.zeros_like(pad) for _ in range(world)]
-    dist.all_gather(outs, pad)
-    return torch.cat([o[: int(sz.item())].cpu() for o, sz in zip(outs, sizes)])
-
-
-def main():
-    args = parse()
-    if args.workload == "config3":
-        return main_config3(args)
-    if args.workload == "config5":
-        return main_config5(args)
-    if args.steps is None:
-        args.steps = 20
-    dist, world, rank, local = dist_setup(args)
-    from pathplanning_amd import scenes
-
-    raw = {"config4": scenes.field512_grid, "polygons": scenes.field512_polygons}.get(
-        args.workload, scenes.field512)()
-    p = make_planner(raw, args.seed + rank, args.window, local)
-    sweep = {}
-    # grow the tree (untimed); on the way time a few windows at 1k and 10k nodes
-    marks = [] if args.no_size_sweep else [1_000, 10_000]
-    while p.tree_size() < args.nodes:
-        if marks and p.tree_size() >= marks[0]:
-            m = marks.pop(0)
-            n0, it0 = p.tree_size(), p.iteration()
-            dt = timed_windows(p, 5, args.window)
-            sweep[str(m)] = {"iterations_per_s": (p.iteration() - it0) / dt, "tree_nodes": n0}
-        p.extend(args.window)
-    p.extend(args.warmup * args.window)
-    p.synchronize()
-
-    n_start = p.tree_size()
-    p.reset_stats()
-    barrier(dist)
-    p.synchronize()
-    t0 = time.perf_counter()
-    p.extend(args.steps * args.window)  # the K steps back to back (windows enqueued without sync)
-    p.synchronize()
-    t_local = time.perf_counter() - t0
-    barrier(dist)
-    st = p.stats()
-    t_max = allreduce_max(dist, t_local)
-    iters_total = allreduce_sum(dist, st["iterations"])
-    value = iters_total / t_max
-    sweep[str(args.nodes)] = {"iterations_per_s": st["iterations"] / t_local, "tree_nodes": n_start}
-
-    # profiled pass over the same workload (the next `steps` windows): HIP events on the planner's
-    # stream around nn_scan and steer_window.  Kept out of the timed region above because every
-    # event record adds a few microseconds of queue gap between the kernels.
-    p.reset_stats()
-    p.set_profiling(True)
-    p.extend(args.steps * args.window)
-    p.synchronize()
-    p.set_profiling(False)
-    sp = p.stats()
-
-    # dominant kernel (nn_scan): algorithmic work per launch / average launch duration (HIP events)
-    launches = max(sp["nn_scan_launches"], 1)
-    avg_ms = sp["nn_scan_ms"] / launches
-    evals_per_launch = sp["node_evals"] / launches
-    achieved_tflops = evals_per_launch * FLOP_PER_EVAL / (avg_ms * 1e-3) / 1e12
-    roofline = {
-        "kernel": "window_kernel (NN screen; workgroup 0 resolves the previous window)",
-        "bound": "valu",
-        "achieved": round(achieved_tflops, 3),
-        "peak": F32_VALU_PEAK_TFLOPS,
-        "unit": "TFLOP/s",
-        "frac": round(achieved_tflops / F32_VALU_PEAK_TFLOPS, 4),
-        "traffic": load_traffic(),
-        "avg_launch_ms": round(avg_ms, 5),
-        "evals_per_launch": int(evals_per_launch),
-        "algorithmic_hbm_view": {
-            "bytes_per_eval": BYTES_PER_EVAL,
-            "achieved_GBs": round(evals_per_launch * BYTES_PER_EVAL / (avg_ms * 1e-3) / 1e9, 1),
-            "peak_GBs": HBM_PEAK_GBS,
-            "note": "8 B/eval as if every eval read its node from HBM (SURVEY §8d); > peak means "
-                    "the batch reuses each node across 256 samples per wave, so VALU is the bound",
-        },
-        "steer_avg_launch_ms": round(sp["steer_ms"] / max(sp["steer_launches"], 1), 5),
-        "measured": f"HIP events on the planner stream, {sp['nn_scan_launches']} launches of the "
-                    "profiled pass that follows the timed region (same workload)",
-    }
-
-    line = {
-        "metric": "RRT extend iterations/sec (2D Dubins, 1k obstacles)",
-        "value": round(value, 1),
-        "unit": "iterations/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1e3 * t_max / args.steps, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic",
-        "config": {
-            "workload": {"config4": "config4: field512 rasterised to a 512x512 bit-packed "
-                                    "occupancy grid (32 KB, point probes)",
-                         "polygons": "polygons: field512's 1024 discs as create_circle polygons "
-                                     f"({sum(len(o) for o in raw.get('obstacle_polygons', []))} "
-                                     "edges, Minkowski buffers, SURVEY §8f row 3)"}.get(
-                             args.workload, "config2: field512 (1024 discs r~U(2,8), 512x512)")
-                        + f", R=4.0, step 0.1, K={args.window} candidates/window, tree grown to "
-                        f"{args.nodes} nodes",
-            "window": args.window,
-            "tree_nodes_at_start": n_start,
-            "obstacles": len(raw.get("obstacle_polygons", raw["circles"])),
-            "parallelism": f"replicas{world}",
-            "nn_screen_dtype": "f32 (exact f64 rescan of near-ties)",
-        },
-        "node_evals_per_s_per_gpu": round(st["node_evals"] / t_local, 1),
-        "sizes": sweep,
-        "stats": {k: st[k] for k in ("iterations", "accepted", "windows", "truncations",
-                                     "repair_rounds", "repairs", "literal_repairs", "nn_flagged")},
-        "roofline": roofline,
-        "cpu_baseline": None,
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(raw, p, args)
-        v, n, t = cb["full_reverify"]
-        vi, ni, ti = cb["incremental"]
-        va, na, ta, th, per = cb["all_cores"]
-        line["cpu_baseline"] = {
-            "value": round(va, 2), "unit": "iterations/s", "cores": th, "kind": "port",
-            "sample": f"{th} independent replicas on {th} host threads, each continuing the same "
-                      f"{n_start}-node tree for {per} iterations (seeds {args.seed + 1000}..), "
-                      f"re-verifying the whole line to the root like rrt.rs:414-426; "
-                      f"{na} iterations in {ta:.1f} s wall",
-            "one_core": {"value": round(v, 2), "iterations": n, "seconds": round(t, 2)},
-            "incremental_verify_one_core": {"value": round(vi, 2), "iterations": ni,
-                                            "seconds": round(ti, 2)},
-        }
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    p.close()
-    if dist is not None:
-        dist.destroy_process_group()
-
-
-def main_config3(args):
-    """BASELINE config 3: `queries` independent planners on the config-2 field (query q: seed
-    42 + q, start/goal from stream q), max_iter each, sharded contiguously over the ranks; a step
-    = one lockstep extend iteration of every query of the rank.  Strong scaling: the total work is
-    fixed, each rank runs queries/world of it; one all_gather of per-query records at the end."""
-    import torch
-
-    backend = "nccl" if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and
-                         torch.cuda.is_available()) else "gloo"
-    dist, world, rank, local = dist_setup(args, backend)
-    from pathplanning_amd import rrt, scenes
-
-    raw = scenes.field512()
-    space = rrt.Space.from_raw(raw)
-    a, b = shard(args.queries, world, rank)
-    starts, goals, seeds = scenes.config3_queries(raw, a, b - a)
-    steps = args.max_iter if args.steps is None else args.steps
-    batch = rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
-                         device=local, window=args.batch_window)
-    batch.extend(args.warmup)  # untimed warmup on a throwaway run
-    batch.close()
-    batch = rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
-                         device=local, window=args.batch_window)
-    barrier(dist)
-    t0 = time.perf_counter()
-    it_local, acc_local = batch.extend(steps)
-    t_local = time.perf_counter() - t0
-    barrier(dist)
-    n, its, evals = batch.state(with_evals=True)
-    rec = np.stack([np.arange(a, b, dtype=np.int64), its.astype(np.int64), n.astype(np.int64)], 1)
-    allrec = gather_records(dist, rec, backend)
-    t_max = allreduce_max(dist, t_local)
-    iters_total = int(allrec[:, 1].sum())
-    value = iters_total / t_max
-    # profiled pass (same workload): HIP events around the batch NN kernel of every step
-    batch.close()
-    batch = rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
-                         device=local, window=args.batch_window)
-    batch.set_profiling(True)
-    batch.extend(steps)
-    sp = batch.stats()
-    _, _, evals_p = batch.state(with_evals=True)
-    nn_ms = sp["nn_scan_ms"] / max(sp["nn_scan_launches"], 1)
-    evals_per_launch = float(evals_p.sum()) / max(sp["nn_scan_launches"], 1)
-    bytes_per_eval = 16  # f64 x + f64 y of one SoA row (exact NN, no f32 screen here)
-    achieved = evals_per_launch * bytes_per_eval / (nn_ms * 1e-3) / 1e9
-    line = {
-        "metric": "RRT extend iterations/sec (2D Dubins, 1k obstacles)",
-        "value": round(value, 1),
-        "unit": "iterations/s",
-        "n_gpus": world,
-        "steps": steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1e3 * t_max / steps, 4),
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic",
-        "config": {
-            "workload": f"config3: {args.queries} independent queries on the config-2 field "
-                        f"(query q: seed 42+q, start/goal from stream q), max_iter "
-                        f"{args.max_iter}, sharded contiguously over {world} rank(s)",
-            "queries": args.queries,
-            "queries_per_rank": b - a,
-            "parallelism": f"query-shard{world}",
-            "window_per_query": args.batch_window or auto_batch_window(b - a),
-            "gather": f"all_gather of per-query records ({backend})",
-        },
-        "iterations_total": iters_total,
-        "nodes_total": int(allrec[:, 2].sum()),
-        "roofline": {
-            "kernel": "mq_sample_nn",
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": load_batch_traffic("config3") if args.queries == 8192 else None,
-            "avg_launch_ms": round(nn_ms, 5),
-            "evals_per_launch": int(evals_per_launch),
-            "bytes_per_eval": bytes_per_eval,
-            "measured": f"HIP events around mq_sample_nn, {sp['nn_scan_launches']} launches of "
-                        "the profiled pass that follows the timed region (same workload)",
-        },
-        "cpu_baseline": None,
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        (v, n, nq, t), (va, na, qa, ta, th) = cpu_baseline_queries(
-            raw, starts, seeds, args.max_iter, args.cpu_seconds)
-        line["cpu_baseline"] = {
-            "value": round(va, 2), "unit": "iterations/s", "cores": th, "kind": "port",
-            "sample": f"the first {qa} whole queries of the same batch ({na} iterations, max_iter "
-                      f"{args.max_iter} each, full re-verify like rrt.rs:414-426) on {th} host "
-                      f"threads, {ta:.1f} s wall",
-            "one_core": {"value": round(v, 2), "queries": nq, "iterations": n,
-                         "seconds": round(t, 2)},
-        }
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    batch.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return {"value": round(qn * max_iter / t, 2), "unit": "iterations/s", "cores": threads,
+            "kind": "port",
+            "sample": f"the first {qn} whole queries of the same batch ({qn * max_iter} "
+                      f"iterations, max_iter {max_iter} each, full re-verify like "
+                      f"rrt.rs:414-426) on {threads} host threads, {t:.1f} s wall",
+            "one_core": {"value": round(done / t_used, 2), "queries": nq, "iterations": done,
+                         "seconds": round(t_used, 2)},
+            "host": host_info()}
 
 
 def cpu_baseline_star(raw, starts, seeds, max_iter, eta, seconds):
     """config 5's CPU baseline: the RRT* oracle (C, orc_star_extend) on the same queries — query
     0 on one core in chunks of 100 iterations until seconds/3 (or max_iter), then `threads` whole
     queries of the batch, each for that many iterations, one per host thread (wall clock)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle  # noqa: E402  (cpu_baseline leg: the oracle is the timed CPU port here)
-
+    oracle = oracle_mod()
     sc = oracle.OracleScene.from_raw(raw)
     tr = oracle.OracleStarTree(tuple(starts[0]), max_iter + 1)
     done, t_used = 0, 0.0
@@ -512,116 +604,223 @@ def cpu_baseline_star(raw, starts, seeds, max_iter, eta, seconds):
     t0 = time.perf_counter()
     oracle.star_queries(sc, starts[:threads], seeds[:threads], done, 0, eta, threads)
     t = time.perf_counter() - t0
-    return (done / t_used, done, t_used), (threads * done / t, threads * done, threads, t, done)
+    return {"value": round(threads * done / t, 2), "unit": "iterations/s", "cores": threads,
+            "kind": "port",
+            "sample": f"the first {threads} queries of the same batch, their first {done} RRT* "
+                      f"iterations each ({threads * done} iterations), on {threads} host "
+                      f"threads, {t:.1f} s wall",
+            "one_core": {"value": round(done / t_used, 2), "iterations": done,
+                         "seconds": round(t_used, 2)},
+            "host": host_info()}
 
 
-def main_config5(args):
-    """BASELINE config 5 (stretch; build-defined RRT*): `queries` independent
-    k-nearest RRT* planners on a 10240-disc field (scenes.config5_field, Steer eta = 16, k =
-    ceil(2e ln n)), max_iter each, sharded contiguously over the ranks like config 3; a step = one
-    lockstep RRT* iteration of every query of the rank; one all_gather of records at the end."""
-    import torch
+# ------------------------------------------------------------------ config 1 and plan (bench6)
+def run_config1(args, D, with_cpu):
+    """BASELINE config 1: the reference's only fully specified scene (benches/all.rs:8-42) —
+    8000 plan_one extend iterations (plan_one minus check_finish, rrt.rs:583-589) of one query
+    from a fresh tree.  GPU: the whole run per window size K (results identical for every K);
+    CPU: the C port's sequential run on one core with the reference's full re-verify."""
+    from pathplanning_amd import scenes
 
-    backend = "nccl" if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and
-                         torch.cuda.is_available()) else "gloo"
-    dist, world, rank, local = dist_setup(args, backend)
-    from pathplanning_amd import rrt, scenes
+    raw = scenes.bench6()
+    n_iter = raw["max_iter"]
+    runs = {}
+    for K in (32, 128, 512, 4096):
+        best = None
+        for rep in range(2):  # the first run of a K warms its buffers
+            p = make_planner(raw, args.seed, K, D.device, capacity=1 << 14)
+            p.synchronize()
+            t0 = time.perf_counter()
+            acc = p.extend(n_iter)
+            p.synchronize()
+            dt = time.perf_counter() - t0
+            st = p.stats()
+            p.close()
+            if rep == 1:
+                best = {"iterations_per_s": round(n_iter / dt, 1), "ms": round(1e3 * dt, 3),
+                        "nodes": acc + 1, "stats": {k: st[k] for k in STAT_KEYS}}
+        runs[str(K)] = best
+    kbest = max(runs, key=lambda k: runs[k]["iterations_per_s"])
+    res = {"value": runs[kbest]["iterations_per_s"], "unit": "iterations/s", "window": int(kbest),
+           "workload": "config1: bench6 (benches/all.rs:8-42: 6 discs, R 0.8, step 0.1), seed "
+                       f"{args.seed}, {n_iter} iterations from the root",
+           "per_window": runs}
+    if with_cpu:
+        oracle = oracle_mod()
+        sc = oracle.OracleScene.from_raw(raw)
+        tr = oracle.OracleTree(raw["start"], n_iter + 1)
+        t0 = time.perf_counter()
+        acc, _, _ = oracle.rrt_extend(sc, tr, args.seed, 0, n_iter, full_reverify=True)
+        t = time.perf_counter() - t0
+        res["cpu_baseline"] = {
+            "value": round(n_iter / t, 1), "unit": "iterations/s", "cores": 1, "kind": "port",
+            "sample": f"the same {n_iter} iterations (seed {args.seed}), sequential, full "
+                      f"re-verify (rrt.rs:414-426), {t:.2f} s; {acc + 1} nodes like the GPU",
+            "nodes": acc + 1}
+    return res
 
-    raw = scenes.config5_field()
-    eta = scenes.CONFIG5_ETA
-    space = rrt.Space.from_raw(raw)
-    a, b = shard(args.queries, world, rank)
-    starts, _, seeds = scenes.config3_queries(raw, a, b - a)
-    steps = args.max_iter if args.steps is None else args.steps
 
-    def fresh():
-        return rrt.RRTStarBatch(starts, args.max_iter, raw["step_size"], space, seeds, k=0,
-                                eta=eta, device=local)
+def run_plan(args, D, with_cpu):
+    """RRT::plan (rrt.rs:599-619) on bench6_open, sequential spec: 8000 plan_one iterations with
+    check_finish (optimize + finalize + verify, rrt.rs:428-540) on every accepted node, the first
+    minimum euclidean_length.  GPU pp_rrt_plan against the C port's plan on one core."""
+    from pathplanning_amd import scenes
 
-    batch = fresh()
-    batch.extend(args.warmup)  # untimed warmup on a throwaway run
-    batch.close()
-    batch = fresh()
-    barrier(dist)
-    t0 = time.perf_counter()
-    batch.extend(steps)
-    t_local = time.perf_counter() - t0
-    barrier(dist)
-    n, its, evals, rw = batch.state()
-    rec = np.stack([np.arange(a, b, dtype=np.int64), its.astype(np.int64), n.astype(np.int64)], 1)
-    allrec = gather_records(dist, rec, backend)
-    t_max = allreduce_max(dist, t_local)
-    iters_total = int(allrec[:, 1].sum())
-    rewires_total = int(allreduce_sum(dist, float(rw.sum())))
-    value = iters_total / t_max
-    # profiled pass (same workload): HIP events around star_sample (the exact NN) of every step
-    batch.close()
-    batch = fresh()
-    batch.set_profiling(True)
-    batch.extend(steps)
-    sp = batch.stats()
-    evals_p = batch.state()[2]
-    nn_ms = sp["nn_scan_ms"] / max(sp["nn_scan_launches"], 1)
-    evals_per_launch = float(evals_p.sum()) / max(sp["nn_scan_launches"], 1)
-    bytes_per_eval = 16  # f64 x + f64 y of one SoA row
-    achieved = evals_per_launch * bytes_per_eval / (nn_ms * 1e-3) / 1e9
-    line = {
-        "metric": "RRT* iterations/sec (SE(2) Dubins, k-nearest rewire, 10k obstacles)",
-        "value": round(value, 1),
+    raw = scenes.bench6_open()
+    n_iter = raw["max_iter"]
+    best = None
+    for rep in range(2):
+        p = make_planner(raw, args.seed, 512, D.device, capacity=1 << 14)
+        p.synchronize()
+        t0 = time.perf_counter()
+        line = p.plan(n_iter)
+        dt = time.perf_counter() - t0
+        bn, bl, nf = p.last_plan
+        # the check_finish share: the same nodes' check_finish batch on its own
+        nodes = np.arange(1, p.tree_size(), dtype=np.int32)
+        t1 = time.perf_counter()
+        p.check_finish_batch(nodes)
+        dcf = time.perf_counter() - t1
+        p.close()
+        best = {"plan_calls_per_s": round(n_iter / dt, 1), "ms": round(1e3 * dt, 3),
+                "best_node": bn, "best_length": bl, "finishes": nf,
+                "line_points": 0 if line is None else len(line),
+                "check_finish_nodes": len(nodes),
+                "check_finish_ms": round(1e3 * dcf, 3),
+                "check_finish_per_s": round(len(nodes) / dcf, 1)}
+    res = {"value": best["plan_calls_per_s"], "unit": "plan_one calls/s (with check_finish)",
+           "workload": f"plan: bench6_open (bench6 scene, start (-3, -3, 45 deg)), seed "
+                       f"{args.seed}, RRT::plan with {n_iter} iterations", **best}
+    if with_cpu:
+        oracle = oracle_mod()
+        sc = oracle.OracleScene.from_raw(raw)
+        tr = oracle.OracleTree(raw["start"], n_iter + 1)
+        t0 = time.perf_counter()
+        acc, obn, obl, _ = oracle.plan(sc, tr, args.seed, 0, n_iter, raw["goal"][:2],
+                                       raw["goal"][2], full_reverify=True)
+        t = time.perf_counter() - t0
+        res["cpu_baseline"] = {
+            "value": round(n_iter / t, 1), "unit": "plan_one calls/s", "cores": 1,
+            "kind": "port",
+            "sample": f"the same plan (seed {args.seed}, {n_iter} iterations, full re-verify), "
+                      f"sequential, {t:.2f} s; best node {obn}, length {obl:.6f}",
+            "same_answer": bool(obn == best["best_node"] and abs(obl - best["best_length"])
+                                <= 1e-9 * max(1.0, abs(obl)))}
+    return res
+
+
+# ---------------------------------------------------------------------------------- main
+def tree_line(args, D, workload, raw, res):
+    wl = {"config4": "config4: field512 rasterised to a 512x512 bit-packed occupancy grid "
+                     "(32 KB, point probes)",
+          "polygons": "polygons: field512's 1024 discs as create_circle polygons "
+                      f"({sum(len(o) for o in raw.get('obstacle_polygons', []))} edges, "
+                      "Minkowski buffers, SURVEY §8f row 3)"}.get(
+        workload, "config2: field512 (1024 discs r~U(2,8), 512x512)")
+    return {
+        "metric": METRIC,
+        "value": round(res["value"], 1),
         "unit": "iterations/s",
-        "n_gpus": world,
-        "steps": steps,
+        "n_gpus": D.world,
+        "steps": res["steps"],
         "warmup": args.warmup,
-        "ms_per_step": round(1e3 * t_max / steps, 4),
+        "ms_per_step": round(1e3 * res["t_max"] / res["steps"], 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": f"config5 (stretch, build-defined RRT*): {args.queries} independent "
-                        f"queries on {raw['name']} (10240 discs r~U(1,4) on 2048^2), Steer eta "
-                        f"{eta}, k = ceil(2e ln n) <= 63, max_iter {args.max_iter}, sharded "
-                        f"contiguously over {world} rank(s)",
-            "queries": args.queries,
-            "queries_per_rank": b - a,
-            "parallelism": f"query-shard{world}",
-            "gather": f"all_gather of per-query records ({backend})",
+            "workload": wl + f", R=4.0, step 0.1, K={args.window} candidates/window, tree grown "
+                             f"to {args.nodes} nodes",
+            "window": args.window,
+            "tree_nodes_at_start": res["n_start"],
+            "obstacles": len(raw.get("obstacle_polygons", raw["circles"])),
+            "parallelism": f"replicas{D.world}",
+            "nn_screen_dtype": "f32 (exact f64 rescan of near-ties)",
         },
-        "iterations_total": iters_total,
-        "nodes_total": int(allrec[:, 2].sum()),
-        "rewires_total": rewires_total,
-        "roofline": {
-            "kernel": "star_sample (exact f64 NN)",
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": load_batch_traffic("config5") if args.queries == 8192 else None,
-            "avg_launch_ms": round(nn_ms, 5),
-            "evals_per_launch": int(evals_per_launch),
-            "bytes_per_eval": bytes_per_eval,
-            "measured": f"HIP events around star_sample, {sp['nn_scan_launches']} launches of "
-                        "the profiled pass that follows the timed region (same workload)",
-        },
-        "cpu_baseline": None,
+        "node_evals_per_s_per_gpu": res["node_evals_per_s_per_gpu"],
+        "sizes": res["sizes"],
+        "stats": res["stats"],
+        "roofline": res["roofline"],
+        "walk_roofline": res["walk_roofline"],
+        "cpu_baseline": res.get("cpu_baseline"),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        (v, n1, t1), (va, na, th, ta, m) = cpu_baseline_star(raw, starts, seeds, args.max_iter,
-                                                             eta, args.cpu_seconds)
-        line["cpu_baseline"] = {
-            "value": round(va, 2), "unit": "iterations/s", "cores": th, "kind": "port",
-            "sample": f"the first {th} queries of the same batch, their first {m} RRT* "
-                      f"iterations each ({na} iterations), on {th} host threads, {ta:.1f} s wall",
-            "one_core": {"value": round(v, 2), "iterations": n1, "seconds": round(t1, 2)},
-        }
-    if rank == 0:
+
+
+def batch_line(args, D, res, star):
+    line = {
+        "metric": ("RRT* iterations/sec (SE(2) Dubins, k-nearest rewire, 10k obstacles)" if star
+                   else METRIC),
+        "value": res["value"], "unit": "iterations/s", "n_gpus": D.world, "steps": res["steps"],
+        "warmup": args.warmup, "ms_per_step": round(res["ms_total"] / res["steps"], 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": res["workload"], "queries": res["queries"],
+                   "queries_per_rank": res["queries_per_rank"],
+                   "parallelism": res["parallelism"], "gather": res["gather"]},
+    }
+    line.update({k: v for k, v in res.items() if k not in line and k not in (
+        "workload", "queries", "queries_per_rank", "parallelism", "gather", "steps", "ms_total")})
+    line.setdefault("cpu_baseline", None)
+    return line
+
+
+def sub(fn, *a):
+    """A sub-result: its dict, or the error that stopped it (the headline line still prints)."""
+    try:
+        return fn(*a)
+    except Exception as e:  # noqa: BLE001 — reported in the line, never hidden
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus)
+    D = Dist(args)
+    prov = provenance(args)
+    cpu = D.rank == 0 and D.world == 1 and not args.no_cpu_baseline
+    from pathplanning_amd import scenes
+
+    wl = args.workload
+    if wl in ("default", "config2", "config4", "polygons"):
+        tw = "config2" if wl == "default" else wl
+        raw = {"config4": scenes.field512_grid, "polygons": scenes.field512_polygons}.get(
+            tw, scenes.field512)()
+        line = tree_line(args, D, tw, raw, run_tree(args, D, raw, tw, cpu))
+        if wl == "default" and not args.no_sub:
+            sa = argparse.Namespace(**vars(args))
+            sa.steps = None  # the batches run their whole max_iter
+            line["config3"] = sub(run_batch, sa, D, False, cpu)
+            line["config5"] = sub(run_batch, sa, D, True, False)
+            if D.world == 1:
+                ta = argparse.Namespace(**vars(args))
+                ta.no_size_sweep = True
+                line["config4"] = sub(lambda: {k: v for k, v in run_tree(
+                    ta, D, scenes.field512_grid(), "config4", False).items()
+                    if k not in ("sizes", "t_max")})
+                line["config1"] = sub(run_config1, args, D, cpu)
+                line["plan"] = sub(run_plan, args, D, cpu)
+    elif wl in ("config3", "config5"):
+        line = batch_line(args, D, run_batch(args, D, wl == "config5", cpu), wl == "config5")
+    elif wl == "config1":
+        res = run_config1(args, D, cpu)
+        line = {"metric": METRIC, "n_gpus": D.world, "steps": 1, "warmup": 1,
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                "data": "synthetic", **res}
+    else:  # plan
+        res = run_plan(args, D, cpu)
+        line = {"metric": "RRT::plan calls/sec (plan_one with check_finish, bench6_open)",
+                "n_gpus": D.world, "steps": 1, "warmup": 1, "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+                **res}
+    line["provenance"] = prov
+    if D.rank == 0:
         print(json.dumps(line), flush=True)
-    batch.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    D.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

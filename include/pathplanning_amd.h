@@ -58,9 +58,10 @@ typedef struct pp_stats {
     int64_t node_evals;       /* sample-node distance evaluations of the NN screen */
     double nn_scan_ms;        /* device time of nn_scan, or of the batch NN (HIP events; profiling on) */
     int64_t nn_scan_launches;
-    double steer_ms;          /* device time of steer_window (HIP events; profiling on) */
+    double steer_ms;          /* device time of steer_walk (HIP events; profiling on) */
     int64_t steer_launches;
     int64_t stamps[8];        /* diagnostic builds only (-DPP_STAMPS): phase ticks (100 MHz) */
+    int64_t walk_points;      /* polyline points the steer walk generated and verified (profiling on) */
 } pp_stats;
 
 int pp_abi_version(void);

@@ -86,6 +86,7 @@ struct HBuf {  // pinned host staging
 };
 
 constexpr int kMaxBatch = 64;  // windows enqueued between two host synchronisations
+constexpr int kWalkTallySlots = 4096;  // >= any steer_walk grid (kWalkMaxWG, 1024 for L2 scenes)
 
 }  // namespace
 
@@ -175,6 +176,7 @@ struct pp_ctx {
     bool mq_any_blocked = false;
     int mq_K = 1;                 // speculative window per query of the current batch
     int mq_K_user = 0;            // pp_batch_set_window (0: automatic)
+    int mq_nsub = 1;              // sub-batches of the current batch (fixed at pp_batch_new)
     DBuf<int64_t> mq_target;      // [Q] iteration targets of the running pp_batch_extend
     DBuf<double> mq_nnd2;         // [Q * kMqMaxK]
     DBuf<SteerTask> mq_tasks;
@@ -207,9 +209,11 @@ struct pp_ctx {
 
     // ---- profiling
     bool prof = false;
-    std::vector<hipEvent_t> ev;  // 4 per window of a batch
+    std::vector<hipEvent_t> ev;  // 4 per window or batch step, 8 per RRT* step
     double nn_scan_ms = 0.0, steer_ms = 0.0;
     int64_t nn_scan_launches = 0, steer_launches = 0;
+    DBuf<long long> wg_pts;  // walked polyline points per walk workgroup (profiling on)
+    long long* prof_points() const { return prof ? wg_pts.p : nullptr; }
 
     ~pp_ctx() {
         for (auto& e : ev)
@@ -337,6 +341,7 @@ struct pp_ctx {
         a.rs.rep = r_rep.p;
         a.rs.repyaw = r_repyaw.p;
         a.lit_scratch = lit_scratch.p;
+        a.wg_points = prof_points();
         return a;
     }
 };
@@ -486,6 +491,7 @@ MqArgs mq_args(pp_ctx* c) {
     a.lit_scratch = c->api_lit_scratch.p;
     a.lit_locks = c->lit_locks.p;
     a.err = c->mq_err.p;
+    a.wg_points = c->prof_points();
     return a;
 }
 
@@ -531,7 +537,7 @@ MqArgs mq_sub_args(pp_ctx* c, int sub, int nsub) {
 // DevState 0: the whole batch; 1 + s: sub-batch s of mq_nsub
 int mq_write_states(pp_ctx* c, hipStream_t st) {
     DevState ds[1 + kMaxSub] = {};
-    const int Q = c->mq_Q, nsub = mq_nsub(Q);
+    const int Q = c->mq_Q, nsub = c->mq_nsub;
     ds[0].W = Q * c->mq_K;
     for (int s = 0; s < nsub; ++s)
         ds[1 + s].W = (int)((int64_t)Q * (s + 1) / nsub - (int64_t)Q * s / nsub) * c->mq_K;
@@ -625,6 +631,7 @@ StarArgs star_args(pp_ctx* c) {
     a.pdbuf = c->sr_pdbuf.p;
     a.lit_scratch = c->api_lit_scratch.p;
     a.err = c->sr_err.p;
+    a.wg_points = c->prof_points();
     return a;
 }
 
@@ -1603,6 +1610,7 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
         ctx->mq_K = K;
     }
     if ((r = mq_reserve_tasks(ctx, q, ctx->mq_K))) return r;
+    ctx->mq_nsub = mq_nsub(q);  // the sub-batch DevStates are written for this split
     if ((r = mq_write_states(ctx, st))) return r;
     PP_HIP(hipMemsetAsync(ctx->mq_err.p, 0, sizeof(int), st));
     PP_HIP(hipStreamSynchronize(st));
@@ -1636,10 +1644,12 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
     if ((n_iterations || n_accepted) && (r = mq_totals(ctx, &it0, &n0))) return r;
     MqArgs a = mq_args(ctx);
     const int K = ctx->mq_K, Q = ctx->mq_Q;
+    // an earlier call's PP_ERR_STEER_OVERFLOW does not stick to this one
+    PP_HIP(hipMemsetAsync(ctx->mq_err.p, 0, sizeof(int), ctx->stream));
     PP_HIP(launch_mq_target(ctx->stream, a.mq, n_steps, ctx->mq_target.p));
     // sub-batches on their own streams (not while profiling: the NN events time whole-batch
     // launches)
-    const int nsub = ctx->prof ? 1 : mq_nsub(Q);
+    const int nsub = ctx->prof ? 1 : ctx->mq_nsub;
     MqArgs sub[kMaxSub];
     hipStream_t sst[kMaxSub] = {ctx->stream};
     for (int i = 0; i < nsub && nsub > 1; ++i) {
@@ -1665,7 +1675,7 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
         for (int64_t done = 0; done < steps;) {
             const int chunk = (int)std::min<int64_t>(steps - done, 256);
             if (ctx->prof) {
-                if ((r = ensure_events(ctx, 2 * (size_t)chunk))) return r;
+                if ((r = ensure_events(ctx, 4 * (size_t)chunk))) return r;
                 a.ev = ctx->ev.data();
             }
             if (nsub > 1) {  // interleaved, so every stream always holds work
@@ -1674,14 +1684,17 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
             } else {
                 PP_HIP(launch_mq_steps(ctx->stream, a, chunk));
             }
-            if (ctx->prof) {
+            if (ctx->prof) {  // events: around mq_sample_nn and around steer_walk
                 PP_HIP(hipStreamSynchronize(ctx->stream));
                 for (int k = 0; k < chunk; ++k) {
                     float ms = 0.f;
-                    PP_HIP(hipEventElapsedTime(&ms, ctx->ev[2 * k], ctx->ev[2 * k + 1]));
+                    PP_HIP(hipEventElapsedTime(&ms, ctx->ev[4 * k], ctx->ev[4 * k + 1]));
                     ctx->nn_scan_ms += ms;
+                    PP_HIP(hipEventElapsedTime(&ms, ctx->ev[4 * k + 2], ctx->ev[4 * k + 3]));
+                    ctx->steer_ms += ms;
                 }
                 ctx->nn_scan_launches += chunk;
+                ctx->steer_launches += chunk;
             }
             done += chunk;
         }
@@ -1831,6 +1844,7 @@ int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t*
     int64_t it0 = 0, n0 = 0, w0 = 0, it1 = 0, n1 = 0, w1 = 0;
     if (tot && (r = star_totals(ctx, &it0, &n0, &w0))) return r;
     StarArgs a = star_args(ctx);
+    PP_HIP(hipMemsetAsync(ctx->sr_err.p, 0, sizeof(int), ctx->stream));  // per call, not sticky
     PP_HIP(launch_mq_target(ctx->stream, a.sd.mq, n_steps, ctx->sr_target.p));
     const int64_t steps = std::min<int64_t>(n_steps, ctx->star_max_iter);  // one iteration a step
     // sub-batches on their own streams, as pp_batch_extend (one stream while profiling)
@@ -1853,7 +1867,7 @@ int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t*
     for (int64_t done = 0; done < steps;) {
         const int chunk = (int)std::min<int64_t>(steps - done, 256);
         if (ctx->prof) {
-            if ((r = ensure_events(ctx, 2 * (size_t)chunk))) return r;
+            if ((r = ensure_events(ctx, 8 * (size_t)chunk))) return r;
             a.ev = ctx->ev.data();
         }
         if (nsub > 1) {  // interleaved, so every stream always holds work
@@ -1862,14 +1876,19 @@ int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t*
         } else {
             PP_HIP(launch_star_steps(ctx->stream, a, chunk));
         }
-        if (ctx->prof) {
+        if (ctx->prof) {  // events: around star_sample, then around each round's walk
             PP_HIP(hipStreamSynchronize(ctx->stream));
             for (int k = 0; k < chunk; ++k) {
                 float ms = 0.f;
-                PP_HIP(hipEventElapsedTime(&ms, ctx->ev[2 * k], ctx->ev[2 * k + 1]));
+                PP_HIP(hipEventElapsedTime(&ms, ctx->ev[8 * k], ctx->ev[8 * k + 1]));
                 ctx->nn_scan_ms += ms;
+                for (int w = 1; w < 4; ++w) {
+                    PP_HIP(hipEventElapsedTime(&ms, ctx->ev[8 * k + 2 * w], ctx->ev[8 * k + 2 * w + 1]));
+                    ctx->steer_ms += ms;
+                }
             }
             ctx->nn_scan_launches += chunk;
+            ctx->steer_launches += 3 * chunk;
         }
         done += chunk;
     }
@@ -1948,6 +1967,12 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out) {
     s.nn_scan_launches = ctx->nn_scan_launches;
     s.steer_ms = ctx->steer_ms;
     s.steer_launches = ctx->steer_launches;
+    if (ctx->wg_pts.p) {  // profiling: the walk workgroups' point tallies
+        std::vector<long long> v(ctx->wg_pts.n);
+        PP_HIP(hipMemcpyAsync(v.data(), ctx->wg_pts.p, v.size() * sizeof(long long), hipMemcpyDeviceToHost, ctx->stream));
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+        for (long long x : v) s.walk_points += x;
+    }
     *out = s;
     return PP_OK;
 }
@@ -1968,11 +1993,21 @@ int pp_rrt_reset_stats(pp_ctx* ctx) {
     }
     ctx->nn_scan_ms = ctx->steer_ms = 0.0;
     ctx->nn_scan_launches = ctx->steer_launches = 0;
+    if (ctx->wg_pts.p) {
+        PP_HIP(hipMemsetAsync(ctx->wg_pts.p, 0, ctx->wg_pts.n * sizeof(long long), ctx->stream));
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+    }
     return PP_OK;
 }
 
 int pp_set_profiling(pp_ctx* ctx, int enabled) {
-    if (!ctx) return set_err(PP_ERR_INVALID_ARGUMENT, "null context");
+    int r = check_ctx(ctx, false, false);
+    if (r) return r;
+    if (enabled && !ctx->wg_pts.p) {  // one tally slot per walk workgroup (any walk grid)
+        PP_HIP(ctx->wg_pts.reserve(kWalkTallySlots));
+        PP_HIP(hipMemsetAsync(ctx->wg_pts.p, 0, kWalkTallySlots * sizeof(long long), ctx->stream));
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+    }
     ctx->prof = enabled != 0;
     return PP_OK;
 }

@@ -41,6 +41,7 @@ struct WindowArgs {
     int* fin_par = nullptr;       // [K] window parent of a resolved sample (kWinParent)
     ResolveScratch rs{};
     double* lit_scratch = nullptr;
+    long long* wg_points = nullptr;  // profiling: walked points per walk workgroup (or null)
 };
 
 // Enqueue window number `seq` on stream s: its window kernel also resolves and commits window
@@ -88,7 +89,8 @@ struct MqArgs {
     double* lit_scratch = nullptr;  // kLiteralWaves buffers
     int* lit_locks = nullptr;       // their slot locks (0 free)
     int* err = nullptr;
-    hipEvent_t* ev = nullptr;  // optional: 2 per step, around mq_sample_nn
+    hipEvent_t* ev = nullptr;  // optional: 4 per step, around mq_sample_nn and steer_walk
+    long long* wg_points = nullptr;  // profiling: walked points per walk workgroup (or null)
 };
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps);
 hipError_t launch_mq_init(hipStream_t s, const MqDev& mq, const double* starts);
@@ -109,7 +111,8 @@ struct StarArgs {
     double* pdbuf = nullptr;
     double* lit_scratch = nullptr;  // kLiteralWaves buffers
     int* err = nullptr;
-    hipEvent_t* ev = nullptr;  // optional: 2 per step, around star_sample (the exact NN)
+    hipEvent_t* ev = nullptr;  // optional: 8 per step, around star_sample and each round's walk
+    long long* wg_points = nullptr;  // profiling: walked points per walk workgroup (or null)
 };
 hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps);
 hipError_t launch_star_init(hipStream_t s, const StarArgs& a, const double* starts);

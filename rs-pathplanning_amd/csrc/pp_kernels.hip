@@ -20,6 +20,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "pp_device.h"
 #include "pp_kernels.h"
@@ -1054,11 +1058,7 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
         }
         const double xq = qx[q], yq = qy[q];
         const float fx = (float)xq, fy = (float)yq;
-#ifdef PP_T_NOAPPEND
-        for (int k = lane; k < 0; k += 64) {
-#else
         for (int k = lane; k < D; k += 64) {  // appended nodes: exact top-2 per lane
-#endif
             const float2 v = k < Dl ? s_dn[k] : make_float2(x32[ns + k], y32[ns + k]);
             const float d = scan_d2(fx, fy, v.x, v.y);
             const Top2 c{d, __builtin_inff(), ns + k};
@@ -1218,7 +1218,6 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     FIN_STAMP(tf3);
     if (!cand) return;  // nearest-only launch (no window)
     // ---- 2. window pairs
-#ifndef PP_T_NOPAIRS
     {
         // wave w: sample j = q0 + w against the window samples i < j of the Morton cells its
         // disc of radius sqrt(D2) touches (the binning is monotone, so the cells are a superset)
@@ -1274,7 +1273,6 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
 #endif
         }
     }
-#endif
     __syncthreads();
     FIN_STAMP(tf4);
     if (wave == 0) {
@@ -1607,20 +1605,19 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
 // and the junction to the parent follows the last grid point.  A kPrepWalk task reads its pd
 // values from pdbuf; a kPrepFallback task (more than kPdCap points) reads its first kPdCap there
 // and continues with the uniform serial `pd += d` walk from the state steer_prep kept, each lane
-// capturing its own point.
+// capturing its own point.  npts (wave-uniform) += the polyline points generated and verified
+// (grid points plus the junction; the profiled walk roofline's unit).
 template <bool kLds>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
                                         const double* __restrict__ pdv, double* __restrict__ gs,
-                                        unsigned long long* stw = nullptr) {
-#ifndef PP_STAMPS_WALK
-    (void)stw;
-#endif
+                                        int& npts) {
     const int lane = threadIdx.x & 63;
     const int state = p->state;
     const double x = p->x, y = p->y, px = p->px, py = p->py;
     if (state == kPrepNone) {  // steer failed: polyline [(x, y), (px, py)] (rrt.rs:313)
         const bool has = lane < 2;
         const double qx = lane == 0 ? x : px, qy = lane == 0 ? y : py;
+        npts += 2;
         return chunk_rejects<kLds>(sc, has, has, lane == 1, qx, qy) ? kReject : kAccept;
     }
     if (state != kPrepWalk && state != kPrepFallback) return state;
@@ -1640,13 +1637,8 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     long long grid = ng;  // grid points stored by steer_prep (0 or kPdCap for kPrepFallback)
     static_assert(kPdCap % 63 == 0, "stored points end on a chunk boundary");
     double carry_x = x, carry_y = y;
-#ifdef PP_STAMPS_WALK
-    int64_t sw_gen = 0, sw_pt = 0, sw_col = 0, sw_chunks = 0;
-#endif
+    npts += 1;  // point 0, the child
     for (int base = 0;; base += 63) {
-#ifdef PP_STAMPS_WALK
-        const int64_t w0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-#endif
         int cnt = 0, my_seg = 0;
         double my_pd = 0.0;
         bool done;
@@ -1671,11 +1663,6 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                 if (lane == 0) gs[0] = w;
                 int u = 0;
                 bool ended = !(fabs(w) <= aL);
-#ifdef PP_T_NOGEN
-                if (lane <= umax) gs[lane] = gpd + lane * gdd;  // timing experiment only
-                u = umax;
-                ended = true;
-#endif
                 while (!ended && u < umax) {
                     double t4[4];
 #pragma unroll
@@ -1727,9 +1714,6 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                 my_seg = g < n0 ? 0 : (g < n01 ? 1 : 2);
             }
         }
-#ifdef PP_STAMPS_WALK
-        const int64_t w1 = (int64_t)__builtin_amdgcn_s_memrealtime() + (int64_t)(my_pd * 0.0);
-#endif
         const bool junction_here = done && cnt < 63;
         const bool isgrid = lane >= 1 && lane <= cnt;
         const bool isj = junction_here && lane == cnt + 1;
@@ -1759,40 +1743,10 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
             qx = px;
             qy = py;
         }
-#ifdef PP_STAMPS_WALK
-        const int64_t w2 = (int64_t)__builtin_amdgcn_s_memrealtime() + (int64_t)(qx * 0.0);
-#endif
         const bool has = lane == 0 || isgrid || isj;
-#ifdef PP_T_NOCOL
-        const bool chk = false;  // timing experiment only
-        if (junction_here) break;
-        carry_x = __shfl(qx, 63);
-        carry_y = __shfl(qy, 63);
-        continue;
-#else
         const bool chk = isgrid || isj || (base == 0 && lane == 0);
-#endif
-#ifdef PP_STAMPS_WALK
-        const bool rj_ = chunk_rejects<kLds>(sc, has, chk, has && lane >= 1, qx, qy);
-        const int64_t w3 = (int64_t)__builtin_amdgcn_s_memrealtime();
-        sw_gen += w1 - w0;
-        sw_pt += w2 - w1;
-        sw_col += w3 - w2;
-        sw_chunks += 1;
-        if (rj_ || junction_here) {
-            if (lane == 0) {
-                atomicAdd((unsigned long long*)&stw[0], (unsigned long long)sw_gen);
-                atomicAdd((unsigned long long*)&stw[1], (unsigned long long)sw_pt);
-                atomicAdd((unsigned long long*)&stw[2], (unsigned long long)sw_col);
-                atomicAdd((unsigned long long*)&stw[3], (unsigned long long)sw_chunks);
-                atomicAdd((unsigned long long*)&stw[4], 1ull);
-                atomicMax((unsigned long long*)&stw[7], (unsigned long long)(sw_gen + sw_pt + sw_col));
-            }
-        }
-        if (rj_) return kReject;
-#else
+        npts += cnt + (junction_here ? 1 : 0);
         if (chunk_rejects<kLds>(sc, has, chk, has && lane >= 1, qx, qy)) return kReject;
-#endif
         if (junction_here) break;
         carry_x = __shfl(qx, 63);
         carry_y = __shfl(qy, 63);
@@ -1812,16 +1766,10 @@ constexpr int kWalkMaxWG = PP_WALKWG;  // 3 resident workgroups per CU
 __host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
     return scene_bytes + kWalkThreads / 64 * kGenSlots * 8;
 }
-// the walk's persistent grid: the workgroups that can be resident at once (the LDS image decides:
-// 160 KB per CU; at most 4 of 8 waves each), so no workgroup starts late with a share of tasks
-inline int walk_grid_cap(int scene_bytes) {
-    const int per_cu = std::max(1, std::min(4, 160 * 1024 / walk_lds_bytes(scene_bytes)));
-    return 256 * per_cu;
-}
-
 // Window mode (pend != nullptr): a snapshot task whose verdict is not final (literal path,
 // error) and that has no nearer window sample is queued for the resolve (the others were queued
-// by nn_finalize's pair search).
+// by nn_finalize's pair search).  wg_points (profiling only, else null): workgroup b adds its
+// walked polyline points to wg_points[b] (its own slot: no atomics on a shared address).
 template <bool kLds>
 __global__ __launch_bounds__(kWalkThreads) void steer_walk_kernel(DevState* __restrict__ st,
                                                          SceneDev sc,
@@ -1830,29 +1778,20 @@ __global__ __launch_bounds__(kWalkThreads) void steer_walk_kernel(DevState* __re
                                                          CandEntry* __restrict__ cand,
                                                          int* __restrict__ snap_status,
                                                          const int* __restrict__ cand_cnt,
-                                                         int* __restrict__ pend) {
+                                                         int* __restrict__ pend,
+                                                         long long* __restrict__ wg_points) {
     const int lane = threadIdx.x & 63;
     const int W = st->W;
     const int total = W + st->ncomp;
     if ((int)blockIdx.x * (kWalkThreads / 64) >= total) return;  // whole workgroup idle
-#ifdef PP_STAMPS_WALK
-    const int64_t ws0 = (int64_t)__builtin_amdgcn_s_memrealtime();
     if (kLds) stage_scene(sc);
-    if (threadIdx.x == 0) {
-        atomicAdd((unsigned long long*)&st->stamps[5], (unsigned long long)((int64_t)__builtin_amdgcn_s_memrealtime() - ws0));
-        atomicAdd((unsigned long long*)&st->stamps[6], 1ull);
-    }
-    unsigned long long* stw = (unsigned long long*)st->stamps;
-#else
-    if (kLds) stage_scene(sc);
-    unsigned long long* stw = nullptr;
-#endif
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) +
                  (threadIdx.x >> 6) * kGenSlots;  // this wave's generator slots
+    int npts = 0;
     for (int t = gw; t < total; t += nw) {
-        const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, stw);
+        const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts);
         if (lane == 0) {
             if (t < W) {
                 snap_status[t] = s;
@@ -1863,6 +1802,49 @@ __global__ __launch_bounds__(kWalkThreads) void steer_walk_kernel(DevState* __re
             }
         }
     }
+    if (wg_points) {
+        __shared__ int s_np[kWalkThreads / 64];
+        if (lane == 0) s_np[threadIdx.x >> 6] = npts;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            long long sum = 0;
+            for (int w = 0; w < kWalkThreads / 64; ++w) sum += s_np[w];
+            wg_points[blockIdx.x] += sum;
+        }
+    }
+}
+
+// The walk's persistent grid: the workgroups that can be resident at once, so no workgroup starts
+// late with a share of tasks — the device's CU count times the workgroups per CU the occupancy
+// API gives for this instantiation and its dynamic LDS (the scene image decides; at most 4 of 8
+// waves each), read once per (device, image size) instead of assuming 256 CUs and 160 KB.
+inline int walk_grid_cap(int scene_bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find({dev, scene_bytes});
+    if (it != cache.end()) return it->second;
+    int cus = 256, per_cu = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+        cus = prop.multiProcessorCount;
+    const hipError_t e =
+        scene_bytes > 0
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, steer_walk_kernel<true>,
+                                                          kWalkThreads, walk_lds_bytes(scene_bytes))
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, steer_walk_kernel<false>,
+                                                          kWalkThreads, walk_lds_bytes(0));
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    per_cu = std::min(4, per_cu);
+    if (const char* v = std::getenv("PP_WALK_PER_CU")) per_cu = std::max(1, std::min(8, std::atoi(v)));
+    const int cap = cus * per_cu;
+    cache[{dev, scene_bytes}] = cap;
+    if (std::getenv("PP_DEBUG"))
+        fprintf(stderr, "[pp] walk grid: %d CUs x %d workgroups (LDS image %d B)\n", cus, per_cu,
+                scene_bytes);
+    return cap;
 }
 
 // A resolve repair (one wave): the (child, parent pose) pair steered and collision-checked anew
@@ -2871,20 +2853,20 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
     const int lds = a.sc.lds_bytes;
     for (int k = 0; k < steps; ++k) {
-        if (a.ev) (void)hipEventRecord(a.ev[2 * k], s);
+        if (a.ev) (void)hipEventRecord(a.ev[4 * k], s);
         mq_sample_nn_kernel<<<nn_blocks, 256, 0, s>>>(a.mq, a.sc.minx, a.sc.maxx, a.sc.miny,
                                                       a.sc.maxy, a.tasks);
-        if (a.ev) (void)hipEventRecord(a.ev[2 * k + 1], s);
+        if (a.ev) (void)hipEventRecord(a.ev[4 * k + 1], s);
         steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, nullptr, nullptr, nullptr,
                                                       nullptr, a.rec, a.pdbuf, a.yaw, a.tasks);
+        if (a.ev) (void)hipEventRecord(a.ev[4 * k + 2], s);
         if (lds > 0)
-            steer_walk_kernel<true><<<walk_blocks, kWalkThreads, walk_lds_bytes(lds), s>>>(a.st, a.sc, a.rec, a.pdbuf,
-                                                                  nullptr, a.status, nullptr,
-                                                                  nullptr);
+            steer_walk_kernel<true><<<walk_blocks, kWalkThreads, walk_lds_bytes(lds), s>>>(
+                a.st, a.sc, a.rec, a.pdbuf, nullptr, a.status, nullptr, nullptr, a.wg_points);
         else
-            steer_walk_kernel<false><<<walk_blocks, kWalkThreads, walk_lds_bytes(0), s>>>(a.st, a.sc, a.rec, a.pdbuf,
-                                                                 nullptr, a.status, nullptr,
-                                                                 nullptr);
+            steer_walk_kernel<false><<<walk_blocks, kWalkThreads, walk_lds_bytes(0), s>>>(
+                a.st, a.sc, a.rec, a.pdbuf, nullptr, a.status, nullptr, nullptr, a.wg_points);
+        if (a.ev) (void)hipEventRecord(a.ev[4 * k + 3], s);
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
                                                     a.lit_scratch, a.lit_locks, a.err);
     }
@@ -3377,30 +3359,34 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
     // wave slot the walk's 48 VGPRs allow (4 workgroups of 8 waves per CU)
     const int walk_cap = lds > 0 ? std::min(kWalkMaxWG, walk_grid_cap(lds)) : 1024;
     const int walkB = std::min((TB + kWalkThreads / 64 - 1) / (kWalkThreads / 64), walk_cap);
+    // ev (profiling): 8 per step — around star_sample, then around each round's walk
     auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, const StarTaskExt* ext,
-                     int* status, double* yaw, double* cost) {
+                     int* status, double* yaw, double* cost, hipEvent_t* ev) {
         steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(st, a.sc, nullptr, nullptr, nullptr, nullptr,
                                                       a.rec, a.pdbuf, yaw, t, cost, ext);
+        if (ev) (void)hipEventRecord(ev[0], s);
         if (lds > 0)
             steer_walk_kernel<true><<<wb, kWalkThreads, walk_lds_bytes(lds), s>>>(
-                st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr);
+                st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr, a.wg_points);
         else
             steer_walk_kernel<false><<<wb, kWalkThreads, walk_lds_bytes(0), s>>>(
-                st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr);
+                st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr, a.wg_points);
+        if (ev) (void)hipEventRecord(ev[1], s);
     };
     for (int k = 0; k < steps; ++k) {
-        if (a.ev) (void)hipEventRecord(a.ev[2 * k], s);
+        hipEvent_t* ev = a.ev ? a.ev + 8 * k : nullptr;
+        if (ev) (void)hipEventRecord(ev[0], s);
         star_sample_kernel<<<qb, 256, 0, s>>>(a.sd, a.sc.minx, a.sc.maxx, a.sc.miny, a.sc.maxy,
                                               a.tA);
-        if (a.ev) (void)hipEventRecord(a.ev[2 * k + 1], s);
-        round(a.sd.stA, prepA, walkA, a.tA, nullptr, a.sA, a.yA, a.cA);
+        if (ev) (void)hipEventRecord(ev[1], s);
+        round(a.sd.stA, prepA, walkA, a.tA, nullptr, a.sA, a.yA, a.cA, ev ? ev + 2 : nullptr);
         star_knn_kernel<<<knn_blocks, 64 * kKnnWaves, 0, s>>>(a.sd, a.sA, a.cA, a.tB, a.eB,
                                                               a.err);
-        round(a.sd.stB, prepB, walkB, a.tB, a.eB, a.sB, a.yB, a.cB);
+        round(a.sd.stB, prepB, walkB, a.tB, a.eB, a.sB, a.yB, a.cB, ev ? ev + 4 : nullptr);
         star_insert_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sc, a.sA, a.yA, a.cA, a.tB, a.sB,
                                                       a.yB, a.cB, a.tC, a.eC, a.lit_scratch,
                                                       a.err);
-        round(a.sd.stC, prepB, walkB, a.tC, a.eC, a.sC, a.yC, a.cC);
+        round(a.sd.stC, prepB, walkB, a.tC, a.eC, a.sC, a.yC, a.cC, ev ? ev + 6 : nullptr);
         star_rewire_kernel<<<lit_blocks, 256, 0, s>>>(a.sd, a.sc, a.tC, a.eC, a.sC, a.cC,
                                                       a.lit_scratch, a.err);
     }
@@ -3525,21 +3511,21 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
         a.st, p, seq, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, wsx, wsy, a.tr.x32, a.tr.y32,
         a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose,
         pair_grid(wk.g, p, a.eps_coord), a.cand_cnt, a.cand, a.pend, wk.sq[p]);
-    if (ev) (void)hipEventRecord(ev[2], s);
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K + kPrepThreads / 8 - 1) / (kPrepThreads / 8);
     steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, wsx, wsy, a.snap_pose, a.cand,
                                                   a.rec, a.pdbuf, a.snap_yaw, nullptr);
+    if (ev) (void)hipEventRecord(ev[2], s);
     const int lds = a.sc.lds_bytes;
     // snapshot tasks plus the usual few candidate tasks in one round of waves
     const int nwg = std::min((K + K / 4 + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
                              std::min(kWalkMaxWG, walk_grid_cap(a.sc.lds_bytes)));
     if (lds > 0)
-        steer_walk_kernel<true><<<nwg, kWalkThreads, walk_lds_bytes(lds), s>>>(a.st, a.sc, a.rec, a.pdbuf, a.cand,
-                                                      a.snap_status, a.cand_cnt, a.pend);
+        steer_walk_kernel<true><<<nwg, kWalkThreads, walk_lds_bytes(lds), s>>>(
+            a.st, a.sc, a.rec, a.pdbuf, a.cand, a.snap_status, a.cand_cnt, a.pend, a.wg_points);
     else
-        steer_walk_kernel<false><<<nwg, kWalkThreads, walk_lds_bytes(0), s>>>(a.st, a.sc, a.rec, a.pdbuf, a.cand,
-                                                     a.snap_status, a.cand_cnt, a.pend);
+        steer_walk_kernel<false><<<nwg, kWalkThreads, walk_lds_bytes(0), s>>>(
+            a.st, a.sc, a.rec, a.pdbuf, a.cand, a.snap_status, a.cand_cnt, a.pend, a.wg_points);
     if (ev) (void)hipEventRecord(ev[3], s);
     return hipGetLastError();
 }

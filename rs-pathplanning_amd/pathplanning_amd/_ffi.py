@@ -63,7 +63,7 @@ class StatsC(C.Structure):
         ("literal_repairs", C.c_int64), ("nn_flagged", C.c_int64), ("node_evals", C.c_int64),
         ("nn_scan_ms", C.c_double), ("nn_scan_launches", C.c_int64),
         ("steer_ms", C.c_double), ("steer_launches", C.c_int64),
-        ("stamps", C.c_int64 * 8),
+        ("stamps", C.c_int64 * 8), ("walk_points", C.c_int64),
     ]
 
     def as_dict(self):

@@ -424,10 +424,9 @@ class RRTBatch:
     def set_profiling(self, on: bool):
         _ffi.check(_ffi.lib().pp_set_profiling(self.ctx.handle, int(bool(on))))
 
-    def tree(self, query: int):
-        """(x, y, yaw, parent) of one query's tree, root first."""
-        n_all, _ = self.state()
-        n = int(n_all[query])
+    def tree(self, query: int, n: int | None = None):
+        """(x, y, yaw, parent) of one query's tree, root first (``n``: its size, when known)."""
+        n = int(self.state()[0][query]) if n is None else int(n)
         x, y, yaw = np.zeros(n), np.zeros(n), np.zeros(n)
         par = np.zeros(n, dtype=np.int32)
         out = C.c_int64(0)
@@ -489,9 +488,10 @@ class RRTStarBatch:
         _ffi.check(_ffi.lib().pp_rrt_get_stats(self.ctx.handle, C.byref(s)))
         return s.as_dict()
 
-    def tree(self, query: int):
-        """(x, y, yaw, parent, cost) of one query's tree, root first."""
-        n = int(self.state()[0][query])
+    def tree(self, query: int, n: int | None = None):
+        """(x, y, yaw, parent, cost) of one query's tree, root first (``n``: its size, when
+        known)."""
+        n = int(self.state()[0][query]) if n is None else int(n)
         x, y, yaw, cost = np.zeros(n), np.zeros(n), np.zeros(n), np.zeros(n)
         par = np.zeros(n, dtype=np.int32)
         out = C.c_int64(0)
