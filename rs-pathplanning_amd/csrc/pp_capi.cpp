@@ -86,7 +86,8 @@ struct HBuf {  // pinned host staging
 };
 
 constexpr int kMaxBatch = 64;  // windows enqueued between two host synchronisations
-constexpr int kWalkTallySlots = 4096;  // >= any steer_walk grid (kWalkMaxWG, 1024 for L2 scenes)
+constexpr int kWalkTallySlots = 4096;
+constexpr int kScreenPad = 64;  // >= any steer_walk grid (kWalkMaxWG, 1024 for L2 scenes)
 
 }  // namespace
 
@@ -144,9 +145,10 @@ struct pp_ctx {
     int Kcap = 0;
     DBuf<double> wsx, wsy, nn_d2, snap_yaw, snap_pose;
     DBuf<float> pbest, psecond, wsx32, wsy32;
-    DBuf<int> perm, cofs;
+    DBuf<int> perm, cofs, ipos;
     DBuf<float2> sxy;
-    DBuf<double> sqb;
+    DBuf<double> sqb, ssx, ssy;
+    DBuf<float2> ob;
     DBuf<int> pidx, nn_idx, cand_cnt, snap_status;
     DBuf<CandEntry> cand;
     DBuf<PrepRec> rec;   // per-task steer records
@@ -323,6 +325,10 @@ struct pp_ctx {
         a.cofs = cofs.p;
         a.sxy = sxy.p;
         a.sq = sqb.p;
+        a.ssx = ssx.p;
+        a.ssy = ssy.p;
+        a.ob = ob.p;
+        a.ipos = ipos.p;
         a.pbest = pbest.p;
         a.psecond = psecond.p;
         a.pidx = pidx.p;
@@ -367,9 +373,13 @@ int ensure_window(pp_ctx* c, int K) {
     PP_HIP(c->wsx32.reserve(2 * k));
     PP_HIP(c->wsy32.reserve(2 * k));
     PP_HIP(c->perm.reserve(2 * k));
+    PP_HIP(c->ipos.reserve(2 * k));
     PP_HIP(c->sxy.reserve(2 * k));
     PP_HIP(c->cofs.reserve(2 * 257));
     PP_HIP(c->sqb.reserve(2 * k));
+    PP_HIP(c->ssx.reserve(2 * k));
+    PP_HIP(c->ssy.reserve(2 * k));
+    PP_HIP(c->ob.reserve(2 * (size_t)kMaxWindow / 256));
     PP_HIP(c->pbest.reserve(k * kMaxChunks));
     PP_HIP(c->psecond.reserve(k * kMaxChunks));
     PP_HIP(c->pidx.reserve(k * kMaxChunks));
@@ -415,8 +425,10 @@ int ensure_tree(pp_ctx* c, int64_t need) {
     int64_t nc = std::max<int64_t>(need, c->cap * 2);
     nc = std::max<int64_t>(nc, 1024);
     int r;
-    if ((r = grow_copy(c, c->x32, c->n, nc))) return r;
-    if ((r = grow_copy(c, c->y32, c->n, nc))) return r;
+    // the f32 screen copies get kScreenPad floats of slack: the screen's LDS-DMA reads whole
+    // float4s, up to 3 floats past the last node
+    if ((r = grow_copy(c, c->x32, c->n, nc + kScreenPad))) return r;
+    if ((r = grow_copy(c, c->y32, c->n, nc + kScreenPad))) return r;
     if ((r = grow_copy(c, c->X, c->n, nc))) return r;
     if ((r = grow_copy(c, c->Y, c->n, nc))) return r;
     if ((r = grow_copy(c, c->YAW, c->n, nc))) return r;

@@ -25,6 +25,10 @@ struct WindowArgs {
     int* cofs = nullptr;          // [2 * 257] start of each Morton cell in the sorted order
     float2* sxy = nullptr;        // [2 * Kcap] the samples in sorted order (f32)
     double* sq = nullptr;         // [2 * Kcap] |q - o|^2 about the screen block's centre
+    double* ssx = nullptr;        // [2 * Kcap] the samples in sorted order (f64)
+    double* ssy = nullptr;
+    float2* ob = nullptr;         // [2 * kMaxWindow / 512] the screen blocks' centres
+    int* ipos = nullptr;          // [2 * Kcap] sample -> sorted position
     float* pbest = nullptr;
     float* psecond = nullptr;
     int* pidx = nullptr;

@@ -30,10 +30,19 @@
 
 namespace ppamd {
 
-#if defined(PP_STAMPS) || defined(PP_STAMPS_RESOLVE) || defined(PP_STAMPS_WALK)
+typedef __attribute__((address_space(3))) void lds_void;  // LDS-DMA operands
+typedef __attribute__((address_space(1))) void glb_void;
+
+#if defined(PP_STAMPS) || defined(PP_STAMPS_RESOLVE)
 #define PP_STAMP(var) const int64_t var = (int64_t)__builtin_amdgcn_s_memrealtime()
 #else
 #define PP_STAMP(var)
+#endif
+// diagnostic build only (-DPP_STAMPS_SCREEN): the screen's phase times per wave
+#ifdef PP_STAMPS_SCREEN
+#define SCREEN_STAMP(var) const int64_t var = (int64_t)__builtin_amdgcn_s_memrealtime()
+#else
+#define SCREEN_STAMP(var)
 #endif
 
 // ------------------------------------------------------------------------------ collision
@@ -549,7 +558,13 @@ constexpr int kScanThreads = 512;                // window_kernel workgroup (8 w
 constexpr bool kWinRepair = true;                // repairs inside the window kernel (no spill)
 #endif
 constexpr int kScanWaves = kScanThreads / 64;
-constexpr int kScanBlk = PP_SCANBLK;             // nodes per scalar-load block
+constexpr int kScanBlk = PP_SCANBLK;             // nodes per block (one block minimum per sample)
+constexpr int kStage = 7936;                     // chunk nodes staged in LDS per round
+constexpr int kGrab = 64;                        // nodes a screen wave takes from the counter
+constexpr int kExactNode = 1 << 30;              // screen partial key: a node index, not a block
+// LDS of a screen workgroup: the wave merge (best, second, key per wave and sample; sample ids;
+// the samples' f32 operands), then the staged chunk
+constexpr int kScreenStageOff = (3 * kScanWaves + 3) * kQPB * 4;
 #ifndef PP_SCANGRID
 #define PP_SCANGRID 255
 #endif
@@ -624,6 +639,11 @@ struct SamplesArgs {
     int* perm[2];
     int* cofs[2];     // [257] first sorted position of each Morton cell (cell 256: W)
     float2* sxy[2];   // sorted position -> (x, y) f32 (the pair search's prefilter)
+    double* ssx[2];   // sorted position -> x, y (f64): the screen's coalesced sample loads
+    double* ssy[2];
+    float2* ob[2];    // [K / kQPB] the screen block's centre o (f32) of each kQPB sorted samples
+    double* sq[2];    // sample -> |q - o|^2 about its block's centre (f64, exact)
+    int* ipos[2];     // sample -> sorted position (the screen's partials are stored by position)
 };
 
 __device__ inline int morton16(int x, int y) {
@@ -633,10 +653,14 @@ __device__ inline int morton16(int x, int y) {
     return m;
 }
 
+// LDS of samples_role: the Morton histogram, each sample's cell, the sorted window's sample ids
+constexpr int kSamplesLds = 256 * 4 + kMaxWindow + kMaxWindow * 4;
+
 __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t start,
                              char* smem) {
     int* s_hist = reinterpret_cast<int*>(smem);                  // [256]
     unsigned char* s_cell = reinterpret_cast<unsigned char*>(s_hist + 256);  // [K]
+    int* s_j = reinterpret_cast<int*>(smem + 256 * 4 + kMaxWindow);  // [K] sorted position -> sample
     const int tid = threadIdx.x, NT = blockDim.x;
     const int64_t rem = g.target - start;
     const int W = (rem <= 0 || st->error) ? 0 : (rem < g.K ? (int)rem : g.K);
@@ -686,10 +710,51 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
     for (int i = tid; i < 256; i += NT) g.cofs[np][i] = s_hist[i];
     if (tid == 0) g.cofs[np][256] = W;
     __syncthreads();  // the cell starts are read before the scatter advances them
-    for (int j = tid; j < W; j += NT) {
-        const int pos = atomicAdd(&s_hist[s_cell[j]], 1);
-        g.perm[np][pos] = j;
-        g.sxy[np][pos] = make_float2(g.wsx32[np][j], g.wsy32[np][j]);
+    for (int j = tid; j < W; j += NT) s_j[atomicAdd(&s_hist[s_cell[j]], 1)] = j;
+    __syncthreads();
+    // the screen's blocks of kQPB sorted samples, one wave each: the sorted window (coalesced; the
+    // coordinates drawn again from the stream, bit-identical), the centre o of the block's
+    // bounding box (f32) and every sample's |q - o|^2 in f64 — (q - o) rounded to f32 per axis,
+    // the screen's own operands, squared exactly (nn_finalize adds it back to the screen values)
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int qb = wv; qb * kQPB < W; qb += NT / 64) {
+        const int p0 = qb * kQPB;
+        double xs[kQPL], ys[kQPL];
+        double x0 = __builtin_inf(), x1 = -__builtin_inf(), y0 = __builtin_inf(), y1 = -__builtin_inf();
+#pragma unroll
+        for (int r = 0; r < kQPL; ++r) {
+            const int pos = p0 + r * 64 + lane;
+            xs[r] = ys[r] = 0.0;
+            if (pos < W) {
+                const int j = s_j[pos];
+                const uint64_t itj = (uint64_t)(start + j);
+                xs[r] = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
+                ys[r] = gen_range(g.seed, 2 * itj + 1, g.miny, g.maxy);
+                g.perm[np][pos] = j;
+                g.ipos[np][j] = pos;
+                g.sxy[np][pos] = make_float2((float)xs[r], (float)ys[r]);
+                g.ssx[np][pos] = xs[r];
+                g.ssy[np][pos] = ys[r];
+                x0 = fmin(x0, xs[r]);
+                x1 = fmax(x1, xs[r]);
+                y0 = fmin(y0, ys[r]);
+                y1 = fmax(y1, ys[r]);
+            }
+        }
+        x0 = wave_min(x0);
+        x1 = wave_max(x1);
+        y0 = wave_min(y0);
+        y1 = wave_max(y1);
+        const float oxf = (float)(0.5 * (x0 + x1)), oyf = (float)(0.5 * (y0 + y1));
+        if (lane == 0) g.ob[np][qb] = make_float2(oxf, oyf);
+#pragma unroll
+        for (int r = 0; r < kQPL; ++r) {
+            const int pos = p0 + r * 64 + lane;
+            if (pos < W) {
+                const float qpx = (float)(xs[r] - (double)oxf), qpy = (float)(ys[r] - (double)oyf);
+                g.sq[np][s_j[pos]] = (double)qpx * (double)qpx + (double)qpy * (double)qpy;
+            }
+        }
     }
 }
 
@@ -754,11 +819,37 @@ struct WinKArgs {
 // shared by the lane's 4 samples) — 3.5 VALU per evaluation instead of 4.5.  nn_finalize adds
 // |q - o|^2 back (sq) and widens the near-tie margin by the expanded form's rounding bound.
 // !kExp (nearest API): the given samples, direct form (sub, sub, mul, fma).
+// The screen's winner re-evaluation of a block no longer in LDS (trees past one staging round):
+// the block's 16 nodes from global memory with the screen's own prep and arithmetic, the lowest
+// u with value == best and the minimum of the others.  Out of line: inlined, the compiler merges
+// it with the LDS path into flat loads.
+template <bool kExp>
+__device__ __attribute__((noinline)) void screen_block_global(const float* __restrict__ bx,
+                                                              const float* __restrict__ by, float qx,
+                                                              float qy, float oxf, float oyf,
+                                                              float best, int& ui, float& other) {
+    for (int u = 0; u < kScanBlk; ++u) {
+        float px = bx[u], py = by[u], pw = 0.0f;
+        if (kExp) {
+            px = px - oxf;
+            py = py - oyf;
+            pw = __builtin_fmaf(py, py, px * px);
+        }
+        const float d = kExp ? __builtin_fmaf(qx, px, __builtin_fmaf(qy, py, pw))
+                             : scan_d2(qx, qy, px, py);
+        if (ui < 0 && d == best)
+            ui = u;
+        else
+            other = __builtin_fminf(other, d);
+    }
+}
+
 template <bool kExp>
 __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& a, int b,
                                                                char* smem) {
     DevState* st = a.st;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    SCREEN_STAMP(ts0);
     const int W = st->Wp[a.p];
     const int ns = st->n_scan;
     if (b == 0 && tid == 0) st->nsp[a.p] = ns;
@@ -771,54 +862,79 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
     const int cl = scan_chunk_len(ns, a.chunks);
     const int c0 = c * cl;
     if (c0 >= ns) return;
-    const int c1 = min(c0 + cl, ns);
-    const double* qxs = a.wsx[a.p];
-    const double* qys = a.wsy[a.p];
+    const int L = min(c0 + cl, ns) - c0;  // the chunk's nodes
+    const float* nx = a.tr.x32;
+    const float* ny = a.tr.y32;
+    // The chunk goes through the workgroup's LDS (x | y | |n-o|^2, kStage nodes a round; one
+    // round up to ~250k tree nodes at K = 4096): LDS-DMA (global_load_lds_dwordx4, lane l brings
+    // nodes 4l..4l+3 of a 256-node quarter, no registers) issued before the samples are read, so
+    // the two latencies overlap; each thread then preps its own float4s in place — (n - o,
+    // |n - o|^2) in the expanded form, each node once instead of once per lane.  The waves take
+    // kGrab-node pieces from an LDS counter (no wave idles at the merge barrier while another
+    // still screens); a wave's pieces come in increasing order, so its first block to reach the
+    // best is its lowest.  The block loop reads its 16 nodes as broadcast ds_read_b128.
+    float* stg = reinterpret_cast<float*>(smem + kScreenStageOff);
+    int* s_next = reinterpret_cast<int*>(stg + 3 * kStage);
+    auto issue_round = [&](int r0) {
+        const int len = min(kStage, L - r0);
+        for (int q4 = wave; q4 * 256 < len; q4 += kScanWaves) {
+            if (q4 * 256 + 4 * lane < len) {  // (a partial float4 reads up to 3 padding floats)
+                const size_t gi = (size_t)(c0 + r0 + q4 * 256 + 4 * lane);
+                __builtin_amdgcn_global_load_lds((glb_void*)(nx + gi), (lds_void*)(stg + q4 * 256), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((glb_void*)(ny + gi), (lds_void*)(stg + kStage + q4 * 256), 16, 0, 0);
+            }
+        }
+    };
+    issue_round(0);
     float qxr[kQPL], qyr[kQPL], best[kQPL], second[kQPL];
     int sid[kQPL], blk[kQPL], bi[kQPL];
-    double xs[kQPL], ys[kQPL];
+    float oxf = 0.0f, oyf = 0.0f;
+    if (kExp) {
+        // window mode: samples_role left the window sorted (f64, coalesced), each screen block's
+        // centre o and every sample's |q - o|^2 (for nn_finalize)
+        const float2 o = a.g.ob[a.p][qb];
+        oxf = o.x;
+        oyf = o.y;
+#pragma unroll
+        for (int r = 0; r < kQPL; ++r) {
+            const int pos = qbase + r * 64 + lane;
+            const bool in = pos < W;
+            sid[r] = in ? a.perm[a.p][pos] : -1;
+            const double xs = in ? a.g.ssx[a.p][pos] : (double)oxf;
+            const double ys = in ? a.g.ssy[a.p][pos] : (double)oyf;
+            const float qpx = (float)(xs - (double)oxf), qpy = (float)(ys - (double)oyf);
+            qxr[r] = -2.0f * qpx;  // exact scaling
+            qyr[r] = -2.0f * qpy;
+        }
+    } else {
+        const double* qxs = a.wsx[a.p];
+        const double* qys = a.wsy[a.p];
+#pragma unroll
+        for (int r = 0; r < kQPL; ++r) {
+            const int pos = qbase + r * 64 + lane;
+            sid[r] = pos < W ? pos : -1;
+            qxr[r] = sid[r] >= 0 ? (float)qxs[pos] : 0.0f;
+            qyr[r] = sid[r] >= 0 ? (float)qys[pos] : 0.0f;
+        }
+    }
 #pragma unroll
     for (int r = 0; r < kQPL; ++r) {
-        const int pos = qbase + r * 64 + lane;
-        sid[r] = pos < W ? (kExp ? a.perm[a.p][pos] : pos) : -1;
-        xs[r] = sid[r] >= 0 ? qxs[sid[r]] : 0.0;
-        ys[r] = sid[r] >= 0 ? qys[sid[r]] : 0.0;
         best[r] = __builtin_inff();
         second[r] = __builtin_inff();
         blk[r] = -1;
         bi[r] = -1;
     }
-    float oxf = 0.0f, oyf = 0.0f;
-    if (kExp) {  // the block's centre (every wave reduces the same 256 samples)
-        double x0 = __builtin_inf(), x1 = -__builtin_inf(), y0 = __builtin_inf(), y1 = -__builtin_inf();
+    {  // wave 0 parks the samples' operands for the winner re-evaluation (read after barriers)
+        float* s_qx = reinterpret_cast<float*>(smem) + (3 * kScanWaves + 1) * kQPB;
+        if (wave == 0) {
 #pragma unroll
-        for (int r = 0; r < kQPL; ++r) {
-            if (sid[r] < 0) continue;
-            x0 = fmin(x0, xs[r]);
-            x1 = fmax(x1, xs[r]);
-            y0 = fmin(y0, ys[r]);
-            y1 = fmax(y1, ys[r]);
-        }
-        x0 = wave_min(x0);
-        x1 = wave_max(x1);
-        y0 = wave_min(y0);
-        y1 = wave_max(y1);
-        oxf = (float)(0.5 * (x0 + x1));
-        oyf = (float)(0.5 * (y0 + y1));
-    }
-#pragma unroll
-    for (int r = 0; r < kQPL; ++r) {
-        if (kExp) {
-            const float qpx = (float)(xs[r] - (double)oxf), qpy = (float)(ys[r] - (double)oyf);
-            qxr[r] = -2.0f * qpx;  // exact scaling
-            qyr[r] = -2.0f * qpy;
-            if (c == 0 && wave == 0 && sid[r] >= 0)  // |q - o|^2 for nn_finalize (exact in f64)
-                a.sq[a.p][sid[r]] = (double)qpx * (double)qpx + (double)qpy * (double)qpy;
-        } else {
-            qxr[r] = (float)xs[r];
-            qyr[r] = (float)ys[r];
+            for (int r = 0; r < kQPL; ++r) {
+                s_qx[r * 64 + lane] = qxr[r];
+                s_qx[kQPB + r * 64 + lane] = qyr[r];
+            }
         }
     }
+    SCREEN_STAMP(ts1);
     // screen value of (sample r, node (nx, ny)); expanded: the node's (x - ox, y - oy, |.|^2)
     auto val = [&](int r, float px, float py, float pw) {
         if (kExp) return __builtin_fmaf(qxr[r], px, __builtin_fmaf(qyr[r], py, pw));
@@ -833,100 +949,95 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
             pw = 0.0f;
         }
     };
-    const float* nx = a.tr.x32;
-    const float* ny = a.tr.y32;
-    // wave-uniform range (kScanBlk-aligned start): readfirstlane lets the compiler use scalar loads
-    const int per = (((c1 - c0) + kScanWaves - 1) / kScanWaves + kScanBlk - 1) & ~(kScanBlk - 1);
-    const int w0 = __builtin_amdgcn_readfirstlane(min(c0 + wave * per, c1));
-    const int w1 = __builtin_amdgcn_readfirstlane(min(w0 + per, c1));
-    const int wb = w0 + ((w1 - w0) / kScanBlk) * kScanBlk;  // end of the whole blocks
-    if (w0 < wb) {
-        float cx[kScanBlk], cy[kScanBlk];
-#pragma unroll
-        for (int u = 0; u < kScanBlk; ++u) {
-            cx[u] = nx[w0 + u];
-            cy[u] = ny[w0 + u];
+    int r0 = 0;
+#ifdef PP_STAMPS_SCREEN
+    int64_t ts2 = 0;
+#endif
+    for (;;) {
+        const int len = min(kStage, L - r0);
+        if (tid == 0) *s_next = 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
+        __syncthreads();                                   // ... and every other wave's
+        for (int i = 4 * tid; i < len; i += 4 * kScanThreads) {  // prep in place
+            float4 x4 = *reinterpret_cast<const float4*>(stg + i);
+            float4 y4 = *reinterpret_cast<const float4*>(stg + kStage + i);
+            float4 w4;
+            prep(x4.x, y4.x, w4.x);
+            prep(x4.y, y4.y, w4.y);
+            prep(x4.z, y4.z, w4.z);
+            prep(x4.w, y4.w, w4.w);
+            *reinterpret_cast<float4*>(stg + i) = x4;
+            *reinterpret_cast<float4*>(stg + kStage + i) = y4;
+            *reinterpret_cast<float4*>(stg + 2 * kStage + i) = w4;
         }
-        for (int k = w0; k < wb; k += kScanBlk) {
-            float px[kScanBlk], py[kScanBlk], pw[kScanBlk];
+        __syncthreads();
+#ifdef PP_STAMPS_SCREEN
+        if (r0 == 0) ts2 = (int64_t)__builtin_amdgcn_s_memrealtime();
+#endif
+        for (;;) {
+            int g0 = 0;
+            if (lane == 0) g0 = atomicAdd(s_next, kGrab);
+            g0 = __builtin_amdgcn_readfirstlane(__shfl(g0, 0));
+            if (g0 >= len) break;
+            const int g1 = min(g0 + kGrab, len);
+            const int gb = g0 + ((g1 - g0) & ~(kScanBlk - 1));  // whole blocks (a tail: the last)
+            for (int u0 = g0; u0 < gb; u0 += kScanBlk) {
+                float px[kScanBlk], py[kScanBlk], pw[kScanBlk];
 #pragma unroll
-            for (int u = 0; u < kScanBlk; ++u) {
-                px[u] = cx[u];
-                py[u] = cy[u];
-                prep(px[u], py[u], pw[u]);
-            }
-            const int kn = k + kScanBlk < wb ? k + kScanBlk : k;  // prefetch the next block
+                for (int v = 0; v < kScanBlk / 4; ++v) {
+                    const float4 ax = *reinterpret_cast<const float4*>(stg + u0 + 4 * v);
+                    const float4 ay = *reinterpret_cast<const float4*>(stg + kStage + u0 + 4 * v);
+                    const float4 aw = *reinterpret_cast<const float4*>(stg + 2 * kStage + u0 + 4 * v);
+                    px[4 * v] = ax.x, px[4 * v + 1] = ax.y, px[4 * v + 2] = ax.z, px[4 * v + 3] = ax.w;
+                    py[4 * v] = ay.x, py[4 * v + 1] = ay.y, py[4 * v + 2] = ay.z, py[4 * v + 3] = ay.w;
+                    pw[4 * v] = aw.x, pw[4 * v + 1] = aw.y, pw[4 * v + 2] = aw.z, pw[4 * v + 3] = aw.w;
+                }
+                float bm[kQPL];
 #pragma unroll
-            for (int u = 0; u < kScanBlk; ++u) {
-                cx[u] = nx[kn + u];
-                cy[u] = ny[kn + u];
-            }
-            float bm[kQPL];
+                for (int u = 0; u < kScanBlk; ++u) {
 #pragma unroll
-            for (int u = 0; u < kScanBlk; ++u) {
+                    for (int r = 0; r < kQPL; ++r) {
+                        const float d = val(r, px[u], py[u], pw[u]);
+                        bm[r] = u == 0 ? d : __builtin_fminf(bm[r], d);
+                    }
+                }
+                const int k = c0 + r0 + u0;
 #pragma unroll
                 for (int r = 0; r < kQPL; ++r) {
-                    const float d = val(r, px[u], py[u], pw[u]);
-                    bm[r] = u == 0 ? d : __builtin_fminf(bm[r], d);
+                    second[r] = __builtin_amdgcn_fmed3f(best[r], bm[r], second[r]);
+                    if (bm[r] < best[r]) {
+                        best[r] = bm[r];
+                        blk[r] = k;
+                    }
                 }
             }
+            for (int u = gb; u < g1; ++u) {  // the chunk's tail (< kScanBlk nodes): exact top-2
+                const float px = stg[u], py = stg[kStage + u], pw = stg[2 * kStage + u];
 #pragma unroll
-            for (int r = 0; r < kQPL; ++r) {
-                second[r] = __builtin_amdgcn_fmed3f(best[r], bm[r], second[r]);
-                if (bm[r] < best[r]) {
-                    best[r] = bm[r];
-                    blk[r] = k;
+                for (int r = 0; r < kQPL; ++r) {
+                    const float d = val(r, px, py, pw);
+                    second[r] = __builtin_amdgcn_fmed3f(best[r], d, second[r]);
+                    if (d < best[r]) {
+                        best[r] = d;
+                        bi[r] = c0 + r0 + u;
+                        blk[r] = -1;  // the best is a tail node, not a block's
+                    }
                 }
             }
         }
-        // the winning block again, bit-identical: lowest index of the best value and the best of
-        // the block's other nodes (the block minima only carried one each)
-#pragma unroll
-        for (int r = 0; r < kQPL; ++r) {
-            if (blk[r] < 0) continue;
-            const float4* bx = reinterpret_cast<const float4*>(nx + blk[r]);
-            const float4* by = reinterpret_cast<const float4*>(ny + blk[r]);
-            float vx[kScanBlk], vy[kScanBlk], vw[kScanBlk];
-#pragma unroll
-            for (int v = 0; v < kScanBlk / 4; ++v) {
-                const float4 a4 = bx[v], b4 = by[v];
-                vx[4 * v] = a4.x;
-                vx[4 * v + 1] = a4.y;
-                vx[4 * v + 2] = a4.z;
-                vx[4 * v + 3] = a4.w;
-                vy[4 * v] = b4.x;
-                vy[4 * v + 1] = b4.y;
-                vy[4 * v + 2] = b4.z;
-                vy[4 * v + 3] = b4.w;
-            }
-            int ui = -1;
-            float other = __builtin_inff();
-#pragma unroll
-            for (int u = 0; u < kScanBlk; ++u) {
-                prep(vx[u], vy[u], vw[u]);
-                const float d = val(r, vx[u], vy[u], vw[u]);
-                if (ui < 0 && d == best[r])
-                    ui = u;
-                else
-                    other = __builtin_fminf(other, d);
-            }
-            bi[r] = blk[r] + ui;
-            second[r] = __builtin_fminf(second[r], other);
-        }
+        if (r0 + len >= L) break;
+        r0 += len;
+        __syncthreads();  // every wave is done with this round before the next overwrites it
+        issue_round(r0);
     }
-    for (int k = wb; k < w1; ++k) {  // tail (< kScanBlk nodes): exact top-2 per node
-        float px = nx[k], py = ny[k], pw;
-        prep(px, py, pw);
-#pragma unroll
-        for (int r = 0; r < kQPL; ++r) {
-            const float d = val(r, px, py, pw);
-            second[r] = __builtin_amdgcn_fmed3f(best[r], d, second[r]);
-            if (d < best[r]) {
-                best[r] = d;
-                bi[r] = k;
-            }
-        }
-    }
+    SCREEN_STAMP(ts3);
+    // The waves' partials per sample go to LDS — (best, second, key): key = the best block's start,
+    // or kExactNode | index when the best is a tail node (tail nodes follow every block of the
+    // chunk, so keys order ties by node index either way), 0x7fffffff when the wave saw no node —
+    // and one thread per sample merges them; only then is the winning block re-evaluated (one
+    // block per sample, not one per wave): the same arithmetic again, bit-identical, for the lowest
+    // index of the best value and the best of the block's other nodes (the block minima carried one
+    // each).  From LDS when the block is in the last round (always up to ~250k nodes).
     float* s_b = reinterpret_cast<float*>(smem);              // [kScanWaves][kQPB]
     float* s_s = s_b + kScanWaves * kQPB;
     int* s_i = reinterpret_cast<int*>(s_s + kScanWaves * kQPB);
@@ -935,29 +1046,108 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
     for (int r = 0; r < kQPL; ++r) {
         s_b[wave * kQPB + r * 64 + lane] = best[r];
         s_s[wave * kQPB + r * 64 + lane] = second[r];
-        s_i[wave * kQPB + r * 64 + lane] = bi[r];
+        s_i[wave * kQPB + r * 64 + lane] =
+            blk[r] >= 0 ? blk[r] : (bi[r] >= 0 ? (bi[r] | kExactNode) : 0x7fffffff);
         if (wave == 0) s_sid[r * 64 + lane] = sid[r];
     }
     __syncthreads();
-    if (tid < kQPB) {  // one thread per sample merges the waves' partials
-        Top2 tt{s_b[tid], s_s[tid], s_i[tid]};
+    SCREEN_STAMP(ts4);
+#ifdef PP_STAMPS_SCREEN
+    int64_t tm1 = ts4, tm3 = ts4;
+#endif
+    if (tid < kQPB) {  // one thread per sample (sorted position qbase + tid)
+        float bb = s_b[tid], ss = s_s[tid];
+        int key = s_i[tid];
 #pragma unroll
-        for (int w = 1; w < kScanWaves; ++w)
-            tt = merge_top2(tt, Top2{s_b[w * kQPB + tid], s_s[w * kQPB + tid], s_i[w * kQPB + tid]});
+        for (int w = 1; w < kScanWaves; ++w) {
+            const float ob = s_b[w * kQPB + tid], os = s_s[w * kQPB + tid];
+            const int ok = s_i[w * kQPB + tid];
+            const bool take = ob < bb || (ob == bb && ok < key);  // (branch-free)
+            ss = fminf(fminf(ss, os), take ? bb : ob);
+            bb = take ? ob : bb;
+            key = take ? ok : key;
+        }
         const int q = s_sid[tid];
-        if (q >= 0) {
-            const size_t o = (size_t)c * a.Kcap + q;
-            a.pbest[o] = tt.b;
-            a.psecond[o] = tt.s;
-            a.pidx[o] = tt.i;
+        int idx = key == 0x7fffffff ? -1 : (key & ~kExactNode);
+#ifdef PP_STAMPS_SCREEN
+        tm1 = (int64_t)__builtin_amdgcn_s_memrealtime() + (int64_t)(bb * 0.0f) + (q & 0);
+#endif
+#ifdef PP_DIAG_NOREEVAL
+        if (false) {
+#else
+        if (q >= 0 && key != 0x7fffffff && !(key & kExactNode)) {
+#endif
+            // the sample's screen operands, as wave 0 held them
+            const float* s_qx = reinterpret_cast<const float*>(smem) + (3 * kScanWaves + 1) * kQPB;
+            const float qx = s_qx[tid], qy = s_qx[kQPB + tid];
+            const int rel = key - c0 - r0;
+            int ui = -1;
+            float other = __builtin_inff();
+#if defined(PP_DIAG_REEVAL_GLOBAL)
+            if (false) {
+#elif defined(PP_DIAG_REEVAL_BCAST)
+            if (rel >= 0) {
+                const int rel_ = rel;
+                const int rel = rel_ & 0;  // every lane the same block: no bank conflicts (wrong results)
+#else
+            if (rel >= 0) {  // (LDS only: a shared pointer select would make these flat loads)
+#endif
+                float vx[kScanBlk], vy[kScanBlk], vw[kScanBlk];
+#pragma unroll
+                for (int v = 0; v < kScanBlk / 4; ++v) {
+                    const float4 a4 = *reinterpret_cast<const float4*>(stg + rel + 4 * v);
+                    const float4 b4 = *reinterpret_cast<const float4*>(stg + kStage + rel + 4 * v);
+                    const float4 w4 = *reinterpret_cast<const float4*>(stg + 2 * kStage + rel + 4 * v);
+                    vx[4 * v] = a4.x, vx[4 * v + 1] = a4.y, vx[4 * v + 2] = a4.z, vx[4 * v + 3] = a4.w;
+                    vy[4 * v] = b4.x, vy[4 * v + 1] = b4.y, vy[4 * v + 2] = b4.z, vy[4 * v + 3] = b4.w;
+                    vw[4 * v] = w4.x, vw[4 * v + 1] = w4.y, vw[4 * v + 2] = w4.z, vw[4 * v + 3] = w4.w;
+                }
+#pragma unroll
+                for (int u = 0; u < kScanBlk; ++u) {
+                    const float d = kExp ? __builtin_fmaf(qx, vx[u], __builtin_fmaf(qy, vy[u], vw[u]))
+                                         : scan_d2(qx, qy, vx[u], vy[u]);
+                    if (ui < 0 && d == bb)
+                        ui = u;
+                    else
+                        other = __builtin_fminf(other, d);
+                }
+            } else {
+                screen_block_global<kExp>(nx + key, ny + key, qx, qy, oxf, oyf, bb, ui, other);
+            }
+            idx = key + ui;
+            ss = __builtin_fminf(ss, other);
+        }
+#ifdef PP_STAMPS_SCREEN
+        tm3 = (int64_t)__builtin_amdgcn_s_memrealtime() + (int64_t)(ss * 0.0f) + (idx & 0);
+#endif
+        if (q >= 0) {  // by sorted position: coalesced (nn_finalize maps samples through ipos)
+            const size_t o = (size_t)c * a.Kcap + qbase + tid;
+            a.pbest[o] = bb;
+            a.psecond[o] = ss;
+            a.pidx[o] = idx;
         }
     }
+#ifdef PP_STAMPS_SCREEN
+    SCREEN_STAMP(ts5);
+    if (tid == 0) {  // wave 0 of every screen workgroup: phase times summed (100 MHz ticks)
+        unsigned long long* sp = reinterpret_cast<unsigned long long*>(st->stamps);
+        // [0] samples + staging, [1] loop, [2] partials + merge + winner re-evaluation, [3] waves,
+        // [4] max wave total; [5..7]: workgroup 0 (window_kernel)
+        atomicAdd(&sp[0], (unsigned long long)(ts2 - ts0));
+        atomicAdd(&sp[1], (unsigned long long)(ts3 - ts2));
+        atomicAdd(&sp[2], (unsigned long long)(ts5 - ts3));
+        atomicAdd(&sp[3], 1ull);
+        atomicMax(&sp[4], (unsigned long long)(ts5 - ts0));
+        (void)tm1;
+        (void)tm3;
+    }
+#endif
 }
 
 // The first window of a batch: its samples (the later ones come from the previous window kernel
 // workgroup 0, after the commit that decides where the next window starts).
 __global__ __launch_bounds__(1024) void window_samples_kernel(DevState* st, SamplesArgs g, int np) {
-    __shared__ __attribute__((aligned(16))) char smem[256 * 4 + kMaxWindow];
+    __shared__ __attribute__((aligned(16))) char smem[kSamplesLds];
     samples_role(st, g, np, st->it_spec, smem);
 }
 
@@ -1004,7 +1194,8 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
     const double* __restrict__ YAW, double eps_coord, int* __restrict__ out_idx,
     double* __restrict__ out_d2, double* __restrict__ out_pose, PairGrid pg,
     int* __restrict__ cand_cnt, CandEntry* __restrict__ cand,
-    int* __restrict__ pend, const double* __restrict__ sq) {
+    int* __restrict__ pend, const double* __restrict__ sq, const int* __restrict__ ipos,
+    SamplesArgs gen, int gen_next) {
     __shared__ double s_nd2[kFinSamples];  // exact snapshot NN d2 of each sample
     __shared__ int s_pc[kFinSamples];      // pair search: nearer window samples found
     __shared__ int s_pi[kFinSamples][kCandCap];
@@ -1023,6 +1214,26 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
 #endif
     FIN_STAMP(tf0);
     const bool voided = st->void_seq == seq || st->error;
+    if (gen_next && blockIdx.x == gridDim.x - 1) {
+        // the extra workgroup: Space::rand_point of the window after this one, into the parity
+        // the committed previous window freed — it starts where this window ends, or, when the
+        // commit voided this window (a truncation), where the committed one stopped (it_spec;
+        // workgroup 0 advances it_spec only when this window is not voided).  Off the critical
+        // path: steer_prep and steer_walk of this window run before the next screen.
+        __shared__ __attribute__((aligned(16))) char s_gen[kSamplesLds];
+        const int64_t start = voided ? st->it_spec : st->wsp[p] + st->Wp[p];
+#ifdef PP_STAMPS_SCREEN
+        const int64_t tg0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+#endif
+        samples_role(st, gen, 1 - p, start, s_gen);
+#ifdef PP_STAMPS_SCREEN
+        __syncthreads();
+        if (threadIdx.x == 0)  // [6] the next window's samples (nn_finalize's extra workgroup)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&st->stamps[6]),
+                      (unsigned long long)((int64_t)__builtin_amdgcn_s_memrealtime() - tg0));
+#endif
+        return;
+    }
     const int W = voided ? 0 : st->Wp[p];
     const int ns = st->nsp[p], n = st->n;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1049,8 +1260,9 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
         const double qq = sq ? sq[q] : 0.0;  // window mode: screen values are d2 - |q - o|^2
         float cb = __builtin_inff(), cs = __builtin_inff();  // this lane's chunk: raw screen top-2
         int ci = -1;
+        const int pq = ipos ? ipos[q] : q;  // the sample's sorted position (the partials' index)
         if (lane < n_chunks) {
-            const size_t o = (size_t)lane * stride + q;
+            const size_t o = (size_t)lane * stride + pq;
             cb = pbest[o];
             cs = psecond[o];
             ci = pidx[o];
@@ -1172,7 +1384,8 @@ __global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
         const double cthr = s_fd[w];
         const int n_chunks = scan_chunks_used(ns, chunks);
         if (wave == 0) {
-            const bool cc = lane < n_chunks && !((double)pbest[(size_t)lane * stride + qf] > cthr);
+            const int pf = ipos ? ipos[qf] : qf;
+            const bool cc = lane < n_chunks && !((double)pbest[(size_t)lane * stride + pf] > cthr);
             const uint64_t cm = __ballot(cc);
             if (lane == 0) s_cmask = cm;
         }
@@ -2283,11 +2496,16 @@ __device__ __attribute__((always_inline)) inline void commit_role(
 constexpr int kWinLds = (int)sizeof(ResolveLds);
 static_assert(kWinLds <= 160 * 1024, "window kernel LDS");
 static_assert((int)((3 * kScanWaves + 1) * kQPB * 4) <= kWinLds, "screen merge fits the LDS image");
+static_assert(kSamplesLds <= kWinLds, "samples_role fits the window kernel's LDS image");
+static_assert(kScreenStageOff % 16 == 0 && kScreenStageOff + 3 * kStage * 4 + 16 <= kWinLds,
+              "screen staging (x, y, |n-o|^2 of kStage nodes + the piece counter) fits");
+static_assert(kStage % 256 == 0 && kGrab % kScanBlk == 0, "whole DMA quarters and blocks");
 
 __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
     __shared__ __attribute__((aligned(16))) char smem[kWinLds];
     if (blockIdx.x == 0) {
         DevState* st = a.st;
+        SCREEN_STAMP(tw0);
         if (a.resolve) {
             const int W = st->W;
             if (W > 0) {
@@ -2314,20 +2532,13 @@ __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
             // store there raced with the early finishers)
             st->weff = 0x7fffffff;
         }
-        if (a.gen_next) {
-            // Space::rand_point of the window after the screened one, into the parity the
-            // committed window just freed: it starts where the screened window ends, or — when
-            // the commit above voided the screened window (a truncation) — where the committed
-            // one stopped (it_spec).  Off the critical path: the screen takes longer.
-            __shared__ int64_t s_start;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                const bool voided = st->void_seq == a.seq || st->error;
-                s_start = voided ? st->it_spec : st->wsp[a.p] + st->Wp[a.p];
-            }
-            __syncthreads();
-            samples_role(st, a.g, 1 - a.p, s_start, smem);
+#ifdef PP_STAMPS_SCREEN
+        if (threadIdx.x == 0) {  // [5] workgroup 0's resolve + commit, [7] its launches
+            unsigned long long* sp = reinterpret_cast<unsigned long long*>(st->stamps);
+            atomicAdd(&sp[5], (unsigned long long)((int64_t)__builtin_amdgcn_s_memrealtime() - tw0));
+            atomicAdd(&sp[7], 1ull);
         }
+#endif
         return;
     }
     if (a.scan) {
@@ -3430,6 +3641,11 @@ SamplesArgs samples_args(const WindowArgs& a) {
         g.perm[q] = a.perm + (size_t)q * a.Kcap;
         g.cofs[q] = a.cofs + (size_t)q * 257;
         g.sxy[q] = a.sxy + (size_t)q * a.Kcap;
+        g.ssx[q] = a.ssx + (size_t)q * a.Kcap;
+        g.ssy[q] = a.ssy + (size_t)q * a.Kcap;
+        g.ob[q] = a.ob + (size_t)q * (kMaxWindow / kQPB);
+        g.sq[q] = a.sq + (size_t)q * a.Kcap;
+        g.ipos[q] = a.ipos + (size_t)q * a.Kcap;
     }
     return g;
 }
@@ -3507,10 +3723,12 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
     if (ev) (void)hipEventRecord(ev[1], s);
     if (resolve_prev && !kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
-    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples, kFinThreads, 0, s>>>(
+    // one workgroup past the samples' draws the next window's samples
+    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples + 1, kFinThreads, 0, s>>>(
         a.st, p, seq, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, wsx, wsy, a.tr.x32, a.tr.y32,
         a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose,
-        pair_grid(wk.g, p, a.eps_coord), a.cand_cnt, a.cand, a.pend, wk.sq[p]);
+        pair_grid(wk.g, p, a.eps_coord), a.cand_cnt, a.cand, a.pend, wk.sq[p], wk.g.ipos[p], wk.g,
+        1);
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K + kPrepThreads / 8 - 1) / (kPrepThreads / 8);
     steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, wsx, wsy, a.snap_pose, a.cand,
@@ -3544,7 +3762,7 @@ hipError_t launch_nearest(hipStream_t s, const WindowArgs& a) {
     nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples, kFinThreads, 0, s>>>(
         a.st, 0, 0, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, a.wsx, a.wsy, a.tr.x32,
         a.tr.y32, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, nullptr, PairGrid{},
-        nullptr, nullptr, nullptr, nullptr);
+        nullptr, nullptr, nullptr, nullptr, nullptr, wk.g, 0);
     return hipGetLastError();
 }
 
