@@ -1262,6 +1262,7 @@ int pp_rrt_new(pp_ctx* ctx, double sx, double sy, double syaw, double gx, double
     s.n_scan = 1;
     s.it_spec = 0;
     s.void_seq = -1;
+    s.kdyn = kMinDynWindow;  // a young tree starts with short windows (the commit adapts them)
     PP_HIP(hipMemcpy(ctx->d_state.p, &s, sizeof(DevState), hipMemcpyHostToDevice));
     ctx->h_state.p[0] = s;
     ctx->n = 1;
@@ -1299,7 +1300,9 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
     hipStream_t st = ctx->stream;
     while (ctx->it < target) {
         const int K = ctx->K;
-        const int64_t nw64 = std::min<int64_t>((target - ctx->it + K - 1) / K, kMaxBatch);
+        // windows draw min(K, kdyn) samples (the device adapts kdyn): enough windows for that
+        const int64_t Kd = std::max(1, std::min(K, ctx->h_state.p[0].kdyn > 0 ? ctx->h_state.p[0].kdyn : K));
+        const int64_t nw64 = std::min<int64_t>((target - ctx->it + Kd - 1) / Kd, kMaxBatch);
         const int nw = (int)nw64;
         if ((r = ensure_tree(ctx, ctx->n + (int64_t)nw * K))) return r;
         WindowArgs a = ctx->window_args(ctx->d_state.p);

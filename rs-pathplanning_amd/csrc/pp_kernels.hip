@@ -663,7 +663,9 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
     int* s_j = reinterpret_cast<int*>(smem + 256 * 4 + kMaxWindow);  // [K] sorted position -> sample
     const int tid = threadIdx.x, NT = blockDim.x;
     const int64_t rem = g.target - start;
-    const int W = (rem <= 0 || st->error) ? 0 : (rem < g.K ? (int)rem : g.K);
+    // the adaptive window (kdyn, set by the commits; results never depend on the window size)
+    const int Kw = st->kdyn > 0 ? min(g.K, st->kdyn) : g.K;
+    const int W = (rem <= 0 || st->error) ? 0 : (rem < Kw ? (int)rem : Kw);
     if (tid == 0) {
         st->Wp[np] = W;
         st->wsp[np] = start;
@@ -2487,6 +2489,18 @@ __device__ __attribute__((always_inline)) inline void commit_role(
             st->it_spec = it0 + Weff;
             if (void_next >= 0) st->void_seq = void_next;
         }
+        // adaptive window (a young tree: the window's samples are mostly nearer to each other than
+        // to the tree, lists overflow and windows are cut): a cut window shrinks the next draws to
+        // the power of two at or above where it stopped, a full one doubles them (<= K, clamped by
+        // the draws).  Only the speed depends on it: the results are those of one sample at a time.
+        int kd = st->kdyn > 0 ? st->kdyn : kMaxWindow;
+        if (Weff < W) {
+            kd = kMinDynWindow;
+            while (kd < Weff) kd <<= 1;
+        } else if (W >= kd) {
+            kd = min(2 * kd, kMaxWindow);
+        }
+        st->kdyn = kd;
     }
 }
 
@@ -2519,9 +2533,16 @@ __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
                 }
                 // (same workgroup: the barrier's workgroup-scope fence orders these stores)
                 __syncthreads();
+#ifdef PP_STAMPS_RESOLVE
+                const int64_t tc0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+#endif
                 commit_role<kScanThreads>(st, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.snap_status,
                                           a.snap_yaw, a.fin_par, a.cand_cnt, W,
                                           a.scan ? a.seq : -1, smem);
+#ifdef PP_STAMPS_RESOLVE
+                __syncthreads();
+                if (threadIdx.x == 0) st->stamps[7] += (int64_t)__builtin_amdgcn_s_memrealtime() - tc0;
+#endif
             }
         }
         if (threadIdx.x == 0) {  // the screened window's counters start at zero

@@ -24,6 +24,7 @@ constexpr int kLiteralCap = 16384;   // points per literal-path scratch buffer
 constexpr int kLiteralWaves = 256;   // literal scratch buffers (explicit-task kernel)
 constexpr int kResolveThreads = 512;  // resolve_tail_kernel (8 waves, 256 VGPRs: the repair path)
 constexpr int kMaxWindow = 4096;     // K limit: the resolve keeps the window's state in LDS
+constexpr int kMinDynWindow = 128;   // the adaptive window's floor (DevState.kdyn)
 constexpr int kSteerPrepBytes = 152; // sizeof(SteerPrep) (checked in pp_kernels.hip)
 constexpr int kPdCap = 63;           // grid points per task stored by steer_prep (one walk chunk)
 constexpr int kPrepLanes = 8;        // lanes per task in steer_prep's phase A
@@ -115,7 +116,7 @@ struct DevState {
     int nsp[2];      // per parity: tree nodes its scan covered
     int64_t void_seq;  // window sequence number voided by a truncated predecessor (-1: none)
     int resolve_bail;  // the window kernel's resolve needed a repair: resolve_tail_kernel redoes it
-    int pad2;
+    int kdyn;          // adaptive window: samples drawn per window (<= K; the commit adapts it)
     // statistics (pp_stats)
     int64_t iterations, accepted, windows, truncations, repair_rounds, repairs, literal_repairs,
         nn_flagged, node_evals;
