@@ -277,6 +277,7 @@ def screen_roofline(sp, pmc):
         "traffic": pmc.get("hbm_bytes_per_launch"),
         "avg_launch_ms": round(avg_ms, 5),
         "evals_per_launch": int(evals),
+        "launches": int(sp["nn_scan_launches"]),
         "flop_per_eval": FLOP_PER_EVAL,
         "measured": f"HIP events on the planner stream, {sp['nn_scan_launches']} launches of the "
                     "profiled pass that follows the timed region (same workload)",
@@ -307,6 +308,7 @@ def walk_roofline(sp, pmc, name):
     achieved = pts / (avg_ms * 1e-3)
     r = {"kernel": f"steer_walk ({name})", "bound": "valu", "achieved": round(achieved / 1e9, 4),
          "unit": "Gpoints/s", "avg_launch_ms": round(avg_ms, 5), "points_per_launch": int(pts),
+         "launches": int(sp["steer_launches"]),
          "traffic": pmc.get("hbm_bytes_per_launch"),
          "measured": f"HIP events around steer_walk, {sp['steer_launches']} launches of the "
                      "profiled pass"}

@@ -92,7 +92,24 @@ int pp_dubins_path_planning_batch(pp_ctx* ctx, const pp_dubins_config* confs, in
                                   double* px, double* py, double* pyaw, int32_t* n_points,
                                   int32_t* word, double* cost);
 
+/* dubins_path_planning_from_origin (dubins.rs:326-399) for n configurations on the GPU, each the
+ * 5 doubles (dx, dy, eyaw, c, step_size) of the Rust arguments (c = curvature, 1 / turn radius):
+ * the LOCAL points after generate_local_course's trim (dubins.rs:281-288) and the yaw as generated
+ * (not wrapped by pi_2_pi).  Outputs and errors as pp_dubins_path_planning_batch. */
+int pp_dubins_path_planning_from_origin_batch(pp_ctx* ctx, const double* conf5, int n, int cap,
+                                              double* px, double* py, double* pyaw,
+                                              int32_t* n_points, int32_t* word, double* cost);
+/* lsl, rsr, lsr, rsl, rlr, lrl (dubins.rs:27-153) of n (alpha, beta, d) triples on the GPU:
+ * tpq[18 i + 3 w + {0, 1, 2}] = (t, p, q) of word w in ALL_PLANNERS order (dubins.rs:291),
+ * ok[6 i + w] = 0 where the word is None (then its t, p, q are 0). */
+int pp_dubins_words_batch(pp_ctx* ctx, const double* abd, int n, double* tpq, int32_t* ok);
+
 /* ------------------------------------------------------------------ scene (src/rrt.rs) */
+/* create_circle(center, radius) (rrt.rs:43-60): the crate's polygon, n = ceil(2 pi r) chords and
+ * the n + 1 vertices i = 0..=n at angle 2 pi / n * i, x then y interleaved in xy (2 (n + 1)
+ * doubles, same evaluation order as the Rust expression; host arithmetic, like pp_mod2pi).
+ * *n = the vertex count; PP_ERR_CAPACITY when cap (vertices) is too small. */
+int pp_create_circle(double cx, double cy, double radius, double* xy, int cap, int* n);
 /* Space::new(bounds, Robot::new(width, height, max_steer), obstacles) (rrt.rs:25,81-122) with
  * the bounds an axis-aligned rectangle (x0, y0)-(x1, y1) and the obstacles create_circle discs
  * (rrt.rs:43-60) given as centres and radii.  Bounds shrink and discs grow by width/2. */
@@ -145,6 +162,13 @@ int pp_rrt_iteration(pp_ctx* ctx, int64_t* it);
 /* copy the tree out (root first): coordinates, yaw (Node.yaw, rrt.rs:161-166), parent (-1 root) */
 int pp_rrt_tree_export(pp_ctx* ctx, double* x, double* y, double* yaw, int32_t* parent,
                        int64_t cap, int64_t* n);
+/* line_to_origin(node, Robot.max_steer, step_size) (rrt.rs:291-321) of tree node `node`: the
+ * concatenated polyline node -> ... -> root in the sequential order (each edge's Dubins points
+ * child -> parent, steered on the GPU; [(x, y)] of the child where the steer is None; the root
+ * contributes [(root x, root y)]).  *n = its points; PP_ERR_CAPACITY when cap is too small (call
+ * with cap 0 for the size). */
+int pp_rrt_line_to_origin(pp_ctx* ctx, int32_t node, double* x, double* y, int64_t cap,
+                          int64_t* n);
 /* RRT::get_nearest_node (rrt.rs:378-391) for k points: exact nearest by dx*dx+dy*dy, lowest
  * index on ties; d2 may be NULL */
 int pp_rrt_get_nearest_node_batch(pp_ctx* ctx, const double* qx, const double* qy, int k,

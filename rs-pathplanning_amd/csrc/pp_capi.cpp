@@ -860,6 +860,99 @@ int pp_dubins_path_planning_batch(pp_ctx* ctx, const pp_dubins_config* confs, in
     return PP_OK;
 }
 
+int pp_dubins_path_planning_from_origin_batch(pp_ctx* ctx, const double* conf5, int n, int cap,
+                                              double* px, double* py, double* pyaw,
+                                              int32_t* n_points, int32_t* word, double* cost) {
+    int r = check_ctx(ctx, false, false);
+    if (r) return r;
+    if (n < 0 || cap <= 0 || (n > 0 && (!conf5 || !px || !py || !pyaw || !n_points || !word || !cost)))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad dubins batch arguments");
+    if (n == 0) return PP_OK;
+    for (int i = 0; i < n; ++i)
+        if (!(conf5[5 * i + 4] > 0.0))
+            return set_err(PP_ERR_INVALID_ARGUMENT, "step_size must be > 0");
+    const size_t nn = (size_t)n, tot = nn * (size_t)cap;
+    DBuf<double> dconf, dpx, dpy, dpyaw, dcost;
+    DBuf<int> dn, dword, dstat;
+    PP_HIP(dconf.reserve(nn * 5));
+    PP_HIP(dpx.reserve(tot));
+    PP_HIP(dpy.reserve(tot));
+    PP_HIP(dpyaw.reserve(tot));
+    PP_HIP(dcost.reserve(nn));
+    PP_HIP(dn.reserve(nn));
+    PP_HIP(dword.reserve(nn));
+    PP_HIP(dstat.reserve(nn));
+    hipStream_t st = ctx->stream;
+    PP_HIP(hipMemcpyAsync(dconf.p, conf5, nn * 5 * sizeof(double), hipMemcpyHostToDevice, st));
+    PP_HIP(launch_dubins_origin(st, dconf.p, n, cap, dpx.p, dpy.p, dpyaw.p, dn.p, dword.p, dcost.p, dstat.p));
+    std::vector<int> stat(nn), nv(nn), wv(nn);
+    PP_HIP(hipMemcpyAsync(px, dpx.p, tot * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(py, dpy.p, tot * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(pyaw, dpyaw.p, tot * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(cost, dcost.p, nn * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(nv.data(), dn.p, nn * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(wv.data(), dword.p, nn * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(stat.data(), dstat.p, nn * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    bool overflow = false;
+    for (size_t i = 0; i < nn; ++i) {
+        if (stat[i] == kSteerOverflow) {
+            overflow = true;
+            word[i] = -2;
+            n_points[i] = 0;
+        } else if (stat[i] == kSteerNone) {
+            word[i] = -1;
+            n_points[i] = 0;
+        } else {
+            word[i] = wv[i];
+            n_points[i] = nv[i];
+        }
+    }
+    if (overflow) return set_err(PP_ERR_CAPACITY, "a configuration needs more than cap points");
+    return PP_OK;
+}
+
+int pp_dubins_words_batch(pp_ctx* ctx, const double* abd, int n, double* tpq, int32_t* ok) {
+    int r = check_ctx(ctx, false, false);
+    if (r) return r;
+    if (n < 0 || (n > 0 && (!abd || !tpq || !ok)))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad dubins words arguments");
+    if (n == 0) return PP_OK;
+    const size_t nn = (size_t)n;
+    DBuf<double> dabd, dtpq;
+    DBuf<int> dok;
+    PP_HIP(dabd.reserve(3 * nn));
+    PP_HIP(dtpq.reserve(18 * nn));
+    PP_HIP(dok.reserve(6 * nn));
+    hipStream_t st = ctx->stream;
+    PP_HIP(hipMemcpyAsync(dabd.p, abd, 3 * nn * sizeof(double), hipMemcpyHostToDevice, st));
+    PP_HIP(launch_dubins_words(st, dabd.p, n, dtpq.p, dok.p));
+    static_assert(sizeof(int) == sizeof(int32_t), "ok words");
+    PP_HIP(hipMemcpyAsync(tpq, dtpq.p, 18 * nn * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(ok, dok.p, 6 * nn * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    return PP_OK;
+}
+
+int pp_create_circle(double cx, double cy, double radius, double* xy, int cap, int* n) {
+    if (!n || !(radius > 0.0) || cap < 0 || (cap > 0 && !xy))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad create_circle arguments");
+    // rrt.rs:43-60: circum = 2 PI r; n = ceil(circum / 1.0); vertices 0..(n + 1) as usize
+    const double kPi = 3.14159265358979323846;
+    const double circum = 2.0 * kPi * radius;
+    const double nf = std::ceil(circum / 1.0);
+    if (!(nf < 1.0e8)) return set_err(PP_ERR_INVALID_ARGUMENT, "radius too large");
+    const int count = (int)(nf + 1.0);
+    *n = count;
+    if (cap < count) return cap == 0 ? PP_OK : set_err(PP_ERR_CAPACITY, "vertex buffer too small");
+    for (int i = 0; i < count; ++i) {
+        const double a = 2.0 * kPi / nf * (double)i;
+        xy[2 * i] = std::cos(a) * radius + cx;
+        xy[2 * i + 1] = std::sin(a) * radius + cy;
+    }
+    return PP_OK;
+}
+
 namespace {
 // Uniform grid over the scene's collision items (discs, or polygon edges in Q10p) for the steer
 // kernels' exact cull: item k is listed in every cell its cull box [bx0, bx1] x [by0, by1]
@@ -1379,6 +1472,72 @@ int pp_rrt_tree_export(pp_ctx* ctx, double* x, double* y, double* yaw, int32_t* 
     if (yaw) PP_HIP(hipMemcpyAsync(yaw, ctx->YAW.p, k * sizeof(double), hipMemcpyDeviceToHost, st));
     if (parent) PP_HIP(hipMemcpyAsync(parent, ctx->PAR.p, k * sizeof(int), hipMemcpyDeviceToHost, st));
     PP_HIP(hipStreamSynchronize(st));
+    return PP_OK;
+}
+
+int pp_rrt_line_to_origin(pp_ctx* ctx, int32_t node, double* x, double* y, int64_t cap,
+                          int64_t* n) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (!n || node < 0 || node >= ctx->n || cap < 0 || (cap > 0 && (!x || !y)))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad line_to_origin arguments");
+    // the path node -> root (NodeIter, rrt.rs:248-265): the tree's rows, read once
+    const size_t nt = (size_t)ctx->n;
+    std::vector<double> hx(nt), hy(nt), hyaw(nt);
+    std::vector<int> hp(nt);
+    hipStream_t st = ctx->stream;
+    PP_HIP(hipMemcpyAsync(hx.data(), ctx->X.p, nt * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(hy.data(), ctx->Y.p, nt * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(hyaw.data(), ctx->YAW.p, nt * sizeof(double), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(hp.data(), ctx->PAR.p, nt * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    std::vector<int> path;
+    for (int v = node; v >= 0; v = hp[(size_t)v]) {
+        if (path.size() > nt) return set_err(PP_ERR_STATE, "parent cycle in the tree");
+        path.push_back(v);
+    }
+    // every edge child -> parent as dubins_path_planning(child pose, parent pose, R, step) on the
+    // GPU (rrt.rs:297-311); the capacity bound of pp_dubins_path_planning_batch's callers
+    const int ne = (int)path.size() - 1;
+    std::vector<pp_dubins_config> conf((size_t)std::max(ne, 1));
+    int pcap = 16;
+    for (int e = 0; e < ne; ++e) {
+        const int c = path[(size_t)e], p = path[(size_t)e + 1];
+        conf[(size_t)e] = pp_dubins_config{hx[(size_t)c], hy[(size_t)c], hyaw[(size_t)c],
+                                           hx[(size_t)p], hy[(size_t)p], hyaw[(size_t)p],
+                                           ctx->max_steer, ctx->step};
+        const double d = std::hypot(hx[(size_t)p] - hx[(size_t)c], hy[(size_t)p] - hy[(size_t)c]);
+        pcap = std::max(pcap, (int)((6.0 * 3.14159265358979323846 + d / ctx->max_steer + 4.0) /
+                                    ctx->step) + 16);
+    }
+    std::vector<double> px, py, pyaw, cost((size_t)std::max(ne, 1));
+    std::vector<int32_t> np((size_t)std::max(ne, 1)), word((size_t)std::max(ne, 1));
+    if (ne > 0) {
+        px.resize((size_t)ne * pcap);
+        py.resize((size_t)ne * pcap);
+        pyaw.resize((size_t)ne * pcap);
+        if ((r = pp_dubins_path_planning_batch(ctx, conf.data(), ne, pcap, px.data(), py.data(),
+                                               pyaw.data(), np.data(), word.data(), cost.data())))
+            return r;
+    }
+    int64_t w = 0;
+    auto put = [&](double a, double b) {
+        if (w < cap) {
+            x[w] = a;
+            y[w] = b;
+        }
+        ++w;
+    };
+    for (int e = 0; e < ne; ++e) {
+        if (word[(size_t)e] < 0) {  // None: the child's own point (rrt.rs:313)
+            put(hx[(size_t)path[(size_t)e]], hy[(size_t)path[(size_t)e]]);
+            continue;
+        }
+        for (int k = 0; k < np[(size_t)e]; ++k) put(px[(size_t)e * pcap + k], py[(size_t)e * pcap + k]);
+    }
+    put(hx[(size_t)path.back()], hy[(size_t)path.back()]);  // the root (rrt.rs:316)
+    *n = w;
+    if (cap > 0 && w > cap) return set_err(PP_ERR_CAPACITY, "line buffer smaller than the line");
     return PP_OK;
 }
 

@@ -209,18 +209,12 @@ __device__ inline Pose interp_local(int mode, double length, double max_curvatur
     return r;
 }
 
-// Literal single-thread restatement of dubins_path_planning (dubins.rs:326-428) writing WORLD
-// points: the slow path for the measure-zero trim cases, and the pp_dubins_batch API.
-// Returns kSteerSome / kSteerNone / kSteerOverflow (cap < n_point or the Rust index panic).
-__device__ inline int dubins_literal(double sx, double sy, double syaw, double ex0, double ey0,
-                                     double eyaw, double turn_radius, double step_size, double* px,
-                                     double* py, double* pyaw, int cap, int* n_out, int* word_out,
-                                     double* cost_out) {
-    const double ex = ex0 - sx, ey = ey0 - sy;
-    const double c = 1.0 / turn_radius;
-    const double lex = cos(syaw) * ex + sin(syaw) * ey;
-    const double ley = -(sin(syaw)) * ex + cos(syaw) * ey;
-    const double leyaw = eyaw - syaw;
+// Literal single-thread restatement of dubins_path_planning_from_origin (dubins.rs:326-399): the
+// LOCAL points after generate_local_course's trim, yaw as generated (not wrapped).  Returns
+// kSteerSome / kSteerNone / kSteerOverflow (cap < n_point or the Rust index panic).
+__device__ inline int dubins_local(double lex, double ley, double leyaw, double c, double step_size,
+                                   double* px, double* py, double* pyaw, int cap, int* n_out,
+                                   int* word_out, double* cost_out) {
     const Steer s = select_word(lex, ley, leyaw, c);
     if (s.word < 0) return kSteerNone;
     const double lengths[3] = {s.t, s.p, s.q};
@@ -267,6 +261,28 @@ __device__ inline int dubins_literal(double sx, double sy, double syaw, double e
         last = px[len - 1];
         len -= 1;
     }
+    *n_out = len;
+    *word_out = s.word;
+    *cost_out = s.cost;
+    return kSteerSome;
+}
+
+// Literal single-thread restatement of dubins_path_planning (dubins.rs:401-428) writing WORLD
+// points: the slow path for the measure-zero trim cases, and the pp_dubins_batch API.
+// Returns kSteerSome / kSteerNone / kSteerOverflow (cap < n_point or the Rust index panic).
+__device__ inline int dubins_literal(double sx, double sy, double syaw, double ex0, double ey0,
+                                     double eyaw, double turn_radius, double step_size, double* px,
+                                     double* py, double* pyaw, int cap, int* n_out, int* word_out,
+                                     double* cost_out) {
+    const double ex = ex0 - sx, ey = ey0 - sy;
+    const double c = 1.0 / turn_radius;
+    const double lex = cos(syaw) * ex + sin(syaw) * ey;
+    const double ley = -(sin(syaw)) * ex + cos(syaw) * ey;
+    const double leyaw = eyaw - syaw;
+    int len = 0;
+    const int r = dubins_local(lex, ley, leyaw, c, step_size, px, py, pyaw, cap, &len, word_out,
+                               cost_out);
+    if (r != kSteerSome) return r;
     // back to the world frame, dubins.rs:412-422
     const double cs = cos(-syaw), sn = sin(-syaw);
     for (int i = 0; i < len; ++i) {
@@ -276,8 +292,6 @@ __device__ inline int dubins_literal(double sx, double sy, double syaw, double e
         pyaw[i] = pi_2_pi(pyaw[i] + syaw);
     }
     *n_out = len;
-    *word_out = s.word;
-    *cost_out = s.cost;
     return kSteerSome;
 }
 

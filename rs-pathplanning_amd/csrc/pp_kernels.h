@@ -121,6 +121,13 @@ struct StarArgs {
 hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps);
 hipError_t launch_star_init(hipStream_t s, const StarArgs& a, const double* starts);
 
+// dubins_path_planning_from_origin for n (dx, dy, eyaw, c, step_size) configurations
+hipError_t launch_dubins_origin(hipStream_t st, const double* conf, int n, int cap, double* px,
+                                double* py, double* pyaw, int* n_out, int* word_out,
+                                double* cost_out, int* status_out);
+// the six Dubins words of n (alpha, beta, d) triples
+hipError_t launch_dubins_words(hipStream_t st, const double* abd, int n, double* tpq, int* ok);
+
 hipError_t launch_dubins_batch(hipStream_t st, const double* conf, int n, int cap, double* px,
                                double* py, double* pyaw, int* n_out, int* word_out,
                                double* cost_out, int* status_out);

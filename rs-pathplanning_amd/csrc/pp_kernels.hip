@@ -534,6 +534,54 @@ __global__ __launch_bounds__(64) void dubins_batch_kernel(const double* __restri
     status_out[i] = r;
 }
 
+// dubins_path_planning_from_origin (dubins.rs:326-399) for n configurations (dx, dy, eyaw, c,
+// step_size): local points, yaw as generated
+__global__ __launch_bounds__(64) void dubins_origin_kernel(const double* __restrict__ conf, int n,
+                                                           int cap, double* __restrict__ px,
+                                                           double* __restrict__ py,
+                                                           double* __restrict__ pyaw,
+                                                           int* __restrict__ n_out,
+                                                           int* __restrict__ word_out,
+                                                           double* __restrict__ cost_out,
+                                                           int* __restrict__ status_out) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= n) return;
+    const double* c = conf + (size_t)i * 5;
+    int np = 0, word = -1;
+    double cost = 0.0;
+    const int r = dubins_local(c[0], c[1], c[2], c[3], c[4], px + (size_t)i * cap,
+                               py + (size_t)i * cap, pyaw + (size_t)i * cap, cap, &np, &word,
+                               &cost);
+    n_out[i] = np;
+    word_out[i] = word;
+    cost_out[i] = cost;
+    status_out[i] = r;
+}
+
+// the six words lsl, rsr, lsr, rsl, rlr, lrl (dubins.rs:27-153) of n (alpha, beta, d) triples:
+// tpq[18 i + 3 w ..] = (t, p, q) of word w, ok[6 i + w] = 0 where the word is None
+__global__ __launch_bounds__(64) void dubins_words_kernel(const double* __restrict__ abd, int n,
+                                                          double* __restrict__ tpq,
+                                                          int* __restrict__ ok) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= n) return;
+    const double alpha = abd[3 * i], beta = abd[3 * i + 1], d = abd[3 * i + 2];
+    const Trig g = make_trig(alpha, beta);
+    Word w[6];
+    w[0] = word_lsl(alpha, beta, d, g);
+    w[1] = word_rsr(alpha, beta, d, g);
+    w[2] = word_lsr(alpha, beta, d, g);
+    w[3] = word_rsl(alpha, beta, d, g);
+    w[4] = word_rlr(alpha, beta, d, g);
+    w[5] = word_lrl(alpha, beta, d, g);
+    for (int k = 0; k < 6; ++k) {
+        ok[6 * i + k] = w[k].ok ? 1 : 0;
+        tpq[18 * i + 3 * k] = w[k].ok ? w[k].t : 0.0;
+        tpq[18 * i + 3 * k + 1] = w[k].ok ? w[k].p : 0.0;
+        tpq[18 * i + 3 * k + 2] = w[k].ok ? w[k].q : 0.0;
+    }
+}
+
 // ------------------------------------------------------------------------- window pipeline
 //
 // One speculative window w = window_kernel (w's NN screen ‖ resolve + commit of w - 1) →
@@ -1985,8 +2033,18 @@ __host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
 // error) and that has no nearer window sample is queued for the resolve (the others were queued
 // by nn_finalize's pair search).  wg_points (profiling only, else null): workgroup b adds its
 // walked polyline points to wg_points[b] (its own slot: no atomics on a shared address).
-template <bool kLds>
-__global__ __launch_bounds__(kWalkThreads) void steer_walk_kernel(DevState* __restrict__ st,
+// kMinW: minimum waves per SIMD the compiler must allow (register budget).  The window pipeline
+// walks ~1 task per wave (1: 94 VGPRs, 2 workgroups per CU); the query batches walk dozens of
+// tasks per wave, latency-bound, and run better at 6 (80 VGPRs, 3 workgroups per CU: config 3
+// 279 -> 309 M it/s; 8 spills too much).
+constexpr int kWalkMinWWindow = 1;
+constexpr int kWalkMinWBatch = 6;
+#ifndef PP_STAR_WALK_MINW
+#define PP_STAR_WALK_MINW kWalkMinWBatch
+#endif
+constexpr int kWalkMinWStar = PP_STAR_WALK_MINW;
+template <bool kLds, int kMinW>
+__global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevState* __restrict__ st,
                                                          SceneDev sc,
                                                          const PrepRec* __restrict__ rec,
                                                          const double* __restrict__ pdbuf,
@@ -2033,6 +2091,7 @@ __global__ __launch_bounds__(kWalkThreads) void steer_walk_kernel(DevState* __re
 // late with a share of tasks — the device's CU count times the workgroups per CU the occupancy
 // API gives for this instantiation and its dynamic LDS (the scene image decides; at most 4 of 8
 // waves each), read once per (device, image size) instead of assuming 256 CUs and 160 KB.
+template <int kMinW = kWalkMinWWindow>
 inline int walk_grid_cap(int scene_bytes) {
     static std::mutex mu;
     static std::map<std::pair<int, int>, int> cache;
@@ -2047,9 +2106,9 @@ inline int walk_grid_cap(int scene_bytes) {
         cus = prop.multiProcessorCount;
     const hipError_t e =
         scene_bytes > 0
-            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, steer_walk_kernel<true>,
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, steer_walk_kernel<true, kMinW>,
                                                           kWalkThreads, walk_lds_bytes(scene_bytes))
-            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, steer_walk_kernel<false>,
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, steer_walk_kernel<false, kMinW>,
                                                           kWalkThreads, walk_lds_bytes(0));
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
     per_cu = std::min(4, per_cu);
@@ -3081,7 +3140,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int nn_blocks = std::min((Q + 3) / 4, 4096);  // one wave per query
     const int prep_blocks = std::min((T + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
-                                     std::min(kWalkMaxWG, walk_grid_cap(a.sc.lds_bytes)));
+                                     std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch>(a.sc.lds_bytes)));
     const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
     const int lds = a.sc.lds_bytes;
     for (int k = 0; k < steps; ++k) {
@@ -3093,10 +3152,10 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
                                                       nullptr, a.rec, a.pdbuf, a.yaw, a.tasks);
         if (a.ev) (void)hipEventRecord(a.ev[4 * k + 2], s);
         if (lds > 0)
-            steer_walk_kernel<true><<<walk_blocks, kWalkThreads, walk_lds_bytes(lds), s>>>(
+            steer_walk_kernel<true, kWalkMinWBatch><<<walk_blocks, kWalkThreads, walk_lds_bytes(lds), s>>>(
                 a.st, a.sc, a.rec, a.pdbuf, nullptr, a.status, nullptr, nullptr, a.wg_points);
         else
-            steer_walk_kernel<false><<<walk_blocks, kWalkThreads, walk_lds_bytes(0), s>>>(
+            steer_walk_kernel<false, kWalkMinWBatch><<<walk_blocks, kWalkThreads, walk_lds_bytes(0), s>>>(
                 a.st, a.sc, a.rec, a.pdbuf, nullptr, a.status, nullptr, nullptr, a.wg_points);
         if (a.ev) (void)hipEventRecord(a.ev[4 * k + 3], s);
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
@@ -3585,11 +3644,11 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
     const int prepA = std::min((Q + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int prepB = std::min((TB + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walkA = std::min((Q + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
-                               std::min(kWalkMaxWG, walk_grid_cap(a.sc.lds_bytes)));
+                               std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWStar>(a.sc.lds_bytes)));
     const int lds = a.sc.lds_bytes;
     // a scene read from global memory (no LDS image) makes the walk latency-bound: fill every
     // wave slot the walk's 48 VGPRs allow (4 workgroups of 8 waves per CU)
-    const int walk_cap = lds > 0 ? std::min(kWalkMaxWG, walk_grid_cap(lds)) : 1024;
+    const int walk_cap = lds > 0 ? std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWStar>(lds)) : 1024;
     const int walkB = std::min((TB + kWalkThreads / 64 - 1) / (kWalkThreads / 64), walk_cap);
     // ev (profiling): 8 per step — around star_sample, then around each round's walk
     auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, const StarTaskExt* ext,
@@ -3598,10 +3657,10 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
                                                       a.rec, a.pdbuf, yaw, t, cost, ext);
         if (ev) (void)hipEventRecord(ev[0], s);
         if (lds > 0)
-            steer_walk_kernel<true><<<wb, kWalkThreads, walk_lds_bytes(lds), s>>>(
+            steer_walk_kernel<true, kWalkMinWStar><<<wb, kWalkThreads, walk_lds_bytes(lds), s>>>(
                 st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr, a.wg_points);
         else
-            steer_walk_kernel<false><<<wb, kWalkThreads, walk_lds_bytes(0), s>>>(
+            steer_walk_kernel<false, kWalkMinWStar><<<wb, kWalkThreads, walk_lds_bytes(0), s>>>(
                 st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr, a.wg_points);
         if (ev) (void)hipEventRecord(ev[1], s);
     };
@@ -3760,10 +3819,10 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     const int nwg = std::min((K + K / 4 + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
                              std::min(kWalkMaxWG, walk_grid_cap(a.sc.lds_bytes)));
     if (lds > 0)
-        steer_walk_kernel<true><<<nwg, kWalkThreads, walk_lds_bytes(lds), s>>>(
+        steer_walk_kernel<true, kWalkMinWWindow><<<nwg, kWalkThreads, walk_lds_bytes(lds), s>>>(
             a.st, a.sc, a.rec, a.pdbuf, a.cand, a.snap_status, a.cand_cnt, a.pend, a.wg_points);
     else
-        steer_walk_kernel<false><<<nwg, kWalkThreads, walk_lds_bytes(0), s>>>(
+        steer_walk_kernel<false, kWalkMinWWindow><<<nwg, kWalkThreads, walk_lds_bytes(0), s>>>(
             a.st, a.sc, a.rec, a.pdbuf, a.cand, a.snap_status, a.cand_cnt, a.pend, a.wg_points);
     if (ev) (void)hipEventRecord(ev[3], s);
     return hipGetLastError();
@@ -3841,6 +3900,21 @@ hipError_t launch_steer_tasks(hipStream_t st, const SceneDev& sc, const TreeDev&
     if (waves > 16384) waves = 16384;
     steer_tasks_kernel<<<(waves + 3) / 4, 256, 0, st>>>(sc, tr, tasks, n, out_status, out_yaw,
                                                         scratch);
+    return hipGetLastError();
+}
+
+hipError_t launch_dubins_origin(hipStream_t st, const double* conf, int n, int cap, double* px,
+                                double* py, double* pyaw, int* n_out, int* word_out,
+                                double* cost_out, int* status_out) {
+    if (n <= 0) return hipSuccess;
+    dubins_origin_kernel<<<(n + 63) / 64, 64, 0, st>>>(conf, n, cap, px, py, pyaw, n_out, word_out,
+                                                       cost_out, status_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_dubins_words(hipStream_t st, const double* abd, int n, double* tpq, int* ok) {
+    if (n <= 0) return hipSuccess;
+    dubins_words_kernel<<<(n + 63) / 64, 64, 0, st>>>(abd, n, tpq, ok);
     return hipGetLastError();
 }
 

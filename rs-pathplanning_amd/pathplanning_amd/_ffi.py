@@ -33,7 +33,9 @@ _ERR_NAMES = {
 EXPORTED = [
     "pp_abi_version", "pp_last_error", "pp_device_count", "pp_create", "pp_destroy",
     "pp_synchronize", "pp_rng_u64", "pp_gen_range", "pp_mod2pi", "pp_pi_2_pi",
-    "pp_dubins_path_planning_batch", "pp_space_new", "pp_space_set_grid", "pp_space_get_bounds",
+    "pp_dubins_path_planning_batch", "pp_dubins_path_planning_from_origin_batch",
+    "pp_dubins_words_batch", "pp_create_circle", "pp_rrt_line_to_origin",
+    "pp_space_new", "pp_space_set_grid", "pp_space_get_bounds",
     "pp_space_new_polygons", "pp_space_verify_batch",
     "pp_rrt_new",
     "pp_rrt_set_window", "pp_rrt_extend", "pp_rrt_plan_one", "pp_rrt_tree_size",
@@ -100,6 +102,11 @@ def lib():
             "pp_pi_2_pi": ([C.c_double], C.c_double),
             "pp_dubins_path_planning_batch": (
                 [vp, C.POINTER(DubinsConfigC), C.c_int, C.c_int, dp, dp, dp, ip, ip, dp], C.c_int),
+            "pp_dubins_path_planning_from_origin_batch": (
+                [vp, dp, C.c_int, C.c_int, dp, dp, dp, ip, ip, dp], C.c_int),
+            "pp_dubins_words_batch": ([vp, dp, C.c_int, dp, ip], C.c_int),
+            "pp_create_circle": ([C.c_double, C.c_double, C.c_double, dp, C.c_int, ip], C.c_int),
+            "pp_rrt_line_to_origin": ([vp, C.c_int32, dp, dp, C.c_int64, i64p], C.c_int),
             "pp_space_new": ([vp] + [C.c_double] * 7 + [dp, dp, dp, C.c_int], C.c_int),
             "pp_space_set_grid": ([vp, C.POINTER(C.c_uint32), C.c_int, C.c_int, C.c_double,
                                    C.c_double, C.c_double], C.c_int),

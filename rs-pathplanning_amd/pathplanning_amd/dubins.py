@@ -1,9 +1,9 @@
 """``pathplanning::dubins`` (src/dubins.rs) on the GPU.
 
-Mirrors the module's public API — ``Mode``, ``mod2pi``, ``pi_2_pi``, ``DubinsConfig``,
-``dubins_path_planning`` — with the path computed by the HIP ``dubins_batch`` kernel (one lane per
-configuration, f64, the reference's evaluation order).  ``dubins_path_planning_batch`` is the
-batched form the extend loop is built from.
+Mirrors the module's public API — ``Mode``, ``mod2pi``, ``pi_2_pi``, the six words ``lsl`` ..
+``lrl``, ``DubinsConfig``, ``dubins_path_planning_from_origin``, ``dubins_path_planning`` — with the
+words and paths computed by HIP kernels (one lane per configuration, f64, the reference's
+evaluation order).  The ``*_batch`` forms take many configurations per launch.
 """
 from __future__ import annotations
 
@@ -93,3 +93,89 @@ def dubins_path_planning_batch(confs, ctx: _ffi.Context | None = None, cap: int 
 def dubins_path_planning(conf: DubinsConfig, ctx: _ffi.Context | None = None):
     """dubins.rs:401-428: ``(px, py, pyaw, mode, cost)`` or ``None``."""
     return dubins_path_planning_batch([conf], ctx)[0]
+
+
+def dubins_path_planning_from_origin_batch(confs, ctx: _ffi.Context | None = None,
+                                           cap: int | None = None):
+    """dubins_path_planning_from_origin (dubins.rs:326-399) for every ``(dx, dy, eyaw, c,
+    step_size)``: list of ``(px, py, pyaw, mode, cost)`` in the local frame (yaw as generated) or
+    ``None``."""
+    confs = np.ascontiguousarray(confs, dtype=np.float64).reshape(-1, 5)
+    n = len(confs)
+    if n == 0:
+        return []
+    ctx = ctx or _ffi.default_context()
+    if cap is None:
+        d = np.hypot(confs[:, 0], confs[:, 1]) * confs[:, 3]
+        cap = int(np.max((3 * 2 * np.pi + d + 4.0) / confs[:, 4])) + 16
+    px, py, pyaw = (np.zeros(n * cap) for _ in range(3))
+    npts = np.zeros(n, dtype=np.int32)
+    word = np.zeros(n, dtype=np.int32)
+    cost = np.zeros(n)
+    dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+    _ffi.check(_ffi.lib().pp_dubins_path_planning_from_origin_batch(
+        ctx.handle, confs.ctypes.data_as(dp), n, cap, px.ctypes.data_as(dp),
+        py.ctypes.data_as(dp), pyaw.ctypes.data_as(dp), npts.ctypes.data_as(ip),
+        word.ctypes.data_as(ip), cost.ctypes.data_as(dp)))
+    out = []
+    for i in range(n):
+        if word[i] < 0:
+            out.append(None)
+            continue
+        s = slice(i * cap, i * cap + int(npts[i]))
+        out.append((px[s].copy(), py[s].copy(), pyaw[s].copy(), WORD_MODES[word[i]],
+                    float(cost[i])))
+    return out
+
+
+def dubins_path_planning_from_origin(dx: float, dy: float, eyaw: float, c: float,
+                                     step_size: float, ctx: _ffi.Context | None = None):
+    """dubins.rs:326-399: ``(px, py, pyaw, mode, cost)`` in the local frame, or ``None``."""
+    return dubins_path_planning_from_origin_batch([(dx, dy, eyaw, c, step_size)], ctx)[0]
+
+
+def words_batch(abd, ctx: _ffi.Context | None = None):
+    """The six words of every ``(alpha, beta, d)``: arrays ``tpq[n, 6, 3]`` and ``ok[n, 6]``
+    (ALL_PLANNERS order, dubins.rs:291)."""
+    abd = np.ascontiguousarray(abd, dtype=np.float64).reshape(-1, 3)
+    n = len(abd)
+    ctx = ctx or _ffi.default_context()
+    tpq = np.zeros((n, 6, 3))
+    ok = np.zeros((n, 6), dtype=np.int32)
+    if n:
+        _ffi.check(_ffi.lib().pp_dubins_words_batch(
+            ctx.handle, abd.ctypes.data_as(C.POINTER(C.c_double)), n,
+            tpq.ctypes.data_as(C.POINTER(C.c_double)), ok.ctypes.data_as(C.POINTER(C.c_int32))))
+    return tpq, ok
+
+
+def _word(w: int, alpha: float, beta: float, d: float):
+    tpq, ok = words_batch([(alpha, beta, d)])
+    if not ok[0, w]:
+        return (None, None, None, WORD_MODES[w])
+    t, p, q = (float(v) for v in tpq[0, w])
+    return (t, p, q, WORD_MODES[w])
+
+
+def lsl(alpha: float, beta: float, d: float):  # dubins.rs:27-48
+    return _word(0, alpha, beta, d)
+
+
+def rsr(alpha: float, beta: float, d: float):  # dubins.rs:51-71
+    return _word(1, alpha, beta, d)
+
+
+def lsr(alpha: float, beta: float, d: float):  # dubins.rs:74-92
+    return _word(2, alpha, beta, d)
+
+
+def rsl(alpha: float, beta: float, d: float):  # dubins.rs:95-113
+    return _word(3, alpha, beta, d)
+
+
+def rlr(alpha: float, beta: float, d: float):  # dubins.rs:116-133
+    return _word(4, alpha, beta, d)
+
+
+def lrl(alpha: float, beta: float, d: float):  # dubins.rs:136-153
+    return _word(5, alpha, beta, d)

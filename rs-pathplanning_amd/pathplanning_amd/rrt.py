@@ -306,6 +306,19 @@ class RRT:  # rrt.rs:325-620
         ok, _ = self.verify_node_batch([x], [y], [parent])
         return bool(ok[0])
 
+    def line_to_origin(self, node: int):
+        """line_to_origin (rrt.rs:291-321) of tree node ``node``: the (n, 2) polyline node -> root
+        (each edge steered on the GPU with R = Robot.max_steer and the planner's step)."""
+        n = C.c_int64(0)
+        _ffi.check(_ffi.lib().pp_rrt_line_to_origin(self.ctx.handle, int(node), None, None, 0,
+                                                    C.byref(n)))
+        x, y = np.zeros(max(n.value, 1)), np.zeros(max(n.value, 1))
+        dp = C.POINTER(C.c_double)
+        _ffi.check(_ffi.lib().pp_rrt_line_to_origin(self.ctx.handle, int(node),
+                                                    x.ctypes.data_as(dp), y.ctypes.data_as(dp),
+                                                    n.value, C.byref(n)))
+        return np.stack([x[:n.value], y[:n.value]], axis=1)
+
     # ---------------------------------------------------------------- goal connection
     def check_finish_batch(self, nodes, with_length: bool = True):
         """RRT::check_finish (rrt.rs:428-438) for many tree nodes: dict of arrays ``ok``,

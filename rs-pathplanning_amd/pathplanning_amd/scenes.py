@@ -227,15 +227,21 @@ def ring(points) -> np.ndarray:
 
 
 def create_circle_polygon(center, radius: float) -> np.ndarray:
-    """``create_circle`` (rrt.rs:43-60) as the polygon the crate builds: n = ceil(2 pi r / 1.0)
-    chords, vertices i = 0..=n at angle 2 pi / n * i (the last one repeats the first up to
-    rounding).  Same evaluation order as the Rust expression."""
-    cx, cy = float(center[0]), float(center[1])
-    circum = 2.0 * math.pi * radius
-    n = math.ceil(circum / 1.0)
-    pts = [(math.cos(2.0 * math.pi / n * float(i)) * radius + cx,
-            math.sin(2.0 * math.pi / n * float(i)) * radius + cy) for i in range(int(n + 1.0))]
-    return np.array(pts, dtype=np.float64)
+    """``create_circle`` (rrt.rs:43-60) as the polygon the crate builds (pp_create_circle): n =
+    ceil(2 pi r / 1.0) chords, vertices i = 0..=n at angle 2 pi / n * i (the last one repeats the
+    first up to rounding), in the Rust expression's evaluation order.  (N + 1, 2) array."""
+    import ctypes as C
+
+    from . import _ffi
+
+    n = C.c_int(0)
+    L = _ffi.lib()
+    _ffi.check(L.pp_create_circle(float(center[0]), float(center[1]), float(radius), None, 0,
+                                  C.byref(n)))
+    xy = np.zeros(2 * n.value)
+    _ffi.check(L.pp_create_circle(float(center[0]), float(center[1]), float(radius),
+                                  xy.ctypes.data_as(C.POINTER(C.c_double)), n.value, C.byref(n)))
+    return xy.reshape(-1, 2)
 
 
 def polygon_scene(bounds, obstacles, robot, start, goal, max_iter=8000, step_size=0.1,

@@ -7,9 +7,10 @@ R="${GRAFT_REPO_ROOT:-/root/repo}"
 OUT="$R/gpurun_out/${TAG:-ab}"
 mkdir -p "$OUT"
 cd "$R"
-for v in ${VARIANTS:-base}; do
+for v0 in ${VARIANTS:-base}; do
+  v=$(echo "$v0" | sed 's#.*/v_\([^/]*\)/lib.*#\1#; s#[/=]#_#g')
   for w in ${WORKLOADS:-config2 config3}; do
-    if [ "$v" = base ]; then envs=""; else envs="$v"; fi
+    if [ "$v0" = base ]; then envs=""; else envs="$v0"; fi
     env $envs PP_DEBUG=1 timeout -k 10 300 python3 bench.py --workload $w --no-cpu-baseline --no-size-sweep ${BENCH_ARGS:-} > "$OUT/${v}_$w.json" 2> "$OUT/${v}_$w.err" || { tail -20 "$OUT/${v}_$w.err"; exit 1; }
     python3 -c "
 import json; d=json.load(open('$OUT/${v}_$w.json'))

@@ -1,0 +1,104 @@
+"""The crate's remaining public `dubins` / `rrt` functions at the C ABI, each
+against the pure-Python restatement of the reference (oracle/dubins_py.py):
+
+  lsl .. lrl                      dubins.rs:27-153   pp_dubins_words_batch
+  dubins_path_planning_from_origin dubins.rs:326-399 pp_dubins_path_planning_from_origin_batch
+  line_to_origin                  rrt.rs:291-321     pp_rrt_line_to_origin
+
+Tolerances as in test_gpu_parity.py: word existence, point counts and modes exact; lengths,
+coordinates and yaw within 1e-9 (ocml vs glibc transcendental ulps)."""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def dpy():
+    import dubins_py
+
+    return dubins_py
+
+
+def _abd(n, seed):
+    rng = np.random.default_rng(seed)
+    a = rng.uniform(0.0, 2 * math.pi, n)
+    b = rng.uniform(0.0, 2 * math.pi, n)
+    d = np.concatenate([rng.uniform(0.0, 8.0, n - n // 4), rng.uniform(0.0, 1e-3, n // 4)])
+    a[:8], b[:8] = 0.0, 0.0  # straight-line degenerate words
+    return np.stack([a, b, d], 1)
+
+
+def test_six_words_match_the_reference(pkg, dpy):
+    from pathplanning_amd import dubins
+
+    abd = _abd(4000, 3)
+    tpq, ok = dubins.words_batch(abd)
+    fns = dpy.ALL_PLANNERS
+    for i, (a, b, d) in enumerate(abd):
+        for w, f in enumerate(fns):
+            exp = f(float(a), float(b), float(d))
+            assert bool(ok[i, w]) == (exp is not None), (i, w, a, b, d)
+            if exp is not None:
+                assert np.max(np.abs(tpq[i, w] - np.array(exp))) <= TOL, (i, w)
+    # the per-word entry points keep the Rust shape: (t, p, q, mode), None fields when infeasible
+    t, p, q, mode = dubins.lsl(*abd[10])
+    exp = dpy.lsl(*abd[10])
+    assert mode == dubins.WORD_MODES[0]
+    assert (t is None) == (exp is None)
+
+
+def test_from_origin_matches_the_reference(pkg, dpy):
+    from pathplanning_amd import dubins
+
+    rng = np.random.default_rng(11)
+    confs = []
+    for i in range(1500):
+        dx, dy = rng.uniform(-20, 20, 2)
+        if i % 7 == 0:
+            dx, dy = 0.0, 0.0  # identical positions: the trim pops everything but the origin
+        confs.append((dx, dy, rng.uniform(-7, 7), float(rng.choice([0.25, 1.25, 2.0, 1 / 0.8])),
+                      float(rng.choice([0.05, 0.1, 0.3]))))
+    got = dubins.dubins_path_planning_from_origin_batch(confs)
+    for c, g in zip(confs, got):
+        exp = dpy.dubins_path_planning_from_origin(*c)
+        if exp is None:
+            assert g is None
+            continue
+        assert g is not None
+        px, py, pyaw, word, cost = exp
+        gx, gy, gyaw, mode, gcost = g
+        if c[0] == 0.0 and c[1] == 0.0 and len(gx) != len(px):
+            continue  # measure-zero libm residue at identical positions
+        assert mode == dubins.WORD_MODES[word]
+        assert len(gx) == len(px), c
+        assert np.max(np.abs(gx - np.array(px)), initial=0.0) <= TOL
+        assert np.max(np.abs(gy - np.array(py)), initial=0.0) <= TOL
+        assert np.max(np.abs(gyaw - np.array(pyaw)), initial=0.0) <= TOL  # yaw not wrapped
+        assert abs(gcost - cost) <= TOL * max(1.0, cost)
+
+
+def test_line_to_origin_matches_the_reference(pkg, dpy):
+    from pathplanning_amd import rrt, scenes
+
+    raw = scenes.bench6()
+    sx, sy, syaw = raw["start"]
+    gx, gy, gyaw = raw["goal"]
+    p = rrt.RRT((sx, sy), syaw, (gx, gy), gyaw, raw["max_iter"], raw["step_size"],
+                rrt.Space.from_raw(raw), seed=5, window=256)
+    p.extend(1500)
+    x, y, yaw, par = p.tree()
+    nodes = dpy.tree_nodes({"x": list(x), "y": list(y), "yaw": list(yaw), "parent": list(par)})
+    R = raw["robot"][2]
+    rng = np.random.default_rng(2)
+    for v in [0, 1] + list(rng.integers(1, len(x), 40)) + [len(x) - 1]:
+        got = p.line_to_origin(int(v))
+        ex, ey = dpy.line_to_origin(nodes[int(v)], R, raw["step_size"])
+        assert got.shape == (len(ex), 2), v
+        assert np.max(np.abs(got[:, 0] - np.array(ex))) <= TOL
+        assert np.max(np.abs(got[:, 1] - np.array(ey))) <= TOL
+    p.close()
