@@ -20,11 +20,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/pathplanning_amd.h"
 #include "pp_device.h"
 #include "pp_kernels.h"
+#include "pp_scene.h"
 
 using namespace ppamd;
 
@@ -954,102 +956,40 @@ int pp_create_circle(double cx, double cy, double radius, double* xy, int cap, i
 }
 
 namespace {
-// Uniform grid over the scene's collision items (discs, or polygon edges in Q10p) for the steer
-// kernels' exact cull: item k is listed in every cell its cull box [bx0, bx1] x [by0, by1]
-// touches (CSR: goff, gitems), cells clamped to the sampling box; f32 cull discs d4 (centre,
-// radius rounded up).  Uploads everything and the LDS image [goff | items | d4] when it fits.
-int build_item_grid(pp_ctx* ctx, double minx, double maxx, double miny, double maxy,
-                    const std::vector<double>& bx0, const std::vector<double>& bx1,
-                    const std::vector<double>& by0, const std::vector<double>& by1,
-                    const std::vector<float4>& d4) {
-    const int m = (int)d4.size();
-    const double spanx = maxx - minx, spany = maxy - miny;
-    const double span = std::max(spanx, spany);
-    auto al = [](size_t b) { return (int)((b + 15) & ~(size_t)15); };
-    constexpr int kLdsImage = 64 * 1024;  // 2 workgroups per CU fit in 160 KB
-    int part_budget = kLdsImage;  // the grid-only image (PP_LDS_GRID_KB: experiments)
-    if (const char* e = std::getenv("PP_LDS_GRID_KB")) part_budget = std::atoi(e) * 1024;
-    // square cells, about one cell per item; a scene whose LDS image [goff | items | d4] does not
-    // fit gets the image without the cull discs (read from global memory), at a coarser grid if
-    // that is what it takes
-    std::vector<int> goff, gitems;
-    int gnx = 1, gny = 1, lds_total = 0, o_goff = 0, o_items = 0, o_d4 = -1;
-    double ginv = 1.0;
-    const int per0 = std::max(1, std::min(256, (int)std::ceil(std::sqrt((double)std::max(m, 1)))));
-    for (int per_axis = per0;; per_axis = per_axis * 3 / 4) {
-        const double cell = span / per_axis;
-        gnx = std::max(1, std::min(256, (int)std::ceil(spanx / cell)));
-        gny = std::max(1, std::min(256, (int)std::ceil(spany / cell)));
-        ginv = 1.0 / cell;
-        auto cell_of = [&](double v, double v0, int n) {
-            const double f = std::floor((v - v0) * ginv);
-            return f < 0.0 ? 0 : (f >= (double)(n - 1) ? n - 1 : (int)f);
-        };
-        goff.assign((size_t)gnx * gny + 1, 0);
-        gitems.clear();
-        std::vector<std::vector<int>> lists((size_t)gnx * gny);
-        for (int k = 0; k < m; ++k) {
-            const int x0c = cell_of(bx0[k], minx, gnx), x1c = cell_of(bx1[k], minx, gnx);
-            const int y0c = cell_of(by0[k], miny, gny), y1c = cell_of(by1[k], miny, gny);
-            for (int gy = y0c; gy <= y1c; ++gy)
-                for (int gx = x0c; gx <= x1c; ++gx) lists[(size_t)gy * gnx + gx].push_back(k);
-        }
-        for (size_t q = 0; q < lists.size(); ++q) {
-            goff[q + 1] = goff[q] + (int)lists[q].size();
-            gitems.insert(gitems.end(), lists[q].begin(), lists[q].end());
-        }
-        o_items = o_goff + al(goff.size() * sizeof(int));
-        const int grid_bytes = o_items + al(gitems.size() * sizeof(int));
-        const int full = grid_bytes + al((size_t)m * sizeof(float4));
-        if (full <= kLdsImage) {  // everything in LDS
-            lds_total = full;
-            o_d4 = grid_bytes;
-            break;
-        }
-        if (grid_bytes <= part_budget && m > 4096) {  // the grid in LDS, the cull discs in L2
-            lds_total = grid_bytes;
-            o_d4 = -1;
-            break;
-        }
-        if (per_axis <= 8 || m <= 4096) {  // no LDS image: the walk reads the scene from L2
-            lds_total = 0;
-            break;
-        }
-    }
-    PP_HIP(ctx->d_goff.reserve(goff.size()));
-    PP_HIP(ctx->d_gitems.reserve(std::max<size_t>(gitems.size(), 1)));
-    PP_HIP(hipMemcpy(ctx->d_goff.p, goff.data(), goff.size() * sizeof(int), hipMemcpyHostToDevice));
-    if (!gitems.empty())
-        PP_HIP(hipMemcpy(ctx->d_gitems.p, gitems.data(), gitems.size() * sizeof(int), hipMemcpyHostToDevice));
-    ctx->lds_bytes = lds_total;
-    if (lds_total > 0) {  // the image, contiguous in global memory (stage_scene copies it whole)
-        std::vector<char> img((size_t)lds_total, 0);
-        std::memcpy(img.data() + o_goff, goff.data(), goff.size() * sizeof(int));
-        if (!gitems.empty())
-            std::memcpy(img.data() + o_items, gitems.data(), gitems.size() * sizeof(int));
-        if (o_d4 >= 0)
-            for (int k = 0; k < m; ++k) std::memcpy(img.data() + o_d4 + 16 * k, &d4[k], 16);
-        PP_HIP(ctx->d_img.reserve((size_t)lds_total / 16));
-        PP_HIP(hipMemcpy(ctx->d_img.p, img.data(), (size_t)lds_total, hipMemcpyHostToDevice));
-    }
-    ctx->lds_goff = o_goff;
-    ctx->lds_items = o_items;
-    ctx->lds_cx = ctx->lds_cy = ctx->lds_r2 = -1;
-    ctx->lds_d4 = o_d4;
-    ctx->gx0 = minx;
-    ctx->gy0 = miny;
-    ctx->ginv = ginv;
-    ctx->gnx = gnx;
-    ctx->gny = gny;
-    PP_HIP(ctx->d_d4.reserve((size_t)std::max(m, 1)));
-    if (m > 0) PP_HIP(hipMemcpy(ctx->d_d4.p, d4.data(), m * sizeof(float4), hipMemcpyHostToDevice));
-    return PP_OK;
-}
+static_assert(sizeof(scene::CullDisc) == sizeof(float4), "cull disc layout");
 
-// f32 cull slack: the rounding of coordinates of magnitude <= mx to f32 (both ends of a
-// difference, both axes) with a wide margin; never below the 1e-3 that covers |c| <= 2^10
-float cull_slack_for(double mx) {
-    return (float)std::max(1.0e-3, 16.0 * mx * std::ldexp(1.0, -24));
+// upload the item grid (pp_scene.cpp) and its LDS image; set the context's grid fields
+int upload_item_grid(pp_ctx* ctx, double minx, double maxx, double miny, double maxy,
+                     const scene::Items& items) {
+    int part_budget = scene::kLdsImage;  // the grid-only image (PP_LDS_GRID_KB: experiments)
+    if (const char* e = std::getenv("PP_LDS_GRID_KB")) part_budget = std::atoi(e) * 1024;
+    const scene::ItemGrid g =
+        scene::build_item_grid(minx, maxx, miny, maxy, items, part_budget);
+    const int m = (int)items.d4.size();
+    PP_HIP(ctx->d_goff.reserve(g.goff.size()));
+    PP_HIP(ctx->d_gitems.reserve(std::max<size_t>(g.gitems.size(), 1)));
+    PP_HIP(hipMemcpy(ctx->d_goff.p, g.goff.data(), g.goff.size() * sizeof(int), hipMemcpyHostToDevice));
+    if (!g.gitems.empty())
+        PP_HIP(hipMemcpy(ctx->d_gitems.p, g.gitems.data(), g.gitems.size() * sizeof(int),
+                         hipMemcpyHostToDevice));
+    ctx->lds_bytes = g.lds_total;
+    if (g.lds_total > 0) {
+        PP_HIP(ctx->d_img.reserve((size_t)g.lds_total / 16));
+        PP_HIP(hipMemcpy(ctx->d_img.p, g.image.data(), (size_t)g.lds_total, hipMemcpyHostToDevice));
+    }
+    ctx->lds_goff = g.o_goff;
+    ctx->lds_items = g.o_items;
+    ctx->lds_cx = ctx->lds_cy = ctx->lds_r2 = -1;
+    ctx->lds_d4 = g.o_d4;
+    ctx->gx0 = g.x0;
+    ctx->gy0 = g.y0;
+    ctx->ginv = g.ginv;
+    ctx->gnx = g.gnx;
+    ctx->gny = g.gny;
+    PP_HIP(ctx->d_d4.reserve((size_t)std::max(m, 1)));
+    if (m > 0)
+        PP_HIP(hipMemcpy(ctx->d_d4.p, items.d4.data(), m * sizeof(float4), hipMemcpyHostToDevice));
+    return PP_OK;
 }
 
 // reset the polygon-mode part of the scene (pp_space_new / pp_space_new_polygons)
@@ -1071,32 +1011,14 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
                  const double* r, int m) {
     int rc = check_ctx(ctx, false, false);
     if (rc) return rc;
-    if (m < 0 || (m > 0 && (!cx || !cy || !r)))
-        return set_err(PP_ERR_INVALID_ARGUMENT, "bad obstacle arrays");
     if (!(robot_width >= 0.0) || !(max_steer > 0.0))
         return set_err(PP_ERR_INVALID_ARGUMENT, "robot width must be >= 0 and max_steer > 0");
-    // Space::new, rrt.rs:82-111: bounds offset by -width/2, obstacles by +width/2
+    scene::DiscScene ds;
+    std::string err;
+    if ((rc = scene::disc_scene(x0, y0, x1, y1, robot_width, cx, cy, r, m, &ds, &err)))
+        return set_err(rc, err);
     const double half = robot_width / 2.0;
-    const double minx = x0 + half, maxx = x1 - half, miny = y0 + half, maxy = y1 - half;
-    if (!(minx < maxx) || !(miny < maxy))  // gen_range asserts low < high (rrt.rs:142-143)
-        return set_err(PP_ERR_INVALID_ARGUMENT, "shrunken bounds are empty");
-    std::vector<double> r2(m), rc_(m), bx0(m), bx1(m), by0(m), by1(m);
-    std::vector<float4> d4(m);
-    double mx = std::max({std::fabs(minx), std::fabs(maxx), std::fabs(miny), std::fabs(maxy)});
-    for (int k = 0; k < m; ++k) {
-        const double reff = r[k] + half;
-        r2[k] = reff * reff;
-        rc_[k] = reff * (1.0 + 1e-9) + 1e-9;
-        // f32 cull copy: the radius rounded up (the cull only ever over-includes)
-        d4[k] = make_float4((float)cx[k], (float)cy[k], std::nextafter((float)rc_[k], 1e30f),
-                            (float)reff);  // w: the radius for the walk's f32 decision band
-        bx0[k] = cx[k] - rc_[k];
-        bx1[k] = cx[k] + rc_[k];
-        by0[k] = cy[k] - rc_[k];
-        by1[k] = cy[k] + rc_[k];
-        mx = std::max({mx, std::fabs(cx[k]) + rc_[k], std::fabs(cy[k]) + rc_[k]});
-    }
-    if ((rc = build_item_grid(ctx, minx, maxx, miny, maxy, bx0, bx1, by0, by1, d4))) return rc;
+    if ((rc = upload_item_grid(ctx, ds.minx, ds.maxx, ds.miny, ds.maxy, ds.items))) return rc;
     const size_t mm = (size_t)std::max(m, 1);
     PP_HIP(ctx->d_cx.reserve(mm));
     PP_HIP(ctx->d_cy.reserve(mm));
@@ -1105,16 +1027,16 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
     if (m > 0) {
         PP_HIP(hipMemcpy(ctx->d_cx.p, cx, m * sizeof(double), hipMemcpyHostToDevice));
         PP_HIP(hipMemcpy(ctx->d_cy.p, cy, m * sizeof(double), hipMemcpyHostToDevice));
-        PP_HIP(hipMemcpy(ctx->d_r2.p, r2.data(), m * sizeof(double), hipMemcpyHostToDevice));
-        PP_HIP(hipMemcpy(ctx->d_rcull.p, rc_.data(), m * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_r2.p, ds.r2.data(), m * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_rcull.p, ds.rcull.data(), m * sizeof(double), hipMemcpyHostToDevice));
     }
     clear_polygons(ctx);
     ctx->h2 = half * half;
-    ctx->cull_slack = cull_slack_for(mx);
-    ctx->minx = minx;
-    ctx->maxx = maxx;
-    ctx->miny = miny;
-    ctx->maxy = maxy;
+    ctx->cull_slack = scene::cull_slack_for(ds.items.mx);
+    ctx->minx = ds.minx;
+    ctx->maxx = ds.maxx;
+    ctx->miny = ds.miny;
+    ctx->maxy = ds.maxy;
     ctx->width = robot_width;
     ctx->height = robot_height;
     ctx->max_steer = max_steer;
@@ -1135,100 +1057,45 @@ int pp_space_new_polygons(pp_ctx* ctx, const double* bounds_xy, int nb, const do
         return set_err(PP_ERR_INVALID_ARGUMENT, "bad polygon arrays (bounds need >= 3 vertices)");
     if (!(robot_width >= 0.0) || !(max_steer > 0.0))
         return set_err(PP_ERR_INVALID_ARGUMENT, "robot width must be >= 0 and max_steer > 0");
-    // rings: a closing repeat of the first vertex is dropped (geo closes rings itself)
-    auto ring = [](const double* xy, int n, std::vector<double>& vx, std::vector<double>& vy) {
-        if (n > 1 && xy[0] == xy[2 * (n - 1)] && xy[1] == xy[2 * (n - 1) + 1]) --n;
-        vx.resize(n);
-        vy.resize(n);
-        for (int i = 0; i < n; ++i) {
-            vx[i] = xy[2 * i];
-            vy[i] = xy[2 * i + 1];
-        }
-    };
-    std::vector<double> bvx, bvy;
-    ring(bounds_xy, nb, bvx, bvy);
-    if (bvx.size() < 3) return set_err(PP_ERR_INVALID_ARGUMENT, "bounds ring has < 3 vertices");
-    for (size_t i = 0; i < bvx.size(); ++i)
-        if (!std::isfinite(bvx[i]) || !std::isfinite(bvy[i]))
-            return set_err(PP_ERR_INVALID_ARGUMENT, "non-finite bounds vertex");
-    // Space::new, rrt.rs:82-106: rand_point samples the bbox of the shrunken bounds — here the
-    // bounds' bbox shrunk by width/2, which contains the eroded polygon (Q10p)
+    scene::PolygonScene ps;
+    std::string err;
+    if ((rc = scene::polygon_scene(bounds_xy, nb, obs_xy, obs_off, n_obs, robot_width, &ps, &err)))
+        return set_err(rc, err);
     const double half = robot_width / 2.0;
-    const double minx = *std::min_element(bvx.begin(), bvx.end()) + half;
-    const double maxx = *std::max_element(bvx.begin(), bvx.end()) - half;
-    const double miny = *std::min_element(bvy.begin(), bvy.end()) + half;
-    const double maxy = *std::max_element(bvy.begin(), bvy.end()) - half;
-    if (!(minx < maxx) || !(miny < maxy))  // gen_range asserts low < high (rrt.rs:142-143)
-        return set_err(PP_ERR_INVALID_ARGUMENT, "shrunken bounds are empty");
-    double mx = 0.0;
-    for (size_t i = 0; i < bvx.size(); ++i) mx = std::max({mx, std::fabs(bvx[i]), std::fabs(bvy[i])});
-    // obstacle edges (rrt.rs:108-111: every obstacle buffered by width/2)
-    std::vector<double> ex0, ey0, ex1, ey1, bx0, bx1, by0, by1;
-    std::vector<int> epoly;
-    std::vector<float4> d4;
-    const double rcull = half * (1.0 + 1e-9) + 1e-9;
-    for (int o = 0; o < n_obs; ++o) {
-        const int a = obs_off[o], b = obs_off[o + 1];
-        if (a < 0 || b < a) return set_err(PP_ERR_INVALID_ARGUMENT, "bad obstacle offsets");
-        std::vector<double> vx, vy;
-        ring(obs_xy + 2 * (size_t)a, b - a, vx, vy);
-        const int n = (int)vx.size();
-        if (n == 0) continue;
-        for (int i = 0; i < n; ++i) {
-            if (!std::isfinite(vx[i]) || !std::isfinite(vy[i]))
-                return set_err(PP_ERR_INVALID_ARGUMENT, "non-finite obstacle vertex");
-            const int j = i + 1 == n ? 0 : i + 1;
-            ex0.push_back(vx[i]);
-            ey0.push_back(vy[i]);
-            ex1.push_back(vx[j]);
-            ey1.push_back(vy[j]);
-            epoly.push_back(o);
-            bx0.push_back(std::min(vx[i], vx[j]) - rcull);
-            bx1.push_back(std::max(vx[i], vx[j]) + rcull);
-            by0.push_back(std::min(vy[i], vy[j]) - rcull);
-            by1.push_back(std::max(vy[i], vy[j]) + rcull);
-            // f32 cull disc: the midpoint, half the length + h, rounded up generously
-            const double hl = 0.5 * std::hypot(vx[j] - vx[i], vy[j] - vy[i]);
-            const double rr = (hl + rcull) * (1.0 + 1e-7) + 1e-9;
-            d4.push_back(make_float4((float)(0.5 * (vx[i] + vx[j])), (float)(0.5 * (vy[i] + vy[j])),
-                                     std::nextafter((float)rr, 1e30f), 0.0f));
-            mx = std::max({mx, std::fabs(vx[i]), std::fabs(vy[i])});
-        }
-    }
-    const int ne = (int)ex0.size();
-    if ((rc = build_item_grid(ctx, minx, maxx, miny, maxy, bx0, bx1, by0, by1, d4))) return rc;
+    if ((rc = upload_item_grid(ctx, ps.minx, ps.maxx, ps.miny, ps.maxy, ps.items))) return rc;
+    const int ne = (int)ps.ex0.size();
     const size_t nn = (size_t)std::max(ne, 1);
     PP_HIP(ctx->d_ex0.reserve(nn));
     PP_HIP(ctx->d_ey0.reserve(nn));
     PP_HIP(ctx->d_ex1.reserve(nn));
     PP_HIP(ctx->d_ey1.reserve(nn));
     PP_HIP(ctx->d_epoly.reserve(nn));
-    PP_HIP(ctx->d_bvx.reserve(bvx.size()));
-    PP_HIP(ctx->d_bvy.reserve(bvy.size()));
+    PP_HIP(ctx->d_bvx.reserve(ps.bvx.size()));
+    PP_HIP(ctx->d_bvy.reserve(ps.bvy.size()));
     if (ne > 0) {
-        PP_HIP(hipMemcpy(ctx->d_ex0.p, ex0.data(), ne * sizeof(double), hipMemcpyHostToDevice));
-        PP_HIP(hipMemcpy(ctx->d_ey0.p, ey0.data(), ne * sizeof(double), hipMemcpyHostToDevice));
-        PP_HIP(hipMemcpy(ctx->d_ex1.p, ex1.data(), ne * sizeof(double), hipMemcpyHostToDevice));
-        PP_HIP(hipMemcpy(ctx->d_ey1.p, ey1.data(), ne * sizeof(double), hipMemcpyHostToDevice));
-        PP_HIP(hipMemcpy(ctx->d_epoly.p, epoly.data(), ne * sizeof(int), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_ex0.p, ps.ex0.data(), ne * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_ey0.p, ps.ey0.data(), ne * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_ex1.p, ps.ex1.data(), ne * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_ey1.p, ps.ey1.data(), ne * sizeof(double), hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->d_epoly.p, ps.epoly.data(), ne * sizeof(int), hipMemcpyHostToDevice));
     }
-    PP_HIP(hipMemcpy(ctx->d_bvx.p, bvx.data(), bvx.size() * sizeof(double), hipMemcpyHostToDevice));
-    PP_HIP(hipMemcpy(ctx->d_bvy.p, bvy.data(), bvy.size() * sizeof(double), hipMemcpyHostToDevice));
-    ctx->h_ex0 = ex0;
-    ctx->h_ey0 = ey0;
-    ctx->h_ex1 = ex1;
-    ctx->h_ey1 = ey1;
-    ctx->h_epoly = epoly;
-    ctx->h_bvx = bvx;
-    ctx->h_bvy = bvy;
+    PP_HIP(hipMemcpy(ctx->d_bvx.p, ps.bvx.data(), ps.bvx.size() * sizeof(double), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->d_bvy.p, ps.bvy.data(), ps.bvy.size() * sizeof(double), hipMemcpyHostToDevice));
+    ctx->h_ex0 = std::move(ps.ex0);
+    ctx->h_ey0 = std::move(ps.ey0);
+    ctx->h_ex1 = std::move(ps.ex1);
+    ctx->h_ey1 = std::move(ps.ey1);
+    ctx->h_epoly = std::move(ps.epoly);
+    ctx->h_bvx = std::move(ps.bvx);
+    ctx->h_bvy = std::move(ps.bvy);
     ctx->ne = ne;
-    ctx->nbv = (int)bvx.size();
+    ctx->nbv = (int)ctx->h_bvx.size();
     ctx->h2 = half * half;
-    ctx->cull_slack = cull_slack_for(mx + half);
-    ctx->minx = minx;
-    ctx->maxx = maxx;
-    ctx->miny = miny;
-    ctx->maxy = maxy;
+    ctx->cull_slack = scene::cull_slack_for(ps.items.mx);
+    ctx->minx = ps.minx;
+    ctx->maxx = ps.maxx;
+    ctx->miny = ps.miny;
+    ctx->maxy = ps.maxy;
     ctx->width = robot_width;
     ctx->height = robot_height;
     ctx->max_steer = max_steer;

@@ -2039,10 +2039,9 @@ __host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
 // 279 -> 309 M it/s; 8 spills too much).
 constexpr int kWalkMinWWindow = 1;
 constexpr int kWalkMinWBatch = 6;
-#ifndef PP_STAR_WALK_MINW
-#define PP_STAR_WALK_MINW kWalkMinWBatch
-#endif
-constexpr int kWalkMinWStar = PP_STAR_WALK_MINW;
+// RRT* scenes (config 5) carry a ~58 KB LDS image, so LDS holds the walk at 2 workgroups per CU
+// whatever the register budget: the uncapped budget wins there (16.46 vs 15.96 M it/s, r02 A/B).
+constexpr int kWalkMinWStar = kWalkMinWWindow;
 template <bool kLds, int kMinW>
 __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevState* __restrict__ st,
                                                          SceneDev sc,

@@ -311,13 +311,13 @@ def bench6_polygons_open(start_yaw: float = math.pi / 4.0) -> dict:
 
 
 def transit(path: str | None = None) -> dict:
-    """The example's own scene, examples/rrt/transit.debug.json (a copy of the data file lives
-    in tests/golden/ so the GPU box, which has no /root/reference, can load it)."""
+    """The example's own scene, examples/rrt/transit.debug.json (the data file ships with the
+    package under data/, so the GPU box, which has no /root/reference, can load it)."""
     import os
 
     if path is None:
-        path = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
-            os.path.abspath(__file__)))), "tests", "golden", "transit.debug.json")
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data",
+                            "transit.debug.json")
     return load_json(path, name="transit")
 
 

@@ -6,7 +6,7 @@ expected outputs come from this independent restatement; the inputs are the refe
 known configurations (examples/dubins/src/main.rs:131-164, benches/all.rs:8-42,102-111) plus a
 seeded random battery and the build's config-2 field.  The C oracle and the HIP path are checked
 against these files.  Re-run with:  python tests/golden/gen_golden.py  (--polygons: only the
-polygon-mode fixtures; transit.debug.json is a verbatim copy of the reference's example scene
+polygon-mode fixtures; transit.debug.json (pathplanning_amd/data/) is a verbatim copy of the reference's example scene
 data, examples/rrt/transit.debug.json; --star: only the RRT* fixtures, oracle/rrtstar_py.py)
 """
 from __future__ import annotations

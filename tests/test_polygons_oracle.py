@@ -13,6 +13,9 @@ import pytest
 
 from conftest import GOLDEN, load_golden
 
+PKG_DATA = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "rs-pathplanning_amd", "pathplanning_amd", "data")
+
 
 def test_load_json_matches_the_example_format():
     from pathplanning_amd import scenes
@@ -154,5 +157,5 @@ def test_transit_fixture_is_the_reference_data():
     src = "/root/reference/examples/rrt/transit.debug.json"
     if not os.path.exists(src):
         pytest.skip("reference not mounted")
-    with open(src, "rb") as a, open(os.path.join(GOLDEN, "transit.debug.json"), "rb") as b:
+    with open(src, "rb") as a, open(os.path.join(PKG_DATA, "transit.debug.json"), "rb") as b:
         assert a.read() == b.read()
