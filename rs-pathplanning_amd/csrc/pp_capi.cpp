@@ -2003,6 +2003,12 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out) {
         s.nn_flagged = d.nn_flagged;
         s.node_evals = d.node_evals;
         for (int k = 0; k < 8; ++k) s.stamps[k] = d.stamps[k];
+    } else if (ctx->has_batch) {  // diagnostic stamps of a query batch: summed over its states
+        DevState ds[1 + kMaxSub];
+        PP_HIP(hipMemcpyAsync(ds, ctx->mq_state.p, sizeof ds, hipMemcpyDeviceToHost, ctx->stream));
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+        for (const DevState& d : ds)
+            for (int k = 0; k < 8; ++k) s.stamps[k] += d.stamps[k];
     }
     s.nn_scan_ms = ctx->nn_scan_ms;
     s.nn_scan_launches = ctx->nn_scan_launches;

@@ -1236,7 +1236,12 @@ __device__ inline Top2 shfl_xor_top2(Top2 t, int m) {
     return Top2{__shfl_xor(t.b, m), __shfl_xor(t.s, m), __shfl_xor(t.i, m)};
 }
 
-__global__ __launch_bounds__(kFinThreads) void nn_finalize_kernel(
+// 8 waves per SIMD (<= 64 VGPRs): two 1024-thread workgroups per CU, so the extra sampling
+// workgroup (the grid's last) runs beside the others instead of waiting for a CU to drain.
+#ifndef PP_FIN_MINW
+#define PP_FIN_MINW 8
+#endif
+__global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
     DevState* __restrict__ st, int p, int64_t seq, int chunks, const float* __restrict__ pbest,
     const float* __restrict__ psecond, const int* __restrict__ pidx, int stride,
     const double* __restrict__ qx, const double* __restrict__ qy, const float* __restrict__ x32,
@@ -2038,10 +2043,45 @@ __host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
 // tasks per wave, latency-bound, and run better at 6 (80 VGPRs, 3 workgroups per CU: config 3
 // 279 -> 309 M it/s; 8 spills too much).
 constexpr int kWalkMinWWindow = 1;
-constexpr int kWalkMinWBatch = 6;
+#ifndef PP_WALK_MINW_BATCH
+#define PP_WALK_MINW_BATCH 6
+#endif
+constexpr int kWalkMinWBatch = PP_WALK_MINW_BATCH;
 // RRT* scenes (config 5) carry a ~58 KB LDS image, so LDS holds the walk at 2 workgroups per CU
 // whatever the register budget: the uncapped budget wins there (16.46 vs 15.96 M it/s, r02 A/B).
 constexpr int kWalkMinWStar = kWalkMinWWindow;
+#ifdef PP_STAMPS_WALK
+// diagnostic build only (-DPP_STAMPS_WALK): per steer_walk launch, the launch span, the mean and
+// the longest wave lifetime (stamps[0..2], [3] launches) — the walk's load imbalance
+__device__ unsigned long long g_wspan[6] = {~0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+struct WalkSpan {
+    DevState* st;
+    unsigned long long t_in = 0;
+    explicit __device__ WalkSpan(DevState* s) : st(s) {
+        t_in = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63) == 0) atomicMin(&g_wspan[0], t_in);
+    }
+    __device__ ~WalkSpan() {
+        if ((threadIdx.x & 63) == 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            atomicMax(&g_wspan[1], t);
+            atomicMax(&g_wspan[2], t - t_in);
+            atomicAdd(&g_wspan[3], t - t_in);
+            __threadfence();
+            const unsigned long long waves = (unsigned long long)gridDim.x * (blockDim.x >> 6);
+            if (atomicAdd(&g_wspan[4], 1ull) == waves - 1) {
+                __threadfence();
+                unsigned long long* sp = reinterpret_cast<unsigned long long*>(st->stamps);
+                sp[0] += atomicAdd(&g_wspan[1], 0ull) - atomicAdd(&g_wspan[0], 0ull);
+                sp[1] += atomicAdd(&g_wspan[3], 0ull) / waves;
+                sp[2] += atomicAdd(&g_wspan[2], 0ull);
+                sp[3] += 1;
+                for (int i = 0; i < 5; ++i) atomicExch(&g_wspan[i], i == 0 ? ~0ull : 0ull);
+            }
+        }
+    }
+};
+#endif
 template <bool kLds, int kMinW>
 __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevState* __restrict__ st,
                                                          SceneDev sc,
@@ -2055,14 +2095,38 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
     const int lane = threadIdx.x & 63;
     const int W = st->W;
     const int total = W + st->ncomp;
+#ifdef PP_STAMPS_WALK
+    WalkSpan walk_span(st);
+#endif
+#ifdef PP_WALK_STATIC
     if ((int)blockIdx.x * (kWalkThreads / 64) >= total) return;  // whole workgroup idle
+#else
+    if ((int)blockIdx.x * ((total + (int)gridDim.x - 1) / (int)gridDim.x) >= total) return;
+#endif
     if (kLds) stage_scene(sc);
-    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) +
                  (threadIdx.x >> 6) * kGenSlots;  // this wave's generator slots
     int npts = 0;
+#ifdef PP_WALK_STATIC
+    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     for (int t = gw; t < total; t += nw) {
+#else
+    // Workgroup b walks the contiguous task range [b * per, (b + 1) * per); its waves take the
+    // range's tasks one at a time from an LDS counter, so a wave that drew short paths takes more
+    // of them (a workgroup's share is a sum of dozens of tasks: far more even than a wave's
+    // handful under a static stride).  No global atomics.
+    __shared__ int s_next;
+    const int per = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int t_end = min(total, ((int)blockIdx.x + 1) * per);
+    if (threadIdx.x == 0) s_next = (int)blockIdx.x * per;
+    __syncthreads();
+    for (;;) {
+        int t = 0;
+        if (lane == 0) t = atomicAdd(&s_next, 1);
+        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+        if (t >= t_end) break;
+#endif
         const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts);
         if (lane == 0) {
             if (t < W) {
@@ -2573,8 +2637,61 @@ static_assert(kScreenStageOff % 16 == 0 && kScreenStageOff + 3 * kStage * 4 + 16
               "screen staging (x, y, |n-o|^2 of kStage nodes + the piece counter) fits");
 static_assert(kStage % 256 == 0 && kGrab % kScanBlk == 0, "whole DMA quarters and blocks");
 
+#ifdef PP_STAMPS_SPAN
+// diagnostic build only (-DPP_STAMPS_SPAN): per window_kernel launch, the span from the first
+// workgroup's start to the last one's end, the start skew and workgroup 0's end (stamps[0..3])
+__device__ unsigned long long g_span[4] = {~0ull, 0ull, 0ull, 0ull};  // min start, max start, max end, done
+__device__ unsigned long long g_span_wg0, g_span_maxdur, g_span_sumdur;
+struct SpanStamp {
+    DevState* st;
+    unsigned long long t_in = 0;
+    explicit __device__ SpanStamp(DevState* s) : st(s) {
+        if (threadIdx.x == 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            t_in = t;
+            atomicMin(&g_span[0], t);
+            atomicMax(&g_span[1], t);
+        }
+    }
+    __device__ ~SpanStamp() {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            if (blockIdx.x == 0) atomicExch(&g_span_wg0, t);
+            else {
+                atomicMax(&g_span_maxdur, t - t_in);
+                atomicAdd(&g_span_sumdur, t - t_in);
+            }
+            atomicMax(&g_span[2], t);
+            __threadfence();
+            if (atomicAdd(&g_span[3], 1ull) == gridDim.x - 1) {
+                __threadfence();
+                const unsigned long long t0 = atomicAdd(&g_span[0], 0ull);
+                const unsigned long long t1 = atomicAdd(&g_span[1], 0ull);
+                const unsigned long long t2 = atomicAdd(&g_span[2], 0ull);
+                const unsigned long long tw = atomicAdd(&g_span_wg0, 0ull);
+                unsigned long long* sp = reinterpret_cast<unsigned long long*>(st->stamps);
+                sp[0] += t2 - t0;
+                sp[1] += t1 - t0;
+                sp[2] += tw - t0;
+                sp[3] += 1;
+                sp[4] += atomicExch(&g_span_maxdur, 0ull);
+                sp[5] += atomicExch(&g_span_sumdur, 0ull) / (gridDim.x > 1 ? gridDim.x - 1 : 1);
+                atomicExch(&g_span[0], ~0ull);
+                atomicExch(&g_span[1], 0ull);
+                atomicExch(&g_span[2], 0ull);
+                atomicExch(&g_span[3], 0ull);
+            }
+        }
+    }
+};
+#endif
+
 __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
     __shared__ __attribute__((aligned(16))) char smem[kWinLds];
+#ifdef PP_STAMPS_SPAN
+    SpanStamp span_stamp(a.st);
+#endif
     if (blockIdx.x == 0) {
         DevState* st = a.st;
         SCREEN_STAMP(tw0);
