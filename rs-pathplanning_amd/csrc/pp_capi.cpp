@@ -2003,6 +2003,9 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out) {
         s.nn_flagged = d.nn_flagged;
         s.node_evals = d.node_evals;
         for (int k = 0; k < 8; ++k) s.stamps[k] = d.stamps[k];
+#ifdef PP_STAMPS_SPAN
+        diag_dump_window_span((int)d.stamps[3]);
+#endif
     } else if (ctx->has_batch) {  // diagnostic stamps of a query batch: summed over its states
         DevState ds[1 + kMaxSub];
         PP_HIP(hipMemcpyAsync(ds, ctx->mq_state.p, sizeof ds, hipMemcpyDeviceToHost, ctx->stream));

@@ -132,4 +132,7 @@ hipError_t launch_dubins_batch(hipStream_t st, const double* conf, int n, int ca
                                double* py, double* pyaw, int* n_out, int* word_out,
                                double* cost_out, int* status_out);
 
+#ifdef PP_STAMPS_SPAN
+void diag_dump_window_span(int launches);
+#endif
 }  // namespace ppamd

@@ -600,7 +600,11 @@ constexpr int kQPL = PP_QPL;                     // samples per lane in the scre
 constexpr int kQPB = 64 * kQPL;                  // samples per screen workgroup (its waves share them)
 #ifdef PP_WIN1024
 constexpr int kScanThreads = 1024;               // window_kernel workgroup (16 waves)
+#ifdef PP_WIN_REPAIR
+constexpr bool kWinRepair = true;                // repairs inside the window kernel (spills)
+#else
 constexpr bool kWinRepair = false;               // repairs in resolve_tail_kernel
+#endif
 #else
 constexpr int kScanThreads = 512;                // window_kernel workgroup (8 waves, 256 VGPRs)
 constexpr bool kWinRepair = true;                // repairs inside the window kernel (no spill)
@@ -1122,26 +1126,14 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
 #ifdef PP_STAMPS_SCREEN
         tm1 = (int64_t)__builtin_amdgcn_s_memrealtime() + (int64_t)(bb * 0.0f) + (q & 0);
 #endif
-#ifdef PP_DIAG_NOREEVAL
-        if (false) {
-#else
         if (q >= 0 && key != 0x7fffffff && !(key & kExactNode)) {
-#endif
             // the sample's screen operands, as wave 0 held them
             const float* s_qx = reinterpret_cast<const float*>(smem) + (3 * kScanWaves + 1) * kQPB;
             const float qx = s_qx[tid], qy = s_qx[kQPB + tid];
             const int rel = key - c0 - r0;
             int ui = -1;
             float other = __builtin_inff();
-#if defined(PP_DIAG_REEVAL_GLOBAL)
-            if (false) {
-#elif defined(PP_DIAG_REEVAL_BCAST)
-            if (rel >= 0) {
-                const int rel_ = rel;
-                const int rel = rel_ & 0;  // every lane the same block: no bank conflicts (wrong results)
-#else
             if (rel >= 0) {  // (LDS only: a shared pointer select would make these flat loads)
-#endif
                 float vx[kScanBlk], vy[kScanBlk], vw[kScanBlk];
 #pragma unroll
                 for (int v = 0; v < kScanBlk / 4; ++v) {
@@ -2642,6 +2634,8 @@ static_assert(kStage % 256 == 0 && kGrab % kScanBlk == 0, "whole DMA quarters an
 // workgroup's start to the last one's end, the start skew and workgroup 0's end (stamps[0..3])
 __device__ unsigned long long g_span[4] = {~0ull, 0ull, 0ull, 0ull};  // min start, max start, max end, done
 __device__ unsigned long long g_span_wg0, g_span_maxdur, g_span_sumdur;
+__device__ unsigned long long g_wgdur[256];  // per workgroup: summed lifetime over the launches
+__device__ unsigned long long g_wgstart[256];  // per workgroup: summed start offset past the first
 struct SpanStamp {
     DevState* st;
     unsigned long long t_in = 0;
@@ -2657,6 +2651,7 @@ struct SpanStamp {
         __syncthreads();
         if (threadIdx.x == 0) {
             const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            if (blockIdx.x < 256 && gridDim.x > 1) g_wgdur[blockIdx.x] += t - t_in;
             if (blockIdx.x == 0) atomicExch(&g_span_wg0, t);
             else {
                 atomicMax(&g_span_maxdur, t - t_in);
@@ -4042,5 +4037,28 @@ hipError_t launch_dubins_batch(hipStream_t st, const double* conf, int n, int ca
                                                       cost_out, status_out);
     return hipGetLastError();
 }
+
+#ifdef PP_STAMPS_SPAN
+// diagnostic build only: per-workgroup window_kernel lifetimes summed over the launches, by XCD
+void diag_dump_window_span(int launches) {
+    unsigned long long d[256];
+    if (hipMemcpyFromSymbol(d, HIP_SYMBOL(g_wgdur), sizeof d) != hipSuccess) return;
+    const double n = launches > 0 ? launches : 1;
+    for (int x = 0; x < 8; ++x) {
+        double mn = 1e30, mx = 0, sum = 0;
+        int c = 0;
+        for (int b = x; b < 256; b += 8) {
+            if (b == 0 || d[b] == 0) continue;
+            const double v = d[b] / n / 100.0;
+            mn = std::min(mn, v), mx = std::max(mx, v), sum += v, ++c;
+        }
+        fprintf(stderr, "[span] XCD %d: %d workgroups, lifetime min %.2f mean %.2f max %.2f us\n", x, c,
+                mn, c ? sum / c : 0.0, mx);
+    }
+    fprintf(stderr, "[span] workgroup 0: %.2f us\n", d[0] / n / 100.0);
+    unsigned long long z[256] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wgdur), z, sizeof z);
+}
+#endif
 
 }  // namespace ppamd

@@ -21,6 +21,8 @@ while p.tree_size() < 100000:
 p.extend(4096 * 4)
 p.set_profiling(True)
 p.reset_stats()
+p.stats()  # (a diagnostic build dumps and clears its per-workgroup sums here)
+print("---- measured windows ----", file=sys.stderr, flush=True)
 p.extend(20 * 4096)
 st = p.stats()
 s = st["stamps"]
