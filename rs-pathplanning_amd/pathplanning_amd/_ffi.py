@@ -86,6 +86,15 @@ def lib():
             return _lib
         if not os.path.exists(LIB_PATH):
             raise PPError(PP_ERR_STATE, f"{LIB_PATH} not built: run __graft_entry__.build()")
+        # One HIP runtime per process: PyTorch (the streams / torch.distributed plumbing) ships
+        # its own libamdhip64 / libhsa-runtime64; loaded first, the library binds to that one
+        # instead of bringing /opt/rocm's beside it.  Measured: the config-3 batch (two sub-batch
+        # streams) 320 -> 342 M it/s, a 1024-query shard 145 -> 172 M; single-stream workloads
+        # unchanged.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         dp, ip, i64p = C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
         vp = C.c_void_p
