@@ -191,6 +191,20 @@ int pp_rrt_check_finish_batch(pp_ctx* ctx, const int32_t* nodes, int k, uint8_t*
  * *n = 0 when *ok = 0.  PP_ERR_CAPACITY when cap is too small. */
 int pp_rrt_check_finish(pp_ctx* ctx, int32_t node, uint8_t* ok, double* x, double* y,
                         int64_t cap, int64_t* n, double* length);
+/* RRT::optimize(node, i) (rrt.rs:463-487) for tree node `node`: *n_chain = 0 when it returns None
+ * (also for i >= RECURSION_LIMIT = 16), else the depth of the returned chain: chain[l] (at most
+ * 16 - i entries) is the tree node the l-th copy connects to, i.e. the returned Node sits at
+ * node's coordinates with parent a copy of chain[0] at its coordinates, ..., ending at the tree
+ * node chain[n - 1]; each copy's yaw is Node::new's compute_yaw toward its parent. */
+int pp_rrt_optimize(pp_ctx* ctx, int32_t node, int i, int32_t* chain, int* n_chain);
+/* RRT::finalize(goal) (rrt.rs:489-540) for the caller-built goal node Node::new_goal((gx, gy),
+ * parent, gyaw) with `parent` a tree node: optimize_from_goal (the planner's goal yaw when
+ * optimize succeeds, rrt.rs:494-498), then every edge's Dubins points, reversed.  The line is
+ * returned whether or not it verifies; *verified (may be NULL) = Space::verify of it (what
+ * check_finish adds).  *n = its points (cap 0 or x/y NULL: the size only); a None steer on the
+ * chain returns PP_ERR_REFERENCE_PANIC (rrt.rs:529). */
+int pp_rrt_finalize(pp_ctx* ctx, double gx, double gy, double gyaw, int32_t parent, double* x,
+                    double* y, int64_t cap, int64_t* n, uint8_t* verified);
 /* RRT::plan (rrt.rs:599-619), sequential spec: n_iter plan_one iterations (extend + check_finish
  * on every accepted node); *best_node = the node whose finish has the minimum euclidean_length
  * (first on ties, -1 when none verified); the line via pp_rrt_check_finish(best_node). */

@@ -434,13 +434,15 @@ def optimize(scene, node, i, chain):  # rrt.rs:463-487, full line_to_origin veri
     return None
 
 
-def finalize(scene, goal):  # rrt.rs:489-540
+def finalize(scene, goal, goal_yaw=None):  # rrt.rs:489-540
+    """goal_yaw: the planner's goal yaw, which optimize_from_goal gives the new goal node when
+    optimize succeeds (rrt.rs:494-498); default: the goal node's own (check_finish: the same)."""
     R, step = scene["turn_radius"], scene["step_size"]
     chain = []
     if goal.parent is not None:
         n = optimize(scene, goal.parent, 0, chain)
         if n is not None:
-            goal = PNode(goal.x, goal.y, goal.yaw, n)
+            goal = PNode(goal.x, goal.y, goal.yaw if goal_yaw is None else goal_yaw, n)
     xs, ys = [], []
     for n in goal.iter_to_root():
         if n.parent is None:

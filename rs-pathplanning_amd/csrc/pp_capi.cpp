@@ -453,7 +453,16 @@ constexpr int kCfBatch = 16384;     // nodes per check_finish launch
 constexpr int kCfPtsCap = 1 << 16;  // line points per check_finish workgroup
 
 // check_finish for nodes[0, k) (device pointer already filled); results on the device
-int cf_launch(pp_ctx* c, int k, int want_line, int grid) {
+// The goal of a check_finish_kernel launch: the planner's (check_finish), or a caller-built goal
+// node (finalize), and the kernel mode / optimize's starting level.
+struct CfGoal {
+    double x, y, yaw, yaw_opt;
+    int level0 = 0, mode = kCfCheck;
+};
+
+int cf_launch(pp_ctx* c, int k, int want_line, int grid, const CfGoal* g = nullptr) {
+    const CfGoal dflt{c->goal[0], c->goal[1], c->goal[2], c->goal[2]};
+    if (!g) g = &dflt;
     PP_HIP(c->cf_ok.reserve(kCfBatch));
     PP_HIP(c->cf_len.reserve(kCfBatch));
     PP_HIP(c->cf_npts.reserve(kCfBatch));
@@ -463,10 +472,11 @@ int cf_launch(pp_ctx* c, int k, int want_line, int grid) {
     PP_HIP(c->cf_etab.reserve((size_t)kCfGrid * 2 * kCfMaxEdges));
     PP_HIP(c->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
     PP_HIP(hipMemsetAsync(c->cf_err.p, 0, sizeof(int), c->stream));
-    PP_HIP(launch_check_finish(c->stream, c->scene_dev(), c->tree_dev(), c->cf_nodes.p, k,
-                               c->goal[0], c->goal[1], c->goal[2], want_line, c->cf_ok.p,
-                               c->cf_len.p, c->cf_npts.p, c->cf_chain.p, c->api_lit_scratch.p,
-                               c->cf_pts.p, kCfPtsCap, c->cf_etab.p, c->cf_err.p, grid));
+    PP_HIP(launch_check_finish(c->stream, c->scene_dev(), c->tree_dev(), c->cf_nodes.p, k, g->x,
+                               g->y, g->yaw, g->yaw_opt, g->level0, g->mode, want_line,
+                               c->cf_ok.p, c->cf_len.p, c->cf_npts.p, c->cf_chain.p,
+                               c->api_lit_scratch.p, c->cf_pts.p, kCfPtsCap, c->cf_etab.p,
+                               c->cf_err.p, grid));
     int err = 0;
     PP_HIP(hipMemcpyAsync(&err, c->cf_err.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     PP_HIP(hipStreamSynchronize(c->stream));
@@ -1548,6 +1558,63 @@ int pp_rrt_check_finish(pp_ctx* ctx, int32_t node, uint8_t* ok, double* x, doubl
             ++w;
         }
     if (n) *n = w;
+    return PP_OK;
+}
+
+int pp_rrt_optimize(pp_ctx* ctx, int32_t node, int i, int32_t* chain, int* n_chain) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (!n_chain || node < 0 || node >= ctx->n || i < 0)
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad arguments");
+    *n_chain = 0;
+    if (i >= kCfLevels) return PP_OK;  // RECURSION_LIMIT (rrt.rs:464-466): None
+    PP_HIP(ctx->cf_nodes.reserve(kCfBatch));
+    PP_HIP(hipMemcpyAsync(ctx->cf_nodes.p, &node, sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+    CfGoal g{ctx->goal[0], ctx->goal[1], ctx->goal[2], ctx->goal[2]};
+    g.level0 = i;
+    g.mode = kCfOptimize;
+    if ((r = cf_launch(ctx, 1, 0, 1, &g))) return r;
+    int row[kCfLevels + 2];
+    PP_HIP(hipMemcpy(row, ctx->cf_chain.p, sizeof(row), hipMemcpyDeviceToHost));
+    *n_chain = row[0];
+    if (chain)
+        for (int l = 0; l < row[0]; ++l) chain[l] = row[2 + l];
+    return PP_OK;
+}
+
+int pp_rrt_finalize(pp_ctx* ctx, double gx, double gy, double gyaw, int32_t parent, double* x,
+                    double* y, int64_t cap, int64_t* n, uint8_t* verified) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (!n || parent < 0 || parent >= ctx->n || !std::isfinite(gx) || !std::isfinite(gy))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad arguments");
+    PP_HIP(ctx->cf_nodes.reserve(kCfBatch));
+    PP_HIP(hipMemcpyAsync(ctx->cf_nodes.p, &parent, sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+    CfGoal g{gx, gy, gyaw, ctx->goal[2]};
+    g.mode = kCfFinalize;
+    if ((r = cf_launch(ctx, 1, 1, 1, &g))) return r;
+    int okv = 0, np = 0, row[kCfLevels + 2];
+    PP_HIP(hipMemcpy(&okv, ctx->cf_ok.p, sizeof(int), hipMemcpyDeviceToHost));
+    PP_HIP(hipMemcpy(&np, ctx->cf_npts.p, sizeof(int), hipMemcpyDeviceToHost));
+    PP_HIP(hipMemcpy(row, ctx->cf_chain.p, sizeof(row), hipMemcpyDeviceToHost));
+    if (verified) *verified = (uint8_t)okv;
+    *n = np;
+    if (!(x && y) || cap == 0) return PP_OK;
+    if (cap < np) return set_err(PP_ERR_CAPACITY, "line buffer smaller than the finalized line");
+    const int E = row[1];
+    std::vector<int> et(2 * (size_t)E);
+    std::vector<double> hx(kCfPtsCap), hy(kCfPtsCap);
+    PP_HIP(hipMemcpy(et.data(), ctx->cf_etab.p, et.size() * sizeof(int), hipMemcpyDeviceToHost));
+    PP_HIP(hipMemcpy(hx.data(), ctx->cf_pts.p, kCfPtsCap * sizeof(double), hipMemcpyDeviceToHost));
+    PP_HIP(hipMemcpy(hy.data(), ctx->cf_pts.p + kCfPtsCap, kCfPtsCap * sizeof(double), hipMemcpyDeviceToHost));
+    int64_t w = 0;  // l.reverse() (rrt.rs:538)
+    for (int e = E - 1; e >= 0; --e)
+        for (int i = et[2 * e + 1] - 1; i >= 0; --i) {
+            x[w] = hx[et[2 * e] + i];
+            y[w] = hy[et[2 * e] + i];
+            ++w;
+        }
+    *n = w;
     return PP_OK;
 }
 

@@ -74,11 +74,14 @@ hipError_t launch_steer_tasks(hipStream_t st, const SceneDev& sc, const TreeDev&
 // kCfLevels + 2 ints per row; want_line: materialise verified lines (length, points of the last
 // node each workgroup handled in pts/etab).  err |= 1 depth > kCfMaxDepth, 2 finalize panic,
 // 4 steer overflow, 8 point capacity.
+// check_finish_kernel modes: check_finish (rrt.rs:428-438), optimize alone (rrt.rs:463-487),
+// finalize of a caller-built goal node (rrt.rs:489-540)
+enum : int { kCfCheck = 0, kCfOptimize = 1, kCfFinalize = 2 };
 hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev& tr,
                                const int* nodes, int k, double gx, double gy, double gyaw,
-                               int want_line, int* ok, double* len, int* npts, int* chain,
-                               double* lit_scratch, double* pts, int pts_cap, int* etab, int* err,
-                               int grid);
+                               double gyaw_opt, int level0, int mode, int want_line, int* ok,
+                               double* len, int* npts, int* chain, double* lit_scratch,
+                               double* pts, int pts_cap, int* etab, int* err, int grid);
 
 // Multi-query batch: `steps` lockstep extend iterations of every query (config 3).
 struct MqArgs {

@@ -2831,9 +2831,15 @@ __device__ inline int cf_npoint(const SceneDev& sc, CfPose a, CfPose b) {
     return (int)nq + 7;
 }
 
+// mode kCfCheck: check_finish of nodes[b] (the goal node Node::new_goal(goal, node, gyaw));
+// kCfOptimize: optimize(nodes[b], level0) alone (ok_out: Some, chain_out: the chosen ancestors);
+// kCfFinalize: finalize of the goal node (gx, gy, gyaw) with parent nodes[b] — the line is built
+// whether it verifies or not (ok_out: it does).  optimize_from_goal gives the goal gyaw_opt when
+// optimize succeeds (rrt.rs:489-501: the planner's goal yaw), else the goal node keeps gyaw.
 __global__ __launch_bounds__(256) void check_finish_kernel(
     SceneDev sc, TreeDev tr, const int* __restrict__ nodes, int k, double gx, double gy,
-    double gyaw, int want_line, int* __restrict__ ok_out, double* __restrict__ len_out,
+    double gyaw, double gyaw_opt, int level0, int mode, int want_line, int* __restrict__ ok_out,
+    double* __restrict__ len_out,
     int* __restrict__ npts_out, int* __restrict__ chain_out, double* __restrict__ lit_scratch,
     double* __restrict__ pts, int pts_cap, int* __restrict__ etab, int* __restrict__ err) {
     __shared__ int s_path[kCfMaxDepth];
@@ -2875,7 +2881,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
         __syncthreads();
         // optimize, level by level
         int L = D - 1, s_lv = 0;
-        for (int level = 0; level < kCfLevels; ++level) {
+        for (int level = 0; level < kCfLevels - level0; ++level) {
             const int c = s_path[L];
             const CfPose a0{tr.x[c], tr.y[c], 0.0};
             int found = -1;
@@ -2911,8 +2917,26 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
             s_lv = level + 1;
         }
         __syncthreads();
+        if (mode == kCfOptimize) {
+            if (tid == 0) {
+                const int bad1 = s_bad;
+                ok_out[b] = (bad1 == 0 && s_lv > 0) ? 1 : 0;
+                len_out[b] = 0.0;
+                npts_out[b] = 0;
+                if (bad1) atomicOr(err, bad1);
+                if (chain_out) {
+                    chain_out[(size_t)b * (kCfLevels + 2)] = s_lv;
+                    chain_out[(size_t)b * (kCfLevels + 2) + 1] = 0;
+                    for (int i = 0; i < s_lv; ++i)
+                        chain_out[(size_t)b * (kCfLevels + 2) + 2 + i] = s_path[s_pos[i]];
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         // finalize: verify the chain's edges
         const int s = s_lv;
+        const double gyaw_e = s > 0 ? gyaw_opt : gyaw;  // optimize_from_goal (rrt.rs:489-501)
         const int ps = s > 0 ? s_pos[s - 1] : D - 1;
         const int E = 1 + s + ps;
         bool vok = s_bad == 0;
@@ -2920,8 +2944,8 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
             const int e = base + wave;
             int st = kAccept;
             if (e < E) {
-                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
-                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
+                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                 st = cf_edge_check<false>(sc, a, bp, e < E - 1, bx);
             }
             if (lane == 0) s_st[wave] = st;
@@ -2945,8 +2969,8 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
         // the remaining edges for None steers
         if (s_bad == 0 && !vok) {
             for (int e = tid; e < E; e += 256) {
-                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
-                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
+                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                 if (cf_npoint(sc, a, bp) == 0) atomicOr(&s_bad, 2);
             }
             __syncthreads();
@@ -2954,11 +2978,11 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
         const int bad = s_bad;
         double len = 0.0;
         int npts = 0;
-        if (vok && bad == 0 && want_line) {
+        if ((vok || mode == kCfFinalize) && bad == 0 && want_line) {
             // edge capacities, offsets, literal points
             for (int e = tid; e < E; e += 256) {
-                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
-                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
+                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                 et[2 * e] = cf_npoint(sc, a, bp);
             }
             __syncthreads();
@@ -2978,8 +3002,8 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
                 if (tid == 0) s_bad = 8;  // (a None / overflowing edge was rejected above)
             } else {
                 for (int e = tid; e < E; e += 256) {
-                    const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
-                    const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw);
+                    const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
+                    const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                     const int o = et[2 * e];
                     const int cap = (e + 1 < E ? et[2 * e + 2] : s_D) - o;
                     int n = 0, word = -1;
@@ -3031,13 +3055,14 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
 
 hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev& tr,
                                const int* nodes, int k, double gx, double gy, double gyaw,
-                               int want_line, int* ok, double* len, int* npts, int* chain,
-                               double* lit_scratch, double* pts, int pts_cap, int* etab, int* err,
-                               int grid) {
+                               double gyaw_opt, int level0, int mode, int want_line, int* ok,
+                               double* len, int* npts, int* chain, double* lit_scratch,
+                               double* pts, int pts_cap, int* etab, int* err, int grid) {
     if (k <= 0) return hipSuccess;
     check_finish_kernel<<<std::min(grid, k), 256, 0, st>>>(sc, tr, nodes, k, gx, gy, gyaw,
-                                                           want_line, ok, len, npts, chain,
-                                                           lit_scratch, pts, pts_cap, etab, err);
+                                                           gyaw_opt, level0, mode, want_line, ok,
+                                                           len, npts, chain, lit_scratch, pts,
+                                                           pts_cap, etab, err);
     return hipGetLastError();
 }
 

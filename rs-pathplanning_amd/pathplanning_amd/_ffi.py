@@ -34,7 +34,8 @@ EXPORTED = [
     "pp_abi_version", "pp_last_error", "pp_device_count", "pp_create", "pp_destroy",
     "pp_synchronize", "pp_rng_u64", "pp_gen_range", "pp_mod2pi", "pp_pi_2_pi",
     "pp_dubins_path_planning_batch", "pp_dubins_path_planning_from_origin_batch",
-    "pp_dubins_words_batch", "pp_create_circle", "pp_rrt_line_to_origin",
+    "pp_dubins_words_batch", "pp_create_circle", "pp_rrt_line_to_origin", "pp_rrt_optimize",
+    "pp_rrt_finalize",
     "pp_space_new", "pp_space_set_grid", "pp_space_get_bounds",
     "pp_space_new_polygons", "pp_space_verify_batch",
     "pp_rrt_new",
@@ -116,6 +117,9 @@ def lib():
             "pp_dubins_words_batch": ([vp, dp, C.c_int, dp, ip], C.c_int),
             "pp_create_circle": ([C.c_double, C.c_double, C.c_double, dp, C.c_int, ip], C.c_int),
             "pp_rrt_line_to_origin": ([vp, C.c_int32, dp, dp, C.c_int64, i64p], C.c_int),
+            "pp_rrt_optimize": ([vp, C.c_int32, C.c_int, ip, ip], C.c_int),
+            "pp_rrt_finalize": ([vp, C.c_double, C.c_double, C.c_double, C.c_int32, dp, dp,
+                                 C.c_int64, i64p, C.POINTER(C.c_uint8)], C.c_int),
             "pp_space_new": ([vp] + [C.c_double] * 7 + [dp, dp, dp, C.c_int], C.c_int),
             "pp_space_set_grid": ([vp, C.POINTER(C.c_uint32), C.c_int, C.c_int, C.c_double,
                                    C.c_double, C.c_double], C.c_int),

@@ -320,6 +320,32 @@ class RRT:  # rrt.rs:325-620
         return np.stack([x[:n.value], y[:n.value]], axis=1)
 
     # ---------------------------------------------------------------- goal connection
+    def optimize(self, node: int, i: int = 0):
+        """RRT::optimize(node, i) (rrt.rs:463-487): None, or the list of tree nodes the returned
+        chain of copies connects to, level by level (the last one is the tree node it ends at)."""
+        chain = np.zeros(16, dtype=np.int32)
+        n = C.c_int(0)
+        _ffi.check(_ffi.lib().pp_rrt_optimize(self.ctx.handle, int(node), int(i),
+                                              chain.ctypes.data_as(C.POINTER(C.c_int32)),
+                                              C.byref(n)))
+        return None if n.value == 0 else chain[:n.value].tolist()
+
+    def finalize(self, goal, goal_yaw: float, parent: int):
+        """RRT::finalize (rrt.rs:489-540) of the goal node Node::new_goal(goal, parent, goal_yaw):
+        ((n, 2) line, verified) — the line whether or not it verifies."""
+        n = C.c_int64(0)
+        ok = C.c_uint8(0)
+        gx, gy = goal
+        L = _ffi.lib()
+        _ffi.check(L.pp_rrt_finalize(self.ctx.handle, float(gx), float(gy), float(goal_yaw),
+                                     int(parent), None, None, 0, C.byref(n), C.byref(ok)))
+        x, y = np.zeros(max(n.value, 1)), np.zeros(max(n.value, 1))
+        dp = C.POINTER(C.c_double)
+        _ffi.check(L.pp_rrt_finalize(self.ctx.handle, float(gx), float(gy), float(goal_yaw),
+                                     int(parent), x.ctypes.data_as(dp), y.ctypes.data_as(dp),
+                                     n.value, C.byref(n), C.byref(ok)))
+        return np.stack([x[:n.value], y[:n.value]], axis=1), bool(ok.value)
+
     def check_finish_batch(self, nodes, with_length: bool = True):
         """RRT::check_finish (rrt.rs:428-438) for many tree nodes: dict of arrays ``ok``,
         ``length`` / ``n_points`` (verified lines only) and ``chain`` (rows of

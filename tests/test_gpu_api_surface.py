@@ -102,3 +102,71 @@ def test_line_to_origin_matches_the_reference(pkg, dpy):
         assert np.max(np.abs(got[:, 0] - np.array(ex))) <= TOL
         assert np.max(np.abs(got[:, 1] - np.array(ey))) <= TOL
     p.close()
+
+
+def _open_planner(seed, n_iter):
+    from pathplanning_amd import rrt, scenes
+
+    raw = scenes.bench6_open()
+    sx, sy, syaw = raw["start"]
+    gx, gy, gyaw = raw["goal"]
+    p = rrt.RRT((sx, sy), syaw, (gx, gy), gyaw, raw["max_iter"], raw["step_size"],
+                rrt.Space.from_raw(raw), seed=seed, window=256)
+    p.extend(n_iter)
+    return raw, p
+
+
+def test_optimize_matches_the_reference(pkg, dpy, oracle_mod):
+    raw, p = _open_planner(3, 600)
+    x, y, yaw, par = p.tree()
+    nodes = dpy.tree_nodes({"x": list(x), "y": list(y), "yaw": list(yaw), "parent": list(par)})
+    index = {id(nd): k for k, nd in enumerate(nodes)}
+    sc = oracle_mod.OracleScene.from_raw(raw).as_dict()
+    rng = np.random.default_rng(4)
+    picks = [0, 1, len(x) - 1] + rng.integers(1, len(x), 12).tolist()
+    seen_some = 0
+    for v in picks:
+        for i in (0, 2, 15, 16):
+            chain = []
+            exp = dpy.optimize(sc, nodes[int(v)], i, chain)
+            got = p.optimize(int(v), i)
+            if exp is None:
+                assert got is None, (v, i)
+                continue
+            seen_some += 1
+            assert got == [index[id(c)] for c in chain], (v, i)
+    assert seen_some > 0
+    p.close()
+
+
+def test_finalize_matches_the_reference(pkg, dpy, oracle_mod):
+    from pathplanning_amd import _ffi
+
+    raw, p = _open_planner(5, 500)
+    x, y, yaw, par = p.tree()
+    nodes = dpy.tree_nodes({"x": list(x), "y": list(y), "yaw": list(yaw), "parent": list(par)})
+    sc = oracle_mod.OracleScene.from_raw(raw).as_dict()
+    planner_goal_yaw = raw["goal"][2]
+    rng = np.random.default_rng(6)
+    x0, y0, x1, y1 = raw["bounds"]
+    cases = [(raw["goal"][0], raw["goal"][1], planner_goal_yaw, int(v))
+             for v in rng.integers(0, len(x), 6)]
+    cases += [(float(rng.uniform(x0, x1)), float(rng.uniform(y0, y1)), float(rng.uniform(-3, 3)),
+               int(rng.integers(0, len(x)))) for _ in range(14)]
+    verified = 0
+    for gx, gy, gyaw, v in cases:
+        goal = dpy.PNode(gx, gy, gyaw, nodes[v])
+        try:
+            ex, ey, _ = dpy.finalize(sc, goal, goal_yaw=planner_goal_yaw)
+        except RuntimeError:  # rrt.rs:529 panics
+            with pytest.raises(_ffi.PPError) as e:
+                p.finalize((gx, gy), gyaw, v)
+            assert e.value.code == _ffi.PP_ERR_REFERENCE_PANIC
+            continue
+        line, ok = p.finalize((gx, gy), gyaw, v)
+        assert line.shape == (len(ex), 2), (gx, gy, v)
+        assert np.max(np.abs(line[:, 0] - np.array(ex)), initial=0.0) <= TOL
+        assert np.max(np.abs(line[:, 1] - np.array(ey)), initial=0.0) <= TOL
+        assert ok == dpy.verify_line(sc, ex, ey), (gx, gy, v)
+        verified += ok
+    p.close()
