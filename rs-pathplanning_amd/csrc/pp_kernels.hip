@@ -1990,8 +1990,10 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                 lx = ox + pd / c * ca;
                 ly = oy + pd / c * sa;
             } else {
-                const double ldx = sin(pd) / c;
-                const double ldy = (1.0 - cos(pd)) / (mm == kModeL ? c : -c);
+                double sp, cp;
+                sincos(pd, &sp, &cp);  // one argument reduction for both (walk −2..3%)
+                const double ldx = sp / c;
+                const double ldy = (1.0 - cp) / (mm == kModeL ? c : -c);
                 const double gdx = ca * ldx + sa * ldy;
                 const double gdy = -sa * ldx + ca * ldy;
                 lx = ox + gdx;
