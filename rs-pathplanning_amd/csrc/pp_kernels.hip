@@ -2094,8 +2094,10 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
 #endif
 #ifdef PP_WALK_STATIC
     if ((int)blockIdx.x * (kWalkThreads / 64) >= total) return;  // whole workgroup idle
-#else
+#elif defined(PP_WALK_CONTIG)
     if ((int)blockIdx.x * ((total + (int)gridDim.x - 1) / (int)gridDim.x) >= total) return;
+#else
+    if ((int)blockIdx.x >= total) return;
 #endif
     if (kLds) stage_scene(sc);
     double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) +
@@ -2106,11 +2108,23 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     for (int t = gw; t < total; t += nw) {
 #else
-    // Workgroup b walks the contiguous task range [b * per, (b + 1) * per); its waves take the
-    // range's tasks one at a time from an LDS counter, so a wave that drew short paths takes more
-    // of them (a workgroup's share is a sum of dozens of tasks: far more even than a wave's
-    // handful under a static stride).  No global atomics.
+    // Workgroup b walks the tasks b, b + G, b + 2G, ... (G = the grid); its waves take them one
+    // at a time from an LDS counter, so a wave that drew short paths takes more of them (a
+    // workgroup's share is a sum of dozens of tasks: far more even than a wave's handful under a
+    // static stride), and consecutive tasks — one query's window, similar paths — land on
+    // different workgroups.  No global atomics.  (-DPP_WALK_CONTIG: contiguous ranges per
+    // workgroup, config 5's walk 10% longer.)
     __shared__ int s_next;
+#ifndef PP_WALK_CONTIG
+    const int G = (int)gridDim.x;
+    if (threadIdx.x == 0) s_next = 0;
+    __syncthreads();
+    for (;;) {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&s_next, 1);
+        const int t = (int)blockIdx.x + G * __builtin_amdgcn_readfirstlane(__shfl(k, 0));
+        if (t >= total) break;
+#else
     const int per = (total + (int)gridDim.x - 1) / (int)gridDim.x;
     const int t_end = min(total, ((int)blockIdx.x + 1) * per);
     if (threadIdx.x == 0) s_next = (int)blockIdx.x * per;
@@ -2120,6 +2134,7 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
         if (lane == 0) t = atomicAdd(&s_next, 1);
         t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
         if (t >= t_end) break;
+#endif
 #endif
         const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts);
         if (lane == 0) {
