@@ -2163,7 +2163,10 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
 // late with a share of tasks — the device's CU count times the workgroups per CU the occupancy
 // API gives for this instantiation and its dynamic LDS (the scene image decides; at most 4 of 8
 // waves each), read once per (device, image size) instead of assuming 256 CUs and 160 KB.
-template <int kMinW = kWalkMinWWindow>
+// kMaxPerCU: the query batch's walk runs beside the other sub-batch stream's kernels and does best
+// at 2 workgroups per CU although 3 fit (a 1024-query shard 171 -> 179-183 M it/s, the 8192-query
+// batch unchanged).
+template <int kMinW = kWalkMinWWindow, int kMaxPerCU = 4>
 inline int walk_grid_cap(int scene_bytes) {
     static std::mutex mu;
     static std::map<std::pair<int, int>, int> cache;
@@ -2183,7 +2186,7 @@ inline int walk_grid_cap(int scene_bytes) {
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, steer_walk_kernel<false, kMinW>,
                                                           kWalkThreads, walk_lds_bytes(0));
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
-    per_cu = std::min(4, per_cu);
+    per_cu = std::min(kMaxPerCU, per_cu);
     if (const char* v = std::getenv("PP_WALK_PER_CU")) per_cu = std::max(1, std::min(8, std::atoi(v)));
     const int cap = cus * per_cu;
     cache[{dev, scene_bytes}] = cap;
@@ -3293,7 +3296,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int nn_blocks = std::min((Q + 3) / 4, 4096);  // one wave per query
     const int prep_blocks = std::min((T + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
-                                     std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch>(a.sc.lds_bytes)));
+                                     std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch, 2>(a.sc.lds_bytes)));
     const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
     const int lds = a.sc.lds_bytes;
     for (int k = 0; k < steps; ++k) {
