@@ -2403,7 +2403,8 @@ __device__ __attribute__((always_inline)) inline bool resolve_role(
             int parent = -1, pos = -1, pq = -1;
             bool blocked = false;
             const int k = s_cnt[q], o = s_off[q];
-            for (int a2 = 0; a2 < k; ++a2) {
+            int a2 = 0;
+            for (; a2 < k; ++a2) {
                 const int code = ent_c(o + a2);
                 if (code >= 0) {
                     if (!__hip_atomic_load(&s_round[code], __ATOMIC_ACQUIRE,
@@ -2421,6 +2422,10 @@ __device__ __attribute__((always_inline)) inline bool resolve_role(
                 break;
             }
             if (blocked) {
+                // the entries before the blocker are final rejections: the next pass starts at
+                // the blocker (only this thread touches slot q's list bounds in the passes)
+                s_off[q] = o + a2;
+                s_cnt[q] = k - a2;
                 left = true;
                 continue;
             }

@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp
 for wl in ${WLS:-config2}; do
   case $wl in
     default) A="" ;;
-    config2|config4|polygons) A="--workload $wl --steps 20 --warmup 3 --no-cpu-baseline --no-size-sweep" ;;
+    config2|config4|polygons) A="--workload $wl --steps 20 --warmup 3 --no-cpu-baseline --no-size-sweep ${EXTRA:-}" ;;
     *) A="--workload $wl --warmup 3 --no-cpu-baseline ${EXTRA:-}" ;;
   esac
   timeout -k 10 400 python3 "$R/bench.py" $A > "$OUT/bench_$wl.json" 2> "$OUT/bench_$wl.err" || { tail -5 "$OUT/bench_$wl.err"; exit 1; }
