@@ -471,12 +471,16 @@ int cf_launch(pp_ctx* c, int k, int want_line, int grid, const CfGoal* g = nullp
     PP_HIP(c->cf_pts.reserve((size_t)kCfGrid * 3 * kCfPtsCap));
     PP_HIP(c->cf_etab.reserve((size_t)kCfGrid * 2 * kCfMaxEdges));
     PP_HIP(c->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
+    if (!c->lit_locks.p) {  // the literal scratch pool's slot locks (zero: free)
+        PP_HIP(c->lit_locks.reserve(kLiteralWaves));
+        PP_HIP(hipMemsetAsync(c->lit_locks.p, 0, kLiteralWaves * sizeof(int), c->stream));
+    }
     PP_HIP(hipMemsetAsync(c->cf_err.p, 0, sizeof(int), c->stream));
     PP_HIP(launch_check_finish(c->stream, c->scene_dev(), c->tree_dev(), c->cf_nodes.p, k, g->x,
                                g->y, g->yaw, g->yaw_opt, g->level0, g->mode, want_line,
                                c->cf_ok.p, c->cf_len.p, c->cf_npts.p, c->cf_chain.p,
-                               c->api_lit_scratch.p, c->cf_pts.p, kCfPtsCap, c->cf_etab.p,
-                               c->cf_err.p, grid));
+                               c->api_lit_scratch.p, c->lit_locks.p, c->cf_pts.p, kCfPtsCap,
+                               c->cf_etab.p, c->cf_err.p, grid));
     int err = 0;
     PP_HIP(hipMemcpyAsync(&err, c->cf_err.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     PP_HIP(hipStreamSynchronize(c->stream));

@@ -81,7 +81,8 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
                                const int* nodes, int k, double gx, double gy, double gyaw,
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,
-                               double* pts, int pts_cap, int* etab, int* err, int grid);
+                               int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
+                               int grid);
 
 // Multi-query batch: `steps` lockstep extend iterations of every query (config 3).
 struct MqArgs {

@@ -2827,15 +2827,43 @@ __device__ inline CfPose cf_pose(int j, int s, int ps, int D, const int* s_path,
 // verify one edge a → b (+ junction chord to b unless junction is false) on one wave; kCfPanic
 // when the steer is None (finalize's panic; verify_node's callers never pass such an edge here).
 enum : int { kCfPanic = 6 };
+// A literal-path scratch buffer (3 x kLiteralCap doubles) from a pool of kLiteralWaves slots,
+// so kernels of any width can run the measure-zero literal path: lane 0 takes a free slot with
+// atomicCAS (0 free, 1 taken), spinning over the pool if every slot is held — a holder is a
+// running wave that releases after its bounded literal walk.  Called by all lanes.
+__device__ __forceinline__ int lit_acquire(int* locks, int hint) {
+    int slot = 0;
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0;; ++i) {
+            const int sl = (hint + i) % kLiteralWaves;
+            if (atomicCAS(&locks[sl], 0, 1) == 0) {
+                slot = sl;
+                break;
+            }
+        }
+    slot = __shfl(slot, 0);
+    __threadfence();
+    return slot;
+}
+__device__ __forceinline__ void lit_release(int* locks, int slot) {
+    __threadfence();
+    if ((threadIdx.x & 63) == 0) atomicExch(&locks[slot], 0);
+}
+
 template <bool kAllowNone>
 __device__ __attribute__((noinline)) int cf_edge_check(const SceneDev& sc, CfPose a, CfPose b,
-                                                       bool junction, double* bx) {
+                                                       bool junction, double* lit_scratch,
+                                                       int* lit_locks) {
     const SteerPrep r = steer_prep(sc, a.x, a.y, a.yaw, b.x, b.y, b.yaw);
     if (!kAllowNone && r.state == kPrepNone) return kCfPanic;
     int st = steer_walk<false>(sc, walk_in(r), nullptr, junction);
-    if (st == kLiteral)
+    if (st == kLiteral) {  // (measure-zero) a scratch buffer from the pool, for this edge only
+        const int slot = lit_acquire(lit_locks, (int)blockIdx.x);
+        double* bx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
         st = steer_collide_literal(sc, a.x, a.y, a.yaw, b.x, b.y, b.yaw, bx, bx + kLiteralCap,
                                    bx + 2 * kLiteralCap, junction);
+        lit_release(lit_locks, slot);
+    }
     return st;
 }
 
@@ -2866,13 +2894,13 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
     double gyaw, double gyaw_opt, int level0, int mode, int want_line, int* __restrict__ ok_out,
     double* __restrict__ len_out,
     int* __restrict__ npts_out, int* __restrict__ chain_out, double* __restrict__ lit_scratch,
-    double* __restrict__ pts, int pts_cap, int* __restrict__ etab, int* __restrict__ err) {
+    int* __restrict__ lit_locks, double* __restrict__ pts, int pts_cap, int* __restrict__ etab,
+    int* __restrict__ err) {
     __shared__ int s_path[kCfMaxDepth];
     __shared__ int s_pos[kCfLevels];
     __shared__ int s_st[4];
     __shared__ int s_D, s_bad;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    double* bx = lit_scratch + (size_t)(blockIdx.x * 4 + wave) * 3 * kLiteralCap;
     double* px = pts + (size_t)blockIdx.x * 3 * pts_cap;
     double* py = px + pts_cap;
     double* pyw = py + pts_cap;
@@ -2917,7 +2945,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
                     const int to = s_path[m];
                     const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
                     const CfPose a{a0.x, a0.y, atan2(bt.y - a0.y, bt.x - a0.x)};
-                    st = cf_edge_check<true>(sc, a, bt, true, bx);
+                    st = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks);
                 }
                 if (lane == 0) s_st[wave] = st;
                 __syncthreads();
@@ -2971,7 +2999,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
             if (e < E) {
                 const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                 const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                st = cf_edge_check<false>(sc, a, bp, e < E - 1, bx);
+                st = cf_edge_check<false>(sc, a, bp, e < E - 1, lit_scratch, lit_locks);
             }
             if (lane == 0) s_st[wave] = st;
             __syncthreads();
@@ -3082,36 +3110,14 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
                                const int* nodes, int k, double gx, double gy, double gyaw,
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,
-                               double* pts, int pts_cap, int* etab, int* err, int grid) {
+                               int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
+                               int grid) {
     if (k <= 0) return hipSuccess;
     check_finish_kernel<<<std::min(grid, k), 256, 0, st>>>(sc, tr, nodes, k, gx, gy, gyaw,
                                                            gyaw_opt, level0, mode, want_line, ok,
-                                                           len, npts, chain, lit_scratch, pts,
-                                                           pts_cap, etab, err);
+                                                           len, npts, chain, lit_scratch,
+                                                           lit_locks, pts, pts_cap, etab, err);
     return hipGetLastError();
-}
-
-// A literal-path scratch buffer (3 x kLiteralCap doubles) from a pool of kLiteralWaves slots,
-// so kernels of any width can run the measure-zero literal path: lane 0 takes a free slot with
-// atomicCAS (0 free, 1 taken), spinning over the pool if every slot is held — a holder is a
-// running wave that releases after its bounded literal walk.  Called by all lanes.
-__device__ __forceinline__ int lit_acquire(int* locks, int hint) {
-    int slot = 0;
-    if ((threadIdx.x & 63) == 0)
-        for (int i = 0;; ++i) {
-            const int sl = (hint + i) % kLiteralWaves;
-            if (atomicCAS(&locks[sl], 0, 1) == 0) {
-                slot = sl;
-                break;
-            }
-        }
-    slot = __shfl(slot, 0);
-    __threadfence();
-    return slot;
-}
-__device__ __forceinline__ void lit_release(int* locks, int slot) {
-    __threadfence();
-    if ((threadIdx.x & 63) == 0) atomicExch(&locks[slot], 0);
 }
 
 // ------------------------------------------------- multi-query batch (config 3)
