@@ -2808,6 +2808,12 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_tail_kernel(WinKArgs 
 struct CfPose {
     double x, y, yaw;
 };
+// check_finish workgroup: kCfWaves candidate / finalize edges checked at a time (one per wave)
+#ifndef PP_CF_WAVES
+#define PP_CF_WAVES 4
+#endif
+constexpr int kCfWaves = PP_CF_WAVES;
+constexpr int kCfThreads = 64 * kCfWaves;
 
 // pose j of the finalize chain: 0 = goal, 1..s = optimised copies, then path[ps], ..., path[0]
 __device__ inline CfPose cf_pose(int j, int s, int ps, int D, const int* s_path, const int* s_pos,
@@ -2889,7 +2895,7 @@ __device__ inline int cf_npoint(const SceneDev& sc, CfPose a, CfPose b) {
 // kCfFinalize: finalize of the goal node (gx, gy, gyaw) with parent nodes[b] — the line is built
 // whether it verifies or not (ok_out: it does).  optimize_from_goal gives the goal gyaw_opt when
 // optimize succeeds (rrt.rs:489-501: the planner's goal yaw), else the goal node keeps gyaw.
-__global__ __launch_bounds__(256) void check_finish_kernel(
+__global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
     SceneDev sc, TreeDev tr, const int* __restrict__ nodes, int k, double gx, double gy,
     double gyaw, double gyaw_opt, int level0, int mode, int want_line, int* __restrict__ ok_out,
     double* __restrict__ len_out,
@@ -2898,7 +2904,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
     int* __restrict__ err) {
     __shared__ int s_path[kCfMaxDepth];
     __shared__ int s_pos[kCfLevels];
-    __shared__ int s_st[4];
+    __shared__ int s_st[kCfWaves];
     __shared__ int s_D, s_bad;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double* px = pts + (size_t)blockIdx.x * 3 * pts_cap;
@@ -2926,7 +2932,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
             __syncthreads();
             continue;
         }
-        for (int i = tid; i < D / 2; i += 256) {
+        for (int i = tid; i < D / 2; i += kCfThreads) {
             const int t = s_path[i];
             s_path[i] = s_path[D - 1 - i];
             s_path[D - 1 - i] = t;
@@ -2938,7 +2944,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
             const int c = s_path[L];
             const CfPose a0{tr.x[c], tr.y[c], 0.0};
             int found = -1;
-            for (int base = 0; base <= L; base += 4) {
+            for (int base = 0; base <= L; base += kCfWaves) {
                 const int m = base + wave;
                 int st = kReject;
                 if (m <= L && !sc.root_blocked) {
@@ -2949,7 +2955,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
                 }
                 if (lane == 0) s_st[wave] = st;
                 __syncthreads();
-                for (int w = 0; w < 4 && found == -1; ++w) {
+                for (int w = 0; w < kCfWaves && found == -1; ++w) {
                     const int sw = s_st[w];
                     if (base + w > L || sw == kReject) continue;
                     if (sw == kAccept)
@@ -2993,7 +2999,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
         const int ps = s > 0 ? s_pos[s - 1] : D - 1;
         const int E = 1 + s + ps;
         bool vok = s_bad == 0;
-        for (int base = 0; base < E && vok; base += 4) {
+        for (int base = 0; base < E && vok; base += kCfWaves) {
             const int e = base + wave;
             int st = kAccept;
             if (e < E) {
@@ -3003,7 +3009,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
             }
             if (lane == 0) s_st[wave] = st;
             __syncthreads();
-            for (int w = 0; w < 4; ++w) {
+            for (int w = 0; w < kCfWaves; ++w) {
                 const int sw = s_st[w];
                 if (sw == kCfPanic || sw == kError) {
                     if (tid == 0) s_bad = sw == kCfPanic ? 2 : 4;
@@ -3021,7 +3027,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
         // a panic anywhere in finalize wins over a rejection (the reference panics first): scan
         // the remaining edges for None steers
         if (s_bad == 0 && !vok) {
-            for (int e = tid; e < E; e += 256) {
+            for (int e = tid; e < E; e += kCfThreads) {
                 const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                 const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                 if (cf_npoint(sc, a, bp) == 0) atomicOr(&s_bad, 2);
@@ -3033,7 +3039,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
         int npts = 0;
         if ((vok || mode == kCfFinalize) && bad == 0 && want_line) {
             // edge capacities, offsets, literal points
-            for (int e = tid; e < E; e += 256) {
+            for (int e = tid; e < E; e += kCfThreads) {
                 const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                 const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                 et[2 * e] = cf_npoint(sc, a, bp);
@@ -3054,7 +3060,7 @@ __global__ __launch_bounds__(256) void check_finish_kernel(
             if (s_D < 0) {
                 if (tid == 0) s_bad = 8;  // (a None / overflowing edge was rejected above)
             } else {
-                for (int e = tid; e < E; e += 256) {
+                for (int e = tid; e < E; e += kCfThreads) {
                     const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                     const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                     const int o = et[2 * e];
@@ -3113,7 +3119,7 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
                                int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
                                int grid) {
     if (k <= 0) return hipSuccess;
-    check_finish_kernel<<<std::min(grid, k), 256, 0, st>>>(sc, tr, nodes, k, gx, gy, gyaw,
+    check_finish_kernel<<<std::min(grid, k), kCfThreads, 0, st>>>(sc, tr, nodes, k, gx, gy, gyaw,
                                                            gyaw_opt, level0, mode, want_line, ok,
                                                            len, npts, chain, lit_scratch,
                                                            lit_locks, pts, pts_cap, etab, err);
