@@ -500,7 +500,8 @@ def run_batch(args, D, star, with_cpu):
     bytes_per_eval = 16  # f64 x + f64 y of one SoA row (exact NN)
     achieved = evals_per_launch * bytes_per_eval / (nn_ms * 1e-3) / 1e9
     wl = "config5" if star else "config3"
-    pmc = load_profile("batch_pmc.json").get(wl, {}) if args.queries == 8192 else {}
+    # the counter passes were taken on the whole 8192-query batch on one GPU
+    pmc = load_profile("batch_pmc.json").get(wl, {}) if args.queries == 8192 and D.world == 1 else {}
     nn_share = sp["nn_scan_ms"] / max(sp["nn_scan_ms"] + sp["steer_ms"], 1e-9)
     res = {
         "value": round(iters_total / t_max, 1),
