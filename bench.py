@@ -161,7 +161,18 @@ class Dist:
 
         if self.dist is None:
             return torch.from_numpy(rec)
-        dev = torch.device("cuda", self.device) if self.gather_backend == "nccl" else None
+        if self.gather_backend == "nccl":
+            try:
+                return self._gather(rec, torch.device("cuda", self.device))
+            except Exception as e:  # RCCL refused (it raises on every rank): the CPU group
+                print(f"[bench] RCCL all_gather failed ({e}); gathering over gloo",
+                      file=sys.stderr, flush=True)
+                self.gather_backend = "gloo (RCCL failed)"
+        return self._gather(rec, None)
+
+    def _gather(self, rec, dev):
+        import torch
+
         n = torch.tensor([rec.shape[0]], dtype=torch.int64, device=dev)
         sizes = [torch.zeros_like(n) for _ in range(self.world)]
         self.dist.all_gather(sizes, n)
