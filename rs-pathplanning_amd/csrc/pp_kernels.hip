@@ -877,12 +877,12 @@ struct WinKArgs {
 // the block's 16 nodes from global memory with the screen's own prep and arithmetic, the lowest
 // u with value == best and the minimum of the others.  Out of line: inlined, the compiler merges
 // it with the LDS path into flat loads.
-template <bool kExp>
+template <bool kExp, int kNodes = kScanBlk>
 __device__ __attribute__((noinline)) void screen_block_global(const float* __restrict__ bx,
                                                               const float* __restrict__ by, float qx,
                                                               float qy, float oxf, float oyf,
                                                               float best, int& ui, float& other) {
-    for (int u = 0; u < kScanBlk; ++u) {
+    for (int u = 0; u < kNodes; ++u) {
         float px = bx[u], py = by[u], pw = 0.0f;
         if (kExp) {
             px = px - oxf;
@@ -1185,6 +1185,232 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
     }
 #endif
 }
+
+#ifdef PP_SCREEN_MFMA
+// The expanded screen on the matrix cores (build variant): for a tile of 32 staged nodes and a
+// group of 32 samples, v_mfma_f32_32x32x2_f32 with A[i] = ((n-o)_y, (n-o)_x) of node i,
+// B[j] = (-2(q-o)_y, -2(q-o)_x) of sample j and C[i][j] = |n_i - o|^2 gives
+// D[i][j] = fma(B1, A1, fma(B0, A0, C)) — bit for bit the VALU chain of scan_role
+// (scripts/micro/mfma_screen_check.hip: 2,048,000 of 2,048,000 results identical), so the winner
+// re-evaluation and nn_finalize's bounds are unchanged.  Lane l holds column j = l % 32 and the
+// rows (r / 4) * 8 + (l / 32) * 4 + r % 4 (r = 0..15): a lane's block is 16 of the tile's rows,
+// the two lane halves are merged at the end, and the winner's whole tile is re-evaluated.
+typedef float pp_floatx16 __attribute__((ext_vector_type(16)));
+constexpr int kMTile = 32;                  // nodes per MFMA tile
+constexpr int kMGroups = kQPB / 32;         // sample groups of 32 per workgroup block
+
+__device__ __attribute__((always_inline)) inline void scan_role_mfma(const WinKArgs& a, int b,
+                                                                    char* smem) {
+    static_assert(kQPB % 32 == 0 && kGrab % kMTile == 0, "whole groups and tiles");
+    DevState* st = a.st;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, j = lane & 31;  // lane half (MFMA k index) and sample column
+    const int W = st->Wp[a.p];
+    const int ns = st->n_scan;
+    if (b == 0 && tid == 0) st->nsp[a.p] = ns;
+    const int G = a.nqb * a.chunks;
+    if (b >= G) return;
+    const int t = (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b;
+    const int qb = t % a.nqb, c = t / a.nqb;
+    const int qbase = qb * kQPB;
+    if (qbase >= W) return;
+    const int cl = scan_chunk_len(ns, a.chunks);
+    const int c0 = c * cl;
+    if (c0 >= ns) return;
+    const int L = min(c0 + cl, ns) - c0;
+    const float* nx = a.tr.x32;
+    const float* ny = a.tr.y32;
+    float* stg = reinterpret_cast<float*>(smem + kScreenStageOff);
+    int* s_next = reinterpret_cast<int*>(stg + 3 * kStage);
+    auto issue_round = [&](int r0) {
+        const int len = min(kStage, L - r0);
+        for (int q4 = wave; q4 * 256 < len; q4 += kScanWaves) {
+            if (q4 * 256 + 4 * lane < len) {
+                const size_t gi = (size_t)(c0 + r0 + q4 * 256 + 4 * lane);
+                __builtin_amdgcn_global_load_lds((glb_void*)(nx + gi), (lds_void*)(stg + q4 * 256), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((glb_void*)(ny + gi), (lds_void*)(stg + kStage + q4 * 256), 16, 0, 0);
+            }
+        }
+    };
+    issue_round(0);
+    // samples: group g holds sorted positions qbase + 32 g + j; this lane the y (h = 0) or the x
+    // (h = 1) operand, -2 (q - o) (exact scaling)
+    const float2 o = a.g.ob[a.p][qb];
+    const float oxf = o.x, oyf = o.y;
+    float bq[kMGroups], best[kMGroups], second[kMGroups];
+    int key[kMGroups];
+#pragma unroll
+    for (int g = 0; g < kMGroups; ++g) {
+        const int pos = qbase + 32 * g + j;
+        const bool in = pos < W;
+        const double v = h == 0 ? (in ? a.g.ssy[a.p][pos] : (double)oyf)
+                                : (in ? a.g.ssx[a.p][pos] : (double)oxf);
+        bq[g] = -2.0f * (float)(v - (double)(h == 0 ? oyf : oxf));
+        best[g] = __builtin_inff();
+        second[g] = __builtin_inff();
+        key[g] = 0x7fffffff;
+    }
+    {  // wave 0 parks every sample's operands for the re-evaluation (slot 32 g + j)
+        float* s_qx = reinterpret_cast<float*>(smem) + (3 * kScanWaves + 1) * kQPB;
+        if (wave == 0) {
+#pragma unroll
+            for (int g = 0; g < kMGroups; ++g) s_qx[(1 - h) * kQPB + 32 * g + j] = bq[g];
+        }
+        int* s_sid = reinterpret_cast<int*>(smem) + 3 * kScanWaves * kQPB;
+        for (int k = tid; k < kQPB; k += kScanThreads) {
+            const int pos = qbase + k;
+            s_sid[k] = pos < W ? a.perm[a.p][pos] : -1;
+        }
+    }
+    int r0 = 0;
+    for (;;) {
+        const int len = min(kStage, L - r0);
+        if (tid == 0) *s_next = 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int i = 4 * tid; i < len; i += 4 * kScanThreads) {  // prep in place: (n-o, |n-o|^2)
+            float4 x4 = *reinterpret_cast<const float4*>(stg + i);
+            float4 y4 = *reinterpret_cast<const float4*>(stg + kStage + i);
+            float4 w4;
+            x4.x -= oxf, x4.y -= oxf, x4.z -= oxf, x4.w -= oxf;
+            y4.x -= oyf, y4.y -= oyf, y4.z -= oyf, y4.w -= oyf;
+            w4.x = __builtin_fmaf(y4.x, y4.x, x4.x * x4.x);
+            w4.y = __builtin_fmaf(y4.y, y4.y, x4.y * x4.y);
+            w4.z = __builtin_fmaf(y4.z, y4.z, x4.z * x4.z);
+            w4.w = __builtin_fmaf(y4.w, y4.w, x4.w * x4.w);
+            *reinterpret_cast<float4*>(stg + i) = x4;
+            *reinterpret_cast<float4*>(stg + kStage + i) = y4;
+            *reinterpret_cast<float4*>(stg + 2 * kStage + i) = w4;
+        }
+        __syncthreads();
+        for (;;) {
+            int g0 = 0;
+            if (lane == 0) g0 = atomicAdd(s_next, kGrab);
+            g0 = __builtin_amdgcn_readfirstlane(__shfl(g0, 0));
+            if (g0 >= len) break;
+            const int g1 = min(g0 + kGrab, len);
+            const int gt = g0 + ((g1 - g0) & ~(kMTile - 1));  // whole tiles (a tail: the last)
+            for (int u0 = g0; u0 < gt; u0 += kMTile) {
+                // A: this lane's node row j, k = h (y, then x); C: the |n-o|^2 of its 16 rows
+                const float av = stg[(h == 0 ? kStage : 0) + u0 + j];
+                pp_floatx16 cw;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const float4 w4 = *reinterpret_cast<const float4*>(stg + 2 * kStage + u0 + 8 * v + 4 * h);
+                    cw[4 * v] = w4.x, cw[4 * v + 1] = w4.y, cw[4 * v + 2] = w4.z, cw[4 * v + 3] = w4.w;
+                }
+                const int k = c0 + r0 + u0;
+                // group g + 1's product is issued before group g's reduction (two accumulators);
+                // minimum (not fminf): the operands are finite, and no canonicalising v_max
+                pp_floatx16 dn = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq[0], cw, 0, 0, 0);
+#pragma unroll
+                for (int g = 0; g < kMGroups; ++g) {
+                    const pp_floatx16 d = dn;
+                    if (g + 1 < kMGroups)
+                        dn = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq[g + 1], cw, 0, 0, 0);
+                    const float m0 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[0], d[1]), d[2]);
+                    const float m1 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[3], d[4]), d[5]);
+                    const float m2 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[6], d[7]), d[8]);
+                    const float m3 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[9], d[10]), d[11]);
+                    const float m4 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[12], d[13]), d[14]);
+                    const float m5 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m0, m1), m2);
+                    const float m6 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m3, m4), d[15]);
+                    const float m = __builtin_elementwise_minimum(m5, m6);
+                    second[g] = __builtin_amdgcn_fmed3f(best[g], m, second[g]);
+                    if (m < best[g]) {
+                        best[g] = m;
+                        key[g] = k;
+                    }
+                }
+            }
+            for (int u = gt; u < g1; ++u) {  // the chunk's tail (< 32 nodes): exact top-2, VALU
+                const float px = stg[u], py = stg[kStage + u], pw = stg[2 * kStage + u];
+#pragma unroll
+                for (int g = 0; g < kMGroups; ++g) {
+                    const float other = __shfl_xor(bq[g], 32);  // the sample's other operand
+                    const float qx = h == 0 ? other : bq[g], qy = h == 0 ? bq[g] : other;
+                    // (one lane half only: the halves' partials are merged as distinct nodes)
+                    const float d = h == 0 ? __builtin_fmaf(qx, px, __builtin_fmaf(qy, py, pw))
+                                           : __builtin_inff();
+                    second[g] = __builtin_amdgcn_fmed3f(best[g], d, second[g]);
+                    if (d < best[g]) {
+                        best[g] = d;
+                        key[g] = (c0 + r0 + u) | kExactNode;
+                    }
+                }
+            }
+        }
+        if (r0 + len >= L) break;
+        r0 += len;
+        __syncthreads();
+        issue_round(r0);
+    }
+    // the two lane halves of each sample (disjoint rows of the same tiles), then the waves, as in
+    // scan_role: keys are tile starts or kExactNode | tail index (the tail follows every tile)
+    float* s_b = reinterpret_cast<float*>(smem);
+    float* s_s = s_b + kScanWaves * kQPB;
+    int* s_i = reinterpret_cast<int*>(s_s + kScanWaves * kQPB);
+    int* s_sid = s_i + kScanWaves * kQPB;
+#pragma unroll
+    for (int g = 0; g < kMGroups; ++g) {
+        const float ob = __shfl_xor(best[g], 32), os = __shfl_xor(second[g], 32);
+        const int ok = __shfl_xor(key[g], 32);
+        const bool take = ob < best[g] || (ob == best[g] && ok < key[g]);
+        const float ss = __builtin_fminf(__builtin_fminf(second[g], os), take ? best[g] : ob);
+        if (h == 0) {
+            s_b[wave * kQPB + 32 * g + j] = take ? ob : best[g];
+            s_s[wave * kQPB + 32 * g + j] = ss;
+            s_i[wave * kQPB + 32 * g + j] = take ? ok : key[g];
+        }
+    }
+    __syncthreads();
+    if (tid < kQPB) {  // one thread per sample slot (sorted position qbase + tid)
+        float bb = s_b[tid], ss = s_s[tid];
+        int kk = s_i[tid];
+#pragma unroll
+        for (int w = 1; w < kScanWaves; ++w) {
+            const float ob = s_b[w * kQPB + tid], os = s_s[w * kQPB + tid];
+            const int ok = s_i[w * kQPB + tid];
+            const bool take = ob < bb || (ob == bb && ok < kk);
+            ss = fminf(fminf(ss, os), take ? bb : ob);
+            bb = take ? ob : bb;
+            kk = take ? ok : kk;
+        }
+        const int q = s_sid[tid];
+        int idx = kk == 0x7fffffff ? -1 : (kk & ~kExactNode);
+        if (q >= 0 && kk != 0x7fffffff && !(kk & kExactNode)) {
+            // the winning tile again, VALU, bit-identical: the lowest index of the best value and
+            // the best of the tile's other nodes (each lane-half block carried one minimum)
+            const float* s_qx = reinterpret_cast<const float*>(smem) + (3 * kScanWaves + 1) * kQPB;
+            const float qx = s_qx[tid], qy = s_qx[kQPB + tid];
+            const int rel = kk - c0 - r0;
+            int ui = -1;
+            float other = __builtin_inff();
+            if (rel >= 0) {
+#pragma unroll 8
+                for (int u = 0; u < kMTile; ++u) {
+                    const float d = __builtin_fmaf(qx, stg[rel + u],
+                                                   __builtin_fmaf(qy, stg[kStage + rel + u], stg[2 * kStage + rel + u]));
+                    if (ui < 0 && d == bb)
+                        ui = u;
+                    else
+                        other = __builtin_fminf(other, d);
+                }
+            } else {
+                screen_block_global<true, kMTile>(nx + kk, ny + kk, qx, qy, oxf, oyf, bb, ui, other);
+            }
+            idx = kk + ui;
+            ss = __builtin_fminf(ss, other);
+        }
+        if (q >= 0) {
+            const size_t o2 = (size_t)c * a.Kcap + qbase + tid;
+            a.pbest[o2] = bb;
+            a.psecond[o2] = ss;
+            a.pidx[o2] = idx;
+        }
+    }
+}
+#endif
 
 // The first window of a batch: its samples (the later ones come from the previous window kernel
 // workgroup 0, after the commit that decides where the next window starts).
@@ -2758,8 +2984,13 @@ __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
         return;
     }
     if (a.scan) {
+#ifdef PP_SCREEN_MFMA
+        if (a.gen)
+            scan_role_mfma(a, (int)blockIdx.x - 1, smem);
+#else
         if (a.gen)
             scan_role<true>(a, (int)blockIdx.x - 1, smem);
+#endif
         else
             scan_role<false>(a, (int)blockIdx.x - 1, smem);
     }
