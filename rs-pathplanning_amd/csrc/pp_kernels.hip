@@ -2272,11 +2272,12 @@ constexpr int kWalkMinWBatch = PP_WALK_MINW_BATCH;
 constexpr int kWalkMinWStar = kWalkMinWWindow;
 #ifdef PP_STAMPS_WALK
 // diagnostic build only (-DPP_STAMPS_WALK): per steer_walk launch, the launch span, the mean and
-// the longest wave lifetime (stamps[0..2], [3] launches) — the walk's load imbalance
+// the longest wave lifetime (stamps[0..2], [3] launches), the longest single task ([4]) — the
+// walk's load imbalance
 __device__ unsigned long long g_wspan[6] = {~0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
 struct WalkSpan {
     DevState* st;
-    unsigned long long t_in = 0;
+    unsigned long long t_in = 0, t_task = 0;  // t_task: this wave's longest single task
     explicit __device__ WalkSpan(DevState* s) : st(s) {
         t_in = __builtin_amdgcn_s_memrealtime();
         if ((threadIdx.x & 63) == 0) atomicMin(&g_wspan[0], t_in);
@@ -2287,6 +2288,7 @@ struct WalkSpan {
             atomicMax(&g_wspan[1], t);
             atomicMax(&g_wspan[2], t - t_in);
             atomicAdd(&g_wspan[3], t - t_in);
+            atomicMax(&g_wspan[5], t_task);
             __threadfence();
             const unsigned long long waves = (unsigned long long)gridDim.x * (blockDim.x >> 6);
             if (atomicAdd(&g_wspan[4], 1ull) == waves - 1) {
@@ -2296,7 +2298,8 @@ struct WalkSpan {
                 sp[1] += atomicAdd(&g_wspan[3], 0ull) / waves;
                 sp[2] += atomicAdd(&g_wspan[2], 0ull);
                 sp[3] += 1;
-                for (int i = 0; i < 5; ++i) atomicExch(&g_wspan[i], i == 0 ? ~0ull : 0ull);
+                sp[4] += atomicAdd(&g_wspan[5], 0ull);
+                for (int i = 0; i < 6; ++i) atomicExch(&g_wspan[i], i == 0 ? ~0ull : 0ull);
             }
         }
     }
@@ -2362,7 +2365,13 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
         if (t >= t_end) break;
 #endif
 #endif
+#ifdef PP_STAMPS_WALK
+        const unsigned long long t_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
         const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts);
+#ifdef PP_STAMPS_WALK
+        walk_span.t_task = max(walk_span.t_task, (unsigned long long)__builtin_amdgcn_s_memrealtime() - t_t0);
+#endif
         if (lane == 0) {
             if (t < W) {
                 snap_status[t] = s;

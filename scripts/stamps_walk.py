@@ -19,8 +19,9 @@ for Q in [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "1024,8192").sp
     b.extend(2000)
     s = b.stats()["stamps"]
     n = max(s[3], 1)
-    print("config3 Q=%d: %d walk launches: span %.2f us, mean wave %.2f us, longest wave %.2f us"
-          % (Q, s[3], s[0] / n / 100, s[1] / n / 100, s[2] / n / 100))
+    print("config3 Q=%d: %d walk launches: span %.2f us, mean wave %.2f us, longest wave %.2f us, "
+          "longest task %.2f us" % (Q, s[3], s[0] / n / 100, s[1] / n / 100, s[2] / n / 100,
+                                     s[4] / n / 100))
     b.close()
 sx, sy, syaw = raw["start"]
 gx, gy, gyaw = raw["goal"]
@@ -32,5 +33,5 @@ p.reset_stats()
 p.extend(20 * 4096)
 s = p.stats()["stamps"]
 n = max(s[3], 1)
-print("config2: %d walk launches: span %.2f us, mean wave %.2f us, longest wave %.2f us"
-      % (s[3], s[0] / n / 100, s[1] / n / 100, s[2] / n / 100))
+print("config2: %d walk launches: span %.2f us, mean wave %.2f us, longest wave %.2f us, "
+      "longest task %.2f us" % (s[3], s[0] / n / 100, s[1] / n / 100, s[2] / n / 100, s[4] / n / 100))
