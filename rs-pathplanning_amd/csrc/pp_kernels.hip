@@ -84,6 +84,15 @@ __device__ inline void stage_scene(const SceneDev& sc) {
     __syncthreads();
 }
 
+#ifdef PP_STAMPS_WALK
+// diagnostic build only: per walk launch, chunks tested, items that pass the chunk's bbox cull,
+// items that pass the per-segment f32 near test (flushed by the walk's last wave)
+__device__ unsigned long long g_cull[3] = {0ull, 0ull, 0ull};
+#define CULL_COUNT(i, v) \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_cull[i], (unsigned long long)(v))
+#else
+#define CULL_COUNT(i, v)
+#endif
 template <bool kLds>
 __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool check_bounds,
                                               bool seg_valid, double qx, double qy,
@@ -140,6 +149,7 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const int lane = threadIdx.x & 63;
     const float bxl = (float)bx0 - sc.cull_slack, bxh = (float)bx1 + sc.cull_slack;
     const float byl = (float)by0 - sc.cull_slack, byh = (float)by1 + sc.cull_slack;
+    CULL_COUNT(0, 1);
     for (int gy = cy0; gy <= cy1; ++gy) {
         for (int gx = cx0; gx <= cx1; ++gx) {
             const int cell = gy * sc.gnx + gx;
@@ -157,6 +167,7 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
                     ov = Dl.x + Dl.z >= bxl && Dl.x - Dl.z <= bxh && Dl.y + Dl.z >= byl &&
                          Dl.y - Dl.z <= byh;
                 }
+                CULL_COUNT(1, __builtin_popcountll(__ballot(ov)));
                 for (uint64_t m = __ballot(ov); m; m &= m - 1) {
                     const int src = (int)__builtin_ctzll(m);
                     const int d = __builtin_amdgcn_readlane(dl, src);
@@ -171,6 +182,7 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
                     const float dxf = D.x - axf, dyf = D.y - ayf, thr = D.z + Lf;
                     bool near = seg_valid && dxf * dxf + dyf * dyf <= thr * thr;
                     if (!__any(near)) continue;
+                    CULL_COUNT(2, 1);
                     if (!poly) {
                         // f32 closest point of the segment to the disc centre, decisive outside
                         // a band of +-eps around the radius (eps bounds the f32 rounding of the
@@ -2299,6 +2311,7 @@ struct WalkSpan {
                 sp[2] += atomicAdd(&g_wspan[2], 0ull);
                 sp[3] += 1;
                 sp[4] += atomicAdd(&g_wspan[5], 0ull);
+                for (int i = 0; i < 3; ++i) sp[5 + i] += atomicExch(&g_cull[i], 0ull);
                 for (int i = 0; i < 6; ++i) atomicExch(&g_wspan[i], i == 0 ? ~0ull : 0ull);
             }
         }

@@ -22,6 +22,8 @@ for Q in [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "1024,8192").sp
     print("config3 Q=%d: %d walk launches: span %.2f us, mean wave %.2f us, longest wave %.2f us, "
           "longest task %.2f us" % (Q, s[3], s[0] / n / 100, s[1] / n / 100, s[2] / n / 100,
                                      s[4] / n / 100))
+    print("  per chunk: %.2f items pass the bbox cull, %.2f the segment near test (%d chunks)"
+          % (s[6] / max(s[5], 1), s[7] / max(s[5], 1), s[5]))
     b.close()
 sx, sy, syaw = raw["start"]
 gx, gy, gyaw = raw["goal"]
@@ -35,3 +37,5 @@ s = p.stats()["stamps"]
 n = max(s[3], 1)
 print("config2: %d walk launches: span %.2f us, mean wave %.2f us, longest wave %.2f us, "
       "longest task %.2f us" % (s[3], s[0] / n / 100, s[1] / n / 100, s[2] / n / 100, s[4] / n / 100))
+print("  per chunk: %.2f items pass the bbox cull, %.2f the segment near test (%d chunks)"
+      % (s[6] / max(s[5], 1), s[7] / max(s[5], 1), s[5]))
