@@ -1820,8 +1820,16 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
         PP_HIP(hipMemcpyAsync(&err, ctx->mq_err.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
         if (err) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
+        const int64_t ran = steps;
         steps = 0;
-        for (int q = 0; q < Q; ++q) steps = std::max(steps, (htg[q] - hit[q] + K - 1) / K);
+        int behind = 0;
+        for (int q = 0; q < Q; ++q) {
+            steps = std::max(steps, (htg[q] - hit[q] + K - 1) / K);
+            behind += htg[q] > hit[q];
+        }
+        if (std::getenv("PP_DEBUG"))  // the top-up passes: queries whose windows stopped early
+            fprintf(stderr, "[pp] batch extend pass %d: %lld steps at K = %d, then %d of %d queries behind\n",
+                    pass, (long long)ran, K, behind, Q);
     }
     if ((n_iterations || n_accepted) && (r = mq_totals(ctx, &it1, &n1))) return r;
     if (n_iterations) *n_iterations = it1 - it0;

@@ -444,6 +444,11 @@ class RRTBatch:
                                               C.byref(acc)))
         return it.value, acc.value
 
+    def set_window(self, k: int):
+        """The window for the following extend calls (a power of two <= 64); the trees do not
+        depend on it."""
+        _ffi.check(_ffi.lib().pp_batch_set_window(self.ctx.handle, int(k)))
+
     def state(self, with_evals: bool = False):
         """(tree sizes int32[q], iterations int64[q]) [+ NN node-distance evals int64[q]]."""
         n = np.zeros(self.q, dtype=np.int32)
