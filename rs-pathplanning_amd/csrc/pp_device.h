@@ -432,4 +432,51 @@ __device__ inline double wave_max(double v) {
     return v;
 }
 
+// f32 wave reductions on DPP (no LDS round trips): quad swaps, half-row and row mirrors, then the
+// gfx9 row broadcasts 15 and 31 into the upper rows; lane 63 holds the result.  All 64 lanes must
+// be active.
+template <int kCtrl, int kRowMask = 0xF>
+__device__ inline float dpp_f32(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v),
+                                                                 __builtin_bit_cast(int, v), kCtrl,
+                                                                 kRowMask, 0xF, false));
+}
+__device__ inline float readlane_f32(float v, int k) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
+}
+__device__ inline float wave_min_f32(float v) {
+    v = __builtin_fminf(v, dpp_f32<0xB1>(v));       // quad_perm [1,0,3,2]
+    v = __builtin_fminf(v, dpp_f32<0x4E>(v));       // quad_perm [2,3,0,1]
+    v = __builtin_fminf(v, dpp_f32<0x141>(v));      // row_half_mirror
+    v = __builtin_fminf(v, dpp_f32<0x140>(v));      // row_mirror
+    v = __builtin_fminf(v, dpp_f32<0x142, 0xA>(v)); // row_bcast:15 into rows 1, 3
+    v = __builtin_fminf(v, dpp_f32<0x143, 0xC>(v)); // row_bcast:31 into rows 2, 3
+    return readlane_f32(v, 63);
+}
+__device__ inline float wave_max_f32(float v) {
+    v = __builtin_fmaxf(v, dpp_f32<0xB1>(v));
+    v = __builtin_fmaxf(v, dpp_f32<0x4E>(v));
+    v = __builtin_fmaxf(v, dpp_f32<0x141>(v));
+    v = __builtin_fmaxf(v, dpp_f32<0x140>(v));
+    v = __builtin_fmaxf(v, dpp_f32<0x142, 0xA>(v));
+    v = __builtin_fmaxf(v, dpp_f32<0x143, 0xC>(v));
+    return readlane_f32(v, 63);
+}
+// __shfl_up(v, 1) on DPP (wave_shr:1): lane l gets lane l - 1's value, lane 0 keeps its own
+__device__ inline double shfl_up1_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(v), __double2loint(v), 0x138, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), 0x138, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+// f32 bounds of an f64 value: lo <= v <= hi (the conversion rounds to nearest; a rounded-past
+// value moves out by far more than its rounding error)
+__device__ inline float f32_below(double v) {
+    const float f = (float)v;
+    return (double)f > v ? f - (__builtin_fabsf(f) * 1.0e-6f + 1.0e-30f) : f;
+}
+__device__ inline float f32_above(double v) {
+    const float f = (float)v;
+    return (double)f < v ? f + (__builtin_fabsf(f) * 1.0e-6f + 1.0e-30f) : f;
+}
+
 }  // namespace ppamd

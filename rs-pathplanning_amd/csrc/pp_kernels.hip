@@ -113,6 +113,7 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     }
     if (sc.m == 0 && sc.ne == 0) return false;
     const bool poly = sc.ne > 0;  // grid items are polygon edges (Q10p), else discs
+#ifdef PP_BBOX_F64
     const double ax = __shfl_up(qx, 1);
     const double ay = __shfl_up(qy, 1);
     const double inf = __builtin_inf();
@@ -120,6 +121,17 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const double bx1 = wave_max(has ? qx : -inf);
     const double by0 = wave_min(has ? qy : inf);
     const double by1 = wave_max(has ? qy : -inf);
+#else
+    // the chunk's bounding box in f32, rounded outward (DPP reductions): a box that contains the
+    // points selects a superset of the cells and items, and the exact test below decides
+    const double ax = shfl_up1_f64(qx);
+    const double ay = shfl_up1_f64(qy);
+    const float inff = __builtin_inff();
+    const float bx0 = wave_min_f32(has ? f32_below(qx) : inff);
+    const float bx1 = wave_max_f32(has ? f32_above(qx) : -inff);
+    const float by0 = wave_min_f32(has ? f32_below(qy) : inff);
+    const float by1 = wave_max_f32(has ? f32_above(qy) : -inff);
+#endif
     PP_STAMP(tq1);
 #ifdef PP_STAMPS
     if (ph) ph[0] += tq1 - tq0;
