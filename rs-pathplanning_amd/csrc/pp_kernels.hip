@@ -162,62 +162,94 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const float bxl = (float)bx0 - sc.cull_slack, bxh = (float)bx1 + sc.cull_slack;
     const float byl = (float)by0 - sc.cull_slack, byh = (float)by1 + sc.cull_slack;
     CULL_COUNT(0, 1);
+    // up to 64 items in parallel, one per lane (kk: its index in the item list, valid: a lane with
+    // an item): the cull disc against the chunk's bbox, then the survivors against every lane's
+    // segment, one at a time
+    auto items_reject = [&](bool valid, int kk) -> bool {
+        int dl = 0;
+        float4 Dl = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        bool ov = false;
+        if (valid) {
+            dl = items[kk];
+            Dl = d4[dl];
+            ov = Dl.x + Dl.z >= bxl && Dl.x - Dl.z <= bxh && Dl.y + Dl.z >= byl && Dl.y - Dl.z <= byh;
+        }
+        CULL_COUNT(1, __builtin_popcountll(__ballot(ov)));
+        for (uint64_t m = __ballot(ov); m; m &= m - 1) {
+            const int src = (int)__builtin_ctzll(m);
+            const int d = __builtin_amdgcn_readlane(dl, src);
+            float4 D;
+            D.x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.x), src));
+            D.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.y), src));
+            D.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.z), src));
+            D.w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.w), src));
+#ifdef PP_STAMPS
+            if (ph) ph[1] += 1;
+#endif
+            const float dxf = D.x - axf, dyf = D.y - ayf, thr = D.z + Lf;
+            bool near = seg_valid && dxf * dxf + dyf * dyf <= thr * thr;
+            if (!__any(near)) continue;
+            CULL_COUNT(2, 1);
+            if (!poly) {
+                // f32 closest point of the segment to the disc centre, decisive outside a band of
+                // +-eps around the radius (eps bounds the f32 rounding of the coordinates, the
+                // radius and this arithmetic): only the band needs the exact f64 test and its
+                // global loads
+                float t = 0.0f;
+                if (l2f > 0.0f)
+                    t = __builtin_fminf(__builtin_fmaxf((dxf * vxf + dyf * vyf) / l2f, 0.0f), 1.0f);
+                const float ex = dxf - t * vxf, ey = dyf - t * vyf;
+                const float e2 = ex * ex + ey * ey;
+                const float eps = sc.cull_slack + 1.0e-4f * (1.0f + thr);
+                const float lo = __builtin_fmaxf(D.w - eps, 0.0f), hi = D.w + eps;
+                if (__any(near && e2 < lo * lo)) return true;  // surely within the disc
+                near = near && e2 <= hi * hi;                  // else surely clear
+                if (!__any(near)) continue;
+            }
+            const bool hit =
+                near && (poly ? seg_hits_edge(ax, ay, qx, qy, sc.ex0[d], sc.ey0[d], sc.ex1[d],
+                                              sc.ey1[d], sc.h2)
+                              : seg_hits_disc(ax, ay, qx, qy, dcx[d], dcy[d], dr2[d]));
+            if (__any(hit)) return true;
+        }
+        return false;
+    };
+    const int ncx = cx1 - cx0 + 1, ncy = cy1 - cy0 + 1;
+    if (ncx <= 0 || ncy <= 0) return false;
+#ifndef PP_CELLS_SERIAL
+    if (ncx * ncy <= 64) {
+        // every cell of the box at once: lane c reads cell c's item range (one LDS round trip
+        // instead of one per cell), then the cells' item lists are dealt out to the lanes as one
+        // list (a cell's items follow the previous cell's), 64 at a time — the result is an OR
+        // over (item, segment) pairs, so the order does not matter
+        const int ncell = ncx * ncy;
+        int k0v = 0, cntv = 0;
+        if (lane < ncell) {
+            const int ry = lane / ncx;
+            const int cell = (cy0 + ry) * sc.gnx + cx0 + (lane - ry * ncx);
+            k0v = goff[cell];
+            cntv = goff[cell + 1] - k0v;
+        }
+        for (int mb = 0;; mb += 64) {
+            const int m = mb + lane;
+            int kk = -1, run = 0;
+            for (int c = 0; c < ncell; ++c) {
+                const int b = __builtin_amdgcn_readlane(k0v, c), n = __builtin_amdgcn_readlane(cntv, c);
+                if (m >= run && m < run + n) kk = b + (m - run);
+                run += n;
+            }
+            if (items_reject(kk >= 0, kk)) return true;
+            if (mb + 64 >= run) break;
+        }
+        return false;
+    }
+#endif
     for (int gy = cy0; gy <= cy1; ++gy) {
         for (int gx = cx0; gx <= cx1; ++gx) {
             const int cell = gy * sc.gnx + gx;
             const int k0 = goff[cell], k1 = goff[cell + 1];
-            // the cell's items in parallel, one per lane: the cull disc against the chunk's bbox;
-            // the survivors are then tested against every lane's segment, one at a time
-            for (int kb = k0; kb < k1; kb += 64) {
-                const int kk = kb + lane;
-                int dl = 0;
-                float4 Dl = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                bool ov = false;
-                if (kk < k1) {
-                    dl = items[kk];
-                    Dl = d4[dl];
-                    ov = Dl.x + Dl.z >= bxl && Dl.x - Dl.z <= bxh && Dl.y + Dl.z >= byl &&
-                         Dl.y - Dl.z <= byh;
-                }
-                CULL_COUNT(1, __builtin_popcountll(__ballot(ov)));
-                for (uint64_t m = __ballot(ov); m; m &= m - 1) {
-                    const int src = (int)__builtin_ctzll(m);
-                    const int d = __builtin_amdgcn_readlane(dl, src);
-                    float4 D;
-                    D.x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.x), src));
-                    D.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.y), src));
-                    D.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.z), src));
-                    D.w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.w), src));
-#ifdef PP_STAMPS
-                    if (ph) ph[1] += 1;
-#endif
-                    const float dxf = D.x - axf, dyf = D.y - ayf, thr = D.z + Lf;
-                    bool near = seg_valid && dxf * dxf + dyf * dyf <= thr * thr;
-                    if (!__any(near)) continue;
-                    CULL_COUNT(2, 1);
-                    if (!poly) {
-                        // f32 closest point of the segment to the disc centre, decisive outside
-                        // a band of +-eps around the radius (eps bounds the f32 rounding of the
-                        // coordinates, the radius and this arithmetic): only the band needs the
-                        // exact f64 test and its global loads
-                        float t = 0.0f;
-                        if (l2f > 0.0f)
-                            t = __builtin_fminf(__builtin_fmaxf((dxf * vxf + dyf * vyf) / l2f, 0.0f), 1.0f);
-                        const float ex = dxf - t * vxf, ey = dyf - t * vyf;
-                        const float e2 = ex * ex + ey * ey;
-                        const float eps = sc.cull_slack + 1.0e-4f * (1.0f + thr);
-                        const float lo = __builtin_fmaxf(D.w - eps, 0.0f), hi = D.w + eps;
-                        if (__any(near && e2 < lo * lo)) return true;  // surely within the disc
-                        near = near && e2 <= hi * hi;                  // else surely clear
-                        if (!__any(near)) continue;
-                    }
-                    const bool hit =
-                        near && (poly ? seg_hits_edge(ax, ay, qx, qy, sc.ex0[d], sc.ey0[d], sc.ex1[d],
-                                                      sc.ey1[d], sc.h2)
-                                      : seg_hits_disc(ax, ay, qx, qy, dcx[d], dcy[d], dr2[d]));
-                    if (__any(hit)) return true;
-                }
-            }
+            for (int kb = k0; kb < k1; kb += 64)
+                if (items_reject(kb + lane < k1, kb + lane)) return true;
         }
     }
     return false;
@@ -418,8 +450,8 @@ __device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
 #endif
         if (rej) return kReject;
         if (end_here) break;
-        carry_x = __shfl(qx, cnt);
-        carry_y = __shfl(qy, cnt);
+        carry_x = readlane_f64(qx, cnt);
+        carry_y = readlane_f64(qy, cnt);
         first = false;
     }
     if (1 + grid > r.n_point - 2) return kLiteral;
@@ -2260,8 +2292,8 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         npts += cnt + (junction_here ? 1 : 0);
         if (chunk_rejects<kLds>(sc, has, chk, has && lane >= 1, qx, qy)) return kReject;
         if (junction_here) break;
-        carry_x = __shfl(qx, 63);
-        carry_y = __shfl(qy, 63);
+        carry_x = readlane_f64(qx, 63);
+        carry_y = readlane_f64(qy, 63);
     }
     // no trailing zero left for the trim (dubins.rs:281-288): the literal path decides
     if (partial && 1 + grid > p->n_point - 2) return kLiteral;
@@ -2376,7 +2408,7 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
     for (;;) {
         int k = 0;
         if (lane == 0) k = atomicAdd(&s_next, 1);
-        const int t = (int)blockIdx.x + G * __builtin_amdgcn_readfirstlane(__shfl(k, 0));
+        const int t = (int)blockIdx.x + G * __builtin_amdgcn_readlane(k, 0);
         if (t >= total) break;
 #else
     const int per = (total + (int)gridDim.x - 1) / (int)gridDim.x;
@@ -2386,7 +2418,7 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
     for (;;) {
         int t = 0;
         if (lane == 0) t = atomicAdd(&s_next, 1);
-        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+        t = __builtin_amdgcn_readlane(t, 0);
         if (t >= t_end) break;
 #endif
 #endif
