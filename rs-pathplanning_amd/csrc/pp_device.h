@@ -468,6 +468,22 @@ __device__ inline double shfl_up1_f64(double v) {
     const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), 0x138, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
 }
+// lane k of every 8-lane group broadcast to the group's lanes (steer_prep's per-task lane
+// groups), on DPP: the quad broadcast of lane k % 4, then the half-row mirror for the other quad.
+// All 64 lanes must be active.
+template <int k>
+__device__ inline int grp8_bcast_i32(int v) {
+    static_assert(k >= 0 && k < 8, "lane of an 8-lane group");
+    constexpr int q = k & 3;
+    const int v1 = __builtin_amdgcn_update_dpp(v, v, q | (q << 2) | (q << 4) | (q << 6), 0xF, 0xF, false);
+    const int v2 = __builtin_amdgcn_update_dpp(v1, v1, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    const bool low = (threadIdx.x & 4) == 0;
+    return (k < 4) == low ? v1 : v2;
+}
+template <int k>
+__device__ inline double grp8_bcast_f64(double v) {
+    return __hiloint2double(grp8_bcast_i32<k>(__double2hiint(v)), grp8_bcast_i32<k>(__double2loint(v)));
+}
 // f32 bounds of an f64 value: lo <= v <= hi (the conversion rounds to nearest; a rounded-past
 // value moves out by far more than its rounding error)
 __device__ inline float f32_below(double v) {

@@ -1922,6 +1922,7 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & (kPrepLanes - 1), g0 = lane & ~(kPrepLanes - 1);
     constexpr int TPW = 64 / kPrepLanes;  // tasks per wave in phase A
+    static_assert(kPrepLanes == 8, "the per-task broadcasts are grp8_bcast (8-lane groups)");
     const double step = sc.step_size;
     const double c = 1.0 / sc.turn_radius;
     constexpr int TPB = kPrepThreads / 64 * TPW;  // tasks per workgroup
@@ -1969,8 +1970,9 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
         // lanes 0/1: sin(alpha), sin(beta); lanes 0/1/2: cos(alpha), cos(beta), cos(alpha - beta)
         const double s_in = sin(r == 0 ? alpha : beta);
         const double c_in = cos(r == 0 ? alpha : (r == 1 ? beta : alpha - beta));
-        const double sa = __shfl(s_in, g0), sb = __shfl(s_in, g0 + 1);
-        const double ca = __shfl(c_in, g0), cb = __shfl(c_in, g0 + 1), c_ab = __shfl(c_in, g0 + 2);
+        const double sa = grp8_bcast_f64<0>(s_in), sb = grp8_bcast_f64<1>(s_in);
+        const double ca = grp8_bcast_f64<0>(c_in), cb = grp8_bcast_f64<1>(c_in),
+                     c_ab = grp8_bcast_f64<2>(c_in);
         // lane r < 6 evaluates word r of ALL_PLANNERS (dubins.rs:27-153, 291)
         const double dd2 = d * d;
         double ya = 0.0, xa = 1.0, psq = -1.0, tmpc = 2.0;
@@ -2036,12 +2038,16 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
         // first strict minimum in ALL_PLANNERS order (dubins.rs:351-360)
         double bc = __builtin_inf();
         int bw = -1;
+        const double wc[6] = {grp8_bcast_f64<0>(wcost), grp8_bcast_f64<1>(wcost),
+                              grp8_bcast_f64<2>(wcost), grp8_bcast_f64<3>(wcost),
+                              grp8_bcast_f64<4>(wcost), grp8_bcast_f64<5>(wcost)};
+        const int wk[6] = {grp8_bcast_i32<0>((int)wok), grp8_bcast_i32<1>((int)wok),
+                           grp8_bcast_i32<2>((int)wok), grp8_bcast_i32<3>((int)wok),
+                           grp8_bcast_i32<4>((int)wok), grp8_bcast_i32<5>((int)wok)};
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
-            const double ck = __shfl(wcost, g0 + k);
-            const int okk = __shfl((int)wok, g0 + k);
-            if (okk && bc > ck) {
-                bc = ck;
+            if (wk[k] && bc > wc[k]) {
+                bc = wc[k];
                 bw = k;
             }
         }
@@ -2071,11 +2077,11 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
             arg = -yaw;
         }
         const double sv = sin(arg), cv = cos(arg);
-        const double ca0 = __shfl(cv, g0), ca1 = __shfl(cv, g0 + 1), ca2 = __shfl(cv, g0 + 2);
-        const double sa0 = __shfl(sv, g0), sa1 = __shfl(sv, g0 + 1), sa2 = __shfl(sv, g0 + 2);
-        const double sl0 = __shfl(sv, g0 + 3), sl1 = __shfl(sv, g0 + 4), sl2 = __shfl(sv, g0 + 5);
-        const double cl0 = __shfl(cv, g0 + 3), cl1 = __shfl(cv, g0 + 4), cl2 = __shfl(cv, g0 + 5);
-        const double cw = __shfl(cv, g0 + 6), sw = __shfl(sv, g0 + 6);
+        const double ca0 = grp8_bcast_f64<0>(cv), ca1 = grp8_bcast_f64<1>(cv), ca2 = grp8_bcast_f64<2>(cv);
+        const double sa0 = grp8_bcast_f64<0>(sv), sa1 = grp8_bcast_f64<1>(sv), sa2 = grp8_bcast_f64<2>(sv);
+        const double sl0 = grp8_bcast_f64<3>(sv), sl1 = grp8_bcast_f64<4>(sv), sl2 = grp8_bcast_f64<5>(sv);
+        const double cl0 = grp8_bcast_f64<3>(cv), cl1 = grp8_bcast_f64<4>(cv), cl2 = grp8_bcast_f64<5>(cv);
+        const double cw = grp8_bcast_f64<6>(cv), sw = grp8_bcast_f64<6>(sv);
         const Pt O1 = seg_end(m0, L0, c, 0.0, 0.0, ca0, sa0, sl0, cl0);
         const Pt O2 = seg_end(m1, L1, c, O1.x, O1.y, ca1, sa1, sl1, cl1);
         const Pt E = seg_end(m2, L2, c, O2.x, O2.y, ca2, sa2, sl2, cl2);
