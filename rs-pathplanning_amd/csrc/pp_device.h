@@ -484,6 +484,54 @@ template <int k>
 __device__ inline double grp8_bcast_f64(double v) {
     return __hiloint2double(grp8_bcast_i32<k>(__double2hiint(v)), grp8_bcast_i32<k>(__double2loint(v)));
 }
+// Butterfly steps without LDS round trips (all 64 lanes active): dpp_pair<kCtrl> gives every lane
+// its partner's 32-bit value under a DPP pattern that pairs disjoint lane sets (quad_perm [1,0,3,2]
+// and [2,3,0,1], row_half_mirror, row_mirror); swap16 / swap32 (gfx950 v_permlane16/32_swap) give
+// every lane the pair {v[l], v[l ^ 16]} / {v[l], v[l ^ 32]} (scripts/micro/permlane_check.hip).
+template <int kCtrl>
+__device__ inline int dpp_pair(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, kCtrl, 0xF, 0xF, false);
+}
+struct LanePair {
+    int a, b;
+};
+__device__ inline LanePair swap16(int v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return {(int)r[0], (int)r[1]};
+}
+__device__ inline LanePair swap32(int v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return {(int)r[0], (int)r[1]};
+}
+// argmin over (d, i) in (d, index) order (ties: lowest index), whole wave; every lane ends with it
+__device__ inline void argmin_step(double& d, int& i, double od, int oi) {
+    if (od < d || (od == d && oi < i)) {
+        d = od;
+        i = oi;
+    }
+}
+template <int kCtrl>
+__device__ inline void argmin_dpp(double& d, int& i) {
+    const double od = __hiloint2double(dpp_pair<kCtrl>(__double2hiint(d)), dpp_pair<kCtrl>(__double2loint(d)));
+    argmin_step(d, i, od, dpp_pair<kCtrl>(i));
+}
+template <bool k32>
+__device__ inline void argmin_swap(double& d, int& i) {
+    const LanePair h = k32 ? swap32(__double2hiint(d)) : swap16(__double2hiint(d));
+    const LanePair l = k32 ? swap32(__double2loint(d)) : swap16(__double2loint(d));
+    const LanePair x = k32 ? swap32(i) : swap16(i);
+    d = __hiloint2double(h.a, l.a);
+    i = x.a;
+    argmin_step(d, i, __hiloint2double(h.b, l.b), x.b);
+}
+__device__ inline void wave_argmin(double& d, int& i) {
+    argmin_dpp<0xB1>(d, i);
+    argmin_dpp<0x4E>(d, i);
+    argmin_dpp<0x141>(d, i);
+    argmin_dpp<0x140>(d, i);
+    argmin_swap<false>(d, i);
+    argmin_swap<true>(d, i);
+}
 // f32 bounds of an f64 value: lo <= v <= hi (the conversion rounds to nearest; a rounded-past
 // value moves out by far more than its rounding error)
 __device__ inline float f32_below(double v) {

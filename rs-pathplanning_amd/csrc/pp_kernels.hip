@@ -1506,8 +1506,30 @@ struct PairGrid {
     float slack;         // f32 prefilter margin for the coordinates' magnitude
 };
 
-__device__ inline Top2 shfl_xor_top2(Top2 t, int m) {
-    return Top2{__shfl_xor(t.b, m), __shfl_xor(t.s, m), __shfl_xor(t.i, m)};
+// the wave's top-2 (every lane ends with it): butterfly steps that merge disjoint lane sets, on
+// DPP and the gfx950 lane swaps (merge_top2 is not idempotent: a set merged with itself would
+// report its best as its second)
+template <int kCtrl>
+__device__ inline Top2 top2_dpp(Top2 t) {
+    return Top2{__builtin_bit_cast(float, dpp_pair<kCtrl>(__builtin_bit_cast(int, t.b))),
+                __builtin_bit_cast(float, dpp_pair<kCtrl>(__builtin_bit_cast(int, t.s))),
+                dpp_pair<kCtrl>(t.i)};
+}
+template <bool k32>
+__device__ inline Top2 top2_swap(Top2 t) {
+    const LanePair b = k32 ? swap32(__builtin_bit_cast(int, t.b)) : swap16(__builtin_bit_cast(int, t.b));
+    const LanePair s = k32 ? swap32(__builtin_bit_cast(int, t.s)) : swap16(__builtin_bit_cast(int, t.s));
+    const LanePair i = k32 ? swap32(t.i) : swap16(t.i);
+    return merge_top2(Top2{__builtin_bit_cast(float, b.a), __builtin_bit_cast(float, s.a), i.a},
+                      Top2{__builtin_bit_cast(float, b.b), __builtin_bit_cast(float, s.b), i.b});
+}
+__device__ inline Top2 wave_top2(Top2 t) {
+    t = merge_top2(t, top2_dpp<0xB1>(t));   // quad_perm [1,0,3,2]
+    t = merge_top2(t, top2_dpp<0x4E>(t));   // quad_perm [2,3,0,1]
+    t = merge_top2(t, top2_dpp<0x141>(t));  // row_half_mirror
+    t = merge_top2(t, top2_dpp<0x140>(t));  // row_mirror
+    t = top2_swap<false>(t);
+    return top2_swap<true>(t);
 }
 
 // 8 waves per SIMD (<= 64 VGPRs): two 1024-thread workgroups per CU, so the extra sampling
@@ -1605,8 +1627,7 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
             const Top2 c{d, __builtin_inff(), ns + k};
             t = merge_top2(t, c);
         }
-#pragma unroll
-        for (int m = 1; m < 64; m <<= 1) t = merge_top2(t, shfl_xor_top2(t, m));
+        t = wave_top2(t);
         bool flag = t.i < 0 || !(t.b < __builtin_inff());
         double cthr = __builtin_inf();  // near-tie: the chunks with pbest <= cthr are rescanned
         if (!flag) {
@@ -1667,9 +1688,7 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
                     argmin_pair(bd, bi, dx * dx + dy * dy, ci);
                 }
             }
-#pragma unroll
-            for (int m = 32; m > 0; m >>= 1)
-                argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+            wave_argmin(bd, bi);
             if (D > 0 && !__any(need)) {
                 const double U = sqrt(bd), tu = 16.0 * eps_coord + 4.0e-6 * (U + 1.0);
                 const double lim = (U + tu) * (U + tu);
@@ -1680,9 +1699,7 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
                         argmin_pair(bd, bi, dx * dx + dy * dy, ns + k);
                     }
                 }
-#pragma unroll
-                for (int m = 32; m > 0; m >>= 1)
-                    argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+                wave_argmin(bd, bi);
             }
             if (lane == 0) atomicAdd(&st->flag_count, 1);  // statistics (nn_flagged)
             if (__any(need) || bi == 0x7fffffff) {
@@ -1735,8 +1752,7 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
             const double dx = xq - X[k], dy = yq - Y[k];
             argmin_pair(bd, bi, dx * dx + dy * dy, k);
         }
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+        wave_argmin(bd, bi);
         if (lane == 0) {
             s_rd[wave] = bd;
             s_ri[wave] = bi;
@@ -3476,8 +3492,14 @@ __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx
                 bi = i;
             }
         }
-        for (int m = K; m < 64; m <<= 1)  // the G lanes of slot k
-            argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+        for (int m = K; m < 64; m <<= 1) {  // the G lanes of slot k
+            if (m == 16)
+                argmin_swap<false>(bd, bi);
+            else if (m == 32)
+                argmin_swap<true>(bd, bi);
+            else
+                argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+        }
         if (g == 0) {
             const int t = q * K + k;
             if (!live) {
@@ -3734,8 +3756,7 @@ __global__ __launch_bounds__(256) void star_sample_kernel(StarDev sd, double min
                 bi = i;
             }
         }
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+        wave_argmin(bd, bi);
         const double nx = X[bi], ny = Y[bi];
         if (sd.eta > 0.0 && bd > sd.eta * sd.eta) {  // Steer(x_nearest, x_rand)
             const double f = sd.eta / sqrt(bd);
@@ -3858,9 +3879,7 @@ __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __
                         bi = i;
                     }
                 }
-#pragma unroll
-                for (int m = 32; m > 0; m >>= 1)
-                    argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+                wave_argmin(bd, bi);
                 pd = bd;
                 pi = bi;
                 if (lane == r) mine = bi;
@@ -3978,8 +3997,7 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
         // choose parent: the first strict minimum of cost(node) + edge cost in candidate order
         double c = feas ? sd.cost[row + node] + e : __builtin_inf();
         int bl = lane;
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) argmin_pair(c, bl, __shfl_xor(c, m), __shfl_xor(bl, m));
+        wave_argmin(c, bl);
         const int best = __shfl(node, bl);
         const double yb = __shfl(yaw, bl), eb = __shfl(e, bl), cb = c;
         if (lane == 0) {
