@@ -532,6 +532,22 @@ __device__ inline void wave_argmin(double& d, int& i) {
     argmin_swap<false>(d, i);
     argmin_swap<true>(d, i);
 }
+// inclusive prefix sum over the wave's 64 lanes on DPP (all lanes active): within each row the
+// three row shifts then the bank-masked shifts by 4 and 8, then the row broadcasts 15 and 31
+template <int kCtrl, int kRowMask, int kBankMask>
+__device__ inline int dpp_zero(int v) {  // lanes without a source (or masked off) read 0
+    return __builtin_amdgcn_update_dpp(0, v, kCtrl, kRowMask, kBankMask, true);
+}
+__device__ inline int wave_incl_scan(int v) {
+    int x = v + dpp_zero<0x111, 0xF, 0xF>(v);  // row_shr:1
+    x += dpp_zero<0x112, 0xF, 0xF>(v);         // row_shr:2
+    x += dpp_zero<0x113, 0xF, 0xF>(v);         // row_shr:3
+    x += dpp_zero<0x114, 0xF, 0xE>(x);         // row_shr:4, banks 1-3
+    x += dpp_zero<0x118, 0xF, 0xC>(x);         // row_shr:8, banks 2-3
+    x += dpp_zero<0x142, 0xA, 0xF>(x);         // row_bcast:15 into rows 1, 3
+    x += dpp_zero<0x143, 0xC, 0xF>(x);         // row_bcast:31 into rows 2, 3
+    return x;
+}
 // f32 bounds of an f64 value: lo <= v <= hi (the conversion rounds to nearest; a rounded-past
 // value moves out by far more than its rounding error)
 __device__ inline float f32_below(double v) {

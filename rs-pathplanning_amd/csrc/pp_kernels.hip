@@ -803,12 +803,7 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
             v[u] = s_hist[4 * tid + u];
             sum += v[u];
         }
-        int x = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o);
-            if (tid >= o) x += y;
-        }
+        const int x = wave_incl_scan(sum);
         int base = x - sum;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -1840,15 +1835,7 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
         const int keep = min(cnt, kCandCap);
         if (jin) cand_cnt[j] = cnt;
         // one reservation per workgroup for the entries and for the queue of pending samples
-        int ex = keep, pc = cnt > 0 ? 1 : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int ye = __shfl_up(ex, o), yp = __shfl_up(pc, o);
-            if (lane >= o) {
-                ex += ye;
-                pc += yp;
-            }
-        }
+        const int ex = wave_incl_scan(keep), pc = wave_incl_scan(cnt > 0 ? 1 : 0);
         const int eo = ex - keep, po = pc - (cnt > 0 ? 1 : 0);
         if (lane == 63) {
             s_pbase = ex > 0 ? atomicAdd(&st->ncomp, ex) : 0;
@@ -2893,12 +2880,7 @@ __device__ __attribute__((always_inline)) inline void commit_role(
     int local = 0;
 #pragma unroll
     for (int u = 0; u < PER; ++u) local += v[u] & 1;
-    int x = local;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
+    const int x = wave_incl_scan(local);
     if (lane == 63) s_wave[wave] = x;
     __syncthreads();
     int base = 0, total = 0;
@@ -3833,13 +3815,8 @@ __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __
             const double T = readlane_f64(bitonic64(lmin, lane).d, k - 1);
             int c = 0;
             for (int i = lane; i < n; i += 64) c += cache[i] <= T;
-            int off = c;  // inclusive prefix over the lanes
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int v = __shfl_up(off, o);
-                if (lane >= o) off += v;
-            }
-            const int C = __shfl(off, 63);
+            int off = wave_incl_scan(c);  // inclusive prefix over the lanes
+            const int C = __builtin_amdgcn_readlane(off, 63);
             if (C <= 64) {  // gather them into one (d2, index) pair per lane and sort the wave
                 off -= c;
                 for (int i = lane; i < n; i += 64)

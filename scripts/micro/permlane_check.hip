@@ -1,9 +1,10 @@
 // Micro-check (GPU): the gfx950 lane swaps used by the wave reductions.  For every lane l,
 // {r0, r1} of v_permlane16_swap(v, v) must be {v[l], v[l ^ 16]} and of v_permlane32_swap(v, v)
-// {v[l], v[l ^ 32]}; and the DPP quad / half-row-mirror / row-mirror steps must pair disjoint
-// lane sets.  Build: hipcc --offload-arch=gfx950 -O2 -o permlane_check permlane_check.hip
+// {v[l], v[l ^ 32]}; wave_incl_scan (pp_device.h, DPP) must equal the serial prefix sums.  Build: hipcc --offload-arch=gfx950 -O2 -o permlane_check permlane_check.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include "../../rs-pathplanning_amd/csrc/pp_device.h"
+__global__ void scan_k(const int* in, int* out) { out[threadIdx.x] = ppamd::wave_incl_scan(in[threadIdx.x]); }
 __global__ void k(const int* in, int* out) {
     const int l = threadIdx.x;
     const int v = in[l];
@@ -34,5 +35,16 @@ int main() {
     }
     printf("permlane16_swap pairs {l, l^16}: %s; permlane32_swap pairs {l, l^32}: %s\n",
            bad16 ? "NO" : "yes", bad32 ? "NO" : "yes");
-    return bad16 || bad32;
+    int bads = 0;
+    for (int rep = 0; rep < 100; ++rep) {
+        unsigned r = 12345u + 7919u * rep;
+        for (int i = 0; i < 64; ++i) { r = r * 1103515245u + 12345u; h[i] = (int)((r >> 16) % 1000) - (rep % 2 ? 0 : 300); }
+        (void)hipMemcpy(din, h, sizeof h, hipMemcpyHostToDevice);
+        scan_k<<<1, 64>>>(din, dout);
+        (void)hipMemcpy(o, dout, 64 * sizeof(int), hipMemcpyDeviceToHost);
+        int acc = 0;
+        for (int i = 0; i < 64; ++i) { acc += h[i]; bads += o[i] != acc; }
+    }
+    printf("wave_incl_scan (DPP): %d of 6400 prefix sums differ\n", bads);
+    return bad16 || bad32 || bads;
 }
