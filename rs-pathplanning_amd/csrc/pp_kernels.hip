@@ -1851,6 +1851,19 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
     }
 #ifdef PP_STAMPS_FIN
     FIN_STAMP(tf5);
+#ifdef PP_STAMPS_FIN_PHASES
+    if (tid == 0) {  // phase sums over the workgroups: [0] staging, [1] per-sample NN, [2] brute
+                     // force, [3] pair search, [4] candidate append, [5] workgroups, [6] max total
+        unsigned long long* sp = reinterpret_cast<unsigned long long*>(st->stamps);
+        atomicAdd(&sp[0], (unsigned long long)(tf1 - tf0));
+        atomicAdd(&sp[1], (unsigned long long)(tf2 - tf1));
+        atomicAdd(&sp[2], (unsigned long long)(tf3 - tf2));
+        atomicAdd(&sp[3], (unsigned long long)(tf4 - tf3));
+        atomicAdd(&sp[4], (unsigned long long)(tf5 - tf4));
+        atomicAdd(&sp[5], 1ull);
+        atomicMax(&sp[6], (unsigned long long)(tf5 - tf0));
+    }
+#else
     if (tid == 0) {  // [0..2] workgroups without a near-tie brute force: sum, count, max;
                      // [3..5] with one; [6] their brute-force time, [7] all pair-search time
         const int o = s_fmask ? 3 : 0;
@@ -1860,6 +1873,7 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
         if (s_fmask) atomicAdd((unsigned long long*)&st->stamps[6], (unsigned long long)(tf3 - tf2));
         atomicAdd((unsigned long long*)&st->stamps[7], (unsigned long long)(tf4 - tf3));
     }
+#endif
 #endif
 }
 

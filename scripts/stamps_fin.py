@@ -11,7 +11,7 @@ raw = scenes.field512()
 sx, sy, syaw = raw["start"]; gx, gy, gyaw = raw["goal"]
 p = rrt.RRT((sx, sy), syaw, (gx, gy), gyaw, 0, raw["step_size"], rrt.Space.from_raw(raw), seed=42,
             capacity=1 << 18)
-for target in (10000, 100000):
+for target in ((100000,) if os.environ.get("PHASES") else (10000, 100000)):
     while p.tree_size() < target:
         p.extend(4096)
     p.reset_stats()
@@ -22,3 +22,10 @@ for target in (10000, 100000):
           "(avg %.2f us, max %.2f, of which brute force %.2f) | pair search avg %.2f us"
           % (s[1] / 20, s[0] / n0 / 100, s[2] / 100, s[4] / 20, s[3] / n1 / 100, s[5] / 100,
              s[6] / n1 / 100, s[7] / (s[1] + s[4]) / 100))
+if os.environ.get("PHASES"):  # a -DPP_STAMPS_FIN -DPP_STAMPS_FIN_PHASES build
+    p.reset_stats()
+    p.extend(20 * 4096)
+    s = p.stats()["stamps"]
+    n = max(s[5], 1)
+    print("phases per workgroup (us): staging %.2f, NN %.2f, brute force %.2f, pair search %.2f, "
+          "append %.2f; max workgroup %.2f" % tuple([v / n / 100 for v in s[:5]] + [s[6] / 100]))
