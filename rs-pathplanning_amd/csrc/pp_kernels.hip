@@ -2224,27 +2224,51 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                 const int kk = lane - pos;
                 const double aL = fabs(Ls);
                 const int umax = 63 - pos;
-                double w = gpd;
-                if (lane == 0) gs[0] = w;
-                int u = 0;
-                bool ended = !(fabs(w) <= aL);
-                while (!ended && u < umax) {
-                    double t4[4];
-#pragma unroll
-                    for (int z = 0; z < 4; ++z) {
-                        w += gdd;
-                        t4[z] = w;
-                    }
-                    if (lane == 0) {
-#pragma unroll
-                        for (int z = 0; z < 4; ++z) gs[u + 1 + z] = t4[z];
-                    }
-                    u += 4;
-                    ended = !(fabs(w) <= aL);
+                int u = umax;
+                double v = gpd;
+                // Closed form first: while the values keep w0's sign and exponent (one ulp u),
+                // fl(w + d) = w + RN_u(d), so when the first two steps agree (w1 - w0 == w2 - w1
+                // = delta; a tie-to-even would alternate them) w_k = w0 + k delta exactly — one
+                // fma per lane, representable, so exact.  Checked over every value up to the
+                // first one past |L|; any other pass (a binade or sign crossing inside the
+                // chunk) takes the serial chain.  tests/test_walk_generator.py restates both.
+                const double w1 = gpd + gdd, w2 = w1 + gdd;
+#ifdef PP_GEN_CHAIN
+                bool cf = false;  // (diagnostic: the serial chain for every pass)
+#else
+                bool cf = (w1 - gpd) == (w2 - w1);
+#endif
+                if (cf) {
+                    const double vc = __builtin_fma((double)(kk > 0 ? kk : 0), w1 - gpd, gpd);
+                    const uint64_t fm = __ballot(kk >= 0 && !(fabs(vc) <= aL));
+                    const int fl = fm ? (int)__builtin_ctzll(fm) : 63;
+                    cf = __ballot(kk >= 0 && lane <= fl &&
+                                  (__double2hiint(vc) >> 20) != (__double2hiint(gpd) >> 20)) == 0;
+                    if (kk >= 0) v = vc;
                 }
-                u = min(u, umax);
-                __builtin_amdgcn_wave_barrier();
-                const double v = (kk >= 0 && kk <= u) ? gs[kk] : gpd;
+                if (!cf) {
+                    double w = gpd;
+                    if (lane == 0) gs[0] = w;
+                    u = 0;
+                    bool ended = !(fabs(w) <= aL);
+                    while (!ended && u < umax) {
+                        double t4[4];
+#pragma unroll
+                        for (int z = 0; z < 4; ++z) {
+                            w += gdd;
+                            t4[z] = w;
+                        }
+                        if (lane == 0) {
+#pragma unroll
+                            for (int z = 0; z < 4; ++z) gs[u + 1 + z] = t4[z];
+                        }
+                        u += 4;
+                        ended = !(fabs(w) <= aL);
+                    }
+                    u = min(u, umax);
+                    __builtin_amdgcn_wave_barrier();
+                    v = (kk >= 0 && kk <= u) ? gs[kk] : gpd;
+                }
                 const uint64_t bad = __ballot(lane >= pos && (kk > u || !(fabs(v) <= aL)));
                 const int m = bad ? (int)__builtin_ctzll(bad) : 64;
                 if (lane >= pos && lane < m) {
