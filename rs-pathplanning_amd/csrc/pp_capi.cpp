@@ -193,6 +193,7 @@ struct pp_ctx {
     // ---- RRT* query batch (BASELINE config 5, build-defined: DESIGN.md §3.7)
     bool has_star = false;
     int star_Q = 0, star_cap = 0, star_kfix = 0;
+    int star_nsub = 1;  // sub-batches of the current RRT* batch (fixed at pp_star_new)
     int64_t star_max_iter = 0;
     double star_step = 0.1, star_eta = 0.0;
     DBuf<double> sr_x, sr_y, sr_yaw, sr_cost, sr_elen, sr_px, sr_py, sr_cb;
@@ -520,6 +521,12 @@ MqArgs mq_args(pp_ctx* c) {
     a.lit_locks = c->lit_locks.p;
     a.err = c->mq_err.p;
     a.wg_points = c->prof_points();
+    // PP_MQ_FUSE=0: a separate mq_sample_nn launch every step (the A/B of the fused insert)
+    static const bool fuse = [] {
+        const char* e = std::getenv("PP_MQ_FUSE");
+        return !(e && e[0] == '0');
+    }();
+    a.fuse_nn = fuse;
     return a;
 }
 
@@ -1792,9 +1799,10 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
             }
             if (nsub > 1) {  // interleaved, so every stream always holds work
                 for (int k = 0; k < chunk; ++k)
-                    for (int i = 0; i < nsub; ++i) PP_HIP(launch_mq_steps(sst[i], sub[i], 1));
+                    for (int i = 0; i < nsub; ++i)
+                        PP_HIP(launch_mq_steps(sst[i], sub[i], 1, done + k > 0, done + k + 1 < steps));
             } else {
-                PP_HIP(launch_mq_steps(ctx->stream, a, chunk));
+                PP_HIP(launch_mq_steps(ctx->stream, a, chunk, done > 0, done + chunk < steps));
             }
             if (ctx->prof) {  // events: around mq_sample_nn and around steer_walk
                 PP_HIP(hipStreamSynchronize(ctx->stream));
@@ -1945,6 +1953,7 @@ int pp_star_new(pp_ctx* ctx, int q, const double* starts, const uint64_t* seeds,
     DevState ds[3 * (1 + kMaxSub)] = {};
     ds[0].W = q;  // round A of the whole batch; sub-batch s: 3 * (1 + s)
     const int nsub = mq_nsub(q, 3);
+    ctx->star_nsub = nsub;  // the sub-batch DevStates are written for this split
     for (int sb = 0; sb < nsub; ++sb)
         ds[3 * (1 + sb)].W = (int)((int64_t)q * (sb + 1) / nsub - (int64_t)q * sb / nsub);
     PP_HIP(hipMemcpyAsync(ctx->sr_state.p, ds, sizeof ds, hipMemcpyHostToDevice, st));
@@ -1968,7 +1977,7 @@ int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t*
     PP_HIP(launch_mq_target(ctx->stream, a.sd.mq, n_steps, ctx->sr_target.p));
     const int64_t steps = std::min<int64_t>(n_steps, ctx->star_max_iter);  // one iteration a step
     // sub-batches on their own streams, as pp_batch_extend (one stream while profiling)
-    const int nsub = ctx->prof ? 1 : mq_nsub(ctx->star_Q, 3);
+    const int nsub = ctx->prof ? 1 : ctx->star_nsub;
     StarArgs sub[kMaxSub];
     hipStream_t sst[kMaxSub] = {ctx->stream};
     for (int i = 0; i < nsub && nsub > 1; ++i) {
