@@ -207,8 +207,11 @@ def provenance(args):
                          "(--allow-variant-lib for experiments)")
     with open(_ffi.LIB_PATH, "rb") as f:
         sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    # the library's run-time knobs (stream splits, A/B switches): a line taken with any set says so
+    knobs = {k: v for k, v in sorted(os.environ.items()) if k.startswith("PP_")}
     return {"lib": os.path.relpath(_ffi.LIB_PATH, ROOT), "lib_sha256_16": sha,
-            "hipcc_flags": " ".join(g.HIPCC_FLAGS), "variant": bool(os.environ.get("PP_AMD_LIB"))}
+            "hipcc_flags": " ".join(g.HIPCC_FLAGS), "variant": bool(os.environ.get("PP_AMD_LIB")),
+            "env_knobs": knobs}
 
 
 def load_profile(name):

@@ -521,12 +521,6 @@ MqArgs mq_args(pp_ctx* c) {
     a.lit_locks = c->lit_locks.p;
     a.err = c->mq_err.p;
     a.wg_points = c->prof_points();
-    // PP_MQ_FUSE=0: a separate mq_sample_nn launch every step (the A/B of the fused insert)
-    static const bool fuse = [] {
-        const char* e = std::getenv("PP_MQ_FUSE");
-        return !(e && e[0] == '0');
-    }();
-    a.fuse_nn = fuse;
     return a;
 }
 
@@ -1799,10 +1793,9 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
             }
             if (nsub > 1) {  // interleaved, so every stream always holds work
                 for (int k = 0; k < chunk; ++k)
-                    for (int i = 0; i < nsub; ++i)
-                        PP_HIP(launch_mq_steps(sst[i], sub[i], 1, done + k > 0, done + k + 1 < steps));
+                    for (int i = 0; i < nsub; ++i) PP_HIP(launch_mq_steps(sst[i], sub[i], 1));
             } else {
-                PP_HIP(launch_mq_steps(ctx->stream, a, chunk, done > 0, done + chunk < steps));
+                PP_HIP(launch_mq_steps(ctx->stream, a, chunk));
             }
             if (ctx->prof) {  // events: around mq_sample_nn and around steer_walk
                 PP_HIP(hipStreamSynchronize(ctx->stream));
