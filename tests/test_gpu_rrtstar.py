@@ -171,3 +171,22 @@ def test_star_large_tree_uncached_knn(pkg, oracle_mod, ctx):
     exp, erw = _oracle(oracle_mod, raw, raw["start"], 21, 4000, 0, 0.0)
     _assert_same(b.tree(0), exp)
     assert b.state()[3][0] == erw
+
+
+def test_star_split_fixed_at_new(pkg, oracle_mod, ctx, monkeypatch):
+    """the sub-batch split (PP_BATCH_STREAMS) is read at pp_star_new only: changing it before
+    pp_star_extend must not leave a sub-batch without its task count"""
+    from pathplanning_amd import scenes
+
+    raw = scenes.bench6_open()
+    starts, _, seeds = scenes.config3_queries(raw, 0, 300)
+    monkeypatch.setenv("PP_BATCH_STREAMS", "2")
+    b = _batch(pkg, raw, starts, seeds, 60, 0, 0.0, ctx=ctx)
+    monkeypatch.setenv("PP_BATCH_STREAMS", "4")
+    b.extend(60)
+    n, it, _, rw = b.state()
+    assert (it == 60).all()
+    for q in (0, 149, 150, 299):
+        exp, erw = _oracle(oracle_mod, raw, tuple(starts[q]), int(seeds[q]), 60, 0, 0.0)
+        _assert_same(b.tree(q), exp)
+        assert rw[q] == erw
