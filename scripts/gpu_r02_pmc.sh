@@ -40,6 +40,9 @@ if [[ " ${WLS:-config2 config4 config3 config5} " == *" config4 "* ]]; then
   job c4_win_F config4 window_kernel FETCH_SIZE
   job c4_win_W config4 window_kernel WRITE_SIZE
   job c4_walk_A config4 steer_walk $SQA
+  job c4_walk_B config4 steer_walk $SQB
+  job c4_walk_F config4 steer_walk FETCH_SIZE
+  job c4_walk_W config4 steer_walk WRITE_SIZE
 fi
 if [[ " ${WLS:-config2 config4 config3 config5} " == *" config3 "* ]]; then
   job c3_walk_A config3 steer_walk $SQA
