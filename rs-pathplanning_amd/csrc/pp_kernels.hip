@@ -4066,6 +4066,7 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
     }
 }
 
+constexpr int kRwReg = 16;  // rewire propagation: node rows per lane and batch of gathers
 __global__ __launch_bounds__(256) void star_rewire_kernel(
     StarDev sd, SceneDev sc, const SteerTask* __restrict__ tasksC,
     const StarTaskExt* __restrict__ extC, const int* __restrict__ statusC,
@@ -4120,19 +4121,36 @@ __global__ __launch_bounds__(256) void star_rewire_kernel(
                 mark[m] = s;
             }
             ++rw;
-            __threadfence();
+            // this wave alone reads and writes query q's rows in this kernel, so its lanes
+            // exchange them through the CU's own cache: a workgroup-scope fence (the stores
+            // complete) orders them, with no L2 writeback or L1 invalidation per pass
+            __threadfence_block();
             // the subtree of m, level by level: a node's parent is final one pass earlier
+            // (lane l holds nodes l, l + 64, ...; a pass loads kRwReg rows of parents per lane,
+            // then issues all of their mark gathers at once, instead of one dependent pair per
+            // 64 nodes)
             for (;;) {
                 bool any = false;
-                for (int j = lane; j < n; j += 64) {
-                    const int pj = par[j];
-                    if (pj >= 0 && mark[pj] == s) {
-                        cost[j] = cost[pj] + elen[j];
-                        mark[j] = s + 1;
-                        any = true;
+                for (int j0 = 0; j0 < n; j0 += 64 * kRwReg) {
+                    int pr[kRwReg], mk[kRwReg];
+#pragma unroll
+                    for (int r = 0; r < kRwReg; ++r) {
+                        const int j = j0 + lane + 64 * r;
+                        pr[r] = j < n ? par[j] : -1;
+                    }
+#pragma unroll
+                    for (int r = 0; r < kRwReg; ++r) mk[r] = pr[r] >= 0 ? mark[pr[r]] : 0;
+#pragma unroll
+                    for (int r = 0; r < kRwReg; ++r) {
+                        if (pr[r] >= 0 && mk[r] == s) {
+                            const int j = j0 + lane + 64 * r;
+                            cost[j] = cost[pr[r]] + elen[j];
+                            mark[j] = s + 1;
+                            any = true;
+                        }
                     }
                 }
-                __threadfence();
+                __threadfence_block();
                 ++s;
                 if (!__ballot(any)) break;
             }
