@@ -3810,132 +3810,158 @@ __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double* cand_d = s_cd[wave];
     int* cand_i = s_ci[wave];
-    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     const MqDev& mq = sd.mq;
     double* cache = s_d2[wave];
-    for (int q = gw; q < mq.Q; q += nw) {
-        const int p = sd.pn[q];
-        if (p < 0) continue;
-        const int n = mq.n[q];
-        const int st = statusA[q];
-        // the gate: the edge new → nearest (a literal-path verdict is settled by star_insert)
-        const bool gate = (st == kLiteral || star_feasible(st, costA[q])) &&
-                          !(mq.blocked && mq.blocked[q]);
-        if (!gate) {
-            if (lane == 0) {
-                if (st == kError) atomicOr(err, 1);  // n_point overflow: the reference panics
-                sd.nnear[q] = -1;
-                mq.it[q] += 1;
-                mq.evals[q] += n;
-            }
-            continue;
-        }
-        const double x = sd.px[q], y = sd.py[q];
-        const size_t row = (size_t)q * mq.cap;
-        const double* __restrict__ X = mq.x + row;
-        const double* __restrict__ Y = mq.y + row;
-        const int k = sd.ksched[n];
-        const bool cached = n <= kKnnCache;
-        int mine = -1;
-        bool done = false;
-        if (cached) {
-            double lmin = __builtin_inf();
-#pragma unroll 8
-            for (int i = lane; i < n; i += 64) {
-                const double dx = x - X[i], dy = y - Y[i];
-                const double d2 = dx * dx + dy * dy;
-                cache[i] = d2;
-                lmin = fmin(lmin, d2);
-            }
-            // T = the k-th smallest lane minimum: k distinct nodes lie within it, so the k nearest
-            // are among the nodes with d2 <= T (usually k..2k of them)
-            const double T = readlane_f64(bitonic64(lmin, lane).d, k - 1);
-            int c = 0;
-            for (int i = lane; i < n; i += 64) c += cache[i] <= T;
-            int off = wave_incl_scan(c);  // inclusive prefix over the lanes
-            const int C = __builtin_amdgcn_readlane(off, 63);
-            if (C <= 64) {  // gather them into one (d2, index) pair per lane and sort the wave
-                off -= c;
-                for (int i = lane; i < n; i += 64)
-                    if (cache[i] <= T) {
-                        cand_d[off] = cache[i];
-                        cand_i[off] = i;
-                        ++off;
-                    }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                Kv kv{__builtin_inf(), 0x7fffffff};
-                if (lane < C) kv = Kv{cand_d[lane], cand_i[lane]};
-                kv = bitonic64(kv.d, lane, kv.i);
-                mine = lane < k ? kv.i : -1;
-                done = true;
-                __builtin_amdgcn_wave_barrier();  // the list is reused by the next query
-            }
-        }
-        if (!done) {
-            // k rounds of the lexicographic (d2, index) successor of the previous winner
-            double pd = -1.0;
-            int pi = -1;
-            for (int r = 0; r < k; ++r) {
-                double bd = __builtin_inf();
-                int bi = 0x7fffffff;
-                for (int i = lane; i < n; i += 64) {
-                    double d2;
-                    if (cached) {
-                        d2 = cache[i];
-                    } else {
-                        const double dx = x - X[i], dy = y - Y[i];
-                        d2 = dx * dx + dy * dy;
-                    }
-                    if ((d2 > pd || (d2 == pd && i > pi)) && d2 < bd) {
-                        bd = d2;
-                        bi = i;
-                    }
+    __shared__ int s_cnt[kKnnWaves], s_base;
+    // wave w of workgroup b serves queries b * kKnnWaves + w (+ the grid's stride): every wave of
+    // a workgroup runs the same iterations, so the round-B task reservation is one atomic per
+    // workgroup instead of one per query (one counter address for the whole launch)
+    for (int qb = (int)blockIdx.x * kKnnWaves; qb < mq.Q; qb += (int)gridDim.x * kKnnWaves) {
+        const int q = qb + wave;
+        const int p = q < mq.Q ? sd.pn[q] : -1;
+        bool live = p >= 0;
+        int n = 0, st = kReject;
+        if (live) {
+            n = mq.n[q];
+            st = statusA[q];
+            // the gate: the edge new → nearest (a literal-path verdict is settled by star_insert)
+            const bool gate = (st == kLiteral || star_feasible(st, costA[q])) &&
+                              !(mq.blocked && mq.blocked[q]);
+            if (!gate) {
+                if (lane == 0) {
+                    if (st == kError) atomicOr(err, 1);  // n_point overflow: the reference panics
+                    sd.nnear[q] = -1;
+                    mq.it[q] += 1;
+                    mq.evals[q] += n;
                 }
-                wave_argmin(bd, bi);
-                pd = bd;
-                pi = bi;
-                if (lane == r) mine = bi;
+                live = false;
             }
         }
-        const bool has = lane < k;
-        if (has) sd.near[(size_t)q * kStarKMax + lane] = mine;
-        // candidates that could still beat the nearest's cost c0 (chord lower bound): the others
-        // can never be the first strict minimum, so they are not steered
-        const double c0 = sd.cost[row + p] + costA[q];
-        bool want = has && mine != p;
-        if (want) {
-            const double dx = x - X[mine], dy = y - Y[mine];
-            want = sd.cost[row + mine] + star_chord_lb(dx * dx + dy * dy, sd.curv) < c0;
+        double x = 0.0, y = 0.0, c0 = 0.0;
+        size_t row = 0;
+        int k = 0, mine = -1;
+        bool want = false;
+        uint64_t bm = 0;
+        const double* __restrict__ X = mq.x;
+        const double* __restrict__ Y = mq.y;
+        if (live) {
+            x = sd.px[q];
+            y = sd.py[q];
+            row = (size_t)q * mq.cap;
+            X = mq.x + row;
+            Y = mq.y + row;
+            k = sd.ksched[n];
+            const bool cached = n <= kKnnCache;
+            bool done = false;
+            if (cached) {
+                double lmin = __builtin_inf();
+#pragma unroll 8
+                for (int i = lane; i < n; i += 64) {
+                    const double dx = x - X[i], dy = y - Y[i];
+                    const double d2 = dx * dx + dy * dy;
+                    cache[i] = d2;
+                    lmin = fmin(lmin, d2);
+                }
+                // T = the k-th smallest lane minimum: k distinct nodes lie within it, so the k
+                // nearest are among the nodes with d2 <= T (usually k..2k of them)
+                const double T = readlane_f64(bitonic64(lmin, lane).d, k - 1);
+                int c = 0;
+                for (int i = lane; i < n; i += 64) c += cache[i] <= T;
+                int off = wave_incl_scan(c);  // inclusive prefix over the lanes
+                const int C = __builtin_amdgcn_readlane(off, 63);
+                if (C <= 64) {  // gather them into one (d2, index) pair per lane and sort the wave
+                    off -= c;
+                    for (int i = lane; i < n; i += 64)
+                        if (cache[i] <= T) {
+                            cand_d[off] = cache[i];
+                            cand_i[off] = i;
+                            ++off;
+                        }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    Kv kv{__builtin_inf(), 0x7fffffff};
+                    if (lane < C) kv = Kv{cand_d[lane], cand_i[lane]};
+                    kv = bitonic64(kv.d, lane, kv.i);
+                    mine = lane < k ? kv.i : -1;
+                    done = true;
+                    __builtin_amdgcn_wave_barrier();  // the list is reused by the next query
+                }
+            }
+            if (!done) {
+                // k rounds of the lexicographic (d2, index) successor of the previous winner
+                double pd = -1.0;
+                int pi = -1;
+                for (int r = 0; r < k; ++r) {
+                    double bd = __builtin_inf();
+                    int bi = 0x7fffffff;
+                    for (int i = lane; i < n; i += 64) {
+                        double d2;
+                        if (cached) {
+                            d2 = cache[i];
+                        } else {
+                            const double dx = x - X[i], dy = y - Y[i];
+                            d2 = dx * dx + dy * dy;
+                        }
+                        if ((d2 > pd || (d2 == pd && i > pi)) && d2 < bd) {
+                            bd = d2;
+                            bi = i;
+                        }
+                    }
+                    wave_argmin(bd, bi);
+                    pd = bd;
+                    pi = bi;
+                    if (lane == r) mine = bi;
+                }
+            }
+            const bool has = lane < k;
+            if (has) sd.near[(size_t)q * kStarKMax + lane] = mine;
+            // candidates that could still beat the nearest's cost c0 (chord lower bound): the
+            // others can never be the first strict minimum, so they are not steered
+            c0 = sd.cost[row + p] + costA[q];
+            want = has && mine != p;
+            if (want) {
+                const double dx = x - X[mine], dy = y - Y[mine];
+                want = sd.cost[row + mine] + star_chord_lb(dx * dx + dy * dy, sd.curv) < c0;
+            }
+            bm = __ballot(want);
         }
-        const uint64_t bm = __ballot(want);
         const int cnt = __popcll(bm);
-        int slot = 0;
-        if (lane == 0) {
-            sd.nnear[q] = k;
-            sd.bmask[q] = bm;
-            slot = cnt > 0 ? atomicAdd(&sd.stB->W, cnt) : 0;
-            sd.bslot[q] = slot;
+        if (lane == 0) s_cnt[wave] = cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int tot = 0;
+            for (int w = 0; w < kKnnWaves; ++w) tot += s_cnt[w];
+            s_base = tot > 0 ? atomicAdd(&sd.stB->W, tot) : 0;
         }
-        slot = __shfl(slot, 0);
-        if (want) {  // X_near order
-            const int idx = __popcll(bm & ((1ull << lane) - 1ull));
-            SteerTask tk{};
-            tk.x = x;
-            tk.y = y;
-            tk.px = X[mine];
-            tk.py = Y[mine];
-            tk.pyaw = mq.yaw[row + mine];
-            tk.pnode = mine;
-            tasksB[slot + idx] = tk;
-            StarTaskExt ex{};
-            ex.cull = 1;  // only a candidate strictly cheaper than the nearest's can win
-            ex.cbase = sd.cost[row + mine];
-            ex.climit = c0;
-            extB[slot + idx] = ex;
+        __syncthreads();
+        if (live) {
+            int slot = s_base;
+            for (int w = 0; w < wave; ++w) slot += s_cnt[w];
+            slot = cnt > 0 ? slot : 0;
+            if (lane == 0) {
+                sd.nnear[q] = k;
+                sd.bmask[q] = bm;
+                sd.bslot[q] = slot;
+            }
+            if (want) {  // X_near order
+                const int idx = __popcll(bm & ((1ull << lane) - 1ull));
+                SteerTask tk{};
+                tk.x = x;
+                tk.y = y;
+                tk.px = X[mine];
+                tk.py = Y[mine];
+                tk.pyaw = mq.yaw[row + mine];
+                tk.pnode = mine;
+                tasksB[slot + idx] = tk;
+                StarTaskExt ex{};
+                ex.cull = 1;  // only a candidate strictly cheaper than the nearest's can win
+                ex.cbase = sd.cost[row + mine];
+                ex.climit = c0;
+                extB[slot + idx] = ex;
+            }
         }
+        __syncthreads();  // s_cnt / s_base are rewritten by the next iteration
     }
 }
 
@@ -3967,102 +3993,129 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
     StarTaskExt* __restrict__ extC, double* __restrict__ lit_scratch, int* __restrict__ err) {
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     const MqDev& mq = sd.mq;
-    for (int q = gw; q < mq.Q; q += nw) {
-        if (sd.pn[q] < 0) continue;
-        const int k = sd.nnear[q];
-        if (k < 0) continue;  // no insert this step (settled by star_knn)
-        const int p = sd.pn[q];
-        const int n = mq.n[q];
-        const size_t row = (size_t)q * mq.cap;
-        const double x = sd.px[q], y = sd.py[q];
-        const int mine = lane < k ? sd.near[(size_t)q * kStarKMax + lane] : -1;
-        // the nearest, then the X_near nodes star_knn steered (the pruned ones cannot win)
-        const int ncand = 1 + __popcll(sd.bmask[q]);
-        const bool act = lane < ncand;
-        int node = p, st = kReject;
-        double yaw = 0.0, e = __builtin_inf();
-        if (lane == 0) {
-            st = statusA[q];
-            yaw = yawA[q];
-            e = costA[q];
-        } else if (act) {
-            const int t = sd.bslot[q] + lane - 1;
-            node = tasksB[t].pnode;
-            st = statusB[t];
-            yaw = yawB[t];
-            e = costB[t];
-        }
-        const double nx = mq.x[row + node], ny = mq.y[row + node], nyaw = mq.yaw[row + node];
-        st = star_settle(sc, st, act, x, y, yaw, nx, ny, nyaw, lit_scratch, sd.lit_locks, gw);
-        if (__ballot(act && st == kError)) {
-            if (lane == 0) atomicOr(err, 1);
-            continue;
-        }
-        const bool feas = act && star_feasible(st, e);
-        if (!__shfl((int)feas, 0)) {  // the gate failed on the literal path
+    const int wave = threadIdx.x >> 6;
+    __shared__ int s_cnt[4], s_base;
+    // every wave of a workgroup runs the same iterations (queries b * 4 + w, + the grid's
+    // stride), so the round-C task reservation is one atomic per workgroup
+    for (int qb = (int)blockIdx.x * 4; qb < mq.Q; qb += (int)gridDim.x * 4) {
+        const int q = qb + wave;
+        bool live = q < mq.Q && sd.pn[q] >= 0;
+        const int k = live ? sd.nnear[q] : -1;
+        live = live && k >= 0;  // (k < 0: no insert this step, settled by star_knn)
+        const int p = live ? sd.pn[q] : 0;
+        const int n = live ? mq.n[q] : 0;
+        const size_t row = (size_t)(live ? q : 0) * mq.cap;
+        double x = 0.0, y = 0.0, cb = 0.0, yb = 0.0;
+        int mine = -1;
+        uint64_t wm = 0;
+        bool want = false;
+        if (live) {
+            x = sd.px[q];
+            y = sd.py[q];
+            mine = lane < k ? sd.near[(size_t)q * kStarKMax + lane] : -1;
+            // the nearest, then the X_near nodes star_knn steered (the pruned ones cannot win)
+            const int ncand = 1 + __popcll(sd.bmask[q]);
+            const bool act = lane < ncand;
+            int node = p, st = kReject;
+            double yaw = 0.0, e = __builtin_inf();
             if (lane == 0) {
-                sd.nnear[q] = -1;
-                mq.it[q] += 1;
-                mq.evals[q] += n;
+                st = statusA[q];
+                yaw = yawA[q];
+                e = costA[q];
+            } else if (act) {
+                const int t = sd.bslot[q] + lane - 1;
+                node = tasksB[t].pnode;
+                st = statusB[t];
+                yaw = yawB[t];
+                e = costB[t];
             }
-            continue;
+            const double nx = mq.x[row + node], ny = mq.y[row + node], nyaw = mq.yaw[row + node];
+            st = star_settle(sc, st, act, x, y, yaw, nx, ny, nyaw, lit_scratch, sd.lit_locks, gw);
+            if (__ballot(act && st == kError)) {
+                if (lane == 0) atomicOr(err, 1);
+                live = false;
+            } else {
+                const bool feas = act && star_feasible(st, e);
+                if (!__shfl((int)feas, 0)) {  // the gate failed on the literal path
+                    if (lane == 0) {
+                        sd.nnear[q] = -1;
+                        mq.it[q] += 1;
+                        mq.evals[q] += n;
+                    }
+                    live = false;
+                } else {
+                    // choose parent: the first strict minimum of cost(node) + edge cost in
+                    // candidate order
+                    double c = feas ? sd.cost[row + node] + e : __builtin_inf();
+                    int bl = lane;
+                    wave_argmin(c, bl);
+                    const int best = __shfl(node, bl);
+                    yb = __shfl(yaw, bl);
+                    const double eb = __shfl(e, bl);
+                    cb = c;
+                    if (lane == 0) {
+                        const size_t o = row + n;
+                        mq.x[o] = x;
+                        mq.y[o] = y;
+                        mq.yaw[o] = yb;
+                        mq.parent[o] = best;
+                        sd.cost[o] = cb;
+                        sd.elen[o] = eb;
+                        mq.n[q] = n + 1;
+                        mq.it[q] += 1;
+                        mq.evals[q] += n;
+                        sd.cb[q] = cb;
+                    }
+                    // rewire tasks: X_near nodes other than the parent that could still get
+                    // cheaper (cost(new) + e >= cost(new) >= cost(m) otherwise; costs only
+                    // decrease)
+                    want = lane < k && mine != best;
+                    if (want) {  // chord lower bound of the rewire edge (prunes only what cannot rewire)
+                        const double dx = x - mq.x[row + mine], dy = y - mq.y[row + mine];
+                        want = cb + star_chord_lb(dx * dx + dy * dy, sd.curv) < sd.cost[row + mine];
+                    }
+                    wm = __ballot(want);
+                }
+            }
         }
-        // choose parent: the first strict minimum of cost(node) + edge cost in candidate order
-        double c = feas ? sd.cost[row + node] + e : __builtin_inf();
-        int bl = lane;
-        wave_argmin(c, bl);
-        const int best = __shfl(node, bl);
-        const double yb = __shfl(yaw, bl), eb = __shfl(e, bl), cb = c;
-        if (lane == 0) {
-            const size_t o = row + n;
-            mq.x[o] = x;
-            mq.y[o] = y;
-            mq.yaw[o] = yb;
-            mq.parent[o] = best;
-            sd.cost[o] = cb;
-            sd.elen[o] = eb;
-            mq.n[q] = n + 1;
-            mq.it[q] += 1;
-            mq.evals[q] += n;
-            sd.cb[q] = cb;
-        }
-        // rewire tasks: X_near nodes other than the parent that could still get cheaper
-        // (cost(new) + e >= cost(new) >= cost(m) otherwise; costs only decrease)
-        bool want = lane < k && mine != best;
-        if (want) {  // chord lower bound of the rewire edge (prunes only what cannot rewire)
-            const double dx = x - mq.x[row + mine], dy = y - mq.y[row + mine];
-            want = cb + star_chord_lb(dx * dx + dy * dy, sd.curv) < sd.cost[row + mine];
-        }
-        const uint64_t wm = __ballot(want);
         const int cnt = __popcll(wm);
-        int slot = -1;
-        if (lane == 0) {
-            slot = cnt > 0 ? atomicAdd(&sd.stC->W, cnt) : -1;
-            sd.cslot[q] = slot;
-            sd.cmask[q] = wm;
+        if (lane == 0) s_cnt[wave] = cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+            s_base = tot > 0 ? atomicAdd(&sd.stC->W, tot) : 0;
         }
-        slot = __shfl(slot, 0);
-        if (want) {
-            SteerTask tk{};
-            tk.x = mq.x[row + mine];
-            tk.y = mq.y[row + mine];
-            tk.px = x;
-            tk.py = y;
-            tk.pyaw = yb;
-            tk.pnode = n;  // the new node (the edge's parent)
-            const int tc = slot + __popcll(wm & ((1ull << lane) - 1ull));
-            tasksC[tc] = tk;
-            StarTaskExt ex{};
-            ex.cyaw = mq.yaw[row + mine];
-            ex.own_yaw = 1;
-            ex.node = mine;
-            ex.cull = 1;  // only a strictly cheaper path through the new node matters
-            ex.cbase = cb;
-            ex.climit = sd.cost[row + mine];
-            extC[tc] = ex;
+        __syncthreads();
+        if (live) {
+            int slot = s_base;
+            for (int w = 0; w < wave; ++w) slot += s_cnt[w];
+            slot = cnt > 0 ? slot : -1;
+            if (lane == 0) {
+                sd.cslot[q] = slot;
+                sd.cmask[q] = wm;
+            }
+            if (want) {
+                SteerTask tk{};
+                tk.x = mq.x[row + mine];
+                tk.y = mq.y[row + mine];
+                tk.px = x;
+                tk.py = y;
+                tk.pyaw = yb;
+                tk.pnode = n;  // the new node (the edge's parent)
+                const int tc = slot + __popcll(wm & ((1ull << lane) - 1ull));
+                tasksC[tc] = tk;
+                StarTaskExt ex{};
+                ex.cyaw = mq.yaw[row + mine];
+                ex.own_yaw = 1;
+                ex.node = mine;
+                ex.cull = 1;  // only a strictly cheaper path through the new node matters
+                ex.cbase = cb;
+                ex.climit = sd.cost[row + mine];
+                extC[tc] = ex;
+            }
         }
+        __syncthreads();  // s_cnt / s_base are rewritten by the next iteration
     }
 }
 
