@@ -468,7 +468,7 @@ int cf_launch(pp_ctx* c, int k, int want_line, int grid, const CfGoal* g = nullp
     PP_HIP(c->cf_len.reserve(kCfBatch));
     PP_HIP(c->cf_npts.reserve(kCfBatch));
     PP_HIP(c->cf_chain.reserve((size_t)kCfBatch * (kCfLevels + 2)));
-    PP_HIP(c->cf_err.reserve(1));
+    PP_HIP(c->cf_err.reserve(2));  // [0] error bits, [1] the kernel's node counter
     PP_HIP(c->cf_pts.reserve((size_t)kCfGrid * 3 * kCfPtsCap));
     PP_HIP(c->cf_etab.reserve((size_t)kCfGrid * 2 * kCfMaxEdges));
     PP_HIP(c->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
@@ -476,7 +476,7 @@ int cf_launch(pp_ctx* c, int k, int want_line, int grid, const CfGoal* g = nullp
         PP_HIP(c->lit_locks.reserve(kLiteralWaves));
         PP_HIP(hipMemsetAsync(c->lit_locks.p, 0, kLiteralWaves * sizeof(int), c->stream));
     }
-    PP_HIP(hipMemsetAsync(c->cf_err.p, 0, sizeof(int), c->stream));
+    PP_HIP(hipMemsetAsync(c->cf_err.p, 0, 2 * sizeof(int), c->stream));
     PP_HIP(launch_check_finish(c->stream, c->scene_dev(), c->tree_dev(), c->cf_nodes.p, k, g->x,
                                g->y, g->yaw, g->yaw_opt, g->level0, g->mode, want_line,
                                c->cf_ok.p, c->cf_len.p, c->cf_npts.p, c->cf_chain.p,

@@ -3250,7 +3250,15 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
     double* py = px + pts_cap;
     double* pyw = py + pts_cap;
     int* et = etab + (size_t)blockIdx.x * 2 * kCfMaxEdges;
-    for (int b = blockIdx.x; b < k; b += gridDim.x) {
+    // nodes are taken one at a time from a launch-wide counter (err[1], zeroed with err): a
+    // node's cost varies with its depth and how far optimize climbs, so a static stride left
+    // workgroups holding a few deep nodes as the launch's tail
+    __shared__ int s_b;
+    for (;;) {
+        if (tid == 0) s_b = atomicAdd(&err[1], 1);
+        __syncthreads();
+        const int b = s_b;
+        if (b >= k) break;
         // ancestor path, node first (NodeIter, rrt.rs:253-265), then reversed: root first
         if (tid == 0) {
             int d = 0, c = nodes[b];

@@ -33,7 +33,10 @@ constexpr int kWalkThreads = 512;    // steer_walk workgroup: 8 tasks at a time 
 constexpr int kCfMaxDepth = 8192;    // check_finish: ancestor path staged in LDS (32 KB)
 constexpr int kCfLevels = 16;        // RECURSION_LIMIT, rrt.rs:14
 constexpr int kCfMaxEdges = kCfLevels + 1 + kCfMaxDepth;
-constexpr int kCfGrid = 256;         // check_finish workgroups (literal scratch from the pool)
+#ifndef PP_CF_GRID
+#define PP_CF_GRID 256
+#endif
+constexpr int kCfGrid = PP_CF_GRID;  // check_finish workgroups (literal scratch from the pool)
 
 // Scene in device memory (Space, rrt.rs:70-78, with Q10 analytic discs).
 struct SceneDev {
