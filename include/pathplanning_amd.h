@@ -24,7 +24,9 @@
 extern "C" {
 #endif
 
-#define PP_ABI_VERSION 1
+/* 2: pp_stats lost the diagnostic stamps and gained the batch / check_finish counters;
+ *    pp_rrt_get_stats takes the caller's sizeof(pp_stats); pp_batch_plan added */
+#define PP_ABI_VERSION 2
 
 #define PP_OK 0
 #define PP_ERR_INVALID_ARGUMENT (-1)
@@ -45,7 +47,9 @@ typedef struct pp_dubins_config {
     double step_size;
 } pp_dubins_config;
 
-/* Counters of the batched extend driver (since pp_rrt_new or the last pp_rrt_reset_stats). */
+/* Counters of the batched extend driver (since pp_rrt_new / pp_batch_new / pp_star_new or the
+ * last pp_rrt_reset_stats).  pp_rrt_get_stats copies min(out_size, sizeof(pp_stats)) bytes, so a
+ * caller built against an older, shorter layout gets a prefix and never an overrun. */
 typedef struct pp_stats {
     int64_t iterations;       /* extend iterations consumed (plan_one calls, minus check_finish) */
     int64_t accepted;         /* nodes inserted */
@@ -60,8 +64,14 @@ typedef struct pp_stats {
     int64_t nn_scan_launches;
     double steer_ms;          /* device time of steer_walk (HIP events; profiling on) */
     int64_t steer_launches;
-    int64_t stamps[8];        /* diagnostic builds only (-DPP_STAMPS): phase ticks (100 MHz) */
     int64_t walk_points;      /* polyline points the steer walk generated and verified (profiling on) */
+    int64_t batch_steps;      /* query batches: lockstep steps launched (each up to the window per query) */
+    int64_t batch_passes;     /* query batches: host passes (the first plus the top-ups of stopped windows) */
+    double finish_ms;         /* device time of check_finish_kernel (HIP events; profiling on) */
+    int64_t finish_launches;
+    int64_t finish_nodes;     /* nodes check_finish ran on (profiling on) */
+    int64_t finish_edges;     /* Dubins edges steered + verified by check_finish (profiling on) */
+    int64_t finish_points;    /* polyline points those edges walked (profiling on) */
 } pp_stats;
 
 int pp_abi_version(void);
@@ -259,7 +269,7 @@ int pp_star_state(pp_ctx* ctx, int32_t* n_nodes, int64_t* iterations, int64_t* n
 int pp_star_tree_export(pp_ctx* ctx, int query, double* x, double* y, double* yaw,
                         int32_t* parent, double* cost, int64_t cap, int64_t* n);
 
-int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out);
+int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out, uint64_t out_size);
 int pp_rrt_reset_stats(pp_ctx* ctx);
 /* record HIP events around the hot kernels (adds a little host overhead per window) */
 int pp_set_profiling(pp_ctx* ctx, int enabled);

@@ -89,7 +89,7 @@ struct HBuf {  // pinned host staging
 
 constexpr int kMaxBatch = 64;  // windows enqueued between two host synchronisations
 constexpr int kWalkTallySlots = 4096;
-constexpr int kScreenPad = 64;  // >= any steer_walk grid (kWalkMaxWG, 1024 for L2 scenes)
+constexpr int kScreenPad = 64;  // f32 screen copies: the LDS-DMA reads whole float4s (<= 3 floats past)
 
 }  // namespace
 
@@ -215,10 +215,23 @@ struct pp_ctx {
     // ---- profiling
     bool prof = false;
     std::vector<hipEvent_t> ev;  // 4 per window or batch step, 8 per RRT* step
-    double nn_scan_ms = 0.0, steer_ms = 0.0;
-    int64_t nn_scan_launches = 0, steer_launches = 0;
+    double nn_scan_ms = 0.0, steer_ms = 0.0, finish_ms = 0.0;
+    int64_t nn_scan_launches = 0, steer_launches = 0, finish_launches = 0;
+    int64_t batch_steps = 0, batch_passes = 0;
+    DBuf<long long> cf_tally;  // check_finish (profiling): [0] nodes, [1] edges, [2] points
     DBuf<long long> wg_pts;  // walked polyline points per walk workgroup (profiling on)
     long long* prof_points() const { return prof ? wg_pts.p : nullptr; }
+    // every counter of pp_stats that lives on the host or in the profiling tallies (not DevState)
+    int reset_host_stats() {
+        nn_scan_ms = steer_ms = finish_ms = 0.0;
+        nn_scan_launches = steer_launches = finish_launches = 0;
+        batch_steps = batch_passes = 0;
+        if (wg_pts.p && hipMemsetAsync(wg_pts.p, 0, wg_pts.n * sizeof(long long), stream) != hipSuccess)
+            return PP_ERR_HIP;
+        if (cf_tally.p && hipMemsetAsync(cf_tally.p, 0, cf_tally.n * sizeof(long long), stream) != hipSuccess)
+            return PP_ERR_HIP;
+        return hipStreamSynchronize(stream) == hipSuccess ? PP_OK : PP_ERR_HIP;
+    }
 
     ~pp_ctx() {
         for (auto& e : ev)
@@ -469,22 +482,39 @@ int cf_launch(pp_ctx* c, int k, int want_line, int grid, const CfGoal* g = nullp
     PP_HIP(c->cf_npts.reserve(kCfBatch));
     PP_HIP(c->cf_chain.reserve((size_t)kCfBatch * (kCfLevels + 2)));
     PP_HIP(c->cf_err.reserve(2));  // [0] error bits, [1] the kernel's node counter
-    PP_HIP(c->cf_pts.reserve((size_t)kCfGrid * 3 * kCfPtsCap));
-    PP_HIP(c->cf_etab.reserve((size_t)kCfGrid * 2 * kCfMaxEdges));
+    // the line buffers (one per workgroup of the launch) only when lines are materialised
+    const int wgs = std::min(grid, k);
+    if (want_line) {
+        PP_HIP(c->cf_pts.reserve((size_t)wgs * 3 * kCfPtsCap));
+        PP_HIP(c->cf_etab.reserve((size_t)wgs * 2 * kCfMaxEdges));
+    }
     PP_HIP(c->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
     if (!c->lit_locks.p) {  // the literal scratch pool's slot locks (zero: free)
         PP_HIP(c->lit_locks.reserve(kLiteralWaves));
         PP_HIP(hipMemsetAsync(c->lit_locks.p, 0, kLiteralWaves * sizeof(int), c->stream));
     }
     PP_HIP(hipMemsetAsync(c->cf_err.p, 0, 2 * sizeof(int), c->stream));
+    if (c->prof) {
+        if (int r = ensure_events(c, 2)) return r;
+        PP_HIP(hipEventRecord(c->ev[0], c->stream));
+    }
     PP_HIP(launch_check_finish(c->stream, c->scene_dev(), c->tree_dev(), c->cf_nodes.p, k, g->x,
                                g->y, g->yaw, g->yaw_opt, g->level0, g->mode, want_line,
                                c->cf_ok.p, c->cf_len.p, c->cf_npts.p, c->cf_chain.p,
-                               c->api_lit_scratch.p, c->lit_locks.p, c->cf_pts.p, kCfPtsCap,
-                               c->cf_etab.p, c->cf_err.p, grid));
+                               c->api_lit_scratch.p, c->lit_locks.p,
+                               want_line ? c->cf_pts.p : nullptr, kCfPtsCap,
+                               want_line ? c->cf_etab.p : nullptr, c->cf_err.p, grid,
+                               c->prof ? c->cf_tally.p : nullptr));
+    if (c->prof) PP_HIP(hipEventRecord(c->ev[1], c->stream));
     int err = 0;
     PP_HIP(hipMemcpyAsync(&err, c->cf_err.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     PP_HIP(hipStreamSynchronize(c->stream));
+    if (c->prof) {
+        float ms = 0.f;
+        PP_HIP(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        c->finish_ms += ms;
+        c->finish_launches += 1;
+    }
     if (err & 2) return set_err(PP_ERR_REFERENCE_PANIC, "finalize: a Dubins edge has no feasible word (rrt.rs:529 panics)");
     if (err & 4) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
     if (err & 1) return set_err(PP_ERR_CAPACITY, "tree deeper than the check_finish path capacity");
@@ -534,7 +564,6 @@ constexpr int kMaxSub = 4;
 // with 2; 4 streams collapse to 10.7M / 2.4M, the box runs 4 hardware queues per process)
 int mq_nsub(int Q, int dflt = 2) {
     int n = Q >= 256 ? dflt : 1;
-    if (const char* e = std::getenv("PP_BATCH_STREAMS")) n = std::max(1, std::min(kMaxSub, std::atoi(e)));
     return std::min(n, std::max(Q, 1));
 }
 MqArgs mq_sub_args(pp_ctx* c, int sub, int nsub) {
@@ -976,10 +1005,8 @@ static_assert(sizeof(scene::CullDisc) == sizeof(float4), "cull disc layout");
 // upload the item grid (pp_scene.cpp) and its LDS image; set the context's grid fields
 int upload_item_grid(pp_ctx* ctx, double minx, double maxx, double miny, double maxy,
                      const scene::Items& items) {
-    int part_budget = scene::kLdsImage;  // the grid-only image (PP_LDS_GRID_KB: experiments)
-    if (const char* e = std::getenv("PP_LDS_GRID_KB")) part_budget = std::atoi(e) * 1024;
     const scene::ItemGrid g =
-        scene::build_item_grid(minx, maxx, miny, maxy, items, part_budget);
+        scene::build_item_grid(minx, maxx, miny, maxy, items, scene::kLdsImage);
     const int m = (int)items.d4.size();
     PP_HIP(ctx->d_goff.reserve(g.goff.size()));
     PP_HIP(ctx->d_gitems.reserve(std::max<size_t>(g.gitems.size(), 1)));
@@ -1211,8 +1238,7 @@ int pp_rrt_new(pp_ctx* ctx, double sx, double sy, double syaw, double gx, double
     ctx->max_iter = max_iter;
     ctx->step = step_size;
     ctx->seed = seed;
-    ctx->nn_scan_ms = ctx->steer_ms = 0.0;
-    ctx->nn_scan_launches = ctx->steer_launches = 0;
+    if ((r = ctx->reset_host_stats())) return set_err(r, "resetting the statistics");
     if ((r = ensure_tree(ctx, std::max<int64_t>(capacity, 1024)))) return r;
     if ((r = ensure_window(ctx, ctx->K))) return r;
     // f32 screen tolerance: coordinates are rounded to f32 with error <= max|c| * 2^-24
@@ -1727,6 +1753,7 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
     if ((r = mq_write_states(ctx, st))) return r;
     PP_HIP(hipMemsetAsync(ctx->mq_err.p, 0, sizeof(int), st));
     PP_HIP(hipStreamSynchronize(st));
+    if ((r = ctx->reset_host_stats())) return set_err(r, "resetting the statistics");
     ctx->has_batch = true;
     return PP_OK;
 }
@@ -1821,16 +1848,10 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
         PP_HIP(hipMemcpyAsync(&err, ctx->mq_err.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
         if (err) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
-        const int64_t ran = steps;
-        steps = 0;
-        int behind = 0;
-        for (int q = 0; q < Q; ++q) {
-            steps = std::max(steps, (htg[q] - hit[q] + K - 1) / K);
-            behind += htg[q] > hit[q];
-        }
-        if (std::getenv("PP_DEBUG"))  // the top-up passes: queries whose windows stopped early
-            fprintf(stderr, "[pp] batch extend pass %d: %lld steps at K = %d, then %d of %d queries behind\n",
-                    pass, (long long)ran, K, behind, Q);
+        ctx->batch_steps += steps;
+        ctx->batch_passes += 1;
+        steps = 0;  // the top-up pass: queries whose windows stopped early
+        for (int q = 0; q < Q; ++q) steps = std::max(steps, (htg[q] - hit[q] + K - 1) / K);
     }
     if ((n_iterations || n_accepted) && (r = mq_totals(ctx, &it1, &n1))) return r;
     if (n_iterations) *n_iterations = it1 - it0;
@@ -1952,6 +1973,7 @@ int pp_star_new(pp_ctx* ctx, int q, const double* starts, const uint64_t* seeds,
     PP_HIP(hipMemcpyAsync(ctx->sr_state.p, ds, sizeof ds, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemsetAsync(ctx->sr_err.p, 0, sizeof(int), st));
     PP_HIP(hipStreamSynchronize(st));
+    if ((r = ctx->reset_host_stats())) return set_err(r, "resetting the statistics");
     ctx->has_star = true;
     return PP_OK;
 }
@@ -2065,7 +2087,7 @@ int pp_star_tree_export(pp_ctx* ctx, int query, double* x, double* y, double* ya
     return PP_OK;
 }
 
-int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out) {
+int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out, uint64_t out_size) {
     if (!ctx || !out) return set_err(PP_ERR_INVALID_ARGUMENT, "null argument");
     int r = check_ctx(ctx, false, false);
     if (r) return r;
@@ -2083,28 +2105,30 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out) {
         s.literal_repairs = d.literal_repairs;
         s.nn_flagged = d.nn_flagged;
         s.node_evals = d.node_evals;
-        for (int k = 0; k < 8; ++k) s.stamps[k] = d.stamps[k];
-#ifdef PP_STAMPS_SPAN
-        diag_dump_window_span((int)d.stamps[3]);
-#endif
-    } else if (ctx->has_batch) {  // diagnostic stamps of a query batch: summed over its states
-        DevState ds[1 + kMaxSub];
-        PP_HIP(hipMemcpyAsync(ds, ctx->mq_state.p, sizeof ds, hipMemcpyDeviceToHost, ctx->stream));
-        PP_HIP(hipStreamSynchronize(ctx->stream));
-        for (const DevState& d : ds)
-            for (int k = 0; k < 8; ++k) s.stamps[k] += d.stamps[k];
     }
     s.nn_scan_ms = ctx->nn_scan_ms;
     s.nn_scan_launches = ctx->nn_scan_launches;
     s.steer_ms = ctx->steer_ms;
     s.steer_launches = ctx->steer_launches;
+    s.batch_steps = ctx->batch_steps;
+    s.batch_passes = ctx->batch_passes;
+    s.finish_ms = ctx->finish_ms;
+    s.finish_launches = ctx->finish_launches;
     if (ctx->wg_pts.p) {  // profiling: the walk workgroups' point tallies
         std::vector<long long> v(ctx->wg_pts.n);
         PP_HIP(hipMemcpyAsync(v.data(), ctx->wg_pts.p, v.size() * sizeof(long long), hipMemcpyDeviceToHost, ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
         for (long long x : v) s.walk_points += x;
     }
-    *out = s;
+    if (ctx->cf_tally.p) {
+        long long t[3];
+        PP_HIP(hipMemcpyAsync(t, ctx->cf_tally.p, sizeof t, hipMemcpyDeviceToHost, ctx->stream));
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+        s.finish_nodes = t[0];
+        s.finish_edges = t[1];
+        s.finish_points = t[2];
+    }
+    std::memcpy(out, &s, (size_t)std::min<uint64_t>(out_size, sizeof s));
     return PP_OK;
 }
 
@@ -2117,17 +2141,11 @@ int pp_rrt_reset_stats(pp_ctx* ctx) {
         DevState d = ctx->h_state.p[0];
         d.iterations = d.accepted = d.windows = d.truncations = d.repair_rounds = d.repairs =
             d.literal_repairs = d.nn_flagged = d.node_evals = 0;
-        for (auto& t : d.stamps) t = 0;
         ctx->h_state.p[0] = d;
         PP_HIP(hipMemcpyAsync(ctx->d_state.p, ctx->h_state.p, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
     }
-    ctx->nn_scan_ms = ctx->steer_ms = 0.0;
-    ctx->nn_scan_launches = ctx->steer_launches = 0;
-    if (ctx->wg_pts.p) {
-        PP_HIP(hipMemsetAsync(ctx->wg_pts.p, 0, ctx->wg_pts.n * sizeof(long long), ctx->stream));
-        PP_HIP(hipStreamSynchronize(ctx->stream));
-    }
+    if ((r = ctx->reset_host_stats())) return set_err(r, "resetting the statistics");
     return PP_OK;
 }
 
@@ -2137,6 +2155,11 @@ int pp_set_profiling(pp_ctx* ctx, int enabled) {
     if (enabled && !ctx->wg_pts.p) {  // one tally slot per walk workgroup (any walk grid)
         PP_HIP(ctx->wg_pts.reserve(kWalkTallySlots));
         PP_HIP(hipMemsetAsync(ctx->wg_pts.p, 0, kWalkTallySlots * sizeof(long long), ctx->stream));
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    if (enabled && !ctx->cf_tally.p) {
+        PP_HIP(ctx->cf_tally.reserve(3));
+        PP_HIP(hipMemsetAsync(ctx->cf_tally.p, 0, 3 * sizeof(long long), ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
     }
     ctx->prof = enabled != 0;

@@ -73,7 +73,8 @@ hipError_t launch_steer_tasks(hipStream_t st, const SceneDev& sc, const TreeDev&
 // per node; chain (optional) = k rows of [levels, edges, optimize's chosen ancestors...] with
 // kCfLevels + 2 ints per row; want_line: materialise verified lines (length, points of the last
 // node each workgroup handled in pts/etab).  err |= 1 depth > kCfMaxDepth, 2 finalize panic,
-// 4 steer overflow, 8 point capacity.
+// 4 steer overflow, 8 point capacity.  tally (profiling, optional): += nodes, edges steered +
+// verified, polyline points walked.
 // check_finish_kernel modes: check_finish (rrt.rs:428-438), optimize alone (rrt.rs:463-487),
 // finalize of a caller-built goal node (rrt.rs:489-540)
 enum : int { kCfCheck = 0, kCfOptimize = 1, kCfFinalize = 2 };
@@ -82,7 +83,7 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,
                                int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
-                               int grid);
+                               int grid, long long* tally = nullptr);
 
 // Multi-query batch: `steps` lockstep extend iterations of every query (config 3).
 struct MqArgs {
@@ -136,7 +137,4 @@ hipError_t launch_dubins_batch(hipStream_t st, const double* conf, int n, int ca
                                double* py, double* pyaw, int* n_out, int* word_out,
                                double* cost_out, int* status_out);
 
-#ifdef PP_STAMPS_SPAN
-void diag_dump_window_span(int launches);
-#endif
 }  // namespace ppamd

@@ -33,18 +33,6 @@ namespace ppamd {
 typedef __attribute__((address_space(3))) void lds_void;  // LDS-DMA operands
 typedef __attribute__((address_space(1))) void glb_void;
 
-#if defined(PP_STAMPS) || defined(PP_STAMPS_RESOLVE)
-#define PP_STAMP(var) const int64_t var = (int64_t)__builtin_amdgcn_s_memrealtime()
-#else
-#define PP_STAMP(var)
-#endif
-// diagnostic build only (-DPP_STAMPS_SCREEN): the screen's phase times per wave
-#ifdef PP_STAMPS_SCREEN
-#define SCREEN_STAMP(var) const int64_t var = (int64_t)__builtin_amdgcn_s_memrealtime()
-#else
-#define SCREEN_STAMP(var)
-#endif
-
 // ------------------------------------------------------------------------------ collision
 
 // One 64-point chunk of a polyline, one point per lane: bounds for the lanes flagged
@@ -84,20 +72,9 @@ __device__ inline void stage_scene(const SceneDev& sc) {
     __syncthreads();
 }
 
-#ifdef PP_STAMPS_WALK
-// diagnostic build only: per walk launch, chunks tested, items that pass the chunk's bbox cull,
-// items that pass the per-segment f32 near test (flushed by the walk's last wave)
-__device__ unsigned long long g_cull[3] = {0ull, 0ull, 0ull};
-#define CULL_COUNT(i, v) \
-    if ((threadIdx.x & 63) == 0) atomicAdd(&g_cull[i], (unsigned long long)(v))
-#else
-#define CULL_COUNT(i, v)
-#endif
 template <bool kLds>
 __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool check_bounds,
-                                              bool seg_valid, double qx, double qy,
-                                              int64_t* ph = nullptr) {
-    PP_STAMP(tq0);
+                                              bool seg_valid, double qx, double qy) {
     bool oob =
         check_bounds && !(qx >= sc.minx && qx <= sc.maxx && qy >= sc.miny && qy <= sc.maxy);
     if (__any(oob)) return true;
@@ -113,15 +90,6 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     }
     if (sc.m == 0 && sc.ne == 0) return false;
     const bool poly = sc.ne > 0;  // grid items are polygon edges (Q10p), else discs
-#ifdef PP_BBOX_F64
-    const double ax = __shfl_up(qx, 1);
-    const double ay = __shfl_up(qy, 1);
-    const double inf = __builtin_inf();
-    const double bx0 = wave_min(has ? qx : inf);
-    const double bx1 = wave_max(has ? qx : -inf);
-    const double by0 = wave_min(has ? qy : inf);
-    const double by1 = wave_max(has ? qy : -inf);
-#else
     // the chunk's bounding box in f32, rounded outward (DPP reductions): a box that contains the
     // points selects a superset of the cells and items, and the exact test below decides
     const double ax = shfl_up1_f64(qx);
@@ -131,11 +99,6 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const float bx1 = wave_max_f32(has ? f32_above(qx) : -inff);
     const float by0 = wave_min_f32(has ? f32_below(qy) : inff);
     const float by1 = wave_max_f32(has ? f32_above(qy) : -inff);
-#endif
-    PP_STAMP(tq1);
-#ifdef PP_STAMPS
-    if (ph) ph[0] += tq1 - tq0;
-#endif
     const int cx0 = __builtin_amdgcn_readfirstlane(grid_cell(bx0, sc.gx0, sc.ginv, sc.gnx));
     const int cx1 = __builtin_amdgcn_readfirstlane(grid_cell(bx1, sc.gx0, sc.ginv, sc.gnx));
     const int cy0 = __builtin_amdgcn_readfirstlane(grid_cell(by0, sc.gy0, sc.ginv, sc.gny));
@@ -161,7 +124,6 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const int lane = threadIdx.x & 63;
     const float bxl = (float)bx0 - sc.cull_slack, bxh = (float)bx1 + sc.cull_slack;
     const float byl = (float)by0 - sc.cull_slack, byh = (float)by1 + sc.cull_slack;
-    CULL_COUNT(0, 1);
     // up to 64 items in parallel, one per lane (kk: its index in the item list, valid: a lane with
     // an item): the cull disc against the chunk's bbox, then the survivors against every lane's
     // segment, one at a time
@@ -174,7 +136,6 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
             Dl = d4[dl];
             ov = Dl.x + Dl.z >= bxl && Dl.x - Dl.z <= bxh && Dl.y + Dl.z >= byl && Dl.y - Dl.z <= byh;
         }
-        CULL_COUNT(1, __builtin_popcountll(__ballot(ov)));
         for (uint64_t m = __ballot(ov); m; m &= m - 1) {
             const int src = (int)__builtin_ctzll(m);
             const int d = __builtin_amdgcn_readlane(dl, src);
@@ -183,13 +144,9 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
             D.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.y), src));
             D.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.z), src));
             D.w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, Dl.w), src));
-#ifdef PP_STAMPS
-            if (ph) ph[1] += 1;
-#endif
             const float dxf = D.x - axf, dyf = D.y - ayf, thr = D.z + Lf;
             bool near = seg_valid && dxf * dxf + dyf * dyf <= thr * thr;
             if (!__any(near)) continue;
-            CULL_COUNT(2, 1);
             if (!poly) {
                 // f32 closest point of the segment to the disc centre, decisive outside a band of
                 // +-eps around the radius (eps bounds the f32 rounding of the coordinates, the
@@ -216,7 +173,6 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     };
     const int ncx = cx1 - cx0 + 1, ncy = cy1 - cy0 + 1;
     if (ncx <= 0 || ncy <= 0) return false;
-#ifndef PP_CELLS_SERIAL
     if (ncx * ncy <= 64) {
         // every cell of the box at once: lane c reads cell c's item range (one LDS round trip
         // instead of one per cell), then the cells' item lists are dealt out to the lanes as one
@@ -243,7 +199,6 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
         }
         return false;
     }
-#endif
     for (int gy = cy0; gy <= cy1; ++gy) {
         for (int gx = cx0; gx <= cx1; ++gx) {
             const int cell = gy * sc.gnx + gx;
@@ -365,11 +320,13 @@ __device__ __forceinline__ WalkIn walk_in(const SteerPrep* __restrict__ p) {
 }
 __device__ __forceinline__ WalkIn walk_in(const SteerPrep& p) { return walk_in(&p); }
 
+// walked (optional, wave-uniform): += the polyline points generated and verified
 template <bool kLds>
 __device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
-                                          int64_t* ph = nullptr, bool junction = true) {
+                                          bool junction = true, int* walked = nullptr) {
     const int lane = threadIdx.x & 63;
     if (r.state == kPrepNone) {  // polyline [(x, y), (px, py)]
+        if (walked) *walked += 2;
         const bool has = lane < 2;
         const double qx = lane == 0 ? r.x : r.px, qy = lane == 0 ? r.y : r.py;
         return chunk_rejects<kLds>(sc, has, has, lane == 1, qx, qy) ? kReject : kAccept;
@@ -432,22 +389,8 @@ __device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
             isjunction = true;  // the parent: already checked unless it is the root
         }
         const bool check_bounds = isgrid || isjunction || (first && lane == 0);
-        PP_STAMP(tc0);
-#ifdef PP_STAMPS
-        int64_t cph[2] = {0, 0};
-        const bool rej = chunk_rejects<kLds>(sc, has, check_bounds, has && lane >= 1, qx, qy, cph);
-#else
         const bool rej = chunk_rejects<kLds>(sc, has, check_bounds, has && lane >= 1, qx, qy);
-#endif
-        PP_STAMP(tc1);
-#ifdef PP_STAMPS
-        if (ph) {
-            ph[2] += tc1 - tc0;
-            ph[3] += 1;
-            ph[4] += cph[0];
-            ph[5] += cph[1];
-        }
-#endif
+        if (walked) *walked += cnt + (first ? 1 : 0) + (junction_here ? 1 : 0);
         if (rej) return kReject;
         if (end_here) break;
         carry_x = readlane_f64(qx, cnt);
@@ -465,7 +408,7 @@ template <bool kLds>
 __device__ int steer_collide_fast(const SceneDev& sc, double x, double y, double yaw, double px,
                                   double py, double pyaw, bool junction = true) {
     const SteerPrep r = steer_prep(sc, x, y, yaw, px, py, pyaw);
-    return steer_walk<kLds>(sc, walk_in(r), nullptr, junction);
+    return steer_walk<kLds>(sc, walk_in(r), junction);
 }
 
 // Literal path (measure-zero trim cases): lane 0 runs dubins_literal into its scratch buffer and
@@ -646,37 +589,19 @@ __global__ __launch_bounds__(64) void dubins_words_kernel(const double* __restri
 // device-resident DevState, so the host enqueues windows back to back and synchronises once per
 // batch.
 
-#ifndef PP_QPL
-#define PP_QPL 8
-#endif
-#ifndef PP_SCANBLK
-#define PP_SCANBLK 16
-#endif
-constexpr int kQPL = PP_QPL;                     // samples per lane in the screen
+constexpr int kQPL = 8;                     // samples per lane in the screen
 constexpr int kQPB = 64 * kQPL;                  // samples per screen workgroup (its waves share them)
-#ifdef PP_WIN1024
-constexpr int kScanThreads = 1024;               // window_kernel workgroup (16 waves)
-#ifdef PP_WIN_REPAIR
-constexpr bool kWinRepair = true;                // repairs inside the window kernel (spills)
-#else
-constexpr bool kWinRepair = false;               // repairs in resolve_tail_kernel
-#endif
-#else
 constexpr int kScanThreads = 512;                // window_kernel workgroup (8 waves, 256 VGPRs)
 constexpr bool kWinRepair = true;                // repairs inside the window kernel (no spill)
-#endif
 constexpr int kScanWaves = kScanThreads / 64;
-constexpr int kScanBlk = PP_SCANBLK;             // nodes per block (one block minimum per sample)
+constexpr int kScanBlk = 16;             // nodes per block (one block minimum per sample)
 constexpr int kStage = 7936;                     // chunk nodes staged in LDS per round
 constexpr int kGrab = 64;                        // nodes a screen wave takes from the counter
 constexpr int kExactNode = 1 << 30;              // screen partial key: a node index, not a block
 // LDS of a screen workgroup: the wave merge (best, second, key per wave and sample; sample ids;
 // the samples' f32 operands), then the staged chunk
 constexpr int kScreenStageOff = (3 * kScanWaves + 3) * kQPB * 4;
-#ifndef PP_SCANGRID
-#define PP_SCANGRID 255
-#endif
-constexpr int kScanGrid = PP_SCANGRID;           // screen workgroups per window (one per CU, with
+constexpr int kScanGrid = 255;           // screen workgroups per window (one per CU, with
                                                  // the resolve workgroup: <= 256 CUs)
 
 // node chunks of the screen for a window of K samples: the nqb sample blocks x chunks workgroups
@@ -954,7 +879,6 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
                                                                char* smem) {
     DevState* st = a.st;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    SCREEN_STAMP(ts0);
     const int W = st->Wp[a.p];
     const int ns = st->n_scan;
     if (b == 0 && tid == 0) st->nsp[a.p] = ns;
@@ -1039,7 +963,6 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
             }
         }
     }
-    SCREEN_STAMP(ts1);
     // screen value of (sample r, node (nx, ny)); expanded: the node's (x - ox, y - oy, |.|^2)
     auto val = [&](int r, float px, float py, float pw) {
         if (kExp) return __builtin_fmaf(qxr[r], px, __builtin_fmaf(qyr[r], py, pw));
@@ -1055,9 +978,6 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
         }
     };
     int r0 = 0;
-#ifdef PP_STAMPS_SCREEN
-    int64_t ts2 = 0;
-#endif
     for (;;) {
         const int len = min(kStage, L - r0);
         if (tid == 0) *s_next = 0;
@@ -1076,9 +996,6 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
             *reinterpret_cast<float4*>(stg + 2 * kStage + i) = w4;
         }
         __syncthreads();
-#ifdef PP_STAMPS_SCREEN
-        if (r0 == 0) ts2 = (int64_t)__builtin_amdgcn_s_memrealtime();
-#endif
         for (;;) {
             int g0 = 0;
             if (lane == 0) g0 = atomicAdd(s_next, kGrab);
@@ -1135,7 +1052,6 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
         __syncthreads();  // every wave is done with this round before the next overwrites it
         issue_round(r0);
     }
-    SCREEN_STAMP(ts3);
     // The waves' partials per sample go to LDS — (best, second, key): key = the best block's start,
     // or kExactNode | index when the best is a tail node (tail nodes follow every block of the
     // chunk, so keys order ties by node index either way), 0x7fffffff when the wave saw no node —
@@ -1156,10 +1072,6 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
         if (wave == 0) s_sid[r * 64 + lane] = sid[r];
     }
     __syncthreads();
-    SCREEN_STAMP(ts4);
-#ifdef PP_STAMPS_SCREEN
-    int64_t tm1 = ts4, tm3 = ts4;
-#endif
     if (tid < kQPB) {  // one thread per sample (sorted position qbase + tid)
         float bb = s_b[tid], ss = s_s[tid];
         int key = s_i[tid];
@@ -1174,9 +1086,6 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
         }
         const int q = s_sid[tid];
         int idx = key == 0x7fffffff ? -1 : (key & ~kExactNode);
-#ifdef PP_STAMPS_SCREEN
-        tm1 = (int64_t)__builtin_amdgcn_s_memrealtime() + (int64_t)(bb * 0.0f) + (q & 0);
-#endif
         if (q >= 0 && key != 0x7fffffff && !(key & kExactNode)) {
             // the sample's screen operands, as wave 0 held them
             const float* s_qx = reinterpret_cast<const float*>(smem) + (3 * kScanWaves + 1) * kQPB;
@@ -1210,9 +1119,6 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
             idx = key + ui;
             ss = __builtin_fminf(ss, other);
         }
-#ifdef PP_STAMPS_SCREEN
-        tm3 = (int64_t)__builtin_amdgcn_s_memrealtime() + (int64_t)(ss * 0.0f) + (idx & 0);
-#endif
         if (q >= 0) {  // by sorted position: coalesced (nn_finalize maps samples through ipos)
             const size_t o = (size_t)c * a.Kcap + qbase + tid;
             a.pbest[o] = bb;
@@ -1220,248 +1126,8 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
             a.pidx[o] = idx;
         }
     }
-#ifdef PP_STAMPS_SCREEN
-    SCREEN_STAMP(ts5);
-    if (tid == 0) {  // wave 0 of every screen workgroup: phase times summed (100 MHz ticks)
-        unsigned long long* sp = reinterpret_cast<unsigned long long*>(st->stamps);
-        // [0] samples + staging, [1] loop, [2] partials + merge + winner re-evaluation, [3] waves,
-        // [4] max wave total; [5..7]: workgroup 0 (window_kernel)
-        atomicAdd(&sp[0], (unsigned long long)(ts2 - ts0));
-        atomicAdd(&sp[1], (unsigned long long)(ts3 - ts2));
-        atomicAdd(&sp[2], (unsigned long long)(ts5 - ts3));
-        atomicAdd(&sp[3], 1ull);
-        atomicMax(&sp[4], (unsigned long long)(ts5 - ts0));
-        (void)tm1;
-        (void)tm3;
-    }
-#endif
 }
 
-#ifdef PP_SCREEN_MFMA
-// The expanded screen on the matrix cores (build variant): for a tile of 32 staged nodes and a
-// group of 32 samples, v_mfma_f32_32x32x2_f32 with A[i] = ((n-o)_y, (n-o)_x) of node i,
-// B[j] = (-2(q-o)_y, -2(q-o)_x) of sample j and C[i][j] = |n_i - o|^2 gives
-// D[i][j] = fma(B1, A1, fma(B0, A0, C)) — bit for bit the VALU chain of scan_role
-// (scripts/micro/mfma_screen_check.hip: 2,048,000 of 2,048,000 results identical), so the winner
-// re-evaluation and nn_finalize's bounds are unchanged.  Lane l holds column j = l % 32 and the
-// rows (r / 4) * 8 + (l / 32) * 4 + r % 4 (r = 0..15): a lane's block is 16 of the tile's rows,
-// the two lane halves are merged at the end, and the winner's whole tile is re-evaluated.
-typedef float pp_floatx16 __attribute__((ext_vector_type(16)));
-constexpr int kMTile = 32;                  // nodes per MFMA tile
-constexpr int kMGroups = kQPB / 32;         // sample groups of 32 per workgroup block
-
-__device__ __attribute__((always_inline)) inline void scan_role_mfma(const WinKArgs& a, int b,
-                                                                    char* smem) {
-    static_assert(kQPB % 32 == 0 && kGrab % kMTile == 0, "whole groups and tiles");
-    DevState* st = a.st;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int h = lane >> 5, j = lane & 31;  // lane half (MFMA k index) and sample column
-    const int W = st->Wp[a.p];
-    const int ns = st->n_scan;
-    if (b == 0 && tid == 0) st->nsp[a.p] = ns;
-    const int G = a.nqb * a.chunks;
-    if (b >= G) return;
-    const int t = (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b;
-    const int qb = t % a.nqb, c = t / a.nqb;
-    const int qbase = qb * kQPB;
-    if (qbase >= W) return;
-    const int cl = scan_chunk_len(ns, a.chunks);
-    const int c0 = c * cl;
-    if (c0 >= ns) return;
-    const int L = min(c0 + cl, ns) - c0;
-    const float* nx = a.tr.x32;
-    const float* ny = a.tr.y32;
-    float* stg = reinterpret_cast<float*>(smem + kScreenStageOff);
-    int* s_next = reinterpret_cast<int*>(stg + 3 * kStage);
-    auto issue_round = [&](int r0) {
-        const int len = min(kStage, L - r0);
-        for (int q4 = wave; q4 * 256 < len; q4 += kScanWaves) {
-            if (q4 * 256 + 4 * lane < len) {
-                const size_t gi = (size_t)(c0 + r0 + q4 * 256 + 4 * lane);
-                __builtin_amdgcn_global_load_lds((glb_void*)(nx + gi), (lds_void*)(stg + q4 * 256), 16, 0, 0);
-                __builtin_amdgcn_global_load_lds((glb_void*)(ny + gi), (lds_void*)(stg + kStage + q4 * 256), 16, 0, 0);
-            }
-        }
-    };
-    issue_round(0);
-    // samples: group g holds sorted positions qbase + 32 g + j; this lane the y (h = 0) or the x
-    // (h = 1) operand, -2 (q - o) (exact scaling)
-    const float2 o = a.g.ob[a.p][qb];
-    const float oxf = o.x, oyf = o.y;
-    float bq[kMGroups], best[kMGroups], second[kMGroups];
-    int key[kMGroups];
-#pragma unroll
-    for (int g = 0; g < kMGroups; ++g) {
-        const int pos = qbase + 32 * g + j;
-        const bool in = pos < W;
-        const double v = h == 0 ? (in ? a.g.ssy[a.p][pos] : (double)oyf)
-                                : (in ? a.g.ssx[a.p][pos] : (double)oxf);
-        bq[g] = -2.0f * (float)(v - (double)(h == 0 ? oyf : oxf));
-        best[g] = __builtin_inff();
-        second[g] = __builtin_inff();
-        key[g] = 0x7fffffff;
-    }
-    {  // wave 0 parks every sample's operands for the re-evaluation (slot 32 g + j)
-        float* s_qx = reinterpret_cast<float*>(smem) + (3 * kScanWaves + 1) * kQPB;
-        if (wave == 0) {
-#pragma unroll
-            for (int g = 0; g < kMGroups; ++g) s_qx[(1 - h) * kQPB + 32 * g + j] = bq[g];
-        }
-        int* s_sid = reinterpret_cast<int*>(smem) + 3 * kScanWaves * kQPB;
-        for (int k = tid; k < kQPB; k += kScanThreads) {
-            const int pos = qbase + k;
-            s_sid[k] = pos < W ? a.perm[a.p][pos] : -1;
-        }
-    }
-    int r0 = 0;
-    for (;;) {
-        const int len = min(kStage, L - r0);
-        if (tid == 0) *s_next = 0;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        for (int i = 4 * tid; i < len; i += 4 * kScanThreads) {  // prep in place: (n-o, |n-o|^2)
-            float4 x4 = *reinterpret_cast<const float4*>(stg + i);
-            float4 y4 = *reinterpret_cast<const float4*>(stg + kStage + i);
-            float4 w4;
-            x4.x -= oxf, x4.y -= oxf, x4.z -= oxf, x4.w -= oxf;
-            y4.x -= oyf, y4.y -= oyf, y4.z -= oyf, y4.w -= oyf;
-            w4.x = __builtin_fmaf(y4.x, y4.x, x4.x * x4.x);
-            w4.y = __builtin_fmaf(y4.y, y4.y, x4.y * x4.y);
-            w4.z = __builtin_fmaf(y4.z, y4.z, x4.z * x4.z);
-            w4.w = __builtin_fmaf(y4.w, y4.w, x4.w * x4.w);
-            *reinterpret_cast<float4*>(stg + i) = x4;
-            *reinterpret_cast<float4*>(stg + kStage + i) = y4;
-            *reinterpret_cast<float4*>(stg + 2 * kStage + i) = w4;
-        }
-        __syncthreads();
-        for (;;) {
-            int g0 = 0;
-            if (lane == 0) g0 = atomicAdd(s_next, kGrab);
-            g0 = __builtin_amdgcn_readfirstlane(__shfl(g0, 0));
-            if (g0 >= len) break;
-            const int g1 = min(g0 + kGrab, len);
-            const int gt = g0 + ((g1 - g0) & ~(kMTile - 1));  // whole tiles (a tail: the last)
-            for (int u0 = g0; u0 < gt; u0 += kMTile) {
-                // A: this lane's node row j, k = h (y, then x); C: the |n-o|^2 of its 16 rows
-                const float av = stg[(h == 0 ? kStage : 0) + u0 + j];
-                pp_floatx16 cw;
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const float4 w4 = *reinterpret_cast<const float4*>(stg + 2 * kStage + u0 + 8 * v + 4 * h);
-                    cw[4 * v] = w4.x, cw[4 * v + 1] = w4.y, cw[4 * v + 2] = w4.z, cw[4 * v + 3] = w4.w;
-                }
-                const int k = c0 + r0 + u0;
-                // group g + 1's product is issued before group g's reduction (two accumulators);
-                // minimum (not fminf): the operands are finite, and no canonicalising v_max
-                pp_floatx16 dn = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq[0], cw, 0, 0, 0);
-#pragma unroll
-                for (int g = 0; g < kMGroups; ++g) {
-                    const pp_floatx16 d = dn;
-                    if (g + 1 < kMGroups)
-                        dn = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq[g + 1], cw, 0, 0, 0);
-                    const float m0 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[0], d[1]), d[2]);
-                    const float m1 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[3], d[4]), d[5]);
-                    const float m2 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[6], d[7]), d[8]);
-                    const float m3 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[9], d[10]), d[11]);
-                    const float m4 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[12], d[13]), d[14]);
-                    const float m5 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m0, m1), m2);
-                    const float m6 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m3, m4), d[15]);
-                    const float m = __builtin_elementwise_minimum(m5, m6);
-                    second[g] = __builtin_amdgcn_fmed3f(best[g], m, second[g]);
-                    if (m < best[g]) {
-                        best[g] = m;
-                        key[g] = k;
-                    }
-                }
-            }
-            for (int u = gt; u < g1; ++u) {  // the chunk's tail (< 32 nodes): exact top-2, VALU
-                const float px = stg[u], py = stg[kStage + u], pw = stg[2 * kStage + u];
-#pragma unroll
-                for (int g = 0; g < kMGroups; ++g) {
-                    const float other = __shfl_xor(bq[g], 32);  // the sample's other operand
-                    const float qx = h == 0 ? other : bq[g], qy = h == 0 ? bq[g] : other;
-                    // (one lane half only: the halves' partials are merged as distinct nodes)
-                    const float d = h == 0 ? __builtin_fmaf(qx, px, __builtin_fmaf(qy, py, pw))
-                                           : __builtin_inff();
-                    second[g] = __builtin_amdgcn_fmed3f(best[g], d, second[g]);
-                    if (d < best[g]) {
-                        best[g] = d;
-                        key[g] = (c0 + r0 + u) | kExactNode;
-                    }
-                }
-            }
-        }
-        if (r0 + len >= L) break;
-        r0 += len;
-        __syncthreads();
-        issue_round(r0);
-    }
-    // the two lane halves of each sample (disjoint rows of the same tiles), then the waves, as in
-    // scan_role: keys are tile starts or kExactNode | tail index (the tail follows every tile)
-    float* s_b = reinterpret_cast<float*>(smem);
-    float* s_s = s_b + kScanWaves * kQPB;
-    int* s_i = reinterpret_cast<int*>(s_s + kScanWaves * kQPB);
-    int* s_sid = s_i + kScanWaves * kQPB;
-#pragma unroll
-    for (int g = 0; g < kMGroups; ++g) {
-        const float ob = __shfl_xor(best[g], 32), os = __shfl_xor(second[g], 32);
-        const int ok = __shfl_xor(key[g], 32);
-        const bool take = ob < best[g] || (ob == best[g] && ok < key[g]);
-        const float ss = __builtin_fminf(__builtin_fminf(second[g], os), take ? best[g] : ob);
-        if (h == 0) {
-            s_b[wave * kQPB + 32 * g + j] = take ? ob : best[g];
-            s_s[wave * kQPB + 32 * g + j] = ss;
-            s_i[wave * kQPB + 32 * g + j] = take ? ok : key[g];
-        }
-    }
-    __syncthreads();
-    if (tid < kQPB) {  // one thread per sample slot (sorted position qbase + tid)
-        float bb = s_b[tid], ss = s_s[tid];
-        int kk = s_i[tid];
-#pragma unroll
-        for (int w = 1; w < kScanWaves; ++w) {
-            const float ob = s_b[w * kQPB + tid], os = s_s[w * kQPB + tid];
-            const int ok = s_i[w * kQPB + tid];
-            const bool take = ob < bb || (ob == bb && ok < kk);
-            ss = fminf(fminf(ss, os), take ? bb : ob);
-            bb = take ? ob : bb;
-            kk = take ? ok : kk;
-        }
-        const int q = s_sid[tid];
-        int idx = kk == 0x7fffffff ? -1 : (kk & ~kExactNode);
-        if (q >= 0 && kk != 0x7fffffff && !(kk & kExactNode)) {
-            // the winning tile again, VALU, bit-identical: the lowest index of the best value and
-            // the best of the tile's other nodes (each lane-half block carried one minimum)
-            const float* s_qx = reinterpret_cast<const float*>(smem) + (3 * kScanWaves + 1) * kQPB;
-            const float qx = s_qx[tid], qy = s_qx[kQPB + tid];
-            const int rel = kk - c0 - r0;
-            int ui = -1;
-            float other = __builtin_inff();
-            if (rel >= 0) {
-#pragma unroll 8
-                for (int u = 0; u < kMTile; ++u) {
-                    const float d = __builtin_fmaf(qx, stg[rel + u],
-                                                   __builtin_fmaf(qy, stg[kStage + rel + u], stg[2 * kStage + rel + u]));
-                    if (ui < 0 && d == bb)
-                        ui = u;
-                    else
-                        other = __builtin_fminf(other, d);
-                }
-            } else {
-                screen_block_global<true, kMTile>(nx + kk, ny + kk, qx, qy, oxf, oyf, bb, ui, other);
-            }
-            idx = kk + ui;
-            ss = __builtin_fminf(ss, other);
-        }
-        if (q >= 0) {
-            const size_t o2 = (size_t)c * a.Kcap + qbase + tid;
-            a.pbest[o2] = bb;
-            a.psecond[o2] = ss;
-            a.pidx[o2] = idx;
-        }
-    }
-}
-#endif
 
 // The first window of a batch: its samples (the later ones come from the previous window kernel
 // workgroup 0, after the commit that decides where the next window starts).
@@ -1529,10 +1195,7 @@ __device__ inline Top2 wave_top2(Top2 t) {
 
 // 8 waves per SIMD (<= 64 VGPRs): two 1024-thread workgroups per CU, so the extra sampling
 // workgroup (the grid's last) runs beside the others instead of waiting for a CU to drain.
-#ifndef PP_FIN_MINW
-#define PP_FIN_MINW 8
-#endif
-__global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
+__global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
     DevState* __restrict__ st, int p, int64_t seq, int chunks, const float* __restrict__ pbest,
     const float* __restrict__ psecond, const int* __restrict__ pidx, int stride,
     const double* __restrict__ qx, const double* __restrict__ qy, const float* __restrict__ x32,
@@ -1553,12 +1216,6 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
     __shared__ double s_rd[kFinWaves];
     __shared__ int s_ri[kFinWaves];
     __shared__ float2 s_dn[kFinDelta];   // nodes appended after the screen's snapshot (f32)
-#ifdef PP_STAMPS_FIN
-#define FIN_STAMP(v) const int64_t v = (int64_t)__builtin_amdgcn_s_memrealtime()
-#else
-#define FIN_STAMP(v)
-#endif
-    FIN_STAMP(tf0);
     const bool voided = st->void_seq == seq || st->error;
     if (gen_next && blockIdx.x == gridDim.x - 1) {
         // the extra workgroup: Space::rand_point of the window after this one, into the parity
@@ -1568,16 +1225,7 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
         // path: steer_prep and steer_walk of this window run before the next screen.
         __shared__ __attribute__((aligned(16))) char s_gen[kSamplesLds];
         const int64_t start = voided ? st->it_spec : st->wsp[p] + st->Wp[p];
-#ifdef PP_STAMPS_SCREEN
-        const int64_t tg0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-#endif
         samples_role(st, gen, 1 - p, start, s_gen);
-#ifdef PP_STAMPS_SCREEN
-        __syncthreads();
-        if (threadIdx.x == 0)  // [6] the next window's samples (nn_finalize's extra workgroup)
-            atomicAdd(reinterpret_cast<unsigned long long*>(&st->stamps[6]),
-                      (unsigned long long)((int64_t)__builtin_amdgcn_s_memrealtime() - tg0));
-#endif
         return;
     }
     const int W = voided ? 0 : st->Wp[p];
@@ -1598,7 +1246,6 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
     if (tid < kFinSamples) s_pc[tid] = 0;
     if (tid == 0) s_fmask = 0;
     __syncthreads();
-    FIN_STAMP(tf1);
     // ---- 1. the sample's nearest node
     if (in) {
         const int n_chunks = scan_chunks_used(ns, chunks);
@@ -1715,7 +1362,6 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
         }
     }
     __syncthreads();
-    FIN_STAMP(tf2);
     // near-ties: the workgroup's exact f64 brute force, over the screen chunks whose f32 minimum
     // could hide the exact nearest (f32 distance within the rounding bound of the f32 winner)
     // and over the appended nodes; lowest index on exact ties (rrt.rs:378-391, Q9)
@@ -1768,7 +1414,6 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
         }
         __syncthreads();
     }
-    FIN_STAMP(tf3);
     if (!cand) return;  // nearest-only launch (no window)
     // ---- 2. window pairs
     {
@@ -1805,29 +1450,9 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
                     }
                 }
             }
-#ifdef PP_PAIR_CHECK
-            int bc = 0, gc = 0;
-            for (int i = lane; i < j; i += 64) {
-                const double dx = xj - qx[i], dy = yj - qy[i];
-                bc += (dx * dx + dy * dy < D2) ? 1 : 0;
-            }
-            for (int o = 32; o > 0; o >>= 1) bc += __shfl_xor(bc, o);
-            gc = s_pc[wave];
-            if (lane == 0 && bc != gc) {
-                atomicAdd((unsigned long long*)&st->stamps[0], 1ull);
-                st->stamps[1] = j;
-                st->stamps[2] = bc;
-                st->stamps[3] = gc;
-                st->stamps[4] = (int64_t)(D2 * 1e6);
-                st->stamps[5] = cx0 * 100 + cx1;
-                st->stamps[6] = cy0 * 100 + cy1;
-                st->stamps[7] = seq;
-            }
-#endif
         }
     }
     __syncthreads();
-    FIN_STAMP(tf4);
     if (wave == 0) {
         const int j = q0 + lane;
         const bool jin = lane < kFinSamples && j < W;
@@ -1849,32 +1474,6 @@ __global__ __launch_bounds__(kFinThreads, PP_FIN_MINW) void nn_finalize_kernel(
         if (cnt > 0) pend[pb] = j;
         if (lane == 0 && ov) atomicMin(&st->weff, q0 + (int)__builtin_ctzll(ov));
     }
-#ifdef PP_STAMPS_FIN
-    FIN_STAMP(tf5);
-#ifdef PP_STAMPS_FIN_PHASES
-    if (tid == 0) {  // phase sums over the workgroups: [0] staging, [1] per-sample NN, [2] brute
-                     // force, [3] pair search, [4] candidate append, [5] workgroups, [6] max total
-        unsigned long long* sp = reinterpret_cast<unsigned long long*>(st->stamps);
-        atomicAdd(&sp[0], (unsigned long long)(tf1 - tf0));
-        atomicAdd(&sp[1], (unsigned long long)(tf2 - tf1));
-        atomicAdd(&sp[2], (unsigned long long)(tf3 - tf2));
-        atomicAdd(&sp[3], (unsigned long long)(tf4 - tf3));
-        atomicAdd(&sp[4], (unsigned long long)(tf5 - tf4));
-        atomicAdd(&sp[5], 1ull);
-        atomicMax(&sp[6], (unsigned long long)(tf5 - tf0));
-    }
-#else
-    if (tid == 0) {  // [0..2] workgroups without a near-tie brute force: sum, count, max;
-                     // [3..5] with one; [6] their brute-force time, [7] all pair-search time
-        const int o = s_fmask ? 3 : 0;
-        atomicAdd((unsigned long long*)&st->stamps[o], (unsigned long long)(tf5 - tf0));
-        atomicAdd((unsigned long long*)&st->stamps[o + 1], 1ull);
-        atomicMax((unsigned long long*)&st->stamps[o + 2], (unsigned long long)(tf5 - tf0));
-        if (s_fmask) atomicAdd((unsigned long long*)&st->stamps[6], (unsigned long long)(tf3 - tf2));
-        atomicAdd((unsigned long long*)&st->stamps[7], (unsigned long long)(tf4 - tf3));
-    }
-#endif
-#endif
 }
 
 // Task t of a window: t < W is (sample t → its snapshot NN); t >= W is candidate entry t - W
@@ -2233,11 +1832,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                 // first one past |L|; any other pass (a binade or sign crossing inside the
                 // chunk) takes the serial chain.  tests/test_walk_generator.py restates both.
                 const double w1 = gpd + gdd, w2 = w1 + gdd;
-#ifdef PP_GEN_CHAIN
-                bool cf = false;  // (diagnostic: the serial chain for every pass)
-#else
                 bool cf = (w1 - gpd) == (w2 - w1);
-#endif
                 if (cf) {
                     const double vc = __builtin_fma((double)(kk > 0 ? kk : 0), w1 - gpd, gpd);
                     const uint64_t fm = __ballot(kk >= 0 && !(fabs(vc) <= aL));
@@ -2350,10 +1945,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
 // steer_walk, one task per wave (persistent grid, grid-stride over the W + ncomp tasks); kLds:
 // the scene's disc grid is staged into this workgroup's LDS first.
 constexpr int kGenSlots = 68;  // per-wave LDS slots of the point generator (63 + 4 overshoot + 1)
-#ifndef PP_WALKWG
-#define PP_WALKWG 768
-#endif
-constexpr int kWalkMaxWG = PP_WALKWG;  // 3 resident workgroups per CU
+constexpr int kWalkMaxWG = 768;  // 3 resident workgroups per CU
 __host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
     return scene_bytes + kWalkThreads / 64 * kGenSlots * 8;
 }
@@ -2366,49 +1958,10 @@ __host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
 // tasks per wave, latency-bound, and run better at 6 (80 VGPRs, 3 workgroups per CU: config 3
 // 279 -> 309 M it/s; 8 spills too much).
 constexpr int kWalkMinWWindow = 1;
-#ifndef PP_WALK_MINW_BATCH
-#define PP_WALK_MINW_BATCH 6
-#endif
-constexpr int kWalkMinWBatch = PP_WALK_MINW_BATCH;
+constexpr int kWalkMinWBatch = 6;
 // RRT* scenes (config 5) carry a ~58 KB LDS image, so LDS holds the walk at 2 workgroups per CU
 // whatever the register budget: the uncapped budget wins there (16.46 vs 15.96 M it/s, r02 A/B).
 constexpr int kWalkMinWStar = kWalkMinWWindow;
-#ifdef PP_STAMPS_WALK
-// diagnostic build only (-DPP_STAMPS_WALK): per steer_walk launch, the launch span, the mean and
-// the longest wave lifetime (stamps[0..2], [3] launches), the longest single task ([4]) — the
-// walk's load imbalance
-__device__ unsigned long long g_wspan[6] = {~0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
-struct WalkSpan {
-    DevState* st;
-    unsigned long long t_in = 0, t_task = 0;  // t_task: this wave's longest single task
-    explicit __device__ WalkSpan(DevState* s) : st(s) {
-        t_in = __builtin_amdgcn_s_memrealtime();
-        if ((threadIdx.x & 63) == 0) atomicMin(&g_wspan[0], t_in);
-    }
-    __device__ ~WalkSpan() {
-        if ((threadIdx.x & 63) == 0) {
-            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-            atomicMax(&g_wspan[1], t);
-            atomicMax(&g_wspan[2], t - t_in);
-            atomicAdd(&g_wspan[3], t - t_in);
-            atomicMax(&g_wspan[5], t_task);
-            __threadfence();
-            const unsigned long long waves = (unsigned long long)gridDim.x * (blockDim.x >> 6);
-            if (atomicAdd(&g_wspan[4], 1ull) == waves - 1) {
-                __threadfence();
-                unsigned long long* sp = reinterpret_cast<unsigned long long*>(st->stamps);
-                sp[0] += atomicAdd(&g_wspan[1], 0ull) - atomicAdd(&g_wspan[0], 0ull);
-                sp[1] += atomicAdd(&g_wspan[3], 0ull) / waves;
-                sp[2] += atomicAdd(&g_wspan[2], 0ull);
-                sp[3] += 1;
-                sp[4] += atomicAdd(&g_wspan[5], 0ull);
-                for (int i = 0; i < 3; ++i) sp[5 + i] += atomicExch(&g_cull[i], 0ull);
-                for (int i = 0; i < 6; ++i) atomicExch(&g_wspan[i], i == 0 ? ~0ull : 0ull);
-            }
-        }
-    }
-};
-#endif
 template <bool kLds, int kMinW>
 __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevState* __restrict__ st,
                                                          SceneDev sc,
@@ -2422,33 +1975,18 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
     const int lane = threadIdx.x & 63;
     const int W = st->W;
     const int total = W + st->ncomp;
-#ifdef PP_STAMPS_WALK
-    WalkSpan walk_span(st);
-#endif
-#ifdef PP_WALK_STATIC
-    if ((int)blockIdx.x * (kWalkThreads / 64) >= total) return;  // whole workgroup idle
-#elif defined(PP_WALK_CONTIG)
-    if ((int)blockIdx.x * ((total + (int)gridDim.x - 1) / (int)gridDim.x) >= total) return;
-#else
     if ((int)blockIdx.x >= total) return;
-#endif
     if (kLds) stage_scene(sc);
     double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) +
                  (threadIdx.x >> 6) * kGenSlots;  // this wave's generator slots
     int npts = 0;
-#ifdef PP_WALK_STATIC
-    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    for (int t = gw; t < total; t += nw) {
-#else
     // Workgroup b walks the tasks b, b + G, b + 2G, ... (G = the grid); its waves take them one
     // at a time from an LDS counter, so a wave that drew short paths takes more of them (a
     // workgroup's share is a sum of dozens of tasks: far more even than a wave's handful under a
     // static stride), and consecutive tasks — one query's window, similar paths — land on
-    // different workgroups.  No global atomics.  (-DPP_WALK_CONTIG: contiguous ranges per
-    // workgroup, config 5's walk 10% longer.)
+    // different workgroups.  No global atomics.  (Contiguous ranges per workgroup measured 10%
+    // slower on config 5's walk.)
     __shared__ int s_next;
-#ifndef PP_WALK_CONTIG
     const int G = (int)gridDim.x;
     if (threadIdx.x == 0) s_next = 0;
     __syncthreads();
@@ -2457,25 +1995,7 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
         if (lane == 0) k = atomicAdd(&s_next, 1);
         const int t = (int)blockIdx.x + G * __builtin_amdgcn_readlane(k, 0);
         if (t >= total) break;
-#else
-    const int per = (total + (int)gridDim.x - 1) / (int)gridDim.x;
-    const int t_end = min(total, ((int)blockIdx.x + 1) * per);
-    if (threadIdx.x == 0) s_next = (int)blockIdx.x * per;
-    __syncthreads();
-    for (;;) {
-        int t = 0;
-        if (lane == 0) t = atomicAdd(&s_next, 1);
-        t = __builtin_amdgcn_readlane(t, 0);
-        if (t >= t_end) break;
-#endif
-#endif
-#ifdef PP_STAMPS_WALK
-        const unsigned long long t_t0 = __builtin_amdgcn_s_memrealtime();
-#endif
         const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts);
-#ifdef PP_STAMPS_WALK
-        walk_span.t_task = max(walk_span.t_task, (unsigned long long)__builtin_amdgcn_s_memrealtime() - t_t0);
-#endif
         if (lane == 0) {
             if (t < W) {
                 snap_status[t] = s;
@@ -2526,12 +2046,8 @@ inline int walk_grid_cap(int scene_bytes) {
                                                           kWalkThreads, walk_lds_bytes(0));
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
     per_cu = std::min(kMaxPerCU, per_cu);
-    if (const char* v = std::getenv("PP_WALK_PER_CU")) per_cu = std::max(1, std::min(8, std::atoi(v)));
     const int cap = cus * per_cu;
     cache[{dev, scene_bytes}] = cap;
-    if (std::getenv("PP_DEBUG"))
-        fprintf(stderr, "[pp] walk grid: %d CUs x %d workgroups (LDS image %d B)\n", cus, per_cu,
-                scene_bytes);
     return cap;
 }
 
@@ -2606,7 +2122,6 @@ __device__ __attribute__((always_inline)) inline bool resolve_role(
     auto& s_err = L.err;
     auto& s_stat = L.stat;
     auto& s_bail = L.bail;
-    PP_STAMP(t_0);
     const int Weff = min(W, st->weff);
     const int npend = min(st->npend, KW);
     const int ncomp = st->ncomp;
@@ -2637,7 +2152,6 @@ __device__ __attribute__((always_inline)) inline bool resolve_role(
         s_rep[q] = -1;
     }
     __syncthreads();
-    PP_STAMP(t_1);
     // 2. lists: each entry goes to its sample's segment (then sorted by (d2, i))
     for (int e = tid; e < ncomp; e += NT) {
         const CandEntry ce = cand[e];
@@ -2721,8 +2235,6 @@ __device__ __attribute__((always_inline)) inline bool resolve_role(
         s_ed[k] = ey;
     }
     __syncthreads();
-
-    PP_STAMP(t_2);
     // 3. decisions, without workgroup barriers: every wave passes over its own slots until all of
     //    them are decided, reading the other slots' decisions from LDS as they appear.  A decision
     //    is final once published (its flag is stored last, with release order), and every
@@ -2849,7 +2361,6 @@ __device__ __attribute__((always_inline)) inline bool resolve_role(
     }
     __syncthreads();
     if (!kRepair && s_bail) return false;
-    PP_STAMP(t_3);
     // 4. publish the pending verdicts for window_commit
     for (int q = tid; q < npend; q += NT) {
         const int j = s_j[q];
@@ -2859,18 +2370,6 @@ __device__ __attribute__((always_inline)) inline bool resolve_role(
         snap_yaw[j] = s_yaw[q];
         fin_par[j] = p;
     }
-    PP_STAMP(t_4);
-#ifdef PP_STAMPS_RESOLVE
-    if (tid == 0) {
-        st->stamps[0] += t_1 - t_0;
-        st->stamps[1] += t_2 - t_1;
-        st->stamps[2] += t_3 - t_2;
-        st->stamps[3] += t_4 - t_3;
-        st->stamps[4] += s_stat[3];
-        st->stamps[5] += npend;
-        st->stamps[6] += ncomp;
-    }
-#endif
     if (tid == 0) {
         if (s_err) st->error = 1;
         st->repair_rounds += s_stat[0];
@@ -2988,67 +2487,11 @@ static_assert(kScreenStageOff % 16 == 0 && kScreenStageOff + 3 * kStage * 4 + 16
               "screen staging (x, y, |n-o|^2 of kStage nodes + the piece counter) fits");
 static_assert(kStage % 256 == 0 && kGrab % kScanBlk == 0, "whole DMA quarters and blocks");
 
-#ifdef PP_STAMPS_SPAN
-// diagnostic build only (-DPP_STAMPS_SPAN): per window_kernel launch, the span from the first
-// workgroup's start to the last one's end, the start skew and workgroup 0's end (stamps[0..3])
-__device__ unsigned long long g_span[4] = {~0ull, 0ull, 0ull, 0ull};  // min start, max start, max end, done
-__device__ unsigned long long g_span_wg0, g_span_maxdur, g_span_sumdur;
-__device__ unsigned long long g_wgdur[256];  // per workgroup: summed lifetime over the launches
-__device__ unsigned long long g_wgstart[256];  // per workgroup: summed start offset past the first
-struct SpanStamp {
-    DevState* st;
-    unsigned long long t_in = 0;
-    explicit __device__ SpanStamp(DevState* s) : st(s) {
-        if (threadIdx.x == 0) {
-            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-            t_in = t;
-            atomicMin(&g_span[0], t);
-            atomicMax(&g_span[1], t);
-        }
-    }
-    __device__ ~SpanStamp() {
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-            if (blockIdx.x < 256 && gridDim.x > 1) g_wgdur[blockIdx.x] += t - t_in;
-            if (blockIdx.x == 0) atomicExch(&g_span_wg0, t);
-            else {
-                atomicMax(&g_span_maxdur, t - t_in);
-                atomicAdd(&g_span_sumdur, t - t_in);
-            }
-            atomicMax(&g_span[2], t);
-            __threadfence();
-            if (atomicAdd(&g_span[3], 1ull) == gridDim.x - 1) {
-                __threadfence();
-                const unsigned long long t0 = atomicAdd(&g_span[0], 0ull);
-                const unsigned long long t1 = atomicAdd(&g_span[1], 0ull);
-                const unsigned long long t2 = atomicAdd(&g_span[2], 0ull);
-                const unsigned long long tw = atomicAdd(&g_span_wg0, 0ull);
-                unsigned long long* sp = reinterpret_cast<unsigned long long*>(st->stamps);
-                sp[0] += t2 - t0;
-                sp[1] += t1 - t0;
-                sp[2] += tw - t0;
-                sp[3] += 1;
-                sp[4] += atomicExch(&g_span_maxdur, 0ull);
-                sp[5] += atomicExch(&g_span_sumdur, 0ull) / (gridDim.x > 1 ? gridDim.x - 1 : 1);
-                atomicExch(&g_span[0], ~0ull);
-                atomicExch(&g_span[1], 0ull);
-                atomicExch(&g_span[2], 0ull);
-                atomicExch(&g_span[3], 0ull);
-            }
-        }
-    }
-};
-#endif
 
 __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
     __shared__ __attribute__((aligned(16))) char smem[kWinLds];
-#ifdef PP_STAMPS_SPAN
-    SpanStamp span_stamp(a.st);
-#endif
     if (blockIdx.x == 0) {
         DevState* st = a.st;
-        SCREEN_STAMP(tw0);
         if (a.resolve) {
             const int W = st->W;
             if (W > 0) {
@@ -3062,16 +2505,9 @@ __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
                 }
                 // (same workgroup: the barrier's workgroup-scope fence orders these stores)
                 __syncthreads();
-#ifdef PP_STAMPS_RESOLVE
-                const int64_t tc0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-#endif
                 commit_role<kScanThreads>(st, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.snap_status,
                                           a.snap_yaw, a.fin_par, a.cand_cnt, W,
                                           a.scan ? a.seq : -1, smem);
-#ifdef PP_STAMPS_RESOLVE
-                __syncthreads();
-                if (threadIdx.x == 0) st->stamps[7] += (int64_t)__builtin_amdgcn_s_memrealtime() - tc0;
-#endif
             }
         }
         if (threadIdx.x == 0) {  // the screened window's counters start at zero
@@ -3082,23 +2518,11 @@ __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
             // store there raced with the early finishers)
             st->weff = 0x7fffffff;
         }
-#ifdef PP_STAMPS_SCREEN
-        if (threadIdx.x == 0) {  // [5] workgroup 0's resolve + commit, [7] its launches
-            unsigned long long* sp = reinterpret_cast<unsigned long long*>(st->stamps);
-            atomicAdd(&sp[5], (unsigned long long)((int64_t)__builtin_amdgcn_s_memrealtime() - tw0));
-            atomicAdd(&sp[7], 1ull);
-        }
-#endif
         return;
     }
     if (a.scan) {
-#ifdef PP_SCREEN_MFMA
-        if (a.gen)
-            scan_role_mfma(a, (int)blockIdx.x - 1, smem);
-#else
         if (a.gen)
             scan_role<true>(a, (int)blockIdx.x - 1, smem);
-#endif
         else
             scan_role<false>(a, (int)blockIdx.x - 1, smem);
     }
@@ -3148,10 +2572,7 @@ struct CfPose {
     double x, y, yaw;
 };
 // check_finish workgroup: kCfWaves candidate / finalize edges checked at a time (one per wave)
-#ifndef PP_CF_WAVES
-#define PP_CF_WAVES 4
-#endif
-constexpr int kCfWaves = PP_CF_WAVES;
+constexpr int kCfWaves = 4;
 constexpr int kCfThreads = 64 * kCfWaves;
 
 // pose j of the finalize chain: 0 = goal, 1..s = optimised copies, then path[ps], ..., path[0]
@@ -3195,13 +2616,15 @@ __device__ __forceinline__ void lit_release(int* locks, int slot) {
     if ((threadIdx.x & 63) == 0) atomicExch(&locks[slot], 0);
 }
 
+// returns the verdict | (polyline points walked << 4)
 template <bool kAllowNone>
 __device__ __attribute__((noinline)) int cf_edge_check(const SceneDev& sc, CfPose a, CfPose b,
                                                        bool junction, double* lit_scratch,
                                                        int* lit_locks) {
     const SteerPrep r = steer_prep(sc, a.x, a.y, a.yaw, b.x, b.y, b.yaw);
     if (!kAllowNone && r.state == kPrepNone) return kCfPanic;
-    int st = steer_walk<false>(sc, walk_in(r), nullptr, junction);
+    int walked = 0;
+    int st = steer_walk<false>(sc, walk_in(r), junction, &walked);
     if (st == kLiteral) {  // (measure-zero) a scratch buffer from the pool, for this edge only
         const int slot = lit_acquire(lit_locks, (int)blockIdx.x);
         double* bx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
@@ -3209,7 +2632,7 @@ __device__ __attribute__((noinline)) int cf_edge_check(const SceneDev& sc, CfPos
                                    bx + 2 * kLiteralCap, junction);
         lit_release(lit_locks, slot);
     }
-    return st;
+    return st | (walked << 4);
 }
 
 // n_point of dubins_path_planning(a → b) (dubins.rs:369), 0 when the steer is None
@@ -3240,7 +2663,7 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
     double* __restrict__ len_out,
     int* __restrict__ npts_out, int* __restrict__ chain_out, double* __restrict__ lit_scratch,
     int* __restrict__ lit_locks, double* __restrict__ pts, int pts_cap, int* __restrict__ etab,
-    int* __restrict__ err) {
+    int* __restrict__ err, long long* __restrict__ tally) {
     __shared__ int s_path[kCfMaxDepth];
     __shared__ int s_pos[kCfLevels];
     __shared__ int s_st[kCfWaves];
@@ -3254,11 +2677,13 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
     // node's cost varies with its depth and how far optimize climbs, so a static stride left
     // workgroups holding a few deep nodes as the launch's tail
     __shared__ int s_b;
+    long long t_nodes = 0, t_edges = 0, t_pts = 0;  // this wave's work (profiling: tally)
     for (;;) {
         if (tid == 0) s_b = atomicAdd(&err[1], 1);
         __syncthreads();
         const int b = s_b;
         if (b >= k) break;
+        ++t_nodes;
         // ancestor path, node first (NodeIter, rrt.rs:253-265), then reversed: root first
         if (tid == 0) {
             int d = 0, c = nodes[b];
@@ -3298,7 +2723,10 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
                     const int to = s_path[m];
                     const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
                     const CfPose a{a0.x, a0.y, atan2(bt.y - a0.y, bt.x - a0.x)};
-                    st = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks);
+                    const int rv = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks);
+                    st = rv & 15;
+                    ++t_edges;
+                    t_pts += rv >> 4;
                 }
                 if (lane == 0) s_st[wave] = st;
                 __syncthreads();
@@ -3352,7 +2780,10 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
             if (e < E) {
                 const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                 const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                st = cf_edge_check<false>(sc, a, bp, e < E - 1, lit_scratch, lit_locks);
+                const int rv = cf_edge_check<false>(sc, a, bp, e < E - 1, lit_scratch, lit_locks);
+                st = rv & 15;
+                ++t_edges;
+                t_pts += rv >> 4;
             }
             if (lane == 0) s_st[wave] = st;
             __syncthreads();
@@ -3457,6 +2888,12 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
         }
         __syncthreads();
     }
+    if (tally && lane == 0) {  // profiling: nodes (counted once, by wave 0), edges, points
+        unsigned long long* tl = reinterpret_cast<unsigned long long*>(tally);
+        if (wave == 0) atomicAdd(&tl[0], (unsigned long long)t_nodes);
+        atomicAdd(&tl[1], (unsigned long long)t_edges);
+        atomicAdd(&tl[2], (unsigned long long)t_pts);
+    }
 }
 
 hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev& tr,
@@ -3464,12 +2901,13 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,
                                int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
-                               int grid) {
+                               int grid, long long* tally) {
     if (k <= 0) return hipSuccess;
     check_finish_kernel<<<std::min(grid, k), kCfThreads, 0, st>>>(sc, tr, nodes, k, gx, gy, gyaw,
                                                            gyaw_opt, level0, mode, want_line, ok,
                                                            len, npts, chain, lit_scratch,
-                                                           lit_locks, pts, pts_cap, etab, err);
+                                                           lit_locks, pts, pts_cap, etab, err,
+                                                           tally);
     return hipGetLastError();
 }
 
@@ -3707,10 +3145,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
 // counts live in DevState W (stA: Q, stB / stC: counted on the device), so a step needs no host
 // round trip.
 constexpr int kKnnWaves = 4;
-#ifndef PP_KNN_CACHE
-#define PP_KNN_CACHE 2048
-#endif
-constexpr int kKnnCache = PP_KNN_CACHE;  // d2 values cached per wave (LDS: 4 x 16 KB)
+constexpr int kKnnCache = 2048;  // d2 values cached per wave (LDS: 4 x 16 KB)
 
 __device__ __forceinline__ bool star_feasible(int status, double e) {
     return status == kAccept && e <= 1.7976931348623157e308;  // Some and verified (finite cost)
@@ -4515,27 +3950,5 @@ hipError_t launch_dubins_batch(hipStream_t st, const double* conf, int n, int ca
     return hipGetLastError();
 }
 
-#ifdef PP_STAMPS_SPAN
-// diagnostic build only: per-workgroup window_kernel lifetimes summed over the launches, by XCD
-void diag_dump_window_span(int launches) {
-    unsigned long long d[256];
-    if (hipMemcpyFromSymbol(d, HIP_SYMBOL(g_wgdur), sizeof d) != hipSuccess) return;
-    const double n = launches > 0 ? launches : 1;
-    for (int x = 0; x < 8; ++x) {
-        double mn = 1e30, mx = 0, sum = 0;
-        int c = 0;
-        for (int b = x; b < 256; b += 8) {
-            if (b == 0 || d[b] == 0) continue;
-            const double v = d[b] / n / 100.0;
-            mn = std::min(mn, v), mx = std::max(mx, v), sum += v, ++c;
-        }
-        fprintf(stderr, "[span] XCD %d: %d workgroups, lifetime min %.2f mean %.2f max %.2f us\n", x, c,
-                mn, c ? sum / c : 0.0, mx);
-    }
-    fprintf(stderr, "[span] workgroup 0: %.2f us\n", d[0] / n / 100.0);
-    unsigned long long z[256] = {};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wgdur), z, sizeof z);
-}
-#endif
 
 }  // namespace ppamd

@@ -33,10 +33,7 @@ constexpr int kWalkThreads = 512;    // steer_walk workgroup: 8 tasks at a time 
 constexpr int kCfMaxDepth = 8192;    // check_finish: ancestor path staged in LDS (32 KB)
 constexpr int kCfLevels = 16;        // RECURSION_LIMIT, rrt.rs:14
 constexpr int kCfMaxEdges = kCfLevels + 1 + kCfMaxDepth;
-#ifndef PP_CF_GRID
-#define PP_CF_GRID 256
-#endif
-constexpr int kCfGrid = PP_CF_GRID;  // check_finish workgroups (literal scratch from the pool)
+constexpr int kCfGrid = 256;  // check_finish workgroups (literal scratch from the pool)
 
 // Scene in device memory (Space, rrt.rs:70-78, with Q10 analytic discs).
 struct SceneDev {
@@ -123,7 +120,6 @@ struct DevState {
     // statistics (pp_stats)
     int64_t iterations, accepted, windows, truncations, repair_rounds, repairs, literal_repairs,
         nn_flagged, node_evals;
-    int64_t stamps[8];  // diagnostic build only (PP_STAMPS): accumulated phase times, 100 MHz ticks
 };
 
 // An explicit steer task: child (x, y) steered toward its parent — tree node `pnode` when

@@ -21,6 +21,7 @@ PP_ERR_STATE = -5
 PP_ERR_STEER_OVERFLOW = -6
 PP_ERR_REFERENCE_PANIC = -7
 PP_CF_CHAIN = 18
+PP_ABI_VERSION = 2
 
 _ERR_NAMES = {
     PP_ERR_INVALID_ARGUMENT: "PP_ERR_INVALID_ARGUMENT", PP_ERR_HIP: "PP_ERR_HIP",
@@ -66,13 +67,13 @@ class StatsC(C.Structure):
         ("literal_repairs", C.c_int64), ("nn_flagged", C.c_int64), ("node_evals", C.c_int64),
         ("nn_scan_ms", C.c_double), ("nn_scan_launches", C.c_int64),
         ("steer_ms", C.c_double), ("steer_launches", C.c_int64),
-        ("stamps", C.c_int64 * 8), ("walk_points", C.c_int64),
+        ("walk_points", C.c_int64), ("batch_steps", C.c_int64), ("batch_passes", C.c_int64),
+        ("finish_ms", C.c_double), ("finish_launches", C.c_int64), ("finish_nodes", C.c_int64),
+        ("finish_edges", C.c_int64), ("finish_points", C.c_int64),
     ]
 
     def as_dict(self):
-        d = {k: getattr(self, k) for k, _ in self._fields_}
-        d["stamps"] = list(self.stamps)
-        return d
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 _lock = threading.Lock()
@@ -97,6 +98,10 @@ def lib():
         except ImportError:
             pass
         L = C.CDLL(LIB_PATH)
+        L.pp_abi_version.restype = C.c_int
+        if L.pp_abi_version() != PP_ABI_VERSION:
+            raise PPError(PP_ERR_STATE, f"{LIB_PATH}: ABI {L.pp_abi_version()}, this binding is "
+                                        f"{PP_ABI_VERSION} (rebuild with __graft_entry__.build())")
         dp, ip, i64p = C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
         vp = C.c_void_p
         sig = {
@@ -155,7 +160,7 @@ def lib():
             "pp_star_extend": ([vp, C.c_int64, i64p, i64p, i64p], C.c_int),
             "pp_star_state": ([vp, ip, i64p, i64p, i64p], C.c_int),
             "pp_star_tree_export": ([vp, C.c_int, dp, dp, dp, ip, dp, C.c_int64, i64p], C.c_int),
-            "pp_rrt_get_stats": ([vp, C.POINTER(StatsC)], C.c_int),
+            "pp_rrt_get_stats": ([vp, C.POINTER(StatsC), C.c_uint64], C.c_int),
             "pp_rrt_reset_stats": ([vp], C.c_int),
             "pp_set_profiling": ([vp, C.c_int], C.c_int),
         }

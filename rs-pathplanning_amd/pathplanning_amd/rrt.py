@@ -397,7 +397,7 @@ class RRT:  # rrt.rs:325-620
     # ---------------------------------------------------------------- instrumentation
     def stats(self) -> dict:
         s = _ffi.StatsC()
-        _ffi.check(_ffi.lib().pp_rrt_get_stats(self.ctx.handle, C.byref(s)))
+        _ffi.check(_ffi.lib().pp_rrt_get_stats(self.ctx.handle, C.byref(s), C.sizeof(s)))
         return s.as_dict()
 
     def reset_stats(self):
@@ -462,7 +462,7 @@ class RRTBatch:
 
     def stats(self) -> dict:
         s = _ffi.StatsC()
-        _ffi.check(_ffi.lib().pp_rrt_get_stats(self.ctx.handle, C.byref(s)))
+        _ffi.check(_ffi.lib().pp_rrt_get_stats(self.ctx.handle, C.byref(s), C.sizeof(s)))
         return s.as_dict()
 
     def set_profiling(self, on: bool):
@@ -529,7 +529,7 @@ class RRTStarBatch:
 
     def stats(self) -> dict:
         s = _ffi.StatsC()
-        _ffi.check(_ffi.lib().pp_rrt_get_stats(self.ctx.handle, C.byref(s)))
+        _ffi.check(_ffi.lib().pp_rrt_get_stats(self.ctx.handle, C.byref(s), C.sizeof(s)))
         return s.as_dict()
 
     def tree(self, query: int, n: int | None = None):

@@ -27,7 +27,8 @@ int main(void) {
     OFF(pp_dubins_config, turn_radius); OFF(pp_dubins_config, step_size);
     OFF(pp_stats, iterations); OFF(pp_stats, node_evals); OFF(pp_stats, nn_scan_ms);
     OFF(pp_stats, nn_scan_launches); OFF(pp_stats, steer_ms); OFF(pp_stats, steer_launches);
-    OFF(pp_stats, stamps); OFF(pp_stats, walk_points);
+    OFF(pp_stats, walk_points); OFF(pp_stats, batch_steps); OFF(pp_stats, batch_passes);
+    OFF(pp_stats, finish_ms); OFF(pp_stats, finish_nodes); OFF(pp_stats, finish_points);
     printf("\"rc_circle\": %d, \"rc_small\": %d, \"n_small\": %d, \"n\": %d, ", rc_circle,
            rc_small, n_small, n);
     printf("\"xy\": [");
