@@ -8,13 +8,19 @@ replica tree on its own GPU (seed 42 + rank): weak scaling, `value` = all ranks'
 slowest rank's time.
 
 Sub-results on the same line (the rows of SURVEY.md §8d the driver would not see otherwise):
-  config3  8192 independent queries sharded contiguously over the N ranks (strong scaling), one
-           all_gather of per-query records over RCCL (nccl) when every rank has its own GPU;
-           `records_digest` is the same at every N when the sharded run equals the 1-rank run
-  config5  the RRT* query batch (build-defined, stretch), sharded the same way
-  config4  config 2 on the 512x512 bit-packed occupancy grid (N = 1 only)
-  config1  the reference's own bench scene (benches/all.rs:8-46), 8000 iterations (N = 1 only)
-  plan     RRT::plan on bench6_open: extend + check_finish of every accepted node (N = 1 only)
+  config3          8192 independent queries sharded contiguously over the N ranks (strong
+                   scaling), one all_gather of per-query records over RCCL (nccl) when every rank
+                   has its own GPU; `records_digest` is the same at every N when the sharded run
+                   equals the 1-rank run
+  config5          the RRT* query batch (build-defined, stretch), sharded the same way
+  config4          config 2 on the 512x512 bit-packed occupancy grid (N = 1 only)
+  polygons         config 2 with the 1024 discs as the crate's create_circle polygons (N = 1)
+  config1          the reference's own bench scene (benches/all.rs:8-46), 8000 iterations, analytic
+                   discs (N = 1 only)
+  config1_polygons the same scene as the bench builds it: create_circle polygons (N = 1 only)
+  plan             RRT::plan on bench6_open: extend + check_finish of every accepted node (N = 1)
+  example_rrt      examples/rrt: RRT::plan on the example's own scene (transit.debug.json,
+                   Robot::new(1.8, 3.0, 0.8), 8000 iterations) (N = 1 only)
 
 `python bench.py --gpus N` without WORLD_SIZE starts N rank processes itself (before anything
 touches the GPU); under torchrun it is one of them.  Prints ONE JSON line (rank 0).  See DESIGN.md
@@ -37,13 +43,28 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "rs-pathplanning_amd"))
 
 F32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, Peak FP32 (vector), spec
+# AMD Instinct MI355X datasheet, FP64 vector (spec).  MI355X_MICROARCH.md has no FP64 row.
+FP64_VALU_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md, HBM3E peak, spec
 CLOCK_GHZ = 2.4               # MI355X_MICROARCH.md, max clock
 VALU_CYC = 2                  # cycles per wave64 VALU instruction on a SIMD-32 (MICROARCH: v_fma_f32)
 FLOP_PER_EVAL = 5             # dx, dy (2 sub), dx*dx (mul), + dy*dy (fma = 2)
 BYTES_PER_EVAL = 8            # f32 x + f32 y of one SoA node
+# Algorithmic f64 work of one polyline point of the walk (dubins.rs:155-198 interpolate, 239-255
+# the pd walk, 412-422 the world transform; rrt.rs:124-137 the bounds test), counted from the
+# reference's expressions:
+#   L/R point: sin + cos of the arc length (SINCOS_FLOP: a Cody-Waite reduction ~8 FLOP and two
+#              degree-13/14 minimax polynomials ~32 FLOP, ocml's sincos), ldx = sin/c (1),
+#              ldy = (1 - cos)/c (2), gdx / gdy = rotate by the segment origin (6), + origin (2)
+#   S point:   x/y = origin + pd/c * cos/sin(origin yaw) (6)
+#   both:      world transform (8: 4 mul, 4 add), pd += d (1), bounds (4 compares)
+# The per-disc segment tests are not counted: the chunk cull passes < 1 disc per 63 points.
+SINCOS_FLOP = 40
+ARC_POINT_FLOP = SINCOS_FLOP + 11 + 8 + 1 + 4
+LINE_POINT_FLOP = 6 + 8 + 1 + 4
 METRIC = "RRT extend iterations/sec (2D Dubins, 1k obstacles)"
-WORKLOADS = ("default", "config1", "config2", "config3", "config4", "polygons", "config5", "plan")
+WORKLOADS = ("default", "config1", "config1_polygons", "config2", "config3", "config4",
+             "polygons", "config5", "plan", "example_rrt")
 
 
 def parse(argv=None):
@@ -54,8 +75,9 @@ def parse(argv=None):
                     help="default: config 2 + the sub-results; config2/config4/polygons: one tree, "
                          "K-candidate windows (config4: 512x512 occupancy grid; polygons: "
                          "create_circle polygons, SURVEY §8f row 3); config3: independent queries "
-                         "sharded over the ranks; config5: RRT* query batch; config1: the "
-                         "reference's bench scene; plan: RRT::plan with check_finish")
+                         "sharded over the ranks; config5: RRT* query batch; config1 / "
+                         "config1_polygons: the reference's bench scene; plan / example_rrt: "
+                         "RRT::plan with check_finish")
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (windows for the one-tree workloads, default 20; lockstep "
                          "iterations for the batches, default max_iter)")
@@ -85,10 +107,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def spawn_ranks(n):
+def spawn_ranks(n, timeout=1800):
     """`--gpus N` without a launcher: N child processes of this script with RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_* set, started before this process touches the GPU (it never does).
-    Returns the worst exit code; rank 0 prints the JSON line."""
+    Returns the worst exit code; rank 0 prints the JSON line.  A rank that fails ends the run:
+    the others are terminated (a peer stuck in a collective would wait for it forever)."""
     env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                 WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
     procs = []
@@ -96,10 +119,28 @@ def spawn_ranks(n):
         env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
+    deadline = time.time() + timeout
     rc = 0
-    for p in procs:
-        c = p.wait()
-        rc = rc or c
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0:
+                rc = rc or c
+        if rc or time.time() > deadline:
+            for p in live:
+                p.terminate()
+            for p in live:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            rc = rc or 124
+            break
+        time.sleep(0.2)
     return rc
 
 
@@ -123,6 +164,8 @@ class Dist:
         self.dist = None
         self.gather_backend = None
         if self.world > 1:
+            import datetime
+
             import torch
             import torch.distributed as dist
 
@@ -135,7 +178,8 @@ class Dist:
             else:
                 backend = "gloo"
                 self.gather_backend = "gloo"
-            dist.init_process_group(backend=backend, rank=self.rank, world_size=self.world)
+            dist.init_process_group(backend=backend, rank=self.rank, world_size=self.world,
+                                    timeout=datetime.timedelta(seconds=600))
             assert dist.get_world_size() == self.world
             self.dist = dist
 
@@ -156,23 +200,13 @@ class Dist:
 
     def gather_records(self, rec):
         """Every rank's per-query records (int64 [q_rank, C]) to every rank: one all_gather of
-        the padded blocks (RCCL over xGMI when gather_backend is nccl)."""
+        the padded blocks (RCCL over xGMI when gather_backend is nccl).  An RCCL failure is not
+        papered over: it raises, and the run ends (spawn_ranks stops the peers)."""
         import torch
 
         if self.dist is None:
             return torch.from_numpy(rec)
-        if self.gather_backend == "nccl":
-            try:
-                return self._gather(rec, torch.device("cuda", self.device))
-            except Exception as e:  # RCCL refused (it raises on every rank): the CPU group
-                print(f"[bench] RCCL all_gather failed ({e}); gathering over gloo",
-                      file=sys.stderr, flush=True)
-                self.gather_backend = "gloo (RCCL failed)"
-        return self._gather(rec, None)
-
-    def _gather(self, rec, dev):
-        import torch
-
+        dev = torch.device("cuda", self.device) if self.gather_backend == "nccl" else None
         n = torch.tensor([rec.shape[0]], dtype=torch.int64, device=dev)
         sizes = [torch.zeros_like(n) for _ in range(self.world)]
         self.dist.all_gather(sizes, n)
@@ -207,7 +241,7 @@ def provenance(args):
                          "(--allow-variant-lib for experiments)")
     with open(_ffi.LIB_PATH, "rb") as f:
         sha = hashlib.sha256(f.read()).hexdigest()[:16]
-    # the library's run-time knobs (stream splits, A/B switches): a line taken with any set says so
+    # PP_* variables in the environment (the library itself reads none; recorded for the record)
     knobs = {k: v for k, v in sorted(os.environ.items()) if k.startswith("PP_")}
     return {"lib": os.path.relpath(_ffi.LIB_PATH, ROOT), "lib_sha256_16": sha,
             "hipcc_flags": " ".join(g.HIPCC_FLAGS), "variant": bool(os.environ.get("PP_AMD_LIB")),
@@ -250,27 +284,10 @@ def oracle_mod():
     return oracle
 
 
-# ------------------------------------------------------------------------- one tree (config 2/4)
-def make_planner(raw, seed, window, device, capacity=1 << 18):
-    from pathplanning_amd import rrt
-
-    sx, sy, syaw = raw["start"]
-    gx, gy, gyaw = raw["goal"]
-    return rrt.RRT((sx, sy), syaw, (gx, gy), gyaw, raw["max_iter"], raw["step_size"],
-                   rrt.Space.from_raw(raw), seed=seed, window=window, device=device,
-                   capacity=capacity)
-
-
-STAT_KEYS = ("iterations", "accepted", "windows", "truncations", "repair_rounds", "repairs",
-             "literal_repairs", "nn_flagged")
-
-
-def timed_windows(p, n_windows, window):
-    p.synchronize()
-    t0 = time.perf_counter()
-    p.extend(n_windows * window)
-    p.synchronize()
-    return time.perf_counter() - t0
+# ------------------------------------------------------------------------------ rooflines
+def walk_flop(points, arc_points):
+    """Algorithmic f64 FLOP of `points` walked polyline points, `arc_points` of them on L/R."""
+    return arc_points * ARC_POINT_FLOP + (points - arc_points) * LINE_POINT_FLOP
 
 
 def screen_roofline(sp, pmc):
@@ -311,37 +328,103 @@ def screen_roofline(sp, pmc):
     return r
 
 
-def walk_roofline(sp, pmc, name):
-    """steer_walk (f64 Dubins interpolation + collision): polyline points per second against the
-    walk's VALU instruction-issue bound (VALU instructions per point from the committed PMC pass)."""
-    launches = max(sp["steer_launches"], 1)
-    if not sp["steer_launches"] or not sp.get("walk_points"):
+def fp64_roofline(kernel, ms, launches, points, arc_points, pmc=None, measured=""):
+    """A walk-type kernel (f64 Dubins interpolation + collision per polyline point): the
+    algorithmic FLOP of the points it walked (walk_flop) / its HIP-event time against the FP64
+    vector peak; the PMC VALU count per point (when a counter pass exists) beside it."""
+    if not launches or not points or ms <= 0:
         return None
-    avg_ms = sp["steer_ms"] / launches
-    pts = sp["walk_points"] / launches
-    achieved = pts / (avg_ms * 1e-3)
-    r = {"kernel": f"steer_walk ({name})", "bound": "valu", "achieved": round(achieved / 1e9, 4),
-         "unit": "Gpoints/s", "avg_launch_ms": round(avg_ms, 5), "points_per_launch": int(pts),
-         "launches": int(sp["steer_launches"]),
-         "traffic": pmc.get("hbm_bytes_per_launch"),
-         "measured": f"HIP events around steer_walk, {sp['steer_launches']} launches of the "
-                     "profiled pass"}
-    vpp = pmc.get("valu_insts_per_point")
+    avg_ms = ms / launches
+    flop = walk_flop(points, arc_points) / launches
+    achieved = flop / (avg_ms * 1e-3) / 1e12
+    r = {"kernel": kernel, "bound": "fp64-valu", "achieved": round(achieved, 4),
+         "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+         "frac": round(achieved / FP64_VALU_PEAK_TFLOPS, 5),
+         "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+         "avg_launch_ms": round(avg_ms, 5), "launches": int(launches),
+         "points_per_launch": int(points / launches),
+         "arc_points_per_launch": int(arc_points / launches),
+         "flop_per_launch": int(flop),
+         "flop_per_point": {"arc": ARC_POINT_FLOP, "line": LINE_POINT_FLOP,
+                            "sincos": SINCOS_FLOP},
+         "gpoints_per_s": round(points / launches / (avg_ms * 1e-3) / 1e9, 4),
+         "peak_source": "AMD MI355X datasheet FP64 vector 78.6 TFLOP/s (spec; the guide has no "
+                        "FP64 row)",
+         "measured": measured}
+    vpp = (pmc or {}).get("valu_insts_per_point")
     if vpp:
         simds = 4 * pmc.get("cus", 256)
-        peak = simds * CLOCK_GHZ * 1e9 / (vpp / 64.0 * VALU_CYC)
-        r.update(peak=round(peak / 1e9, 4), frac=round(achieved / peak, 4),
-                 valu_insts_per_point=vpp,
-                 note="peak = points/s if every SIMD issued one wave64 VALU instruction per 2 "
-                      "cycles at 2.4 GHz with the measured instruction count per point (f64 and "
-                      "transcendental instructions take longer: the true bound is lower)")
+        issue_peak = simds * CLOCK_GHZ * 1e9 / (vpp / 64.0 * VALU_CYC)
+        r["issue"] = {"valu_insts_per_point": vpp,
+                      "points_per_s_at_issue_rate": round(issue_peak / 1e9, 3),
+                      "frac_of_issue_rate": round(points / launches / (avg_ms * 1e-3) / issue_peak, 4),
+                      "note": "the measured VALU instruction count per point at one wave64 "
+                              "instruction per 2 cycles per SIMD: the instruction-issue ceiling "
+                              "of the code as compiled"}
     return r
+
+
+def walk_roofline(sp, pmc, name):
+    return fp64_roofline(f"steer_walk ({name})", sp["steer_ms"], sp["steer_launches"],
+                         sp.get("walk_points", 0), sp.get("walk_arc_points", 0), pmc,
+                         f"HIP events around steer_walk, {sp['steer_launches']} launches of the "
+                         "profiled pass (the timed schedule's streams)")
+
+
+def finish_roofline(sp):
+    """check_finish_kernel (goal connection): the optimize candidates' and finalize's edges
+    (steer + verify, the same per-point walk) against the FP64 peak."""
+    r = fp64_roofline("check_finish_kernel", sp.get("finish_ms", 0.0),
+                      sp.get("finish_launches", 0), sp.get("finish_points", 0),
+                      sp.get("finish_arc_points", 0), None,
+                      "HIP events around check_finish_kernel in a profiled run of the same plan")
+    if r:
+        r["nodes"] = int(sp.get("finish_nodes", 0))
+        r["edges"] = int(sp.get("finish_edges", 0))
+        r["edges_per_node"] = round(sp.get("finish_edges", 0) / max(sp.get("finish_nodes", 1), 1), 2)
+    return r
+
+
+def window_chain(sp):
+    """Per-window device time of each kernel of the window pipeline, µs."""
+    w = max(sp["nn_scan_launches"], 1)
+    return {"window_kernel": round(1e3 * sp["nn_scan_ms"] / w, 2),
+            "nn_finalize": round(1e3 * sp["finalize_ms"] / w, 2),
+            "steer_prep": round(1e3 * sp["prep_ms"] / w, 2),
+            "steer_walk": round(1e3 * sp["steer_ms"] / w, 2),
+            "windows": int(sp["nn_scan_launches"])}
+
+
+# ------------------------------------------------------------------------- one tree (config 2/4)
+def make_planner(raw, seed, window, device, capacity=1 << 18):
+    from pathplanning_amd import rrt
+
+    sx, sy, syaw = raw["start"]
+    gx, gy, gyaw = raw["goal"]
+    return rrt.RRT((sx, sy), syaw, (gx, gy), gyaw, raw["max_iter"], raw["step_size"],
+                   rrt.Space.from_raw(raw), seed=seed, window=window, device=device,
+                   capacity=capacity)
+
+
+STAT_KEYS = ("iterations", "accepted", "windows", "truncations", "repair_rounds", "repairs",
+             "literal_repairs", "nn_flagged")
+
+
+def timed_windows(p, n_windows, window):
+    p.synchronize()
+    t0 = time.perf_counter()
+    p.extend(n_windows * window)
+    p.synchronize()
+    return time.perf_counter() - t0
+
+
+TREE_TAG = {"config2": "", "config4": "_config4", "polygons": "_polygons"}
 
 
 def run_tree(args, D, raw, workload, with_cpu):
     """Config 2 / 4 / polygons: grow a tree to args.nodes (untimed; windows at ~1k and ~10k nodes
     timed on the way), W warmup windows, then `steps` windows timed back to back, then a profiled
-    pass of as many windows (HIP events around the screen and the walk)."""
+    pass of as many windows (HIP events around every kernel)."""
     steps = args.steps or 20
     p = make_planner(raw, args.seed + D.rank, args.window, D.device)
     sweep = {}
@@ -381,13 +464,14 @@ def run_tree(args, D, raw, workload, with_cpu):
     p.synchronize()
     p.set_profiling(False)
     sp = p.stats()
-    tag = {"config2": "", "config4": "_config4", "polygons": "_polygons"}[workload]
+    tag = TREE_TAG[workload]
     res = {
         "value": iters_total / t_max, "t_max": t_max, "steps": steps, "n_start": n_start,
         "node_evals_per_s_per_gpu": round(st["node_evals"] / t_local, 1),
         "sizes": sweep, "stats": {k: st[k] for k in STAT_KEYS},
         "roofline": screen_roofline(sp, load_profile(f"window_kernel_pmc{tag}.json")),
         "walk_roofline": walk_roofline(sp, load_profile(f"steer_walk_pmc{tag}.json"), workload),
+        "window_chain_us": window_chain(sp),
     }
     if with_cpu:
         res["cpu_baseline"] = cpu_baseline_tree(raw, p, args)
@@ -433,10 +517,10 @@ def cpu_baseline_tree(raw, p, args):
         "value": round(threads * per / t, 2), "unit": "iterations/s", "cores": threads,
         "kind": "port",
         "sample": f"{threads} independent replicas on {threads} host threads, each continuing the "
-                  f"same {n}-node tree for {per} iterations (seeds {args.seed + 1000}..), "
-                  f"re-verifying the whole line to the root like rrt.rs:414-426, exact brute-force "
-                  f"NN (the crate's R-tree is rstar, not buildable here); "
-                  f"{threads * per} iterations in {t:.1f} s wall",
+                  f"same {n}-node tree ({raw.get('name', 'scene')}) for {per} iterations (seeds "
+                  f"{args.seed + 1000}..), re-verifying the whole line to the root like "
+                  f"rrt.rs:414-426, exact brute-force NN (the crate's R-tree is rstar, not "
+                  f"buildable here); {threads * per} iterations in {t:.1f} s wall",
         "one_core": {"value": round(v, 2), "iterations": nn, "seconds": round(tt, 2)},
         "incremental_verify_one_core": {"value": round(vi, 2), "iterations": ni,
                                         "seconds": round(ti, 2)},
@@ -464,7 +548,7 @@ def run_batch(args, D, star, with_cpu):
     """Config 3 (star=False) / config 5 (star=True): args.queries independent planners, sharded
     contiguously over the ranks; a step = one lockstep iteration of every query of the rank; the
     timed region is the whole max_iter-step run of a fresh batch after an untimed warmup batch;
-    then a profiled pass of the same run (HIP events around the NN and the walk)."""
+    then a profiled pass of the same run, on the same streams (HIP events around every kernel)."""
     from pathplanning_amd import rrt, scenes
 
     raw = scenes.config5_field() if star else scenes.field512()
@@ -492,6 +576,7 @@ def run_batch(args, D, star, with_cpu):
     D.barrier()
     stt = batch.state()
     n, its = stt[0], stt[1]
+    st_timed = batch.stats()
     dig = batch_digests(batch, star)
     rec = np.stack([np.arange(a, b, dtype=np.int64), its.astype(np.int64), n.astype(np.int64),
                     dig], 1)
@@ -501,7 +586,12 @@ def run_batch(args, D, star, with_cpu):
     extra = {}
     if star:
         extra["rewires_total"] = int(D.allreduce(float(stt[3].sum()), "sum"))
-    # profiled pass (same workload): HIP events around the NN and the walks of every step
+    else:
+        extra["passes"] = {"steps": int(st_timed["batch_steps"]),
+                           "host_passes": int(st_timed["batch_passes"]),
+                           "ideal_steps": -(-steps // (args.batch_window or
+                                                       auto_batch_window(b - a)))}
+    # profiled pass (same workload, same streams): HIP events around every kernel of every step
     batch.close()
     batch = fresh()
     batch.set_profiling(True)
@@ -517,6 +607,7 @@ def run_batch(args, D, star, with_cpu):
     # the counter passes were taken on the whole 8192-query batch on one GPU
     pmc = load_profile("batch_pmc.json").get(wl, {}) if args.queries == 8192 and D.world == 1 else {}
     nn_share = sp["nn_scan_ms"] / max(sp["nn_scan_ms"] + sp["steer_ms"], 1e-9)
+    launches = max(sp["nn_scan_launches"], 1)
     res = {
         "value": round(iters_total / t_max, 1),
         "unit": "iterations/s",
@@ -544,6 +635,14 @@ def run_batch(args, D, star, with_cpu):
         },
         **extra,
     }
+    if not star:
+        res["step_chain_us"] = {"mq_sample_nn": round(1e3 * sp["nn_scan_ms"] / launches, 2),
+                                "steer_prep": round(1e3 * sp["prep_ms"] / launches, 2),
+                                "steer_walk": round(1e3 * sp["steer_ms"] / launches, 2),
+                                "mq_insert": round(1e3 * sp["insert_ms"] / launches, 2),
+                                "launches_per_kernel": int(launches),
+                                "note": "per launch, each sub-batch stream's launch counted "
+                                        "(the schedule of the timed region)"}
     if star:
         res["workload"] = (f"config5 (stretch, build-defined RRT*): {args.queries} queries on "
                            f"{raw['name']} (10240 discs r~U(1,4) on 2048^2), Steer eta {eta}, "
@@ -631,15 +730,35 @@ def cpu_baseline_star(raw, starts, seeds, max_iter, eta, seconds):
             "host": host_info()}
 
 
-# ------------------------------------------------------------------ config 1 and plan (bench6)
-def run_config1(args, D, with_cpu):
+# ------------------------------------------------------ config 1, plan and the example (bench6)
+def dominant_kernel(sp, pmc_tag="", walk_name="walk"):
+    """The kernel of the window chain with the largest device time and its algorithmic roofline
+    (a short run of small trees is latency-bound: the chain's 4 dependent launches per window)."""
+    chain = window_chain(sp)
+    times = {k: v for k, v in chain.items() if k != "windows"}
+    dom = max(times, key=times.get)
+    if dom == "window_kernel":
+        r = screen_roofline(sp, {})
+    else:
+        r = walk_roofline(sp, {}, walk_name) or {}
+        r = dict(r)
+        if dom != "steer_walk":
+            r["note"] = f"{dom} has the largest share; the walk's roofline is shown"
+    r["dominant"] = dom
+    r["window_chain_us"] = chain
+    return r
+
+
+def run_config1(args, D, with_cpu, polygons=False):
     """BASELINE config 1: the reference's only fully specified scene (benches/all.rs:8-42) —
     8000 plan_one extend iterations (plan_one minus check_finish, rrt.rs:583-589) of one query
-    from a fresh tree.  GPU: the whole run per window size K (results identical for every K);
-    CPU: the C port's sequential run on one core with the reference's full re-verify."""
+    from a fresh tree.  GPU: the whole run per window size K (results identical for every K),
+    then a profiled run at the best K; CPU: the C port's sequential run on one core with the
+    reference's full re-verify.  polygons: the obstacles as the crate's create_circle polygons
+    and the bounds as a ring, the way benches/all.rs:12-28 builds them (Q10p)."""
     from pathplanning_amd import scenes
 
-    raw = scenes.bench6()
+    raw = scenes.bench6_polygons() if polygons else scenes.bench6()
     n_iter = raw["max_iter"]
     runs = {}
     for K in (32, 128, 512, 4096):
@@ -658,10 +777,20 @@ def run_config1(args, D, with_cpu):
                         "nodes": acc + 1, "stats": {k: st[k] for k in STAT_KEYS}}
         runs[str(K)] = best
     kbest = max(runs, key=lambda k: runs[k]["iterations_per_s"])
+    p = make_planner(raw, args.seed, int(kbest), D.device, capacity=1 << 14)
+    p.set_profiling(True)
+    p.extend(n_iter)
+    p.synchronize()
+    sp = p.stats()
+    p.close()
+    name = "config1_polygons" if polygons else "config1"
+    geom = ("create_circle polygons + ring bounds, exact Minkowski buffers (Q10p)" if polygons
+            else "analytic discs r + w/2 (Q10)")
     res = {"value": runs[kbest]["iterations_per_s"], "unit": "iterations/s", "window": int(kbest),
-           "workload": "config1: bench6 (benches/all.rs:8-42: 6 discs, R 0.8, step 0.1), seed "
-                       f"{args.seed}, {n_iter} iterations from the root",
-           "per_window": runs}
+           "workload": f"{name}: bench6 (benches/all.rs:8-42: 6 obstacles, R 0.8, step 0.1; "
+                       f"{geom}), seed {args.seed}, {n_iter} iterations from the root",
+           "per_window": runs,
+           "roofline": dominant_kernel(sp, walk_name=name)}
     if with_cpu:
         oracle = oracle_mod()
         sc = oracle.OracleScene.from_raw(raw)
@@ -677,13 +806,16 @@ def run_config1(args, D, with_cpu):
     return res
 
 
-def run_plan(args, D, with_cpu):
-    """RRT::plan (rrt.rs:599-619) on bench6_open, sequential spec: 8000 plan_one iterations with
-    check_finish (optimize + finalize + verify, rrt.rs:428-540) on every accepted node, the first
-    minimum euclidean_length.  GPU pp_rrt_plan against the C port's plan on one core."""
+def run_plan(args, D, with_cpu, example=False):
+    """RRT::plan (rrt.rs:599-619), sequential spec: 8000 plan_one iterations with check_finish
+    (optimize + finalize + verify, rrt.rs:428-540) on every accepted node, the first minimum
+    euclidean_length.  GPU pp_rrt_plan (two runs, the second timed; then a profiled run for the
+    check_finish_kernel roofline) against the C port's plan on one core.  example: the scene of
+    examples/rrt (transit.debug.json, Robot::new(1.8, 3.0, 0.8), RRT::new(.., 8000, 0.1, ..),
+    examples/rrt/src/main.rs:44-75) instead of bench6_open."""
     from pathplanning_amd import scenes
 
-    raw = scenes.bench6_open()
+    raw = scenes.transit() if example else scenes.bench6_open()
     n_iter = raw["max_iter"]
     best = None
     for rep in range(2):
@@ -705,9 +837,19 @@ def run_plan(args, D, with_cpu):
                 "check_finish_nodes": len(nodes),
                 "check_finish_ms": round(1e3 * dcf, 3),
                 "check_finish_per_s": round(len(nodes) / dcf, 1)}
+    p = make_planner(raw, args.seed, 512, D.device, capacity=1 << 14)
+    p.set_profiling(True)
+    p.plan(n_iter)
+    sp = p.stats()
+    p.close()
+    scene = ("examples/rrt: transit.debug.json (20-vertex bounds ring, 3 polygon obstacles), "
+             "Robot(1.8, 3.0, 0.8)" if example else
+             "bench6_open (bench6 scene, start (-3, -3, 45 deg))")
     res = {"value": best["plan_calls_per_s"], "unit": "plan_one calls/s (with check_finish)",
-           "workload": f"plan: bench6_open (bench6 scene, start (-3, -3, 45 deg)), seed "
-                       f"{args.seed}, RRT::plan with {n_iter} iterations", **best}
+           "workload": f"{'example_rrt' if example else 'plan'}: {scene}, seed {args.seed}, "
+                       f"RRT::plan with {n_iter} iterations", **best,
+           "roofline": finish_roofline(sp),
+           "extend_window_chain_us": window_chain(sp)}
     if with_cpu:
         oracle = oracle_mod()
         sc = oracle.OracleScene.from_raw(raw)
@@ -721,8 +863,9 @@ def run_plan(args, D, with_cpu):
             "kind": "port",
             "sample": f"the same plan (seed {args.seed}, {n_iter} iterations, full re-verify), "
                       f"sequential, {t:.2f} s; best node {obn}, length {obl:.6f}",
-            "same_answer": bool(obn == best["best_node"] and abs(obl - best["best_length"])
-                                <= 1e-9 * max(1.0, abs(obl)))}
+            "same_answer": bool(obn == best["best_node"] and
+                                (obn < 0 or abs(obl - best["best_length"])
+                                 <= 1e-9 * max(1.0, abs(obl))))}
     return res
 
 
@@ -761,6 +904,7 @@ def tree_line(args, D, workload, raw, res):
         "stats": res["stats"],
         "roofline": res["roofline"],
         "walk_roofline": res["walk_roofline"],
+        "window_chain_us": res["window_chain_us"],
         "cpu_baseline": res.get("cpu_baseline"),
     }
 
@@ -783,12 +927,23 @@ def batch_line(args, D, res, star):
     return line
 
 
-def sub(fn, *a):
-    """A sub-result: its dict, or the error that stopped it (the headline line still prints)."""
+def sub(D, fn, *a):
+    """A sub-result: its dict, or the error that stopped it (the headline line still prints).
+    With several ranks a failure is raised instead: a rank that skipped a collective the others
+    entered would leave them waiting (spawn_ranks then ends the run)."""
     try:
         return fn(*a)
     except Exception as e:  # noqa: BLE001 — reported in the line, never hidden
+        if D.world > 1:
+            raise
         return {"error": f"{type(e).__name__}: {e}"}
+
+
+def tree_sub(args, D, raw, workload, cpu):
+    ta = argparse.Namespace(**vars(args))
+    ta.no_size_sweep = True
+    return {k: v for k, v in run_tree(ta, D, raw, workload, cpu).items()
+            if k not in ("sizes", "t_max")}
 
 
 def main():
@@ -809,26 +964,26 @@ def main():
         if wl == "default" and not args.no_sub:
             sa = argparse.Namespace(**vars(args))
             sa.steps = None  # the batches run their whole max_iter
-            line["config3"] = sub(run_batch, sa, D, False, cpu)
-            line["config5"] = sub(run_batch, sa, D, True, False)
+            line["config3"] = sub(D, run_batch, sa, D, False, cpu)
+            line["config5"] = sub(D, run_batch, sa, D, True, cpu)
             if D.world == 1:
-                ta = argparse.Namespace(**vars(args))
-                ta.no_size_sweep = True
-                line["config4"] = sub(lambda: {k: v for k, v in run_tree(
-                    ta, D, scenes.field512_grid(), "config4", False).items()
-                    if k not in ("sizes", "t_max")})
-                line["config1"] = sub(run_config1, args, D, cpu)
-                line["plan"] = sub(run_plan, args, D, cpu)
+                line["config4"] = sub(D, tree_sub, args, D, scenes.field512_grid(), "config4", cpu)
+                line["polygons"] = sub(D, tree_sub, args, D, scenes.field512_polygons(),
+                                       "polygons", cpu)
+                line["config1"] = sub(D, run_config1, args, D, cpu)
+                line["config1_polygons"] = sub(D, run_config1, args, D, cpu, True)
+                line["plan"] = sub(D, run_plan, args, D, cpu)
+                line["example_rrt"] = sub(D, run_plan, args, D, cpu, True)
     elif wl in ("config3", "config5"):
         line = batch_line(args, D, run_batch(args, D, wl == "config5", cpu), wl == "config5")
-    elif wl == "config1":
-        res = run_config1(args, D, cpu)
+    elif wl in ("config1", "config1_polygons"):
+        res = run_config1(args, D, cpu, wl == "config1_polygons")
         line = {"metric": METRIC, "n_gpus": D.world, "steps": 1, "warmup": 1,
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                 "data": "synthetic", **res}
-    else:  # plan
-        res = run_plan(args, D, cpu)
-        line = {"metric": "RRT::plan calls/sec (plan_one with check_finish, bench6_open)",
+    else:  # plan / example_rrt
+        res = run_plan(args, D, cpu, wl == "example_rrt")
+        line = {"metric": "RRT::plan calls/sec (plan_one with check_finish)",
                 "n_gpus": D.world, "steps": 1, "warmup": 1, "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
                 **res}

@@ -60,11 +60,18 @@ typedef struct pp_stats {
     int64_t literal_repairs;  /* candidates re-run on the literal single-lane path */
     int64_t nn_flagged;       /* samples whose f32 NN screen needed the exact f64 rescan */
     int64_t node_evals;       /* sample-node distance evaluations of the NN screen */
-    double nn_scan_ms;        /* device time of nn_scan, or of the batch NN (HIP events; profiling on) */
+    /* HIP events around every kernel of a window / batch step (profiling on), summed over the
+     * launches; the batches keep their timed schedule (sub-batch streams) while profiled */
+    double nn_scan_ms;        /* window_kernel (the NN screen + the previous window's resolve), or
+                                 the batch NN (mq_sample_nn / star_sample) */
     int64_t nn_scan_launches;
-    double steer_ms;          /* device time of steer_walk (HIP events; profiling on) */
+    double steer_ms;          /* steer_walk */
     int64_t steer_launches;
+    double finalize_ms;       /* nn_finalize (one tree: one launch per nn_scan launch) */
+    double prep_ms;           /* steer_prep (one launch per steer launch) */
+    double insert_ms;         /* mq_insert (query batch: one launch per nn_scan launch) */
     int64_t walk_points;      /* polyline points the steer walk generated and verified (profiling on) */
+    int64_t walk_arc_points;  /* ... of them on L / R segments (one sincos each) */
     int64_t batch_steps;      /* query batches: lockstep steps launched (each up to the window per query) */
     int64_t batch_passes;     /* query batches: host passes (the first plus the top-ups of stopped windows) */
     double finish_ms;         /* device time of check_finish_kernel (HIP events; profiling on) */
@@ -72,6 +79,7 @@ typedef struct pp_stats {
     int64_t finish_nodes;     /* nodes check_finish ran on (profiling on) */
     int64_t finish_edges;     /* Dubins edges steered + verified by check_finish (profiling on) */
     int64_t finish_points;    /* polyline points those edges walked (profiling on) */
+    int64_t finish_arc_points;  /* ... of them on L / R segments */
 } pp_stats;
 
 int pp_abi_version(void);

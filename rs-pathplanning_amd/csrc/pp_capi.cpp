@@ -88,7 +88,6 @@ struct HBuf {  // pinned host staging
 };
 
 constexpr int kMaxBatch = 64;  // windows enqueued between two host synchronisations
-constexpr int kWalkTallySlots = 4096;
 constexpr int kScreenPad = 64;  // f32 screen copies: the LDS-DMA reads whole float4s (<= 3 floats past)
 
 }  // namespace
@@ -215,15 +214,16 @@ struct pp_ctx {
     // ---- profiling
     bool prof = false;
     std::vector<hipEvent_t> ev;  // 4 per window or batch step, 8 per RRT* step
-    double nn_scan_ms = 0.0, steer_ms = 0.0, finish_ms = 0.0;
+    double nn_scan_ms = 0.0, steer_ms = 0.0, finish_ms = 0.0, finalize_ms = 0.0, prep_ms = 0.0,
+           insert_ms = 0.0;
     int64_t nn_scan_launches = 0, steer_launches = 0, finish_launches = 0;
     int64_t batch_steps = 0, batch_passes = 0;
-    DBuf<long long> cf_tally;  // check_finish (profiling): [0] nodes, [1] edges, [2] points
+    DBuf<long long> cf_tally;  // check_finish (profiling): nodes, edges, points, arc points
     DBuf<long long> wg_pts;  // walked polyline points per walk workgroup (profiling on)
     long long* prof_points() const { return prof ? wg_pts.p : nullptr; }
     // every counter of pp_stats that lives on the host or in the profiling tallies (not DevState)
     int reset_host_stats() {
-        nn_scan_ms = steer_ms = finish_ms = 0.0;
+        nn_scan_ms = steer_ms = finish_ms = finalize_ms = prep_ms = insert_ms = 0.0;
         nn_scan_launches = steer_launches = finish_launches = 0;
         batch_steps = batch_passes = 0;
         if (wg_pts.p && hipMemsetAsync(wg_pts.p, 0, wg_pts.n * sizeof(long long), stream) != hipSuccess)
@@ -1309,12 +1309,12 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
         WindowArgs a = ctx->window_args(ctx->d_state.p);
         a.K = K;
         a.target = target;
-        if (ctx->prof && (r = ensure_events(ctx, 4 * (size_t)nw))) return r;
+        if (ctx->prof && (r = ensure_events(ctx, 5 * (size_t)nw))) return r;
         const int64_t windows_before = ctx->h_state.p[0].windows;
         // windows are pipelined: window w's kernel resolves and commits w - 1; the drain launch
         // commits the batch's last window before the host reads the state
         for (int w = 0; w < nw; ++w)
-            PP_HIP(launch_window(st, a, ctx->prof ? &ctx->ev[4 * w] : nullptr, ctx->seq++, w > 0));
+            PP_HIP(launch_window(st, a, ctx->prof ? &ctx->ev[5 * w] : nullptr, ctx->seq++, w > 0));
         PP_HIP(launch_drain(st, a, ctx->seq));
         PP_HIP(hipMemcpyAsync(ctx->h_state.p, ctx->d_state.p, sizeof(DevState), hipMemcpyDeviceToHost, st));
         PP_HIP(hipStreamSynchronize(st));
@@ -1327,11 +1327,12 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
         if (ctx->prof) {
             const int64_t active = std::min<int64_t>(s.windows - windows_before, nw);
             for (int64_t w = 0; w < active; ++w) {
-                float ms = 0.f;
-                PP_HIP(hipEventElapsedTime(&ms, ctx->ev[4 * w], ctx->ev[4 * w + 1]));
-                ctx->nn_scan_ms += ms;
-                PP_HIP(hipEventElapsedTime(&ms, ctx->ev[4 * w + 2], ctx->ev[4 * w + 3]));
-                ctx->steer_ms += ms;
+                double* acc[4] = {&ctx->nn_scan_ms, &ctx->finalize_ms, &ctx->prep_ms, &ctx->steer_ms};
+                for (int k = 0; k < 4; ++k) {
+                    float ms = 0.f;
+                    PP_HIP(hipEventElapsedTime(&ms, ctx->ev[5 * w + k], ctx->ev[5 * w + k + 1]));
+                    *acc[k] += ms;
+                }
             }
             ctx->nn_scan_launches += active;
             ctx->steer_launches += active;
@@ -1787,9 +1788,8 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
     // an earlier call's PP_ERR_STEER_OVERFLOW does not stick to this one
     PP_HIP(hipMemsetAsync(ctx->mq_err.p, 0, sizeof(int), ctx->stream));
     PP_HIP(launch_mq_target(ctx->stream, a.mq, n_steps, ctx->mq_target.p));
-    // sub-batches on their own streams (not while profiling: the NN events time whole-batch
-    // launches)
-    const int nsub = ctx->prof ? 1 : ctx->mq_nsub;
+    // sub-batches on their own streams (profiled too: the events time the schedule that runs)
+    const int nsub = ctx->mq_nsub;
     MqArgs sub[kMaxSub];
     hipStream_t sst[kMaxSub] = {ctx->stream};
     for (int i = 0; i < nsub && nsub > 1; ++i) {
@@ -1814,27 +1814,28 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
         if (pass > 64 + n_steps) return set_err(PP_ERR_HIP, "batch extend made no progress");
         for (int64_t done = 0; done < steps;) {
             const int chunk = (int)std::min<int64_t>(steps - done, 256);
-            if (ctx->prof) {
-                if ((r = ensure_events(ctx, 4 * (size_t)chunk))) return r;
-                a.ev = ctx->ev.data();
-            }
+            if (ctx->prof && (r = ensure_events(ctx, 5 * (size_t)chunk * nsub))) return r;
             if (nsub > 1) {  // interleaved, so every stream always holds work
                 for (int k = 0; k < chunk; ++k)
-                    for (int i = 0; i < nsub; ++i) PP_HIP(launch_mq_steps(sst[i], sub[i], 1));
+                    for (int i = 0; i < nsub; ++i) {
+                        sub[i].ev = ctx->prof ? ctx->ev.data() + 5 * ((size_t)k * nsub + i) : nullptr;
+                        PP_HIP(launch_mq_steps(sst[i], sub[i], 1));
+                    }
             } else {
+                a.ev = ctx->prof ? ctx->ev.data() : nullptr;
                 PP_HIP(launch_mq_steps(ctx->stream, a, chunk));
             }
-            if (ctx->prof) {  // events: around mq_sample_nn and around steer_walk
-                PP_HIP(hipStreamSynchronize(ctx->stream));
-                for (int k = 0; k < chunk; ++k) {
-                    float ms = 0.f;
-                    PP_HIP(hipEventElapsedTime(&ms, ctx->ev[4 * k], ctx->ev[4 * k + 1]));
-                    ctx->nn_scan_ms += ms;
-                    PP_HIP(hipEventElapsedTime(&ms, ctx->ev[4 * k + 2], ctx->ev[4 * k + 3]));
-                    ctx->steer_ms += ms;
-                }
-                ctx->nn_scan_launches += chunk;
-                ctx->steer_launches += chunk;
+            if (ctx->prof) {  // events: before mq_sample_nn, after it, prep, walk and insert
+                for (int i = 0; i < nsub; ++i) PP_HIP(hipStreamSynchronize(sst[i]));
+                double* acc[4] = {&ctx->nn_scan_ms, &ctx->prep_ms, &ctx->steer_ms, &ctx->insert_ms};
+                for (size_t e = 0; e < (size_t)chunk * nsub; ++e)
+                    for (int k = 0; k < 4; ++k) {
+                        float ms = 0.f;
+                        PP_HIP(hipEventElapsedTime(&ms, ctx->ev[5 * e + k], ctx->ev[5 * e + k + 1]));
+                        *acc[k] += ms;
+                    }
+                ctx->nn_scan_launches += (int64_t)chunk * nsub;
+                ctx->steer_launches += (int64_t)chunk * nsub;
             }
             done += chunk;
         }
@@ -1991,8 +1992,8 @@ int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t*
     PP_HIP(hipMemsetAsync(ctx->sr_err.p, 0, sizeof(int), ctx->stream));  // per call, not sticky
     PP_HIP(launch_mq_target(ctx->stream, a.sd.mq, n_steps, ctx->sr_target.p));
     const int64_t steps = std::min<int64_t>(n_steps, ctx->star_max_iter);  // one iteration a step
-    // sub-batches on their own streams, as pp_batch_extend (one stream while profiling)
-    const int nsub = ctx->prof ? 1 : ctx->star_nsub;
+    // sub-batches on their own streams, as pp_batch_extend (profiled too)
+    const int nsub = ctx->star_nsub;
     StarArgs sub[kMaxSub];
     hipStream_t sst[kMaxSub] = {ctx->stream};
     for (int i = 0; i < nsub && nsub > 1; ++i) {
@@ -2010,29 +2011,30 @@ int pp_star_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t*
     }
     for (int64_t done = 0; done < steps;) {
         const int chunk = (int)std::min<int64_t>(steps - done, 256);
-        if (ctx->prof) {
-            if ((r = ensure_events(ctx, 8 * (size_t)chunk))) return r;
-            a.ev = ctx->ev.data();
-        }
+        if (ctx->prof && (r = ensure_events(ctx, 8 * (size_t)chunk * nsub))) return r;
         if (nsub > 1) {  // interleaved, so every stream always holds work
             for (int k = 0; k < chunk; ++k)
-                for (int i = 0; i < nsub; ++i) PP_HIP(launch_star_steps(sst[i], sub[i], 1));
+                for (int i = 0; i < nsub; ++i) {
+                    sub[i].ev = ctx->prof ? ctx->ev.data() + 8 * ((size_t)k * nsub + i) : nullptr;
+                    PP_HIP(launch_star_steps(sst[i], sub[i], 1));
+                }
         } else {
+            a.ev = ctx->prof ? ctx->ev.data() : nullptr;
             PP_HIP(launch_star_steps(ctx->stream, a, chunk));
         }
         if (ctx->prof) {  // events: around star_sample, then around each round's walk
-            PP_HIP(hipStreamSynchronize(ctx->stream));
-            for (int k = 0; k < chunk; ++k) {
+            for (int i = 0; i < nsub; ++i) PP_HIP(hipStreamSynchronize(sst[i]));
+            for (size_t e = 0; e < (size_t)chunk * nsub; ++e) {
                 float ms = 0.f;
-                PP_HIP(hipEventElapsedTime(&ms, ctx->ev[8 * k], ctx->ev[8 * k + 1]));
+                PP_HIP(hipEventElapsedTime(&ms, ctx->ev[8 * e], ctx->ev[8 * e + 1]));
                 ctx->nn_scan_ms += ms;
                 for (int w = 1; w < 4; ++w) {
-                    PP_HIP(hipEventElapsedTime(&ms, ctx->ev[8 * k + 2 * w], ctx->ev[8 * k + 2 * w + 1]));
+                    PP_HIP(hipEventElapsedTime(&ms, ctx->ev[8 * e + 2 * w], ctx->ev[8 * e + 2 * w + 1]));
                     ctx->steer_ms += ms;
                 }
             }
-            ctx->nn_scan_launches += chunk;
-            ctx->steer_launches += 3 * chunk;
+            ctx->nn_scan_launches += (int64_t)chunk * nsub;
+            ctx->steer_launches += 3 * (int64_t)chunk * nsub;
         }
         done += chunk;
     }
@@ -2110,6 +2112,9 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out, uint64_t out_size) {
     s.nn_scan_launches = ctx->nn_scan_launches;
     s.steer_ms = ctx->steer_ms;
     s.steer_launches = ctx->steer_launches;
+    s.finalize_ms = ctx->finalize_ms;
+    s.prep_ms = ctx->prep_ms;
+    s.insert_ms = ctx->insert_ms;
     s.batch_steps = ctx->batch_steps;
     s.batch_passes = ctx->batch_passes;
     s.finish_ms = ctx->finish_ms;
@@ -2118,15 +2123,16 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out, uint64_t out_size) {
         std::vector<long long> v(ctx->wg_pts.n);
         PP_HIP(hipMemcpyAsync(v.data(), ctx->wg_pts.p, v.size() * sizeof(long long), hipMemcpyDeviceToHost, ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
-        for (long long x : v) s.walk_points += x;
+        for (size_t i = 0; i < v.size(); ++i) (i < (size_t)kWalkTallySlots ? s.walk_points : s.walk_arc_points) += v[i];
     }
     if (ctx->cf_tally.p) {
-        long long t[3];
+        long long t[4];
         PP_HIP(hipMemcpyAsync(t, ctx->cf_tally.p, sizeof t, hipMemcpyDeviceToHost, ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
         s.finish_nodes = t[0];
         s.finish_edges = t[1];
         s.finish_points = t[2];
+        s.finish_arc_points = t[3];
     }
     std::memcpy(out, &s, (size_t)std::min<uint64_t>(out_size, sizeof s));
     return PP_OK;
@@ -2153,13 +2159,13 @@ int pp_set_profiling(pp_ctx* ctx, int enabled) {
     int r = check_ctx(ctx, false, false);
     if (r) return r;
     if (enabled && !ctx->wg_pts.p) {  // one tally slot per walk workgroup (any walk grid)
-        PP_HIP(ctx->wg_pts.reserve(kWalkTallySlots));
-        PP_HIP(hipMemsetAsync(ctx->wg_pts.p, 0, kWalkTallySlots * sizeof(long long), ctx->stream));
+        PP_HIP(ctx->wg_pts.reserve(2 * kWalkTallySlots));
+        PP_HIP(hipMemsetAsync(ctx->wg_pts.p, 0, 2 * kWalkTallySlots * sizeof(long long), ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
     }
     if (enabled && !ctx->cf_tally.p) {
-        PP_HIP(ctx->cf_tally.reserve(3));
-        PP_HIP(hipMemsetAsync(ctx->cf_tally.p, 0, 3 * sizeof(long long), ctx->stream));
+        PP_HIP(ctx->cf_tally.reserve(4));
+        PP_HIP(hipMemsetAsync(ctx->cf_tally.p, 0, 4 * sizeof(long long), ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
     }
     ctx->prof = enabled != 0;

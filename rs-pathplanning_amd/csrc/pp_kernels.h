@@ -49,8 +49,8 @@ struct WindowArgs {
 };
 
 // Enqueue window number `seq` on stream s: its window kernel also resolves and commits window
-// seq - 1 when resolve_prev (the previous window of the same batch).  ev (optional) = 4 timing
-// events: around the window kernel (the NN screen) and around the steer (prep + walk).
+// seq - 1 when resolve_prev (the previous window of the same batch).  ev (optional) = 5 timing
+// events: before the window kernel, then after it, nn_finalize, steer_prep and steer_walk.
 hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int64_t seq,
                          int resolve_prev);
 // Resolve and commit the last enqueued window (seq_next - 1): ends a batch.
@@ -98,7 +98,8 @@ struct MqArgs {
     double* lit_scratch = nullptr;  // kLiteralWaves buffers
     int* lit_locks = nullptr;       // their slot locks (0 free)
     int* err = nullptr;
-    hipEvent_t* ev = nullptr;  // optional: 4 per step, around mq_sample_nn and steer_walk
+    hipEvent_t* ev = nullptr;  // optional: 5 per step: before mq_sample_nn, then after it, steer_prep,
+                               // steer_walk and mq_insert
     long long* wg_points = nullptr;  // profiling: walked points per walk workgroup (or null)
 };
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps);

@@ -320,10 +320,12 @@ __device__ __forceinline__ WalkIn walk_in(const SteerPrep* __restrict__ p) {
 }
 __device__ __forceinline__ WalkIn walk_in(const SteerPrep& p) { return walk_in(&p); }
 
-// walked (optional, wave-uniform): += the polyline points generated and verified
+// walked / walked_arc (optional, wave-uniform): += the polyline points generated and verified /
+// those of them on L and R segments (the sincos points of the walk's FLOP count)
 template <bool kLds>
 __device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
-                                          bool junction = true, int* walked = nullptr) {
+                                          bool junction = true, int* walked = nullptr,
+                                          int* walked_arc = nullptr) {
     const int lane = threadIdx.x & 63;
     if (r.state == kPrepNone) {  // polyline [(x, y), (px, py)]
         if (walked) *walked += 2;
@@ -370,13 +372,14 @@ __device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
         const bool end_here = (seg >= 3) && cnt < 63;
         const bool junction_here = end_here && junction;
         double qx = carry_x, qy = carry_y;
-        bool has = (lane == 0), isgrid = false, isjunction = false;
+        bool has = (lane == 0), isgrid = false, isjunction = false, isarc = false;
         if (lane >= 1 && lane <= cnt) {
             Pose o;
             o.x = my_seg == 0 ? 0.0 : (my_seg == 1 ? o1x : o2x);
             o.y = my_seg == 0 ? 0.0 : (my_seg == 1 ? o1y : o2y);
             o.yaw = my_seg == 0 ? 0.0 : (my_seg == 1 ? o1yaw : o2yaw);
             const int mm = my_seg == 0 ? m0 : (my_seg == 1 ? m1 : m2);
+            isarc = mm != kModeS;
             const Pose p = interp_local(mm, my_pd, r.c, o);
             qx = r.cw * p.x + r.sw * p.y + r.x;   // dubins.rs:415
             qy = -r.sw * p.x + r.cw * p.y + r.y;  // dubins.rs:420
@@ -391,6 +394,7 @@ __device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
         const bool check_bounds = isgrid || isjunction || (first && lane == 0);
         const bool rej = chunk_rejects<kLds>(sc, has, check_bounds, has && lane >= 1, qx, qy);
         if (walked) *walked += cnt + (first ? 1 : 0) + (junction_here ? 1 : 0);
+        if (walked_arc) *walked_arc += __popcll(__ballot(isarc));
         if (rej) return kReject;
         if (end_here) break;
         carry_x = readlane_f64(qx, cnt);
@@ -1774,7 +1778,7 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
 template <bool kLds>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
                                         const double* __restrict__ pdv, double* __restrict__ gs,
-                                        int& npts) {
+                                        int& npts, int& napts) {
     const int lane = threadIdx.x & 63;
     const int state = p->state;
     const double x = p->x, y = p->y, px = p->px, py = p->py;
@@ -1932,6 +1936,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         const bool has = lane == 0 || isgrid || isj;
         const bool chk = isgrid || isj || (base == 0 && lane == 0);
         npts += cnt + (junction_here ? 1 : 0);
+        napts += __popcll(__ballot(isgrid && (my_seg == 0 ? m0 : (my_seg == 1 ? m1 : m2)) != kModeS));
         if (chunk_rejects<kLds>(sc, has, chk, has && lane >= 1, qx, qy)) return kReject;
         if (junction_here) break;
         carry_x = readlane_f64(qx, 63);
@@ -1979,7 +1984,7 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
     if (kLds) stage_scene(sc);
     double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) +
                  (threadIdx.x >> 6) * kGenSlots;  // this wave's generator slots
-    int npts = 0;
+    int npts = 0, napts = 0;
     // Workgroup b walks the tasks b, b + G, b + 2G, ... (G = the grid); its waves take them one
     // at a time from an LDS counter, so a wave that drew short paths takes more of them (a
     // workgroup's share is a sum of dozens of tasks: far more even than a wave's handful under a
@@ -1995,7 +2000,7 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
         if (lane == 0) k = atomicAdd(&s_next, 1);
         const int t = (int)blockIdx.x + G * __builtin_amdgcn_readlane(k, 0);
         if (t >= total) break;
-        const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts);
+        const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts, napts);
         if (lane == 0) {
             if (t < W) {
                 snap_status[t] = s;
@@ -2006,14 +2011,17 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
             }
         }
     }
-    if (wg_points) {
-        __shared__ int s_np[kWalkThreads / 64];
-        if (lane == 0) s_np[threadIdx.x >> 6] = npts;
+    if (wg_points) {  // [b]: points, [kWalkTallySlots + b]: their arc points
+        __shared__ int s_np[2][kWalkThreads / 64];
+        if (lane == 0) {
+            s_np[0][threadIdx.x >> 6] = npts;
+            s_np[1][threadIdx.x >> 6] = napts;
+        }
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (threadIdx.x < 2) {
             long long sum = 0;
-            for (int w = 0; w < kWalkThreads / 64; ++w) sum += s_np[w];
-            wg_points[blockIdx.x] += sum;
+            for (int w = 0; w < kWalkThreads / 64; ++w) sum += s_np[threadIdx.x][w];
+            wg_points[blockIdx.x + threadIdx.x * kWalkTallySlots] += sum;
         }
     }
 }
@@ -2616,15 +2624,15 @@ __device__ __forceinline__ void lit_release(int* locks, int slot) {
     if ((threadIdx.x & 63) == 0) atomicExch(&locks[slot], 0);
 }
 
-// returns the verdict | (polyline points walked << 4)
+// returns the verdict | (polyline points walked << 4) | (their arc points << 34)
 template <bool kAllowNone>
-__device__ __attribute__((noinline)) int cf_edge_check(const SceneDev& sc, CfPose a, CfPose b,
-                                                       bool junction, double* lit_scratch,
-                                                       int* lit_locks) {
+__device__ __attribute__((noinline)) long long cf_edge_check(const SceneDev& sc, CfPose a,
+                                                             CfPose b, bool junction,
+                                                             double* lit_scratch, int* lit_locks) {
     const SteerPrep r = steer_prep(sc, a.x, a.y, a.yaw, b.x, b.y, b.yaw);
     if (!kAllowNone && r.state == kPrepNone) return kCfPanic;
-    int walked = 0;
-    int st = steer_walk<false>(sc, walk_in(r), junction, &walked);
+    int walked = 0, walked_arc = 0;
+    int st = steer_walk<false>(sc, walk_in(r), junction, &walked, &walked_arc);
     if (st == kLiteral) {  // (measure-zero) a scratch buffer from the pool, for this edge only
         const int slot = lit_acquire(lit_locks, (int)blockIdx.x);
         double* bx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
@@ -2632,7 +2640,7 @@ __device__ __attribute__((noinline)) int cf_edge_check(const SceneDev& sc, CfPos
                                    bx + 2 * kLiteralCap, junction);
         lit_release(lit_locks, slot);
     }
-    return st | (walked << 4);
+    return (long long)st | ((long long)walked << 4) | ((long long)walked_arc << 34);
 }
 
 // n_point of dubins_path_planning(a → b) (dubins.rs:369), 0 when the steer is None
@@ -2677,7 +2685,7 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
     // node's cost varies with its depth and how far optimize climbs, so a static stride left
     // workgroups holding a few deep nodes as the launch's tail
     __shared__ int s_b;
-    long long t_nodes = 0, t_edges = 0, t_pts = 0;  // this wave's work (profiling: tally)
+    long long t_nodes = 0, t_edges = 0, t_pts = 0, t_arc = 0;  // this wave's work (profiling)
     for (;;) {
         if (tid == 0) s_b = atomicAdd(&err[1], 1);
         __syncthreads();
@@ -2723,10 +2731,11 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
                     const int to = s_path[m];
                     const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
                     const CfPose a{a0.x, a0.y, atan2(bt.y - a0.y, bt.x - a0.x)};
-                    const int rv = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks);
-                    st = rv & 15;
+                    const long long rv = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks);
+                    st = (int)(rv & 15);
                     ++t_edges;
-                    t_pts += rv >> 4;
+                    t_pts += (rv >> 4) & 0x3fffffff;
+                    t_arc += rv >> 34;
                 }
                 if (lane == 0) s_st[wave] = st;
                 __syncthreads();
@@ -2780,10 +2789,11 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
             if (e < E) {
                 const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                 const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                const int rv = cf_edge_check<false>(sc, a, bp, e < E - 1, lit_scratch, lit_locks);
-                st = rv & 15;
+                const long long rv = cf_edge_check<false>(sc, a, bp, e < E - 1, lit_scratch, lit_locks);
+                st = (int)(rv & 15);
                 ++t_edges;
-                t_pts += rv >> 4;
+                t_pts += (rv >> 4) & 0x3fffffff;
+                t_arc += rv >> 34;
             }
             if (lane == 0) s_st[wave] = st;
             __syncthreads();
@@ -2893,6 +2903,7 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
         if (wave == 0) atomicAdd(&tl[0], (unsigned long long)t_nodes);
         atomicAdd(&tl[1], (unsigned long long)t_edges);
         atomicAdd(&tl[2], (unsigned long long)t_pts);
+        atomicAdd(&tl[3], (unsigned long long)t_arc);
     }
 }
 
@@ -3108,22 +3119,24 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
     const int lds = a.sc.lds_bytes;
     for (int k = 0; k < steps; ++k) {
-        if (a.ev) (void)hipEventRecord(a.ev[4 * k], s);
+        hipEvent_t* ev = a.ev ? a.ev + 5 * k : nullptr;
+        if (ev) (void)hipEventRecord(ev[0], s);
         mq_sample_nn_kernel<<<nn_blocks, 256, 0, s>>>(a.mq, a.sc.minx, a.sc.maxx, a.sc.miny,
                                                       a.sc.maxy, a.tasks);
-        if (a.ev) (void)hipEventRecord(a.ev[4 * k + 1], s);
+        if (ev) (void)hipEventRecord(ev[1], s);
         steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, nullptr, nullptr, nullptr,
                                                       nullptr, a.rec, a.pdbuf, a.yaw, a.tasks);
-        if (a.ev) (void)hipEventRecord(a.ev[4 * k + 2], s);
+        if (ev) (void)hipEventRecord(ev[2], s);
         if (lds > 0)
             steer_walk_kernel<true, kWalkMinWBatch><<<walk_blocks, kWalkThreads, walk_lds_bytes(lds), s>>>(
                 a.st, a.sc, a.rec, a.pdbuf, nullptr, a.status, nullptr, nullptr, a.wg_points);
         else
             steer_walk_kernel<false, kWalkMinWBatch><<<walk_blocks, kWalkThreads, walk_lds_bytes(0), s>>>(
                 a.st, a.sc, a.rec, a.pdbuf, nullptr, a.status, nullptr, nullptr, a.wg_points);
-        if (a.ev) (void)hipEventRecord(a.ev[4 * k + 3], s);
+        if (ev) (void)hipEventRecord(ev[3], s);
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
                                                     a.lit_scratch, a.lit_locks, a.err);
+        if (ev) (void)hipEventRecord(ev[4], s);
     }
     return hipGetLastError();
 }
@@ -3824,19 +3837,20 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     double* wsy = a.wsy + (size_t)p * a.Kcap;
     if (ev) (void)hipEventRecord(ev[0], s);
     window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
-    if (ev) (void)hipEventRecord(ev[1], s);
     if (resolve_prev && !kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
+    if (ev) (void)hipEventRecord(ev[1], s);
     // one workgroup past the samples' draws the next window's samples
     nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples + 1, kFinThreads, 0, s>>>(
         a.st, p, seq, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, wsx, wsy, a.tr.x32, a.tr.y32,
         a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose,
         pair_grid(wk.g, p, a.eps_coord), a.cand_cnt, a.cand, a.pend, wk.sq[p], wk.g.ipos[p], wk.g,
         1);
+    if (ev) (void)hipEventRecord(ev[2], s);
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K + kPrepThreads / 8 - 1) / (kPrepThreads / 8);
     steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, wsx, wsy, a.snap_pose, a.cand,
                                                   a.rec, a.pdbuf, a.snap_yaw, nullptr);
-    if (ev) (void)hipEventRecord(ev[2], s);
+    if (ev) (void)hipEventRecord(ev[3], s);
     const int lds = a.sc.lds_bytes;
     // snapshot tasks plus the usual few candidate tasks in one round of waves
     const int nwg = std::min((K + K / 4 + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
@@ -3847,7 +3861,7 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     else
         steer_walk_kernel<false, kWalkMinWWindow><<<nwg, kWalkThreads, walk_lds_bytes(0), s>>>(
             a.st, a.sc, a.rec, a.pdbuf, a.cand, a.snap_status, a.cand_cnt, a.pend, a.wg_points);
-    if (ev) (void)hipEventRecord(ev[3], s);
+    if (ev) (void)hipEventRecord(ev[4], s);
     return hipGetLastError();
 }
 

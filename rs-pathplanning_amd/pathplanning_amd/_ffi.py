@@ -67,9 +67,11 @@ class StatsC(C.Structure):
         ("literal_repairs", C.c_int64), ("nn_flagged", C.c_int64), ("node_evals", C.c_int64),
         ("nn_scan_ms", C.c_double), ("nn_scan_launches", C.c_int64),
         ("steer_ms", C.c_double), ("steer_launches", C.c_int64),
-        ("walk_points", C.c_int64), ("batch_steps", C.c_int64), ("batch_passes", C.c_int64),
+        ("finalize_ms", C.c_double), ("prep_ms", C.c_double), ("insert_ms", C.c_double),
+        ("walk_points", C.c_int64), ("walk_arc_points", C.c_int64), ("batch_steps", C.c_int64), ("batch_passes", C.c_int64),
         ("finish_ms", C.c_double), ("finish_launches", C.c_int64), ("finish_nodes", C.c_int64),
         ("finish_edges", C.c_int64), ("finish_points", C.c_int64),
+        ("finish_arc_points", C.c_int64),
     ]
 
     def as_dict(self):

@@ -1,5 +1,5 @@
 """bench.py's provenance block (CPU, no GPU call): the measured library's hash and build flags,
-the PP_* run-time knobs a line was taken with, and the refusal of a PP_AMD_LIB variant build
+the PP_* variables a line was taken with (the library reads none), and the refusal of a PP_AMD_LIB variant build
 unless --allow-variant-lib is given."""
 import argparse
 import os
@@ -20,11 +20,11 @@ def _bench():
 def test_provenance_records_knobs(monkeypatch):
     bench = _bench()
     monkeypatch.delenv("PP_AMD_LIB", raising=False)
-    monkeypatch.setenv("PP_BATCH_STREAMS", "3")
+    monkeypatch.setenv("PP_SOME_KNOB", "3")
     p = bench.provenance(argparse.Namespace(allow_variant_lib=False))
     assert p["lib"].endswith("libpathplanning_amd.so") and len(p["lib_sha256_16"]) == 16
     assert "--offload-arch=gfx950" in p["hipcc_flags"] and p["variant"] is False
-    assert p["env_knobs"].get("PP_BATCH_STREAMS") == "3"
+    assert p["env_knobs"].get("PP_SOME_KNOB") == "3"
 
 
 def test_provenance_refuses_variant_lib(monkeypatch):
