@@ -578,12 +578,42 @@ def run_batch(args, D, star, with_cpu):
     n, its = stt[0], stt[1]
     st_timed = batch.stats()
     dig = batch_digests(batch, star)
-    rec = np.stack([np.arange(a, b, dtype=np.int64), its.astype(np.int64), n.astype(np.int64),
-                    dig], 1)
+    cols = [np.arange(a, b, dtype=np.int64), its.astype(np.int64), n.astype(np.int64), dig]
+    t_plan = None
+    if not star:
+        # RRT::plan of every query (check_finish of every accepted node, the first minimum
+        # length): the per-query record of SURVEY §8e — (ok, n_nodes, path_len, cost, iterations)
+        D.barrier()
+        t0 = time.perf_counter()
+        pr = batch.plan()
+        t_plan_local = time.perf_counter() - t0
+        D.barrier()
+        t_plan = D.allreduce(t_plan_local, "max")
+        cols += [(pr["best_node"] >= 0).astype(np.int64), pr["best_node"].astype(np.int64),
+                 pr["n_points"].astype(np.int64), pr["length"].view(np.int64),
+                 pr["n_finishes"].astype(np.int64)]
+        checked = int(D.allreduce(pr["checked"], "sum"))
+    rec = np.stack(cols, 1)
     allrec = D.gather_records(rec).numpy()
     t_max = D.allreduce(t_local, "max")
     iters_total = int(allrec[:, 1].sum())
     extra = {}
+    if not star:
+        ok = allrec[:, 4] == 1
+        lens = allrec[ok, 7].view(np.float64)
+        extra["plan"] = {
+            "value": round(iters_total / (t_max + t_plan), 1),
+            "unit": "plan_one calls/s (extend + check_finish of every accepted node)",
+            "check_finish_ms": round(1e3 * t_plan, 3),
+            "extend_ms": round(1e3 * t_max, 3),
+            "nodes_checked": checked,
+            "check_finish_per_s": round(checked / t_plan, 1) if t_plan > 0 else None,
+            "queries_with_path": int(ok.sum()),
+            "finishes_total": int(allrec[:, 8].sum()),
+            "mean_length": round(float(lens.mean()), 4) if len(lens) else None,
+            "record": "per query: (query, iterations, n_nodes, tree digest, ok, best node, "
+                      "path points, length bits, finishes), gathered with the extend records",
+        }
     if star:
         extra["rewires_total"] = int(D.allreduce(float(stt[3].sum()), "sum"))
     else:
@@ -598,6 +628,9 @@ def run_batch(args, D, star, with_cpu):
     batch.extend(steps)
     sp = batch.stats()
     evals_p = batch.state()[2] if star else batch.state(with_evals=True)[2]
+    if not star:
+        batch.plan()
+        extra["plan"]["roofline"] = finish_roofline(batch.stats())
     batch.close()
     nn_ms = sp["nn_scan_ms"] / max(sp["nn_scan_launches"], 1)
     evals_per_launch = float(evals_p.sum()) / max(sp["nn_scan_launches"], 1)
@@ -657,7 +690,36 @@ def run_batch(args, D, star, with_cpu):
                                                  args.cpu_seconds) if star else
                                cpu_baseline_queries(raw, starts, seeds, args.max_iter,
                                                     args.cpu_seconds))
+        if not star:
+            res["plan"]["cpu_baseline"] = cpu_baseline_batch_plan(
+                raw, starts, goals, seeds, args.max_iter, args.cpu_seconds,
+                allrec[:, 5], allrec[:, 7].view(np.float64))
     return res
+
+
+def cpu_baseline_batch_plan(raw, starts, goals, seeds, max_iter, seconds, best, length):
+    """config 3's RRT::plan CPU baseline: the oracle's sequential plan (rrt.rs:599-619, full
+    re-verify) of whole queries of the same batch, one after another on one core until
+    `seconds` / 2; the answers are compared with the GPU's records."""
+    oracle = oracle_mod()
+    sc = oracle.OracleScene.from_raw(raw)
+    done, t_used, same = 0, 0.0, True
+    for q in range(len(seeds)):
+        tr = oracle.OracleTree(tuple(starts[q]), max_iter + 1)
+        t0 = time.perf_counter()
+        _, bn, bl, _ = oracle.plan(sc, tr, int(seeds[q]), 0, max_iter, goals[q][:2], goals[q][2],
+                                   full_reverify=True)
+        t_used += time.perf_counter() - t0
+        same &= bool(bn == best[q] and (bn < 0 or abs(bl - length[q]) <= 1e-9 * bl))
+        done += 1
+        if t_used >= seconds / 2.0:
+            break
+    return {"value": round(done * max_iter / t_used, 1),
+            "unit": "plan_one calls/s (with check_finish)", "cores": 1, "kind": "port",
+            "sample": f"the first {done} queries of the same batch planned in full (extend + "
+                      f"check_finish, full re-verify), sequential on one core, "
+                      f"{t_used:.1f} s",
+            "same_answer": same, "host": host_info()}
 
 
 def auto_batch_window(q):

@@ -247,6 +247,15 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
  * each); any may be NULL.  With pp_set_profiling on, pp_batch_extend times its NN kernel with
  * HIP events into pp_stats.nn_scan_ms / nn_scan_launches. */
 int pp_batch_state(pp_ctx* ctx, int32_t* n_nodes, int64_t* iterations, int64_t* node_evals);
+/* RRT::plan (rrt.rs:599-619) of every query of the batch, on its tree as extended so far:
+ * check_finish (rrt.rs:428-438: optimize_from_goal, finalize, verify) of every node the query
+ * inserted (1 .. n_q - 1 in insertion order, rrt.rs:591) with the query's goal from
+ * pp_batch_new, then the first minimum euclidean_length (rrt.rs:607-617).  Per query (q entries
+ * each, any may be NULL): best_node (-1: no finish, the reference's None), length (inf when none),
+ * n_points of the finalized line, n_finishes (verified check_finish lines); n_checked = the
+ * (query, node) pairs checked. */
+int pp_batch_plan(pp_ctx* ctx, int32_t* best_node, double* length, int32_t* n_points,
+                  int32_t* n_finishes, int64_t* n_checked);
 /* one query's tree (root first), like pp_rrt_tree_export */
 int pp_batch_tree_export(pp_ctx* ctx, int query, double* x, double* y, double* yaw,
                          int32_t* parent, int64_t cap, int64_t* n);

@@ -187,7 +187,10 @@ struct pp_ctx {
     DBuf<DevState> mq_state;      // [3]: the whole batch, then one per sub-batch (mq_sub_args)
     hipStream_t sub_stream[4] = {};  // sub-batch streams 1.. (0 is `stream`), created on first use
     hipEvent_t fork_ev = nullptr;
-    std::vector<double> mq_goal;  // 3 per query (kept for the host; the batch path is extend only)
+    std::vector<double> mq_goal;  // 3 per query (RRT::new's goal; pp_batch_plan)
+    DBuf<double> mq_goal_d;       // [3Q] the goals on the device (pp_batch_plan)
+    DBuf<int> mp_off, mp_qidx, mp_nodes, mp_ok, mp_npts, mp_best, mp_bpts, mp_nfin;
+    DBuf<double> mp_len, mp_blen;
 
     // ---- RRT* query batch (BASELINE config 5, build-defined: DESIGN.md §3.7)
     bool has_star = false;
@@ -474,13 +477,19 @@ struct CfGoal {
     int level0 = 0, mode = kCfCheck;
 };
 
-int cf_launch(pp_ctx* c, int k, int want_line, int grid, const CfGoal* g = nullptr) {
-    const CfGoal dflt{c->goal[0], c->goal[1], c->goal[2], c->goal[2]};
-    if (!g) g = &dflt;
-    PP_HIP(c->cf_ok.reserve(kCfBatch));
-    PP_HIP(c->cf_len.reserve(kCfBatch));
-    PP_HIP(c->cf_npts.reserve(kCfBatch));
-    PP_HIP(c->cf_chain.reserve((size_t)kCfBatch * (kCfLevels + 2)));
+// Where a check_finish_kernel launch writes its per-node results (device pointers).
+struct CfOut {
+    int* ok;
+    double* len;
+    int* npts;
+    int* chain;  // may be null
+};
+
+// check_finish_kernel over nodes[0, k) (device) with its error handling; the one-tree planner
+// (cb.qidx null: the context's tree, goal g) or a query batch (cb)
+int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line, int grid,
+           const CfGoal& gg, const CfOut& o, const CfBatch& cb) {
+    const CfGoal* g = &gg;
     PP_HIP(c->cf_err.reserve(2));  // [0] error bits, [1] the kernel's node counter
     // the line buffers (one per workgroup of the launch) only when lines are materialised
     const int wgs = std::min(grid, k);
@@ -498,13 +507,12 @@ int cf_launch(pp_ctx* c, int k, int want_line, int grid, const CfGoal* g = nullp
         if (int r = ensure_events(c, 2)) return r;
         PP_HIP(hipEventRecord(c->ev[0], c->stream));
     }
-    PP_HIP(launch_check_finish(c->stream, c->scene_dev(), c->tree_dev(), c->cf_nodes.p, k, g->x,
-                               g->y, g->yaw, g->yaw_opt, g->level0, g->mode, want_line,
-                               c->cf_ok.p, c->cf_len.p, c->cf_npts.p, c->cf_chain.p,
-                               c->api_lit_scratch.p, c->lit_locks.p,
+    PP_HIP(launch_check_finish(c->stream, c->scene_dev(), tr, nodes, k, g->x, g->y,
+                               g->yaw, g->yaw_opt, g->level0, g->mode, want_line, o.ok, o.len,
+                               o.npts, o.chain, c->api_lit_scratch.p, c->lit_locks.p,
                                want_line ? c->cf_pts.p : nullptr, kCfPtsCap,
                                want_line ? c->cf_etab.p : nullptr, c->cf_err.p, grid,
-                               c->prof ? c->cf_tally.p : nullptr));
+                               c->prof ? c->cf_tally.p : nullptr, cb));
     if (c->prof) PP_HIP(hipEventRecord(c->ev[1], c->stream));
     int err = 0;
     PP_HIP(hipMemcpyAsync(&err, c->cf_err.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -520,6 +528,17 @@ int cf_launch(pp_ctx* c, int k, int want_line, int grid, const CfGoal* g = nullp
     if (err & 1) return set_err(PP_ERR_CAPACITY, "tree deeper than the check_finish path capacity");
     if (err & 8) return set_err(PP_ERR_CAPACITY, "finalized line longer than the point capacity");
     return PP_OK;
+}
+
+// check_finish of the one-tree planner for cf_nodes[0, k) into the context's cf_* buffers
+int cf_launch(pp_ctx* c, int k, int want_line, int grid, const CfGoal* g = nullptr) {
+    const CfGoal dflt{c->goal[0], c->goal[1], c->goal[2], c->goal[2]};
+    PP_HIP(c->cf_ok.reserve(kCfBatch));
+    PP_HIP(c->cf_len.reserve(kCfBatch));
+    PP_HIP(c->cf_npts.reserve(kCfBatch));
+    PP_HIP(c->cf_chain.reserve((size_t)kCfBatch * (kCfLevels + 2)));
+    return cf_run(c, c->tree_dev(), c->cf_nodes.p, k, want_line, grid, g ? *g : dflt,
+                  CfOut{c->cf_ok.p, c->cf_len.p, c->cf_npts.p, c->cf_chain.p}, CfBatch{});
 }
 
 MqArgs mq_args(pp_ctx* c) {
@@ -1887,6 +1906,67 @@ int pp_batch_tree_export(pp_ctx* ctx, int query, double* x, double* y, double* y
     if (y) PP_HIP(hipMemcpyAsync(y, ctx->mq_y.p + o, nn * sizeof(double), hipMemcpyDeviceToHost, st));
     if (yaw) PP_HIP(hipMemcpyAsync(yaw, ctx->mq_yaw.p + o, nn * sizeof(double), hipMemcpyDeviceToHost, st));
     if (parent) PP_HIP(hipMemcpyAsync(parent, ctx->mq_par.p + o, nn * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    return PP_OK;
+}
+
+int pp_batch_plan(pp_ctx* ctx, int32_t* best_node, double* length, int32_t* n_points,
+                  int32_t* n_finishes, int64_t* n_checked) {
+    int r = check_ctx(ctx, true, false);
+    if (r) return r;
+    if (!ctx->has_batch) return set_err(PP_ERR_STATE, "pp_batch_new has not been called");
+    const int Q = ctx->mq_Q;
+    hipStream_t st = ctx->stream;
+    // the accepted nodes of every query (1 .. n_q - 1, rrt.rs:591), flattened
+    std::vector<int> hn(Q), off((size_t)Q + 1, 0);
+    PP_HIP(hipMemcpyAsync(hn.data(), ctx->mq_n.p, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    int64_t total = 0;
+    for (int q = 0; q < Q; ++q) {
+        off[q] = (int)total;
+        total += std::max(hn[q] - 1, 0);
+        if (total > (int64_t)0x7fff0000) return set_err(PP_ERR_CAPACITY, "too many nodes to plan");
+    }
+    off[Q] = (int)total;
+    if (n_checked) *n_checked = total;
+    const size_t tk = (size_t)std::max<int64_t>(total, 1);
+    PP_HIP(ctx->mp_off.reserve((size_t)Q + 1));
+    PP_HIP(ctx->mp_qidx.reserve(tk));
+    PP_HIP(ctx->mp_nodes.reserve(tk));
+    PP_HIP(ctx->mp_ok.reserve(tk));
+    PP_HIP(ctx->mp_npts.reserve(tk));
+    PP_HIP(ctx->mp_len.reserve(tk));
+    PP_HIP(ctx->mp_best.reserve(Q));
+    PP_HIP(ctx->mp_bpts.reserve(Q));
+    PP_HIP(ctx->mp_nfin.reserve(Q));
+    PP_HIP(ctx->mp_blen.reserve(Q));
+    PP_HIP(ctx->mq_goal_d.reserve(3 * (size_t)Q));
+    PP_HIP(hipMemcpyAsync(ctx->mp_off.p, off.data(), off.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    PP_HIP(hipMemcpyAsync(ctx->mq_goal_d.p, ctx->mq_goal.data(), 3 * (size_t)Q * sizeof(double),
+                          hipMemcpyHostToDevice, st));
+    PP_HIP(launch_mq_plan_items(st, Q, ctx->mp_off.p, ctx->mp_qidx.p, ctx->mp_nodes.p));
+    if (total > 0) {
+        CfBatch cb;
+        cb.qidx = ctx->mp_qidx.p;
+        cb.row_cap = ctx->mq_cap;
+        cb.goals = ctx->mq_goal_d.p;
+        cb.blocked = ctx->mq_any_blocked ? ctx->mq_blocked.p : nullptr;
+        TreeDev tr{};  // the batch's SoA rows (query q: offset q * mq_cap, cb.row_cap)
+        tr.x = ctx->mq_x.p;
+        tr.y = ctx->mq_y.p;
+        tr.yaw = ctx->mq_yaw.p;
+        tr.parent = ctx->mq_par.p;
+        const CfGoal g{0.0, 0.0, 0.0, 0.0};  // (per query: cb.goals)
+        if ((r = cf_run(ctx, tr, ctx->mp_nodes.p, (int)total, 1, kCfGrid, g,
+                        CfOut{ctx->mp_ok.p, ctx->mp_len.p, ctx->mp_npts.p, nullptr}, cb)))
+            return r;
+    }
+    PP_HIP(launch_mq_plan_reduce(st, Q, ctx->mp_off.p, ctx->mp_ok.p, ctx->mp_len.p, ctx->mp_npts.p,
+                                 ctx->mp_best.p, ctx->mp_blen.p, ctx->mp_bpts.p, ctx->mp_nfin.p));
+    if (best_node) PP_HIP(hipMemcpyAsync(best_node, ctx->mp_best.p, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+    if (length) PP_HIP(hipMemcpyAsync(length, ctx->mp_blen.p, Q * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (n_points) PP_HIP(hipMemcpyAsync(n_points, ctx->mp_bpts.p, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+    if (n_finishes) PP_HIP(hipMemcpyAsync(n_finishes, ctx->mp_nfin.p, Q * sizeof(int), hipMemcpyDeviceToHost, st));
     PP_HIP(hipStreamSynchronize(st));
     return PP_OK;
 }

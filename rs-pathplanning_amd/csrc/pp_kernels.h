@@ -78,12 +78,27 @@ hipError_t launch_steer_tasks(hipStream_t st, const SceneDev& sc, const TreeDev&
 // check_finish_kernel modes: check_finish (rrt.rs:428-438), optimize alone (rrt.rs:463-487),
 // finalize of a caller-built goal node (rrt.rs:489-540)
 enum : int { kCfCheck = 0, kCfOptimize = 1, kCfFinalize = 2 };
+// check_finish over a query batch (pp_batch_plan): item b = node nodes[b] of query qidx[b]
+struct CfBatch {
+    const int* qidx = nullptr;  // null: the one-tree planner
+    int row_cap = 0;            // SoA rows per query
+    const double* goals = nullptr;   // [3Q] goal x, y, yaw
+    const uint8_t* blocked = nullptr;  // [Q] polygon mode: the root fails verify (may be null)
+};
 hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev& tr,
                                const int* nodes, int k, double gx, double gy, double gyaw,
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,
                                int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
-                               int grid, long long* tally = nullptr);
+                               int grid, long long* tally = nullptr,
+                               const CfBatch& cb = CfBatch{});
+
+// pp_batch_plan: the (query, node) items of the accepted nodes (off: [Q + 1] exclusive scan of
+// n_q - 1), and per query the first minimum length over its items' check_finish results
+hipError_t launch_mq_plan_items(hipStream_t s, int Q, const int* off, int* qidx, int* nodes);
+hipError_t launch_mq_plan_reduce(hipStream_t s, int Q, const int* off, const int* ok,
+                                 const double* len, const int* npts, int* best_node,
+                                 double* best_len, int* best_npts, int* n_fin);
 
 // Multi-query batch: `steps` lockstep extend iterations of every query (config 3).
 struct MqArgs {

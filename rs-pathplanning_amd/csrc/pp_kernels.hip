@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <tuple>
 
 #include "pp_device.h"
 #include "pp_kernels.h"
@@ -72,24 +73,38 @@ __device__ inline void stage_scene(const SceneDev& sc) {
     __syncthreads();
 }
 
-template <bool kLds>
+// The scene modes a walk can be compiled for: kSceneAny tests the SceneDev fields at run time;
+// the others drop the code (and the kernel-argument registers) of the modes they exclude.
+enum : int { kSceneAny = 0, kSceneDisc = 1, kSceneGrid = 2, kScenePoly = 3 };
+__host__ __device__ inline int scene_kind(const SceneDev& sc) {
+    if (sc.bits) return kSceneGrid;
+    if (sc.ne > 0 || sc.nbv > 0) return kScenePoly;
+    return kSceneDisc;
+}
+
+template <bool kLds, int kScene = kSceneAny>
 __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool check_bounds,
                                               bool seg_valid, double qx, double qy) {
     bool oob =
         check_bounds && !(qx >= sc.minx && qx <= sc.maxx && qy >= sc.miny && qy <= sc.maxy);
     if (__any(oob)) return true;
-    if (sc.nbv > 0) {  // polygon bounds (Q10p): the eroded ring, per lane over every bounds edge
+    if ((kScene == kSceneAny || kScene == kScenePoly) && sc.nbv > 0) {
+        // polygon bounds (Q10p): the eroded ring, per lane over every bounds edge
         oob = check_bounds && !in_poly_bounds(sc.nbv, sc.bvx, sc.bvy, sc.h2, qx, qy);
         if (__any(oob)) return true;
     }
-    if (sc.bits) {  // config 4: every point of the line probes its cell (1 bit), no segments
+    if (kScene == kSceneGrid || (kScene == kSceneAny && sc.bits)) {
+        // config 4: every point of the line probes its cell (1 bit), no segments
         const uint32_t* B = kLds ? reinterpret_cast<const uint32_t*>(pp_smem) : sc.bits;
         const bool hit = check_bounds && grid_occupied(B, sc.bw, sc.bh, sc.bwords, sc.bx0, sc.by0,
                                                        sc.binv, qx, qy);
         return __any(hit);
     }
-    if (sc.m == 0 && sc.ne == 0) return false;
-    const bool poly = sc.ne > 0;  // grid items are polygon edges (Q10p), else discs
+    if (kScene == kSceneDisc ? sc.m == 0
+                             : (kScene == kScenePoly ? sc.ne == 0 : (sc.m == 0 && sc.ne == 0)))
+        return false;
+    // grid items are polygon edges (Q10p), else discs
+    const bool poly = kScene == kScenePoly || (kScene == kSceneAny && sc.ne > 0);
     // the chunk's bounding box in f32, rounded outward (DPP reductions): a box that contains the
     // points selects a superset of the cells and items, and the exact test below decides
     const double ax = shfl_up1_f64(qx);
@@ -1775,10 +1790,10 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
 // and continues with the uniform serial `pd += d` walk from the state steer_prep kept, each lane
 // capturing its own point.  npts (wave-uniform) += the polyline points generated and verified
 // (grid points plus the junction; the profiled walk roofline's unit).
-template <bool kLds>
+template <bool kLds, int kScene = kSceneAny>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
                                         const double* __restrict__ pdv, double* __restrict__ gs,
-                                        int& npts, int& napts) {
+                                        int& npts, int& napts, bool junction = true) {
     const int lane = threadIdx.x & 63;
     const int state = p->state;
     const double x = p->x, y = p->y, px = p->px, py = p->py;
@@ -1786,7 +1801,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         const bool has = lane < 2;
         const double qx = lane == 0 ? x : px, qy = lane == 0 ? y : py;
         npts += 2;
-        return chunk_rejects<kLds>(sc, has, has, lane == 1, qx, qy) ? kReject : kAccept;
+        return chunk_rejects<kLds, kScene>(sc, has, has, lane == 1, qx, qy) ? kReject : kAccept;
     }
     if (state != kPrepWalk && state != kPrepFallback) return state;
     const bool partial = state == kPrepFallback;  // pdbuf holds the first ng points only (0 or kPdCap)
@@ -1904,7 +1919,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         }
         const bool junction_here = done && cnt < 63;
         const bool isgrid = lane >= 1 && lane <= cnt;
-        const bool isj = junction_here && lane == cnt + 1;
+        const bool isj = junction && junction_here && lane == cnt + 1;
         double qx = carry_x, qy = carry_y;
         if (isgrid) {
             const int mm = my_seg == 0 ? m0 : (my_seg == 1 ? m1 : m2);
@@ -1935,9 +1950,9 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         }
         const bool has = lane == 0 || isgrid || isj;
         const bool chk = isgrid || isj || (base == 0 && lane == 0);
-        npts += cnt + (junction_here ? 1 : 0);
+        npts += cnt + (junction && junction_here ? 1 : 0);
         napts += __popcll(__ballot(isgrid && (my_seg == 0 ? m0 : (my_seg == 1 ? m1 : m2)) != kModeS));
-        if (chunk_rejects<kLds>(sc, has, chk, has && lane >= 1, qx, qy)) return kReject;
+        if (chunk_rejects<kLds, kScene>(sc, has, chk, has && lane >= 1, qx, qy)) return kReject;
         if (junction_here) break;
         carry_x = readlane_f64(qx, 63);
         carry_y = readlane_f64(qy, 63);
@@ -1945,6 +1960,55 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     // no trailing zero left for the trim (dubins.rs:281-288): the literal path decides
     if (partial && 1 + grid > p->n_point - 2) return kLiteral;
     return kAccept;
+}
+
+// One edge on one wave from the wave-uniform SteerPrep of steer_prep(): the PrepRec that
+// steer_prep_kernel would have written for it (segment trig of the origin yaws, the generator's
+// initial state, no stored grid points), walked by walk_rec — the lane-parallel exact `pd`
+// generator instead of the serial one of steer_walk.  junction = false: the polyline ends at the
+// edge's last point (finalize's edge into the root).  gs: this wave's kGenSlots LDS doubles.
+template <bool kLds>
+__device__ __forceinline__ int walk_edge(const SceneDev& sc, const SteerPrep& r, double* gs,
+                                         bool junction, int& npts, int& napts) {
+    if (r.state != kPrepWalk && r.state != kPrepNone) return r.state;
+    PrepRec p;
+    p.x = r.x;
+    p.y = r.y;
+    p.px = r.px;
+    p.py = r.py;
+    p.c = r.c;
+    p.cw = r.cw;
+    p.sw = r.sw;
+    p.ox[0] = 0.0;
+    p.oy[0] = 0.0;
+    p.ox[1] = r.o1x;
+    p.oy[1] = r.o1y;
+    p.ox[2] = r.o2x;
+    p.oy[2] = r.o2y;
+    // segment trig (dubins.rs:155-198): S cos/sin(origin yaw), L/R cos/sin(-origin yaw)
+    const double a0 = 0.0;
+    const double a1 = r.m1 == kModeS ? r.o1yaw : -r.o1yaw;
+    const double a2 = r.m2 == kModeS ? r.o2yaw : -r.o2yaw;
+    p.ca[0] = cos(a0);
+    p.sa[0] = sin(a0);
+    p.ca[1] = cos(a1);
+    p.sa[1] = sin(a1);
+    p.ca[2] = cos(a2);
+    p.sa[2] = sin(a2);
+    p.L[0] = r.L0;
+    p.L[1] = r.L1;
+    p.L[2] = r.L2;
+    p.m[0] = r.m0;
+    p.m[1] = r.m1;
+    p.m[2] = r.m2;
+    p.cnt[0] = p.cnt[1] = p.cnt[2] = 0;
+    p.n_point = r.n_point;
+    p.state = r.state == kPrepNone ? kPrepNone : kPrepFallback;
+    p.fb_dd = (r.L0 > 0.0) ? sc.step_size : -sc.step_size;
+    p.fb_pd = p.fb_dd - 0.0;  // dubins.rs:239-241
+    p.fb_seg = 0;
+    p.yaw = p.pyaw = 0.0;
+    return walk_rec<kLds>(sc, &p, nullptr, gs, npts, napts, junction);
 }
 
 // steer_walk, one task per wave (persistent grid, grid-stride over the W + ncomp tasks); kLds:
@@ -1967,7 +2031,7 @@ constexpr int kWalkMinWBatch = 6;
 // RRT* scenes (config 5) carry a ~58 KB LDS image, so LDS holds the walk at 2 workgroups per CU
 // whatever the register budget: the uncapped budget wins there (16.46 vs 15.96 M it/s, r02 A/B).
 constexpr int kWalkMinWStar = kWalkMinWWindow;
-template <bool kLds, int kMinW>
+template <bool kLds, int kMinW, int kScene>
 __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevState* __restrict__ st,
                                                          SceneDev sc,
                                                          const PrepRec* __restrict__ rec,
@@ -2000,7 +2064,7 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
         if (lane == 0) k = atomicAdd(&s_next, 1);
         const int t = (int)blockIdx.x + G * __builtin_amdgcn_readlane(k, 0);
         if (t >= total) break;
-        const int s = walk_rec<kLds>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts, napts);
+        const int s = walk_rec<kLds, kScene>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts, napts);
         if (lane == 0) {
             if (t < W) {
                 snap_status[t] = s;
@@ -2033,30 +2097,59 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
 // kMaxPerCU: the query batch's walk runs beside the other sub-batch stream's kernels and does best
 // at 2 workgroups per CU although 3 fit (a 1024-query shard 171 -> 179-183 M it/s, the 8192-query
 // batch unchanged).
+// The walk instantiation for a scene: LDS image or not, and its mode (scene_kind), as a callable
+// applied to the kernel (launch or occupancy query).
+template <int kMinW, typename F>
+inline hipError_t walk_kernel_for(const SceneDev& sc, F&& f) {
+    const bool lds = sc.lds_bytes > 0;
+    switch (scene_kind(sc)) {
+        case kSceneGrid:
+            return lds ? f(steer_walk_kernel<true, kMinW, kSceneGrid>)
+                       : f(steer_walk_kernel<false, kMinW, kSceneGrid>);
+        case kScenePoly:
+            return lds ? f(steer_walk_kernel<true, kMinW, kScenePoly>)
+                       : f(steer_walk_kernel<false, kMinW, kScenePoly>);
+        default:
+            return lds ? f(steer_walk_kernel<true, kMinW, kSceneDisc>)
+                       : f(steer_walk_kernel<false, kMinW, kSceneDisc>);
+    }
+}
+
 template <int kMinW = kWalkMinWWindow, int kMaxPerCU = 4>
-inline int walk_grid_cap(int scene_bytes) {
+inline int walk_grid_cap(const SceneDev& sc) {
     static std::mutex mu;
-    static std::map<std::pair<int, int>, int> cache;
+    static std::map<std::tuple<int, int, int>, int> cache;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     std::lock_guard<std::mutex> lk(mu);
-    auto it = cache.find({dev, scene_bytes});
+    const std::tuple<int, int, int> key{dev, sc.lds_bytes, scene_kind(sc)};
+    auto it = cache.find(key);
     if (it != cache.end()) return it->second;
     int cus = 256, per_cu = 0;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
         cus = prop.multiProcessorCount;
-    const hipError_t e =
-        scene_bytes > 0
-            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, steer_walk_kernel<true, kMinW>,
-                                                          kWalkThreads, walk_lds_bytes(scene_bytes))
-            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, steer_walk_kernel<false, kMinW>,
-                                                          kWalkThreads, walk_lds_bytes(0));
+    const hipError_t e = walk_kernel_for<kMinW>(sc, [&](auto kern) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kWalkThreads,
+                                                            walk_lds_bytes(sc.lds_bytes));
+    });
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
     per_cu = std::min(kMaxPerCU, per_cu);
     const int cap = cus * per_cu;
-    cache[{dev, scene_bytes}] = cap;
+    cache[key] = cap;
     return cap;
+}
+
+// steer_walk_kernel over a task set on stream s (its instantiation for the scene)
+template <int kMinW>
+inline void launch_walk(hipStream_t s, int blocks, DevState* st, const SceneDev& sc,
+                        const PrepRec* rec, const double* pdbuf, CandEntry* cand, int* status,
+                        const int* cand_cnt, int* pend, long long* wg_points) {
+    (void)walk_kernel_for<kMinW>(sc, [&](auto kern) {
+        kern<<<blocks, kWalkThreads, walk_lds_bytes(sc.lds_bytes), s>>>(
+            st, sc, rec, pdbuf, cand, status, cand_cnt, pend, wg_points);
+        return hipSuccess;
+    });
 }
 
 // A resolve repair (one wave): the (child, parent pose) pair steered and collision-checked anew
@@ -2583,6 +2676,12 @@ struct CfPose {
 constexpr int kCfWaves = 4;
 constexpr int kCfThreads = 64 * kCfWaves;
 
+__device__ inline bool same_pose(const CfPose& a, const CfPose& b) {
+    return __double_as_longlong(a.x) == __double_as_longlong(b.x) &&
+           __double_as_longlong(a.y) == __double_as_longlong(b.y) &&
+           __double_as_longlong(a.yaw) == __double_as_longlong(b.yaw);
+}
+
 // pose j of the finalize chain: 0 = goal, 1..s = optimised copies, then path[ps], ..., path[0]
 __device__ inline CfPose cf_pose(int j, int s, int ps, int D, const int* s_path, const int* s_pos,
                                  const TreeDev& tr, double gx, double gy, double gyaw) {
@@ -2628,11 +2727,12 @@ __device__ __forceinline__ void lit_release(int* locks, int slot) {
 template <bool kAllowNone>
 __device__ __attribute__((noinline)) long long cf_edge_check(const SceneDev& sc, CfPose a,
                                                              CfPose b, bool junction,
-                                                             double* lit_scratch, int* lit_locks) {
+                                                             double* lit_scratch, int* lit_locks,
+                                                             double* gs) {
     const SteerPrep r = steer_prep(sc, a.x, a.y, a.yaw, b.x, b.y, b.yaw);
     if (!kAllowNone && r.state == kPrepNone) return kCfPanic;
     int walked = 0, walked_arc = 0;
-    int st = steer_walk<false>(sc, walk_in(r), junction, &walked, &walked_arc);
+    int st = walk_edge<false>(sc, r, gs, junction, walked, walked_arc);
     if (st == kLiteral) {  // (measure-zero) a scratch buffer from the pool, for this edge only
         const int slot = lit_acquire(lit_locks, (int)blockIdx.x);
         double* bx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
@@ -2665,14 +2765,21 @@ __device__ inline int cf_npoint(const SceneDev& sc, CfPose a, CfPose b) {
 // kCfFinalize: finalize of the goal node (gx, gy, gyaw) with parent nodes[b] — the line is built
 // whether it verifies or not (ok_out: it does).  optimize_from_goal gives the goal gyaw_opt when
 // optimize succeeds (rrt.rs:489-501: the planner's goal yaw), else the goal node keeps gyaw.
-__global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
-    SceneDev sc, TreeDev tr, const int* __restrict__ nodes, int k, double gx, double gy,
-    double gyaw, double gyaw_opt, int level0, int mode, int want_line, int* __restrict__ ok_out,
-    double* __restrict__ len_out,
+// cb.qidx != nullptr (a query batch, pp_batch_plan): work item b is node nodes[b] of query
+// qidx[b], whose tree is rows [q * row_cap, ...) of the SoA arrays and whose goal (both yaws) is
+// goals[3q..3q+2]; its polygon-mode root block flag is blocked[q].
+// 2 waves per SIMD (<= 256 registers): two workgroups per CU (kCfGrid 512).  Measured on the
+// config-3 batch plan (598k nodes): 531 ms at 1 wave per SIMD / 256 workgroups, 302 ms here,
+// 383 ms at 4 (the register cap spills the walk)
+__global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
+    SceneDev sc, TreeDev tr_in, const int* __restrict__ nodes, int k, double gx_in, double gy_in,
+    double gyaw_in, double gyaw_opt_in, int level0, int mode, int want_line,
+    int* __restrict__ ok_out, double* __restrict__ len_out,
     int* __restrict__ npts_out, int* __restrict__ chain_out, double* __restrict__ lit_scratch,
     int* __restrict__ lit_locks, double* __restrict__ pts, int pts_cap, int* __restrict__ etab,
-    int* __restrict__ err, long long* __restrict__ tally) {
+    int* __restrict__ err, long long* __restrict__ tally, CfBatch cb) {
     __shared__ int s_path[kCfMaxDepth];
+    __shared__ double s_gs[kCfWaves][kGenSlots];  // walk_rec's generator slots, one set per wave
     __shared__ int s_pos[kCfLevels];
     __shared__ int s_st[kCfWaves];
     __shared__ int s_D, s_bad;
@@ -2692,6 +2799,21 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
         const int b = s_b;
         if (b >= k) break;
         ++t_nodes;
+        TreeDev tr = tr_in;
+        double gx = gx_in, gy = gy_in, gyaw = gyaw_in, gyaw_opt = gyaw_opt_in;
+        int root_blocked = sc.root_blocked;
+        if (cb.qidx) {
+            const int q = cb.qidx[b];
+            const size_t o = (size_t)q * cb.row_cap;
+            tr.x += o;
+            tr.y += o;
+            tr.yaw += o;
+            tr.parent += o;
+            gx = cb.goals[3 * q];
+            gy = cb.goals[3 * q + 1];
+            gyaw = gyaw_opt = cb.goals[3 * q + 2];
+            root_blocked = cb.blocked ? cb.blocked[q] : 0;
+        }
         // ancestor path, node first (NodeIter, rrt.rs:253-265), then reversed: root first
         if (tid == 0) {
             int d = 0, c = nodes[b];
@@ -2721,17 +2843,19 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
         // optimize, level by level
         int L = D - 1, s_lv = 0;
         for (int level = 0; level < kCfLevels - level0; ++level) {
+            const int Lstart = L;
             const int c = s_path[L];
             const CfPose a0{tr.x[c], tr.y[c], 0.0};
             int found = -1;
             for (int base = 0; base <= L; base += kCfWaves) {
                 const int m = base + wave;
                 int st = kReject;
-                if (m <= L && !sc.root_blocked) {
+                if (m <= L && !root_blocked) {
                     const int to = s_path[m];
                     const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
                     const CfPose a{a0.x, a0.y, atan2(bt.y - a0.y, bt.x - a0.x)};
-                    const long long rv = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks);
+                    const long long rv =
+                        cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks, s_gs[wave]);
                     st = (int)(rv & 15);
                     ++t_edges;
                     t_pts += (rv >> 4) & 0x3fffffff;
@@ -2758,6 +2882,16 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
             if (tid == 0) s_pos[level] = found;
             L = found;
             s_lv = level + 1;
+            if (Lstart == 0) {
+                // a level at the root tried its one candidate, the root copy (yaw atan2(0, 0))
+                // into the root itself, and accepted it: every further level is the very same
+                // edge with the same verdict — the chain of root copies
+                // runs to the recursion limit
+                for (int l2 = level + 1; l2 < kCfLevels - level0; ++l2)
+                    if (tid == 0) s_pos[l2] = 0;
+                s_lv = kCfLevels - level0;
+                break;
+            }
         }
         __syncthreads();
         if (mode == kCfOptimize) {
@@ -2789,11 +2923,22 @@ __global__ __launch_bounds__(kCfThreads) void check_finish_kernel(
             if (e < E) {
                 const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
                 const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                const long long rv = cf_edge_check<false>(sc, a, bp, e < E - 1, lit_scratch, lit_locks);
-                st = (int)(rv & 15);
-                ++t_edges;
-                t_pts += (rv >> 4) & 0x3fffffff;
-                t_arc += rv >> 34;
+                // an edge identical to the previous one (consecutive root copies: both poses
+                // equal bit for bit, both with the junction) has that edge's verdict, which a
+                // wave checks: only one of a run of identical edges is steered
+                bool dup = false;
+                if (e >= 1 && e < E - 1) {
+                    const CfPose ap = cf_pose(e - 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
+                    dup = same_pose(ap, a) && same_pose(a, bp);
+                }
+                if (!dup) {
+                    const long long rv = cf_edge_check<false>(sc, a, bp, e < E - 1, lit_scratch,
+                                                              lit_locks, s_gs[wave]);
+                    st = (int)(rv & 15);
+                    ++t_edges;
+                    t_pts += (rv >> 4) & 0x3fffffff;
+                    t_arc += rv >> 34;
+                }
             }
             if (lane == 0) s_st[wave] = st;
             __syncthreads();
@@ -2912,13 +3057,75 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,
                                int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
-                               int grid, long long* tally) {
+                               int grid, long long* tally, const CfBatch& cb) {
     if (k <= 0) return hipSuccess;
     check_finish_kernel<<<std::min(grid, k), kCfThreads, 0, st>>>(sc, tr, nodes, k, gx, gy, gyaw,
                                                            gyaw_opt, level0, mode, want_line, ok,
                                                            len, npts, chain, lit_scratch,
                                                            lit_locks, pts, pts_cap, etab, err,
-                                                           tally);
+                                                           tally, cb);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ RRT::plan of a query batch
+//
+// pp_batch_plan: check_finish (rrt.rs:428-438) of every accepted node of every query — nodes
+// 1 .. n_q - 1 in insertion (= iteration) order, rrt.rs:591 — by check_finish_kernel over the
+// flattened (query, node) items, then per query the first minimum euclidean_length
+// (rrt.rs:607-617).  Items of query q are [off[q], off[q + 1]), node = 1 + (b - off[q]).
+__global__ __launch_bounds__(256) void mq_plan_items_kernel(int Q, const int* __restrict__ off,
+                                                            int* __restrict__ qidx,
+                                                            int* __restrict__ nodes) {
+    const int lane = threadIdx.x & 63;
+    const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    for (int q = gw; q < Q; q += nw) {
+        const int a = off[q], e = off[q + 1];
+        for (int b = a + lane; b < e; b += 64) {
+            qidx[b] = q;
+            nodes[b] = 1 + (b - a);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void mq_plan_reduce_kernel(
+    int Q, const int* __restrict__ off, const int* __restrict__ ok, const double* __restrict__ len,
+    const int* __restrict__ npts, int* __restrict__ best_node, double* __restrict__ best_len,
+    int* __restrict__ best_npts, int* __restrict__ n_fin) {
+    const int lane = threadIdx.x & 63;
+    const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    for (int q = gw; q < Q; q += nw) {
+        const int a = off[q], e = off[q + 1];
+        double bd = __builtin_inf();
+        int bi = 0x7fffffff, cnt = 0;
+        for (int b = a + lane; b < e; b += 64) {
+            if (!ok[b]) continue;
+            ++cnt;
+            argmin_pair(bd, bi, len[b], b);  // first minimum: the lowest item on ties
+        }
+        wave_argmin(bd, bi);
+        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+        if (lane == 0) {
+            const bool any = bi != 0x7fffffff;
+            best_node[q] = any ? 1 + (bi - a) : -1;
+            best_len[q] = any ? bd : __builtin_inf();
+            best_npts[q] = any ? npts[bi] : 0;
+            n_fin[q] = cnt;
+        }
+    }
+}
+
+hipError_t launch_mq_plan_items(hipStream_t s, int Q, const int* off, int* qidx, int* nodes) {
+    mq_plan_items_kernel<<<std::min((Q + 3) / 4, 4096), 256, 0, s>>>(Q, off, qidx, nodes);
+    return hipGetLastError();
+}
+
+hipError_t launch_mq_plan_reduce(hipStream_t s, int Q, const int* off, const int* ok,
+                                 const double* len, const int* npts, int* best_node,
+                                 double* best_len, int* best_npts, int* n_fin) {
+    mq_plan_reduce_kernel<<<std::min((Q + 3) / 4, 4096), 256, 0, s>>>(
+        Q, off, ok, len, npts, best_node, best_len, best_npts, n_fin);
     return hipGetLastError();
 }
 
@@ -3115,9 +3322,8 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int nn_blocks = std::min((Q + 3) / 4, 4096);  // one wave per query
     const int prep_blocks = std::min((T + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
-                                     std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch, 2>(a.sc.lds_bytes)));
+                                     std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch, 2>(a.sc)));
     const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
-    const int lds = a.sc.lds_bytes;
     for (int k = 0; k < steps; ++k) {
         hipEvent_t* ev = a.ev ? a.ev + 5 * k : nullptr;
         if (ev) (void)hipEventRecord(ev[0], s);
@@ -3127,12 +3333,8 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
         steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, nullptr, nullptr, nullptr,
                                                       nullptr, a.rec, a.pdbuf, a.yaw, a.tasks);
         if (ev) (void)hipEventRecord(ev[2], s);
-        if (lds > 0)
-            steer_walk_kernel<true, kWalkMinWBatch><<<walk_blocks, kWalkThreads, walk_lds_bytes(lds), s>>>(
-                a.st, a.sc, a.rec, a.pdbuf, nullptr, a.status, nullptr, nullptr, a.wg_points);
-        else
-            steer_walk_kernel<false, kWalkMinWBatch><<<walk_blocks, kWalkThreads, walk_lds_bytes(0), s>>>(
-                a.st, a.sc, a.rec, a.pdbuf, nullptr, a.status, nullptr, nullptr, a.wg_points);
+        launch_walk<kWalkMinWBatch>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf, nullptr, a.status,
+                                    nullptr, nullptr, a.wg_points);
         if (ev) (void)hipEventRecord(ev[3], s);
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
                                                     a.lit_scratch, a.lit_locks, a.err);
@@ -3680,11 +3882,11 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
     const int prepA = std::min((Q + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int prepB = std::min((TB + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walkA = std::min((Q + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
-                               std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWStar>(a.sc.lds_bytes)));
+                               std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWStar>(a.sc)));
     const int lds = a.sc.lds_bytes;
     // a scene read from global memory (no LDS image) makes the walk latency-bound: fill every
     // wave slot the walk's 48 VGPRs allow (4 workgroups of 8 waves per CU)
-    const int walk_cap = lds > 0 ? std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWStar>(lds)) : 1024;
+    const int walk_cap = lds > 0 ? std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWStar>(a.sc)) : 1024;
     const int walkB = std::min((TB + kWalkThreads / 64 - 1) / (kWalkThreads / 64), walk_cap);
     // ev (profiling): 8 per step — around star_sample, then around each round's walk
     auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, const StarTaskExt* ext,
@@ -3692,12 +3894,8 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
         steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(st, a.sc, nullptr, nullptr, nullptr, nullptr,
                                                       a.rec, a.pdbuf, yaw, t, cost, ext);
         if (ev) (void)hipEventRecord(ev[0], s);
-        if (lds > 0)
-            steer_walk_kernel<true, kWalkMinWStar><<<wb, kWalkThreads, walk_lds_bytes(lds), s>>>(
-                st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr, a.wg_points);
-        else
-            steer_walk_kernel<false, kWalkMinWStar><<<wb, kWalkThreads, walk_lds_bytes(0), s>>>(
-                st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr, nullptr, a.wg_points);
+        launch_walk<kWalkMinWStar>(s, wb, st, a.sc, a.rec, a.pdbuf, nullptr, status, nullptr,
+                                   nullptr, a.wg_points);
         if (ev) (void)hipEventRecord(ev[1], s);
     };
     for (int k = 0; k < steps; ++k) {
@@ -3851,16 +4049,11 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, wsx, wsy, a.snap_pose, a.cand,
                                                   a.rec, a.pdbuf, a.snap_yaw, nullptr);
     if (ev) (void)hipEventRecord(ev[3], s);
-    const int lds = a.sc.lds_bytes;
     // snapshot tasks plus the usual few candidate tasks in one round of waves
     const int nwg = std::min((K + K / 4 + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
-                             std::min(kWalkMaxWG, walk_grid_cap(a.sc.lds_bytes)));
-    if (lds > 0)
-        steer_walk_kernel<true, kWalkMinWWindow><<<nwg, kWalkThreads, walk_lds_bytes(lds), s>>>(
-            a.st, a.sc, a.rec, a.pdbuf, a.cand, a.snap_status, a.cand_cnt, a.pend, a.wg_points);
-    else
-        steer_walk_kernel<false, kWalkMinWWindow><<<nwg, kWalkThreads, walk_lds_bytes(0), s>>>(
-            a.st, a.sc, a.rec, a.pdbuf, a.cand, a.snap_status, a.cand_cnt, a.pend, a.wg_points);
+                             std::min(kWalkMaxWG, walk_grid_cap(a.sc)));
+    launch_walk<kWalkMinWWindow>(s, nwg, a.st, a.sc, a.rec, a.pdbuf, a.cand, a.snap_status,
+                                 a.cand_cnt, a.pend, a.wg_points);
     if (ev) (void)hipEventRecord(ev[4], s);
     return hipGetLastError();
 }

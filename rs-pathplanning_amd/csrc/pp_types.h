@@ -34,7 +34,7 @@ constexpr int kWalkTallySlots = 4096;  // profiling: walk point tallies per work
 constexpr int kCfMaxDepth = 8192;    // check_finish: ancestor path staged in LDS (32 KB)
 constexpr int kCfLevels = 16;        // RECURSION_LIMIT, rrt.rs:14
 constexpr int kCfMaxEdges = kCfLevels + 1 + kCfMaxDepth;
-constexpr int kCfGrid = 256;  // check_finish workgroups (literal scratch from the pool)
+constexpr int kCfGrid = 512;        // check_finish workgroups: 2 per CU (literal scratch: the pool)
 
 // Scene in device memory (Space, rrt.rs:70-78, with Q10 analytic discs).
 struct SceneDev {

@@ -44,6 +44,7 @@ EXPORTED = [
     "pp_rrt_iteration", "pp_rrt_tree_export", "pp_rrt_get_nearest_node_batch",
     "pp_rrt_verify_node_batch", "pp_rrt_check_finish_batch", "pp_rrt_check_finish",
     "pp_rrt_plan", "pp_batch_new", "pp_batch_set_window", "pp_batch_extend", "pp_batch_state", "pp_batch_tree_export",
+    "pp_batch_plan",
     "pp_star_new", "pp_star_extend", "pp_star_state", "pp_star_tree_export",
     "pp_rrt_get_stats", "pp_rrt_reset_stats", "pp_set_profiling",
 ]
@@ -157,6 +158,7 @@ def lib():
             "pp_batch_extend": ([vp, C.c_int64, i64p, i64p], C.c_int),
             "pp_batch_state": ([vp, ip, i64p, i64p], C.c_int),
             "pp_batch_tree_export": ([vp, C.c_int, dp, dp, dp, ip, C.c_int64, i64p], C.c_int),
+            "pp_batch_plan": ([vp, ip, dp, ip, ip, i64p], C.c_int),
             "pp_star_new": ([vp, C.c_int, dp, C.POINTER(C.c_uint64), C.c_int64, C.c_double,
                              C.c_int, C.c_double], C.c_int),
             "pp_star_extend": ([vp, C.c_int64, i64p, i64p, i64p], C.c_int),

@@ -468,6 +468,23 @@ class RRTBatch:
     def set_profiling(self, on: bool):
         _ffi.check(_ffi.lib().pp_set_profiling(self.ctx.handle, int(bool(on))))
 
+    def plan(self):
+        """RRT::plan (rrt.rs:599-619) of every query on its tree as extended so far: check_finish
+        of every node the query inserted, the first minimum euclidean_length.  dict of per-query
+        arrays ``best_node`` (-1: None), ``length`` (inf: None), ``n_points`` (of the finalized
+        line), ``n_finishes``; ``checked`` = the (query, node) pairs checked."""
+        bn = np.zeros(self.q, dtype=np.int32)
+        ln = np.zeros(self.q)
+        npts = np.zeros(self.q, dtype=np.int32)
+        nf = np.zeros(self.q, dtype=np.int32)
+        chk = C.c_int64(0)
+        ip = C.POINTER(C.c_int32)
+        _ffi.check(_ffi.lib().pp_batch_plan(
+            self.ctx.handle, bn.ctypes.data_as(ip), ln.ctypes.data_as(C.POINTER(C.c_double)),
+            npts.ctypes.data_as(ip), nf.ctypes.data_as(ip), C.byref(chk)))
+        return {"best_node": bn, "length": ln, "n_points": npts, "n_finishes": nf,
+                "checked": chk.value}
+
     def tree(self, query: int, n: int | None = None):
         """(x, y, yaw, parent) of one query's tree, root first (``n``: its size, when known)."""
         n = int(self.state()[0][query]) if n is None else int(n)

@@ -1,0 +1,138 @@
+"""GPU: how often the device's libm (ocml) and the oracle's (glibc, the reference's own libm via
+Rust's f64 methods) change a discrete result of the reference's arithmetic.
+
+The decision points that a last-bit difference can flip are (a) the trailing-zero trim of
+generate_local_course (dubins.rs:281-288) on a same-position configuration, whose endpoint's local
+x is a pure rounding residue, (b) the strict-`>` word choice between mathematically tied words and
+(c) a point landing exactly on |pd| = |L|.  Measured here, and pinned:
+
+  * check_finish verdicts (optimize chains and Some/None) over EVERY node of a bench6_open tree
+    (8000 iterations) and of the example's transit tree: no flip allowed;
+  * 100k same-position Dubins configurations (dx = dy = 0, random yaws): words equal, point counts
+    may differ by the trim only (one point), at a rate below 5 %, points of the common prefix
+    within 1e-9;
+  * 100k distinct-position configurations: words and point counts all equal.
+
+The counts are printed and, with PP_FLIP_REPORT=<path>, written as JSON (profiles/)."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPORT = {}
+
+
+@pytest.fixture(scope="module")
+def ctx(pkg):
+    c = pkg.Context(0)
+    yield c
+    c.close()
+    path = os.environ.get("PP_FLIP_REPORT")
+    if path and REPORT:
+        with open(path, "w") as f:
+            json.dump(REPORT, f, indent=1, sort_keys=True)
+
+
+def _planner(raw, seed, ctx):
+    from pathplanning_amd import rrt
+
+    sx, sy, syaw = raw["start"]
+    gx, gy, gyaw = raw["goal"]
+    return rrt.RRT((sx, sy), syaw, (gx, gy), gyaw, raw["max_iter"], raw["step_size"],
+                   rrt.Space.from_raw(raw), seed=seed, window=4096, capacity=1 << 15, ctx=ctx)
+
+
+@pytest.mark.parametrize("scene,n_iter", [("bench6_open", 8000), ("transit", 2000)])
+def test_check_finish_every_node_no_verdict_flip(pkg, ctx, oracle_mod, scene, n_iter):
+    from pathplanning_amd import scenes
+
+    raw = getattr(scenes, scene)()
+    p = _planner(raw, 42, ctx)
+    p.extend(n_iter)
+    nodes = np.arange(1, p.tree_size(), dtype=np.int32)
+    r = p.check_finish_batch(nodes)
+    sc = oracle_mod.OracleScene.from_raw(raw)
+    tr = oracle_mod.OracleTree(raw["start"], n_iter + 1)
+    oracle_mod.rrt_extend(sc, tr, 42, 0, n_iter)
+    assert tr.n == p.tree_size()
+    verdict_flips = chain_flips = length_flips = ok_count = 0
+    for i, n in enumerate(nodes):
+        e = oracle_mod.check_finish(sc, tr, int(n), raw["goal"][:2], raw["goal"][2])
+        verdict_flips += bool(r["ok"][i]) != e["ok"]
+        levels = int(r["chain"][i, 0])
+        chain_flips += r["chain"][i, 2:2 + levels].tolist() != e["chain"]
+        if e["ok"] and r["ok"][i]:
+            ok_count += 1
+            if r["n_points"][i] != e["n"] or abs(r["length"][i] - e["length"]) > 1e-9 * e["length"]:
+                length_flips += 1
+    REPORT[f"check_finish_{scene}"] = {"nodes": len(nodes), "finishes": ok_count,
+                                       "verdict_flips": verdict_flips,
+                                       "chain_flips": chain_flips,
+                                       "one_point_line_flips": length_flips}
+    print(scene, REPORT[f"check_finish_{scene}"])
+    assert verdict_flips == 0 and chain_flips == 0
+    assert length_flips <= max(1, ok_count // 20)
+
+
+def _battery(pkg, ctx, oracle_mod, same, n, seed):
+    from pathplanning_amd import dubins
+
+    rng = np.random.default_rng(seed)
+    R = 0.8
+    confs = []
+    for _ in range(n):
+        sx, sy = rng.uniform(-50, 50, 2)
+        if same:
+            ex, ey = sx, sy
+        else:
+            ex, ey = sx + rng.uniform(-8, 8), sy + rng.uniform(-8, 8)
+        confs.append(dubins.DubinsConfig(sx, sy, rng.uniform(-math.pi, math.pi), ex, ey,
+                                         rng.uniform(-math.pi, math.pi), R, 0.1))
+    got = []
+    for k in range(0, n, 20000):
+        got += dubins.dubins_path_planning_batch(confs[k:k + 20000], ctx)
+    word_flips = count_flips = 0
+    worst = 0.0
+    for c, g in zip(confs, got):
+        e = oracle_mod.dubins(c.sx, c.sy, c.syaw, c.ex, c.ey, c.eyaw, c.turn_radius, c.step_size)
+        if (g is None) != (e is None):
+            word_flips += 1
+            continue
+        if g is None:
+            continue
+        if dubins.WORD_MODES.index(g[3]) != e[3]:
+            word_flips += 1
+            continue
+        m = min(len(g[0]), len(e[0]))
+        if len(g[0]) != len(e[0]):
+            count_flips += 1
+            assert abs(len(g[0]) - len(e[0])) == 1  # the trim: one point more or less
+        if m:
+            worst = max(worst, float(np.max(np.abs(g[0][:m] - e[0][:m]))),
+                        float(np.max(np.abs(g[1][:m] - e[1][:m]))))
+    return word_flips, count_flips, worst
+
+
+def test_same_position_dubins_battery(pkg, ctx, oracle_mod):
+    n = 100_000
+    w, c, worst = _battery(pkg, ctx, oracle_mod, True, n, 11)
+    REPORT["dubins_same_position"] = {"configs": n, "word_flips": w, "point_count_flips": c,
+                                      "max_point_diff": worst}
+    print(REPORT["dubins_same_position"])
+    assert w == 0
+    assert c <= n // 20
+    assert worst <= 1e-9
+
+
+def test_distinct_position_dubins_battery(pkg, ctx, oracle_mod):
+    n = 100_000
+    w, c, worst = _battery(pkg, ctx, oracle_mod, False, n, 12)
+    REPORT["dubins_distinct_position"] = {"configs": n, "word_flips": w, "point_count_flips": c,
+                                          "max_point_diff": worst}
+    print(REPORT["dubins_distinct_position"])
+    assert w == 0 and c == 0
+    assert worst <= 1e-9
