@@ -134,6 +134,11 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const float vxf = (float)(qx - ax), vyf = (float)(qy - ay);
     const float l2f = vxf * vxf + vyf * vyf;
     const float Lf = __builtin_sqrtf(l2f) * 1.000001f + sc.cull_slack;
+    // the closest-point parameter below uses 1 / |b - a|^2 (one reciprocal per lane and chunk, not
+    // a division per item): t is only approximate anyway — any t in [0, 1] gives a point of the
+    // segment, so "surely within" stays exact, and the error of "surely clear" is second order in
+    // the error of t (t minimises the distance), far inside the band
+    const float il2f = l2f > 0.0f ? __builtin_amdgcn_rcpf(l2f) : 0.0f;
     // the chunk's bbox in f32, widened by the rounding slack: an item whose cull disc misses it
     // cannot meet any of the chunk's segments
     const int lane = threadIdx.x & 63;
@@ -167,9 +172,8 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
                 // +-eps around the radius (eps bounds the f32 rounding of the coordinates, the
                 // radius and this arithmetic): only the band needs the exact f64 test and its
                 // global loads
-                float t = 0.0f;
-                if (l2f > 0.0f)
-                    t = __builtin_fminf(__builtin_fmaxf((dxf * vxf + dyf * vyf) / l2f, 0.0f), 1.0f);
+                const float t =
+                    __builtin_fminf(__builtin_fmaxf((dxf * vxf + dyf * vyf) * il2f, 0.0f), 1.0f);
                 const float ex = dxf - t * vxf, ey = dyf - t * vyf;
                 const float e2 = ex * ex + ey * ey;
                 const float eps = sc.cull_slack + 1.0e-4f * (1.0f + thr);
@@ -1790,6 +1794,23 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
 // and continues with the uniform serial `pd += d` walk from the state steer_prep kept, each lane
 // capturing its own point.  npts (wave-uniform) += the polyline points generated and verified
 // (grid points plus the junction; the profiled walk roofline's unit).
+//
+// gs: the wave's kGenSlots LDS doubles — the generator's kGenPts value slots, then the task's
+// segment table (kSegRow doubles per segment: origin x, y, trig ca, sa, mode), written once per task
+// by lanes 0-2, from which each point's lane reads its own segment's row (two ds_read_b128)
+// instead of selecting among the twelve wave-uniform values.
+//
+// The three divisions by the curvature c per point (dubins.rs:169-178: length / c, sin / c,
+// (1 - cos) / +-c) are x / c = q + (x - q c) / c rounded once: q = RN(x rc), the residual
+// fma(-q, c, x) is exact, and RN(q + residual rc) with rc = RN(1 / c) is the correctly rounded
+// quotient (Markstein's theorem; no x here is subnormal), i.e. bit-identical to the division —
+// tests/test_div_identity.py checks the identity for the scenes' curvatures.  3 VALU instead of 9.
+constexpr int kGenPts = 68;  // generator slots: 63 points + 4 overshoot + 1
+constexpr int kSegRow = 6;   // segment-table row (16-byte aligned rows: ds_read_b128)
+__device__ __forceinline__ double div_by(double x, double c, double rc) {
+    const double q = x * rc;
+    return __builtin_fma(__builtin_fma(-q, c, x), rc, q);
+}
 template <bool kLds, int kScene = kSceneAny>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
                                         const double* __restrict__ pdv, double* __restrict__ gs,
@@ -1813,6 +1834,17 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     const double L0 = p->L[0], L1 = p->L[1], L2 = p->L[2];
     const int m0 = p->m[0], m1 = p->m[1], m2 = p->m[2];
     const int n0 = p->cnt[0], n01 = n0 + p->cnt[1], ng = n01 + p->cnt[2];
+    const double rc = 1.0 / c;
+    double* segt = gs + kGenPts;
+    if (lane < 3) {
+        double* row = segt + kSegRow * lane;
+        row[0] = lane == 0 ? 0.0 : (lane == 1 ? ox1 : ox2);
+        row[1] = lane == 0 ? 0.0 : (lane == 1 ? oy1 : oy2);
+        row[2] = lane == 0 ? ca0 : (lane == 1 ? ca1 : ca2);
+        row[3] = lane == 0 ? sa0 : (lane == 1 ? sa1 : sa2);
+        row[4] = (double)(lane == 0 ? m0 : (lane == 1 ? m1 : m2));
+    }
+    __builtin_amdgcn_wave_barrier();
     // serial generator (kPrepFallback past the stored points), resumed where steer_prep stopped
     int gseg = p->fb_seg;
     double gdd = p->fb_dd;
@@ -1921,22 +1953,25 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         const bool isgrid = lane >= 1 && lane <= cnt;
         const bool isj = junction && junction_here && lane == cnt + 1;
         double qx = carry_x, qy = carry_y;
+        int mm = kModeS;
         if (isgrid) {
-            const int mm = my_seg == 0 ? m0 : (my_seg == 1 ? m1 : m2);
-            const double ox = my_seg == 0 ? 0.0 : (my_seg == 1 ? ox1 : ox2);
-            const double oy = my_seg == 0 ? 0.0 : (my_seg == 1 ? oy1 : oy2);
-            const double ca = my_seg == 0 ? ca0 : (my_seg == 1 ? ca1 : ca2);
-            const double sa = my_seg == 0 ? sa0 : (my_seg == 1 ? sa1 : sa2);
+            const double* row = segt + kSegRow * my_seg;
+            const double2 o2 = *reinterpret_cast<const double2*>(row);
+            const double2 t2 = *reinterpret_cast<const double2*>(row + 2);
+            mm = (int)row[4];
+            const double ox = o2.x, oy = o2.y, ca = t2.x, sa = t2.y;
             const double pd = my_pd;
             double lx, ly;
             if (mm == kModeS) {
-                lx = ox + pd / c * ca;
-                ly = oy + pd / c * sa;
+                const double pc = div_by(pd, c, rc);
+                lx = ox + pc * ca;
+                ly = oy + pc * sa;
             } else {
                 double sp, cp;
                 sincos(pd, &sp, &cp);  // one argument reduction for both (walk −2..3%)
-                const double ldx = sp / c;
-                const double ldy = (1.0 - cp) / (mm == kModeL ? c : -c);
+                const double ldx = div_by(sp, c, rc);
+                const double ld1 = div_by(1.0 - cp, c, rc);  // (1 - cos) / -c = -((1 - cos) / c)
+                const double ldy = mm == kModeL ? ld1 : -ld1;
                 const double gdx = ca * ldx + sa * ldy;
                 const double gdy = -sa * ldx + ca * ldy;
                 lx = ox + gdx;
@@ -1951,7 +1986,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         const bool has = lane == 0 || isgrid || isj;
         const bool chk = isgrid || isj || (base == 0 && lane == 0);
         npts += cnt + (junction && junction_here ? 1 : 0);
-        napts += __popcll(__ballot(isgrid && (my_seg == 0 ? m0 : (my_seg == 1 ? m1 : m2)) != kModeS));
+        napts += __popcll(__ballot(isgrid && mm != kModeS));
         if (chunk_rejects<kLds, kScene>(sc, has, chk, has && lane >= 1, qx, qy)) return kReject;
         if (junction_here) break;
         carry_x = readlane_f64(qx, 63);
@@ -2013,7 +2048,7 @@ __device__ __forceinline__ int walk_edge(const SceneDev& sc, const SteerPrep& r,
 
 // steer_walk, one task per wave (persistent grid, grid-stride over the W + ncomp tasks); kLds:
 // the scene's disc grid is staged into this workgroup's LDS first.
-constexpr int kGenSlots = 68;  // per-wave LDS slots of the point generator (63 + 4 overshoot + 1)
+constexpr int kGenSlots = kGenPts + 3 * kSegRow;  // per-wave LDS doubles of walk_rec
 constexpr int kWalkMaxWG = 768;  // 3 resident workgroups per CU
 __host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
     return scene_bytes + kWalkThreads / 64 * kGenSlots * 8;
@@ -2779,7 +2814,7 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
     int* __restrict__ lit_locks, double* __restrict__ pts, int pts_cap, int* __restrict__ etab,
     int* __restrict__ err, long long* __restrict__ tally, CfBatch cb) {
     __shared__ int s_path[kCfMaxDepth];
-    __shared__ double s_gs[kCfWaves][kGenSlots];  // walk_rec's generator slots, one set per wave
+    __shared__ __attribute__((aligned(16))) double s_gs[kCfWaves][kGenSlots];  // walk_rec's LDS, one set per wave
     __shared__ int s_pos[kCfLevels];
     __shared__ int s_st[kCfWaves];
     __shared__ int s_D, s_bad;
