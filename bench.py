@@ -1004,8 +1004,10 @@ def sub(D, fn, *a):
 def tree_sub(args, D, raw, workload, cpu):
     ta = argparse.Namespace(**vars(args))
     ta.no_size_sweep = True
-    return {k: v for k, v in run_tree(ta, D, raw, workload, cpu).items()
-            if k not in ("sizes", "t_max")}
+    res = {k: v for k, v in run_tree(ta, D, raw, workload, cpu).items()
+           if k not in ("sizes", "t_max")}
+    res.setdefault("unit", "iterations/s")
+    return res
 
 
 def main():
