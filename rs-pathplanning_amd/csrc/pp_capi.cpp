@@ -164,7 +164,7 @@ struct pp_ctx {
     DBuf<double> api_lit_scratch;
     HBuf<SteerTask> h_tasks;
     // check_finish
-    DBuf<int> cf_nodes, cf_ok, cf_npts, cf_chain, cf_etab, cf_err;
+    DBuf<int> cf_nodes, cf_ok, cf_npts, cf_chain, cf_etab, cf_err, cf_path, cf_items;
     DBuf<double> cf_len, cf_pts;
     // ---- multi-query batch (config 3)
     bool has_batch = false;
@@ -496,7 +496,13 @@ int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line,
     if (want_line) {
         PP_HIP(c->cf_pts.reserve((size_t)wgs * 3 * kCfPtsCap));
         PP_HIP(c->cf_etab.reserve((size_t)wgs * 2 * kCfMaxEdges));
+        PP_HIP(c->cf_items.reserve(1 + (size_t)k * kCfItem));
+        PP_HIP(hipMemsetAsync(c->cf_items.p, 0, sizeof(int), c->stream));
     }
+    // the ancestor paths: check_finish_kernel's waves (kCfWaves per workgroup, at most
+    // min(grid, k / kCfWaves) workgroups) and cf_line_kernel's workgroups (min(grid, k), each in
+    // its first wave's region)
+    PP_HIP(c->cf_path.reserve((size_t)wgs * kCfWaves * kCfMaxDepth));
     PP_HIP(c->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
     if (!c->lit_locks.p) {  // the literal scratch pool's slot locks (zero: free)
         PP_HIP(c->lit_locks.reserve(kLiteralWaves));
@@ -512,7 +518,8 @@ int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line,
                                o.npts, o.chain, c->api_lit_scratch.p, c->lit_locks.p,
                                want_line ? c->cf_pts.p : nullptr, kCfPtsCap,
                                want_line ? c->cf_etab.p : nullptr, c->cf_err.p, grid,
-                               c->prof ? c->cf_tally.p : nullptr, cb));
+                               c->prof ? c->cf_tally.p : nullptr, cb, c->cf_path.p,
+                               want_line ? c->cf_items.p : nullptr));
     if (c->prof) PP_HIP(hipEventRecord(c->ev[1], c->stream));
     int err = 0;
     PP_HIP(hipMemcpyAsync(&err, c->cf_err.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));

@@ -69,12 +69,14 @@ hipError_t launch_steer_tasks(hipStream_t st, const SceneDev& sc, const TreeDev&
                               const SteerTask* tasks, int n, int* out_status, double* out_yaw,
                               double* scratch);
 
-// RRT::check_finish for k tree nodes (one workgroup per node, `grid` workgroups).  ok/len/npts
-// per node; chain (optional) = k rows of [levels, edges, optimize's chosen ancestors...] with
-// kCfLevels + 2 ints per row; want_line: materialise verified lines (length, points of the last
-// node each workgroup handled in pts/etab).  err |= 1 depth > kCfMaxDepth, 2 finalize panic,
-// 4 steer overflow, 8 point capacity.  tally (profiling, optional): += nodes, edges steered +
-// verified, polyline points walked.
+// RRT::check_finish for k tree nodes (one wave per node, at most `grid` workgroups of kCfWaves
+// waves; gpath: grid * kCfWaves * kCfMaxDepth ints, the waves' ancestor paths).  ok/len/npts per
+// node; chain (optional) = k rows of [levels, edges, optimize's chosen ancestors...] with
+// kCfLevels + 2 ints per row; want_line: materialise the lines of the verified finishes (length;
+// points of line item i in workgroup i's pts/etab, items: 1 + k * kCfItem ints, items[0] zeroed
+// before the launch).  err |= 1 depth > kCfMaxDepth, 2 finalize panic, 4 steer overflow, 8 point
+// capacity.  tally (profiling, optional): += nodes, edges steered + verified, polyline points
+// walked.
 // check_finish_kernel modes: check_finish (rrt.rs:428-438), optimize alone (rrt.rs:463-487),
 // finalize of a caller-built goal node (rrt.rs:489-540)
 enum : int { kCfCheck = 0, kCfOptimize = 1, kCfFinalize = 2 };
@@ -90,8 +92,10 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,
                                int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
-                               int grid, long long* tally = nullptr,
-                               const CfBatch& cb = CfBatch{});
+                               int grid, long long* tally, const CfBatch& cb, int* gpath,
+                               int* items);
+constexpr int kCfWaves = 4;                     // check_finish: waves (nodes in flight) per workgroup
+constexpr int kCfItem = 4 + kCfLevels;          // a line item: b, s, verified, 0, pos[kCfLevels]
 
 // pp_batch_plan: the (query, node) items of the accepted nodes (off: [Q + 1] exclusive scan of
 // n_q - 1), and per query the first minimum length over its items' check_finish results

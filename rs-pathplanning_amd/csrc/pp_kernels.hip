@@ -2707,29 +2707,12 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_tail_kernel(WinKArgs 
 struct CfPose {
     double x, y, yaw;
 };
-// check_finish workgroup: kCfWaves candidate / finalize edges checked at a time (one per wave)
-constexpr int kCfWaves = 4;
 constexpr int kCfThreads = 64 * kCfWaves;
 
 __device__ inline bool same_pose(const CfPose& a, const CfPose& b) {
     return __double_as_longlong(a.x) == __double_as_longlong(b.x) &&
            __double_as_longlong(a.y) == __double_as_longlong(b.y) &&
            __double_as_longlong(a.yaw) == __double_as_longlong(b.yaw);
-}
-
-// pose j of the finalize chain: 0 = goal, 1..s = optimised copies, then path[ps], ..., path[0]
-__device__ inline CfPose cf_pose(int j, int s, int ps, int D, const int* s_path, const int* s_pos,
-                                 const TreeDev& tr, double gx, double gy, double gyaw) {
-    if (j == 0) return CfPose{gx, gy, gyaw};
-    if (j <= s) {
-        const int i = j - 1;
-        const int here = s_path[i == 0 ? D - 1 : s_pos[i - 1]];
-        const int to = s_path[s_pos[i]];
-        const double x = tr.x[here], y = tr.y[here];
-        return CfPose{x, y, atan2(tr.y[to] - y, tr.x[to] - x)};  // Node::new (compute_yaw)
-    }
-    const int node = s_path[ps - (j - s - 1)];
-    return CfPose{tr.x[node], tr.y[node], tr.yaw[node]};
 }
 
 // verify one edge a → b (+ junction chord to b unless junction is false) on one wave; kCfPanic
@@ -2803,118 +2786,130 @@ __device__ inline int cf_npoint(const SceneDev& sc, CfPose a, CfPose b) {
 // cb.qidx != nullptr (a query batch, pp_batch_plan): work item b is node nodes[b] of query
 // qidx[b], whose tree is rows [q * row_cap, ...) of the SoA arrays and whose goal (both yaws) is
 // goals[3q..3q+2]; its polygon-mode root block flag is blocked[q].
-// 2 waves per SIMD (<= 256 registers): two workgroups per CU (kCfGrid 512).  Measured on the
-// config-3 batch plan (598k nodes): 531 ms at 1 wave per SIMD / 256 workgroups, 302 ms here,
-// 383 ms at 4 (the register cap spills the walk)
+//
+// Two launches.  check_finish_kernel: ONE WAVE PER NODE — the waves of a workgroup are
+// independent (no barrier): each takes nodes from a launch-wide counter and runs optimize and
+// finalize's verification edge by edge, in the reference's own order, so no edge is steered
+// speculatively (the r02 form checked four candidates at a time across the workgroup's waves and
+// discarded the ones past the first accept; it also held the workgroup at a barrier per round).
+// A node whose line is wanted (a verified finish, or kCfFinalize) becomes a line item; the
+// points and the length of the line items are cf_line_kernel's, one workgroup per item.
+__device__ inline void cf_node_setup(const TreeDev& tr_in, const CfBatch& cb, int b,
+                                     double gx_in, double gy_in, double gyaw_in,
+                                     double gyaw_opt_in, int root_blocked_in, TreeDev& tr,
+                                     double& gx, double& gy, double& gyaw, double& gyaw_opt,
+                                     int& root_blocked) {
+    tr = tr_in;
+    gx = gx_in;
+    gy = gy_in;
+    gyaw = gyaw_in;
+    gyaw_opt = gyaw_opt_in;
+    root_blocked = root_blocked_in;
+    if (cb.qidx) {
+        const int q = cb.qidx[b];
+        const size_t o = (size_t)q * cb.row_cap;
+        tr.x += o;
+        tr.y += o;
+        tr.yaw += o;
+        tr.parent += o;
+        gx = cb.goals[3 * q];
+        gy = cb.goals[3 * q + 1];
+        gyaw = gyaw_opt = cb.goals[3 * q + 2];
+        root_blocked = cb.blocked ? cb.blocked[q] : 0;
+    }
+}
+
+// A node's ancestor path root first into path[0, D) (NodeIter, rrt.rs:253-265, reversed), by the
+// calling wave (lane 0 follows the parents, then the lanes reverse it); -1 past kCfMaxDepth.
+__device__ inline int cf_path(const TreeDev& tr, int node, int* __restrict__ path) {
+    const int lane = threadIdx.x & 63;
+    int d = 0;
+    if (lane == 0) {
+        int c = node;
+        while (c >= 0 && d < kCfMaxDepth) {
+            path[d++] = c;
+            c = tr.parent[c];
+        }
+        if (c >= 0) d = -1;
+    }
+    d = __shfl(d, 0);
+    __builtin_amdgcn_wave_barrier();
+    if (d > 0)
+        for (int i = lane; i < d / 2; i += 64) {
+            const int t = path[i];
+            path[i] = path[d - 1 - i];
+            path[d - 1 - i] = t;
+        }
+    __builtin_amdgcn_wave_barrier();
+    return d;
+}
+
+
 __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
     SceneDev sc, TreeDev tr_in, const int* __restrict__ nodes, int k, double gx_in, double gy_in,
     double gyaw_in, double gyaw_opt_in, int level0, int mode, int want_line,
     int* __restrict__ ok_out, double* __restrict__ len_out,
     int* __restrict__ npts_out, int* __restrict__ chain_out, double* __restrict__ lit_scratch,
-    int* __restrict__ lit_locks, double* __restrict__ pts, int pts_cap, int* __restrict__ etab,
-    int* __restrict__ err, long long* __restrict__ tally, CfBatch cb) {
-    __shared__ int s_path[kCfMaxDepth];
+    int* __restrict__ lit_locks, int* __restrict__ err, long long* __restrict__ tally, CfBatch cb,
+    int* __restrict__ gpath, int* __restrict__ items) {
     __shared__ __attribute__((aligned(16))) double s_gs[kCfWaves][kGenSlots];  // walk_rec's LDS, one set per wave
-    __shared__ int s_pos[kCfLevels];
-    __shared__ int s_st[kCfWaves];
-    __shared__ int s_D, s_bad;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    double* px = pts + (size_t)blockIdx.x * 3 * pts_cap;
-    double* py = px + pts_cap;
-    double* pyw = py + pts_cap;
-    int* et = etab + (size_t)blockIdx.x * 2 * kCfMaxEdges;
-    // nodes are taken one at a time from a launch-wide counter (err[1], zeroed with err): a
-    // node's cost varies with its depth and how far optimize climbs, so a static stride left
-    // workgroups holding a few deep nodes as the launch's tail
-    __shared__ int s_b;
+    __shared__ int s_pos[kCfWaves][kCfLevels];  // the optimize chain's path positions per wave
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    int* path = gpath + ((size_t)blockIdx.x * kCfWaves + wave) * kCfMaxDepth;  // this wave's
+    double* gs = s_gs[wave];
+    int* pos = s_pos[wave];
     long long t_nodes = 0, t_edges = 0, t_pts = 0, t_arc = 0;  // this wave's work (profiling)
     for (;;) {
-        if (tid == 0) s_b = atomicAdd(&err[1], 1);
-        __syncthreads();
-        const int b = s_b;
+        // nodes one at a time from a launch-wide counter (err[1], zeroed with err): a node's
+        // cost varies with its depth and how far optimize climbs
+        int b = 0;
+        if (lane == 0) b = atomicAdd(&err[1], 1);
+        b = __builtin_amdgcn_readfirstlane(__shfl(b, 0));
         if (b >= k) break;
         ++t_nodes;
-        TreeDev tr = tr_in;
-        double gx = gx_in, gy = gy_in, gyaw = gyaw_in, gyaw_opt = gyaw_opt_in;
-        int root_blocked = sc.root_blocked;
-        if (cb.qidx) {
-            const int q = cb.qidx[b];
-            const size_t o = (size_t)q * cb.row_cap;
-            tr.x += o;
-            tr.y += o;
-            tr.yaw += o;
-            tr.parent += o;
-            gx = cb.goals[3 * q];
-            gy = cb.goals[3 * q + 1];
-            gyaw = gyaw_opt = cb.goals[3 * q + 2];
-            root_blocked = cb.blocked ? cb.blocked[q] : 0;
-        }
-        // ancestor path, node first (NodeIter, rrt.rs:253-265), then reversed: root first
-        if (tid == 0) {
-            int d = 0, c = nodes[b];
-            while (c >= 0 && d < kCfMaxDepth) {
-                s_path[d++] = c;
-                c = tr.parent[c];
-            }
-            s_D = c >= 0 ? -1 : d;
-            s_bad = 0;
-        }
-        __syncthreads();
-        const int D = s_D;
+        TreeDev tr;
+        double gx, gy, gyaw, gyaw_opt;
+        int root_blocked;
+        cf_node_setup(tr_in, cb, b, gx_in, gy_in, gyaw_in, gyaw_opt_in, sc.root_blocked, tr, gx,
+                      gy, gyaw, gyaw_opt, root_blocked);
+        const int D = cf_path(tr, nodes[b], path);
         if (D < 0) {
-            if (tid == 0) {
+            if (lane == 0) {
                 ok_out[b] = 0;
                 atomicOr(err, 1);
             }
-            __syncthreads();
             continue;
         }
-        for (int i = tid; i < D / 2; i += kCfThreads) {
-            const int t = s_path[i];
-            s_path[i] = s_path[D - 1 - i];
-            s_path[D - 1 - i] = t;
-        }
-        __syncthreads();
-        // optimize, level by level
+        // optimize (rrt.rs:463-487), level by level: candidates path[0..L] root first, the first
+        // accepted one wins (kError before it: the reference's panic); RECURSION_LIMIT levels
+        int bad = 0;
         int L = D - 1, s_lv = 0;
         for (int level = 0; level < kCfLevels - level0; ++level) {
             const int Lstart = L;
-            const int c = s_path[L];
-            const CfPose a0{tr.x[c], tr.y[c], 0.0};
+            const int c = path[L];
+            const double ax = tr.x[c], ay = tr.y[c];
             int found = -1;
-            for (int base = 0; base <= L; base += kCfWaves) {
-                const int m = base + wave;
-                int st = kReject;
-                if (m <= L && !root_blocked) {
-                    const int to = s_path[m];
-                    const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
-                    const CfPose a{a0.x, a0.y, atan2(bt.y - a0.y, bt.x - a0.x)};
-                    const long long rv =
-                        cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks, s_gs[wave]);
-                    st = (int)(rv & 15);
-                    ++t_edges;
-                    t_pts += (rv >> 4) & 0x3fffffff;
-                    t_arc += rv >> 34;
-                }
-                if (lane == 0) s_st[wave] = st;
-                __syncthreads();
-                for (int w = 0; w < kCfWaves && found == -1; ++w) {
-                    const int sw = s_st[w];
-                    if (base + w > L || sw == kReject) continue;
-                    if (sw == kAccept)
-                        found = base + w;
-                    else
-                        found = -2;  // kError before any accept: the reference would panic
-                }
-                __syncthreads();
-                if (found != -1) break;
+            for (int m = 0; m <= L && !root_blocked; ++m) {
+                const int to = path[m];
+                const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
+                const CfPose a{ax, ay, atan2(bt.y - ay, bt.x - ax)};
+                const long long rv = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks, gs);
+                const int st = (int)(rv & 15);
+                ++t_edges;
+                t_pts += (rv >> 4) & 0x3fffffff;
+                t_arc += rv >> 34;
+                if (st == kReject) continue;
+                found = st == kAccept ? m : -2;
+                break;
             }
             if (found == -2) {
-                if (tid == 0) s_bad = 4;
+                bad = 4;
                 break;
             }
             if (found < 0) break;
-            if (tid == 0) s_pos[level] = found;
+            if (lane == 0) pos[level] = found;
+            __builtin_amdgcn_wave_barrier();
             L = found;
             s_lv = level + 1;
             if (Lstart == 0) {
@@ -2922,135 +2917,215 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
                 // into the root itself, and accepted it: every further level is the very same
                 // edge with the same verdict — the chain of root copies
                 // runs to the recursion limit
-                for (int l2 = level + 1; l2 < kCfLevels - level0; ++l2)
-                    if (tid == 0) s_pos[l2] = 0;
+                if (lane == 0)
+                    for (int l2 = level + 1; l2 < kCfLevels - level0; ++l2) pos[l2] = 0;
+                __builtin_amdgcn_wave_barrier();
                 s_lv = kCfLevels - level0;
                 break;
             }
         }
-        __syncthreads();
         if (mode == kCfOptimize) {
-            if (tid == 0) {
-                const int bad1 = s_bad;
-                ok_out[b] = (bad1 == 0 && s_lv > 0) ? 1 : 0;
+            if (lane == 0) {
+                ok_out[b] = (bad == 0 && s_lv > 0) ? 1 : 0;
                 len_out[b] = 0.0;
                 npts_out[b] = 0;
-                if (bad1) atomicOr(err, bad1);
+                if (bad) atomicOr(err, bad);
                 if (chain_out) {
                     chain_out[(size_t)b * (kCfLevels + 2)] = s_lv;
                     chain_out[(size_t)b * (kCfLevels + 2) + 1] = 0;
                     for (int i = 0; i < s_lv; ++i)
-                        chain_out[(size_t)b * (kCfLevels + 2) + 2 + i] = s_path[s_pos[i]];
+                        chain_out[(size_t)b * (kCfLevels + 2) + 2 + i] = path[pos[i]];
                 }
             }
-            __syncthreads();
             continue;
         }
-        // finalize: verify the chain's edges
+        // finalize (rrt.rs:503-540): the chain goal -> optimised copies -> tree path -> root,
+        // every edge verified with its junction chord, the edge into the root without one
         const int s = s_lv;
         const double gyaw_e = s > 0 ? gyaw_opt : gyaw;  // optimize_from_goal (rrt.rs:489-501)
-        const int ps = s > 0 ? s_pos[s - 1] : D - 1;
+        const int ps = s > 0 ? pos[s - 1] : D - 1;
         const int E = 1 + s + ps;
-        bool vok = s_bad == 0;
-        for (int base = 0; base < E && vok; base += kCfWaves) {
-            const int e = base + wave;
-            int st = kAccept;
-            if (e < E) {
-                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
+        bool vok = bad == 0;
+        // pose j of the chain (cf_pose's indexing, the chain positions in registers)
+        auto pose = [&](int j) -> CfPose {
+            if (j == 0) return CfPose{gx, gy, gyaw_e};
+            if (j <= s) {
+                const int i = j - 1;
+                const int here = path[i == 0 ? D - 1 : pos[i - 1]];
+                const int to = path[pos[i]];
+                const double x = tr.x[here], y = tr.y[here];
+                return CfPose{x, y, atan2(tr.y[to] - y, tr.x[to] - x)};  // Node::new (compute_yaw)
+            }
+            const int node = path[ps - (j - s - 1)];
+            return CfPose{tr.x[node], tr.y[node], tr.yaw[node]};
+        };
+        if (vok) {
+            CfPose prev{0.0, 0.0, 0.0}, a = pose(0);
+            int prev_st = kAccept;
+            for (int e = 0; e < E; ++e) {
+                const CfPose bp = pose(e + 1);
                 // an edge identical to the previous one (consecutive root copies: both poses
-                // equal bit for bit, both with the junction) has that edge's verdict, which a
-                // wave checks: only one of a run of identical edges is steered
-                bool dup = false;
-                if (e >= 1 && e < E - 1) {
-                    const CfPose ap = cf_pose(e - 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                    dup = same_pose(ap, a) && same_pose(a, bp);
-                }
+                // equal bit for bit, both with the junction) has that edge's verdict
+                const bool dup = e >= 1 && e < E - 1 && same_pose(prev, a) && same_pose(a, bp);
+                int st = prev_st;
                 if (!dup) {
                     const long long rv = cf_edge_check<false>(sc, a, bp, e < E - 1, lit_scratch,
-                                                              lit_locks, s_gs[wave]);
+                                                              lit_locks, gs);
                     st = (int)(rv & 15);
                     ++t_edges;
                     t_pts += (rv >> 4) & 0x3fffffff;
                     t_arc += rv >> 34;
                 }
-            }
-            if (lane == 0) s_st[wave] = st;
-            __syncthreads();
-            for (int w = 0; w < kCfWaves; ++w) {
-                const int sw = s_st[w];
-                if (sw == kCfPanic || sw == kError) {
-                    if (tid == 0) s_bad = sw == kCfPanic ? 2 : 4;
+                if (st != kAccept) {
+                    if (st == kCfPanic) bad = 2;
+                    else if (st == kError) bad = 4;
                     vok = false;
-                } else if (sw != kAccept) {
-                    vok = false;
+                    break;
                 }
+                prev = a;
+                a = bp;
+                prev_st = st;
             }
-            __syncthreads();
         }
         // polygon mode: the chain's line is connected and no segment met an edge buffer, so it
         // lies on one side of every obstacle boundary — the goal decides (Q10p)
         if (vok && sc.ne > 0 && in_obstacle(sc.ne, sc.ex0, sc.ey0, sc.ex1, sc.ey1, sc.epoly, gx, gy))
             vok = false;
-        // a panic anywhere in finalize wins over a rejection (the reference panics first): scan
-        // the remaining edges for None steers
-        if (s_bad == 0 && !vok) {
-            for (int e = tid; e < E; e += kCfThreads) {
-                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                if (cf_npoint(sc, a, bp) == 0) atomicOr(&s_bad, 2);
-            }
-            __syncthreads();
+        // a panic anywhere in finalize wins over a rejection (the reference builds the whole line
+        // before it verifies): the other edges' steers, lane-parallel
+        if (bad == 0 && !vok) {
+            bool none = false;
+            for (int e = lane; e < E; e += 64)
+                if (cf_npoint(sc, pose(e), pose(e + 1)) == 0) none = true;
+            if (__any(none)) bad = 2;
         }
-        const int bad = s_bad;
-        double len = 0.0;
-        int npts = 0;
         if ((vok || mode == kCfFinalize) && bad == 0 && want_line) {
-            // edge capacities, offsets, literal points
+            // the line's points and length: a cf_line_kernel item
+            if (lane == 0) {
+                const int it = atomicAdd(&items[0], 1);
+                int* o = items + 1 + (size_t)it * kCfItem;
+                o[0] = b;
+                o[1] = s;
+                o[2] = vok ? 1 : 0;
+                o[3] = 0;
+                for (int i = 0; i < kCfLevels; ++i) o[4 + i] = i < s ? pos[i] : 0;
+            }
+        } else if (lane == 0) {
+            ok_out[b] = (vok && bad == 0) ? 1 : 0;
+            len_out[b] = 0.0;
+            npts_out[b] = 0;
+            if (bad) atomicOr(err, bad);
+        }
+        if (lane == 0 && chain_out) {
+            chain_out[(size_t)b * (kCfLevels + 2)] = s;
+            chain_out[(size_t)b * (kCfLevels + 2) + 1] = E;
+            for (int i = 0; i < s; ++i)
+                chain_out[(size_t)b * (kCfLevels + 2) + 2 + i] = path[pos[i]];
+        }
+    }
+    if (tally && lane == 0) {  // profiling: nodes, edges, points
+        unsigned long long* tl = reinterpret_cast<unsigned long long*>(tally);
+        atomicAdd(&tl[0], (unsigned long long)t_nodes);
+        atomicAdd(&tl[1], (unsigned long long)t_edges);
+        atomicAdd(&tl[2], (unsigned long long)t_pts);
+        atomicAdd(&tl[3], (unsigned long long)t_arc);
+    }
+}
+
+// The lines of check_finish_kernel's line items: workgroup w takes items w, w + grid, ... (item
+// i < grid: the workgroup-i buffers, so a one-node call's line is in workgroup 0's); every
+// edge's literal Dubins points (dubins_literal, a lane per edge) into the workgroup's pts / etab,
+// then l.reverse() and geo's euclidean_length in that order (rrt.rs:538, one lane: a sum of
+// hypot in line order).
+__global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
+    SceneDev sc, TreeDev tr_in, const int* __restrict__ nodes, double gx_in, double gy_in,
+    double gyaw_in, double gyaw_opt_in, int* __restrict__ ok_out, double* __restrict__ len_out,
+    int* __restrict__ npts_out, double* __restrict__ pts, int pts_cap, int* __restrict__ etab,
+    int* __restrict__ err, CfBatch cb, int* __restrict__ gpath, const int* __restrict__ items) {
+    __shared__ int s_off, s_bad;
+    __shared__ int s_pos[kCfLevels];
+    const int tid = threadIdx.x;
+    double* px = pts + (size_t)blockIdx.x * 3 * pts_cap;
+    double* py = px + pts_cap;
+    double* pyw = py + pts_cap;
+    int* et = etab + (size_t)blockIdx.x * 2 * kCfMaxEdges;
+    int* path = gpath + (size_t)blockIdx.x * kCfWaves * kCfMaxDepth;  // (wave 0's region)
+    const int n_items = items[0];
+    for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+        const int* o = items + 1 + (size_t)it * kCfItem;
+        const int b = o[0], s = o[1], vok = o[2];
+        if (tid < kCfLevels) s_pos[tid] = o[4 + tid];
+        const int* pos = s_pos;
+        TreeDev tr;
+        double gx, gy, gyaw, gyaw_opt;
+        int root_blocked;
+        cf_node_setup(tr_in, cb, b, gx_in, gy_in, gyaw_in, gyaw_opt_in, sc.root_blocked, tr, gx,
+                      gy, gyaw, gyaw_opt, root_blocked);
+        int D = 0;
+        if (tid < 64) D = cf_path(tr, nodes[b], path);
+        if (tid == 0) s_off = D;
+        __syncthreads();
+        D = s_off;
+        const double gyaw_e = s > 0 ? gyaw_opt : gyaw;
+        const int ps = s > 0 ? pos[s - 1] : D - 1;
+        const int E = 1 + s + ps;
+        auto pose = [&](int j) -> CfPose {
+            if (j == 0) return CfPose{gx, gy, gyaw_e};
+            if (j <= s) {
+                const int i = j - 1;
+                const int here = path[i == 0 ? D - 1 : pos[i - 1]];
+                const int to = path[pos[i]];
+                const double x = tr.x[here], y = tr.y[here];
+                return CfPose{x, y, atan2(tr.y[to] - y, tr.x[to] - x)};
+            }
+            const int node = path[ps - (j - s - 1)];
+            return CfPose{tr.x[node], tr.y[node], tr.yaw[node]};
+        };
+        if (tid == 0) s_bad = 0;
+        for (int e = tid; e < E; e += kCfThreads) et[2 * e] = cf_npoint(sc, pose(e), pose(e + 1));
+        __syncthreads();
+        if (tid == 0) {  // edge capacities -> offsets
+            int off = 0;
+            bool neg = false;
+            for (int e = 0; e < E; ++e) {
+                const int c = et[2 * e];
+                neg |= c <= 0;
+                et[2 * e] = off;
+                off += c > 0 ? c : 0;
+            }
+            s_off = (off <= pts_cap && !neg) ? off : -1;
+        }
+        __syncthreads();
+        const int total = s_off;
+        if (total < 0) {
+            if (tid == 0) s_bad = 8;  // (a None / overflowing edge was rejected before)
+        } else {
             for (int e = tid; e < E; e += kCfThreads) {
-                const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                et[2 * e] = cf_npoint(sc, a, bp);
+                const int off = et[2 * e];
+                const int cap = (e + 1 < E ? et[2 * e + 2] : total) - off;
+                const CfPose a = pose(e), bp = pose(e + 1);
+                int n = 0, word = -1;
+                double cost = 0.0;
+                const int r = dubins_literal(a.x, a.y, a.yaw, bp.x, bp.y, bp.yaw, sc.turn_radius,
+                                             sc.step_size, px + off, py + off, pyw + off, cap, &n,
+                                             &word, &cost);
+                et[2 * e + 1] = r == kSteerSome ? n : 0;
+                if (r != kSteerSome) atomicOr(&s_bad, 2);
             }
-            __syncthreads();
-            if (tid == 0) {
-                int off = 0;
-                bool neg = false;
-                for (int e = 0; e < E; ++e) {
-                    const int c = et[2 * e];
-                    neg |= c <= 0;
-                    et[2 * e] = off;
-                    off += c > 0 ? c : 0;
-                }
-                s_D = (off <= pts_cap && !neg) ? off : -1;
-            }
-            __syncthreads();
-            if (s_D < 0) {
-                if (tid == 0) s_bad = 8;  // (a None / overflowing edge was rejected above)
-            } else {
-                for (int e = tid; e < E; e += kCfThreads) {
-                    const CfPose a = cf_pose(e, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                    const CfPose bp = cf_pose(e + 1, s, ps, D, s_path, s_pos, tr, gx, gy, gyaw_e);
-                    const int o = et[2 * e];
-                    const int cap = (e + 1 < E ? et[2 * e + 2] : s_D) - o;
-                    int n = 0, word = -1;
-                    double cost = 0.0;
-                    const int r = dubins_literal(a.x, a.y, a.yaw, bp.x, bp.y, bp.yaw,
-                                                 sc.turn_radius, sc.step_size, px + o, py + o,
-                                                 pyw + o, cap, &n, &word, &cost);
-                    et[2 * e + 1] = r == kSteerSome ? n : 0;
-                    if (r != kSteerSome) atomicOr(&s_bad, 2);
-                }
-            }
-            __syncthreads();
-            if (tid == 0 && s_bad == 0) {
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double len = 0.0;
+            int npts = 0;
+            const int bad = s_bad;
+            if (bad == 0) {
                 // l.reverse() (rrt.rs:538), then euclidean_length in that order
                 bool have = false;
                 double qx = 0.0, qy = 0.0;
                 for (int e = E - 1; e >= 0; --e) {
-                    const int o = et[2 * e], n = et[2 * e + 1];
+                    const int off = et[2 * e], n = et[2 * e + 1];
                     for (int i = n - 1; i >= 0; --i) {
-                        const double x = px[o + i], y = py[o + i];
+                        const double x = px[off + i], y = py[off + i];
                         if (have) len += hypot(x - qx, y - qy);
                         qx = x;
                         qy = y;
@@ -3058,32 +3133,13 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
                     }
                     npts += n;
                 }
-                s_D = npts;
             }
-            __syncthreads();
-            npts = s_D;
+            ok_out[b] = (vok && bad == 0) ? 1 : 0;
+            len_out[b] = bad == 0 ? len : 0.0;
+            npts_out[b] = bad == 0 ? npts : 0;
+            if (bad) atomicOr(err, bad);
         }
-        if (tid == 0) {
-            const int bad2 = s_bad;
-            ok_out[b] = (vok && bad2 == 0) ? 1 : 0;
-            len_out[b] = len;
-            npts_out[b] = npts;
-            if (bad2) atomicOr(err, bad2);
-            if (chain_out) {
-                chain_out[(size_t)b * (kCfLevels + 2)] = s;
-                chain_out[(size_t)b * (kCfLevels + 2) + 1] = E;
-                for (int i = 0; i < s; ++i)
-                    chain_out[(size_t)b * (kCfLevels + 2) + 2 + i] = s_path[s_pos[i]];
-            }
-        }
-        __syncthreads();
-    }
-    if (tally && lane == 0) {  // profiling: nodes (counted once, by wave 0), edges, points
-        unsigned long long* tl = reinterpret_cast<unsigned long long*>(tally);
-        if (wave == 0) atomicAdd(&tl[0], (unsigned long long)t_nodes);
-        atomicAdd(&tl[1], (unsigned long long)t_edges);
-        atomicAdd(&tl[2], (unsigned long long)t_pts);
-        atomicAdd(&tl[3], (unsigned long long)t_arc);
+        __syncthreads();  // the buffers and s_off serve the next item
     }
 }
 
@@ -3092,13 +3148,18 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,
                                int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
-                               int grid, long long* tally, const CfBatch& cb) {
+                               int grid, long long* tally, const CfBatch& cb, int* gpath,
+                               int* items) {
     if (k <= 0) return hipSuccess;
-    check_finish_kernel<<<std::min(grid, k), kCfThreads, 0, st>>>(sc, tr, nodes, k, gx, gy, gyaw,
-                                                           gyaw_opt, level0, mode, want_line, ok,
-                                                           len, npts, chain, lit_scratch,
-                                                           lit_locks, pts, pts_cap, etab, err,
-                                                           tally, cb);
+    const int wgs = std::min(grid, (k + kCfWaves - 1) / kCfWaves);
+    check_finish_kernel<<<wgs, kCfThreads, 0, st>>>(sc, tr, nodes, k, gx, gy, gyaw, gyaw_opt,
+                                                    level0, mode, want_line, ok, len, npts, chain,
+                                                    lit_scratch, lit_locks, err, tally, cb, gpath,
+                                                    items);
+    if (want_line && mode != kCfOptimize)
+        cf_line_kernel<<<std::min(grid, k), kCfThreads, 0, st>>>(
+            sc, tr, nodes, gx, gy, gyaw, gyaw_opt, ok, len, npts, pts, pts_cap, etab, err, cb,
+            gpath, items);
     return hipGetLastError();
 }
 
