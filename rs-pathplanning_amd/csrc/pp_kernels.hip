@@ -1541,6 +1541,207 @@ __device__ inline Pt seg_end(int mode, double len, double c, double ox, double o
     return r;
 }
 
+// The per-task body of steer_prep: the 8 lanes r of one task group (all 64 lanes of the wave
+// call it: the word choice broadcasts within 8-lane groups).  act: an active task (else a
+// kReject record); write: this group owns task t (lane r == 0 stores rec[t], *yaw_dst and
+// cost_out[t]).
+__device__ __forceinline__ void prep_task(const SceneDev& sc, int r, int g0, int t, bool write,
+                                          bool act, double x, double y, double px, double py,
+                                          double pyaw, int own, double cyaw, int cull, double cbase,
+                                          double climit, PrepRec* __restrict__ rec,
+                                          double* yaw_dst, double* __restrict__ cost_out) {
+    const double step = sc.step_size;
+    const double c = 1.0 / sc.turn_radius;
+    const double cy_atan = atan2(py - y, px - x);
+    const double yaw = own ? cyaw : cy_atan;
+    // dubins_path_planning, dubins.rs:401-408 (s = child, e = parent)
+    const double ex = px - x, ey = py - y;
+    const double cyw = cos(yaw), syw = sin(yaw);
+    const double lex = cyw * ex + syw * ey;
+    const double ley = -(syw)*ex + cyw * ey;
+    const double leyaw = pyaw - yaw;
+    // dubins_path_planning_from_origin, dubins.rs:333-348
+    const double hyp = hypot(lex, ley);
+    const double d = hyp * c;
+    const double theta = mod2pi(atan2(ley, lex));
+    const double alpha = mod2pi(-theta);
+    const double beta = mod2pi(leyaw - theta);
+    // lanes 0/1: sin(alpha), sin(beta); lanes 0/1/2: cos(alpha), cos(beta), cos(alpha - beta)
+    const double s_in = sin(r == 0 ? alpha : beta);
+    const double c_in = cos(r == 0 ? alpha : (r == 1 ? beta : alpha - beta));
+    const double sa = grp8_bcast_f64<0>(s_in), sb = grp8_bcast_f64<1>(s_in);
+    const double ca = grp8_bcast_f64<0>(c_in), cb = grp8_bcast_f64<1>(c_in),
+                 c_ab = grp8_bcast_f64<2>(c_in);
+    // lane r < 6 evaluates word r of ALL_PLANNERS (dubins.rs:27-153, 291)
+    const double dd2 = d * d;
+    double ya = 0.0, xa = 1.0, psq = -1.0, tmpc = 2.0;
+    if (r == 0) {
+        psq = 2.0 + dd2 - (2.0 * c_ab) + (2.0 * d * (sa - sb));
+        ya = cb - ca;
+        xa = d + sa - sb;
+    } else if (r == 1) {
+        psq = 2.0 + dd2 - (2.0 * c_ab) + (2.0 * d * (sb - sa));
+        ya = ca - cb;
+        xa = d - sa + sb;
+    } else if (r == 2) {
+        psq = -2.0 + dd2 + (2.0 * c_ab) + (2.0 * d * (sa + sb));
+        ya = -ca - cb;
+        xa = d + sa + sb;
+    } else if (r == 3) {
+        psq = -2.0 + dd2 + (2.0 * c_ab) - (2.0 * d * (sa + sb));
+        ya = ca + cb;
+        xa = d - sa - sb;
+    } else if (r == 4) {
+        tmpc = (6.0 - dd2 + 2.0 * c_ab + 2.0 * d * (sa - sb)) / 8.0;
+        ya = ca - cb;
+        xa = d - sa + sb;
+    } else if (r == 5) {
+        tmpc = (6.0 - dd2 + 2.0 * c_ab + 2.0 * d * (-sa + sb)) / 8.0;
+        ya = ca - cb;
+        xa = d + sa - sb;
+    }
+    const bool wok = r < 4 ? !(psq < 0.0) : (r < 6 ? !(fabs(tmpc) > 1.0) : false);
+    const double A1 = atan2(ya, xa);
+    const double pp = sqrt(r < 4 && wok ? psq : 0.0);
+    const double A2 = atan2(r == 2 ? -2.0 : 2.0, pp);
+    const double Cc = acos(r >= 4 && wok ? tmpc : 0.0);
+    double wt = 0.0, wp = 0.0, wq = 0.0;
+    if (r == 0) {
+        wt = mod2pi(-alpha + A1);
+        wp = pp;
+        wq = mod2pi(beta - A1);
+    } else if (r == 1) {
+        wt = mod2pi(alpha - A1);
+        wp = pp;
+        wq = mod2pi(-beta + A1);
+    } else if (r == 2) {
+        const double tm = A1 - A2;
+        wt = mod2pi(-alpha + tm);
+        wp = pp;
+        wq = mod2pi(-mod2pi(beta) + tm);
+    } else if (r == 3) {
+        const double tm = A1 - A2;
+        wt = mod2pi(alpha - tm);
+        wp = pp;
+        wq = mod2pi(beta - tm);
+    } else if (r == 4) {
+        wp = mod2pi(2.0 * kPi - Cc);
+        wt = mod2pi(alpha - A1 + mod2pi(wp / 2.0));
+        wq = mod2pi(alpha - beta - wt + mod2pi(wp));
+    } else if (r == 5) {
+        wp = mod2pi(2.0 * kPi - Cc);
+        wt = mod2pi(-alpha - A1 + wp / 2.0);
+        wq = mod2pi(mod2pi(beta) - alpha - wt + mod2pi(wp));
+    }
+    const double wcost = fabs(wt) + fabs(wp) + fabs(wq);
+    // first strict minimum in ALL_PLANNERS order (dubins.rs:351-360)
+    double bc = __builtin_inf();
+    int bw = -1;
+    const double wc[6] = {grp8_bcast_f64<0>(wcost), grp8_bcast_f64<1>(wcost),
+                          grp8_bcast_f64<2>(wcost), grp8_bcast_f64<3>(wcost),
+                          grp8_bcast_f64<4>(wcost), grp8_bcast_f64<5>(wcost)};
+    const int wk[6] = {grp8_bcast_i32<0>((int)wok), grp8_bcast_i32<1>((int)wok),
+                       grp8_bcast_i32<2>((int)wok), grp8_bcast_i32<3>((int)wok),
+                       grp8_bcast_i32<4>((int)wok), grp8_bcast_i32<5>((int)wok)};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        if (wk[k] && bc > wc[k]) {
+            bc = wc[k];
+            bw = k;
+        }
+    }
+    const int src = g0 + (bw < 0 ? 0 : bw);
+    const double L0 = __shfl(wt, src), L1 = __shfl(wp, src), L2 = __shfl(wq, src);
+    const int m0 = word_mode(bw, 0), m1 = word_mode(bw, 1), m2 = word_mode(bw, 2);
+    int state = !act ? kReject : (bw < 0 ? kPrepNone : kPrepWalk);
+    double tot = 0.0;
+    tot += L0;
+    tot += L1;
+    tot += L2;
+    const double nq = trunc(tot / step);
+    if (state == kPrepWalk && (!(nq >= 0.0) || nq > 1.0e8)) state = kError;
+    // segment origin headings (interpolate's yaw, dubins.rs:191-196)
+    const double oy0 = 0.0;
+    const double oy1 = m0 == kModeL ? oy0 + L0 : (m0 == kModeR ? oy0 - L0 : oy0);
+    const double oy2 = m1 == kModeL ? oy1 + L1 : (m1 == kModeR ? oy1 - L1 : oy1);
+    // lanes 0..2: segment trig, 3..5: sin/cos of the lengths, 6: the world transform
+    double arg = 0.0;
+    if (r < 3) {
+        const int ms = r == 0 ? m0 : (r == 1 ? m1 : m2);
+        const double oys = r == 0 ? oy0 : (r == 1 ? oy1 : oy2);
+        arg = ms == kModeS ? oys : -oys;
+    } else if (r < 6) {
+        arg = r == 3 ? L0 : (r == 4 ? L1 : L2);
+    } else if (r == 6) {
+        arg = -yaw;
+    }
+    const double sv = sin(arg), cv = cos(arg);
+    const double ca0 = grp8_bcast_f64<0>(cv), ca1 = grp8_bcast_f64<1>(cv), ca2 = grp8_bcast_f64<2>(cv);
+    const double sa0 = grp8_bcast_f64<0>(sv), sa1 = grp8_bcast_f64<1>(sv), sa2 = grp8_bcast_f64<2>(sv);
+    const double sl0 = grp8_bcast_f64<3>(sv), sl1 = grp8_bcast_f64<4>(sv), sl2 = grp8_bcast_f64<5>(sv);
+    const double cl0 = grp8_bcast_f64<3>(cv), cl1 = grp8_bcast_f64<4>(cv), cl2 = grp8_bcast_f64<5>(cv);
+    const double cw = grp8_bcast_f64<6>(cv), sw = grp8_bcast_f64<6>(sv);
+    const Pt O1 = seg_end(m0, L0, c, 0.0, 0.0, ca0, sa0, sl0, cl0);
+    const Pt O2 = seg_end(m1, L1, c, O1.x, O1.y, ca1, sa1, sl1, cl1);
+    const Pt E = seg_end(m2, L2, c, O2.x, O2.y, ca2, sa2, sl2, cl2);
+    // the trim (dubins.rs:281-288) drops exactly the endpoint unless its local x is 0.0
+    if (state == kPrepWalk && E.x == 0.0) state = kLiteral;
+    int cnt0 = 0, cnt1 = 0, cnt2 = 0, fb_seg = 0;
+    double fb_pd = 0.0, fb_dd = 0.0;
+    // no grid points are stored: steer_walk generates them all, lane-parallel and bit-exact,
+    // from the walk's initial state (segment 0, pd = d - 0.0, dubins.rs:239-241), and runs
+    // the trailing-zero check itself
+    if (state == kPrepWalk) {
+        state = kPrepFallback;
+        fb_dd = (L0 > 0.0) ? step : -step;
+        fb_pd = fb_dd - 0.0;
+    }
+    // RRT* cull: an edge whose cost cannot beat the limit is settled without its walk
+    if (act && cull && !(cbase + bc < climit)) state = kReject;
+    if (write && r == 0) {  // idle batch tasks get a kReject record (act == false)
+        PrepRec o;
+        o.x = x;
+        o.y = y;
+        o.px = px;
+        o.py = py;
+        o.yaw = yaw;
+        o.pyaw = pyaw;
+        o.c = c;
+        o.cw = cw;
+        o.sw = sw;
+        o.ox[0] = 0.0;
+        o.oy[0] = 0.0;
+        o.ox[1] = O1.x;
+        o.oy[1] = O1.y;
+        o.ox[2] = O2.x;
+        o.oy[2] = O2.y;
+        o.ca[0] = ca0;
+        o.ca[1] = ca1;
+        o.ca[2] = ca2;
+        o.sa[0] = sa0;
+        o.sa[1] = sa1;
+        o.sa[2] = sa2;
+        o.L[0] = L0;
+        o.L[1] = L1;
+        o.L[2] = L2;
+        o.n_point = (long long)nq + 3 + 4;
+        o.fb_pd = fb_pd;
+        o.fb_dd = fb_dd;
+        o.fb_seg = fb_seg;
+        o.m[0] = m0;
+        o.m[1] = m1;
+        o.m[2] = m2;
+        o.cnt[0] = cnt0;
+        o.cnt[1] = cnt1;
+        o.cnt[2] = cnt2;
+        o.state = state;
+        rec[t] = o;
+        if (yaw_dst) *yaw_dst = yaw;
+        // the Dubins cost (dubins.rs:351-361; inf on None): the RRT* edge cost
+        if (cost_out) cost_out[t] = bc;
+    }
+}
+
 // steer_prep: kPrepLanes lanes per task, 8 tasks per wave (persistent grid over the
 // window's W + ncomp tasks): compute_yaw (rrt.rs:267-271),
 // dubins_path_planning's frame change and word choice (dubins.rs:333-363, 401-408) and the
@@ -1562,8 +1763,6 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     const int r = lane & (kPrepLanes - 1), g0 = lane & ~(kPrepLanes - 1);
     constexpr int TPW = 64 / kPrepLanes;  // tasks per wave in phase A
     static_assert(kPrepLanes == 8, "the per-task broadcasts are grp8_bcast (8-lane groups)");
-    const double step = sc.step_size;
-    const double c = 1.0 / sc.turn_radius;
     constexpr int TPB = kPrepThreads / 64 * TPW;  // tasks per workgroup
     for (int blk = blockIdx.x; blk * TPB < total; blk += gridDim.x) {
         const int t = blk * TPB + wave * TPW + lane / kPrepLanes;
@@ -1592,197 +1791,10 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
             x = wsx[j];
             y = wsy[j];
         }
-        const double cy_atan = atan2(py - y, px - x);
-        const double yaw = own ? cyaw : cy_atan;
-        // dubins_path_planning, dubins.rs:401-408 (s = child, e = parent)
-        const double ex = px - x, ey = py - y;
-        const double cyw = cos(yaw), syw = sin(yaw);
-        const double lex = cyw * ex + syw * ey;
-        const double ley = -(syw)*ex + cyw * ey;
-        const double leyaw = pyaw - yaw;
-        // dubins_path_planning_from_origin, dubins.rs:333-348
-        const double hyp = hypot(lex, ley);
-        const double d = hyp * c;
-        const double theta = mod2pi(atan2(ley, lex));
-        const double alpha = mod2pi(-theta);
-        const double beta = mod2pi(leyaw - theta);
-        // lanes 0/1: sin(alpha), sin(beta); lanes 0/1/2: cos(alpha), cos(beta), cos(alpha - beta)
-        const double s_in = sin(r == 0 ? alpha : beta);
-        const double c_in = cos(r == 0 ? alpha : (r == 1 ? beta : alpha - beta));
-        const double sa = grp8_bcast_f64<0>(s_in), sb = grp8_bcast_f64<1>(s_in);
-        const double ca = grp8_bcast_f64<0>(c_in), cb = grp8_bcast_f64<1>(c_in),
-                     c_ab = grp8_bcast_f64<2>(c_in);
-        // lane r < 6 evaluates word r of ALL_PLANNERS (dubins.rs:27-153, 291)
-        const double dd2 = d * d;
-        double ya = 0.0, xa = 1.0, psq = -1.0, tmpc = 2.0;
-        if (r == 0) {
-            psq = 2.0 + dd2 - (2.0 * c_ab) + (2.0 * d * (sa - sb));
-            ya = cb - ca;
-            xa = d + sa - sb;
-        } else if (r == 1) {
-            psq = 2.0 + dd2 - (2.0 * c_ab) + (2.0 * d * (sb - sa));
-            ya = ca - cb;
-            xa = d - sa + sb;
-        } else if (r == 2) {
-            psq = -2.0 + dd2 + (2.0 * c_ab) + (2.0 * d * (sa + sb));
-            ya = -ca - cb;
-            xa = d + sa + sb;
-        } else if (r == 3) {
-            psq = -2.0 + dd2 + (2.0 * c_ab) - (2.0 * d * (sa + sb));
-            ya = ca + cb;
-            xa = d - sa - sb;
-        } else if (r == 4) {
-            tmpc = (6.0 - dd2 + 2.0 * c_ab + 2.0 * d * (sa - sb)) / 8.0;
-            ya = ca - cb;
-            xa = d - sa + sb;
-        } else if (r == 5) {
-            tmpc = (6.0 - dd2 + 2.0 * c_ab + 2.0 * d * (-sa + sb)) / 8.0;
-            ya = ca - cb;
-            xa = d + sa - sb;
-        }
-        const bool wok = r < 4 ? !(psq < 0.0) : (r < 6 ? !(fabs(tmpc) > 1.0) : false);
-        const double A1 = atan2(ya, xa);
-        const double pp = sqrt(r < 4 && wok ? psq : 0.0);
-        const double A2 = atan2(r == 2 ? -2.0 : 2.0, pp);
-        const double Cc = acos(r >= 4 && wok ? tmpc : 0.0);
-        double wt = 0.0, wp = 0.0, wq = 0.0;
-        if (r == 0) {
-            wt = mod2pi(-alpha + A1);
-            wp = pp;
-            wq = mod2pi(beta - A1);
-        } else if (r == 1) {
-            wt = mod2pi(alpha - A1);
-            wp = pp;
-            wq = mod2pi(-beta + A1);
-        } else if (r == 2) {
-            const double tm = A1 - A2;
-            wt = mod2pi(-alpha + tm);
-            wp = pp;
-            wq = mod2pi(-mod2pi(beta) + tm);
-        } else if (r == 3) {
-            const double tm = A1 - A2;
-            wt = mod2pi(alpha - tm);
-            wp = pp;
-            wq = mod2pi(beta - tm);
-        } else if (r == 4) {
-            wp = mod2pi(2.0 * kPi - Cc);
-            wt = mod2pi(alpha - A1 + mod2pi(wp / 2.0));
-            wq = mod2pi(alpha - beta - wt + mod2pi(wp));
-        } else if (r == 5) {
-            wp = mod2pi(2.0 * kPi - Cc);
-            wt = mod2pi(-alpha - A1 + wp / 2.0);
-            wq = mod2pi(mod2pi(beta) - alpha - wt + mod2pi(wp));
-        }
-        const double wcost = fabs(wt) + fabs(wp) + fabs(wq);
-        // first strict minimum in ALL_PLANNERS order (dubins.rs:351-360)
-        double bc = __builtin_inf();
-        int bw = -1;
-        const double wc[6] = {grp8_bcast_f64<0>(wcost), grp8_bcast_f64<1>(wcost),
-                              grp8_bcast_f64<2>(wcost), grp8_bcast_f64<3>(wcost),
-                              grp8_bcast_f64<4>(wcost), grp8_bcast_f64<5>(wcost)};
-        const int wk[6] = {grp8_bcast_i32<0>((int)wok), grp8_bcast_i32<1>((int)wok),
-                           grp8_bcast_i32<2>((int)wok), grp8_bcast_i32<3>((int)wok),
-                           grp8_bcast_i32<4>((int)wok), grp8_bcast_i32<5>((int)wok)};
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            if (wk[k] && bc > wc[k]) {
-                bc = wc[k];
-                bw = k;
-            }
-        }
-        const int src = g0 + (bw < 0 ? 0 : bw);
-        const double L0 = __shfl(wt, src), L1 = __shfl(wp, src), L2 = __shfl(wq, src);
-        const int m0 = word_mode(bw, 0), m1 = word_mode(bw, 1), m2 = word_mode(bw, 2);
-        int state = !act ? kReject : (bw < 0 ? kPrepNone : kPrepWalk);
-        double tot = 0.0;
-        tot += L0;
-        tot += L1;
-        tot += L2;
-        const double nq = trunc(tot / step);
-        if (state == kPrepWalk && (!(nq >= 0.0) || nq > 1.0e8)) state = kError;
-        // segment origin headings (interpolate's yaw, dubins.rs:191-196)
-        const double oy0 = 0.0;
-        const double oy1 = m0 == kModeL ? oy0 + L0 : (m0 == kModeR ? oy0 - L0 : oy0);
-        const double oy2 = m1 == kModeL ? oy1 + L1 : (m1 == kModeR ? oy1 - L1 : oy1);
-        // lanes 0..2: segment trig, 3..5: sin/cos of the lengths, 6: the world transform
-        double arg = 0.0;
-        if (r < 3) {
-            const int ms = r == 0 ? m0 : (r == 1 ? m1 : m2);
-            const double oys = r == 0 ? oy0 : (r == 1 ? oy1 : oy2);
-            arg = ms == kModeS ? oys : -oys;
-        } else if (r < 6) {
-            arg = r == 3 ? L0 : (r == 4 ? L1 : L2);
-        } else if (r == 6) {
-            arg = -yaw;
-        }
-        const double sv = sin(arg), cv = cos(arg);
-        const double ca0 = grp8_bcast_f64<0>(cv), ca1 = grp8_bcast_f64<1>(cv), ca2 = grp8_bcast_f64<2>(cv);
-        const double sa0 = grp8_bcast_f64<0>(sv), sa1 = grp8_bcast_f64<1>(sv), sa2 = grp8_bcast_f64<2>(sv);
-        const double sl0 = grp8_bcast_f64<3>(sv), sl1 = grp8_bcast_f64<4>(sv), sl2 = grp8_bcast_f64<5>(sv);
-        const double cl0 = grp8_bcast_f64<3>(cv), cl1 = grp8_bcast_f64<4>(cv), cl2 = grp8_bcast_f64<5>(cv);
-        const double cw = grp8_bcast_f64<6>(cv), sw = grp8_bcast_f64<6>(sv);
-        const Pt O1 = seg_end(m0, L0, c, 0.0, 0.0, ca0, sa0, sl0, cl0);
-        const Pt O2 = seg_end(m1, L1, c, O1.x, O1.y, ca1, sa1, sl1, cl1);
-        const Pt E = seg_end(m2, L2, c, O2.x, O2.y, ca2, sa2, sl2, cl2);
-        // the trim (dubins.rs:281-288) drops exactly the endpoint unless its local x is 0.0
-        if (state == kPrepWalk && E.x == 0.0) state = kLiteral;
-        int cnt0 = 0, cnt1 = 0, cnt2 = 0, fb_seg = 0;
-        double fb_pd = 0.0, fb_dd = 0.0;
-        // no grid points are stored: steer_walk generates them all, lane-parallel and bit-exact,
-        // from the walk's initial state (segment 0, pd = d - 0.0, dubins.rs:239-241), and runs
-        // the trailing-zero check itself
-        if (state == kPrepWalk) {
-            state = kPrepFallback;
-            fb_dd = (L0 > 0.0) ? step : -step;
-            fb_pd = fb_dd - 0.0;
-        }
-        // RRT* cull: an edge whose cost cannot beat the limit is settled without its walk
-        if (act && cull && !(cbase + bc < climit)) state = kReject;
-        if (t < total && r == 0) {  // idle batch tasks get a kReject record (act == false)
-            PrepRec o;
-            o.x = x;
-            o.y = y;
-            o.px = px;
-            o.py = py;
-            o.yaw = yaw;
-            o.pyaw = pyaw;
-            o.c = c;
-            o.cw = cw;
-            o.sw = sw;
-            o.ox[0] = 0.0;
-            o.oy[0] = 0.0;
-            o.ox[1] = O1.x;
-            o.oy[1] = O1.y;
-            o.ox[2] = O2.x;
-            o.oy[2] = O2.y;
-            o.ca[0] = ca0;
-            o.ca[1] = ca1;
-            o.ca[2] = ca2;
-            o.sa[0] = sa0;
-            o.sa[1] = sa1;
-            o.sa[2] = sa2;
-            o.L[0] = L0;
-            o.L[1] = L1;
-            o.L[2] = L2;
-            o.n_point = (long long)nq + 3 + 4;
-            o.fb_pd = fb_pd;
-            o.fb_dd = fb_dd;
-            o.fb_seg = fb_seg;
-            o.m[0] = m0;
-            o.m[1] = m1;
-            o.m[2] = m2;
-            o.cnt[0] = cnt0;
-            o.cnt[1] = cnt1;
-            o.cnt[2] = cnt2;
-            o.state = state;
-            rec[t] = o;
-            if (t < W || tasks)
-                snap_yaw[t] = yaw;
-            else
-                cand[t - W].yaw = yaw;
-            // the Dubins cost (dubins.rs:351-361; inf on None): the RRT* edge cost
-            if (cost_out) cost_out[t] = bc;
-        }
+        double* yaw_dst = nullptr;
+        if (t < total) yaw_dst = (t < W || tasks) ? snap_yaw + t : &cand[t - W].yaw;
+        prep_task(sc, r, g0, t, t < total, act, x, y, px, py, pyaw, own, cyaw, cull, cbase, climit,
+                  rec, yaw_dst, cost_out);
     }
 }
 
@@ -2742,15 +2754,21 @@ __device__ __forceinline__ void lit_release(int* locks, int slot) {
 }
 
 // returns the verdict | (polyline points walked << 4) | (their arc points << 34)
+// The edge's steer_prep runs on the wave's eight 8-lane groups (prep_task: the word choice across
+// a group's lanes, ~9 transcendental calls deep instead of ~32 on one lane), every group on the
+// same edge; group 0 writes the record to the wave's LDS slot lrec, which walk_rec then walks.
 template <bool kAllowNone>
 __device__ __attribute__((noinline)) long long cf_edge_check(const SceneDev& sc, CfPose a,
                                                              CfPose b, bool junction,
                                                              double* lit_scratch, int* lit_locks,
-                                                             double* gs) {
-    const SteerPrep r = steer_prep(sc, a.x, a.y, a.yaw, b.x, b.y, b.yaw);
-    if (!kAllowNone && r.state == kPrepNone) return kCfPanic;
+                                                             double* gs, PrepRec* lrec) {
+    const int lane = threadIdx.x & 63;
+    prep_task(sc, lane & 7, lane & ~7, 0, lane < 8, true, a.x, a.y, b.x, b.y, b.yaw, 1, a.yaw, 0,
+              0.0, 0.0, lrec, nullptr, nullptr);
+    __builtin_amdgcn_wave_barrier();
+    if (!kAllowNone && lrec->state == kPrepNone) return kCfPanic;
     int walked = 0, walked_arc = 0;
-    int st = walk_edge<false>(sc, r, gs, junction, walked, walked_arc);
+    int st = walk_rec<false>(sc, lrec, nullptr, gs, walked, walked_arc, junction);
     if (st == kLiteral) {  // (measure-zero) a scratch buffer from the pool, for this edge only
         const int slot = lit_acquire(lit_locks, (int)blockIdx.x);
         double* bx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
@@ -2854,11 +2872,13 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
     int* __restrict__ gpath, int* __restrict__ items) {
     __shared__ __attribute__((aligned(16))) double s_gs[kCfWaves][kGenSlots];  // walk_rec's LDS, one set per wave
     __shared__ int s_pos[kCfWaves][kCfLevels];  // the optimize chain's path positions per wave
+    __shared__ PrepRec s_rec[kCfWaves];          // the wave's edge record (cf_edge_check)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int* path = gpath + ((size_t)blockIdx.x * kCfWaves + wave) * kCfMaxDepth;  // this wave's
     double* gs = s_gs[wave];
     int* pos = s_pos[wave];
+    PrepRec* lrec = &s_rec[wave];
     long long t_nodes = 0, t_edges = 0, t_pts = 0, t_arc = 0;  // this wave's work (profiling)
     for (;;) {
         // nodes one at a time from a launch-wide counter (err[1], zeroed with err): a node's
@@ -2894,7 +2914,7 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
                 const int to = path[m];
                 const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
                 const CfPose a{ax, ay, atan2(bt.y - ay, bt.x - ax)};
-                const long long rv = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks, gs);
+                const long long rv = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks, gs, lrec);
                 const int st = (int)(rv & 15);
                 ++t_edges;
                 t_pts += (rv >> 4) & 0x3fffffff;
@@ -2970,7 +2990,7 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
                 int st = prev_st;
                 if (!dup) {
                     const long long rv = cf_edge_check<false>(sc, a, bp, e < E - 1, lit_scratch,
-                                                              lit_locks, gs);
+                                                              lit_locks, gs, lrec);
                     st = (int)(rv & 15);
                     ++t_edges;
                     t_pts += (rv >> 4) & 0x3fffffff;
