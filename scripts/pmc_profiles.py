@@ -1,4 +1,4 @@
-"""Summarise scripts/gpu_r02_pmc.sh (gpurun_out/<tag>/) into the committed counter profiles the
+"""Summarise scripts/gpu_pmc.sh (gpurun_out/<tag>/) into the committed counter profiles the
 bench reads for its rooflines:
 
   profiles/window_kernel_pmc.json          config 2 NN screen: VALU instructions per eval, HBM bytes
@@ -90,7 +90,7 @@ def write(name, d):
     print(name, json.dumps({k: v for k, v in d.items() if not k.startswith("counters")}))
 
 
-NOTE = ("rocprofv3 --pmc passes (scripts/gpu_r02_pmc.sh), the profiled pass's dispatches only; "
+NOTE = ("rocprofv3 --pmc passes (scripts/gpu_pmc.sh), the profiled pass's dispatches only; "
         "valu_insts_* = SQ_INSTS_VALU x 64 lanes per unit; valu_busy = SQ_ACTIVE_INST_VALU / "
         "SQ_WAVE_CYCLES (per wave), wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES; HBM bytes = "
         "FETCH_SIZE x 2 + WRITE_SIZE (MI355X_MICROARCH.md §HBM)")
