@@ -27,18 +27,32 @@ KERNEL_DECL = r"""
 __device__ unsigned long long* g_diag;
 extern "C" void ppdiag_setup(void* buf, unsigned cap) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &buf, sizeof buf);
-    (void)hipMemset(buf, 0, 64 * 8);
+    (void)hipMemset(buf, 0, 128 * 8);
 }
-extern "C" unsigned ppdiag_count() { return 64; }
+extern "C" unsigned ppdiag_count() { return 128; }
 """
 
 # per-wave sums in registers, one fire-and-forget atomicAdd each at the wave's exit:
 # [0] tasks [1] points [2] task cycles [3] rec-load cycles [4] generate+interpolate cycles
 # [5] chunk_rejects cycles [6] chunks [7] wave span cycles (first task start .. exit)
-# [8..31] per-task cycle histogram, bin = floor(log2(cycles)) - 8
+# [8..31] per-task cycle histogram, bin = floor(log2(cycles)) - 8; [32..63] chunks per task (31: more)
 PATCHES_K = [
     ("extern __shared__ __attribute__((aligned(16))) char pp_smem[];",
      "extern __shared__ __attribute__((aligned(16))) char pp_smem[];\n" + KERNEL_DECL),
+    ("""    const int ncx = cx1 - cx0 + 1, ncy = cy1 - cy0 + 1;
+    if (ncx <= 0 || ncy <= 0) return false;""",
+     """    const int ncx = cx1 - cx0 + 1, ncy = cy1 - cy0 + 1;
+    if (g_diag && lane == 0) {
+        const int nc = (ncx > 0 && ncy > 0) ? ncx * ncy : 0;
+        atomicAdd(g_diag + 64 + (nc < 31 ? nc : 31), 1ull);
+    }
+    if (ncx <= 0 || ncy <= 0) return false;"""),
+    ("""            if (items_reject(kk >= 0, kk)) return true;
+            if (mb + 64 >= run) break;""",
+     """            if (g_diag && lane == 0 && mb == 0) atomicAdd(g_diag + 96 + (run < 31 ? run : 31), 1ull);
+            if (items_reject(kk >= 0, kk)) return true;
+            if (mb + 64 >= run) break;"""),
+
     ("""                                        int& npts, int& napts, bool junction = true) {
     const int lane = threadIdx.x & 63;
     const int state = p->state;
@@ -91,8 +105,9 @@ PATCHES_K = [
     if (threadIdx.x == 0) s_next = 0;
     __syncthreads();
     long long dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int dh[24];
+    int dh[24], dcn[32];
     for (int i = 0; i < 24; ++i) dh[i] = 0;
+    for (int i = 0; i < 32; ++i) dcn[i] = 0;
     long long dfirst = -1;
     for (;;) {
         int k = 0;
@@ -117,6 +132,8 @@ PATCHES_K = [
             int b = 63 - __builtin_clzll((unsigned long long)(dc | 1)) - 8;
             b = b < 0 ? 0 : (b > 23 ? 23 : b);
             for (int i = 0; i < 24; ++i) dh[i] += (i == b);
+            const int ch = (int)(dg[3] < 31 ? dg[3] : 31);
+            for (int i = 0; i < 32; ++i) dcn[i] += (i == ch);
         }"""),
     ("""    if (wg_points) {  // [b]: points, [kWalkTallySlots + b]: their arc points""",
      """    if (g_diag && lane == 0 && dsum[0] > 0) {
@@ -124,6 +141,8 @@ PATCHES_K = [
         for (int i = 0; i < 8; ++i) atomicAdd(g_diag + i, (unsigned long long)dsum[i]);
         for (int i = 0; i < 24; ++i)
             if (dh[i]) atomicAdd(g_diag + 8 + i, (unsigned long long)dh[i]);
+        for (int i = 0; i < 32; ++i)
+            if (dcn[i]) atomicAdd(g_diag + 32 + i, (unsigned long long)dcn[i]);
     }
     if (wg_points) {  // [b]: points, [kWalkTallySlots + b]: their arc points"""),
 ]
@@ -134,22 +153,22 @@ extern "C" void ppdiag_setup(void* buf, unsigned cap);
 static void* g_diag_buf = nullptr;
 static void diag_begin() {
     if (!getenv("PP_DIAG_OUT")) return;
-    if (!g_diag_buf) (void)hipMalloc(&g_diag_buf, 64 * 8);
-    ppdiag_setup(g_diag_buf, 64);
+    if (!g_diag_buf) (void)hipMalloc(&g_diag_buf, 128 * 8);
+    ppdiag_setup(g_diag_buf, 128);
     (void)hipDeviceSynchronize();
 }
 static void diag_end(const char* what) {
     const char* path = getenv("PP_DIAG_OUT");
     if (!path || !g_diag_buf) return;
     (void)hipDeviceSynchronize();
-    unsigned long long h[64];
+    unsigned long long h[128];
     (void)hipMemcpy(h, g_diag_buf, sizeof h, hipMemcpyDeviceToHost);
     FILE* f = fopen(path, "ab");
     if (!f) return;
     char tag[16] = {};
     strncpy(tag, what, 15);
     fwrite(tag, 1, 16, f);
-    fwrite(h, 8, 64, f);
+    fwrite(h, 8, 128, f);
     fclose(f);
 }
 extern "C" int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted) {
@@ -204,7 +223,7 @@ def load(path):
             tag = f.read(16)
             if len(tag) < 16:
                 break
-            a = np.frombuffer(f.read(64 * 8), dtype=np.uint64).astype(np.float64)
+            a = np.frombuffer(f.read(128 * 8), dtype=np.uint64).astype(np.float64)
             calls.append((tag.rstrip(b"\0").decode(), a))
     return calls
 
@@ -224,6 +243,12 @@ def report(path):
         h = a[8:32]
         tot = h.sum()
         print("  task cycles histogram: " + "  ".join(f"2^{i + 8}:{h[i] / tot * 100:.1f}%" for i in range(24) if h[i] > 0))
+        c = a[32:64]
+        print("  chunks per task: " + "  ".join(f"{i}:{int(c[i])}" for i in range(32) if c[i] > 0))
+        c = a[64:96]
+        print("  cells per chunk (all chunk_rejects calls): " + "  ".join(f"{i}:{int(c[i])}" for i in range(32) if c[i] > 0))
+        c = a[96:128]
+        print("  items listed per chunk (<= 64 cells): " + "  ".join(f"{i}:{int(c[i])}" for i in range(32) if c[i] > 0))
 
 
 if __name__ == "__main__":
