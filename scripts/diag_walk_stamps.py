@@ -33,8 +33,9 @@ extern "C" unsigned ppdiag_count() { return 128; }
 """
 
 # per-wave sums in registers, one fire-and-forget atomicAdd each at the wave's exit:
-# [0] tasks [1] points [2] task cycles [3] rec-load cycles [4] generate+interpolate cycles
-# [5] chunk_rejects cycles [6] chunks [7] wave span cycles (first task start .. exit)
+# [0] tasks [1] points [2] task cycles [3] rec-load cycles [4] interpolate cycles
+# [5] chunk_rejects items cycles [6] chunks [7] wave span cycles (first task start .. exit)
+# [30] generate cycles [31] chunk_rejects setup cycles (bounds, bbox, cells)
 # [8..31] per-task cycle histogram, bin = floor(log2(cycles)) - 8; [32..63] chunks per task (31: more)
 PATCHES_K = [
     ("extern __shared__ __attribute__((aligned(16))) char pp_smem[];",
@@ -53,6 +54,25 @@ PATCHES_K = [
             if (items_reject(kk >= 0, kk)) return true;
             if (mb + 64 >= run) break;"""),
 
+    ("""__device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool check_bounds,
+                                              bool seg_valid, double qx, double qy) {""",
+     """__device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool check_bounds,
+                                              bool seg_valid, double qx, double qy,
+                                              long long* dgc = nullptr) {"""),
+    ("""    auto items_reject = [&](bool valid, int kk) -> bool {""",
+     """    if (dgc) {
+        __builtin_amdgcn_s_waitcnt(0);
+        dgc[0] = __builtin_amdgcn_s_memtime();
+    }
+    auto items_reject = [&](bool valid, int kk) -> bool {"""),
+    ("""        const bool junction_here = done && cnt < 63;""",
+     """        if (dg) {
+            __builtin_amdgcn_s_waitcnt(0);
+            const long long t = __builtin_amdgcn_s_memtime();
+            dg[4] += t - dt0;
+            dt0 = t;
+        }
+        const bool junction_here = done && cnt < 63;"""),
     ("""                                        int& npts, int& napts, bool junction = true) {
     const int lane = threadIdx.x & 63;
     const int state = p->state;
@@ -82,10 +102,17 @@ PATCHES_K = [
         const bool chk = isgrid || isj || (base == 0 && lane == 0);"""),
     ("""        if (chunk_rejects<kLds, kScene>(sc, has, chk, has && lane >= 1, qx, qy)) return kReject;
         if (junction_here) break;""",
-     """        const bool rj = chunk_rejects<kLds, kScene>(sc, has, chk, has && lane >= 1, qx, qy);
+     """        long long dgc[1] = {0};
+        const bool rj = chunk_rejects<kLds, kScene>(sc, has, chk, has && lane >= 1, qx, qy,
+                                                    dg ? dgc : nullptr);
         if (dg) {
             const long long t = __builtin_amdgcn_s_memtime();
-            dg[2] += t - dt0;
+            if (dgc[0] > 0) {  // (0: returned before the items: bounds, or no cell)
+                dg[5] += dgc[0] - dt0;
+                dg[2] += t - dgc[0];
+            } else {
+                dg[5] += t - dt0;
+            }
             dt0 = t;
         }
         if (rj) return kReject;
@@ -104,7 +131,7 @@ PATCHES_K = [
     const int G = (int)gridDim.x;
     if (threadIdx.x == 0) s_next = 0;
     __syncthreads();
-    long long dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long dsum[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     int dh[24], dcn[32];
     for (int i = 0; i < 24; ++i) dh[i] = 0;
     for (int i = 0; i < 32; ++i) dcn[i] = 0;
@@ -117,7 +144,7 @@ PATCHES_K = [
         const long long dc0 = __builtin_amdgcn_s_memtime();
         if (dfirst < 0) dfirst = dc0;
         const int dp0 = npts;
-        long long dg[4] = {0, 0, 0, 0};
+        long long dg[6] = {0, 0, 0, 0, 0, 0};
         const int s = walk_rec<kLds, kScene>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts, napts,
                                              true, g_diag ? dg : nullptr);
         {
@@ -129,9 +156,11 @@ PATCHES_K = [
             dsum[4] += dg[1];
             dsum[5] += dg[2];
             dsum[6] += dg[3];
+            dsum[8] += dg[4];
+            dsum[9] += dg[5];
             int b = 63 - __builtin_clzll((unsigned long long)(dc | 1)) - 8;
-            b = b < 0 ? 0 : (b > 23 ? 23 : b);
-            for (int i = 0; i < 24; ++i) dh[i] += (i == b);
+            b = b < 0 ? 0 : (b > 21 ? 21 : b);
+            for (int i = 0; i < 22; ++i) dh[i] += (i == b);
             const int ch = (int)(dg[3] < 31 ? dg[3] : 31);
             for (int i = 0; i < 32; ++i) dcn[i] += (i == ch);
         }"""),
@@ -139,7 +168,9 @@ PATCHES_K = [
      """    if (g_diag && lane == 0 && dsum[0] > 0) {
         dsum[7] = __builtin_amdgcn_s_memtime() - dfirst;
         for (int i = 0; i < 8; ++i) atomicAdd(g_diag + i, (unsigned long long)dsum[i]);
-        for (int i = 0; i < 24; ++i)
+        atomicAdd(g_diag + 30, (unsigned long long)dsum[8]);
+        atomicAdd(g_diag + 31, (unsigned long long)dsum[9]);
+        for (int i = 0; i < 22; ++i)
             if (dh[i]) atomicAdd(g_diag + 8 + i, (unsigned long long)dh[i]);
         for (int i = 0; i < 32; ++i)
             if (dcn[i]) atomicAdd(g_diag + 32 + i, (unsigned long long)dcn[i]);
@@ -236,13 +267,17 @@ def report(path):
         cyc = a[2]
         print(f"call {ci} {tag}: tasks {n:.0f}  points/task {a[1] / n:.1f}  chunks/task {a[6] / n:.2f}  "
               f"cycles/task {cyc / n:.0f}  cycles/chunk {cyc / max(a[6], 1):.0f}")
-        print(f"  share of task cycles: rec load {a[3] / cyc:.3f}  generate+interpolate {a[4] / cyc:.3f}  "
-              f"chunk_rejects {a[5] / cyc:.3f}  other {(cyc - a[3] - a[4] - a[5]) / cyc:.3f}")
-        print(f"  per chunk: gen+interp {a[4] / max(a[6], 1):.0f} cycles, chunk_rejects {a[5] / max(a[6], 1):.0f} cycles; "
-              f"per task rec load {a[3] / n:.0f} cycles; wave busy share {cyc / max(a[7], 1):.3f}")
-        h = a[8:32]
+        rest = cyc - a[3] - a[30] - a[4] - a[31] - a[5]
+        print(f"  share of task cycles: rec load {a[3] / cyc:.3f}  generate {a[30] / cyc:.3f}  "
+              f"interpolate {a[4] / cyc:.3f}  rejects setup (bounds, bbox, cells) {a[31] / cyc:.3f}  "
+              f"items {a[5] / cyc:.3f}  other {rest / cyc:.3f}")
+        print(f"  per task rec load {a[3] / n:.0f} cycles; wave busy share {cyc / max(a[7], 1):.3f}")
+        h = a[8:30]
         tot = h.sum()
-        print("  task cycles histogram: " + "  ".join(f"2^{i + 8}:{h[i] / tot * 100:.1f}%" for i in range(24) if h[i] > 0))
+        print("  task cycles histogram: " + "  ".join(f"2^{i + 8}:{h[i] / tot * 100:.1f}%" for i in range(22) if h[i] > 0))
+        ch = max(a[6], 1)
+        print(f"  per chunk cycles: generate {a[30] / ch:.0f}, interpolate {a[4] / ch:.0f}, "
+              f"rejects setup (bounds, bbox, cells) {a[31] / ch:.0f}, items {a[5] / ch:.0f}")
         c = a[32:64]
         print("  chunks per task: " + "  ".join(f"{i}:{int(c[i])}" for i in range(32) if c[i] > 0))
         c = a[64:96]
