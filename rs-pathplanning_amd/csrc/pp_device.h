@@ -18,8 +18,14 @@ constexpr double kPi = 3.14159265358979323846;  // std::f64::consts::PI
 constexpr double kTwoPi = 2.0 * kPi;
 
 // dubins.rs:14-20
+// theta / 2pi as the correctly rounded FMA quotient (q = RN(theta r), r = RN(1 / 2pi), then
+// RN(q + fma(-q, 2pi, theta) r): Markstein's theorem, bit-identical to the IEEE division;
+// tests/test_div_identity.py checks it for 2pi), 3 FP64 ops instead of the division sequence
+constexpr double kInvTwoPi = 1.0 / kTwoPi;
 __host__ __device__ inline double mod2pi(double theta) {
-    return theta - kTwoPi * floor(theta / kTwoPi);
+    const double q = theta * kInvTwoPi;
+    const double quo = fma(fma(-q, kTwoPi, theta), kInvTwoPi, q);
+    return theta - kTwoPi * floor(quo);
 }
 // dubins.rs:22-24 (Rust `%` == fmod: truncated, negative angles are not wrapped)
 __host__ __device__ inline double pi_2_pi(double angle) {

@@ -1,5 +1,5 @@
-"""CPU: the walk's division by the curvature (walk_rec, csrc/pp_kernels.hip div_by) is bit-identical
-to IEEE division.  interpolate (dubins.rs:169-178) divides every point's length, sin and 1 - cos by
+"""CPU: the walk's division by the curvature (walk_rec, csrc/pp_kernels.hip div_by) and mod2pi's
+division by 2pi (csrc/pp_device.h) are bit-identical to IEEE division.  interpolate (dubins.rs:169-178) divides every point's length, sin and 1 - cos by
 max_curvature c; the walk computes x / c as q = RN(x rc), then RN(q + fma(-q, c, x) rc) with
 rc = RN(1 / c) — Markstein's correctly rounded quotient.  Checked here in C (gcc, FMA as the
 device's v_fma_f64) for the curvatures of every scene the tests and the bench use, over the value
@@ -19,7 +19,9 @@ static double u01(void) { return (double)(xr() >> 11) / 9007199254740992.0; }
 int main(int argc, char** argv) {
     long long n = atoll(argv[1]), bad = 0;
     for (int a = 2; a < argc; ++a) {
-        const double c = 1.0 / atof(argv[a]);  /* the walk's c: 1 / turn_radius */
+        /* the walk's c = 1 / turn_radius; "2pi": mod2pi's divisor (pp_device.h) */
+        const double c = argv[a][0] == '2' && argv[a][1] == 'p' ? 2.0 * 3.141592653589793
+                                                               : 1.0 / atof(argv[a]);
         const double rc = 1.0 / c;
         for (long long k = 0; k < n; ++k) {
             double x;
@@ -55,6 +57,7 @@ def test_division_by_curvature_is_exact(tmp_path):
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(c), "-lm"], check=True)
     # turn radii of scenes.py (bench6 0.8, the fields 4.0, transit 0.8 / 3.0 in the example) and a
     # spread of others
-    radii = ["0.8", "4.0", "3.0", "1.8", "1.0", "2.5", "0.3", "7.0", "0.1", "0.3333333333333333"]
+    radii = ["0.8", "4.0", "3.0", "1.8", "1.0", "2.5", "0.3", "7.0", "0.1", "0.3333333333333333",
+             "2pi"]
     r = subprocess.run([str(exe), "2000000"] + radii, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
