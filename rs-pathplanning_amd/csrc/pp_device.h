@@ -22,6 +22,11 @@ constexpr double kTwoPi = 2.0 * kPi;
 // RN(q + fma(-q, 2pi, theta) r): Markstein's theorem, bit-identical to the IEEE division;
 // tests/test_div_identity.py checks it for 2pi), 3 FP64 ops instead of the division sequence
 constexpr double kInvTwoPi = 1.0 / kTwoPi;
+// x / c given rc = RN(1 / c): the same correctly rounded quotient
+__host__ __device__ inline double div_by(double x, double c, double rc) {
+    const double q = x * rc;
+    return fma(fma(-q, c, x), rc, q);
+}
 __host__ __device__ inline double mod2pi(double theta) {
     const double q = theta * kInvTwoPi;
     const double quo = fma(fma(-q, kTwoPi, theta), kInvTwoPi, q);

@@ -1524,15 +1524,18 @@ __device__ inline void window_task(int t, int W, const double* wsx, const double
 struct Pt {
     double x, y;
 };
-__device__ inline Pt seg_end(int mode, double len, double c, double ox, double oy, double ca,
-                             double sa, double sl, double cl) {
+// (x / c as div_by: the correctly rounded FMA quotient, bit-identical to the division)
+__device__ inline Pt seg_end(int mode, double len, double c, double rc, double ox, double oy,
+                             double ca, double sa, double sl, double cl) {
     Pt r;
     if (mode == kModeS) {
-        r.x = ox + len / c * ca;
-        r.y = oy + len / c * sa;
+        const double lc = div_by(len, c, rc);
+        r.x = ox + lc * ca;
+        r.y = oy + lc * sa;
     } else {
-        const double ldx = sl / c;
-        const double ldy = mode == kModeL ? (1.0 - cl) / c : (1.0 - cl) / -c;
+        const double ldx = div_by(sl, c, rc);
+        const double l1 = div_by(1.0 - cl, c, rc);  // (1 - cos) / -c = -((1 - cos) / c)
+        const double ldy = mode == kModeL ? l1 : -l1;
         const double gdx = ca * ldx + sa * ldy;
         const double gdy = -sa * ldx + ca * ldy;
         r.x = ox + gdx;
@@ -1681,9 +1684,10 @@ __device__ __forceinline__ void prep_task(const SceneDev& sc, int r, int g0, int
     const double sl0 = grp8_bcast_f64<3>(sv), sl1 = grp8_bcast_f64<4>(sv), sl2 = grp8_bcast_f64<5>(sv);
     const double cl0 = grp8_bcast_f64<3>(cv), cl1 = grp8_bcast_f64<4>(cv), cl2 = grp8_bcast_f64<5>(cv);
     const double cw = grp8_bcast_f64<6>(cv), sw = grp8_bcast_f64<6>(sv);
-    const Pt O1 = seg_end(m0, L0, c, 0.0, 0.0, ca0, sa0, sl0, cl0);
-    const Pt O2 = seg_end(m1, L1, c, O1.x, O1.y, ca1, sa1, sl1, cl1);
-    const Pt E = seg_end(m2, L2, c, O2.x, O2.y, ca2, sa2, sl2, cl2);
+    const double rc = 1.0 / c;
+    const Pt O1 = seg_end(m0, L0, c, rc, 0.0, 0.0, ca0, sa0, sl0, cl0);
+    const Pt O2 = seg_end(m1, L1, c, rc, O1.x, O1.y, ca1, sa1, sl1, cl1);
+    const Pt E = seg_end(m2, L2, c, rc, O2.x, O2.y, ca2, sa2, sl2, cl2);
     // the trim (dubins.rs:281-288) drops exactly the endpoint unless its local x is 0.0
     if (state == kPrepWalk && E.x == 0.0) state = kLiteral;
     int cnt0 = 0, cnt1 = 0, cnt2 = 0, fb_seg = 0;
@@ -1819,10 +1823,6 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
 // tests/test_div_identity.py checks the identity for the scenes' curvatures.  3 VALU instead of 9.
 constexpr int kGenPts = 68;  // generator slots: 63 points + 4 overshoot + 1
 constexpr int kSegRow = 6;   // segment-table row (16-byte aligned rows: ds_read_b128)
-__device__ __forceinline__ double div_by(double x, double c, double rc) {
-    const double q = x * rc;
-    return __builtin_fma(__builtin_fma(-q, c, x), rc, q);
-}
 template <bool kLds, int kScene = kSceneAny>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
                                         const double* __restrict__ pdv, double* __restrict__ gs,
