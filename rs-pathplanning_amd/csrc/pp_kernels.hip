@@ -2979,10 +2979,17 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
             const int node = path[ps - (j - s - 1)];
             return CfPose{tr.x[node], tr.y[node], tr.yaw[node]};
         };
+        // Only the goal edge and the s copy edges are steered: edges s + 1 .. E - 1 are tree edges
+        // (node -> parent, both with their stored poses) whose polyline with its junction chord
+        // passed verify when the node was inserted (verify_node, rrt.rs:414-426: the incremental
+        // form, §2), and the edge into the root is checked without its chord, a subset.  Both
+        // Contains and Intersects decompose over the concatenation, so those edges cannot change
+        // the verdict (tests: every check_finish verdict equals the oracle's full-line verify).
+        const int Ev = 1 + s;
         if (vok) {
             CfPose prev{0.0, 0.0, 0.0}, a = pose(0);
             int prev_st = kAccept;
-            for (int e = 0; e < E; ++e) {
+            for (int e = 0; e < Ev; ++e) {
                 const CfPose bp = pose(e + 1);
                 // an edge identical to the previous one (consecutive root copies: both poses
                 // equal bit for bit, both with the junction) has that edge's verdict
