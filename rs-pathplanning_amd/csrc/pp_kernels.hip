@@ -2757,8 +2757,10 @@ __device__ __forceinline__ void lit_release(int* locks, int slot) {
 // The edge's steer_prep runs on the wave's eight 8-lane groups (prep_task: the word choice across
 // a group's lanes, ~9 transcendental calls deep instead of ~32 on one lane), every group on the
 // same edge; group 0 writes the record to the wave's LDS slot lrec, which walk_rec then walks.
+// Inlined at its two call sites: as a call, its frame spilled 512 B per lane around every edge
+// (the config-3 batch plan's check_finish 103 -> 80 ms inlined, 96 B of scratch left).
 template <bool kAllowNone>
-__device__ __attribute__((noinline)) long long cf_edge_check(const SceneDev& sc, CfPose a,
+__device__ __forceinline__ long long cf_edge_check(const SceneDev& sc, CfPose a,
                                                              CfPose b, bool junction,
                                                              double* lit_scratch, int* lit_locks,
                                                              double* gs, PrepRec* lrec) {
