@@ -165,6 +165,7 @@ struct pp_ctx {
     HBuf<SteerTask> h_tasks;
     // check_finish
     DBuf<int> cf_nodes, cf_ok, cf_npts, cf_chain, cf_etab, cf_err, cf_path, cf_items;
+    DBuf<int> cf_memo;  // check_finish_kernel's optimize memo (CfBatch::ftab / gtab), per launch
     DBuf<double> cf_len, cf_pts;
     // ---- multi-query batch (config 3)
     bool has_batch = false;
@@ -488,9 +489,17 @@ struct CfOut {
 // check_finish_kernel over nodes[0, k) (device) with its error handling; the one-tree planner
 // (cb.qidx null: the context's tree, goal g) or a query batch (cb)
 int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line, int grid,
-           const CfGoal& gg, const CfOut& o, const CfBatch& cb) {
+           const CfGoal& gg, const CfOut& o, const CfBatch& cb_in) {
     const CfGoal* g = &gg;
     PP_HIP(c->cf_err.reserve(2));  // [0] error bits, [1] the kernel's node counter
+    // optimize's memo: two ints per tree row (the batch's Q * row_cap rows, or the tree's nodes),
+    // zeroed for this launch
+    CfBatch cb = cb_in;
+    const size_t rows = cb.qidx ? (size_t)c->mq_Q * (size_t)cb.row_cap : (size_t)c->n;
+    PP_HIP(c->cf_memo.reserve(2 * std::max<size_t>(rows, 1)));
+    PP_HIP(hipMemsetAsync(c->cf_memo.p, 0, 2 * rows * sizeof(int), c->stream));
+    cb.ftab = c->cf_memo.p;
+    cb.gtab = c->cf_memo.p + rows;
     // the line buffers (one per workgroup of the launch) only when lines are materialised
     const int wgs = std::min(grid, k);
     if (want_line) {

@@ -86,6 +86,12 @@ struct CfBatch {
     int row_cap = 0;            // SoA rows per query
     const double* goals = nullptr;   // [3Q] goal x, y, yaw
     const uint8_t* blocked = nullptr;  // [Q] polygon mode: the root fails verify (may be null)
+    // optimize's memo (rows as the tree's SoA: query q at q * row_cap; zeroed per launch, may be
+    // null): ftab[v] = 0 unknown, 1 no candidate of v verifies, 2 + m (| 1 << 30 when that edge's
+    // steer is None) — v's first verifying candidate root first is its depth-m ancestor; gtab[v] =
+    // 0 unknown, else 1 + the verdict of finalize's copy edge from v (see check_finish_kernel)
+    int* ftab = nullptr;
+    int* gtab = nullptr;
 };
 hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev& tr,
                                const int* nodes, int k, double gx, double gy, double gyaw,

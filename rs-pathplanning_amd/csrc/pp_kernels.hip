@@ -434,67 +434,47 @@ __device__ int steer_collide_fast(const SceneDev& sc, double x, double y, double
     return steer_walk<kLds>(sc, walk_in(r), junction);
 }
 
-// Literal path (measure-zero trim cases): lane 0 runs dubins_literal into its scratch buffer and
-// verifies the polyline alone.  Slow, exact, essentially never taken.
+// Literal path (the trim cases the fast walk cannot reproduce: an endpoint local x of 0.0, a
+// buffer with no trailing zero): lane 0 runs dubins_literal into its scratch buffer, then the
+// whole wave verifies the polyline with the walk's chunk test — chunks of 63 segments, lane 0 the
+// previous chunk's last point (bounds-checked in the first chunk only), lanes 1..63 the next
+// points — instead of one lane looping over every point and obstacle.  Rare in the extend, but
+// check_finish meets it on optimize's self-connections (a node's copy into the node itself): the
+// serial test held a scratch slot of the shared pool for a whole scene scan, and hundreds of waves
+// queued for the slots.
 __device__ int steer_collide_literal(const SceneDev& sc, double x, double y, double yaw, double px,
                                      double py, double pyaw, double* bx, double* by, double* byaw,
                                      bool junction = true) {
     const int lane = threadIdx.x & 63;
-    int st = kReject;
+    int n = 0, r = 0;
     if (lane == 0) {
-        int n = 0, word = -1;
+        int word = -1;
         double cost = 0.0;
-        const int r = dubins_literal(x, y, yaw, px, py, pyaw, sc.turn_radius, sc.step_size, bx,
-                                     by, byaw, kLiteralCap - 1, &n, &word, &cost);
-        if (r == kSteerOverflow) {
-            st = kError;
-        } else {
+        r = dubins_literal(x, y, yaw, px, py, pyaw, sc.turn_radius, sc.step_size, bx, by, byaw,
+                           kLiteralCap - 1, &n, &word, &cost);
+        if (r != kSteerOverflow) {
             if (r == kSteerNone) {
                 bx[0] = x;
                 by[0] = y;
                 n = 1;
             }
-            bool ok = true;
             bx[n] = px;
             by[n] = py;
-            const int np = junction ? n + 1 : n;  // the junction point is bounds-checked too
-            for (int i = 0; i < np && ok; ++i) ok = point_in_bounds(sc, bx[i], by[i]);
-            if (sc.bits) {  // config 4: point probes only
-                for (int i = 0; i < np && ok; ++i)
-                    ok = !grid_occupied(sc.bits, sc.bw, sc.bh, sc.bwords, sc.bx0, sc.by0, sc.binv,
-                                        bx[i], by[i]);
-            } else {
-                double x0 = bx[0], x1 = bx[0], y0 = by[0], y1 = by[0];
-                for (int i = 1; i < np; ++i) {
-                    x0 = fmin(x0, bx[i]);
-                    x1 = fmax(x1, bx[i]);
-                    y0 = fmin(y0, by[i]);
-                    y1 = fmax(y1, by[i]);
-                }
-                for (int k = 0; k < sc.ne && ok; ++k) {  // polygon edges (Q10p)
-                    const double e0x = sc.ex0[k], e0y = sc.ey0[k], e1x = sc.ex1[k], e1y = sc.ey1[k];
-                    const double rc = sqrt(sc.h2) * (1.0 + 1e-9) + 1e-9;
-                    if (!((fmax(e0x, e1x) + rc >= x0) && (fmin(e0x, e1x) - rc <= x1) &&
-                          (fmax(e0y, e1y) + rc >= y0) && (fmin(e0y, e1y) - rc <= y1)))
-                        continue;
-                    for (int i = 0; i + 1 < np && ok; ++i)
-                        if (seg_hits_edge(bx[i], by[i], bx[i + 1], by[i + 1], e0x, e0y, e1x, e1y,
-                                          sc.h2))
-                            ok = false;
-                }
-                for (int k = 0; k < sc.m && ok; ++k) {
-                    const double cx = sc.cx[k], cy = sc.cy[k], rc = sc.rcull[k];
-                    if (!((cx + rc >= x0) && (cx - rc <= x1) && (cy + rc >= y0) && (cy - rc <= y1)))
-                        continue;
-                    for (int i = 0; i + 1 < np && ok; ++i)
-                        if (seg_hits_disc(bx[i], by[i], bx[i + 1], by[i + 1], cx, cy, sc.r2[k]))
-                            ok = false;
-                }
-            }
-            st = ok ? kAccept : kReject;
         }
     }
-    return __shfl(st, 0);
+    r = __shfl(r, 0);
+    n = __shfl(n, 0);
+    if (r == kSteerOverflow) return kError;
+    __threadfence_block();  // lane 0's points before the wave reads them
+    const int np = junction ? n + 1 : n;  // the junction point is bounds-checked too
+    for (int base = 0; base == 0 || base + 1 < np; base += 63) {
+        const int i = base + lane;
+        const bool has = i < np;
+        const double qx = has ? bx[i] : x, qy = has ? by[i] : y;
+        if (chunk_rejects<false>(sc, has, has && (lane >= 1 || base == 0), has && lane >= 1, qx, qy))
+            return kReject;
+    }
+    return kAccept;
 }
 
 // Explicit tasks (the verify_node API); waves <= kLiteralWaves so each wave owns one literal
@@ -2818,8 +2798,11 @@ __device__ inline void cf_node_setup(const TreeDev& tr_in, const CfBatch& cb, in
                                      double gx_in, double gy_in, double gyaw_in,
                                      double gyaw_opt_in, int root_blocked_in, TreeDev& tr,
                                      double& gx, double& gy, double& gyaw, double& gyaw_opt,
-                                     int& root_blocked) {
+                                     int& root_blocked, int** ftab = nullptr,
+                                     int** gtab = nullptr) {
     tr = tr_in;
+    if (ftab) *ftab = cb.ftab;
+    if (gtab) *gtab = cb.gtab;
     gx = gx_in;
     gy = gy_in;
     gyaw = gyaw_in;
@@ -2836,6 +2819,8 @@ __device__ inline void cf_node_setup(const TreeDev& tr_in, const CfBatch& cb, in
         gy = cb.goals[3 * q + 1];
         gyaw = gyaw_opt = cb.goals[3 * q + 2];
         root_blocked = cb.blocked ? cb.blocked[q] : 0;
+        if (ftab && *ftab) *ftab += o;
+        if (gtab && *gtab) *gtab += o;
     }
 }
 
@@ -2893,8 +2878,9 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
         TreeDev tr;
         double gx, gy, gyaw, gyaw_opt;
         int root_blocked;
+        int *ftab = nullptr, *gtab = nullptr;
         cf_node_setup(tr_in, cb, b, gx_in, gy_in, gyaw_in, gyaw_opt_in, sc.root_blocked, tr, gx,
-                      gy, gyaw, gyaw_opt, root_blocked);
+                      gy, gyaw, gyaw_opt, root_blocked, &ftab, &gtab);
         const int D = cf_path(tr, nodes[b], path);
         if (D < 0) {
             if (lane == 0) {
@@ -2905,25 +2891,41 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
         }
         // optimize (rrt.rs:463-487), level by level: candidates path[0..L] root first, the first
         // accepted one wins (kError before it: the reference's panic); RECURSION_LIMIT levels
+        // The first verifying candidate of a tree node c (root first over c's ancestors and c)
+        // depends on c alone — its ancestors' poses — not on the item whose chain reaches it, and
+        // every item of a plan climbs through its ancestors' own levels: ftab memoises it
+        // (cb.ftab; the value is the candidate's depth, which is its position in every path through
+        // c).  Concurrent waves computing the same entry store the same value.
         int bad = 0;
         int L = D - 1, s_lv = 0;
+        int fnone = 0;  // the last accepted candidate edge's steer was None (finalize panics)
         for (int level = 0; level < kCfLevels - level0; ++level) {
             const int Lstart = L;
             const int c = path[L];
-            const double ax = tr.x[c], ay = tr.y[c];
+            const int fm = ftab ? __builtin_amdgcn_readfirstlane(ftab[c]) : 0;
             int found = -1;
-            for (int m = 0; m <= L && !root_blocked; ++m) {
-                const int to = path[m];
-                const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
-                const CfPose a{ax, ay, atan2(bt.y - ay, bt.x - ax)};
-                const long long rv = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks, gs, lrec);
-                const int st = (int)(rv & 15);
-                ++t_edges;
-                t_pts += (rv >> 4) & 0x3fffffff;
-                t_arc += rv >> 34;
-                if (st == kReject) continue;
-                found = st == kAccept ? m : -2;
-                break;
+            if (fm >= 2) {
+                found = fm & 0x3fffffff;
+                found -= 2;
+                fnone = fm >> 30;
+            } else if (fm == 0) {
+                const double ax = tr.x[c], ay = tr.y[c];
+                for (int m = 0; m <= L && !root_blocked; ++m) {
+                    const int to = path[m];
+                    const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
+                    const CfPose a{ax, ay, atan2(bt.y - ay, bt.x - ax)};
+                    const long long rv = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks, gs, lrec);
+                    const int st = (int)(rv & 15);
+                    ++t_edges;
+                    t_pts += (rv >> 4) & 0x3fffffff;
+                    t_arc += rv >> 34;
+                    if (st == kReject) continue;
+                    found = st == kAccept ? m : -2;
+                    fnone = lrec->state == kPrepNone ? 1 : 0;
+                    break;
+                }
+                if (ftab && lane == 0 && found != -2)
+                    ftab[c] = found >= 0 ? (2 + found) | (fnone << 30) : 1;
             }
             if (found == -2) {
                 bad = 4;
@@ -2987,6 +2989,12 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
         // form, §2), and the edge into the root is checked without its chord, a subset.  Both
         // Contains and Intersects decompose over the concatenation, so those edges cannot change
         // the verdict (tests: every check_finish verdict equals the oracle's full-line verify).
+        // Edge s (the last copy into the tree node optimize's last level accepted) is that
+        // level's candidate edge: it verified with its junction chord (without the chord, into
+        // the root, a subset), so only its None steer matters (finalize's panic; fnone).  Copy
+        // edge e in 1..s-1 runs from the copy at chain node v = path[pos[e - 2]] (the item's node
+        // for e = 1) toward F(v) to the copy at F(v) toward F(F(v)): a function of v alone, so
+        // gtab memoises its verdict like ftab.
         const int Ev = 1 + s;
         if (vok) {
             CfPose prev{0.0, 0.0, 0.0}, a = pose(0);
@@ -2996,14 +3004,21 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
                 // an edge identical to the previous one (consecutive root copies: both poses
                 // equal bit for bit, both with the junction) has that edge's verdict
                 const bool dup = e >= 1 && e < E - 1 && same_pose(prev, a) && same_pose(a, bp);
+                const int gv = (e >= 1 && e < s) ? path[e == 1 ? D - 1 : pos[e - 2]] : -1;
+                const int gm = (gtab && gv >= 0) ? __builtin_amdgcn_readfirstlane(gtab[gv]) : 0;
                 int st = prev_st;
-                if (!dup) {
+                if (e >= 1 && e == s) {
+                    st = fnone ? kCfPanic : kAccept;
+                } else if (gm > 0) {
+                    st = gm - 1;
+                } else if (!dup) {
                     const long long rv = cf_edge_check<false>(sc, a, bp, e < E - 1, lit_scratch,
                                                               lit_locks, gs, lrec);
                     st = (int)(rv & 15);
                     ++t_edges;
                     t_pts += (rv >> 4) & 0x3fffffff;
                     t_arc += rv >> 34;
+                    if (gtab && gv >= 0 && lane == 0) gtab[gv] = st + 1;
                 }
                 if (st != kAccept) {
                     if (st == kCfPanic) bad = 2;
