@@ -106,3 +106,15 @@ def test_batch_plan_before_extend_and_reuse(pkg, ctx, oracle_mod):
     for k in ("best_node", "n_points", "n_finishes"):
         assert np.array_equal(g1[k], g2[k])
     assert np.array_equal(g1["length"], g2["length"])
+
+
+def test_batch_plan_field512_128(pkg, ctx, oracle_mod):
+    """config 3's recipe at 128 queries x 2000 iterations (~10k check_finish items in one launch:
+    thousands of waves share optimize's memo) — every query's plan equals its
+    sequential oracle plan"""
+    from pathplanning_amd import scenes
+
+    raw = scenes.field512()
+    got, exp, checked = _run(ctx, oracle_mod, raw, 0, 128, 2000)
+    assert checked >= 8192
+    _check(got, exp, checked, raw)
