@@ -48,8 +48,14 @@ typedef struct pp_dubins_config {
 } pp_dubins_config;
 
 /* Counters of the batched extend driver (since pp_rrt_new / pp_batch_new / pp_star_new or the
- * last pp_rrt_reset_stats).  pp_rrt_get_stats copies min(out_size, sizeof(pp_stats)) bytes, so a
- * caller built against an older, shorter layout gets a prefix and never an overrun. */
+ * last pp_rrt_reset_stats).  pp_rrt_get_stats copies min(out_size, sizeof(pp_stats)) bytes: the
+ * size argument guards ABI 2+ callers only (ABI 1's entry point had no out_size and a different
+ * layout; a v1 binary must be rebuilt).  From ABI 2 on, fields are only ever appended, so an ABI 2
+ * caller of a later library gets the prefix it knows and never an overrun.
+ * The *_ms fields are HIP-event spans on the kernel's own stream: with the query batches' two or
+ * three sub-batch streams a span also covers time the other streams' kernels held the GPU, so
+ * their sums are stream-span times, not isolated kernel durations (those come from a rocprofv3
+ * kernel trace: profiles/r*_kernel_durations.json). */
 typedef struct pp_stats {
     int64_t iterations;       /* extend iterations consumed (plan_one calls, minus check_finish) */
     int64_t accepted;         /* nodes inserted */

@@ -37,7 +37,10 @@ WORD_MODES = [(L, S, L), (R, S, R), (L, S, R), (R, S, L), (R, L, R), (L, R, L)]
 
 
 def fmodr(x, y):  # dubins.rs:14-16
-    return x - y * math.floor(x / y)
+    q = x / y
+    # f64::floor passes NaN / inf through (math.floor raises): a NaN pose gives NaN words, which
+    # never win `bcost > cost` (dubins.rs:354), so the steer is None as in Rust
+    return x - y * (math.floor(q) if math.isfinite(q) else q)
 
 
 def mod2pi(theta):  # dubins.rs:18-20

@@ -2683,13 +2683,14 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_tail_kernel(WinKArgs 
 
 // ---------------------------------------------------------------- check_finish
 //
-// RRT::check_finish (rrt.rs:428-438) for a batch of tree nodes, one workgroup per node
-// (persistent over the batch), the node's ancestor path root..node staged in LDS:
-//   optimize (rrt.rs:463-487)   level i: candidates path[0..L] root first, 4 waves steer+collide
-//                               4 candidates at a time, the first accepted one wins; recursion
-//                               = the next level on that ancestor; RECURSION_LIMIT 16.  Every
-//                               candidate parent is a tree node, so verifying edge ++ [to] is
-//                               verify(line_to_origin(new)).
+// RRT::check_finish (rrt.rs:428-438) for a batch of tree nodes, ONE WAVE PER NODE (kCfWaves
+// independent waves per workgroup, nodes from a launch-wide counter), the node's ancestor path
+// root..node in the wave's region of a global path buffer (kCfMaxDepth ints per wave):
+//   optimize (rrt.rs:463-487)   level i: candidates path[0..L] root first, steered + collided one
+//                               at a time on the wave, the first accepted one wins (memoised per
+//                               tree node in ftab); recursion = the next level on that ancestor;
+//                               RECURSION_LIMIT 16.  Every candidate parent is a tree node, so
+//                               verifying edge ++ [to] is verify(line_to_origin(new)) (§3.2).
 //   finalize (rrt.rs:503-540)   the chain goal → optimised copies → tree path → root; every edge
 //                               is verified with its junction chord, the edge into the root
 //                               without one (the root contributes no point); a None steer is the
@@ -3036,10 +3037,14 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
         if (vok && sc.ne > 0 && in_obstacle(sc.ne, sc.ex0, sc.ey0, sc.ex1, sc.ey1, sc.epoly, gx, gy))
             vok = false;
         // a panic anywhere in finalize wins over a rejection (the reference builds the whole line
-        // before it verifies): the other edges' steers, lane-parallel
-        if (bad == 0 && !vok) {
+        // before it verifies): the other edges' steers, lane-parallel.  A verified chain also
+        // scans its tree edges s + 1 .. E - 1, which were not steered above: insertion accepts a
+        // None steer as the straight polyline (rrt.rs:313), finalize panics on it (rrt.rs:529).
+        // (None needs a non-finite pose — LSL's and RSR's p² differ only in the sign of one
+        // term, so one of them is >= 0 — e.g. a NaN start yaw; only finishes pay the scan.)
+        if (bad == 0 && (!vok || E > Ev)) {
             bool none = false;
-            for (int e = lane; e < E; e += 64)
+            for (int e = (vok ? Ev : 0) + lane; e < E; e += 64)
                 if (cf_npoint(sc, pose(e), pose(e + 1)) == 0) none = true;
             if (__any(none)) bad = 2;
         }
@@ -3130,19 +3135,22 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
         __syncthreads();
         if (tid == 0) {  // edge capacities -> offsets
             int off = 0;
-            bool neg = false;
+            bool none = false, neg = false;
             for (int e = 0; e < E; ++e) {
                 const int c = et[2 * e];
-                neg |= c <= 0;
+                none |= c == 0;
+                neg |= c < 0;
                 et[2 * e] = off;
                 off += c > 0 ? c : 0;
             }
-            s_off = (off <= pts_cap && !neg) ? off : -1;
+            // a None steer is finalize's panic (rrt.rs:529); an overflowing count or a line
+            // past the point capacity is the capacity error
+            s_off = none ? -2 : (off <= pts_cap && !neg) ? off : -1;
         }
         __syncthreads();
         const int total = s_off;
         if (total < 0) {
-            if (tid == 0) s_bad = 8;  // (a None / overflowing edge was rejected before)
+            if (tid == 0) s_bad = total == -2 ? 2 : 8;
         } else {
             for (int e = tid; e < E; e += kCfThreads) {
                 const int off = et[2 * e];

@@ -31,7 +31,9 @@ constexpr int kPrepLanes = 8;        // lanes per task in steer_prep's phase A
 constexpr int kPrepThreads = 256;    // steer_prep workgroup: 32 tasks (8 per wave)
 constexpr int kWalkThreads = 512;    // steer_walk workgroup: 8 tasks at a time (3 workgroups per CU)
 constexpr int kWalkTallySlots = 4096;  // profiling: walk point tallies per workgroup (x2: arcs)
-constexpr int kCfMaxDepth = 8192;    // check_finish: ancestor path staged in LDS (32 KB)
+constexpr int kCfMaxDepth = 8192;    // check_finish: ancestor path per wave, in a global buffer of
+                                     // grid * kCfWaves * kCfMaxDepth ints (kCfGrid 512: 64 MiB per
+                                     // context, allocated on the first check_finish)
 constexpr int kCfLevels = 16;        // RECURSION_LIMIT, rrt.rs:14
 constexpr int kCfMaxEdges = kCfLevels + 1 + kCfMaxDepth;
 constexpr int kCfGrid = 512;        // check_finish workgroups: 2 per CU (literal scratch: the pool)

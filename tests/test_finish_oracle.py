@@ -74,3 +74,31 @@ def test_bench6_start_never_finishes(oracle_mod):
     assert acc > 50 and bn == -1 and not (log == 1).any()
     r = oracle_mod.check_finish(sc, tr, 1, raw["goal"][:2], raw["goal"][2])
     assert r["chain"][-1] == 0 and len(r["chain"]) == 16  # ... → root copies to the limit
+
+
+def test_none_steers_nan_start_yaw(oracle_mod):
+    """A None Dubins steer needs a non-finite pose (LSL's and RSR's p² differ only in the sign of
+    one term, so one of them is >= 0 for finite inputs).  A NaN start yaw makes every edge into
+    the root None: insertion takes it as the straight polyline [(x, y), root] (rrt.rs:313,
+    line_to_origin), and finalize panics on it (rrt.rs:529).  Both restatements agree: the same
+    tree, and check_finish of every node is the panic."""
+    import dubins_py as dpy
+    from pathplanning_amd import scenes
+
+    raw = scenes.bench6_open(float("nan"))
+    sc = oracle_mod.OracleScene.from_raw(raw)
+    tr = oracle_mod.OracleTree(raw["start"], 1 << 12)
+    oracle_mod.rrt_extend(sc, tr, 7, 0, 300)
+    x, y, yaw, par = tr.arrays()
+    ptree = {"x": [raw["start"][0]], "y": [raw["start"][1]], "yaw": [float("nan")], "parent": [-1]}
+    dpy.rrt_extend(sc.as_dict(), ptree, 7, 0, 300)
+    assert len(x) == len(ptree["x"]) > 50
+    assert np.array_equal(x, ptree["x"]) and np.array_equal(y, ptree["y"])
+    assert np.array_equal(par, ptree["parent"])
+    assert int((par == 0).sum()) > 1  # several None edges into the root were inserted
+    nodes = dpy.tree_nodes(ptree)
+    for v in range(1, len(x), 7):
+        with pytest.raises(RuntimeError):
+            oracle_mod.check_finish(sc, tr, v, raw["goal"][:2], raw["goal"][2])
+        with pytest.raises(RuntimeError):
+            dpy.check_finish(sc.as_dict(), nodes[v], raw["goal"][:2], raw["goal"][2])

@@ -21,7 +21,12 @@ def _bench(*args, timeout=240):
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]  # rank 0 prints the only line
-    return json.loads(lines[0])
+    # strict: the driver's parser refuses Infinity / NaN (round 3's line failed exactly so)
+    return json.loads(lines[0], parse_constant=_refuse)
+
+
+def _refuse(tok):
+    raise ValueError(f"non-standard JSON constant {tok!r} in the bench line")
 
 
 @pytest.mark.gpu
