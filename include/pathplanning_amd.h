@@ -25,8 +25,9 @@ extern "C" {
 #endif
 
 /* 2: pp_stats lost the diagnostic stamps and gained the batch / check_finish counters;
- *    pp_rrt_get_stats takes the caller's sizeof(pp_stats); pp_batch_plan added */
-#define PP_ABI_VERSION 2
+ *    pp_rrt_get_stats takes the caller's sizeof(pp_stats); pp_batch_plan added
+ * 3: pp_batch_set_schedule (the persistent batch kernel); pp_stats appended its counters */
+#define PP_ABI_VERSION 3
 
 #define PP_OK 0
 #define PP_ERR_INVALID_ARGUMENT (-1)
@@ -86,6 +87,13 @@ typedef struct pp_stats {
     int64_t finish_edges;     /* Dubins edges steered + verified by check_finish (profiling on) */
     int64_t finish_points;    /* polyline points those edges walked (profiling on) */
     int64_t finish_arc_points;  /* ... of them on L / R segments */
+    /* ABI 3: the persistent query-batch kernel (pp_batch_set_schedule) */
+    int64_t batch_query_steps;  /* query batches: window steps summed over the queries */
+    double persist_ms;          /* HIP events around the persistent batch kernel (profiling on) */
+    int64_t persist_launches;
+    int64_t persist_cycles[5];  /* its phases, shader clock cycles of one thread per workgroup summed
+                                   over the workgroups (profiling on): query refill, samples +
+                                   nearest node, steer_prep, steer_walk, insert */
 } pp_stats;
 
 int pp_abi_version(void);
@@ -245,6 +253,15 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
  * 2048 queries, else 16 while the step holds at most 131072 tasks).  Results do not depend on it: every query's tree equals its one-at-a-time
  * sequential run.  Applies to the current batch and the next ones. */
 int pp_batch_set_window(pp_ctx* ctx, int k);
+/* How pp_batch_extend runs a batch (results are identical):
+ *   PP_BATCH_PERSISTENT (default)  one launch per call: every workgroup takes queries from a
+ *                                  counter and steps their windows itself (samples + nearest node,
+ *                                  steer, collide, insert) until each reaches its target;
+ *   PP_BATCH_LOCKSTEP              four launches per step over the whole batch (two sub-batch
+ *                                  streams), the host topping up queries whose windows stopped. */
+#define PP_BATCH_PERSISTENT 0
+#define PP_BATCH_LOCKSTEP 1
+int pp_batch_set_schedule(pp_ctx* ctx, int schedule);
 /* n_steps lockstep steps: every query runs one plan_one extend iteration (rrt.rs:583-589) per
  * step until it reaches max_iter.  Totals over the batch are returned (may be NULL).  On the
  * GPU a step evaluates up to the batch window's iterations per query at once. */

@@ -187,6 +187,9 @@ struct pp_ctx {
     DBuf<PrepRec> mq_rec;
     DBuf<DevState> mq_state;      // [3]: the whole batch, then one per sub-batch (mq_sub_args)
     hipStream_t sub_stream[4] = {};  // sub-batch streams 1.. (0 is `stream`), created on first use
+    int mq_sched = PP_BATCH_PERSISTENT;  // pp_batch_set_schedule
+    DBuf<int> pq_next;                   // the persistent kernel's query counter
+    DBuf<long long> pq_tally;            // its tally (PqArgs::tally): 8 counters
     hipEvent_t fork_ev = nullptr;
     std::vector<double> mq_goal;  // 3 per query (RRT::new's goal; pp_batch_plan)
     DBuf<double> mq_goal_d;       // [3Q] the goals on the device (pp_batch_plan)
@@ -222,6 +225,8 @@ struct pp_ctx {
            insert_ms = 0.0;
     int64_t nn_scan_launches = 0, steer_launches = 0, finish_launches = 0;
     int64_t batch_steps = 0, batch_passes = 0;
+    double persist_ms = 0.0;
+    int64_t persist_launches = 0;
     DBuf<long long> cf_tally;  // check_finish (profiling): nodes, edges, points, arc points
     DBuf<long long> wg_pts;  // walked polyline points per walk workgroup (profiling on)
     long long* prof_points() const { return prof ? wg_pts.p : nullptr; }
@@ -230,6 +235,10 @@ struct pp_ctx {
         nn_scan_ms = steer_ms = finish_ms = finalize_ms = prep_ms = insert_ms = 0.0;
         nn_scan_launches = steer_launches = finish_launches = 0;
         batch_steps = batch_passes = 0;
+        persist_ms = 0.0;
+        persist_launches = 0;
+        if (pq_tally.p && hipMemsetAsync(pq_tally.p, 0, pq_tally.n * sizeof(long long), stream) != hipSuccess)
+            return PP_ERR_HIP;
         if (wg_pts.p && hipMemsetAsync(wg_pts.p, 0, wg_pts.n * sizeof(long long), stream) != hipSuccess)
             return PP_ERR_HIP;
         if (cf_tally.p && hipMemsetAsync(cf_tally.p, 0, cf_tally.n * sizeof(long long), stream) != hipSuccess)
@@ -1811,6 +1820,57 @@ int pp_batch_set_window(pp_ctx* ctx, int k) {
     return PP_OK;
 }
 
+int pp_batch_set_schedule(pp_ctx* ctx, int schedule) {
+    if (!ctx) return set_err(PP_ERR_INVALID_ARGUMENT, "null context");
+    if (schedule != PP_BATCH_PERSISTENT && schedule != PP_BATCH_LOCKSTEP)
+        return set_err(PP_ERR_INVALID_ARGUMENT, "schedule must be PP_BATCH_PERSISTENT or PP_BATCH_LOCKSTEP");
+    ctx->mq_sched = schedule;
+    return PP_OK;
+}
+
+namespace {
+// pp_batch_extend, persistent schedule: one launch runs every query to its target (the window
+// stops and resumes inside the kernel, so there are no top-up passes)
+int batch_extend_persistent(pp_ctx* ctx, const MqArgs& a) {
+    hipStream_t st = ctx->stream;
+    if (!ctx->pq_next.p) PP_HIP(ctx->pq_next.reserve(1));
+    if (!ctx->pq_tally.p) {
+        PP_HIP(ctx->pq_tally.reserve(8));
+        PP_HIP(hipMemsetAsync(ctx->pq_tally.p, 0, 8 * sizeof(long long), st));
+    }
+    PP_HIP(hipMemsetAsync(ctx->pq_next.p, 0, sizeof(int), st));
+    PqArgs pa;
+    pa.mq = a.mq;
+    pa.sc = a.sc;
+    pa.slots = std::max(1, std::min(kPqMaxSlots, kPqMaxTasks / std::max(1, a.mq.K)));
+    pa.qnext = ctx->pq_next.p;
+    pa.lit_scratch = a.lit_scratch;
+    pa.lit_locks = a.lit_locks;
+    pa.err = a.err;
+    pa.tally = ctx->pq_tally.p;
+    if (ctx->prof) {
+        int r = ensure_events(ctx, 2);
+        if (r) return r;
+        PP_HIP(hipEventRecord(ctx->ev[0], st));
+    }
+    PP_HIP(launch_mq_persist(st, pa));
+    if (ctx->prof) {
+        PP_HIP(hipEventRecord(ctx->ev[1], st));
+        PP_HIP(hipEventSynchronize(ctx->ev[1]));
+        float ms = 0.f;
+        PP_HIP(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
+        ctx->persist_ms += ms;
+        ctx->persist_launches += 1;
+    }
+    int err = 0;
+    PP_HIP(hipMemcpyAsync(&err, ctx->mq_err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    if (err) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
+    ctx->batch_passes += 1;
+    return PP_OK;
+}
+}  // namespace
+
 int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted) {
     int r = check_ctx(ctx, true, false);
     if (r) return r;
@@ -1823,6 +1883,13 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
     // an earlier call's PP_ERR_STEER_OVERFLOW does not stick to this one
     PP_HIP(hipMemsetAsync(ctx->mq_err.p, 0, sizeof(int), ctx->stream));
     PP_HIP(launch_mq_target(ctx->stream, a.mq, n_steps, ctx->mq_target.p));
+    if (ctx->mq_sched == PP_BATCH_PERSISTENT) {
+        if ((r = batch_extend_persistent(ctx, a))) return r;
+        if ((n_iterations || n_accepted) && (r = mq_totals(ctx, &it1, &n1))) return r;
+        if (n_iterations) *n_iterations = it1 - it0;
+        if (n_accepted) *n_accepted = n1 - n0;
+        return PP_OK;
+    }
     // sub-batches on their own streams (profiled too: the events time the schedule that runs)
     const int nsub = ctx->mq_nsub;
     MqArgs sub[kMaxSub];
@@ -2229,6 +2296,17 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out, uint64_t out_size) {
         s.finish_edges = t[1];
         s.finish_points = t[2];
         s.finish_arc_points = t[3];
+    }
+    s.persist_ms = ctx->persist_ms;
+    s.persist_launches = ctx->persist_launches;
+    if (ctx->pq_tally.p) {  // the persistent batch kernel: query-steps, points, phase cycles
+        long long t[8];
+        PP_HIP(hipMemcpyAsync(t, ctx->pq_tally.p, sizeof t, hipMemcpyDeviceToHost, ctx->stream));
+        PP_HIP(hipStreamSynchronize(ctx->stream));
+        s.batch_query_steps = t[0];
+        s.walk_points += t[1];
+        s.walk_arc_points += t[2];
+        for (int p = 0; p < 5; ++p) s.persist_cycles[p] = t[3 + p];
     }
     std::memcpy(out, &s, (size_t)std::min<uint64_t>(out_size, sizeof s));
     return PP_OK;

@@ -128,6 +128,26 @@ struct MqArgs {
     long long* wg_points = nullptr;  // profiling: walked points per walk workgroup (or null)
 };
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps);
+// Persistent form (round 4): ONE launch runs every query to mq.target.  A workgroup owns `slots`
+// queries at a time (a launch-wide counter hands them out; qnext zeroed before the launch) and
+// steps their windows itself — samples + NN, steer_prep, steer_walk, insert — with the records in
+// LDS.  slots * mq.K <= kPqMaxTasks, both powers of two.
+constexpr int kPqMaxTasks = 64;
+constexpr int kPqThreads = 512;   // 8 waves per workgroup
+constexpr int kPqMaxSlots = 8;    // queries per workgroup (the insert: one wave each)
+struct PqArgs {
+    MqDev mq{};
+    SceneDev sc{};
+    int slots = 1;
+    int* qnext = nullptr;
+    double* lit_scratch = nullptr;  // kLiteralWaves buffers
+    int* lit_locks = nullptr;
+    int* err = nullptr;
+    long long* tally = nullptr;  // profiling (or null): query-steps, walked points, arc points,
+                                 // then thread 0's clock cycles per phase (refill, NN, prep, walk,
+                                 // insert) summed over the workgroups: 8 int64, zeroed before
+};
+hipError_t launch_mq_persist(hipStream_t s, const PqArgs& a);
 hipError_t launch_mq_init(hipStream_t s, const MqDev& mq, const double* starts);
 // the per-query iteration targets of a pp_batch_extend(n_steps) call
 hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int64_t* target);

@@ -1617,22 +1617,16 @@ __device__ __forceinline__ void prep_task(const SceneDev& sc, int r, int g0, int
         wq = mod2pi(mod2pi(beta) - alpha - wt + mod2pi(wp));
     }
     const double wcost = fabs(wt) + fabs(wp) + fabs(wq);
-    // first strict minimum in ALL_PLANNERS order (dubins.rs:351-360)
-    double bc = __builtin_inf();
-    int bw = -1;
-    const double wc[6] = {grp8_bcast_f64<0>(wcost), grp8_bcast_f64<1>(wcost),
-                          grp8_bcast_f64<2>(wcost), grp8_bcast_f64<3>(wcost),
-                          grp8_bcast_f64<4>(wcost), grp8_bcast_f64<5>(wcost)};
-    const int wk[6] = {grp8_bcast_i32<0>((int)wok), grp8_bcast_i32<1>((int)wok),
-                       grp8_bcast_i32<2>((int)wok), grp8_bcast_i32<3>((int)wok),
-                       grp8_bcast_i32<4>((int)wok), grp8_bcast_i32<5>((int)wok)};
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        if (wk[k] && bc > wc[k]) {
-            bc = wc[k];
-            bw = k;
-        }
-    }
+    // first strict minimum in ALL_PLANNERS order (dubins.rs:351-360: bcost starts at inf and a
+    // word wins on `bcost > cost`, so a NaN or inf cost never wins and ties keep the earlier
+    // word) = the (cost, word) argmin over the group's valid words: a DPP butterfly over the
+    // 8-lane group (xor 1, xor 2, half-row mirror), no per-word broadcasts
+    double bc = (r < 6 && wok && wcost < __builtin_inf()) ? wcost : __builtin_inf();
+    int bw = bc < __builtin_inf() ? r : 0x7fffffff;
+    argmin_dpp<0xB1>(bc, bw);
+    argmin_dpp<0x4E>(bc, bw);
+    argmin_dpp<0x141>(bc, bw);
+    if (!(bc < __builtin_inf())) bw = -1;
     const int src = g0 + (bw < 0 ? 0 : bw);
     const double L0 = __shfl(wt, src), L1 = __shfl(wp, src), L2 = __shfl(wq, src);
     const int m0 = word_mode(bw, 0), m1 = word_mode(bw, 1), m2 = word_mode(bw, 2);
@@ -3489,6 +3483,369 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
         if (ev) (void)hipEventRecord(ev[4], s);
     }
     return hipGetLastError();
+}
+
+// ------------------------------------------- persistent query batch (config 3, round 4)
+//
+// One launch runs every query of the batch to its target.  A workgroup owns `slots` queries at a
+// time (taken from a launch-wide counter: one atomic per query, not per task) and advances them
+// window by window inside the workgroup, the phases of a step separated by workgroup barriers:
+//   1. samples + exact NN   task t = (slot s, window slot k): iteration it_s + k of query q_s
+//                           (rand_point rrt.rs:139-146 on the query's stream; get_nearest_node
+//                           rrt.rs:378-391 in f64, lowest index on ties): kPqThreads / T threads
+//                           per task stride the query's rows, an LDS argmin merges them
+//   2. steer_prep           prep_task, 8 lanes per task, the PrepRec into LDS (never HBM)
+//   3. steer_walk           the waves draw the step's tasks from an LDS counter and walk the LDS
+//                           record (walk_rec; the scene image staged once per workgroup)
+//   4. insert               one wave per slot: literal re-runs, then mq_insert_kernel's in-order
+//                           replay — the window stops at the first iteration an accepted window
+//                           sample is strictly nearer to than its snapshot NN — and the append
+//                           (rrt.rs:586-589)
+// Every query's tree is exactly its one-iteration-at-a-time run (the same rule as the lockstep
+// kernels).  No step waits for another workgroup: a long path holds only its own workgroup's
+// step, the step costs no launch, and a cut costs the rest of the window, not a relaunch.
+constexpr int kPqWaves = kPqThreads / 64;
+static_assert(kPqMaxSlots <= kPqWaves, "the insert runs one wave per slot");
+constexpr int kPqMinW = 4;            // waves per SIMD the register budget allows
+
+// The workgroup's LDS after the scene image and the waves' generator slots; T = slots * K <=
+// kPqMaxTasks window slots per step.
+struct PqLds {
+    PrepRec rec[kPqMaxTasks];
+    double tx[kPqMaxTasks], ty[kPqMaxTasks], td2[kPqMaxTasks];
+    double rd[kPqThreads];
+    int ri[kPqThreads];
+    int tpn[kPqMaxTasks], tst[kPqMaxTasks];
+    long long sit[kPqMaxSlots], stg[kPqMaxSlots];
+    int sq[kPqMaxSlots], sn[kPqMaxSlots];
+    int next, any;
+};
+__host__ __device__ inline int pq_lds_bytes(int scene_bytes) {
+    return scene_bytes + kPqWaves * kGenSlots * 8 + (int)((sizeof(PqLds) + 15) & ~(size_t)15);
+}
+
+// The walk's record as wave-uniform values (SGPRs): an LDS record is read with ds_read into VGPRs,
+// ~60 of them for the ~30 fields the walk keeps live; readfirstlane moves each into SGPRs, as the
+// scalar loads of a global record do.
+__device__ __forceinline__ double ufl(double v) {
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+__device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ PrepRec uniform_rec(const PrepRec& r) {
+    PrepRec u;
+    u.x = ufl(r.x);
+    u.y = ufl(r.y);
+    u.px = ufl(r.px);
+    u.py = ufl(r.py);
+    u.yaw = ufl(r.yaw);
+    u.pyaw = ufl(r.pyaw);
+    u.c = ufl(r.c);
+    u.cw = ufl(r.cw);
+    u.sw = ufl(r.sw);
+    for (int i = 0; i < 3; ++i) {
+        u.ox[i] = ufl(r.ox[i]);
+        u.oy[i] = ufl(r.oy[i]);
+        u.ca[i] = ufl(r.ca[i]);
+        u.sa[i] = ufl(r.sa[i]);
+        u.L[i] = ufl(r.L[i]);
+        u.m[i] = ufl(r.m[i]);
+        u.cnt[i] = ufl(r.cnt[i]);
+    }
+    u.fb_pd = ufl(r.fb_pd);
+    u.fb_dd = ufl(r.fb_dd);
+    u.n_point = ((long long)ufl((int)(r.n_point >> 32)) << 32) |
+                (unsigned int)ufl((int)(r.n_point & 0xffffffff));
+    u.state = ufl(r.state);
+    u.fb_seg = ufl(r.fb_seg);
+    return u;
+}
+
+// the literal path out of line: it runs once in a few thousand steps, and inlined its registers
+// would set the whole kernel's budget
+__device__ __noinline__ int pq_literal(const SceneDev& sc, const PrepRec* R, double* bx) {
+    return steer_collide_literal(sc, R->x, R->y, R->yaw, R->px, R->py, R->pyaw, bx,
+                                 bx + kLiteralCap, bx + 2 * kLiteralCap);
+}
+
+template <bool kLds, int kScene>
+__global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs a) {
+    const MqDev& mq = a.mq;
+    const SceneDev& sc = a.sc;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int K = mq.K, QS = a.slots, T = QS * K;
+    const int G = kPqThreads / T;  // NN threads per task (T is a power of two <= kPqMaxTasks)
+    if (kLds) stage_scene(sc);
+    char* base = pp_smem + (kLds ? sc.lds_bytes : 0);
+    double* gs = reinterpret_cast<double*>(base) + wave * kGenSlots;
+    PqLds& L = *reinterpret_cast<PqLds*>(base + kPqWaves * kGenSlots * 8);
+    if (tid < kPqMaxSlots) L.sq[tid] = -1;
+    __syncthreads();
+    long long npts = 0, napts = 0, qsteps = 0;
+    long long cyc[5] = {0, 0, 0, 0, 0};  // thread 0, profiling: refill, NN, prep, walk, insert
+    const bool prof = a.tally != nullptr;
+    long long c0 = prof ? (long long)clock64() : 0;
+    auto stamp = [&](int ph) {
+        if (prof && tid == 0) {
+            const long long c1 = (long long)clock64();
+            cyc[ph] += c1 - c0;
+            c0 = c1;
+        }
+    };
+    for (;;) {
+        // 0. refill: a slot whose query reached its target takes the next query that has work
+        //    (-2: the counter is exhausted, never ask again)
+        if (tid < QS) {
+            int q = L.sq[tid];
+            if (q == -1 || (q >= 0 && L.sit[tid] >= L.stg[tid])) {
+                for (;;) {
+                    q = atomicAdd(a.qnext, 1);
+                    if (q >= mq.Q) {
+                        q = -2;
+                        break;
+                    }
+                    const long long it = mq.it[q], tg = mq.target[q];
+                    if (it < tg) {
+                        L.sn[tid] = mq.n[q];
+                        L.sit[tid] = it;
+                        L.stg[tid] = tg;
+                        break;
+                    }
+                }
+                L.sq[tid] = q;
+            }
+        }
+        if (tid == 0) L.next = 0;
+        __syncthreads();
+        int any = 0;
+        for (int s = 0; s < QS; ++s) any |= L.sq[s] >= 0 ? 1 : 0;
+        if (!any) break;
+        if (tid == 0)
+            for (int s = 0; s < QS; ++s) qsteps += L.sq[s] >= 0 ? 1 : 0;
+        stamp(0);
+        // 1. samples and the exact nearest node of each (thread tid: task tid % T, rows i = g mod G)
+        {
+            const int t = tid % T, g = tid / T;
+            const int s = t / K, k = t - s * K;
+            const int q = L.sq[s];
+            double x = 0.0, y = 0.0, bd = __builtin_inf();
+            int bi = 0x7fffffff;
+            bool live = false;
+            if (q >= 0) {
+                const long long it = L.sit[s] + k;
+                live = it < L.stg[s];
+                if (live) {
+                    const uint64_t seed = mq.seed[q];
+                    x = gen_range(seed, 2 * (uint64_t)it, sc.minx, sc.maxx);
+                    y = gen_range(seed, 2 * (uint64_t)it + 1, sc.miny, sc.maxy);
+                    const size_t row = (size_t)q * mq.cap;
+                    const double* __restrict__ X = mq.x + row;
+                    const double* __restrict__ Y = mq.y + row;
+                    const int n = L.sn[s];
+#pragma unroll 4
+                    for (int i = g; i < n; i += G) {
+                        const double dx = x - X[i], dy = y - Y[i];
+                        const double d2 = dx * dx + dy * dy;
+                        if (d2 < bd) {
+                            bd = d2;
+                            bi = i;
+                        }
+                    }
+                }
+            }
+            L.rd[tid] = bd;
+            L.ri[tid] = bi;
+            if (g == 0) {
+                L.tx[t] = x;
+                L.ty[t] = y;
+                L.tpn[t] = live ? 0 : -1;
+            }
+        }
+        __syncthreads();
+        if (tid < T) {
+            double bd = L.rd[tid];
+            int bi = L.ri[tid];
+            for (int g = 1; g < G; ++g) argmin_pair(bd, bi, L.rd[tid + g * T], L.ri[tid + g * T]);
+            if (L.tpn[tid] >= 0) {
+                L.tpn[tid] = bi;
+                L.td2[tid] = bd;
+            }
+        }
+        __syncthreads();
+        stamp(1);
+        // 2. steer_prep: 8 lanes per task (every lane of every wave calls prep_task)
+        for (int b0 = 0; b0 < T; b0 += kPqThreads / 8) {
+            const int t = b0 + tid / 8;
+            const bool in = t < T;
+            const int pn = in ? L.tpn[t] : -1;
+            const bool act = pn >= 0;
+            double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0;
+            if (in) {
+                x = L.tx[t];
+                y = L.ty[t];
+            }
+            if (act) {
+                const size_t o = (size_t)L.sq[t / K] * mq.cap + pn;
+                px = mq.x[o];
+                py = mq.y[o];
+                pyaw = mq.yaw[o];
+            }
+            prep_task(sc, tid & 7, lane & ~7, t, in, act, x, y, px, py, pyaw, 0, 0.0, 0, 0.0, 0.0,
+                      L.rec, nullptr, nullptr);
+        }
+        __syncthreads();
+        stamp(2);
+        // 3. steer_walk: one task at a time per wave from the LDS counter
+        for (;;) {
+            int k = 0;
+            if (lane == 0) k = atomicAdd(&L.next, 1);
+            const int t = __builtin_amdgcn_readlane(k, 0);
+            if (t >= T) break;
+            int np = 0, na = 0;
+            const PrepRec R = uniform_rec(L.rec[t]);
+            const int st = walk_rec<kLds, kScene>(sc, &R, nullptr, gs, np, na);
+            if (lane == 0) L.tst[t] = st;
+            npts += np;
+            napts += na;
+        }
+        __syncthreads();
+        stamp(3);
+        // 4. insert: wave s replays slot s's window in order (lane k: window slot k)
+        if (wave < QS && L.sq[wave] >= 0) {
+            const int s = wave, q = L.sq[s];
+            const int k = lane;
+            const bool inw = k < K;
+            const int t = s * K + k;
+            int st = kReject, pn = -1;
+            double x = 0.0, y = 0.0, yw = 0.0, d2nn = 0.0;
+            if (inw) {
+                pn = L.tpn[t];
+                st = L.tst[t];
+                x = L.tx[t];
+                y = L.ty[t];
+                yw = L.rec[t].yaw;
+                d2nn = L.td2[t];
+            }
+            const bool act = inw && pn >= 0;
+            if (uint64_t lit = __ballot(act && st == kLiteral)) {  // measure-zero trim cases
+                const int slot = lit_acquire(a.lit_locks, (int)blockIdx.x * kPqMaxSlots + s);
+                double* bx = a.lit_scratch + (size_t)slot * 3 * kLiteralCap;
+                for (; lit; lit &= lit - 1) {
+                    const int l = __builtin_ctzll(lit);
+                    const int r = pq_literal(sc, &L.rec[s * K + l], bx);
+                    if (lane == l) st = r;
+                }
+                lit_release(a.lit_locks, slot);
+            }
+            const bool blocked = mq.blocked && mq.blocked[q];
+            const uint64_t accm = __ballot(act && st == kAccept && !blocked);
+            bool cut = !act;
+            for (int j = 0; j < K; ++j) {
+                const double xj = __shfl(x, j), yj = __shfl(y, j);
+                if (((accm >> j) & 1ull) && k > j && act) {
+                    const double dx = x - xj, dy = y - yj;
+                    if (dx * dx + dy * dy < d2nn) cut = true;
+                }
+            }
+            const uint64_t kmask = K >= 64 ? ~0ull : ((1ull << K) - 1ull);
+            const uint64_t cutm = __ballot(inw && cut) & kmask;
+            const int Tc = cutm ? (int)__builtin_ctzll(cutm) : K;  // iterations consumed (>= 1)
+            const uint64_t keep = accm & (Tc >= 64 ? ~0ull : ((1ull << Tc) - 1ull));
+            const bool bad = __ballot(k < Tc && act && st == kError) != 0;
+            const int n = L.sn[s];
+            const int before = __popcll(keep & ((1ull << lane) - 1ull));
+            if (!bad && k < Tc && ((keep >> lane) & 1ull)) {
+                const size_t o = (size_t)q * mq.cap + n + before;
+                mq.x[o] = x;
+                mq.y[o] = y;
+                mq.yaw[o] = yw;
+                mq.parent[o] = pn;
+            }
+            // the sequential spec's node-distance evaluations: iteration k scans n + before nodes
+            long long ev = (inw && k < Tc) ? (long long)(n + before) : 0;
+            for (int o = 1; o < 64; o <<= 1) ev += __shfl_xor(ev, o);
+            if (lane == 0) {
+                if (bad) {
+                    atomicOr(a.err, 1);
+                    L.sit[s] = L.stg[s];  // the reference panics: the query stops here
+                } else {
+                    const int nn = n + __popcll(keep);
+                    const long long it = L.sit[s] + Tc;
+                    L.sn[s] = nn;
+                    L.sit[s] = it;
+                    mq.n[q] = nn;
+                    mq.it[q] = it;
+                    mq.evals[q] += ev;
+                }
+            }
+        }
+        __syncthreads();
+        stamp(4);
+    }
+    if (prof) {  // [0] query-steps, [1] walked points, [2] their arc points, [3..7] phase cycles
+        unsigned long long* tl = reinterpret_cast<unsigned long long*>(a.tally);
+        if (lane == 0) {
+            atomicAdd(&tl[1], (unsigned long long)npts);
+            atomicAdd(&tl[2], (unsigned long long)napts);
+        }
+        if (tid == 0) {
+            atomicAdd(&tl[0], (unsigned long long)qsteps);
+            for (int p = 0; p < 5; ++p) atomicAdd(&tl[3 + p], (unsigned long long)cyc[p]);
+        }
+    }
+}
+
+template <typename F>
+inline hipError_t pq_kernel_for(const SceneDev& sc, F&& f) {
+    const bool lds = sc.lds_bytes > 0;
+    switch (scene_kind(sc)) {
+        case kSceneGrid:
+            return lds ? f(mq_persist_kernel<true, kSceneGrid>)
+                       : f(mq_persist_kernel<false, kSceneGrid>);
+        case kScenePoly:
+            return lds ? f(mq_persist_kernel<true, kScenePoly>)
+                       : f(mq_persist_kernel<false, kScenePoly>);
+        default:
+            return lds ? f(mq_persist_kernel<true, kSceneDisc>)
+                       : f(mq_persist_kernel<false, kSceneDisc>);
+    }
+}
+
+// the resident workgroups of the persistent kernel (occupancy API with its dynamic LDS)
+int pq_grid_cap(const SceneDev& sc) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int>, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    const std::tuple<int, int, int> key{dev, sc.lds_bytes, scene_kind(sc)};
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int cus = 256, per_cu = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+        cus = prop.multiProcessorCount;
+    const hipError_t e = pq_kernel_for(sc, [&](auto kern) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kPqThreads,
+                                                            pq_lds_bytes(sc.lds_bytes));
+    });
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    const int cap = cus * per_cu;
+    cache[key] = cap;
+    return cap;
+}
+
+hipError_t launch_mq_persist(hipStream_t s, const PqArgs& a) {
+    const int K = a.mq.K;
+    if (K < 1 || (K & (K - 1)) || a.slots < 1 || a.slots > kPqMaxSlots ||
+        a.slots * K > kPqMaxTasks || (a.slots & (a.slots - 1)))
+        return hipErrorInvalidValue;
+    const int grid = std::min((a.mq.Q + a.slots - 1) / a.slots, pq_grid_cap(a.sc));
+    return pq_kernel_for(a.sc, [&](auto kern) {
+        kern<<<grid, kPqThreads, pq_lds_bytes(a.sc.lds_bytes), s>>>(a);
+        return hipGetLastError();
+    });
 }
 
 // ------------------------------------------------------- RRT* query batch (config 5, §3.7)
