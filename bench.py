@@ -87,6 +87,9 @@ def parse(argv=None):
                     help="config3: iterations per query evaluated speculatively per GPU step "
                          "(power of two <= 64; 0 = automatic)")
     ap.add_argument("--max-iter", type=int, default=2000, help="config3/5: RRT.max_iter per query")
+    ap.add_argument("--schedule", choices=("persistent", "lockstep"), default="persistent",
+                    help="config3: one persistent launch per extend call (default) or four "
+                         "launches per lockstep step (pp_batch_set_schedule; identical trees)")
     ap.add_argument("--window", type=int, default=4096)
     ap.add_argument("--nodes", type=int, default=100_000, help="tree size before timing")
     ap.add_argument("--seed", type=int, default=42)
@@ -563,7 +566,7 @@ def run_batch(args, D, star, with_cpu):
             return rrt.RRTStarBatch(starts, args.max_iter, raw["step_size"], space, seeds, k=0,
                                     eta=eta, device=D.device)
         return rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
-                            device=D.device, window=args.batch_window)
+                            device=D.device, window=args.batch_window, schedule=args.schedule)
 
     batch = fresh()
     batch.extend(args.warmup)  # untimed warmup on a throwaway run
@@ -617,10 +620,14 @@ def run_batch(args, D, star, with_cpu):
     if star:
         extra["rewires_total"] = int(D.allreduce(float(stt[3].sum()), "sum"))
     else:
-        extra["passes"] = {"steps": int(st_timed["batch_steps"]),
-                           "host_passes": int(st_timed["batch_passes"]),
-                           "ideal_steps": -(-steps // (args.batch_window or
-                                                       auto_batch_window(b - a)))}
+        ideal = -(-steps // (args.batch_window or auto_batch_window(b - a)))
+        if args.schedule == "persistent":
+            extra["passes"] = {"window_steps_per_query": round(
+                                   st_timed["batch_query_steps"] / max(b - a, 1), 2),
+                               "ideal_steps": ideal, "launches": int(st_timed["batch_passes"])}
+        else:
+            extra["passes"] = {"steps": int(st_timed["batch_steps"]),
+                               "host_passes": int(st_timed["batch_passes"]), "ideal_steps": ideal}
     # profiled pass (same workload, same streams): HIP events around every kernel of every step
     batch.close()
     batch = fresh()
@@ -632,15 +639,17 @@ def run_batch(args, D, star, with_cpu):
         batch.plan()
         extra["plan"]["roofline"] = finish_roofline(batch.stats())
     batch.close()
-    nn_ms = sp["nn_scan_ms"] / max(sp["nn_scan_launches"], 1)
-    evals_per_launch = float(evals_p.sum()) / max(sp["nn_scan_launches"], 1)
-    bytes_per_eval = 16  # f64 x + f64 y of one SoA row (exact NN)
-    achieved = evals_per_launch * bytes_per_eval / (nn_ms * 1e-3) / 1e9
     wl = "config5" if star else "config3"
     # the counter passes were taken on the whole 8192-query batch on one GPU
     pmc = load_profile("batch_pmc.json").get(wl, {}) if args.queries == 8192 and D.world == 1 else {}
-    nn_share = sp["nn_scan_ms"] / max(sp["nn_scan_ms"] + sp["steer_ms"], 1e-9)
-    launches = max(sp["nn_scan_launches"], 1)
+    evals_total = float(evals_p.sum())
+    persistent = not star and args.schedule == "persistent"
+    if persistent:
+        roof, nn_roof, phases = persist_rooflines(sp, evals_total, pmc.get("persist", {}))
+    else:
+        roof = walk_roofline(sp, pmc.get("steer_walk", {}), wl)
+        nn_roof = lockstep_nn_roofline(sp, evals_total, star, pmc)
+        phases = None
     res = {
         "value": round(iters_total / t_max, 1),
         "unit": "iterations/s",
@@ -656,26 +665,23 @@ def run_batch(args, D, star, with_cpu):
         "iterations_total": iters_total,
         "nodes_total": int(allrec[:, 2].sum()),
         "records_digest": hashlib.sha256(allrec.astype(np.int64).tobytes()).hexdigest()[:16],
-        "roofline": walk_roofline(sp, pmc.get("steer_walk", {}), wl),
-        "nn_roofline": {
-            "kernel": "star_sample (exact f64 NN)" if star else "mq_sample_nn (exact f64 NN)",
-            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc.get("nn", {}).get("hbm_bytes_per_launch"),
-            "avg_launch_ms": round(nn_ms, 5), "evals_per_launch": int(evals_per_launch),
-            "bytes_per_eval": bytes_per_eval,
-            "share_of_nn_plus_walk_time": round(nn_share, 4),
-        },
+        "roofline": roof,
+        "nn_roofline": nn_roof,
         **extra,
     }
-    if not star:
+    if persistent:
+        res["schedule"] = "persistent (one launch: every workgroup steps its own queries)"
+        res["phase_share"] = phases
+    elif not star:
+        launches = max(sp["nn_scan_launches"], 1)
+        res["schedule"] = "lockstep (four launches per step, two sub-batch streams)"
         res["step_chain_us"] = {"mq_sample_nn": round(1e3 * sp["nn_scan_ms"] / launches, 2),
                                 "steer_prep": round(1e3 * sp["prep_ms"] / launches, 2),
                                 "steer_walk": round(1e3 * sp["steer_ms"] / launches, 2),
                                 "mq_insert": round(1e3 * sp["insert_ms"] / launches, 2),
                                 "launches_per_kernel": int(launches),
-                                "note": "per launch, each sub-batch stream's launch counted "
-                                        "(the schedule of the timed region)"}
+                                "note": "HIP-event stream spans per launch (the sub-batch streams "
+                                        "overlap, so these include the other stream's kernels)"}
     if star:
         res["workload"] = (f"config5 (stretch, build-defined RRT*): {args.queries} queries on "
                            f"{raw['name']} (10240 discs r~U(1,4) on 2048^2), Steer eta {eta}, "
@@ -695,6 +701,64 @@ def run_batch(args, D, star, with_cpu):
                 raw, starts, goals, seeds, args.max_iter, args.cpu_seconds,
                 allrec[:, 5], allrec[:, 7].view(np.float64))
     return res
+
+
+PHASES = ("serial", "steer_prep", "steer_walk", "idle", "unused")
+
+
+def persist_rooflines(sp, evals_total, pmc):
+    """The persistent batch kernel (one launch per extend call): its walked points' algorithmic
+    FP64 FLOP against the whole launch (HIP events) and against its walk items alone (their share
+    of the waves' time), and the serial phases' f64 row reads (insert + samples + nearest node:
+    an upper bound of the NN's own time)."""
+    cyc = sp.get("persist_cycles") or [0] * 5
+    tot = float(sum(cyc)) or 1.0
+    share = {p: round(c / tot, 4) for p, c in zip(PHASES, cyc) if p != "unused"}
+    r = fp64_roofline("mq_persist_kernel (whole launch: samples + NN, steer_prep, steer_walk, "
+                      "insert)", sp.get("persist_ms", 0.0), sp.get("persist_launches", 0),
+                      sp.get("walk_points", 0), sp.get("walk_arc_points", 0), pmc,
+                      "HIP events around the persistent launch of the profiled pass")
+    if r:
+        wshare = share["steer_walk"] or 1.0
+        r["walk_phase"] = {"share_of_wave_time": wshare,
+                           "achieved": round(r["achieved"] / wshare, 4),
+                           "frac": round(r["frac"] / wshare, 5),
+                           "note": "the same FLOP over the launch time x the walk items' share "
+                                   "of the waves' time"}
+    nn = None
+    launches = max(sp.get("persist_launches", 0), 1)
+    ms = sp.get("persist_ms", 0.0) / launches * share["serial"]
+    if ms > 0:
+        bpe = 16  # f64 x + f64 y of one SoA row (exact NN)
+        ach = evals_total / launches * bpe / (ms * 1e-3) / 1e9
+        nn = {"kernel": "mq_persist_kernel serial items: insert + samples + exact f64 NN",
+              "bound": "hbm",
+              "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+              "phase_ms_per_launch": round(ms, 5), "bytes_per_eval": bpe,
+              "evals_per_launch": int(evals_total / launches),
+              "note": "time = launch time x the serial items' share of the waves' time (an upper "
+                      "bound of the NN's own time, so frac is a lower bound)"}
+    return r, nn, share
+
+
+def lockstep_nn_roofline(sp, evals_total, star, pmc):
+    nn_ms = sp["nn_scan_ms"] / max(sp["nn_scan_launches"], 1)
+    if nn_ms <= 0:
+        return None
+    evals_per_launch = evals_total / max(sp["nn_scan_launches"], 1)
+    bytes_per_eval = 16  # f64 x + f64 y of one SoA row (exact NN)
+    achieved = evals_per_launch * bytes_per_eval / (nn_ms * 1e-3) / 1e9
+    nn_share = sp["nn_scan_ms"] / max(sp["nn_scan_ms"] + sp["steer_ms"], 1e-9)
+    return {
+        "kernel": "star_sample (exact f64 NN)" if star else "mq_sample_nn (exact f64 NN)",
+        "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": pmc.get("nn", {}).get("hbm_bytes_per_launch"),
+        "avg_launch_ms": round(nn_ms, 5), "evals_per_launch": int(evals_per_launch),
+        "bytes_per_eval": bytes_per_eval,
+        "share_of_nn_plus_walk_time": round(nn_share, 4),
+    }
 
 
 def cpu_baseline_batch_plan(raw, starts, goals, seeds, max_iter, seconds, best, length):

@@ -91,9 +91,9 @@ typedef struct pp_stats {
     int64_t batch_query_steps;  /* query batches: window steps summed over the queries */
     double persist_ms;          /* HIP events around the persistent batch kernel (profiling on) */
     int64_t persist_launches;
-    int64_t persist_cycles[5];  /* its phases, shader clock cycles of one thread per workgroup summed
-                                   over the workgroups (profiling on): query refill, samples +
-                                   nearest node, steer_prep, steer_walk, insert */
+    int64_t persist_cycles[5];  /* its waves' time (wall_clock64 ticks, 100 MHz, summed over the
+                                   waves; profiling on): serial items (insert, next query, samples
+                                   + nearest nodes), steer_prep passes, steer_walk tasks, idle, 0 */
 } pp_stats;
 
 int pp_abi_version(void);

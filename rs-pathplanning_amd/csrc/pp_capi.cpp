@@ -190,6 +190,7 @@ struct pp_ctx {
     int mq_sched = PP_BATCH_PERSISTENT;  // pp_batch_set_schedule
     DBuf<int> pq_next;                   // the persistent kernel's query counter
     DBuf<long long> pq_tally;            // its tally (PqArgs::tally): 8 counters
+    DBuf<SceneDev> pq_scene;             // the scene in device memory (PqArgs::sc_global)
     hipEvent_t fork_ev = nullptr;
     std::vector<double> mq_goal;  // 3 per query (RRT::new's goal; pp_batch_plan)
     DBuf<double> mq_goal_d;       // [3Q] the goals on the device (pp_batch_plan)
@@ -1839,10 +1840,17 @@ int batch_extend_persistent(pp_ctx* ctx, const MqArgs& a) {
         PP_HIP(hipMemsetAsync(ctx->pq_tally.p, 0, 8 * sizeof(long long), st));
     }
     PP_HIP(hipMemsetAsync(ctx->pq_next.p, 0, sizeof(int), st));
+    if (!ctx->pq_scene.p) PP_HIP(ctx->pq_scene.reserve(1));
+    PP_HIP(hipMemcpyAsync(ctx->pq_scene.p, &a.sc, sizeof(SceneDev), hipMemcpyHostToDevice, st));
     PqArgs pa;
     pa.mq = a.mq;
     pa.sc = a.sc;
-    pa.slots = std::max(1, std::min(kPqMaxSlots, kPqMaxTasks / std::max(1, a.mq.K)));
+    pa.sc_global = ctx->pq_scene.p;
+    // slots per workgroup: every query in flight at once when the resident workgroups allow it
+    // (a 1024-query shard: 2 per workgroup at 2 workgroups per CU), at most kPqMaxTasks tasks
+    const int K = std::max(1, a.mq.K);
+    const int cap = std::max(1, pq_grid_cap_host(a.sc));
+    pa.slots = std::max(1, std::min({kPqMaxSlots, kPqMaxTasks / K, (a.mq.Q + cap - 1) / cap}));
     pa.qnext = ctx->pq_next.p;
     pa.lit_scratch = a.lit_scratch;
     pa.lit_locks = a.lit_locks;

@@ -1795,6 +1795,14 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
 // fma(-q, c, x) is exact, and RN(q + residual rc) with rc = RN(1 / c) is the correctly rounded
 // quotient (Markstein's theorem; no x here is subnormal), i.e. bit-identical to the division —
 // tests/test_div_identity.py checks the identity for the scenes' curvatures.  3 VALU instead of 9.
+// A wave-uniform value into SGPRs: walk_rec's record fields.  A record in LDS is read with
+// ds_read into VGPRs (~60 of them for the ~30 fields the walk keeps live); readfirstlane moves
+// each into SGPRs, as the scalar loads of a global record do (there it folds away).
+__device__ __forceinline__ double ufl(double v) {
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+__device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
 constexpr int kGenPts = 68;  // generator slots: 63 points + 4 overshoot + 1
 constexpr int kSegRow = 6;   // segment-table row (16-byte aligned rows: ds_read_b128)
 template <bool kLds, int kScene = kSceneAny>
@@ -1802,8 +1810,8 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                                         const double* __restrict__ pdv, double* __restrict__ gs,
                                         int& npts, int& napts, bool junction = true) {
     const int lane = threadIdx.x & 63;
-    const int state = p->state;
-    const double x = p->x, y = p->y, px = p->px, py = p->py;
+    const int state = ufl(p->state);
+    const double x = ufl(p->x), y = ufl(p->y), px = ufl(p->px), py = ufl(p->py);
     if (state == kPrepNone) {  // steer failed: polyline [(x, y), (px, py)] (rrt.rs:313)
         const bool has = lane < 2;
         const double qx = lane == 0 ? x : px, qy = lane == 0 ? y : py;
@@ -1813,13 +1821,13 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     if (state != kPrepWalk && state != kPrepFallback) return state;
     const bool partial = state == kPrepFallback;  // pdbuf holds the first ng points only (0 or kPdCap)
     const double step = sc.step_size;
-    const double c = p->c, cw = p->cw, sw = p->sw;
-    const double ox1 = p->ox[1], oy1 = p->oy[1], ox2 = p->ox[2], oy2 = p->oy[2];
-    const double ca0 = p->ca[0], ca1 = p->ca[1], ca2 = p->ca[2];
-    const double sa0 = p->sa[0], sa1 = p->sa[1], sa2 = p->sa[2];
-    const double L0 = p->L[0], L1 = p->L[1], L2 = p->L[2];
-    const int m0 = p->m[0], m1 = p->m[1], m2 = p->m[2];
-    const int n0 = p->cnt[0], n01 = n0 + p->cnt[1], ng = n01 + p->cnt[2];
+    const double c = ufl(p->c), cw = ufl(p->cw), sw = ufl(p->sw);
+    const double ox1 = ufl(p->ox[1]), oy1 = ufl(p->oy[1]), ox2 = ufl(p->ox[2]), oy2 = ufl(p->oy[2]);
+    const double ca0 = ufl(p->ca[0]), ca1 = ufl(p->ca[1]), ca2 = ufl(p->ca[2]);
+    const double sa0 = ufl(p->sa[0]), sa1 = ufl(p->sa[1]), sa2 = ufl(p->sa[2]);
+    const double L0 = ufl(p->L[0]), L1 = ufl(p->L[1]), L2 = ufl(p->L[2]);
+    const int m0 = ufl(p->m[0]), m1 = ufl(p->m[1]), m2 = ufl(p->m[2]);
+    const int n0 = ufl(p->cnt[0]), n01 = n0 + ufl(p->cnt[1]), ng = n01 + ufl(p->cnt[2]);
     const double rc = 1.0 / c;
     double* segt = gs + kGenPts;
     if (lane < 3) {
@@ -1832,9 +1840,9 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     }
     __builtin_amdgcn_wave_barrier();
     // serial generator (kPrepFallback past the stored points), resumed where steer_prep stopped
-    int gseg = p->fb_seg;
-    double gdd = p->fb_dd;
-    double gpd = p->fb_pd;
+    int gseg = ufl(p->fb_seg);
+    double gdd = ufl(p->fb_dd);
+    double gpd = ufl(p->fb_pd);
     long long grid = ng;  // grid points stored by steer_prep (0 or kPdCap for kPrepFallback)
     static_assert(kPdCap % 63 == 0, "stored points end on a chunk boundary");
     double carry_x = x, carry_y = y;
@@ -1979,7 +1987,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         carry_y = readlane_f64(qy, 63);
     }
     // no trailing zero left for the trim (dubins.rs:281-288): the literal path decides
-    if (partial && 1 + grid > p->n_point - 2) return kLiteral;
+    if (partial && 1 + grid > (long long)ufl((double)p->n_point) - 2) return kLiteral;
     return kAccept;
 }
 
@@ -3488,84 +3496,91 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
 // ------------------------------------------- persistent query batch (config 3, round 4)
 //
 // One launch runs every query of the batch to its target.  A workgroup owns `slots` queries at a
-// time (taken from a launch-wide counter: one atomic per query, not per task) and advances them
-// window by window inside the workgroup, the phases of a step separated by workgroup barriers:
-//   1. samples + exact NN   task t = (slot s, window slot k): iteration it_s + k of query q_s
-//                           (rand_point rrt.rs:139-146 on the query's stream; get_nearest_node
-//                           rrt.rs:378-391 in f64, lowest index on ties): kPqThreads / T threads
-//                           per task stride the query's rows, an LDS argmin merges them
-//   2. steer_prep           prep_task, 8 lanes per task, the PrepRec into LDS (never HBM)
-//   3. steer_walk           the waves draw the step's tasks from an LDS counter and walk the LDS
-//                           record (walk_rec; the scene image staged once per workgroup)
-//   4. insert               one wave per slot: literal re-runs, then mq_insert_kernel's in-order
-//                           replay — the window stops at the first iteration an accepted window
-//                           sample is strictly nearer to than its snapshot NN — and the append
-//                           (rrt.rs:586-589)
-// Every query's tree is exactly its one-iteration-at-a-time run (the same rule as the lockstep
-// kernels).  No step waits for another workgroup: a long path holds only its own workgroup's
-// step, the step costs no launch, and a cut costs the rest of the window, not a relaunch.
+// time (taken from a launch-wide counter: one atomic per query, not per task).  A slot's step —
+// one speculative window of K iterations of its query — is a chain of three phases:
+//   prep    steer_prep of the window's K tasks (prep_task, 8 lanes per task: ceil(K / 8) passes
+//           of 8 tasks), the PrepRecs into LDS (they never reach HBM)
+//   walk    steer_walk of the K tasks (walk_rec on the LDS record; the scene image is staged once
+//           per workgroup)
+//   serial  one wave: literal re-runs, the in-order replay of mq_insert_kernel — the window stops
+//           at the first iteration an accepted window sample is strictly nearer to than its
+//           snapshot NN — and the append (rrt.rs:586-589); the next query when this one reached
+//           its target; then the next window's samples (rand_point, rrt.rs:139-146, the query's
+//           stream) and their exact f64 nearest nodes (rrt.rs:378-391, lowest index on ties)
+// There is no workgroup barrier in the loop.  The waves are workers: each takes the next item —
+// a prep pass or a walk task — of any slot from that slot's LDS counter, and the wave that
+// finishes a phase's last item starts the slot's next phase (the serial one itself).  A long path
+// holds only its own slot's step while the other waves walk the other slots' tasks; a cut costs
+// the rest of the window, not a relaunch.
+//
+// Slot protocol (LDS): grab[s] = (epoch << 32) | items taken, one 64-bit atomic, so a worker learns
+// the phase and its item from the same atomic (epoch even: prep, odd: walk; kEpBusy: serial or
+// not started, kEpRetired: no query left); done[s] counts finished items, reset by the finisher
+// before it opens the next epoch.  Workgroup-scope fences order the records, verdicts and tree
+// rows between the waves (all on one CU).
+//
+// Every query's tree is exactly its one-iteration-at-a-time run (the lockstep kernels' rule).
 constexpr int kPqWaves = kPqThreads / 64;
-static_assert(kPqMaxSlots <= kPqWaves, "the insert runs one wave per slot");
-constexpr int kPqMinW = 4;            // waves per SIMD the register budget allows
+constexpr int kPqMinW = 4;  // waves per SIMD the register budget allows
+constexpr unsigned kEpBusy = 0xFFFFFFFEu, kEpRetired = 0xFFFFFFFFu;
 
-// The workgroup's LDS after the scene image and the waves' generator slots; T = slots * K <=
-// kPqMaxTasks window slots per step.
+// The workgroup's LDS after the scene image and the waves' generator slots: slot s's window is
+// tasks [s K, s K + K).
 struct PqLds {
     PrepRec rec[kPqMaxTasks];
     double tx[kPqMaxTasks], ty[kPqMaxTasks], td2[kPqMaxTasks];
-    double rd[kPqThreads];
-    int ri[kPqThreads];
     int tpn[kPqMaxTasks], tst[kPqMaxTasks];
+    unsigned long long grab[kPqMaxSlots];
     long long sit[kPqMaxSlots], stg[kPqMaxSlots];
-    int sq[kPqMaxSlots], sn[kPqMaxSlots];
-    int next, any;
+    int sq[kPqMaxSlots], sn[kPqMaxSlots], done[kPqMaxSlots];
+    int nretired;
 };
 __host__ __device__ inline int pq_lds_bytes(int scene_bytes) {
     return scene_bytes + kPqWaves * kGenSlots * 8 + (int)((sizeof(PqLds) + 15) & ~(size_t)15);
 }
 
-// The walk's record as wave-uniform values (SGPRs): an LDS record is read with ds_read into VGPRs,
-// ~60 of them for the ~30 fields the walk keeps live; readfirstlane moves each into SGPRs, as the
-// scalar loads of a global record do.
-__device__ __forceinline__ double ufl(double v) {
-    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
-                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
-}
-__device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ PrepRec uniform_rec(const PrepRec& r) {
-    PrepRec u;
-    u.x = ufl(r.x);
-    u.y = ufl(r.y);
-    u.px = ufl(r.px);
-    u.py = ufl(r.py);
-    u.yaw = ufl(r.yaw);
-    u.pyaw = ufl(r.pyaw);
-    u.c = ufl(r.c);
-    u.cw = ufl(r.cw);
-    u.sw = ufl(r.sw);
-    for (int i = 0; i < 3; ++i) {
-        u.ox[i] = ufl(r.ox[i]);
-        u.oy[i] = ufl(r.oy[i]);
-        u.ca[i] = ufl(r.ca[i]);
-        u.sa[i] = ufl(r.sa[i]);
-        u.L[i] = ufl(r.L[i]);
-        u.m[i] = ufl(r.m[i]);
-        u.cnt[i] = ufl(r.cnt[i]);
+// A prep pass out of line: prep_task's transcendental chains need ~160 VGPRs (the standalone
+// steer_prep kernel's allocation); inlined, they would set the whole kernel's budget.  Tasks
+// t0 .. t0 + 7 of the LDS task arrays, one per 8-lane group (all 64 lanes call prep_task); only
+// tasks below t_end are written.  prep_task reads only the step and the radius of the scene.
+__device__ __noinline__ void pq_prep(double step, double turn_radius, int lds_off,
+                                     const double* __restrict__ mx, const double* __restrict__ my,
+                                     const double* __restrict__ myaw, size_t row, int t0,
+                                     int t_end) {
+    PqLds& L = *reinterpret_cast<PqLds*>(pp_smem + lds_off);
+    SceneDev sc;
+    sc.step_size = step;
+    sc.turn_radius = turn_radius;
+    const int lane = threadIdx.x & 63;
+    const int t = t0 + lane / 8;
+    const bool in = t < t_end;
+    const int pn = in ? L.tpn[t] : -1;
+    const bool act = pn >= 0;
+    double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0;
+    if (in) {
+        x = L.tx[t];
+        y = L.ty[t];
     }
-    u.fb_pd = ufl(r.fb_pd);
-    u.fb_dd = ufl(r.fb_dd);
-    u.n_point = ((long long)ufl((int)(r.n_point >> 32)) << 32) |
-                (unsigned int)ufl((int)(r.n_point & 0xffffffff));
-    u.state = ufl(r.state);
-    u.fb_seg = ufl(r.fb_seg);
-    return u;
+    if (act) {
+        px = mx[row + pn];
+        py = my[row + pn];
+        pyaw = myaw[row + pn];
+    }
+    prep_task(sc, lane & 7, lane & ~7, t, in, act, x, y, px, py, pyaw, 0, 0.0, 0, 0.0, 0.0,
+              L.rec, nullptr, nullptr);
 }
 
 // the literal path out of line: it runs once in a few thousand steps, and inlined its registers
-// would set the whole kernel's budget
-__device__ __noinline__ int pq_literal(const SceneDev& sc, const PrepRec* R, double* bx) {
-    return steer_collide_literal(sc, R->x, R->y, R->yaw, R->px, R->py, R->pyaw, bx,
+// would set the whole kernel's budget.  The scene comes from its global-memory copy: a reference
+// to the kernel argument would make the compiler copy the whole argument block to the stack.
+__device__ __noinline__ int pq_literal(const SceneDev* __restrict__ sc, const PrepRec* R,
+                                       double* bx) {
+    return steer_collide_literal(*sc, R->x, R->y, R->yaw, R->px, R->py, R->pyaw, bx,
                                  bx + kLiteralCap, bx + 2 * kLiteralCap);
+}
+
+__device__ __forceinline__ unsigned long long lds_load_u64(const unsigned long long* p) {
+    return __atomic_load_n(p, __ATOMIC_RELAXED);
 }
 
 template <bool kLds, int kScene>
@@ -3574,149 +3589,33 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
     const SceneDev& sc = a.sc;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int K = mq.K, QS = a.slots, T = QS * K;
-    const int G = kPqThreads / T;  // NN threads per task (T is a power of two <= kPqMaxTasks)
+    const int K = mq.K, QS = a.slots;
+    const int npass = (K + 7) / 8;
     if (kLds) stage_scene(sc);
-    char* base = pp_smem + (kLds ? sc.lds_bytes : 0);
-    double* gs = reinterpret_cast<double*>(base) + wave * kGenSlots;
-    PqLds& L = *reinterpret_cast<PqLds*>(base + kPqWaves * kGenSlots * 8);
-    if (tid < kPqMaxSlots) L.sq[tid] = -1;
+    double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) + wave * kGenSlots;
+    const int lds_off = (kLds ? sc.lds_bytes : 0) + kPqWaves * kGenSlots * 8;
+    PqLds& L = *reinterpret_cast<PqLds*>(pp_smem + lds_off);
+    if (tid < kPqMaxSlots) {
+        L.grab[tid] = (unsigned long long)kEpBusy << 32;
+        L.done[tid] = 0;
+        L.sq[tid] = -1;
+    }
+    if (tid == 0) L.nretired = 0;
     __syncthreads();
     long long npts = 0, napts = 0, qsteps = 0;
-    long long cyc[5] = {0, 0, 0, 0, 0};  // thread 0, profiling: refill, NN, prep, walk, insert
+    long long cyc[4] = {0, 0, 0, 0};  // this wave: serial, prep, walk, idle (profiling)
     const bool prof = a.tally != nullptr;
-    long long c0 = prof ? (long long)clock64() : 0;
-    auto stamp = [&](int ph) {
-        if (prof && tid == 0) {
-            const long long c1 = (long long)clock64();
-            cyc[ph] += c1 - c0;
-            c0 = c1;
-        }
-    };
-    for (;;) {
-        // 0. refill: a slot whose query reached its target takes the next query that has work
-        //    (-2: the counter is exhausted, never ask again)
-        if (tid < QS) {
-            int q = L.sq[tid];
-            if (q == -1 || (q >= 0 && L.sit[tid] >= L.stg[tid])) {
-                for (;;) {
-                    q = atomicAdd(a.qnext, 1);
-                    if (q >= mq.Q) {
-                        q = -2;
-                        break;
-                    }
-                    const long long it = mq.it[q], tg = mq.target[q];
-                    if (it < tg) {
-                        L.sn[tid] = mq.n[q];
-                        L.sit[tid] = it;
-                        L.stg[tid] = tg;
-                        break;
-                    }
-                }
-                L.sq[tid] = q;
-            }
-        }
-        if (tid == 0) L.next = 0;
-        __syncthreads();
-        int any = 0;
-        for (int s = 0; s < QS; ++s) any |= L.sq[s] >= 0 ? 1 : 0;
-        if (!any) break;
-        if (tid == 0)
-            for (int s = 0; s < QS; ++s) qsteps += L.sq[s] >= 0 ? 1 : 0;
-        stamp(0);
-        // 1. samples and the exact nearest node of each (thread tid: task tid % T, rows i = g mod G)
-        {
-            const int t = tid % T, g = tid / T;
-            const int s = t / K, k = t - s * K;
+
+    // the serial phase of slot s on this wave: insert the finished window (when `insert`), the
+    // next query when this one is done, the next window's samples and nearest nodes, then open
+    // the prep epoch `ep` (or retire the slot)
+    auto serial = [&](int s, bool insert, unsigned ep) {
+        const int base = s * K;
+        if (insert) {
             const int q = L.sq[s];
-            double x = 0.0, y = 0.0, bd = __builtin_inf();
-            int bi = 0x7fffffff;
-            bool live = false;
-            if (q >= 0) {
-                const long long it = L.sit[s] + k;
-                live = it < L.stg[s];
-                if (live) {
-                    const uint64_t seed = mq.seed[q];
-                    x = gen_range(seed, 2 * (uint64_t)it, sc.minx, sc.maxx);
-                    y = gen_range(seed, 2 * (uint64_t)it + 1, sc.miny, sc.maxy);
-                    const size_t row = (size_t)q * mq.cap;
-                    const double* __restrict__ X = mq.x + row;
-                    const double* __restrict__ Y = mq.y + row;
-                    const int n = L.sn[s];
-#pragma unroll 4
-                    for (int i = g; i < n; i += G) {
-                        const double dx = x - X[i], dy = y - Y[i];
-                        const double d2 = dx * dx + dy * dy;
-                        if (d2 < bd) {
-                            bd = d2;
-                            bi = i;
-                        }
-                    }
-                }
-            }
-            L.rd[tid] = bd;
-            L.ri[tid] = bi;
-            if (g == 0) {
-                L.tx[t] = x;
-                L.ty[t] = y;
-                L.tpn[t] = live ? 0 : -1;
-            }
-        }
-        __syncthreads();
-        if (tid < T) {
-            double bd = L.rd[tid];
-            int bi = L.ri[tid];
-            for (int g = 1; g < G; ++g) argmin_pair(bd, bi, L.rd[tid + g * T], L.ri[tid + g * T]);
-            if (L.tpn[tid] >= 0) {
-                L.tpn[tid] = bi;
-                L.td2[tid] = bd;
-            }
-        }
-        __syncthreads();
-        stamp(1);
-        // 2. steer_prep: 8 lanes per task (every lane of every wave calls prep_task)
-        for (int b0 = 0; b0 < T; b0 += kPqThreads / 8) {
-            const int t = b0 + tid / 8;
-            const bool in = t < T;
-            const int pn = in ? L.tpn[t] : -1;
-            const bool act = pn >= 0;
-            double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0;
-            if (in) {
-                x = L.tx[t];
-                y = L.ty[t];
-            }
-            if (act) {
-                const size_t o = (size_t)L.sq[t / K] * mq.cap + pn;
-                px = mq.x[o];
-                py = mq.y[o];
-                pyaw = mq.yaw[o];
-            }
-            prep_task(sc, tid & 7, lane & ~7, t, in, act, x, y, px, py, pyaw, 0, 0.0, 0, 0.0, 0.0,
-                      L.rec, nullptr, nullptr);
-        }
-        __syncthreads();
-        stamp(2);
-        // 3. steer_walk: one task at a time per wave from the LDS counter
-        for (;;) {
-            int k = 0;
-            if (lane == 0) k = atomicAdd(&L.next, 1);
-            const int t = __builtin_amdgcn_readlane(k, 0);
-            if (t >= T) break;
-            int np = 0, na = 0;
-            const PrepRec R = uniform_rec(L.rec[t]);
-            const int st = walk_rec<kLds, kScene>(sc, &R, nullptr, gs, np, na);
-            if (lane == 0) L.tst[t] = st;
-            npts += np;
-            napts += na;
-        }
-        __syncthreads();
-        stamp(3);
-        // 4. insert: wave s replays slot s's window in order (lane k: window slot k)
-        if (wave < QS && L.sq[wave] >= 0) {
-            const int s = wave, q = L.sq[s];
             const int k = lane;
             const bool inw = k < K;
-            const int t = s * K + k;
+            const int t = base + k;
             int st = kReject, pn = -1;
             double x = 0.0, y = 0.0, yw = 0.0, d2nn = 0.0;
             if (inw) {
@@ -3733,7 +3632,7 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
                 double* bx = a.lit_scratch + (size_t)slot * 3 * kLiteralCap;
                 for (; lit; lit &= lit - 1) {
                     const int l = __builtin_ctzll(lit);
-                    const int r = pq_literal(sc, &L.rec[s * K + l], bx);
+                    const int r = pq_literal(a.sc_global, &L.rec[base + l], bx);
                     if (lane == l) st = r;
                 }
                 lit_release(a.lit_locks, slot);
@@ -3779,19 +3678,171 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
                     mq.evals[q] += ev;
                 }
             }
+            ++qsteps;
+            __threadfence_block();  // this wave's LDS and tree-row writes before the reads below
         }
-        __syncthreads();
-        stamp(4);
+        // the next query when this one reached its target (lane 0; the counter hands out each
+        // query once)
+        int q = L.sq[s];
+        if (q == -1 || L.sit[s] >= L.stg[s]) {
+            if (lane == 0) {
+                for (;;) {
+                    q = atomicAdd(a.qnext, 1);
+                    if (q >= mq.Q) {
+                        q = -2;
+                        break;
+                    }
+                    const long long it = mq.it[q], tg = mq.target[q];
+                    if (it < tg) {
+                        L.sn[s] = mq.n[q];
+                        L.sit[s] = it;
+                        L.stg[s] = tg;
+                        break;
+                    }
+                }
+                L.sq[s] = q;
+            }
+            q = __shfl(q, 0);
+            __threadfence_block();
+        }
+        if (q < 0) {  // no query left: retire the slot
+            if (lane == 0) {
+                L.grab[s] = (unsigned long long)kEpRetired << 32;
+                atomicAdd(&L.nretired, 1);
+            }
+            return;
+        }
+        // the next window: lane l serves window slot k = l mod K over rows i = l / K mod 64 / K
+        {
+            const int G = 64 / K;
+            const int k = lane & (K - 1), g = lane / K;
+            const long long it = L.sit[s] + k;
+            const bool live = it < L.stg[s];
+            const uint64_t seed = mq.seed[q];
+            double x = 0.0, y = 0.0, bd = __builtin_inf();
+            int bi = 0x7fffffff;
+            if (live) {
+                x = gen_range(seed, 2 * (uint64_t)it, sc.minx, sc.maxx);
+                y = gen_range(seed, 2 * (uint64_t)it + 1, sc.miny, sc.maxy);
+                const size_t row = (size_t)q * mq.cap;
+                const double* __restrict__ X = mq.x + row;
+                const double* __restrict__ Y = mq.y + row;
+                const int n = L.sn[s];
+#pragma unroll 4
+                for (int i = g; i < n; i += G) {
+                    const double dx = x - X[i], dy = y - Y[i];
+                    const double d2 = dx * dx + dy * dy;
+                    if (d2 < bd) {
+                        bd = d2;
+                        bi = i;
+                    }
+                }
+            }
+            for (int m = K; m < 64; m <<= 1) {  // the G lanes of window slot k
+                if (m == 16)
+                    argmin_swap<false>(bd, bi);
+                else if (m == 32)
+                    argmin_swap<true>(bd, bi);
+                else
+                    argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+            }
+            if (g == 0) {
+                L.tx[base + k] = x;
+                L.ty[base + k] = y;
+                L.tpn[base + k] = live ? bi : -1;
+                L.td2[base + k] = bd;
+            }
+        }
+        __threadfence_block();
+        if (lane == 0) {
+            L.done[s] = 0;
+            __threadfence_block();
+            atomicExch(&L.grab[s], (unsigned long long)ep << 32);  // open the prep epoch
+        }
+    };
+
+    long long c0 = prof ? (long long)wall_clock64() : 0;
+    auto stamp = [&](int ph) {
+        if (prof) {
+            const long long c1 = (long long)wall_clock64();
+            cyc[ph] += c1 - c0;
+            c0 = c1;
+        }
+    };
+    if (wave < QS) {  // every slot's first query and window
+        serial(wave, false, 0u);
+        stamp(0);
     }
-    if (prof) {  // [0] query-steps, [1] walked points, [2] their arc points, [3..7] phase cycles
+    for (int rr = 0;; ++rr) {
+        // an item of any slot, starting at this wave's own slot
+        int s = -1, item = 0;
+        unsigned ep = 0;
+        for (int i = 0; i < QS && s < 0; ++i) {
+            const int c = (wave + rr + i) % QS;
+            const unsigned long long v = lds_load_u64(&L.grab[c]);
+            const unsigned e = (unsigned)(v >> 32);
+            if (e >= kEpBusy) continue;
+            const unsigned lim = (e & 1u) ? (unsigned)K : (unsigned)npass;
+            if ((unsigned)v >= lim) continue;  // every item of the phase is taken
+            unsigned long long old = 0;
+            if (lane == 0) old = atomicAdd(&L.grab[c], 1ull);
+            old = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(old >> 32)) << 32) |
+                  (unsigned)__builtin_amdgcn_readfirstlane((int)old);
+            const unsigned e2 = (unsigned)(old >> 32);
+            if (e2 >= kEpBusy) continue;
+            const unsigned lim2 = (e2 & 1u) ? (unsigned)K : (unsigned)npass;
+            if ((unsigned)old < lim2) {
+                s = c;
+                item = (int)(unsigned)old;
+                ep = e2;
+            }
+        }
+        if (s < 0) {
+            if (__atomic_load_n(&L.nretired, __ATOMIC_RELAXED) >= QS) break;
+            __builtin_amdgcn_s_sleep(2);
+            stamp(3);
+            continue;
+        }
+        __threadfence_block();  // the phase's inputs (records, samples) were published before
+        const int base = s * K;
+        const bool walk = ep & 1u;
+        if (walk) {
+            int np = 0, na = 0;
+            const int st = walk_rec<kLds, kScene>(sc, &L.rec[base + item], nullptr, gs, np, na);
+            if (lane == 0) L.tst[base + item] = st;
+            npts += np;
+            napts += na;
+            stamp(2);
+        } else {
+            pq_prep(sc.step_size, sc.turn_radius, lds_off, mq.x, mq.y, mq.yaw,
+                    (size_t)L.sq[s] * mq.cap, base + 8 * item, base + K);
+            stamp(1);
+        }
+        __threadfence_block();  // this item's results before it counts as done
+        int d = 0;
+        if (lane == 0) d = atomicAdd(&L.done[s], 1);
+        d = __builtin_amdgcn_readfirstlane(d);
+        if (d != (walk ? K : npass) - 1) continue;
+        // the phase's last item: this wave opens the slot's next phase
+        if (!walk) {
+            if (lane == 0) {
+                L.done[s] = 0;
+                __threadfence_block();
+                atomicExch(&L.grab[s], (unsigned long long)(ep + 1) << 32);  // the walk epoch
+            }
+        } else {
+            if (lane == 0) L.grab[s] = (unsigned long long)kEpBusy << 32;
+            serial(s, true, ep + 1 >= kEpBusy - 1 ? 0u : ep + 1);
+            stamp(0);
+        }
+    }
+    if (prof) {  // [0] query-steps, [1] walked points, [2] their arc points, [3..6] wave time
         unsigned long long* tl = reinterpret_cast<unsigned long long*>(a.tally);
         if (lane == 0) {
+            atomicAdd(&tl[0], (unsigned long long)qsteps);
             atomicAdd(&tl[1], (unsigned long long)npts);
             atomicAdd(&tl[2], (unsigned long long)napts);
-        }
-        if (tid == 0) {
-            atomicAdd(&tl[0], (unsigned long long)qsteps);
-            for (int p = 0; p < 5; ++p) atomicAdd(&tl[3 + p], (unsigned long long)cyc[p]);
+            for (int p = 0; p < 4; ++p) atomicAdd(&tl[3 + p], (unsigned long long)cyc[p]);
         }
     }
 }
@@ -3836,10 +3887,12 @@ int pq_grid_cap(const SceneDev& sc) {
     return cap;
 }
 
+int pq_grid_cap_host(const SceneDev& sc) { return pq_grid_cap(sc); }
+
 hipError_t launch_mq_persist(hipStream_t s, const PqArgs& a) {
     const int K = a.mq.K;
-    if (K < 1 || (K & (K - 1)) || a.slots < 1 || a.slots > kPqMaxSlots ||
-        a.slots * K > kPqMaxTasks || (a.slots & (a.slots - 1)))
+    if (K < 1 || K > 64 || (K & (K - 1)) || a.slots < 1 || a.slots > kPqMaxSlots ||
+        a.slots * K > kPqMaxTasks)
         return hipErrorInvalidValue;
     const int grid = std::min((a.mq.Q + a.slots - 1) / a.slots, pq_grid_cap(a.sc));
     return pq_kernel_for(a.sc, [&](auto kern) {
