@@ -410,7 +410,7 @@ def make_planner(raw, seed, window, device, capacity=1 << 18):
 
 
 STAT_KEYS = ("iterations", "accepted", "windows", "truncations", "repair_rounds", "repairs",
-             "literal_repairs", "nn_flagged")
+             "literal_repairs", "nn_flagged", "samples_blocked")
 
 
 def timed_windows(p, n_windows, window):
@@ -672,6 +672,10 @@ def run_batch(args, D, star, with_cpu):
     if persistent:
         res["schedule"] = "persistent (one launch: every workgroup steps its own queries)"
         res["phase_share"] = phases
+        res["window_slots"] = {"evaluated": int(sp.get("samples_evaluated", 0)),
+                               "sample_in_obstacle": int(sp.get("samples_blocked", 0)),
+                               "note": "slots whose sample lies in an obstacle are rejected "
+                                       "whatever the parent: no steer_prep / steer_walk, no cut"}
     elif not star:
         launches = max(sp["nn_scan_launches"], 1)
         res["schedule"] = "lockstep (four launches per step, two sub-batch streams)"

@@ -94,6 +94,10 @@ typedef struct pp_stats {
     int64_t persist_cycles[5];  /* its waves' time (wall_clock64 ticks, 100 MHz, summed over the
                                    waves; profiling on): serial items (insert, next query, samples
                                    + nearest nodes), steer_prep passes, steer_walk tasks, idle, 0 */
+    int64_t samples_evaluated;  /* extend samples evaluated (one tree: the iterations; the persistent
+                                   batch: its window slots) */
+    int64_t samples_blocked;    /* ... of them whose point lies in an obstacle: rejected whatever
+                                   the parent, without steer_prep / steer_walk or a pair list */
 } pp_stats;
 
 int pp_abi_version(void);

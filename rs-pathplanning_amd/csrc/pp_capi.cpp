@@ -155,6 +155,8 @@ struct pp_ctx {
     DBuf<PrepRec> rec;   // per-task steer records
     DBuf<double> pdbuf;  // per-task grid-point distances (kPdCap per task)
     DBuf<int> r_order, r_rep, pend, fin_par;
+    DBuf<unsigned char> blk;   // [2 Kcap] window samples in an obstacle (point_blocked)
+    DBuf<SceneDev> d_scene;    // the scene in device memory (samples_role, the literal paths)
     DBuf<double> r_repyaw;
     DBuf<double> lit_scratch;  // resolve: one literal buffer per wave
     // verify_node API
@@ -189,7 +191,7 @@ struct pp_ctx {
     hipStream_t sub_stream[4] = {};  // sub-batch streams 1.. (0 is `stream`), created on first use
     int mq_sched = PP_BATCH_PERSISTENT;  // pp_batch_set_schedule
     DBuf<int> pq_next;                   // the persistent kernel's query counter
-    DBuf<long long> pq_tally;            // its tally (PqArgs::tally): 8 counters
+    DBuf<long long> pq_tally;            // its tally (PqArgs::tally): kPqTally counters
     DBuf<SceneDev> pq_scene;             // the scene in device memory (PqArgs::sc_global)
     hipEvent_t fork_ev = nullptr;
     std::vector<double> mq_goal;  // 3 per query (RRT::new's goal; pp_batch_plan)
@@ -378,6 +380,8 @@ struct pp_ctx {
         a.rs.repyaw = r_repyaw.p;
         a.lit_scratch = lit_scratch.p;
         a.wg_points = prof_points();
+        a.scp = d_scene.p;
+        a.blk = d_scene.p ? blk.p : nullptr;
         return a;
     }
 };
@@ -426,6 +430,7 @@ int ensure_window(pp_ctx* c, int K) {
     PP_HIP(c->r_rep.reserve(k));
     PP_HIP(c->pend.reserve(k));
     PP_HIP(c->fin_par.reserve(k));
+    PP_HIP(c->blk.reserve(2 * k));
     PP_HIP(hipMemsetAsync(c->cand_cnt.p, 0, k * sizeof(int), c->stream));
     PP_HIP(c->r_repyaw.reserve(k));
     PP_HIP(c->tasks.reserve(k));
@@ -1344,6 +1349,11 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
     const int64_t target = ctx->it + n_iter;
     const int64_t n_before = ctx->n;
     hipStream_t st = ctx->stream;
+    {  // the scene in device memory for samples_role's point_blocked pre-test
+        if (!ctx->d_scene.p) PP_HIP(ctx->d_scene.reserve(1));
+        const SceneDev sd = ctx->scene_dev();
+        PP_HIP(hipMemcpy(ctx->d_scene.p, &sd, sizeof sd, hipMemcpyHostToDevice));
+    }
     while (ctx->it < target) {
         const int K = ctx->K;
         // windows draw min(K, kdyn) samples (the device adapts kdyn): enough windows for that
@@ -1836,8 +1846,8 @@ int batch_extend_persistent(pp_ctx* ctx, const MqArgs& a) {
     hipStream_t st = ctx->stream;
     if (!ctx->pq_next.p) PP_HIP(ctx->pq_next.reserve(1));
     if (!ctx->pq_tally.p) {
-        PP_HIP(ctx->pq_tally.reserve(8));
-        PP_HIP(hipMemsetAsync(ctx->pq_tally.p, 0, 8 * sizeof(long long), st));
+        PP_HIP(ctx->pq_tally.reserve(kPqTally));
+        PP_HIP(hipMemsetAsync(ctx->pq_tally.p, 0, kPqTally * sizeof(long long), st));
     }
     PP_HIP(hipMemsetAsync(ctx->pq_next.p, 0, sizeof(int), st));
     if (!ctx->pq_scene.p) PP_HIP(ctx->pq_scene.reserve(1));
@@ -2278,6 +2288,8 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out, uint64_t out_size) {
         s.literal_repairs = d.literal_repairs;
         s.nn_flagged = d.nn_flagged;
         s.node_evals = d.node_evals;
+        s.samples_evaluated = d.iterations;
+        s.samples_blocked = d.blocked;
     }
     s.nn_scan_ms = ctx->nn_scan_ms;
     s.nn_scan_launches = ctx->nn_scan_launches;
@@ -2308,13 +2320,15 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out, uint64_t out_size) {
     s.persist_ms = ctx->persist_ms;
     s.persist_launches = ctx->persist_launches;
     if (ctx->pq_tally.p) {  // the persistent batch kernel: query-steps, points, phase cycles
-        long long t[8];
+        long long t[kPqTally];
         PP_HIP(hipMemcpyAsync(t, ctx->pq_tally.p, sizeof t, hipMemcpyDeviceToHost, ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
         s.batch_query_steps = t[0];
         s.walk_points += t[1];
         s.walk_arc_points += t[2];
         for (int p = 0; p < 5; ++p) s.persist_cycles[p] = t[3 + p];
+        s.samples_evaluated += t[8];
+        s.samples_blocked += t[9];
     }
     std::memcpy(out, &s, (size_t)std::min<uint64_t>(out_size, sizeof s));
     return PP_OK;
@@ -2328,7 +2342,7 @@ int pp_rrt_reset_stats(pp_ctx* ctx) {
         PP_HIP(hipStreamSynchronize(ctx->stream));
         DevState d = ctx->h_state.p[0];
         d.iterations = d.accepted = d.windows = d.truncations = d.repair_rounds = d.repairs =
-            d.literal_repairs = d.nn_flagged = d.node_evals = 0;
+            d.literal_repairs = d.nn_flagged = d.node_evals = d.blocked = 0;
         ctx->h_state.p[0] = d;
         PP_HIP(hipMemcpyAsync(ctx->d_state.p, ctx->h_state.p, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));

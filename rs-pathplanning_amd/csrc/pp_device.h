@@ -156,7 +156,9 @@ struct Steer {
 
 // dubins.rs:333-363: evaluate LSL, RSR, LSR, RSL, RLR, LRL in order and keep the first strict
 // minimum of |t|+|p|+|q|.  All lanes compute the same (wave-uniform) values.
-__device__ inline Steer select_word(double lex, double ley, double leyaw, double c) {
+// (select_word_fi / interp_local_fi: always inlined, for a literal path that must take its
+// caller's register budget; the plain names are ordinary inline functions)
+__device__ __forceinline__ Steer select_word_fi(double lex, double ley, double leyaw, double c) {
     const double hyp = hypot(lex, ley);
     const double d = hyp * c;
     const double theta = mod2pi(atan2(ley, lex));
@@ -188,13 +190,17 @@ __device__ inline Steer select_word(double lex, double ley, double leyaw, double
     s.cost = bcost;
     return s;
 }
+__device__ inline Steer select_word(double lex, double ley, double leyaw, double c) {
+    return select_word_fi(lex, ley, leyaw, c);
+}
 
 struct Pose {
     double x, y, yaw;
 };
 
 // dubins.rs:155-198 (x, y, yaw of one sample; directions are not part of the output)
-__device__ inline Pose interp_local(int mode, double length, double max_curvature, Pose o) {
+__device__ __forceinline__ Pose interp_local_fi(int mode, double length, double max_curvature,
+                                                Pose o) {
     Pose r;
     if (mode == kModeS) {
         r.x = o.x + length / max_curvature * cos(o.yaw);
@@ -219,14 +225,18 @@ __device__ inline Pose interp_local(int mode, double length, double max_curvatur
         r.yaw = o.yaw - length;
     return r;
 }
+__device__ inline Pose interp_local(int mode, double length, double max_curvature, Pose o) {
+    return interp_local_fi(mode, length, max_curvature, o);
+}
 
 // Literal single-thread restatement of dubins_path_planning_from_origin (dubins.rs:326-399): the
 // LOCAL points after generate_local_course's trim, yaw as generated (not wrapped).  Returns
 // kSteerSome / kSteerNone / kSteerOverflow (cap < n_point or the Rust index panic).
+template <bool kFI = false>
 __device__ inline int dubins_local(double lex, double ley, double leyaw, double c, double step_size,
                                    double* px, double* py, double* pyaw, int cap, int* n_out,
                                    int* word_out, double* cost_out) {
-    const Steer s = select_word(lex, ley, leyaw, c);
+    const Steer s = kFI ? select_word_fi(lex, ley, leyaw, c) : select_word(lex, ley, leyaw, c);
     if (s.word < 0) return kSteerNone;
     const double lengths[3] = {s.t, s.p, s.q};
     double total = 0.0;
@@ -251,7 +261,7 @@ __device__ inline int dubins_local(double lex, double ley, double leyaw, double 
         while (fabs(pd) <= fabs(l)) {
             ind += 1;
             if (ind >= n_point) return kSteerOverflow;
-            Pose r = interp_local(m, pd, c, o);
+            Pose r = kFI ? interp_local_fi(m, pd, c, o) : interp_local(m, pd, c, o);
             px[ind] = r.x;
             py[ind] = r.y;
             pyaw[ind] = r.yaw;
@@ -260,7 +270,7 @@ __device__ inline int dubins_local(double lex, double ley, double leyaw, double 
         ll = l - pd - d;
         ind += 1;
         if (ind >= n_point) return kSteerOverflow;
-        Pose r = interp_local(m, l, c, o);
+        Pose r = kFI ? interp_local_fi(m, l, c, o) : interp_local(m, l, c, o);
         px[ind] = r.x;
         py[ind] = r.y;
         pyaw[ind] = r.yaw;
@@ -281,6 +291,7 @@ __device__ inline int dubins_local(double lex, double ley, double leyaw, double 
 // Literal single-thread restatement of dubins_path_planning (dubins.rs:401-428) writing WORLD
 // points: the slow path for the measure-zero trim cases, and the pp_dubins_batch API.
 // Returns kSteerSome / kSteerNone / kSteerOverflow (cap < n_point or the Rust index panic).
+template <bool kFI = false>
 __device__ inline int dubins_literal(double sx, double sy, double syaw, double ex0, double ey0,
                                      double eyaw, double turn_radius, double step_size, double* px,
                                      double* py, double* pyaw, int cap, int* n_out, int* word_out,
@@ -291,7 +302,7 @@ __device__ inline int dubins_literal(double sx, double sy, double syaw, double e
     const double ley = -(sin(syaw)) * ex + cos(syaw) * ey;
     const double leyaw = eyaw - syaw;
     int len = 0;
-    const int r = dubins_local(lex, ley, leyaw, c, step_size, px, py, pyaw, cap, &len, word_out,
+    const int r = dubins_local<kFI>(lex, ley, leyaw, c, step_size, px, py, pyaw, cap, &len, word_out,
                                cost_out);
     if (r != kSteerSome) return r;
     // back to the world frame, dubins.rs:412-422

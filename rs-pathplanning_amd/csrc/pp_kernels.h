@@ -46,6 +46,8 @@ struct WindowArgs {
     ResolveScratch rs{};
     double* lit_scratch = nullptr;
     long long* wg_points = nullptr;  // profiling: walked points per walk workgroup (or null)
+    const SceneDev* scp = nullptr;  // the scene in device memory (samples_role's point_blocked)
+    unsigned char* blk = nullptr;   // [2 * Kcap] sample in an obstacle (null: no pre-test)
 };
 
 // Enqueue window number `seq` on stream s: its window kernel also resolves and commits window
@@ -136,6 +138,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps);
 constexpr int kPqMaxTasks = 128;
 constexpr int kPqThreads = 512;   // 8 waves per workgroup
 constexpr int kPqMaxSlots = 8;    // queries per workgroup (the insert: one wave each)
+constexpr int kPqTally = 10;
 struct PqArgs {
     MqDev mq{};
     SceneDev sc{};
@@ -145,9 +148,10 @@ struct PqArgs {
     double* lit_scratch = nullptr;  // kLiteralWaves buffers
     int* lit_locks = nullptr;
     int* err = nullptr;
-    long long* tally = nullptr;  // profiling (or null): query-steps, walked points, arc points,
-                                 // then the waves' time (wall_clock64 ticks, 100 MHz) in the
-                                 // serial phases, prep passes, walk tasks and idle: 8 int64
+    long long* tally = nullptr;  // profiling (or null), kPqTally int64: query-steps, walked points,
+                                 // arc points, the waves' time (wall_clock64 ticks, 100 MHz) in
+                                 // the serial phases, prep passes, walk tasks and idle, 0, window
+                                 // slots evaluated, of them decided by point_blocked
 };
 hipError_t launch_mq_persist(hipStream_t s, const PqArgs& a);
 // resident workgroups of the persistent kernel for a scene (occupancy API)

@@ -229,6 +229,33 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     return false;
 }
 
+// Point 0 of a candidate's line — the sample itself — inside an obstacle: the line is rejected
+// whatever its parent and its Dubins path (verify, rrt.rs:124-137: the first segment starts inside
+// the disc / on an occupied cell), so the candidate needs neither steer_prep nor steer_walk and its
+// verdict cannot depend on which node is its parent.  Discs: the disc grid's cell of the point
+// (every disc is listed in each cell its cull box touches), clearly inside only — d2 below r2 by a
+// relative 1e-9, far beyond the rounding of the walk's exact segment test, which therefore finds
+// the same hit; the grid mode probes the very bit the walk probes.  Polygon scenes: no pre-test.
+template <bool kLds, int kScene>
+__device__ __forceinline__ bool point_blocked(const SceneDev& sc, double x, double y) {
+    if (kScene == kSceneGrid || (kScene == kSceneAny && sc.bits)) {
+        const uint32_t* B = kLds ? reinterpret_cast<const uint32_t*>(pp_smem) : sc.bits;
+        return grid_occupied(B, sc.bw, sc.bh, sc.bwords, sc.bx0, sc.by0, sc.binv, x, y);
+    }
+    if (kScene == kScenePoly || (kScene == kSceneAny && (sc.ne > 0 || sc.nbv > 0)) || sc.m == 0)
+        return false;
+    const int* goff = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_goff) : sc.goff;
+    const int* items = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_items) : sc.gitems;
+    const int cell = grid_cell(y, sc.gy0, sc.ginv, sc.gny) * sc.gnx + grid_cell(x, sc.gx0, sc.ginv, sc.gnx);
+    const int k1 = goff[cell + 1];
+    for (int k = goff[cell]; k < k1; ++k) {
+        const int d = items[k];
+        const double dx = x - sc.cx[d], dy = y - sc.cy[d];
+        if (dx * dx + dy * dy < sc.r2[d] * (1.0 - 1.0e-9)) return true;
+    }
+    return false;
+}
+
 // Fast path of verify_node for the edge child (x, y, yaw) → parent (px, py, pyaw): the Dubins
 // polyline of line_to_origin (rrt.rs:295-315) plus the junction to the parent, whose own line
 // was verified when it was inserted.  Split in two:
@@ -442,15 +469,17 @@ __device__ int steer_collide_fast(const SceneDev& sc, double x, double y, double
 // check_finish meets it on optimize's self-connections (a node's copy into the node itself): the
 // serial test held a scratch slot of the shared pool for a whole scene scan, and hundreds of waves
 // queued for the slots.
-__device__ int steer_collide_literal(const SceneDev& sc, double x, double y, double yaw, double px,
-                                     double py, double pyaw, double* bx, double* by, double* byaw,
-                                     bool junction = true) {
+template <bool kFI>
+__device__ __forceinline__ int steer_collide_literal_body(const SceneDev& sc, double x, double y,
+                                                          double yaw, double px, double py,
+                                                          double pyaw, double* bx, double* by,
+                                                          double* byaw, bool junction) {
     const int lane = threadIdx.x & 63;
     int n = 0, r = 0;
     if (lane == 0) {
         int word = -1;
         double cost = 0.0;
-        r = dubins_literal(x, y, yaw, px, py, pyaw, sc.turn_radius, sc.step_size, bx, by, byaw,
+        r = dubins_literal<kFI>(x, y, yaw, px, py, pyaw, sc.turn_radius, sc.step_size, bx, by, byaw,
                            kLiteralCap - 1, &n, &word, &cost);
         if (r != kSteerOverflow) {
             if (r == kSteerNone) {
@@ -475,6 +504,11 @@ __device__ int steer_collide_literal(const SceneDev& sc, double x, double y, dou
             return kReject;
     }
     return kAccept;
+}
+__device__ int steer_collide_literal(const SceneDev& sc, double x, double y, double yaw, double px,
+                                     double py, double pyaw, double* bx, double* by, double* byaw,
+                                     bool junction = true) {
+    return steer_collide_literal_body<false>(sc, x, y, yaw, px, py, pyaw, bx, by, byaw, junction);
 }
 
 // Explicit tasks (the verify_node API); waves <= kLiteralWaves so each wave owns one literal
@@ -680,6 +714,8 @@ struct SamplesArgs {
     float2* ob[2];    // [K / kQPB] the screen block's centre o (f32) of each kQPB sorted samples
     double* sq[2];    // sample -> |q - o|^2 about its block's centre (f64, exact)
     int* ipos[2];     // sample -> sorted position (the screen's partials are stored by position)
+    const SceneDev* scp = nullptr;       // the scene in device memory (point_blocked)
+    unsigned char* blk[2] = {nullptr, nullptr};  // sample -> its point lies in an obstacle
 };
 
 __device__ inline int morton16(int x, int y) {
@@ -717,6 +753,7 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
         g.wsy[np][j] = y;
         g.wsx32[np][j] = (float)x;
         g.wsy32[np][j] = (float)y;
+        if (g.blk[np]) g.blk[np][j] = point_blocked<false, kSceneAny>(*g.scp, x, y) ? 1 : 0;
         const int cx = min(max((int)((x - g.minx) * fx), 0), 15);  // == sample_cell
         const int cy = min(max((int)((y - g.miny) * fy), 0), 15);
         const int cell = morton16(cx, cy);
@@ -1207,7 +1244,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
     double* __restrict__ out_d2, double* __restrict__ out_pose, PairGrid pg,
     int* __restrict__ cand_cnt, CandEntry* __restrict__ cand,
     int* __restrict__ pend, const double* __restrict__ sq, const int* __restrict__ ipos,
-    SamplesArgs gen, int gen_next) {
+    SamplesArgs gen, int gen_next, const unsigned char* __restrict__ blk) {
     __shared__ double s_nd2[kFinSamples];  // exact snapshot NN d2 of each sample
     __shared__ int s_pc[kFinSamples];      // pair search: nearer window samples found
     __shared__ int s_pi[kFinSamples][kCandCap];
@@ -1243,7 +1280,10 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int q = q0 + wave;
-    const bool in = q < W;
+    // a sample in an obstacle is rejected whatever its parent: no nearest node, no pair list, and
+    // it is nobody's candidate parent (samples_role's point_blocked)
+    const bool qblk = blk && q < W && blk[q];
+    const bool in = q < W && !qblk;
     const int D = n - ns, Dl = min(D, kFinDelta);  // appended nodes (staged: the first kFinDelta)
     for (int k = tid; k < Dl; k += kFinThreads) s_dn[k] = make_float2(x32[ns + k], y32[ns + k]);
     if (tid < kFinSamples) s_pc[tid] = 0;
@@ -1423,7 +1463,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
         // wave w: sample j = q0 + w against the window samples i < j of the Morton cells its
         // disc of radius sqrt(D2) touches (the binning is monotone, so the cells are a superset)
         const int j = q0 + wave;
-        if (j < W) {
+        if (j < W && !qblk) {
             const double xj = qx[j], yj = qy[j];
             const float xjf = (float)xj, yjf = (float)yj;
             const double D2 = s_nd2[wave];
@@ -1440,7 +1480,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
                         const float2 v = pg.sxy[pos];
                         if (!(scan_d2(xjf, yjf, v.x, v.y) <= thr)) continue;
                         const int ii = pg.perm[pos];
-                        if (ii >= j) continue;
+                        if (ii >= j || (blk && blk[ii])) continue;
                         const double dx = xj - qx[ii], dy = yj - qy[ii];
                         const double d2 = dx * dx + dy * dy;
                         if (d2 < D2) {  // strictly nearer than the snapshot NN (which wins ties)
@@ -1476,6 +1516,10 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
             cand[eb + k] = CandEntry{j, s_pi[lane][k], s_pd[lane][k], 0.0, -1, 0};
         if (cnt > 0) pend[pb] = j;
         if (lane == 0 && ov) atomicMin(&st->weff, q0 + (int)__builtin_ctzll(ov));
+        if (blk) {  // statistics (pp_stats.samples_blocked): one atomic per workgroup
+            const uint64_t bm = __ballot(jin && blk[j]);
+            if (lane == 0 && bm) atomicAdd((unsigned long long*)&st->blocked, (unsigned long long)__popcll(bm));
+        }
     }
 }
 
@@ -1732,7 +1776,8 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     const double* __restrict__ wsy, const double* __restrict__ snap_pose,
     CandEntry* __restrict__ cand, PrepRec* __restrict__ rec, double* __restrict__ pdbuf,
     double* __restrict__ snap_yaw, const SteerTask* __restrict__ tasks,
-    double* __restrict__ cost_out = nullptr, const StarTaskExt* __restrict__ ext = nullptr) {
+    double* __restrict__ cost_out = nullptr, const StarTaskExt* __restrict__ ext = nullptr,
+    const unsigned char* __restrict__ blk_in = nullptr) {
     // tasks != nullptr: explicit (child, parent pose) tasks [0, W) (multi-query batch); a task
     // with pnode < 0 is idle; own_yaw: the child keeps its heading cyaw (RRT* rewire edges)
     const int W = st->W;
@@ -1744,7 +1789,8 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     constexpr int TPB = kPrepThreads / 64 * TPW;  // tasks per workgroup
     for (int blk = blockIdx.x; blk * TPB < total; blk += gridDim.x) {
         const int t = blk * TPB + wave * TPW + lane / kPrepLanes;
-        bool act = t < total;
+        // (window mode: a sample in an obstacle needs no steer — a kReject record)
+        bool act = t < total && !(blk_in && t < W && blk_in[t]);
         int j = 0, own = 0, cull = 0;
         double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0, cyaw = 0.0;
         double cbase = 0.0, climit = 0.0;
@@ -3530,9 +3576,11 @@ struct PqLds {
     PrepRec rec[kPqMaxTasks];
     double tx[kPqMaxTasks], ty[kPqMaxTasks], td2[kPqMaxTasks];
     int tpn[kPqMaxTasks], tst[kPqMaxTasks];
+    int tlist[kPqMaxTasks];          // slot s: its window slots that need steering, in order
+    unsigned char tpre[kPqMaxTasks]; // the sample lies in an obstacle (point_blocked)
     unsigned long long grab[kPqMaxSlots];
     long long sit[kPqMaxSlots], stg[kPqMaxSlots];
-    int sq[kPqMaxSlots], sn[kPqMaxSlots], done[kPqMaxSlots];
+    int sq[kPqMaxSlots], sn[kPqMaxSlots], done[kPqMaxSlots], nact[kPqMaxSlots];
     int nretired;
 };
 __host__ __device__ inline int pq_lds_bytes(int scene_bytes) {
@@ -3545,29 +3593,27 @@ __host__ __device__ inline int pq_lds_bytes(int scene_bytes) {
 // tasks below t_end are written.  prep_task reads only the step and the radius of the scene.
 __device__ __noinline__ void pq_prep(double step, double turn_radius, int lds_off,
                                      const double* __restrict__ mx, const double* __restrict__ my,
-                                     const double* __restrict__ myaw, size_t row, int t0,
-                                     int t_end) {
+                                     const double* __restrict__ myaw, size_t row, int base, int i0,
+                                     int nact) {
     PqLds& L = *reinterpret_cast<PqLds*>(pp_smem + lds_off);
     SceneDev sc;
     sc.step_size = step;
     sc.turn_radius = turn_radius;
     const int lane = threadIdx.x & 63;
-    const int t = t0 + lane / 8;
-    const bool in = t < t_end;
+    const int i = i0 + lane / 8;  // entry of the slot's task list
+    const bool in = i < nact;
+    const int t = in ? base + L.tlist[base + i] : base;
     const int pn = in ? L.tpn[t] : -1;
-    const bool act = pn >= 0;
     double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0;
     if (in) {
         x = L.tx[t];
         y = L.ty[t];
-    }
-    if (act) {
         px = mx[row + pn];
         py = my[row + pn];
         pyaw = myaw[row + pn];
     }
-    prep_task(sc, lane & 7, lane & ~7, t, in, act, x, y, px, py, pyaw, 0, 0.0, 0, 0.0, 0.0,
-              L.rec, nullptr, nullptr);
+    prep_task(sc, lane & 7, lane & ~7, t, in, in, x, y, px, py, pyaw, 0, 0.0, 0, 0.0, 0.0, L.rec,
+              nullptr, nullptr);
 }
 
 // the literal path out of line: it runs once in a few thousand steps, and inlined its registers
@@ -3575,8 +3621,9 @@ __device__ __noinline__ void pq_prep(double step, double turn_radius, int lds_of
 // to the kernel argument would make the compiler copy the whole argument block to the stack.
 __device__ __noinline__ int pq_literal(const SceneDev* __restrict__ sc, const PrepRec* R,
                                        double* bx) {
-    return steer_collide_literal(*sc, R->x, R->y, R->yaw, R->px, R->py, R->pyaw, bx,
-                                 bx + kLiteralCap, bx + 2 * kLiteralCap);
+    // (its own inlined copy: a function only these kernels call gets their register budget)
+    return steer_collide_literal_body<true>(*sc, R->x, R->y, R->yaw, R->px, R->py, R->pyaw, bx,
+                                      bx + kLiteralCap, bx + 2 * kLiteralCap, true);
 }
 
 __device__ __forceinline__ unsigned long long lds_load_u64(const unsigned long long* p) {
@@ -3590,7 +3637,6 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int K = mq.K, QS = a.slots;
-    const int npass = (K + 7) / 8;
     if (kLds) stage_scene(sc);
     double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) + wave * kGenSlots;
     const int lds_off = (kLds ? sc.lds_bytes : 0) + kPqWaves * kGenSlots * 8;
@@ -3602,7 +3648,7 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
     }
     if (tid == 0) L.nretired = 0;
     __syncthreads();
-    long long npts = 0, napts = 0, qsteps = 0;
+    long long npts = 0, napts = 0, qsteps = 0, ntask = 0, npre = 0;
     long long cyc[4] = {0, 0, 0, 0};  // this wave: serial, prep, walk, idle (profiling)
     const bool prof = a.tally != nullptr;
 
@@ -3611,19 +3657,23 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
     // the prep epoch `ep` (or retire the slot)
     auto serial = [&](int s, bool insert, unsigned ep) {
         const int base = s * K;
+        int nact = 0;
+        for (;;) {  // (an all-rejected window is replayed at once)
         if (insert) {
             const int q = L.sq[s];
             const int k = lane;
             const bool inw = k < K;
             const int t = base + k;
             int st = kReject, pn = -1;
+            bool pre = false;
             double x = 0.0, y = 0.0, yw = 0.0, d2nn = 0.0;
             if (inw) {
                 pn = L.tpn[t];
-                st = L.tst[t];
+                pre = L.tpre[t];
+                st = pre ? kReject : L.tst[t];
                 x = L.tx[t];
                 y = L.ty[t];
-                yw = L.rec[t].yaw;
+                yw = pre ? 0.0 : L.rec[t].yaw;
                 d2nn = L.td2[t];
             }
             const bool act = inw && pn >= 0;
@@ -3642,7 +3692,8 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
             bool cut = !act;
             for (int j = 0; j < K; ++j) {
                 const double xj = __shfl(x, j), yj = __shfl(y, j);
-                if (((accm >> j) & 1ull) && k > j && act) {
+                // (a sample in an obstacle is rejected whatever its parent: never cut there)
+                if (((accm >> j) & 1ull) && k > j && act && !pre) {
                     const double dx = x - xj, dy = y - yj;
                     if (dx * dx + dy * dy < d2nn) cut = true;
                 }
@@ -3746,14 +3797,26 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
                 else
                     argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
             }
+            // the samples in an obstacle are decided here; the others are listed for prep + walk
+            const bool pre = live && point_blocked<kLds, kScene>(sc, x, y);
+            const uint64_t am = __ballot(g == 0 && live && !pre);
             if (g == 0) {
                 L.tx[base + k] = x;
                 L.ty[base + k] = y;
                 L.tpn[base + k] = live ? bi : -1;
                 L.td2[base + k] = bd;
+                L.tpre[base + k] = pre ? 1 : 0;
+                if (live && !pre) L.tlist[base + __popcll(am & ((1ull << lane) - 1ull))] = k;
             }
+            nact = __popcll(am);
+            ntask += __popcll(__ballot(g == 0 && live));
+            npre += __popcll(__ballot(g == 0 && pre));
         }
         __threadfence_block();
+        if (nact > 0) break;
+        insert = true;
+        }
+        if (lane == 0) L.nact[s] = nact;
         if (lane == 0) {
             L.done[s] = 0;
             __threadfence_block();
@@ -3782,7 +3845,8 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
             const unsigned long long v = lds_load_u64(&L.grab[c]);
             const unsigned e = (unsigned)(v >> 32);
             if (e >= kEpBusy) continue;
-            const unsigned lim = (e & 1u) ? (unsigned)K : (unsigned)npass;
+            const int na = L.nact[c];
+            const unsigned lim = (e & 1u) ? (unsigned)na : (unsigned)((na + 7) / 8);
             if ((unsigned)v >= lim) continue;  // every item of the phase is taken
             unsigned long long old = 0;
             if (lane == 0) old = atomicAdd(&L.grab[c], 1ull);
@@ -3790,7 +3854,8 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
                   (unsigned)__builtin_amdgcn_readfirstlane((int)old);
             const unsigned e2 = (unsigned)(old >> 32);
             if (e2 >= kEpBusy) continue;
-            const unsigned lim2 = (e2 & 1u) ? (unsigned)K : (unsigned)npass;
+            const int na2 = L.nact[c];
+            const unsigned lim2 = (e2 & 1u) ? (unsigned)na2 : (unsigned)((na2 + 7) / 8);
             if ((unsigned)old < lim2) {
                 s = c;
                 item = (int)(unsigned)old;
@@ -3806,23 +3871,25 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
         __threadfence_block();  // the phase's inputs (records, samples) were published before
         const int base = s * K;
         const bool walk = ep & 1u;
+        const int nact = L.nact[s];
         if (walk) {
             int np = 0, na = 0;
-            const int st = walk_rec<kLds, kScene>(sc, &L.rec[base + item], nullptr, gs, np, na);
-            if (lane == 0) L.tst[base + item] = st;
+            const int t = base + L.tlist[base + item];
+            const int st = walk_rec<kLds, kScene>(sc, &L.rec[t], nullptr, gs, np, na);
+            if (lane == 0) L.tst[t] = st;
             npts += np;
             napts += na;
             stamp(2);
         } else {
             pq_prep(sc.step_size, sc.turn_radius, lds_off, mq.x, mq.y, mq.yaw,
-                    (size_t)L.sq[s] * mq.cap, base + 8 * item, base + K);
+                    (size_t)L.sq[s] * mq.cap, base, 8 * item, nact);
             stamp(1);
         }
         __threadfence_block();  // this item's results before it counts as done
         int d = 0;
         if (lane == 0) d = atomicAdd(&L.done[s], 1);
         d = __builtin_amdgcn_readfirstlane(d);
-        if (d != (walk ? K : npass) - 1) continue;
+        if (d != (walk ? nact : (nact + 7) / 8) - 1) continue;
         // the phase's last item: this wave opens the slot's next phase
         if (!walk) {
             if (lane == 0) {
@@ -3836,13 +3903,16 @@ __global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs 
             stamp(0);
         }
     }
-    if (prof) {  // [0] query-steps, [1] walked points, [2] their arc points, [3..6] wave time
+    if (prof) {  // [0] query-steps, [1] walked points, [2] their arc points, [3..6] wave time,
+                 // [8] window slots evaluated, [9] of them decided by point_blocked
         unsigned long long* tl = reinterpret_cast<unsigned long long*>(a.tally);
         if (lane == 0) {
             atomicAdd(&tl[0], (unsigned long long)qsteps);
             atomicAdd(&tl[1], (unsigned long long)npts);
             atomicAdd(&tl[2], (unsigned long long)napts);
             for (int p = 0; p < 4; ++p) atomicAdd(&tl[3 + p], (unsigned long long)cyc[p]);
+            atomicAdd(&tl[8], (unsigned long long)ntask);
+            atomicAdd(&tl[9], (unsigned long long)npre);
         }
     }
 }
@@ -4518,7 +4588,9 @@ SamplesArgs samples_args(const WindowArgs& a) {
         g.ob[q] = a.ob + (size_t)q * (kMaxWindow / kQPB);
         g.sq[q] = a.sq + (size_t)q * a.Kcap;
         g.ipos[q] = a.ipos + (size_t)q * a.Kcap;
+        g.blk[q] = a.blk ? a.blk + (size_t)q * a.Kcap : nullptr;
     }
+    g.scp = a.scp;
     return g;
 }
 PairGrid pair_grid(const SamplesArgs& g, int p, double eps_coord) {
@@ -4600,12 +4672,13 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
         a.st, p, seq, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, wsx, wsy, a.tr.x32, a.tr.y32,
         a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose,
         pair_grid(wk.g, p, a.eps_coord), a.cand_cnt, a.cand, a.pend, wk.sq[p], wk.g.ipos[p], wk.g,
-        1);
+        1, wk.g.blk[p]);
     if (ev) (void)hipEventRecord(ev[2], s);
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K + kPrepThreads / 8 - 1) / (kPrepThreads / 8);
     steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, wsx, wsy, a.snap_pose, a.cand,
-                                                  a.rec, a.pdbuf, a.snap_yaw, nullptr);
+                                                  a.rec, a.pdbuf, a.snap_yaw, nullptr, nullptr,
+                                                  nullptr, wk.g.blk[p]);
     if (ev) (void)hipEventRecord(ev[3], s);
     // snapshot tasks plus the usual few candidate tasks in one round of waves
     const int nwg = std::min((K + K / 4 + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
@@ -4630,7 +4703,7 @@ hipError_t launch_nearest(hipStream_t s, const WindowArgs& a) {
     nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples, kFinThreads, 0, s>>>(
         a.st, 0, 0, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, a.wsx, a.wsy, a.tr.x32,
         a.tr.y32, a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, nullptr, PairGrid{},
-        nullptr, nullptr, nullptr, nullptr, nullptr, wk.g, 0);
+        nullptr, nullptr, nullptr, nullptr, nullptr, wk.g, 0, nullptr);
     return hipGetLastError();
 }
 

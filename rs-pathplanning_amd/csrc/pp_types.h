@@ -123,6 +123,7 @@ struct DevState {
     // statistics (pp_stats)
     int64_t iterations, accepted, windows, truncations, repair_rounds, repairs, literal_repairs,
         nn_flagged, node_evals;
+    int64_t blocked;  // samples in an obstacle (point_blocked): rejected without steer or pair list
 };
 
 // An explicit steer task: child (x, y) steered toward its parent — tree node `pnode` when

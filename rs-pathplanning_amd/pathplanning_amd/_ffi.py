@@ -77,6 +77,7 @@ class StatsC(C.Structure):
         ("finish_arc_points", C.c_int64),
         ("batch_query_steps", C.c_int64), ("persist_ms", C.c_double),
         ("persist_launches", C.c_int64), ("persist_cycles", C.c_int64 * 5),
+        ("samples_evaluated", C.c_int64), ("samples_blocked", C.c_int64),
     ]
 
     def as_dict(self):
