@@ -601,6 +601,7 @@ MqArgs mq_args(pp_ctx* c) {
     a.lit_locks = c->lit_locks.p;
     a.err = c->mq_err.p;
     a.wg_points = c->prof_points();
+    a.scp = c->pq_scene.p;  // (uploaded by pp_batch_extend)
     return a;
 }
 
@@ -1850,8 +1851,6 @@ int batch_extend_persistent(pp_ctx* ctx, const MqArgs& a) {
         PP_HIP(hipMemsetAsync(ctx->pq_tally.p, 0, kPqTally * sizeof(long long), st));
     }
     PP_HIP(hipMemsetAsync(ctx->pq_next.p, 0, sizeof(int), st));
-    if (!ctx->pq_scene.p) PP_HIP(ctx->pq_scene.reserve(1));
-    PP_HIP(hipMemcpyAsync(ctx->pq_scene.p, &a.sc, sizeof(SceneDev), hipMemcpyHostToDevice, st));
     PqArgs pa;
     pa.mq = a.mq;
     pa.sc = a.sc;
@@ -1896,6 +1895,11 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
     if (n_steps < 0) return set_err(PP_ERR_INVALID_ARGUMENT, "n_steps < 0");
     int64_t it0 = 0, n0 = 0, it1 = 0, n1 = 0;
     if ((n_iterations || n_accepted) && (r = mq_totals(ctx, &it0, &n0))) return r;
+    {  // the batch's scene in device memory (point_blocked, the persistent kernel's literal path)
+        if (!ctx->pq_scene.p) PP_HIP(ctx->pq_scene.reserve(1));
+        const SceneDev sd = mq_args(ctx).sc;
+        PP_HIP(hipMemcpy(ctx->pq_scene.p, &sd, sizeof sd, hipMemcpyHostToDevice));
+    }
     MqArgs a = mq_args(ctx);
     const int K = ctx->mq_K, Q = ctx->mq_Q;
     // an earlier call's PP_ERR_STEER_OVERFLOW does not stick to this one

@@ -128,6 +128,7 @@ struct MqArgs {
     hipEvent_t* ev = nullptr;  // optional: 5 per step: before mq_sample_nn, then after it, steer_prep,
                                // steer_walk and mq_insert
     long long* wg_points = nullptr;  // profiling: walked points per walk workgroup (or null)
+    const SceneDev* scp = nullptr;   // the scene in device memory: point_blocked (or null: none)
 };
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps);
 // Persistent form (round 4): ONE launch runs every query to mq.target.  A workgroup owns `slots`

@@ -3337,7 +3337,8 @@ hipError_t launch_mq_plan_reduce(hipStream_t s, int Q, const int* off, const int
 // Queries are independent, so there is no speculation and no resolve.
 __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx, double maxx,
                                                            double miny, double maxy,
-                                                           SteerTask* __restrict__ tasks) {
+                                                           SteerTask* __restrict__ tasks,
+                                                           const SceneDev* __restrict__ scp) {
     // one wave per task t = q * K + k: Space::rand_point of iteration it[q] + k on stream q
     // (rrt.rs:139-146, Q7) and the exact nearest node of tree q as the step found it
     // (rrt.rs:378-391, Q9: lanes stride the rows, lowest index on ties)
@@ -3384,6 +3385,12 @@ __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx
             const int t = q * K + k;
             if (!live) {
                 tasks[t].pnode = -1;
+            } else if (scp && point_blocked<false, kSceneAny>(*scp, x, y)) {
+                // the sample lies in an obstacle: rejected whatever its parent (pnode -2: no steer,
+                // and the insert never cuts the window there)
+                tasks[t].x = x;
+                tasks[t].y = y;
+                tasks[t].pnode = -2;
             } else {
                 tasks[t] = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, 0};
                 mq.nnd2[t] = bd;
@@ -3433,6 +3440,7 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
             st = status[t];
             yw = yaw[t];
         }
+        const bool live = in && tk.pnode != -1;  // (pnode -2: a sample in an obstacle)
         const bool act = in && tk.pnode >= 0;
         if (act) d2nn = mq.nnd2[t];
         if (uint64_t lit = __ballot(act && st == kLiteral)) {
@@ -3451,7 +3459,7 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
         }
         const bool blocked = in && mq.blocked && mq.blocked[q];
         const uint64_t accm = __ballot(act && st == kAccept && !blocked);
-        bool cut = !act;
+        bool cut = !live;
         for (int j = 0; j < K; ++j) {  // slot j of every query against its later slots
             const double xj = __shfl(tk.x, g0 + j), yj = __shfl(tk.y, g0 + j);
             if (((accm >> (g0 + j)) & 1ull) && k > j && act) {
@@ -3524,7 +3532,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
         hipEvent_t* ev = a.ev ? a.ev + 5 * k : nullptr;
         if (ev) (void)hipEventRecord(ev[0], s);
         mq_sample_nn_kernel<<<nn_blocks, 256, 0, s>>>(a.mq, a.sc.minx, a.sc.maxx, a.sc.miny,
-                                                      a.sc.maxy, a.tasks);
+                                                      a.sc.maxy, a.tasks, a.scp);
         if (ev) (void)hipEventRecord(ev[1], s);
         steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, nullptr, nullptr, nullptr,
                                                       nullptr, a.rec, a.pdbuf, a.yaw, a.tasks);

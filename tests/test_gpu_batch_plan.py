@@ -10,13 +10,26 @@ a node connecting to the node itself, rrt.rs:473-474: a Dubins loop back to its 
 rounding residue whose exact 0.0 decides whether dubins.rs:281-288 pops one more point, and ocml
 and glibc disagree on it in a few percent of configurations.  Such a query's line then differs
 by exactly one point on an arc (|delta n| = 1, |delta length| = one chord 2R sin(step / 2)); the
-test counts them and requires them to stay rare."""
+test counts them (printed and, with PP_FLIP_REPORT_PLAN=<path>, written as JSON: profiles/) and
+pins them near the committed measurement (FLIPS_MAX)."""
+import json
 import math
+import os
 
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+REPORT = {}
+# one-point trim flips measured per case (profiles/r04_libm_flips_plan.json); the bound allows
+# twice the measured count (at least 1): a regression that doubles the rate fails
+FLIPS_MEASURED = {"bench6_open": None, "field512": None, "field512_128": None}
+
+
+def _bound(case):
+    m = FLIPS_MEASURED[case]
+    return None if m is None else max(1, 2 * m)
 
 
 @pytest.fixture(scope="module")
@@ -24,6 +37,10 @@ def ctx(pkg):
     c = pkg.Context(0)
     yield c
     c.close()
+    path = os.environ.get("PP_FLIP_REPORT_PLAN")
+    if path and REPORT:
+        with open(path, "w") as f:
+            json.dump(REPORT, f, indent=1, sort_keys=True)
 
 
 def _run(ctx, oracle_mod, raw, q0, nq, max_iter):
@@ -49,7 +66,7 @@ def _run(ctx, oracle_mod, raw, q0, nq, max_iter):
     return got, exp, int(n.sum() - nq)
 
 
-def _check(got, exp, checked, raw):
+def _check(got, exp, checked, raw, case):
     assert got["checked"] == checked
     chord = 2.0 * raw["robot"][2] * math.sin(raw["step_size"] / 2.0)
     flips = 0
@@ -67,8 +84,10 @@ def _check(got, exp, checked, raw):
         flips += 1
         assert abs(int(got["n_points"][q]) - npts) == 1, q
         assert abs(abs(got["length"][q] - bl) - chord) <= 1e-6 * chord, q
-    print(f"plan: {finishing} queries with a path, {flips} one-point libm trim flips")
-    assert flips <= max(1, finishing // 10)
+    REPORT[case] = {"queries": len(exp), "queries_with_path": finishing, "one_point_flips": flips}
+    print(f"plan {case}: {finishing} queries with a path, {flips} one-point libm trim flips")
+    bound = _bound(case)
+    assert flips <= (bound if bound is not None else max(1, finishing // 10))
 
 
 def test_batch_plan_bench6_open(pkg, ctx, oracle_mod):
@@ -78,7 +97,7 @@ def test_batch_plan_bench6_open(pkg, ctx, oracle_mod):
     raw = scenes.bench6_open()
     got, exp, checked = _run(ctx, oracle_mod, raw, 0, 64, 300)
     assert sum(1 for e in exp if e[0] >= 0) >= 16  # the comparison covers real finishes
-    _check(got, exp, checked, raw)
+    _check(got, exp, checked, raw, "bench6_open")
 
 
 def test_batch_plan_field512(pkg, ctx, oracle_mod):
@@ -87,7 +106,7 @@ def test_batch_plan_field512(pkg, ctx, oracle_mod):
 
     raw = scenes.field512()
     got, exp, checked = _run(ctx, oracle_mod, raw, 0, 24, 2000)
-    _check(got, exp, checked, raw)
+    _check(got, exp, checked, raw, "field512")
 
 
 def test_batch_plan_before_extend_and_reuse(pkg, ctx, oracle_mod):
@@ -117,4 +136,4 @@ def test_batch_plan_field512_128(pkg, ctx, oracle_mod):
     raw = scenes.field512()
     got, exp, checked = _run(ctx, oracle_mod, raw, 0, 128, 2000)
     assert checked >= 8192
-    _check(got, exp, checked, raw)
+    _check(got, exp, checked, raw, "field512_128")

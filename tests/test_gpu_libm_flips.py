@@ -9,8 +9,8 @@ x is a pure rounding residue, (b) the strict-`>` word choice between mathematica
   * check_finish verdicts (optimize chains and Some/None) over EVERY node of a bench6_open tree
     (8000 iterations) and of the example's transit tree: no flip allowed;
   * 100k same-position Dubins configurations (dx = dy = 0, random yaws): words equal, point counts
-    may differ by the trim only (one point), at a rate below 5 %, points of the common prefix
-    within 1e-9;
+    may differ by the trim only (one point), at most twice the committed count
+    (profiles/r03_libm_flips.json: 2589, 2.6 %), points of the common prefix within 1e-9;
   * 100k distinct-position configurations: words and point counts all equal.
 
 The counts are printed and, with PP_FLIP_REPORT=<path>, written as JSON (profiles/)."""
@@ -24,6 +24,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 REPORT = {}
+SAME_POSITION_FLIPS = 2589  # the committed measurement (seed 11, 100k configurations)
 
 
 @pytest.fixture(scope="module")
@@ -75,7 +76,8 @@ def test_check_finish_every_node_no_verdict_flip(pkg, ctx, oracle_mod, scene, n_
                                        "one_point_line_flips": length_flips}
     print(scene, REPORT[f"check_finish_{scene}"])
     assert verdict_flips == 0 and chain_flips == 0
-    assert length_flips <= max(1, ok_count // 20)
+    # measured 0 on both scenes (profiles/r03_libm_flips.json): at most one
+    assert length_flips <= 1
 
 
 def _battery(pkg, ctx, oracle_mod, same, n, seed):
@@ -124,7 +126,7 @@ def test_same_position_dubins_battery(pkg, ctx, oracle_mod):
                                       "max_point_diff": worst}
     print(REPORT["dubins_same_position"])
     assert w == 0
-    assert c <= n // 20
+    assert c <= 2 * SAME_POSITION_FLIPS  # measured 2589 of 100k (profiles/r03_libm_flips.json)
     assert worst <= 1e-9
 
 
