@@ -537,7 +537,9 @@ int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line,
         if (int r = ensure_events(c, 2)) return r;
         PP_HIP(hipEventRecord(c->ev[0], c->stream));
     }
-    PP_HIP(launch_check_finish(c->stream, c->scene_dev(), tr, nodes, k, g->x, g->y,
+    SceneDev sd = c->scene_dev();
+    if (cb.qidx) sd.step_size = c->mq_step;  // a query batch's edges use the batch's step
+    PP_HIP(launch_check_finish(c->stream, sd, tr, nodes, k, g->x, g->y,
                                g->yaw, g->yaw_opt, g->level0, g->mode, want_line, o.ok, o.len,
                                o.npts, o.chain, c->api_lit_scratch.p, c->lit_locks.p,
                                want_line ? c->cf_pts.p : nullptr, kCfPtsCap,
