@@ -88,6 +88,7 @@ struct HBuf {  // pinned host staging
 };
 
 constexpr int kMaxBatch = 64;  // windows enqueued between two host synchronisations
+constexpr int kInsideCells = 2048;  // the inside bitmap's cells per axis (point_blocked)
 constexpr int kScreenPad = 64;  // f32 screen copies: the LDS-DMA reads whole float4s (<= 3 floats past)
 
 }  // namespace
@@ -115,6 +116,10 @@ struct pp_ctx {
     double bx0 = 0, by0 = 0, binv = 1;
     // polygon mode (pp_space_new_polygons, Q10p): obstacle edges, bounds ring; host copies for
     // the point checks (root / query starts)
+    // disc scenes: the inside bitmap (scene::inside_bitmap), the point_blocked pre-test
+    DBuf<uint32_t> d_ibits;
+    int ibn = 0;
+    double ibx0 = 0.0, iby0 = 0.0, ibinv = 1.0;
     int ne = 0, nbv = 0;
     double h2 = 0.0;
     float cull_slack = 1.0e-3f;
@@ -310,6 +315,12 @@ struct pp_ctx {
         s.bvy = d_bvy.p;
         s.cull_slack = cull_slack;
         s.root_blocked = root_blocked ? 1 : 0;
+        s.ibits = ibn > 0 ? d_ibits.p : nullptr;
+        s.ibn = ibn;
+        s.ibwords = ibn / 32;
+        s.ibx0 = ibx0;
+        s.iby0 = iby0;
+        s.ibinv = ibinv;
         return s;
     }
     // Space::verify of the one-point line [(x, y)] on the host, polygon mode (Q10p; the same
@@ -1089,6 +1100,7 @@ int upload_item_grid(pp_ctx* ctx, double minx, double maxx, double miny, double 
 
 // reset the polygon-mode part of the scene (pp_space_new / pp_space_new_polygons)
 void clear_polygons(pp_ctx* ctx) {
+    ctx->ibn = 0;  // (pp_space_new builds its inside bitmap after this)
     ctx->ne = 0;
     ctx->nbv = 0;
     ctx->h_ex0.clear();
@@ -1126,6 +1138,19 @@ int pp_space_new(pp_ctx* ctx, double x0, double y0, double x1, double y1, double
         PP_HIP(hipMemcpy(ctx->d_rcull.p, ds.rcull.data(), m * sizeof(double), hipMemcpyHostToDevice));
     }
     clear_polygons(ctx);
+    {  // the inside bitmap: 2048^2 cells (512 KB, L2-resident)
+        const scene::InsideBits ib =
+            scene::inside_bitmap(ds.minx, ds.maxx, ds.miny, ds.maxy, cx, cy, ds.r2, kInsideCells);
+        ctx->ibn = ib.n;
+        if (ib.n > 0) {
+            PP_HIP(ctx->d_ibits.reserve(ib.bits.size()));
+            PP_HIP(hipMemcpy(ctx->d_ibits.p, ib.bits.data(), ib.bits.size() * sizeof(uint32_t),
+                             hipMemcpyHostToDevice));
+            ctx->ibx0 = ib.x0;
+            ctx->iby0 = ib.y0;
+            ctx->ibinv = ib.inv;
+        }
+    }
     ctx->h2 = half * half;
     ctx->cull_slack = scene::cull_slack_for(ds.items.mx);
     ctx->minx = ds.minx;

@@ -232,10 +232,11 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
 // Point 0 of a candidate's line — the sample itself — inside an obstacle: the line is rejected
 // whatever its parent and its Dubins path (verify, rrt.rs:124-137: the first segment starts inside
 // the disc / on an occupied cell), so the candidate needs neither steer_prep nor steer_walk and its
-// verdict cannot depend on which node is its parent.  Discs: the disc grid's cell of the point
-// (every disc is listed in each cell its cull box touches), clearly inside only — d2 below r2 by a
-// relative 1e-9, far beyond the rounding of the walk's exact segment test, which therefore finds
-// the same hit; the grid mode probes the very bit the walk probes.  Polygon scenes: no pre-test.
+// verdict cannot depend on which node is its parent.  Discs: one bit of the inside bitmap (the
+// point's cell lies wholly inside a disc), else the disc grid's cell of the point (every disc is
+// listed in each cell its cull box touches); clearly inside only — d2 below r2 by a relative 1e-9,
+// far beyond the rounding of the walk's exact segment test, which therefore finds the same hit;
+// the grid mode probes the very bit the walk probes.  Polygon scenes: no pre-test.
 template <bool kLds, int kScene>
 __device__ __forceinline__ bool point_blocked(const SceneDev& sc, double x, double y) {
     if (kScene == kSceneGrid || (kScene == kSceneAny && sc.bits)) {
@@ -244,6 +245,13 @@ __device__ __forceinline__ bool point_blocked(const SceneDev& sc, double x, doub
     }
     if (kScene == kScenePoly || (kScene == kSceneAny && (sc.ne > 0 || sc.nbv > 0)) || sc.m == 0)
         return false;
+    if (sc.ibits) {  // one load: the cell lies wholly inside a disc (scene::inside_bitmap)
+        const double fx = floor((x - sc.ibx0) * sc.ibinv), fy = floor((y - sc.iby0) * sc.ibinv);
+        if (!(fx >= 0.0) || !(fy >= 0.0) || fx >= (double)sc.ibn || fy >= (double)sc.ibn)
+            return false;
+        const int i = (int)fx, j = (int)fy;
+        return (sc.ibits[(size_t)j * sc.ibwords + (i >> 5)] >> (i & 31)) & 1u;
+    }
     const int* goff = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_goff) : sc.goff;
     const int* items = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_items) : sc.gitems;
     const int cell = grid_cell(y, sc.gy0, sc.ginv, sc.gny) * sc.gnx + grid_cell(x, sc.gx0, sc.ginv, sc.gnx);
@@ -725,14 +733,29 @@ __device__ inline int morton16(int x, int y) {
     return m;
 }
 
-// LDS of samples_role: the Morton histogram, each sample's cell, the sorted window's sample ids
-constexpr int kSamplesLds = 256 * 4 + kMaxWindow + kMaxWindow * 4;
+// LDS of samples_role: the Morton histogram, each sample's cell, the sorted window's sample ids,
+// the count of samples in an obstacle
+constexpr int kSamplesLds = 256 * 4 + kMaxWindow + kMaxWindow * 4 + 16;
+
+// The screen's geometry for Ws screened samples (window mode): nqb blocks of kQPB samples x
+// chunks node chunks on at most kScanGrid workgroups, nqb x chunks a multiple of 8 when it can be
+// (the XCD-aware mapping), chunks <= kMaxChunks (the partials' capacity).
+__host__ __device__ inline int screen_chunks(int Ws) {
+    const int nqb = (Ws + kQPB - 1) / kQPB;
+    if (nqb <= 0) return 1;
+    int c = kScanGrid / nqb;
+    if (c > kMaxChunks) c = kMaxChunks;
+    for (int d = c; d >= 1 && d * 4 >= c * 3; --d)
+        if (((nqb * d) & 7) == 0) return d;
+    return c < 1 ? 1 : c;
+}
 
 __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t start,
                              char* smem) {
     int* s_hist = reinterpret_cast<int*>(smem);                  // [256]
     unsigned char* s_cell = reinterpret_cast<unsigned char*>(s_hist + 256);  // [K]
     int* s_j = reinterpret_cast<int*>(smem + 256 * 4 + kMaxWindow);  // [K] sorted position -> sample
+    int* s_nb = s_j + kMaxWindow;  // samples in an obstacle (sorted after the screened ones)
     const int tid = threadIdx.x, NT = blockDim.x;
     const int64_t rem = g.target - start;
     // the adaptive window (kdyn, set by the commits; results never depend on the window size)
@@ -743,6 +766,7 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
         st->wsp[np] = start;
     }
     for (int i = tid; i < 256; i += NT) s_hist[i] = 0;
+    if (tid == 0) *s_nb = 0;
     __syncthreads();
     const double fx = 16.0 / (g.maxx - g.minx), fy = 16.0 / (g.maxy - g.miny);
     for (int j = tid; j < W; j += NT) {
@@ -753,14 +777,25 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
         g.wsy[np][j] = y;
         g.wsx32[np][j] = (float)x;
         g.wsy32[np][j] = (float)y;
-        if (g.blk[np]) g.blk[np][j] = point_blocked<false, kSceneAny>(*g.scp, x, y) ? 1 : 0;
+        const bool bk = g.blk[np] && point_blocked<false, kSceneAny>(*g.scp, x, y);
+        if (g.blk[np]) g.blk[np][j] = bk ? 1 : 0;
         const int cx = min(max((int)((x - g.minx) * fx), 0), 15);  // == sample_cell
         const int cy = min(max((int)((y - g.miny) * fy), 0), 15);
         const int cell = morton16(cx, cy);
         s_cell[j] = (unsigned char)cell;
-        atomicAdd(&s_hist[cell], 1);
+        // a sample in an obstacle needs no nearest node and is nobody's candidate parent: it is
+        // sorted after the screened samples, out of the screen and the pair grid
+        if (bk)
+            atomicAdd(s_nb, 1);
+        else
+            atomicAdd(&s_hist[cell], 1);
     }
     __syncthreads();
+    const int Ws = W - *s_nb;  // screened samples: sorted positions [0, Ws)
+    if (tid == 0) {
+        st->Wsp[np] = Ws;
+        st->chp[np] = screen_chunks(Ws);
+    }
     if (tid < 64) {  // exclusive prefix of the 256 cell counts, 4 per lane
         int v[4], sum = 0;
 #pragma unroll
@@ -778,16 +813,25 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
     }
     __syncthreads();
     for (int i = tid; i < 256; i += NT) g.cofs[np][i] = s_hist[i];
-    if (tid == 0) g.cofs[np][256] = W;
+    if (tid == 0) {
+        g.cofs[np][256] = Ws;
+        *s_nb = Ws;  // (now the next free position of the blocked bucket)
+    }
     __syncthreads();  // the cell starts are read before the scatter advances them
-    for (int j = tid; j < W; j += NT) s_j[atomicAdd(&s_hist[s_cell[j]], 1)] = j;
+    for (int j = tid; j < W; j += NT)
+        s_j[(g.blk[np] && g.blk[np][j]) ? atomicAdd(s_nb, 1) : atomicAdd(&s_hist[s_cell[j]], 1)] = j;
     __syncthreads();
     // the screen's blocks of kQPB sorted samples, one wave each: the sorted window (coalesced; the
     // coordinates drawn again from the stream, bit-identical), the centre o of the block's
     // bounding box (f32) and every sample's |q - o|^2 in f64 — (q - o) rounded to f32 per axis,
     // the screen's own operands, squared exactly (nn_finalize adds it back to the screen values)
     const int lane = tid & 63, wv = tid >> 6;
-    for (int qb = wv; qb * kQPB < W; qb += NT / 64) {
+    for (int pos = Ws + tid; pos < W; pos += NT) {  // the blocked bucket: perm / ipos only
+        const int j = s_j[pos];
+        g.perm[np][pos] = j;
+        g.ipos[np][j] = pos;
+    }
+    for (int qb = wv; qb * kQPB < Ws; qb += NT / 64) {
         const int p0 = qb * kQPB;
         double xs[kQPL], ys[kQPL];
         double x0 = __builtin_inf(), x1 = -__builtin_inf(), y0 = __builtin_inf(), y1 = -__builtin_inf();
@@ -795,7 +839,7 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
         for (int r = 0; r < kQPL; ++r) {
             const int pos = p0 + r * 64 + lane;
             xs[r] = ys[r] = 0.0;
-            if (pos < W) {
+            if (pos < Ws) {
                 const int j = s_j[pos];
                 const uint64_t itj = (uint64_t)(start + j);
                 xs[r] = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
@@ -820,7 +864,7 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
 #pragma unroll
         for (int r = 0; r < kQPL; ++r) {
             const int pos = p0 + r * 64 + lane;
-            if (pos < W) {
+            if (pos < Ws) {
                 const float qpx = (float)(xs[r] - (double)oxf), qpy = (float)(ys[r] - (double)oyf);
                 g.sq[np][s_j[pos]] = (double)qpx * (double)qpx + (double)qpy * (double)qpy;
             }
@@ -919,16 +963,20 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
                                                                char* smem) {
     DevState* st = a.st;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int W = st->Wp[a.p];
+    // window mode: the samples not in an obstacle (sorted first) on the geometry samples_role
+    // chose for them; the nearest API: the given samples on the launch's geometry
+    const int W = kExp ? st->Wsp[a.p] : st->Wp[a.p];
     const int ns = st->n_scan;
     if (b == 0 && tid == 0) st->nsp[a.p] = ns;
-    const int G = a.nqb * a.chunks;
+    const int chunks = kExp ? st->chp[a.p] : a.chunks;
+    const int nqb = kExp ? (W + kQPB - 1) / kQPB : a.nqb;
+    const int G = nqb * chunks;
     if (b >= G) return;
     const int t = (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b;
-    const int qb = t % a.nqb, c = t / a.nqb;
+    const int qb = t % nqb, c = t / nqb;
     const int qbase = qb * kQPB;
     if (qbase >= W) return;
-    const int cl = scan_chunk_len(ns, a.chunks);
+    const int cl = scan_chunk_len(ns, chunks);
     const int c0 = c * cl;
     if (c0 >= ns) return;
     const int L = min(c0 + cl, ns) - c0;  // the chunk's nodes
@@ -1236,7 +1284,7 @@ __device__ inline Top2 wave_top2(Top2 t) {
 // 8 waves per SIMD (<= 64 VGPRs): two 1024-thread workgroups per CU, so the extra sampling
 // workgroup (the grid's last) runs beside the others instead of waiting for a CU to drain.
 __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
-    DevState* __restrict__ st, int p, int64_t seq, int chunks, const float* __restrict__ pbest,
+    DevState* __restrict__ st, int p, int64_t seq, int chunks_api, const float* __restrict__ pbest,
     const float* __restrict__ psecond, const int* __restrict__ pidx, int stride,
     const double* __restrict__ qx, const double* __restrict__ qy, const float* __restrict__ x32,
     const float* __restrict__ y32, const double* __restrict__ X, const double* __restrict__ Y,
@@ -1270,6 +1318,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
     }
     const int W = voided ? 0 : st->Wp[p];
     const int ns = st->nsp[p], n = st->n;
+    const int chunks = cand ? st->chp[p] : chunks_api;  // window mode: samples_role's geometry
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->W = W;
         st->n_scan = n;
@@ -4672,7 +4721,9 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     double* wsx = a.wsx + (size_t)p * a.Kcap;
     double* wsy = a.wsy + (size_t)p * a.Kcap;
     if (ev) (void)hipEventRecord(ev[0], s);
-    window_kernel<<<1 + wk.nqb * wk.chunks, kScanThreads, 0, s>>>(wk);
+    // (the screen's geometry is decided on the device, from the samples not in an obstacle:
+    // every workgroup past it returns at once)
+    window_kernel<<<1 + kScanGrid, kScanThreads, 0, s>>>(wk);
     if (resolve_prev && !kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
     if (ev) (void)hipEventRecord(ev[1], s);
     // one workgroup past the samples' draws the next window's samples

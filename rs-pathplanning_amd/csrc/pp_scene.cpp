@@ -211,5 +211,41 @@ ItemGrid build_item_grid(double minx, double maxx, double miny, double maxy, con
     return g;
 }
 
+InsideBits inside_bitmap(double minx, double maxx, double miny, double maxy, const double* cx,
+                         const double* cy, const std::vector<double>& r2, int n) {
+    InsideBits ib;
+    const int m = (int)r2.size();
+    if (n <= 0 || (n & 31) || m == 0 || !(maxx > minx) || !(maxy > miny)) return ib;
+    const double span = std::max(maxx - minx, maxy - miny);
+    const double cell = span / n;
+    ib.n = n;
+    ib.x0 = minx;
+    ib.y0 = miny;
+    ib.inv = 1.0 / cell;
+    const int words = n / 32;
+    ib.bits.assign((size_t)n * words, 0u);
+    // a point maps to cell floor((v - v0) * inv): the corners are widened by a margin far above
+    // that rounding, so every point the device maps into the cell lies in the tested square
+    const double eps = 1e-6 * cell + 1e-9 * (std::fabs(minx) + std::fabs(miny) + span);
+    for (int k = 0; k < m; ++k) {
+        const double r = std::sqrt(r2[k]);
+        const int i0 = std::max(0, (int)std::floor((cx[k] - r - minx) / cell));
+        const int i1 = std::min(n - 1, (int)std::floor((cx[k] + r - minx) / cell));
+        const int j0 = std::max(0, (int)std::floor((cy[k] - r - miny) / cell));
+        const int j1 = std::min(n - 1, (int)std::floor((cy[k] + r - miny) / cell));
+        const double lim = r2[k] * (1.0 - 1e-9);
+        for (int j = j0; j <= j1; ++j) {
+            const double ya = miny + j * cell - eps - cy[k], yb = miny + (j + 1) * cell + eps - cy[k];
+            const double dy2 = std::max(ya * ya, yb * yb);
+            for (int i = i0; i <= i1; ++i) {
+                const double xa = minx + i * cell - eps - cx[k], xb = minx + (i + 1) * cell + eps - cx[k];
+                const double dx2 = std::max(xa * xa, xb * xb);
+                if (dx2 + dy2 < lim) ib.bits[(size_t)j * words + (i >> 5)] |= 1u << (i & 31);
+            }
+        }
+    }
+    return ib;
+}
+
 }  // namespace scene
 }  // namespace ppamd

@@ -66,5 +66,18 @@ ItemGrid build_item_grid(double minx, double maxx, double miny, double maxy, con
 // f32 cull slack for coordinates of magnitude <= mx
 float cull_slack_for(double mx);
 
+// The cells of an n x n grid over the sampling box (square cells of the larger span, from
+// (minx, miny), 1 / inv per cell) that lie wholly inside an inflated disc — every corner,
+// widened by a rounding margin, at d2 < r2 (1 - 1e-9): bit i % 32 of word j * (n / 32) + i / 32
+// for cell (i, j).  A sample in such a cell is inside the disc (convexity), so its line is
+// rejected whatever its parent (point_blocked); cells the boundary crosses stay clear.
+struct InsideBits {
+    std::vector<uint32_t> bits;
+    int n = 0;
+    double x0 = 0.0, y0 = 0.0, inv = 1.0;
+};
+InsideBits inside_bitmap(double minx, double maxx, double miny, double maxy, const double* cx,
+                         const double* cy, const std::vector<double>& r2, int n);
+
 }  // namespace scene
 }  // namespace ppamd

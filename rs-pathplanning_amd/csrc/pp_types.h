@@ -85,6 +85,11 @@ struct SceneDev {
     const double* bvx;
     const double* bvy;
     float cull_slack;  // f32 cull slack for the scene's coordinate magnitude
+    // disc scenes: the cells of an ibn x ibn grid over the sampling box that lie wholly inside an
+    // inflated disc (scene::inside_bitmap), the one-load point_blocked pre-test; null: none
+    const uint32_t* ibits;
+    int ibn, ibwords;
+    double ibx0, iby0, ibinv;
     int root_blocked;  // planner (polygon mode): the root itself fails verify, so every
                        // line_to_origin does (check_finish: optimize accepts no candidate)
 };
@@ -117,6 +122,9 @@ struct DevState {
     int64_t wsp[2];  // per parity: first iteration of the window the scan generated
     int Wp[2];       // per parity: its sample count
     int nsp[2];      // per parity: tree nodes its scan covered
+    int Wsp[2];      // per parity: samples the screen covers (the window's samples not in an
+                     // obstacle: sorted positions [0, Wsp); samples_role)
+    int chp[2];      // per parity: the screen's node chunks for those samples
     int64_t void_seq;  // window sequence number voided by a truncated predecessor (-1: none)
     int resolve_bail;  // the window kernel's resolve needed a repair: resolve_tail_kernel redoes it
     int kdyn;          // adaptive window: samples drawn per window (<= K; the commit adapts it)

@@ -215,6 +215,38 @@ int main(int argc, char** argv) {
             std::printf("%s[%d, %d, %ld, %d, %d]", b ? ", " : "", g.gnx, g.gny, entries, g.lds_total, g.o_d4);
         }
         std::printf("], \"cull_slack\": %.9g, ", (double)sc::cull_slack_for(items.mx));
+        if (!poly) {  // the inside bitmap: every point a set cell maps to is inside some disc
+            const int m = (int)ds.r2.size();
+            std::vector<double> bx(m), by(m);
+            for (int k = 0; k < m; ++k) {
+                bx[k] = c3[3 * k];
+                by[k] = c3[3 * k + 1];
+            }
+            const sc::InsideBits ib = sc::inside_bitmap(minx, maxx, miny, maxy, bx.data(), by.data(), ds.r2, 256);
+            long set = 0, bad = 0;
+            for (int j = 0; j < ib.n; ++j)
+                for (int i = 0; i < ib.n; ++i) {
+                    if (!((ib.bits[(size_t)j * (ib.n / 32) + (i >> 5)] >> (i & 31)) & 1u)) continue;
+                    ++set;
+                    for (int u = 0; u <= 4; ++u)
+                        for (int v = 0; v <= 4; ++v) {
+                            // points across the cell, its edges pushed to the last double that
+                            // still maps into it (the device's floor((x - x0) * inv))
+                            double x = ib.x0 + (i + u / 4.0) / ib.inv, y = ib.y0 + (j + v / 4.0) / ib.inv;
+                            while (std::floor((x - ib.x0) * ib.inv) > i) x = std::nextafter(x, -1e300);
+                            while (std::floor((x - ib.x0) * ib.inv) < i) x = std::nextafter(x, 1e300);
+                            while (std::floor((y - ib.y0) * ib.inv) > j) y = std::nextafter(y, -1e300);
+                            while (std::floor((y - ib.y0) * ib.inv) < j) y = std::nextafter(y, 1e300);
+                            bool in = false;
+                            for (int k = 0; k < m && !in; ++k) {
+                                const double dx = x - bx[k], dy = y - by[k];
+                                in = dx * dx + dy * dy < ds.r2[k] * (1.0 - 1e-9);
+                            }
+                            bad += !in;
+                        }
+                }
+            std::printf("\"inside\": [%ld, %ld], ", set, bad);
+        }
         // the oracle on the same scene
         std::vector<double> cx, cy;
         orc_scene o{};

@@ -130,6 +130,12 @@ def test_sanitized_scene_builder_and_oracle_run_clean(san_run):
             assert 1 <= gnx <= 256 and 1 <= gny <= 256 and entries >= 0
             assert 0 <= lds <= 64 * 1024
     assert res["field512_6000"]["grids"][2][3] == 0  # zero budget: no grid-only image
+    # the inside bitmap (point_blocked): cells set on a dense field, and every point a set cell
+    # maps to lies inside a disc
+    for name, r in res.items():
+        if "inside" in r:
+            assert r["inside"][1] == 0, (name, r["inside"])
+    assert res["field512_6000"]["inside"][0] > 1000
     # invalid inputs are refused (PP_ERR_INVALID_ARGUMENT) with a message
     for name in ("bad_offsets", "nan_vertex", "ring_too_small", "empty_box", "inf_disc"):
         assert res[name]["rc"] == -1 and res[name]["err"], res[name]
