@@ -769,26 +769,47 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
     if (tid == 0) *s_nb = 0;
     __syncthreads();
     const double fx = 16.0 / (g.maxx - g.minx), fy = 16.0 / (g.maxy - g.miny);
-    for (int j = tid; j < W; j += NT) {
-        const uint64_t itj = (uint64_t)(start + j);
-        const double x = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
-        const double y = gen_range(g.seed, 2 * itj + 1, g.miny, g.maxy);
-        g.wsx[np][j] = x;
-        g.wsy[np][j] = y;
-        g.wsx32[np][j] = (float)x;
-        g.wsy32[np][j] = (float)y;
-        const bool bk = g.blk[np] && point_blocked<false, kSceneAny>(*g.scp, x, y);
-        if (g.blk[np]) g.blk[np][j] = bk ? 1 : 0;
-        const int cx = min(max((int)((x - g.minx) * fx), 0), 15);  // == sample_cell
-        const int cy = min(max((int)((y - g.miny) * fy), 0), 15);
-        const int cell = morton16(cx, cy);
-        s_cell[j] = (unsigned char)cell;
-        // a sample in an obstacle needs no nearest node and is nobody's candidate parent: it is
-        // sorted after the screened samples, out of the screen and the pair grid
-        if (bk)
-            atomicAdd(s_nb, 1);
-        else
-            atomicAdd(&s_hist[cell], 1);
+    // (kU samples per thread per pass: their pre-test loads are in flight together)
+    constexpr int kU = 4;
+    const bool pre = g.blk[np] != nullptr;
+    const SceneDev* scp = g.scp;
+    for (int j0 = tid; j0 < W; j0 += NT * kU) {
+        double xs[kU], ys[kU];
+        bool bks[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int j = j0 + u * NT;
+            xs[u] = ys[u] = 0.0;
+            if (j < W) {
+                const uint64_t itj = (uint64_t)(start + j);
+                xs[u] = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
+                ys[u] = gen_range(g.seed, 2 * itj + 1, g.miny, g.maxy);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            bks[u] = pre && j0 + u * NT < W && point_blocked<false, kSceneAny>(*scp, xs[u], ys[u]);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int j = j0 + u * NT;
+            if (j >= W) continue;
+            const double x = xs[u], y = ys[u];
+            g.wsx[np][j] = x;
+            g.wsy[np][j] = y;
+            g.wsx32[np][j] = (float)x;
+            g.wsy32[np][j] = (float)y;
+            if (pre) g.blk[np][j] = bks[u] ? 1 : 0;
+            const int cx = min(max((int)((x - g.minx) * fx), 0), 15);  // == sample_cell
+            const int cy = min(max((int)((y - g.miny) * fy), 0), 15);
+            const int cell = morton16(cx, cy);
+            s_cell[j] = (unsigned char)cell;
+            // a sample in an obstacle needs no nearest node and is nobody's candidate parent: it
+            // is sorted after the screened samples, out of the screen and the pair grid
+            if (bks[u])
+                atomicAdd(s_nb, 1);
+            else
+                atomicAdd(&s_hist[cell], 1);
+        }
     }
     __syncthreads();
     const int Ws = W - *s_nb;  // screened samples: sorted positions [0, Ws)
