@@ -87,9 +87,9 @@ def parse(argv=None):
                     help="config3: iterations per query evaluated speculatively per GPU step "
                          "(power of two <= 64; 0 = automatic)")
     ap.add_argument("--max-iter", type=int, default=2000, help="config3/5: RRT.max_iter per query")
-    ap.add_argument("--schedule", choices=("persistent", "lockstep"), default="persistent",
-                    help="config3: one persistent launch per extend call (default) or four "
-                         "launches per lockstep step (pp_batch_set_schedule; identical trees)")
+    ap.add_argument("--schedule", choices=("persistent", "lockstep"), default="lockstep",
+                    help="config3: four launches per lockstep step (default) or one persistent "
+                         "launch per extend call (pp_batch_set_schedule; identical trees)")
     ap.add_argument("--window", type=int, default=4096)
     ap.add_argument("--nodes", type=int, default=100_000, help="tree size before timing")
     ap.add_argument("--seed", type=int, default=42)

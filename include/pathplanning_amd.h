@@ -258,11 +258,11 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
  * sequential run.  Applies to the current batch and the next ones. */
 int pp_batch_set_window(pp_ctx* ctx, int k);
 /* How pp_batch_extend runs a batch (results are identical):
- *   PP_BATCH_PERSISTENT (default)  one launch per call: every workgroup takes queries from a
+ *   PP_BATCH_LOCKSTEP (default)    four launches per step over the whole batch (two sub-batch
+ *                                  streams), the host topping up queries whose windows stopped;
+ *   PP_BATCH_PERSISTENT            one launch per call: every workgroup takes queries from a
  *                                  counter and steps their windows itself (samples + nearest node,
- *                                  steer, collide, insert) until each reaches its target;
- *   PP_BATCH_LOCKSTEP              four launches per step over the whole batch (two sub-batch
- *                                  streams), the host topping up queries whose windows stopped. */
+ *                                  steer, collide, insert) until each reaches its target. */
 #define PP_BATCH_PERSISTENT 0
 #define PP_BATCH_LOCKSTEP 1
 int pp_batch_set_schedule(pp_ctx* ctx, int schedule);

@@ -194,7 +194,7 @@ struct pp_ctx {
     DBuf<PrepRec> mq_rec;
     DBuf<DevState> mq_state;      // [3]: the whole batch, then one per sub-batch (mq_sub_args)
     hipStream_t sub_stream[4] = {};  // sub-batch streams 1.. (0 is `stream`), created on first use
-    int mq_sched = PP_BATCH_PERSISTENT;  // pp_batch_set_schedule
+    int mq_sched = PP_BATCH_LOCKSTEP;  // pp_batch_set_schedule (the faster one: DESIGN.md §3.4)
     DBuf<int> pq_next;                   // the persistent kernel's query counter
     DBuf<long long> pq_tally;            // its tally (PqArgs::tally): kPqTally counters
     DBuf<SceneDev> pq_scene;             // the scene in device memory (PqArgs::sc_global)

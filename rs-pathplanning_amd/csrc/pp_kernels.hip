@@ -772,7 +772,37 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
     // (kU samples per thread per pass: their pre-test loads are in flight together)
     constexpr int kU = 4;
     const bool pre = g.blk[np] != nullptr;
-    const SceneDev* scp = g.scp;
+    // the pre-test's scene fields, loaded once (through the pointer they would be reloaded after
+    // every store below, which the compiler cannot prove disjoint)
+    SceneDev scl{};
+    if (pre) {
+        scl.bits = g.scp->bits;
+        scl.bw = g.scp->bw;
+        scl.bh = g.scp->bh;
+        scl.bwords = g.scp->bwords;
+        scl.bx0 = g.scp->bx0;
+        scl.by0 = g.scp->by0;
+        scl.binv = g.scp->binv;
+        scl.ne = g.scp->ne;
+        scl.nbv = g.scp->nbv;
+        scl.m = g.scp->m;
+        scl.ibits = g.scp->ibits;
+        scl.ibn = g.scp->ibn;
+        scl.ibwords = g.scp->ibwords;
+        scl.ibx0 = g.scp->ibx0;
+        scl.iby0 = g.scp->iby0;
+        scl.ibinv = g.scp->ibinv;
+        scl.goff = g.scp->goff;
+        scl.gitems = g.scp->gitems;
+        scl.cx = g.scp->cx;
+        scl.cy = g.scp->cy;
+        scl.r2 = g.scp->r2;
+        scl.gx0 = g.scp->gx0;
+        scl.gy0 = g.scp->gy0;
+        scl.ginv = g.scp->ginv;
+        scl.gnx = g.scp->gnx;
+        scl.gny = g.scp->gny;
+    }
     for (int j0 = tid; j0 < W; j0 += NT * kU) {
         double xs[kU], ys[kU];
         bool bks[kU];
@@ -788,7 +818,7 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u)
-            bks[u] = pre && j0 + u * NT < W && point_blocked<false, kSceneAny>(*scp, xs[u], ys[u]);
+            bks[u] = pre && j0 + u * NT < W && point_blocked<false, kSceneAny>(scl, xs[u], ys[u]);
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int j = j0 + u * NT;

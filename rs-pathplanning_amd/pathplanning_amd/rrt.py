@@ -424,13 +424,14 @@ class RRTBatch:
     plan_one extend iteration (rrt.rs:583-589) of every query per step — on one GPU.  ``window``:
     iterations per query evaluated speculatively per GPU step (a power of two <= 64, 0 =
     automatic: 16 up to 131072 tasks per step); every query's tree equals its sequential run.
-    ``schedule``: "persistent" (one launch per extend call, every workgroup stepping its own
-    queries) or "lockstep" (four launches per step over the whole batch) — identical trees."""
+    ``schedule``: "lockstep" (four launches per step over the whole batch; the default, the faster
+    one here) or "persistent" (one launch per extend call, every workgroup stepping its own
+    queries) — identical trees."""
 
     SCHEDULES = {"persistent": _ffi.PP_BATCH_PERSISTENT, "lockstep": _ffi.PP_BATCH_LOCKSTEP}
 
     def __init__(self, starts, goals, max_iter, step_size, space: Space, seeds, device: int = 0,
-                 ctx: _ffi.Context | None = None, window: int = 0, schedule: str = "persistent"):
+                 ctx: _ffi.Context | None = None, window: int = 0, schedule: str = "lockstep"):
         self.ctx = ctx or _ffi.Context(device)
         self.space = space
         starts = np.ascontiguousarray(starts, dtype=np.float64).reshape(-1, 3)
