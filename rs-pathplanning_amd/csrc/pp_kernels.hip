@@ -2327,139 +2327,6 @@ inline void launch_walk(hipStream_t s, int blocks, DevState* st, const SceneDev&
     });
 }
 
-// The query batch's steer in ONE launch (round 4; replaces steer_prep + steer_walk on the
-// lockstep schedule): each wave takes 8 of its workgroup's strided tasks at a time from the LDS
-// counter, preps them on its eight 8-lane groups into its 8 LDS records (prep_task, out of line:
-// its chains need more registers than the walk's budget), then walks them one by one.  The
-// records never reach HBM and a step has one launch less.  A task whose sample lies in an
-// obstacle (pnode -2) or an idle slot (pnode -1) gets a kReject record and no walk.
-__device__ __noinline__ void wb_prep8(double step, double turn_radius,
-                                      const SteerTask* __restrict__ tasks, int t0, int G,
-                                      int total, PrepRec* lrec, double* __restrict__ yaw_out) {
-    SceneDev sc;  // prep_task reads only the step and the radius
-    sc.step_size = step;
-    sc.turn_radius = turn_radius;
-    const int lane = threadIdx.x & 63, i = lane >> 3;
-    const int t = t0 + G * i;
-    const bool in = t < total;
-    bool act = false;
-    double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0;
-    if (in) {
-        const SteerTask tk = tasks[t];
-        act = tk.pnode >= 0;
-        x = tk.x;
-        y = tk.y;
-        if (act) {
-            px = tk.px;
-            py = tk.py;
-            pyaw = tk.pyaw;
-        }
-    }
-    prep_task(sc, lane & 7, lane & ~7, i, in, act, x, y, px, py, pyaw, 0, 0.0, 0, 0.0, 0.0, lrec,
-              in ? yaw_out + t : nullptr, nullptr);
-}
-
-constexpr int kPwRecs = 8;  // records per wave
-__host__ __device__ inline int prepwalk_lds_bytes(int scene_bytes) {
-    return scene_bytes + kWalkThreads / 64 * (kGenSlots * 8 + kPwRecs * (int)sizeof(PrepRec));
-}
-
-template <bool kLds, int kMinW, int kScene>
-__global__ __launch_bounds__(kWalkThreads, kMinW) void steer_prepwalk_kernel(
-    const DevState* __restrict__ st, SceneDev sc, const SteerTask* __restrict__ tasks,
-    int* __restrict__ status, double* __restrict__ yaw, long long* __restrict__ wg_points) {
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int total = st->W + st->ncomp;
-    if ((int)blockIdx.x >= total) return;
-    if (kLds) stage_scene(sc);
-    char* base = pp_smem + (kLds ? sc.lds_bytes : 0);
-    double* gs = reinterpret_cast<double*>(base) + wave * kGenSlots;
-    PrepRec* lrec = reinterpret_cast<PrepRec*>(base + kWalkThreads / 64 * kGenSlots * 8) +
-                    wave * kPwRecs;
-    int npts = 0, napts = 0;
-    __shared__ int s_next;
-    const int G = (int)gridDim.x;
-    if (threadIdx.x == 0) s_next = 0;
-    __syncthreads();
-    for (;;) {
-        int k = 0;
-        if (lane == 0) k = atomicAdd(&s_next, kPwRecs);
-        const int k0 = __builtin_amdgcn_readlane(k, 0);
-        const int t0 = (int)blockIdx.x + G * k0;
-        if (t0 >= total) break;
-        // any task of the 8 to steer?  (idle slots and samples in an obstacle need no prep)
-        const int ti = t0 + G * (lane >> 3);
-        const bool need = (lane & 7) == 0 && ti < total && tasks[ti].pnode >= 0;
-        if (__any(need)) {
-            wb_prep8(sc.step_size, sc.turn_radius, tasks, t0, G, total, lrec, yaw);
-            __builtin_amdgcn_wave_barrier();
-        }
-        for (int i = 0; i < kPwRecs; ++i) {
-            const int t = t0 + G * i;
-            if (t >= total) break;
-            const int pn = __builtin_amdgcn_readfirstlane(tasks[t].pnode);
-            const int s = pn >= 0 ? walk_rec<kLds, kScene>(sc, &lrec[i], nullptr, gs, npts, napts)
-                                  : kReject;
-            if (lane == 0) status[t] = s;
-        }
-    }
-    if (wg_points) {  // [b]: points, [kWalkTallySlots + b]: their arc points
-        __shared__ int s_np[2][kWalkThreads / 64];
-        if (lane == 0) {
-            s_np[0][threadIdx.x >> 6] = npts;
-            s_np[1][threadIdx.x >> 6] = napts;
-        }
-        __syncthreads();
-        if (threadIdx.x < 2) {
-            long long sum = 0;
-            for (int w = 0; w < kWalkThreads / 64; ++w) sum += s_np[threadIdx.x][w];
-            wg_points[blockIdx.x + threadIdx.x * kWalkTallySlots] += sum;
-        }
-    }
-}
-
-template <int kMinW, typename F>
-inline hipError_t prepwalk_kernel_for(const SceneDev& sc, F&& f) {
-    const bool lds = sc.lds_bytes > 0;
-    switch (scene_kind(sc)) {
-        case kSceneGrid:
-            return lds ? f(steer_prepwalk_kernel<true, kMinW, kSceneGrid>)
-                       : f(steer_prepwalk_kernel<false, kMinW, kSceneGrid>);
-        case kScenePoly:
-            return lds ? f(steer_prepwalk_kernel<true, kMinW, kScenePoly>)
-                       : f(steer_prepwalk_kernel<false, kMinW, kScenePoly>);
-        default:
-            return lds ? f(steer_prepwalk_kernel<true, kMinW, kSceneDisc>)
-                       : f(steer_prepwalk_kernel<false, kMinW, kSceneDisc>);
-    }
-}
-
-template <int kMinW, int kMaxPerCU>
-inline int prepwalk_grid_cap(const SceneDev& sc) {
-    static std::mutex mu;
-    static std::map<std::tuple<int, int, int>, int> cache;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    std::lock_guard<std::mutex> lk(mu);
-    const std::tuple<int, int, int> key{dev, sc.lds_bytes, scene_kind(sc)};
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    int cus = 256, per_cu = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
-        cus = prop.multiProcessorCount;
-    const hipError_t e = prepwalk_kernel_for<kMinW>(sc, [&](auto kern) {
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kWalkThreads,
-                                                            prepwalk_lds_bytes(sc.lds_bytes));
-    });
-    if (e != hipSuccess || per_cu < 1) per_cu = 1;
-    per_cu = std::min(kMaxPerCU, per_cu);
-    const int cap = cus * per_cu;
-    cache[key] = cap;
-    return cap;
-}
-
 // A resolve repair (one wave): the (child, parent pose) pair steered and collision-checked anew
 // (only resolve_tail_kernel compiles it: inlined there it needs no scratch).
 __device__ __forceinline__ int resolve_repair(const SceneDev& sc, double x, double y,
@@ -3753,10 +3620,6 @@ hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int
     return hipGetLastError();
 }
 
-// the lockstep batch steers with steer_prepwalk_kernel (one launch) instead of steer_prep +
-// steer_walk
-constexpr bool kBatchPrepInWalk = false;
-
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int Q = a.mq.Q;
     const int T = Q * a.mq.K;  // tasks per step
@@ -3765,31 +3628,19 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
                                      std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch, 2>(a.sc)));
     const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
-    const int pw_blocks =
-        kBatchPrepInWalk ? std::min((T + kPwRecs * kWalkThreads / 64 - 1) / (kPwRecs * kWalkThreads / 64),
-                                    std::min(kWalkMaxWG, prepwalk_grid_cap<kWalkMinWBatch, 2>(a.sc)))
-                         : 0;
+
     for (int k = 0; k < steps; ++k) {
         hipEvent_t* ev = a.ev ? a.ev + 5 * k : nullptr;
         if (ev) (void)hipEventRecord(ev[0], s);
         mq_sample_nn_kernel<<<nn_blocks, 256, 0, s>>>(a.mq, a.sc.minx, a.sc.maxx, a.sc.miny,
                                                       a.sc.maxy, a.tasks, a.scp);
         if (ev) (void)hipEventRecord(ev[1], s);
-        if (kBatchPrepInWalk) {  // one launch: the waves prep their own tasks (records in LDS)
-            if (ev) (void)hipEventRecord(ev[2], s);
-            (void)prepwalk_kernel_for<kWalkMinWBatch>(a.sc, [&](auto kern) {
-                kern<<<pw_blocks, kWalkThreads, prepwalk_lds_bytes(a.sc.lds_bytes), s>>>(
-                    a.st, a.sc, a.tasks, a.status, a.yaw, a.wg_points);
-                return hipSuccess;
-            });
-        } else {
-            steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, nullptr, nullptr,
-                                                                  nullptr, nullptr, a.rec, a.pdbuf,
-                                                                  a.yaw, a.tasks);
-            if (ev) (void)hipEventRecord(ev[2], s);
-            launch_walk<kWalkMinWBatch>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf, nullptr,
-                                        a.status, nullptr, nullptr, a.wg_points);
-        }
+        steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, nullptr, nullptr,
+                                                              nullptr, nullptr, a.rec, a.pdbuf,
+                                                              a.yaw, a.tasks);
+        if (ev) (void)hipEventRecord(ev[2], s);
+        launch_walk<kWalkMinWBatch>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf, nullptr,
+                                    a.status, nullptr, nullptr, a.wg_points);
         if (ev) (void)hipEventRecord(ev[3], s);
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
                                                     a.lit_scratch, a.lit_locks, a.err);
