@@ -162,6 +162,9 @@ struct pp_ctx {
     DBuf<int> r_order, r_rep, pend, fin_par;
     DBuf<unsigned char> blk;   // [2 Kcap] window samples in an obstacle (point_blocked)
     DBuf<SceneDev> d_scene;    // the scene in device memory (samples_role, the literal paths)
+    DBuf<SceneDev> cf_scene;   // check_finish_kernel's scene (its step may be a batch's)
+    SceneDev cf_scene_host{};  // what cf_scene holds (the source of its last upload)
+    bool cf_scene_ok = false;
     DBuf<double> r_repyaw;
     DBuf<double> lit_scratch;  // resolve: one literal buffer per wave
     // verify_node API
@@ -550,7 +553,17 @@ int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line,
     }
     SceneDev sd = c->scene_dev();
     if (cb.qidx) sd.step_size = c->mq_step;  // a query batch's edges use the batch's step
-    PP_HIP(launch_check_finish(c->stream, sd, tr, nodes, k, g->x, g->y,
+    // check_finish_kernel reads the scene from device memory (a reference to the kernel-argument
+    // struct would copy it to every lane's stack); uploaded when it changed.  The stream is
+    // synchronised at the end of every cf_run, so the host copy is never overwritten in flight.
+    if (!c->cf_scene_ok || std::memcmp(&c->cf_scene_host, &sd, sizeof sd) != 0) {
+        if (!c->cf_scene.p) PP_HIP(c->cf_scene.reserve(1));
+        c->cf_scene_host = sd;
+        PP_HIP(hipMemcpyAsync(c->cf_scene.p, &c->cf_scene_host, sizeof sd,
+                              hipMemcpyHostToDevice, c->stream));
+        c->cf_scene_ok = true;
+    }
+    PP_HIP(launch_check_finish(c->stream, sd, c->cf_scene.p, tr, nodes, k, g->x, g->y,
                                g->yaw, g->yaw_opt, g->level0, g->mode, want_line, o.ok, o.len,
                                o.npts, o.chain, c->api_lit_scratch.p, c->lit_locks.p,
                                want_line ? c->cf_pts.p : nullptr, kCfPtsCap,

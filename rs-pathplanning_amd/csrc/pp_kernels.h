@@ -95,7 +95,8 @@ struct CfBatch {
     int* ftab = nullptr;
     int* gtab = nullptr;
 };
-hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev& tr,
+hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const SceneDev* scg,
+                               const TreeDev& tr,
                                const int* nodes, int k, double gx, double gy, double gyaw,
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,

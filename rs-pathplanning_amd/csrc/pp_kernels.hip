@@ -229,6 +229,151 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     return false;
 }
 
+// ------------------------------------------------ straight segments, analytically (round 4)
+//
+// The S segment of LSL / LSR / RSL / RSR (segment 1) puts its grid points at A + (pd / c) u: A
+// its origin, u its world direction, pd the generator's values (interpolate's S branch and the
+// world transform, dubins.rs:168-171, 412-422), up to a few ulps of the coordinates (< 1e-12
+// relative).  Against the discs of a Q10 scene, with dl = 1e-9 (1 + |A| + |B|) far above that
+// rounding:
+//   kSClear    every disc centre lies farther than r + dl from the ideal segment AB, and A, B lie
+//              dl inside the bounds: every S point and every polyline segment between two S
+//              points then lies farther than r from every centre and inside the bounds, so the
+//              walk keeps only the first and the last S point (the chord between them clears
+//              too) — the verdict is the one of the full polyline;
+//   kSHit      some disc's (r - dl) chord on AB, clipped to the stretch the S points surely
+//              cover (from 3d past A: the first pd is at most 3d, dubins.rs:239-241; to d
+//              before B), is longer than the points' spacing: an S point lies strictly inside
+//              the disc, and verify rejects (rrt.rs:124-137) whatever the other segments;
+//   kSUnknown  otherwise: the walk tests every point.
+// The discs come from the item grid's cells that AB's box (widened by dl) touches: a disc within
+// r + dl of AB has its cull box (>= r) in one of them.  Called by all 64 lanes; returns a
+// wave-uniform class.
+enum : int { kSUnknown = 0, kSClear = 1, kSHit = 2 };
+constexpr int kSMinPts = 24;     // S segments shorter than this many points are walked as they are
+constexpr int kSMaxCells = 256;  // ... and so are those whose box spans more item-grid cells
+template <bool kLds>
+__device__ int s_classify(const SceneDev& sc, double ax, double ay, double bx, double by,
+                          double t_lo, double t_hi, double gap, double dl) {
+    const int lane = threadIdx.x & 63;
+    const double ux0 = bx - ax, uy0 = by - ay;
+    const double len = sqrt(ux0 * ux0 + uy0 * uy0);
+    if (!(len > 0.0)) return kSUnknown;
+    const double ux = ux0 / len, uy = uy0 / len;
+    int res = (fmin(ax, bx) >= sc.minx + dl && fmax(ax, bx) <= sc.maxx - dl &&
+               fmin(ay, by) >= sc.miny + dl && fmax(ay, by) <= sc.maxy - dl)
+                  ? kSClear
+                  : kSUnknown;
+    const int cx0 = __builtin_amdgcn_readfirstlane(grid_cell(fmin(ax, bx) - dl, sc.gx0, sc.ginv, sc.gnx));
+    const int cx1 = __builtin_amdgcn_readfirstlane(grid_cell(fmax(ax, bx) + dl, sc.gx0, sc.ginv, sc.gnx));
+    const int cy0 = __builtin_amdgcn_readfirstlane(grid_cell(fmin(ay, by) - dl, sc.gy0, sc.ginv, sc.gny));
+    const int cy1 = __builtin_amdgcn_readfirstlane(grid_cell(fmax(ay, by) + dl, sc.gy0, sc.ginv, sc.gny));
+    const int ncx = cx1 - cx0 + 1, ncell = ncx * (cy1 - cy0 + 1);
+    if (ncell > kSMaxCells) return kSUnknown;
+    const int* goff = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_goff) : sc.goff;
+    const int* items = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_items) : sc.gitems;
+    for (int cb = 0; cb < ncell; cb += 64) {
+        // lane c: cell cb + c's item range; the cells' items are then dealt to the lanes as one
+        // list, 64 at a time (a disc listed in several cells is tested several times)
+        const int nb = min(64, ncell - cb);
+        int k0v = 0, cntv = 0;
+        if (lane < nb) {
+            const int cl = cb + lane, ry = cl / ncx;
+            const int cell = (cy0 + ry) * sc.gnx + cx0 + (cl - ry * ncx);
+            k0v = goff[cell];
+            cntv = goff[cell + 1] - k0v;
+        }
+        for (int mb = 0;; mb += 64) {
+            const int m = mb + lane;
+            int kk = -1, run = 0;
+            for (int c = 0; c < nb; ++c) {
+                const int b = __builtin_amdgcn_readlane(k0v, c), n = __builtin_amdgcn_readlane(cntv, c);
+                if (m >= run && m < run + n) kk = b + (m - run);
+                run += n;
+            }
+            bool near = false, hit = false;
+            if (kk >= 0) {
+                const int d = items[kk];
+                const double wx = sc.cx[d] - ax, wy = sc.cy[d] - ay;
+                const double t = wx * ux + wy * uy;
+                const double tc = fmin(fmax(t, 0.0), len);
+                const double ex = wx - tc * ux, ey = wy - tc * uy;
+                const double rr = sqrt(sc.r2[d]);
+                const double ro = rr + dl;
+                near = ex * ex + ey * ey <= ro * ro;
+                const double px = wx - t * ux, py = wy - t * uy;
+                const double p2 = px * px + py * py, ri = rr - dl;
+                if (ri > 0.0 && p2 < ri * ri) {
+                    const double h = sqrt(ri * ri - p2) - dl;
+                    hit = fmin(t + h, t_hi) - fmax(t - h, t_lo) >= gap;
+                }
+            }
+            if (__any(hit)) return kSHit;
+            if (__any(near)) res = kSUnknown;
+            if (mb + 64 >= run) break;
+        }
+    }
+    return res;
+}
+
+// Count-only run of the `pd += d` generator over one segment from its first value w (the same
+// passes as walk_rec's generator, every lane a value: the closed form inside a binade, else the
+// serial chain through the wave's LDS slots gs): n values with |pd| <= |Ls|, the last of them
+// and the first one past (the segment's end, dubins.rs:243-256).  Wave-uniform results.
+__device__ inline void seg_count(double w, double dd, double Ls, double* __restrict__ gs,
+                                 long long& n, double& last, double& exitv) {
+    const int lane = threadIdx.x & 63;
+    const double aL = fabs(Ls);
+    n = 0;
+    last = w;
+    for (;;) {
+        int u = 63;
+        double v = w;
+        const double w1 = w + dd, w2 = w1 + dd;
+        bool cf = (w1 - w) == (w2 - w1);
+        if (cf) {
+            const double vc = __builtin_fma((double)lane, w1 - w, w);
+            const uint64_t fm = __ballot(!(fabs(vc) <= aL));
+            const int fl = fm ? (int)__builtin_ctzll(fm) : 63;
+            cf = __ballot(lane <= fl && (__double2hiint(vc) >> 20) != (__double2hiint(w) >> 20)) == 0;
+            v = vc;
+        }
+        if (!cf) {
+            double s = w;
+            if (lane == 0) gs[0] = s;
+            u = 0;
+            bool ended = !(fabs(s) <= aL);
+            while (!ended && u < 63) {
+                double t4[4];
+#pragma unroll
+                for (int z = 0; z < 4; ++z) {
+                    s += dd;
+                    t4[z] = s;
+                }
+                if (lane == 0) {
+#pragma unroll
+                    for (int z = 0; z < 4; ++z) gs[u + 1 + z] = t4[z];
+                }
+                u += 4;
+                ended = !(fabs(s) <= aL);
+            }
+            u = min(u, 63);
+            __builtin_amdgcn_wave_barrier();
+            v = lane <= u ? gs[lane] : w;
+            __builtin_amdgcn_wave_barrier();
+        }
+        const uint64_t bad = __ballot(lane > u || !(fabs(v) <= aL));
+        const int m = bad ? (int)__builtin_ctzll(bad) : 64;
+        n += m;
+        if (m > 0) last = readlane_f64(v, m - 1);
+        if (m <= 63) {
+            exitv = readlane_f64(v, m);
+            return;
+        }
+        w = readlane_f64(v, 63) + dd;
+    }
+}
+
 // Point 0 of a candidate's line — the sample itself — inside an obstacle: the line is rejected
 // whatever its parent and its Dubins path (verify, rrt.rs:124-137: the first segment starts inside
 // the disc / on an occupied cell), so the candidate needs neither steer_prep nor steer_walk and its
@@ -1993,6 +2138,29 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     static_assert(kPdCap % 63 == 0, "stored points end on a chunk boundary");
     double carry_x = x, carry_y = y;
     npts += 1;  // point 0, the child
+    // a long S segment against the discs, analytically (s_classify): a sure hit rejects at once,
+    // a sure clearance keeps only its first and last point (s_state 1: counted, s_emit of them
+    // placed in lanes so far)
+    bool s_clear = false;
+    int s_state = 0, s_emit = 0;
+    long long s_n = 0;
+    double s_first = 0.0, s_last = 0.0, s_exit = 0.0;
+    const bool discs = (kScene == kSceneDisc ||
+                        (kScene == kSceneAny && !sc.bits && sc.ne == 0 && sc.nbv == 0)) &&
+                       sc.m > 0;
+    if (discs && partial && ng == 0 && m1 == kModeS && L1 >= kSMinPts * step) {
+        const double ax = cw * ox1 + sw * oy1 + x, ay = -sw * ox1 + cw * oy1 + y;
+        const double pcb = div_by(L1, c, rc);
+        const double lxb = ox1 + pcb * ca1, lyb = oy1 + pcb * sa1;
+        const double bx = cw * lxb + sw * lyb + x, by = -sw * lxb + cw * lyb + y;
+        const double dl = 1.0e-9 * (1.0 + fabs(ax) + fabs(ay) + fabs(bx) + fabs(by));
+        const double sp = step * rc;  // the S points' spacing along AB
+        const int cls = s_classify<kLds>(sc, ax, ay, bx, by, 3.0 * sp * (1.0 + 1.0e-9) + dl,
+                                         (L1 - step) * rc * (1.0 - 1.0e-9) - dl,
+                                         sp * (1.0 + 1.0e-9) + 2.0 * dl, dl);
+        if (cls == kSHit) return kReject;
+        s_clear = cls == kSClear;
+    }
     for (int base = 0;; base += 63) {
         int cnt = 0, my_seg = 0;
         double my_pd = 0.0;
@@ -2005,6 +2173,33 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
             // gives ll and the next segment's start, dubins.rs:256-259)
             int pos = 1;
             while (pos <= 63 && gseg < 3) {
+                if (s_clear && gseg == 1) {
+                    // the cleared S segment: its first and last points only (s_classify), the
+                    // rest counted; then the segment's end as the generator would reach it
+                    if (s_state == 0) {
+                        seg_count(gpd, gdd, L1, gs, s_n, s_last, s_exit);
+                        s_first = gpd;
+                        s_state = 1;
+                    }
+                    const int n_emit = s_n >= 2 ? 2 : (int)s_n;
+                    while (s_emit < n_emit && pos <= 63) {
+                        if (lane == pos) {
+                            my_seg = 1;
+                            my_pd = s_emit == 0 ? s_first : s_last;
+                        }
+                        ++s_emit;
+                        ++pos;
+                        ++cnt;
+                    }
+                    if (s_emit < n_emit) break;  // the chunk is full: the next one goes on
+                    grid += s_n - n_emit;
+                    npts += s_n - n_emit;
+                    const double ll = L1 - s_exit - gdd;
+                    gseg = 2;
+                    gdd = (L2 > 0.0) ? step : -step;
+                    gpd = ((L1 * L2) > 0.0) ? (-gdd - ll) : (gdd - ll);
+                    continue;
+                }
                 const double Ls = gseg == 0 ? L0 : (gseg == 1 ? L1 : L2);
                 // the serial chain w_u = gpd (+ gdd) x u is the same in every lane: one f64 add
                 // per step, lane 0 parks the values in the wave's LDS slots (gs) and lane pos + u
@@ -2886,29 +3081,52 @@ __device__ __forceinline__ void lit_release(int* locks, int slot) {
 // The edge's steer_prep runs on the wave's eight 8-lane groups (prep_task: the word choice across
 // a group's lanes, ~9 transcendental calls deep instead of ~32 on one lane), every group on the
 // same edge; group 0 writes the record to the wave's LDS slot lrec, which walk_rec then walks.
-// Inlined at its two call sites: as a call, its frame spilled 512 B per lane around every edge
-// (the config-3 batch plan's check_finish 103 -> 80 ms inlined, 96 B of scratch left).
-template <bool kAllowNone>
-__device__ __forceinline__ long long cf_edge_check(const SceneDev& sc, CfPose a,
-                                                             CfPose b, bool junction,
-                                                             double* lit_scratch, int* lit_locks,
-                                                             double* gs, PrepRec* lrec) {
+// ONE out-of-line body for both call sites, reading the scene through a device-memory pointer
+// (round 4): a reference to the kernel-argument SceneDev would copy the struct to the stack, and
+// inlined at two sites (round 3) the kernel sat at 256 VGPRs with 608 B/lane of scratch and 571
+// SGPR spills (the literal call's save area) — 2 waves per SIMD.
+// the edge's prep and walk as separate bodies: each gets its own register allocation under the
+// kernel's budget (one inlined body held both chains' values at once)
+__device__ __noinline__ void cf_prep(const SceneDev* __restrict__ scg, double ax, double ay,
+                                     double ayaw, double bx, double by, double byaw,
+                                     PrepRec* lrec) {
     const int lane = threadIdx.x & 63;
-    prep_task(sc, lane & 7, lane & ~7, 0, lane < 8, true, a.x, a.y, b.x, b.y, b.yaw, 1, a.yaw, 0,
+    prep_task(*scg, lane & 7, lane & ~7, 0, lane < 8, true, ax, ay, bx, by, byaw, 1, ayaw, 0,
               0.0, 0.0, lrec, nullptr, nullptr);
+}
+__device__ __noinline__ int cf_walk(const SceneDev* __restrict__ scg, const PrepRec* lrec,
+                                    double* gs, bool junction, int& walked, int& walked_arc) {
+    int w = 0, wa = 0;
+    const int st = walk_rec<false>(*scg, lrec, nullptr, gs, w, wa, junction);
+    walked = w;
+    walked_arc = wa;
+    return st;
+}
+__device__ __noinline__ long long cf_edge_check(const SceneDev* __restrict__ scg, double ax,
+                                                double ay, double ayaw, double bx, double by,
+                                                double byaw, int flags, double* lit_scratch,
+                                                int* lit_locks, double* gs, PrepRec* lrec) {
+    const SceneDev& sc = *scg;
+    const bool junction = flags & 1, allow_none = flags & 2;
+    cf_prep(scg, ax, ay, ayaw, bx, by, byaw, lrec);
     __builtin_amdgcn_wave_barrier();
-    if (!kAllowNone && lrec->state == kPrepNone) return kCfPanic;
+    if (!allow_none && ufl(lrec->state) == kPrepNone) return kCfPanic;
     int walked = 0, walked_arc = 0;
-    int st = walk_rec<false>(sc, lrec, nullptr, gs, walked, walked_arc, junction);
+    int st = cf_walk(scg, lrec, gs, junction, walked, walked_arc);
     if (st == kLiteral) {  // (measure-zero) a scratch buffer from the pool, for this edge only
         const int slot = lit_acquire(lit_locks, (int)blockIdx.x);
-        double* bx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
-        st = steer_collide_literal(sc, a.x, a.y, a.yaw, b.x, b.y, b.yaw, bx, bx + kLiteralCap,
-                                   bx + 2 * kLiteralCap, junction);
+        double* sx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
+        st = steer_collide_literal(sc, ax, ay, ayaw, bx, by, byaw, sx, sx + kLiteralCap,
+                                   sx + 2 * kLiteralCap, junction);
         lit_release(lit_locks, slot);
     }
     return (long long)st | ((long long)walked << 4) | ((long long)walked_arc << 34);
 }
+
+// compute_yaw out of line: check_finish_kernel's own body is bookkeeping, and an inlined ocml
+// atan2 (its polynomial constants hoisted out of the item loop) held ~100 VGPRs live across the
+// edge calls
+__device__ __noinline__ double cf_atan2(double y, double x) { return atan2(y, x); }
 
 // n_point of dubins_path_planning(a → b) (dubins.rs:369), 0 when the steer is None
 __device__ inline int cf_npoint(const SceneDev& sc, CfPose a, CfPose b) {
@@ -2925,6 +3143,10 @@ __device__ inline int cf_npoint(const SceneDev& sc, CfPose a, CfPose b) {
     const double nq = trunc(tot / sc.step_size);
     if (!(nq >= 0.0) || nq > 1.0e8) return -1;
     return (int)nq + 7;
+}
+
+__device__ __noinline__ int cf_npoint_ool(const SceneDev* __restrict__ scg, CfPose a, CfPose b) {
+    return cf_npoint(*scg, a, b);
 }
 
 // mode kCfCheck: check_finish of nodes[b] (the goal node Node::new_goal(goal, node, gyaw));
@@ -2999,8 +3221,8 @@ __device__ inline int cf_path(const TreeDev& tr, int node, int* __restrict__ pat
 }
 
 
-__global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
-    SceneDev sc, TreeDev tr_in, const int* __restrict__ nodes, int k, double gx_in, double gy_in,
+__global__ __launch_bounds__(kCfThreads, kCfMinW) void check_finish_kernel(
+    const SceneDev* __restrict__ scg, TreeDev tr_in, const int* __restrict__ nodes, int k, double gx_in, double gy_in,
     double gyaw_in, double gyaw_opt_in, int level0, int mode, int want_line,
     int* __restrict__ ok_out, double* __restrict__ len_out,
     int* __restrict__ npts_out, int* __restrict__ chain_out, double* __restrict__ lit_scratch,
@@ -3009,6 +3231,7 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
     __shared__ __attribute__((aligned(16))) double s_gs[kCfWaves][kGenSlots];  // walk_rec's LDS, one set per wave
     __shared__ int s_pos[kCfWaves][kCfLevels];  // the optimize chain's path positions per wave
     __shared__ PrepRec s_rec[kCfWaves];          // the wave's edge record (cf_edge_check)
+    const SceneDev& sc = *scg;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int* path = gpath + ((size_t)blockIdx.x * kCfWaves + wave) * kCfMaxDepth;  // this wave's
@@ -3062,8 +3285,9 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
                 for (int m = 0; m <= L && !root_blocked; ++m) {
                     const int to = path[m];
                     const CfPose bt{tr.x[to], tr.y[to], tr.yaw[to]};
-                    const CfPose a{ax, ay, atan2(bt.y - ay, bt.x - ax)};
-                    const long long rv = cf_edge_check<true>(sc, a, bt, true, lit_scratch, lit_locks, gs, lrec);
+                    const CfPose a{ax, ay, cf_atan2(bt.y - ay, bt.x - ax)};
+                    const long long rv = cf_edge_check(scg, a.x, a.y, a.yaw, bt.x, bt.y, bt.yaw,
+                                                       3, lit_scratch, lit_locks, gs, lrec);
                     const int st = (int)(rv & 15);
                     ++t_edges;
                     t_pts += (rv >> 4) & 0x3fffffff;
@@ -3127,7 +3351,7 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
                 const int here = path[i == 0 ? D - 1 : pos[i - 1]];
                 const int to = path[pos[i]];
                 const double x = tr.x[here], y = tr.y[here];
-                return CfPose{x, y, atan2(tr.y[to] - y, tr.x[to] - x)};  // Node::new (compute_yaw)
+                return CfPose{x, y, cf_atan2(tr.y[to] - y, tr.x[to] - x)};  // Node::new (compute_yaw)
             }
             const int node = path[ps - (j - s - 1)];
             return CfPose{tr.x[node], tr.y[node], tr.yaw[node]};
@@ -3161,8 +3385,9 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
                 } else if (gm > 0) {
                     st = gm - 1;
                 } else if (!dup) {
-                    const long long rv = cf_edge_check<false>(sc, a, bp, e < E - 1, lit_scratch,
-                                                              lit_locks, gs, lrec);
+                    const long long rv = cf_edge_check(scg, a.x, a.y, a.yaw, bp.x, bp.y, bp.yaw,
+                                                       e < E - 1 ? 1 : 0, lit_scratch, lit_locks,
+                                                       gs, lrec);
                     st = (int)(rv & 15);
                     ++t_edges;
                     t_pts += (rv >> 4) & 0x3fffffff;
@@ -3193,7 +3418,7 @@ __global__ __launch_bounds__(kCfThreads, 2) void check_finish_kernel(
         if (bad == 0 && (!vok || E > Ev)) {
             bool none = false;
             for (int e = (vok ? Ev : 0) + lane; e < E; e += 64)
-                if (cf_npoint(sc, pose(e), pose(e + 1)) == 0) none = true;
+                if (cf_npoint_ool(scg, pose(e), pose(e + 1)) == 0) none = true;
             if (__any(none)) bad = 2;
         }
         if ((vok || mode == kCfFinalize) && bad == 0 && want_line) {
@@ -3343,7 +3568,8 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
     }
 }
 
-hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev& tr,
+hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const SceneDev* scg,
+                               const TreeDev& tr,
                                const int* nodes, int k, double gx, double gy, double gyaw,
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,
@@ -3352,7 +3578,7 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const TreeDev
                                int* items) {
     if (k <= 0) return hipSuccess;
     const int wgs = std::min(grid, (k + kCfWaves - 1) / kCfWaves);
-    check_finish_kernel<<<wgs, kCfThreads, 0, st>>>(sc, tr, nodes, k, gx, gy, gyaw, gyaw_opt,
+    check_finish_kernel<<<wgs, kCfThreads, 0, st>>>(scg, tr, nodes, k, gx, gy, gyaw, gyaw_opt,
                                                     level0, mode, want_line, ok, len, npts, chain,
                                                     lit_scratch, lit_locks, err, tally, cb, gpath,
                                                     items);

@@ -32,11 +32,15 @@ constexpr int kPrepThreads = 256;    // steer_prep workgroup: 32 tasks (8 per wa
 constexpr int kWalkThreads = 512;    // steer_walk workgroup: 8 tasks at a time (3 workgroups per CU)
 constexpr int kWalkTallySlots = 4096;  // profiling: walk point tallies per workgroup (x2: arcs)
 constexpr int kCfMaxDepth = 8192;    // check_finish: ancestor path per wave, in a global buffer of
-                                     // grid * kCfWaves * kCfMaxDepth ints (kCfGrid 512: 64 MiB per
-                                     // context, allocated on the first check_finish)
+                                     // grid * kCfWaves * kCfMaxDepth ints (32 MiB per 256
+                                     // workgroups, allocated on the first check_finish)
 constexpr int kCfLevels = 16;        // RECURSION_LIMIT, rrt.rs:14
 constexpr int kCfMaxEdges = kCfLevels + 1 + kCfMaxDepth;
-constexpr int kCfGrid = 512;        // check_finish workgroups: 2 per CU (literal scratch: the pool)
+#ifndef PP_CF_MINW
+#define PP_CF_MINW 2
+#endif
+constexpr int kCfMinW = PP_CF_MINW;  // check_finish: waves per SIMD (its register budget)
+constexpr int kCfGrid = 256 * kCfMinW;  // check_finish workgroups: kCfMinW per CU
 
 // Scene in device memory (Space, rrt.rs:70-78, with Q10 analytic discs).
 struct SceneDev {

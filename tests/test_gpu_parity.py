@@ -269,6 +269,55 @@ def test_verify_node_batch_vs_oracle(pkg, ctx, oracle_mod):
         assert abs(gyaw[i] - eyaw) <= ANG_TOL
 
 
+def test_straight_segment_shortcut_vs_oracle(pkg, ctx, oracle_mod):
+    """The walk's analytic S-segment classes (s_classify: a sure hit rejects at once, a sure
+    clearance keeps the segment's first and last point) must not change a verdict: candidates
+    whose child -> parent line grazes an inflated disc (tangent at r + eps, eps from -1e-2 to
+    1e-2 and exactly 0), plus far parents (long S segments), against the oracle's full verify."""
+    from pathplanning_amd import scenes
+
+    raw = scenes.field512()
+    p = _planner(pkg, raw, 8, 4096, ctx)
+    p.extend(8000)
+    x, y, yaw, par = p.tree()
+    sc = oracle_mod.OracleScene.from_raw(raw)
+    otr = oracle_mod.OracleTree(raw["start"], len(x) + 1)
+    otr.x[:len(x)], otr.y[:len(x)], otr.yaw[:len(x)], otr.parent[:len(x)] = x, y, yaw, par
+    otr._c.n = len(x)
+    circ = np.asarray(raw["circles"], dtype=np.float64).reshape(-1, 3)
+    half = raw["robot"][0] / 2.0
+    rng = np.random.default_rng(7)
+    cx, cy, cp = [], [], []
+    epss = [0.0, 1e-12, -1e-12, 1e-9, -1e-9, 1e-6, -1e-6, 1e-4, -1e-4, 1e-2, -1e-2]
+    while len(cx) < 6000:
+        i = int(rng.integers(0, len(x)))
+        d = int(rng.integers(0, len(circ)))
+        ccx, ccy, rr = circ[d, 0], circ[d, 1], circ[d, 2] + half
+        dist = math.hypot(ccx - x[i], ccy - y[i])
+        rho = rr + epss[len(cx) % len(epss)]
+        if not (rho < dist < 120.0):
+            continue
+        a = math.asin(rho / dist) * (1 if rng.random() < 0.5 else -1)
+        b = math.atan2(ccy - y[i], ccx - x[i]) + a
+        ln = dist * math.cos(a) + rng.uniform(0.5, 30.0)
+        qx, qy = x[i] + ln * math.cos(b), y[i] + ln * math.sin(b)
+        if 0.5 < qx < 511.5 and 0.5 < qy < 511.5:
+            cx.append(qx)
+            cy.append(qy)
+            cp.append(i)
+    # far parents: long S segments across the field
+    far = rng.integers(0, len(x), 3000)
+    cx += list(rng.uniform(0.5, 511.5, 3000))
+    cy += list(rng.uniform(0.5, 511.5, 3000))
+    cp += list(far)
+    cx, cy, cp = np.array(cx), np.array(cy), np.array(cp, dtype=np.int32)
+    ok, _ = p.verify_node_batch(cx, cy, cp)
+    bad = [i for i in range(len(cx))
+           if bool(ok[i]) != oracle_mod.verify_candidate(sc, otr, cx[i], cy[i], int(cp[i]))[0]]
+    assert not bad, (len(bad), bad[:10])
+    assert 0 < int(np.sum(ok)) < len(ok)
+
+
 # ------------------------------------------------------------------------- full-size properties
 def test_100k_tree_properties(pkg, ctx, oracle_mod):
     """BASELINE config 2 at full size: grow past 100k nodes, then check size-independent
