@@ -206,6 +206,18 @@ struct pp_ctx {
     DBuf<double> mq_goal_d;       // [3Q] the goals on the device (pp_batch_plan)
     DBuf<int> mp_off, mp_qidx, mp_nodes, mp_ok, mp_npts, mp_best, mp_bpts, mp_nfin;
     DBuf<double> mp_len, mp_blen;
+    // pp_batch_plan's check_finish in steer rounds (CfbArgs)
+    DBuf<int> cfb_nodei;   // [4 (nitems + Q)]: depth, open, tfirst, tcnt
+    DBuf<int> cfb_rows;    // [3 rows]: gclaim, tnone, tnone_up
+    DBuf<int> cfb_gotab, cfb_plist, cfb_tnode, cfb_status, cfb_misc;
+    DBuf<SteerTask> cfb_tasks;
+    DBuf<StarTaskExt> cfb_ext;
+    DBuf<PrepRec> cfb_rec;
+    DBuf<double> cfb_yaw;
+    DBuf<DevState> cfb_state;
+    DBuf<long long> cfb_pts;  // profiling: the rounds' walk point tallies
+    int64_t cfb_nodes = 0, cfb_edges = 0, cfb_points = 0, cfb_arc = 0;  // profiling
+    bool cf_rounds = true;  // pp_batch_plan in steer rounds (PP_AMD_CF_ROUNDS=0: one kernel, A/B)
 
     // ---- RRT* query batch (BASELINE config 5, build-defined: DESIGN.md §3.7)
     bool has_star = false;
@@ -248,6 +260,7 @@ struct pp_ctx {
         batch_steps = batch_passes = 0;
         persist_ms = 0.0;
         persist_launches = 0;
+        cfb_nodes = cfb_edges = cfb_points = cfb_arc = 0;
         if (pq_tally.p && hipMemsetAsync(pq_tally.p, 0, pq_tally.n * sizeof(long long), stream) != hipSuccess)
             return PP_ERR_HIP;
         if (wg_pts.p && hipMemsetAsync(wg_pts.p, 0, wg_pts.n * sizeof(long long), stream) != hipSuccess)
@@ -587,6 +600,144 @@ int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line,
     return PP_OK;
 }
 
+// pp_batch_plan's check_finish in steer rounds (CfbArgs, pp_kernels.hip): phase A rounds fill
+// ftab for every node, phase B the goal and copy edges, the assemble kernel decides every item
+// whose verdicts are known, and check_finish_kernel runs the rest (literal paths, errors) with
+// the memo filled.  The same results as cf_run over all items; polygon scenes and batches with
+// a blocked root take cf_run.
+int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in, const CfOut& o) {
+    const int Q = c->mq_Q;
+    const size_t nn = (size_t)total + Q;
+    const size_t rows = (size_t)Q * (size_t)cb_in.row_cap;
+    const size_t cap_tasks = std::max<size_t>(4 * nn, 1);  // phase A: <= kCfbSpan per node; B: <= 2 per node
+    hipStream_t st = c->stream;
+    PP_HIP(c->cf_err.reserve(2));
+    PP_HIP(c->cf_memo.reserve(2 * std::max<size_t>(rows, 1)));
+    PP_HIP(c->cf_items.reserve(1 + (size_t)total * kCfItem));
+    const int wgs = std::min(kCfGrid, total);
+    PP_HIP(c->cf_pts.reserve((size_t)wgs * 3 * kCfPtsCap));
+    PP_HIP(c->cf_etab.reserve((size_t)wgs * 2 * kCfMaxEdges));
+    PP_HIP(c->cf_path.reserve((size_t)wgs * kCfWaves * kCfMaxDepth));
+    PP_HIP(c->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
+    if (!c->lit_locks.p) {
+        PP_HIP(c->lit_locks.reserve(kLiteralWaves));
+        PP_HIP(hipMemsetAsync(c->lit_locks.p, 0, kLiteralWaves * sizeof(int), st));
+    }
+    PP_HIP(c->cfb_nodei.reserve(4 * nn));
+    PP_HIP(c->cfb_rows.reserve(3 * std::max<size_t>(rows, 1)));
+    PP_HIP(c->cfb_gotab.reserve(std::max(total, 1)));
+    PP_HIP(c->cfb_plist.reserve(std::max(total, 1)));
+    PP_HIP(c->cfb_tnode.reserve(cap_tasks));
+    PP_HIP(c->cfb_status.reserve(cap_tasks));
+    PP_HIP(c->cfb_tasks.reserve(cap_tasks));
+    PP_HIP(c->cfb_ext.reserve(cap_tasks));
+    PP_HIP(c->cfb_rec.reserve(cap_tasks));
+    PP_HIP(c->cfb_yaw.reserve(cap_tasks));
+    PP_HIP(c->cfb_state.reserve(1));
+    PP_HIP(c->cfb_misc.reserve(4));
+    if (c->prof) PP_HIP(c->cfb_pts.reserve(2 * kWalkTallySlots));
+    SceneDev sd = c->scene_dev();
+    sd.step_size = c->mq_step;
+    // the kernel's scene in device memory (cf_run's upload)
+    if (!c->cf_scene_ok || std::memcmp(&c->cf_scene_host, &sd, sizeof sd) != 0) {
+        if (!c->cf_scene.p) PP_HIP(c->cf_scene.reserve(1));
+        c->cf_scene_host = sd;
+        PP_HIP(hipMemcpyAsync(c->cf_scene.p, &c->cf_scene_host, sizeof sd, hipMemcpyHostToDevice, st));
+        c->cf_scene_ok = true;
+    }
+    CfbArgs a;
+    a.tr = tr;
+    a.row_cap = cb_in.row_cap;
+    a.nitems = total;
+    a.Q = Q;
+    a.qidx = cb_in.qidx;
+    a.nodes = c->mp_nodes.p;
+    a.goals = cb_in.goals;
+    a.ftab = c->cf_memo.p;
+    a.gtab = c->cf_memo.p + rows;
+    a.gotab = c->cfb_gotab.p;
+    a.gclaim = c->cfb_rows.p;
+    a.tnone = c->cfb_rows.p + rows;
+    a.tnone_up = c->cfb_rows.p + 2 * rows;
+    a.depth = c->cfb_nodei.p;
+    a.open = c->cfb_nodei.p + nn;
+    a.tfirst = c->cfb_nodei.p + 2 * nn;
+    a.tcnt = c->cfb_nodei.p + 3 * nn;
+    a.tnode = c->cfb_tnode.p;
+    a.tasks = c->cfb_tasks.p;
+    a.ext = c->cfb_ext.p;
+    a.rec = c->cfb_rec.p;
+    a.status = c->cfb_status.p;
+    a.yaw = c->cfb_yaw.p;
+    a.st = c->cfb_state.p;
+    a.maxdepth = c->cfb_misc.p;
+    a.pcount = c->cfb_misc.p + 1;
+    a.wsum = c->cfb_misc.p + 2;  // (the rounds' task counts: profiling)
+    // per launch: memo, goal verdicts, claims, line items, error bits, counters, DevState
+    PP_HIP(hipMemsetAsync(c->cf_memo.p, 0, 2 * rows * sizeof(int), st));
+    PP_HIP(hipMemsetAsync(c->cfb_gotab.p, 0, (size_t)total * sizeof(int), st));
+    PP_HIP(hipMemsetAsync(c->cfb_rows.p, 0, rows * sizeof(int), st));
+    PP_HIP(hipMemsetAsync(c->cf_items.p, 0, sizeof(int), st));
+    PP_HIP(hipMemsetAsync(c->cf_err.p, 0, 2 * sizeof(int), st));
+    PP_HIP(hipMemsetAsync(c->cfb_misc.p, 0, 4 * sizeof(int), st));
+    PP_HIP(hipMemsetAsync(c->cfb_state.p, 0, sizeof(DevState), st));
+    if (c->prof) PP_HIP(hipMemsetAsync(c->cfb_pts.p, 0, 2 * kWalkTallySlots * sizeof(long long), st));
+    if (c->prof) {
+        if (int r = ensure_events(c, 2)) return r;
+        PP_HIP(hipEventRecord(c->ev[0], st));
+    }
+    PP_HIP(launch_cfb(st, sd, a, kCfbDepth, 0));
+    int misc[4] = {0, 0, 0, 0};
+    PP_HIP(hipMemcpyAsync(misc, c->cfb_misc.p, sizeof misc, hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    const int rounds = (misc[0] + 1 + kCfbSpan - 1) / kCfbSpan;
+    long long* wpts = c->prof ? c->cfb_pts.p : nullptr;
+    for (int r = 0; r < rounds; ++r) {
+        PP_HIP(launch_cfb(st, sd, a, kCfbEmitA, r));
+        PP_HIP(launch_cfb_steer(st, sd, a, (int)std::min<size_t>(cap_tasks, (size_t)kCfbSpan * nn), false, wpts));
+        PP_HIP(launch_cfb(st, sd, a, kCfbConsumeA, r));
+    }
+    PP_HIP(launch_cfb(st, sd, a, kCfbEmitB, 0));
+    PP_HIP(launch_cfb_steer(st, sd, a, (int)std::min<size_t>(cap_tasks, 2 * nn), true, wpts));
+    PP_HIP(launch_cfb(st, sd, a, kCfbStoreB, (int)std::min<size_t>(cap_tasks, 2 * nn)));
+    PP_HIP(launch_cfb(st, sd, a, kCfbAssemble, 0, o.ok, o.len, o.npts, c->cf_err.p, c->cf_items.p,
+                      c->cfb_plist.p));
+    PP_HIP(hipMemcpyAsync(misc, c->cfb_misc.p, sizeof misc, hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    const int np = misc[1];
+    CfBatch cb = cb_in;
+    cb.ftab = a.ftab;
+    cb.gtab = a.gtab;
+    cb.gotab = a.gotab;
+    // the items left (unknown verdicts) on check_finish_kernel, then every line item's points
+    PP_HIP(launch_check_finish(st, sd, c->cf_scene.p, tr, c->mp_nodes.p, np, 0.0, 0.0, 0.0, 0.0, 0,
+                               kCfCheck, 1, o.ok, o.len, o.npts, nullptr, c->api_lit_scratch.p,
+                               c->lit_locks.p, c->cf_pts.p, kCfPtsCap, c->cf_etab.p, c->cf_err.p,
+                               kCfGrid, c->prof ? c->cf_tally.p : nullptr, cb, c->cf_path.p,
+                               c->cf_items.p, c->cfb_plist.p, wgs));
+    if (c->prof) PP_HIP(hipEventRecord(c->ev[1], st));
+    int err = 0;
+    PP_HIP(hipMemcpyAsync(&err, c->cf_err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(misc, c->cfb_misc.p, sizeof misc, hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    if (c->prof) {
+        float ms = 0.f;
+        PP_HIP(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        c->finish_ms += ms;
+        c->finish_launches += 1;
+        c->cfb_nodes += total - np;
+        c->cfb_edges += misc[2];
+        std::vector<long long> v(2 * kWalkTallySlots);
+        PP_HIP(hipMemcpy(v.data(), c->cfb_pts.p, v.size() * sizeof(long long), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < v.size(); ++i) (i < (size_t)kWalkTallySlots ? c->cfb_points : c->cfb_arc) += v[i];
+    }
+    if (err & 2) return set_err(PP_ERR_REFERENCE_PANIC, "finalize: a Dubins edge has no feasible word (rrt.rs:529 panics)");
+    if (err & 4) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
+    if (err & 1) return set_err(PP_ERR_CAPACITY, "tree deeper than the check_finish path capacity");
+    if (err & 8) return set_err(PP_ERR_CAPACITY, "finalized line longer than the point capacity");
+    return PP_OK;
+}
+
 // check_finish of the one-tree planner for cf_nodes[0, k) into the context's cf_* buffers
 int cf_launch(pp_ctx* c, int k, int want_line, int grid, const CfGoal* g = nullptr) {
     const CfGoal dflt{c->goal[0], c->goal[1], c->goal[2], c->goal[2]};
@@ -893,6 +1044,7 @@ int pp_create(int device, pp_ctx** out) {
         return set_err(PP_ERR_NO_DEVICE, std::string("built for gfx950, device is ") + prop.gcnArchName);
     pp_ctx* c = new pp_ctx();
     c->device = device;
+    if (const char* v = std::getenv("PP_AMD_CF_ROUNDS")) c->cf_rounds = std::atoi(v) != 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = c->d_state.reserve(1);
     if (e == hipSuccess) e = c->d_api_state.reserve(1);
@@ -2102,8 +2254,11 @@ int pp_batch_plan(pp_ctx* ctx, int32_t* best_node, double* length, int32_t* n_po
         tr.yaw = ctx->mq_yaw.p;
         tr.parent = ctx->mq_par.p;
         const CfGoal g{0.0, 0.0, 0.0, 0.0};  // (per query: cb.goals)
-        if ((r = cf_run(ctx, tr, ctx->mp_nodes.p, (int)total, 1, kCfGrid, g,
-                        CfOut{ctx->mp_ok.p, ctx->mp_len.p, ctx->mp_npts.p, nullptr}, cb)))
+        const CfOut out{ctx->mp_ok.p, ctx->mp_len.p, ctx->mp_npts.p, nullptr};
+        // steer rounds unless polygon mode or a blocked root (check_finish_kernel handles those)
+        const bool rounds = ctx->cf_rounds && !cb.blocked && ctx->ne == 0 && ctx->nbv == 0;
+        if ((r = rounds ? cf_run_rounds(ctx, tr, (int)total, cb, out)
+                        : cf_run(ctx, tr, ctx->mp_nodes.p, (int)total, 1, kCfGrid, g, out, cb)))
             return r;
     }
     PP_HIP(launch_mq_plan_reduce(st, Q, ctx->mp_off.p, ctx->mp_ok.p, ctx->mp_len.p, ctx->mp_npts.p,
@@ -2356,10 +2511,11 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out, uint64_t out_size) {
         long long t[4];
         PP_HIP(hipMemcpyAsync(t, ctx->cf_tally.p, sizeof t, hipMemcpyDeviceToHost, ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
-        s.finish_nodes = t[0];
-        s.finish_edges = t[1];
-        s.finish_points = t[2];
-        s.finish_arc_points = t[3];
+        // (+ the batch plan's steer rounds: their nodes, edges and walked points)
+        s.finish_nodes = t[0] + ctx->cfb_nodes;
+        s.finish_edges = t[1] + ctx->cfb_edges;
+        s.finish_points = t[2] + ctx->cfb_points;
+        s.finish_arc_points = t[3] + ctx->cfb_arc;
     }
     s.persist_ms = ctx->persist_ms;
     s.persist_launches = ctx->persist_launches;

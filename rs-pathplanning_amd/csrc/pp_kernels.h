@@ -94,7 +94,49 @@ struct CfBatch {
     // 0 unknown, else 1 + the verdict of finalize's copy edge from v (see check_finish_kernel)
     int* ftab = nullptr;
     int* gtab = nullptr;
+    // the batch plan's goal-edge verdicts per item (0 unknown, else 1 + verdict; may be null)
+    const int* gotab = nullptr;
 };
+
+// check_finish of a query batch in steer rounds (pp_batch_plan, see pp_kernels.hip): phase A
+// fills ftab for every node, phase B the goal edges (gotab) and copy edges (gtab), the assemble
+// kernel decides every item whose verdicts are all known and lists the others (plist, pcount)
+// for check_finish_kernel.  Node b < nitems is item b, b - nitems < Q query's root.
+struct CfbArgs {
+    TreeDev tr{};
+    int row_cap = 0;
+    int nitems = 0, Q = 0;
+    const int* qidx = nullptr;
+    const int* nodes = nullptr;
+    const double* goals = nullptr;
+    int* ftab = nullptr;      // rows (the memo of CfBatch)
+    int* gtab = nullptr;      // rows
+    int* gotab = nullptr;     // [nitems]
+    int* gclaim = nullptr;    // rows: copy edge claimed for phase B
+    int* tnone = nullptr;     // rows: the node's own tree edge has a None steer
+    int* tnone_up = nullptr;  // rows: any tree edge from the node down to the root has one
+    int* depth = nullptr;     // [nitems + Q]
+    int* open = nullptr;      // [nitems + Q] phase A: not settled yet
+    int* tfirst = nullptr;    // [nitems + Q] the round's first task of the node
+    int* tcnt = nullptr;      // [nitems + Q] ... and its count
+    int* tnode = nullptr;     // [tasks] phase A: node b; phase B: item b, or -1 - row (copy edge)
+    SteerTask* tasks = nullptr;
+    StarTaskExt* ext = nullptr;
+    PrepRec* rec = nullptr;
+    int* status = nullptr;
+    double* yaw = nullptr;
+    DevState* st = nullptr;   // st->W: the round's task count (ncomp 0)
+    int* maxdepth = nullptr;
+    int* pcount = nullptr;
+    int* wsum = nullptr;      // (profiling) += every round's task count
+};
+enum : int { kCfbDepth = 0, kCfbEmitA, kCfbConsumeA, kCfbEmitB, kCfbStoreB, kCfbAssemble };
+constexpr int kCfbSpan = 4;  // phase A candidates per node and round
+hipError_t launch_cfb(hipStream_t s, const SceneDev& sc, CfbArgs a, int phase, int round,
+                      int* ok = nullptr, double* len = nullptr, int* npts = nullptr,
+                      int* err = nullptr, int* items = nullptr, int* plist = nullptr);
+hipError_t launch_cfb_steer(hipStream_t s, const SceneDev& sc, const CfbArgs& a, int max_tasks,
+                            bool own_yaw, long long* wg_points = nullptr);
 hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const SceneDev* scg,
                                const TreeDev& tr,
                                const int* nodes, int k, double gx, double gy, double gyaw,
@@ -102,7 +144,7 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const SceneDe
                                double* len, int* npts, int* chain, double* lit_scratch,
                                int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
                                int grid, long long* tally, const CfBatch& cb, int* gpath,
-                               int* items);
+                               int* items, const int* blist = nullptr, int line_grid = 0);
 constexpr int kCfWaves = 4;                     // check_finish: waves (nodes in flight) per workgroup
 constexpr int kCfItem = 4 + kCfLevels;          // a line item: b, s, verified, 0, pos[kCfLevels]
 

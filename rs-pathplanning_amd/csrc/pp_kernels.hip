@@ -246,12 +246,13 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
 //              before B), is longer than the points' spacing: an S point lies strictly inside
 //              the disc, and verify rejects (rrt.rs:124-137) whatever the other segments;
 //   kSUnknown  otherwise: the walk tests every point.
-// The discs come from the item grid's cells that AB's box (widened by dl) touches: a disc within
-// r + dl of AB has its cull box (>= r) in one of them.  Called by all 64 lanes; returns a
-// wave-uniform class.
+// The discs come from the item grid's cells within dl of AB, row by row: lane r takes row
+// cy0 + r, clips AB to the row's band (widened by dl; the edge rows extend to infinity, as the
+// grid clamps), and the cells of that stretch (widened by dl) are one contiguous item range of
+// the row-major CSR.  A disc within r + dl of AB has its cull box (>= r) within dl of AB, so in
+// one of those cells.  Called by all 64 lanes; returns a wave-uniform class.
 enum : int { kSUnknown = 0, kSClear = 1, kSHit = 2 };
-constexpr int kSMinPts = 24;     // S segments shorter than this many points are walked as they are
-constexpr int kSMaxCells = 256;  // ... and so are those whose box spans more item-grid cells
+constexpr int kSMinPts = 24;  // S segments shorter than this many points are walked as they are
 template <bool kLds>
 __device__ int s_classify(const SceneDev& sc, double ax, double ay, double bx, double by,
                           double t_lo, double t_hi, double gap, double dl) {
@@ -264,54 +265,69 @@ __device__ int s_classify(const SceneDev& sc, double ax, double ay, double bx, d
                fmin(ay, by) >= sc.miny + dl && fmax(ay, by) <= sc.maxy - dl)
                   ? kSClear
                   : kSUnknown;
-    const int cx0 = __builtin_amdgcn_readfirstlane(grid_cell(fmin(ax, bx) - dl, sc.gx0, sc.ginv, sc.gnx));
-    const int cx1 = __builtin_amdgcn_readfirstlane(grid_cell(fmax(ax, bx) + dl, sc.gx0, sc.ginv, sc.gnx));
     const int cy0 = __builtin_amdgcn_readfirstlane(grid_cell(fmin(ay, by) - dl, sc.gy0, sc.ginv, sc.gny));
     const int cy1 = __builtin_amdgcn_readfirstlane(grid_cell(fmax(ay, by) + dl, sc.gy0, sc.ginv, sc.gny));
-    const int ncx = cx1 - cx0 + 1, ncell = ncx * (cy1 - cy0 + 1);
-    if (ncell > kSMaxCells) return kSUnknown;
+    const int ny = cy1 - cy0 + 1;
+    if (ny > 64) return kSUnknown;
     const int* goff = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_goff) : sc.goff;
     const int* items = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_items) : sc.gitems;
-    for (int cb = 0; cb < ncell; cb += 64) {
-        // lane c: cell cb + c's item range; the cells' items are then dealt to the lanes as one
-        // list, 64 at a time (a disc listed in several cells is tested several times)
-        const int nb = min(64, ncell - cb);
-        int k0v = 0, cntv = 0;
-        if (lane < nb) {
-            const int cl = cb + lane, ry = cl / ncx;
-            const int cell = (cy0 + ry) * sc.gnx + cx0 + (cl - ry * ncx);
-            k0v = goff[cell];
-            cntv = goff[cell + 1] - k0v;
-        }
-        for (int mb = 0;; mb += 64) {
-            const int m = mb + lane;
-            int kk = -1, run = 0;
-            for (int c = 0; c < nb; ++c) {
-                const int b = __builtin_amdgcn_readlane(k0v, c), n = __builtin_amdgcn_readlane(cntv, c);
-                if (m >= run && m < run + n) kk = b + (m - run);
-                run += n;
+    int k0v = 0, cntv = 0;
+    if (lane < ny) {
+        const int gy = cy0 + lane;
+        const double cell = 1.0 / sc.ginv;
+        const double ylo = gy == 0 ? -__builtin_inf() : sc.gy0 + gy * cell - dl;
+        const double yhi = gy == sc.gny - 1 ? __builtin_inf() : sc.gy0 + (gy + 1) * cell + dl;
+        double t0 = 0.0, t1 = 1.0;
+        if (uy0 != 0.0) {
+            double ta = (ylo - ay) / uy0, tb = (yhi - ay) / uy0;
+            if (ta > tb) {
+                const double tt = ta;
+                ta = tb;
+                tb = tt;
             }
-            bool near = false, hit = false;
-            if (kk >= 0) {
-                const int d = items[kk];
-                const double wx = sc.cx[d] - ax, wy = sc.cy[d] - ay;
-                const double t = wx * ux + wy * uy;
-                const double tc = fmin(fmax(t, 0.0), len);
-                const double ex = wx - tc * ux, ey = wy - tc * uy;
-                const double rr = sqrt(sc.r2[d]);
-                const double ro = rr + dl;
-                near = ex * ex + ey * ey <= ro * ro;
-                const double px = wx - t * ux, py = wy - t * uy;
-                const double p2 = px * px + py * py, ri = rr - dl;
-                if (ri > 0.0 && p2 < ri * ri) {
-                    const double h = sqrt(ri * ri - p2) - dl;
-                    hit = fmin(t + h, t_hi) - fmax(t - h, t_lo) >= gap;
-                }
-            }
-            if (__any(hit)) return kSHit;
-            if (__any(near)) res = kSUnknown;
-            if (mb + 64 >= run) break;
+            t0 = fmax(t0, ta);
+            t1 = fmin(t1, tb);
+        } else if (!(ay >= ylo && ay <= yhi)) {
+            t1 = -1.0;
         }
+        if (t0 <= t1) {
+            const double xa = ax + t0 * ux0, xb = ax + t1 * ux0;
+            const int ca = grid_cell(fmin(xa, xb) - dl, sc.gx0, sc.ginv, sc.gnx);
+            const int cb = grid_cell(fmax(xa, xb) + dl, sc.gx0, sc.ginv, sc.gnx);
+            k0v = goff[gy * sc.gnx + ca];
+            cntv = goff[gy * sc.gnx + cb + 1] - k0v;
+        }
+    }
+    // the rows' item ranges dealt to the lanes as one list, 64 at a time (a disc listed in
+    // several cells is tested several times)
+    for (int mb = 0;; mb += 64) {
+        const int m = mb + lane;
+        int kk = -1, run = 0;
+        for (int r = 0; r < ny; ++r) {
+            const int b = __builtin_amdgcn_readlane(k0v, r), n = __builtin_amdgcn_readlane(cntv, r);
+            if (m >= run && m < run + n) kk = b + (m - run);
+            run += n;
+        }
+        bool near = false, hit = false;
+        if (kk >= 0) {
+            const int d = items[kk];
+            const double wx = sc.cx[d] - ax, wy = sc.cy[d] - ay;
+            const double t = wx * ux + wy * uy;
+            const double tc = fmin(fmax(t, 0.0), len);
+            const double ex = wx - tc * ux, ey = wy - tc * uy;
+            const double rr = sqrt(sc.r2[d]);
+            const double ro = rr + dl;
+            near = ex * ex + ey * ey <= ro * ro;
+            const double px = wx - t * ux, py = wy - t * uy;
+            const double p2 = px * px + py * py, ri = rr - dl;
+            if (ri > 0.0 && p2 < ri * ri) {
+                const double h = sqrt(ri * ri - p2) - dl;
+                hit = fmin(t + h, t_hi) - fmax(t - h, t_lo) >= gap;
+            }
+        }
+        if (__any(hit)) return kSHit;
+        if (__any(near)) res = kSUnknown;
+        if (mb + 64 >= run) break;
     }
     return res;
 }
@@ -2096,7 +2112,7 @@ __device__ __forceinline__ double ufl(double v) {
 __device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
 constexpr int kGenPts = 68;  // generator slots: 63 points + 4 overshoot + 1
 constexpr int kSegRow = 6;   // segment-table row (16-byte aligned rows: ds_read_b128)
-template <bool kLds, int kScene = kSceneAny>
+template <bool kLds, int kScene = kSceneAny, bool kS = false>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
                                         const double* __restrict__ pdv, double* __restrict__ gs,
                                         int& npts, int& napts, bool junction = true) {
@@ -2145,7 +2161,8 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     int s_state = 0, s_emit = 0;
     long long s_n = 0;
     double s_first = 0.0, s_last = 0.0, s_exit = 0.0;
-    const bool discs = (kScene == kSceneDisc ||
+    const bool discs = kS &&
+                       (kScene == kSceneDisc ||
                         (kScene == kSceneAny && !sc.bits && sc.ne == 0 && sc.nbv == 0)) &&
                        sc.m > 0;
     if (discs && partial && ng == 0 && m1 == kModeS && L1 >= kSMinPts * step) {
@@ -2401,7 +2418,7 @@ constexpr int kWalkMinWBatch = 6;
 // RRT* scenes (config 5) carry a ~58 KB LDS image, so LDS holds the walk at 2 workgroups per CU
 // whatever the register budget: the uncapped budget wins there (16.46 vs 15.96 M it/s, r02 A/B).
 constexpr int kWalkMinWStar = kWalkMinWWindow;
-template <bool kLds, int kMinW, int kScene>
+template <bool kLds, int kMinW, int kScene, bool kS>
 __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevState* __restrict__ st,
                                                          SceneDev sc,
                                                          const PrepRec* __restrict__ rec,
@@ -2434,7 +2451,7 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
         if (lane == 0) k = atomicAdd(&s_next, 1);
         const int t = (int)blockIdx.x + G * __builtin_amdgcn_readlane(k, 0);
         if (t >= total) break;
-        const int s = walk_rec<kLds, kScene>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts, napts);
+        const int s = walk_rec<kLds, kScene, kS>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts, napts);
         if (lane == 0) {
             if (t < W) {
                 snap_status[t] = s;
@@ -2469,19 +2486,19 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
 // batch unchanged).
 // The walk instantiation for a scene: LDS image or not, and its mode (scene_kind), as a callable
 // applied to the kernel (launch or occupancy query).
-template <int kMinW, typename F>
+template <int kMinW, bool kS = false, typename F>
 inline hipError_t walk_kernel_for(const SceneDev& sc, F&& f) {
     const bool lds = sc.lds_bytes > 0;
     switch (scene_kind(sc)) {
         case kSceneGrid:
-            return lds ? f(steer_walk_kernel<true, kMinW, kSceneGrid>)
-                       : f(steer_walk_kernel<false, kMinW, kSceneGrid>);
+            return lds ? f(steer_walk_kernel<true, kMinW, kSceneGrid, kS>)
+                       : f(steer_walk_kernel<false, kMinW, kSceneGrid, kS>);
         case kScenePoly:
-            return lds ? f(steer_walk_kernel<true, kMinW, kScenePoly>)
-                       : f(steer_walk_kernel<false, kMinW, kScenePoly>);
+            return lds ? f(steer_walk_kernel<true, kMinW, kScenePoly, kS>)
+                       : f(steer_walk_kernel<false, kMinW, kScenePoly, kS>);
         default:
-            return lds ? f(steer_walk_kernel<true, kMinW, kSceneDisc>)
-                       : f(steer_walk_kernel<false, kMinW, kSceneDisc>);
+            return lds ? f(steer_walk_kernel<true, kMinW, kSceneDisc, kS>)
+                       : f(steer_walk_kernel<false, kMinW, kSceneDisc, kS>);
     }
 }
 
@@ -2511,11 +2528,11 @@ inline int walk_grid_cap(const SceneDev& sc) {
 }
 
 // steer_walk_kernel over a task set on stream s (its instantiation for the scene)
-template <int kMinW>
+template <int kMinW, bool kS = false>
 inline void launch_walk(hipStream_t s, int blocks, DevState* st, const SceneDev& sc,
                         const PrepRec* rec, const double* pdbuf, CandEntry* cand, int* status,
                         const int* cand_cnt, int* pend, long long* wg_points) {
-    (void)walk_kernel_for<kMinW>(sc, [&](auto kern) {
+    (void)walk_kernel_for<kMinW, kS>(sc, [&](auto kern) {
         kern<<<blocks, kWalkThreads, walk_lds_bytes(sc.lds_bytes), s>>>(
             st, sc, rec, pdbuf, cand, status, cand_cnt, pend, wg_points);
         return hipSuccess;
@@ -3097,7 +3114,7 @@ __device__ __noinline__ void cf_prep(const SceneDev* __restrict__ scg, double ax
 __device__ __noinline__ int cf_walk(const SceneDev* __restrict__ scg, const PrepRec* lrec,
                                     double* gs, bool junction, int& walked, int& walked_arc) {
     int w = 0, wa = 0;
-    const int st = walk_rec<false>(*scg, lrec, nullptr, gs, w, wa, junction);
+    const int st = walk_rec<false, kSceneAny, true>(*scg, lrec, nullptr, gs, w, wa, junction);
     walked = w;
     walked_arc = wa;
     return st;
@@ -3227,7 +3244,7 @@ __global__ __launch_bounds__(kCfThreads, kCfMinW) void check_finish_kernel(
     int* __restrict__ ok_out, double* __restrict__ len_out,
     int* __restrict__ npts_out, int* __restrict__ chain_out, double* __restrict__ lit_scratch,
     int* __restrict__ lit_locks, int* __restrict__ err, long long* __restrict__ tally, CfBatch cb,
-    int* __restrict__ gpath, int* __restrict__ items) {
+    int* __restrict__ gpath, int* __restrict__ items, const int* __restrict__ blist) {
     __shared__ __attribute__((aligned(16))) double s_gs[kCfWaves][kGenSlots];  // walk_rec's LDS, one set per wave
     __shared__ int s_pos[kCfWaves][kCfLevels];  // the optimize chain's path positions per wave
     __shared__ PrepRec s_rec[kCfWaves];          // the wave's edge record (cf_edge_check)
@@ -3246,6 +3263,7 @@ __global__ __launch_bounds__(kCfThreads, kCfMinW) void check_finish_kernel(
         if (lane == 0) b = atomicAdd(&err[1], 1);
         b = __builtin_amdgcn_readfirstlane(__shfl(b, 0));
         if (b >= k) break;
+        if (blist) b = __builtin_amdgcn_readfirstlane(blist[b]);  // (a sub-list of the items)
         ++t_nodes;
         TreeDev tr;
         double gx, gy, gyaw, gyaw_opt;
@@ -3378,7 +3396,11 @@ __global__ __launch_bounds__(kCfThreads, kCfMinW) void check_finish_kernel(
                 // equal bit for bit, both with the junction) has that edge's verdict
                 const bool dup = e >= 1 && e < E - 1 && same_pose(prev, a) && same_pose(a, bp);
                 const int gv = (e >= 1 && e < s) ? path[e == 1 ? D - 1 : pos[e - 2]] : -1;
-                const int gm = (gtab && gv >= 0) ? __builtin_amdgcn_readfirstlane(gtab[gv]) : 0;
+                // the goal edge's verdict from the batch plan's steer round (cb.gotab), the copy
+                // edges' from gtab
+                const int gm = (e == 0 && cb.gotab)
+                                   ? __builtin_amdgcn_readfirstlane(cb.gotab[b])
+                                   : ((gtab && gv >= 0) ? __builtin_amdgcn_readfirstlane(gtab[gv]) : 0);
                 int st = prev_st;
                 if (e >= 1 && e == s) {
                     st = fnone ? kCfPanic : kAccept;
@@ -3575,15 +3597,16 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const SceneDe
                                double* len, int* npts, int* chain, double* lit_scratch,
                                int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
                                int grid, long long* tally, const CfBatch& cb, int* gpath,
-                               int* items) {
-    if (k <= 0) return hipSuccess;
+                               int* items, const int* blist, int line_grid) {
+    if (k <= 0 && line_grid <= 0) return hipSuccess;
     const int wgs = std::min(grid, (k + kCfWaves - 1) / kCfWaves);
-    check_finish_kernel<<<wgs, kCfThreads, 0, st>>>(scg, tr, nodes, k, gx, gy, gyaw, gyaw_opt,
-                                                    level0, mode, want_line, ok, len, npts, chain,
-                                                    lit_scratch, lit_locks, err, tally, cb, gpath,
-                                                    items);
+    if (k > 0)
+        check_finish_kernel<<<wgs, kCfThreads, 0, st>>>(scg, tr, nodes, k, gx, gy, gyaw, gyaw_opt,
+                                                        level0, mode, want_line, ok, len, npts,
+                                                        chain, lit_scratch, lit_locks, err, tally,
+                                                        cb, gpath, items, blist);
     if (want_line && mode != kCfOptimize)
-        cf_line_kernel<<<std::min(grid, k), kCfThreads, 0, st>>>(
+        cf_line_kernel<<<line_grid > 0 ? line_grid : std::min(grid, k), kCfThreads, 0, st>>>(
             sc, tr, nodes, gx, gy, gyaw, gyaw_opt, ok, len, npts, pts, pts_cap, etab, err, cb,
             gpath, items);
     return hipGetLastError();
@@ -3648,6 +3671,386 @@ hipError_t launch_mq_plan_reduce(hipStream_t s, int Q, const int* off, const int
                                  double* best_len, int* best_npts, int* n_fin) {
     mq_plan_reduce_kernel<<<std::min((Q + 3) / 4, 4096), 256, 0, s>>>(
         Q, off, ok, len, npts, best_node, best_len, best_npts, n_fin);
+    return hipGetLastError();
+}
+
+// --------------------------------- check_finish of a query batch in steer rounds (round 4)
+//
+// check_finish_kernel runs every item's edges one after the other on one wave, at 2 waves per
+// SIMD (its register budget): a latency chain.  For a batch plan, every edge whose verdict
+// depends on one tree node or one item is steered up front instead, by the query batch's own
+// steer_prep / steer_walk at their occupancy, and written to the memo tables the kernel already
+// reads (CfBatch::ftab / gtab, and gotab: the goal edge of each item):
+//   phase A  ftab of every node (optimize's level for node c: the first of c's ancestors, root
+//            first, and c itself whose edge verifies, rrt.rs:463-487): rounds of kCfbSpan
+//            candidates per open node, in order; a node settles at its first verdict that is
+//            not a rejection (a literal-path or error verdict leaves ftab unknown);
+//   phase B  each item's chain follows ftab; its goal edge (Node::new_goal, rrt.rs:430-436,
+//            the goal keeping its own yaw) and its copy edges (one per chain node v, claimed by
+//            the first item that reaches v) are steered in one round: gotab / gtab;
+//   assemble one lane per item: the chain, the verdicts in finalize's order, the panic scan from
+//            the None flags (a None steer is a panic status in the memo; the tree edges' flags
+//            are tnone_up), the outputs or a line item.  An item with any unknown verdict goes
+//            to a list that check_finish_kernel runs as before (with every memo entry there).
+// Results are those of check_finish_kernel: the same edges, the same verdicts, the same order
+// of precedence (a panic anywhere wins over a rejection; verify decides the rest).
+
+// phase A node list: b < nitems is item b (qidx[b], nodes[b]); b - nitems < Q is query's root
+__device__ inline void cfb_node(const CfbArgs& a, int b, int& q, int& c) {
+    if (b < a.nitems) {
+        q = a.qidx[b];
+        c = a.nodes[b];
+    } else {
+        q = b - a.nitems;
+        c = 0;
+    }
+}
+
+// depth of every phase-A node, its own tree edge's None flag (the steer from its pose to its
+// parent's, rrt.rs:313 / 529), and the open state; maxdepth for the host
+__global__ __launch_bounds__(256) void cfb_depth_kernel(CfbArgs a, SceneDev sc) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.nitems + a.Q) return;
+    int q, c;
+    cfb_node(a, b, q, c);
+    const size_t o = (size_t)q * a.row_cap;
+    int d = 0;
+    for (int k = c; a.tr.parent[o + k] >= 0; k = a.tr.parent[o + k]) ++d;
+    a.depth[b] = d;
+    a.open[b] = 1;
+    atomicMax(a.maxdepth, d);
+    int none = 0;
+    if (c > 0) {
+        const int p = a.tr.parent[o + c];
+        const CfPose from{a.tr.x[o + c], a.tr.y[o + c], a.tr.yaw[o + c]};
+        const CfPose to{a.tr.x[o + p], a.tr.y[o + p], a.tr.yaw[o + p]};
+        none = cf_npoint(sc, from, to) == 0 ? 1 : 0;
+    }
+    a.tnone[o + c] = none;
+}
+
+// tnone_up[c]: any tree edge from c down to the root has a None steer
+__global__ __launch_bounds__(256) void cfb_tnone_up_kernel(CfbArgs a) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.nitems + a.Q) return;
+    int q, c;
+    cfb_node(a, b, q, c);
+    const size_t o = (size_t)q * a.row_cap;
+    int any = 0;
+    for (int k = c; k > 0; k = a.tr.parent[o + k]) any |= a.tnone[o + k];
+    a.tnone_up[o + c] = any;
+}
+
+// a lane's task count -> its first task index, one atomic per wave on the round's counter
+__device__ inline int cfb_reserve(int* counter, int cnt, int* wsum) {
+    const int lane = threadIdx.x & 63;
+    const int incl = wave_incl_scan(cnt);
+    int base = 0;
+    if (lane == 63) {
+        base = atomicAdd(counter, incl);
+        if (wsum) atomicAdd(wsum, incl);
+    }
+    base = __builtin_amdgcn_readlane(base, 63);
+    return base + incl - cnt;
+}
+
+// phase A round r: the next kCfbSpan candidates (depth 4r .. 4r + 3, root first) of every open
+// node, as explicit (child, parent pose) tasks: child = the node's position (compute_yaw toward
+// the candidate, as Node::new does), parent = the candidate's stored pose
+__global__ __launch_bounds__(256) void cfb_emit_a_kernel(CfbArgs a, int round) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    int cnt = 0, q = 0, c = 0, d = 0;
+    const int m0 = round * kCfbSpan;
+    if (b < a.nitems + a.Q && a.open[b]) {
+        cfb_node(a, b, q, c);
+        d = a.depth[b];
+        cnt = min(kCfbSpan, d + 1 - m0);
+        if (cnt < 0) cnt = 0;
+    }
+    const int t0 = cfb_reserve(&a.st->W, cnt, a.wsum);
+    if (b < a.nitems + a.Q) {
+        a.tfirst[b] = t0;
+        a.tcnt[b] = cnt;
+    }
+    if (cnt == 0) return;
+    const size_t o = (size_t)q * a.row_cap;
+    const double x = a.tr.x[o + c], y = a.tr.y[o + c];
+    // climb to depth m0 + cnt - 1, then emit the candidates downward to depth m0
+    int k = c;
+    for (int dd = d; dd > m0 + cnt - 1; --dd) k = a.tr.parent[o + k];
+    for (int i = cnt - 1; i >= 0; --i) {
+        const int t = t0 + i;
+        SteerTask tk;
+        tk.x = x;
+        tk.y = y;
+        tk.px = a.tr.x[o + k];
+        tk.py = a.tr.y[o + k];
+        tk.pyaw = a.tr.yaw[o + k];
+        tk.pnode = k;
+        tk.literal = 0;
+        a.tasks[t] = tk;
+        a.tnode[t] = b;
+        if (i > 0) k = a.tr.parent[o + k];
+    }
+}
+
+// phase A round r, after the walk: a node settles at its first candidate (in order) that is not
+// rejected — accepted: ftab = 2 + depth (| 1 << 30 for a None steer, finalize's panic); literal
+// path or error: left unknown for check_finish_kernel — or when its last candidate was rejected:
+// ftab = 1 (no candidate)
+__global__ __launch_bounds__(256) void cfb_consume_a_kernel(CfbArgs a, int round) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b == 0) a.st->W = 0;  // the next round's counter (every reader of W has finished)
+    if (b >= a.nitems + a.Q) return;
+    const int cnt = a.tcnt[b];
+    if (cnt == 0) return;
+    int q, c;
+    cfb_node(a, b, q, c);
+    const size_t o = (size_t)q * a.row_cap;
+    const int t0 = a.tfirst[b], m0 = round * kCfbSpan;
+    for (int i = 0; i < cnt; ++i) {
+        const int s = a.status[t0 + i];
+        if (s == kReject) continue;
+        if (s == kAccept) {
+            const int fnone = a.rec[t0 + i].state == kPrepNone ? 1 : 0;
+            a.ftab[o + c] = (2 + m0 + i) | (fnone << 30);
+        }
+        a.open[b] = 0;
+        return;
+    }
+    if (m0 + cnt > a.depth[b]) {
+        a.ftab[o + c] = 1;
+        a.open[b] = 0;
+    }
+}
+
+// an item's optimize chain from ftab (check_finish_kernel's level loop): n[0] = the item's node,
+// n[l + 1] = its level-l candidate (pos[l] = that node's depth); false when an entry on the way
+// is unknown
+__device__ inline bool cfb_chain(const CfbArgs& a, size_t o, int c, int d, int* n, int* pos,
+                                 int& s, int& fnone) {
+    s = 0;
+    fnone = 0;
+    n[0] = c;
+    int cur = c, curd = d;
+    for (int level = 0; level < kCfLevels; ++level) {
+        const int fm = a.ftab[o + cur];
+        if (fm == 0) return false;
+        if (fm == 1) break;
+        const int found = (fm & 0x3fffffff) - 2;
+        fnone = fm >> 30;
+        pos[level] = found;
+        s = level + 1;
+        if (curd == 0) {  // a level at the root: root copies to the recursion limit
+            for (int l2 = level + 1; l2 < kCfLevels; ++l2) pos[l2] = 0;
+            for (int l2 = level + 1; l2 <= kCfLevels; ++l2) n[l2] = cur;
+            s = kCfLevels;
+            break;
+        }
+        while (curd > found) {
+            cur = a.tr.parent[o + cur];
+            --curd;
+        }
+        n[level + 1] = cur;
+    }
+    return true;
+}
+
+// phase B: every item's goal edge, and the copy edges of its chain that no other item claimed
+__global__ __launch_bounds__(256) void cfb_emit_b_kernel(CfbArgs a) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    int n[kCfLevels + 1], pos[kCfLevels];
+    int s = 0, fnone = 0, cnt = 0, q = 0, c = 0;
+    size_t o = 0;
+    bool ok = false;
+    unsigned claimed = 0;  // bit e: this item steers copy edge e (1 <= e < s)
+    if (b < a.nitems) {
+        cfb_node(a, b, q, c);
+        o = (size_t)q * a.row_cap;
+        ok = cfb_chain(a, o, c, a.depth[b], n, pos, s, fnone);
+        if (ok) {
+            cnt = 1;
+            for (int e = 1; e < s; ++e)
+                if (atomicExch(&a.gclaim[o + n[e - 1]], 1) == 0) {
+                    claimed |= 1u << e;
+                    ++cnt;
+                }
+        }
+    }
+    const int t0 = cfb_reserve(&a.st->W, cnt, a.wsum);
+    if (!ok) return;
+    const double* X = a.tr.x + o;
+    const double* Y = a.tr.y + o;
+    // the goal edge: Node::new_goal (the goal keeps its yaw: the planner's optimised yaw when
+    // optimize succeeded, rrt.rs:489-501) into pose 1 — the copy at the node toward n[1], or
+    // the node's stored pose when the chain is empty
+    const double gyaw = a.goals[3 * q + 2];
+    SteerTask tk;
+    tk.x = a.goals[3 * q];
+    tk.y = a.goals[3 * q + 1];
+    if (s > 0) {
+        tk.px = X[c];
+        tk.py = Y[c];
+        tk.pyaw = cf_atan2(Y[n[1]] - Y[c], X[n[1]] - X[c]);
+    } else {
+        tk.px = X[c];
+        tk.py = Y[c];
+        tk.pyaw = a.tr.yaw[o + c];
+    }
+    tk.pnode = 0;
+    tk.literal = 0;
+    a.tasks[t0] = tk;
+    StarTaskExt ex{};
+    ex.own_yaw = 1;
+    ex.cyaw = gyaw;
+    a.ext[t0] = ex;
+    a.tnode[t0] = b;
+    int t = t0 + 1;
+    for (int e = 1; e < s; ++e) {
+        if (!((claimed >> e) & 1u)) continue;
+        // copy edge e: from the copy at v = n[e - 1] toward n[e] (compute_yaw) to the copy at
+        // n[e] toward n[e + 1]
+        const int v = n[e - 1], w = n[e], w2 = n[e + 1];
+        SteerTask ct;
+        ct.x = X[v];
+        ct.y = Y[v];
+        ct.px = X[w];
+        ct.py = Y[w];
+        ct.pyaw = cf_atan2(Y[w2] - Y[w], X[w2] - X[w]);
+        ct.pnode = w;
+        ct.literal = 0;
+        a.tasks[t] = ct;
+        a.ext[t] = StarTaskExt{};
+        a.tnode[t] = -1 - (int)(o + v);
+        ++t;
+    }
+}
+
+// phase B, after the walk: the verdicts into gotab / gtab (a None steer: finalize's panic; a
+// literal-path or error verdict stays unknown)
+__global__ __launch_bounds__(256) void cfb_store_b_kernel(CfbArgs a) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.st->W) return;
+    int s = a.status[t];
+    if (a.rec[t].state == kPrepNone) s = kCfPanic;
+    else if (s != kAccept && s != kReject) return;
+    const int n = a.tnode[t];
+    if (n >= 0)
+        a.gotab[n] = s + 1;
+    else
+        a.gtab[-1 - n] = s + 1;
+}
+
+// one lane per item: finalize's verdict from the memo (check_finish_kernel's order and
+// precedence), its outputs or its line item; an item with an unknown verdict goes to plist
+__global__ __launch_bounds__(256) void cfb_assemble_kernel(CfbArgs a, int* __restrict__ ok_out,
+                                                           double* __restrict__ len_out,
+                                                           int* __restrict__ npts_out,
+                                                           int* __restrict__ err,
+                                                           int* __restrict__ items,
+                                                           int* __restrict__ plist) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.nitems) return;
+    int q, c;
+    cfb_node(a, b, q, c);
+    const size_t o = (size_t)q * a.row_cap;
+    int n[kCfLevels + 1], pos[kCfLevels];
+    int s = 0, fnone = 0;
+    bool known = cfb_chain(a, o, c, a.depth[b], n, pos, s, fnone);
+    // verdicts in finalize's order: 0 accept, 1 reject, 2 panic (the first non-accepted decides,
+    // a None steer anywhere wins over a rejection)
+    int first = 0;
+    bool any_none = false;
+    if (known) {
+        const int g = a.gotab[b];
+        known = g == 1 + kAccept || g == 1 + kReject || g == 1 + kCfPanic;
+        if (known && g != 1 + kAccept) first = g == 1 + kReject ? 1 : 2;
+        any_none = g == 1 + kCfPanic;
+    }
+    for (int e = 1; known && e < s; ++e) {
+        const int g = a.gtab[o + n[e - 1]];
+        known = g == 1 + kAccept || g == 1 + kReject || g == 1 + kCfPanic;
+        if (known && g != 1 + kAccept && first == 0) first = g == 1 + kReject ? 1 : 2;
+        any_none |= g == 1 + kCfPanic;
+    }
+    if (!known) {
+        plist[atomicAdd(&a.pcount[0], 1)] = b;
+        return;
+    }
+    if (s >= 1 && fnone) {  // edge s: the last level's accepted candidate edge
+        any_none = true;
+        if (first == 0) first = 2;
+    }
+    const bool tree_none = a.tnone_up[o + n[s]] != 0;  // edges s + 1 .. E - 1
+    int bad = 0;
+    bool vok = false;
+    if (first == 2) {
+        bad = 2;
+    } else if (first == 1) {
+        if (any_none || tree_none) bad = 2;
+    } else {
+        vok = true;
+        if (tree_none) bad = 2;
+    }
+    if (vok && bad == 0) {
+        const int it = atomicAdd(&items[0], 1);
+        int* ob = items + 1 + (size_t)it * kCfItem;
+        ob[0] = b;
+        ob[1] = s;
+        ob[2] = 1;
+        ob[3] = 0;
+        for (int i = 0; i < kCfLevels; ++i) ob[4 + i] = i < s ? pos[i] : 0;
+    } else {
+        ok_out[b] = 0;
+        len_out[b] = 0.0;
+        npts_out[b] = 0;
+        if (bad) atomicOr(err, bad);
+    }
+}
+
+hipError_t launch_cfb(hipStream_t s, const SceneDev& sc, CfbArgs a, int phase, int round,
+                      int* ok, double* len, int* npts, int* err, int* items, int* plist) {
+    const int nn = a.nitems + a.Q;
+    const int g = (nn + 255) / 256;
+    switch (phase) {
+        case kCfbDepth:
+            cfb_depth_kernel<<<g, 256, 0, s>>>(a, sc);
+            cfb_tnone_up_kernel<<<g, 256, 0, s>>>(a);
+            break;
+        case kCfbEmitA:
+            cfb_emit_a_kernel<<<g, 256, 0, s>>>(a, round);
+            break;
+        case kCfbConsumeA:
+            cfb_consume_a_kernel<<<g, 256, 0, s>>>(a, round);
+            break;
+        case kCfbEmitB:
+            cfb_emit_b_kernel<<<(a.nitems + 255) / 256, 256, 0, s>>>(a);
+            break;
+        case kCfbStoreB:
+            cfb_store_b_kernel<<<(round + 255) / 256, 256, 0, s>>>(a);  // round: the task bound
+            break;
+        case kCfbAssemble:
+            cfb_assemble_kernel<<<(a.nitems + 255) / 256, 256, 0, s>>>(a, ok, len, npts, err,
+                                                                        items, plist);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// a steer round over the tasks the emit kernel counted in st->W (the query batch's kernels)
+hipError_t launch_cfb_steer(hipStream_t s, const SceneDev& sc, const CfbArgs& a, int max_tasks,
+                            bool own_yaw, long long* wg_points) {
+    if (max_tasks <= 0) return hipSuccess;
+    const int pb = std::min((max_tasks + 31) / 32, 8192);
+    steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(a.st, sc, nullptr, nullptr, nullptr, nullptr,
+                                                  a.rec, nullptr, a.yaw, a.tasks, nullptr,
+                                                  own_yaw ? a.ext : nullptr);
+    const int wb = std::min(std::max(1, (max_tasks + kWalkThreads / 64 - 1) / (kWalkThreads / 64)),
+                            std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch>(sc)));
+    launch_walk<kWalkMinWBatch, true>(s, wb, a.st, sc, a.rec, nullptr, nullptr, a.status, nullptr,
+                                      nullptr, wg_points);
     return hipGetLastError();
 }
 
@@ -3846,6 +4249,10 @@ hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int
     return hipGetLastError();
 }
 
+#ifndef PP_S_BATCH_TASKS
+#define PP_S_BATCH_TASKS 32768
+#endif
+constexpr int kSBatchTasks = PP_S_BATCH_TASKS;  // tasks per step from which the batch walk uses s_classify
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int Q = a.mq.Q;
     const int T = Q * a.mq.K;  // tasks per step
@@ -3865,8 +4272,14 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
                                                               nullptr, nullptr, a.rec, a.pdbuf,
                                                               a.yaw, a.tasks);
         if (ev) (void)hipEventRecord(ev[2], s);
-        launch_walk<kWalkMinWBatch>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf, nullptr,
-                                    a.status, nullptr, nullptr, a.wg_points);
+        // the analytic straight segments (s_classify) pay where the walk is throughput-bound:
+        // large steps; a small shard's step is latency-bound and walks without them
+        if (T >= kSBatchTasks)
+            launch_walk<kWalkMinWBatch, true>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf, nullptr,
+                                              a.status, nullptr, nullptr, a.wg_points);
+        else
+            launch_walk<kWalkMinWBatch, false>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf, nullptr,
+                                               a.status, nullptr, nullptr, a.wg_points);
         if (ev) (void)hipEventRecord(ev[3], s);
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
                                                     a.lit_scratch, a.lit_locks, a.err);

@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 REPORT = {}
 # one-point trim flips measured per case (profiles/r04_libm_flips_plan.json); the bound allows
 # twice the measured count (at least 1): a regression that doubles the rate fails
-FLIPS_MEASURED = {"bench6_open": None, "field512": None, "field512_128": None}
+FLIPS_MEASURED = {"bench6_open": 1, "field512": 0, "field512_128": 0}
 
 
 def _bound(case):
@@ -137,3 +137,31 @@ def test_batch_plan_field512_128(pkg, ctx, oracle_mod):
     got, exp, checked = _run(ctx, oracle_mod, raw, 0, 128, 2000)
     assert checked >= 8192
     _check(got, exp, checked, raw, "field512_128")
+
+
+def test_batch_plan_rounds_equal_one_kernel(pkg, ctx, monkeypatch):
+    """pp_batch_plan's steer rounds (phase A / B memo fill, lane-per-item assemble, DESIGN.md
+    §3.3) against check_finish_kernel alone (PP_AMD_CF_ROUNDS=0 at context creation): the same
+    best node, length (bit for bit), point count and finish count for every query of a
+    512-query config-3 batch"""
+    from pathplanning_amd import rrt, scenes
+
+    raw = scenes.field512()
+    starts, goals, seeds = scenes.config3_queries(raw, 0, 512)
+    out = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PP_AMD_CF_ROUNDS", mode)
+        c = pkg.Context(0)
+        try:
+            b = rrt.RRTBatch(starts, goals, 2000, raw["step_size"], rrt.Space.from_raw(raw),
+                             seeds, ctx=c)
+            b.extend(2000)
+            out.append(b.plan())
+        finally:
+            c.close()
+    a, k = out
+    assert a["checked"] == k["checked"] > 0
+    for key in ("best_node", "n_points", "n_finishes"):
+        assert np.array_equal(a[key], k[key]), key
+    assert np.array_equal(a["length"], k["length"])
+    assert int((a["best_node"] >= 0).sum()) > 0
