@@ -896,7 +896,7 @@ __device__ inline int morton16(int x, int y) {
 
 // LDS of samples_role: the Morton histogram, each sample's cell, the sorted window's sample ids,
 // the count of samples in an obstacle
-constexpr int kSamplesLds = 256 * 4 + kMaxWindow + kMaxWindow * 4 + 16;
+constexpr int kSamplesLds = 256 * 4 + kMaxWindow + kMaxWindow * 4 + 16 + kMaxWindow;
 
 // The screen's geometry for Ws screened samples (window mode): nqb blocks of kQPB samples x
 // chunks node chunks on at most kScanGrid workgroups, nqb x chunks a multiple of 8 when it can be
@@ -917,6 +917,7 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
     unsigned char* s_cell = reinterpret_cast<unsigned char*>(s_hist + 256);  // [K]
     int* s_j = reinterpret_cast<int*>(smem + 256 * 4 + kMaxWindow);  // [K] sorted position -> sample
     int* s_nb = s_j + kMaxWindow;  // samples in an obstacle (sorted after the screened ones)
+    unsigned char* s_bk = reinterpret_cast<unsigned char*>(s_nb + 4);  // [K] sample in an obstacle
     const int tid = threadIdx.x, NT = blockDim.x;
     const int64_t rem = g.target - start;
     // the adaptive window (kdyn, set by the commits; results never depend on the window size)
@@ -983,23 +984,25 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int j = j0 + u * NT;
-            if (j >= W) continue;
+            const bool valid = j < W;
+            // a sample in an obstacle needs no nearest node and is nobody's candidate parent: it
+            // is sorted after the screened samples, out of the screen and the pair grid (counted
+            // per wave: one LDS atomic instead of one per sample on a single address)
+            const uint64_t mb = __ballot(valid && bks[u]);
+            if ((threadIdx.x & 63) == 0 && mb) atomicAdd(s_nb, (int)__popcll(mb));
+            if (!valid) continue;
             const double x = xs[u], y = ys[u];
             g.wsx[np][j] = x;
             g.wsy[np][j] = y;
             g.wsx32[np][j] = (float)x;
             g.wsy32[np][j] = (float)y;
             if (pre) g.blk[np][j] = bks[u] ? 1 : 0;
+            s_bk[j] = bks[u] ? 1 : 0;
             const int cx = min(max((int)((x - g.minx) * fx), 0), 15);  // == sample_cell
             const int cy = min(max((int)((y - g.miny) * fy), 0), 15);
             const int cell = morton16(cx, cy);
             s_cell[j] = (unsigned char)cell;
-            // a sample in an obstacle needs no nearest node and is nobody's candidate parent: it
-            // is sorted after the screened samples, out of the screen and the pair grid
-            if (bks[u])
-                atomicAdd(s_nb, 1);
-            else
-                atomicAdd(&s_hist[cell], 1);
+            if (!bks[u]) atomicAdd(&s_hist[cell], 1);
         }
     }
     __syncthreads();
@@ -1030,8 +1033,17 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
         *s_nb = Ws;  // (now the next free position of the blocked bucket)
     }
     __syncthreads();  // the cell starts are read before the scatter advances them
-    for (int j = tid; j < W; j += NT)
-        s_j[(g.blk[np] && g.blk[np][j]) ? atomicAdd(s_nb, 1) : atomicAdd(&s_hist[s_cell[j]], 1)] = j;
+    for (int j0 = tid - (tid & 63); j0 < W; j0 += NT) {  // whole waves (the ballot below)
+        const int j = j0 + (tid & 63);
+        const bool bk = j < W && s_bk[j];
+        // the blocked bucket: a wave's blocked samples take consecutive positions (one atomic)
+        const uint64_t mb = __ballot(bk);
+        int base = 0;
+        if ((tid & 63) == 0 && mb) base = atomicAdd(s_nb, (int)__popcll(mb));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (j >= W) continue;
+        s_j[bk ? base + (int)__popcll(mb & ((1ull << (tid & 63)) - 1)) : atomicAdd(&s_hist[s_cell[j]], 1)] = j;
+    }
     __syncthreads();
     // the screen's blocks of kQPB sorted samples, one wave each: the sorted window (coalesced; the
     // coordinates drawn again from the stream, bit-identical), the centre o of the block's
@@ -1967,8 +1979,10 @@ __device__ __forceinline__ void prep_task(const SceneDev& sc, int r, int g0, int
     const Pt O1 = seg_end(m0, L0, c, rc, 0.0, 0.0, ca0, sa0, sl0, cl0);
     const Pt O2 = seg_end(m1, L1, c, rc, O1.x, O1.y, ca1, sa1, sl1, cl1);
     const Pt E = seg_end(m2, L2, c, rc, O2.x, O2.y, ca2, sa2, sl2, cl2);
-    // the trim (dubins.rs:281-288) drops exactly the endpoint unless its local x is 0.0
-    if (state == kPrepWalk && E.x == 0.0) state = kLiteral;
+    // the trim (dubins.rs:281-288) drops exactly the endpoint unless its local x is 0.0; then it
+    // drops the last grid point too, and goes on while the dropped x is 0.0: the walk drops that
+    // point and hands the rest (its x 0.0 as well) to the literal path
+    const int trim1 = (state == kPrepWalk && E.x == 0.0) ? 1 : 0;
     int cnt0 = 0, cnt1 = 0, cnt2 = 0, fb_seg = 0;
     double fb_pd = 0.0, fb_dd = 0.0;
     // no grid points are stored: steer_walk generates them all, lane-parallel and bit-exact,
@@ -2018,6 +2032,7 @@ __device__ __forceinline__ void prep_task(const SceneDev& sc, int r, int g0, int
         o.cnt[1] = cnt1;
         o.cnt[2] = cnt2;
         o.state = state;
+        o.trim1 = trim1;
         rec[t] = o;
         if (yaw_dst) *yaw_dst = yaw;
         // the Dubins cost (dubins.rs:351-361; inf on None): the RRT* edge cost
@@ -2161,7 +2176,8 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     int s_state = 0, s_emit = 0;
     long long s_n = 0;
     double s_first = 0.0, s_last = 0.0, s_exit = 0.0;
-    const bool discs = kS &&
+    const int trim1 = ufl(p->trim1);
+    const bool discs = kS && !trim1 &&
                        (kScene == kSceneDisc ||
                         (kScene == kSceneAny && !sc.bits && sc.ne == 0 && sc.nbv == 0)) &&
                        sc.m > 0;
@@ -2301,12 +2317,20 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                 my_seg = g < n0 ? 0 : (g < n01 ? 1 : 2);
             }
         }
+        // trim1 (prep_task): the chunk where the last segment ends pops its last grid point with
+        // the endpoint; one generated in the previous chunk was tested already: literal path
+        const bool drop = trim1 && done;
+        if (drop && cnt == 0) return kLiteral;
+        const int cnt_gen = cnt;  // grid points generated in this chunk (lanes 1 .. cnt_gen)
+        if (drop) cnt -= 1;       // ... and kept
         const bool junction_here = done && cnt < 63;
+        const bool isgen = lane >= 1 && lane <= cnt_gen;
         const bool isgrid = lane >= 1 && lane <= cnt;
         const bool isj = junction && junction_here && lane == cnt + 1;
         double qx = carry_x, qy = carry_y;
         int mm = kModeS;
-        if (isgrid) {
+        bool pop_more = false;  // the popped point's local x is 0.0 too: the trim goes on
+        if (isgen) {
             const double* row = segt + kSegRow * my_seg;
             const double2 o2 = *reinterpret_cast<const double2*>(row);
             const double2 t2 = *reinterpret_cast<const double2*>(row + 2);
@@ -2331,10 +2355,13 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
             }
             qx = cw * lx + sw * ly + x;   // dubins.rs:415
             qy = -sw * lx + cw * ly + y;  // dubins.rs:420
-        } else if (isj) {
+            pop_more = drop && lane == cnt_gen && lx == 0.0;
+        }
+        if (isj) {
             qx = px;
             qy = py;
         }
+        if (__any(pop_more)) return kLiteral;
         const bool has = lane == 0 || isgrid || isj;
         const bool chk = isgrid || isj || (base == 0 && lane == 0);
         npts += cnt + (junction && junction_here ? 1 : 0);
@@ -2394,6 +2421,7 @@ __device__ __forceinline__ int walk_edge(const SceneDev& sc, const SteerPrep& r,
     p.fb_dd = (r.L0 > 0.0) ? sc.step_size : -sc.step_size;
     p.fb_pd = p.fb_dd - 0.0;  // dubins.rs:239-241
     p.fb_seg = 0;
+    p.trim1 = 0;
     p.yaw = p.pyaw = 0.0;
     return walk_rec<kLds>(sc, &p, nullptr, gs, npts, napts, junction);
 }
@@ -3561,25 +3589,41 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
             }
         }
         __syncthreads();
+        // l.reverse() (rrt.rs:538), then euclidean_length in that order: the line's points in
+        // forward order f = 0 .. np - 1 (edge by edge), the reversed line's k-th segment is
+        // (f + 1 -> f) for f = np - 2 down to 0.  Every segment's hypot in parallel (into the
+        // yaw buffer, by forward index), then one lane adds them in the reversed order — the
+        // same operands, the same order of the sum
+        const int bad0 = s_bad;
+        if (bad0 == 0) {
+            int cb = 0;
+            for (int e = 0; e < E; ++e) {
+                const int off = et[2 * e], n = et[2 * e + 1];
+                for (int i = tid; i < n; i += kCfThreads) {
+                    int noff = -1;
+                    if (i + 1 < n) {
+                        noff = off + i + 1;
+                    } else {
+                        for (int e2 = e + 1; e2 < E; ++e2)
+                            if (et[2 * e2 + 1] > 0) {
+                                noff = et[2 * e2];
+                                break;
+                            }
+                    }
+                    if (noff >= 0)
+                        pyw[cb + i] = hypot(px[off + i] - px[noff], py[off + i] - py[noff]);
+                }
+                cb += n;
+            }
+        }
+        __syncthreads();
         if (tid == 0) {
             double len = 0.0;
             int npts = 0;
             const int bad = s_bad;
             if (bad == 0) {
-                // l.reverse() (rrt.rs:538), then euclidean_length in that order
-                bool have = false;
-                double qx = 0.0, qy = 0.0;
-                for (int e = E - 1; e >= 0; --e) {
-                    const int off = et[2 * e], n = et[2 * e + 1];
-                    for (int i = n - 1; i >= 0; --i) {
-                        const double x = px[off + i], y = py[off + i];
-                        if (have) len += hypot(x - qx, y - qy);
-                        qx = x;
-                        qy = y;
-                        have = true;
-                    }
-                    npts += n;
-                }
+                for (int e = 0; e < E; ++e) npts += et[2 * e + 1];
+                for (int f = npts - 2; f >= 0; --f) len += pyw[f];
             }
             ok_out[b] = (vok && bad == 0) ? 1 : 0;
             len_out[b] = bad == 0 ? len : 0.0;
@@ -3741,17 +3785,24 @@ __global__ __launch_bounds__(256) void cfb_tnone_up_kernel(CfbArgs a) {
     a.tnone_up[o + c] = any;
 }
 
-// a lane's task count -> its first task index, one atomic per wave on the round's counter
+// a thread's task count -> its first task index: one atomic per 256-thread workgroup on the
+// round's counter (per wave, ~9k waves contending for one address cost ~0.2 ms a round).  Every
+// thread of the workgroup must call it.
 __device__ inline int cfb_reserve(int* counter, int cnt, int* wsum) {
-    const int lane = threadIdx.x & 63;
+    __shared__ int s_wt[4], s_base;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int incl = wave_incl_scan(cnt);
-    int base = 0;
-    if (lane == 63) {
-        base = atomicAdd(counter, incl);
-        if (wsum) atomicAdd(wsum, incl);
+    if (lane == 63) s_wt[w] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int tot = s_wt[0] + s_wt[1] + s_wt[2] + s_wt[3];
+        s_base = tot ? atomicAdd(counter, tot) : 0;
+        if (wsum && tot) atomicAdd(wsum, tot);
     }
-    base = __builtin_amdgcn_readlane(base, 63);
-    return base + incl - cnt;
+    __syncthreads();
+    int wb = s_base;
+    for (int k = 0; k < w; ++k) wb += s_wt[k];
+    return wb + incl - cnt;
 }
 
 // phase A round r: the next kCfbSpan candidates (depth 4r .. 4r + 3, root first) of every open
@@ -4250,7 +4301,7 @@ hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int
 }
 
 #ifndef PP_S_BATCH_TASKS
-#define PP_S_BATCH_TASKS 32768
+#define PP_S_BATCH_TASKS 0
 #endif
 constexpr int kSBatchTasks = PP_S_BATCH_TASKS;  // tasks per step from which the batch walk uses s_classify
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {

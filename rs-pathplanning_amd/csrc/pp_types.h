@@ -184,6 +184,8 @@ struct PrepRec {
     int m[3], cnt[3];                // segment modes, grid points per segment (of the stored ones)
     int state, fb_seg;               // kPrepWalk / kPrepNone / kPrepFallback or a verdict; the
                                      // kPrepFallback walk's segment at point kPdCap
+    int trim1;                       // the endpoint's local x is 0.0: the trim also pops the last
+                                     // grid point (dubins.rs:281-288; the walk checks its x)
 };
 enum : int { kPrepWalk = -1, kPrepNone = 4, kPrepFallback = 5 };
 
