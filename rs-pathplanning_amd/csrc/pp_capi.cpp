@@ -511,6 +511,7 @@ int ensure_events(pp_ctx* c, size_t count) {
 static_assert(PP_CF_CHAIN == kCfLevels + 2, "chain row layout");
 constexpr int kCfBatch = 16384;     // nodes per check_finish launch
 constexpr int kCfPtsCap = 1 << 16;  // line points per check_finish workgroup
+constexpr int kCfLineGrid = 2048;   // the batch plan's cf_line_kernel workgroups (1.5 MB each)
 
 // check_finish for nodes[0, k) (device pointer already filled); results on the device
 // The goal of a check_finish_kernel launch: the planner's (check_finish), or a caller-built goal
@@ -614,7 +615,9 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     PP_HIP(c->cf_err.reserve(2));
     PP_HIP(c->cf_memo.reserve(2 * std::max<size_t>(rows, 1)));
     PP_HIP(c->cf_items.reserve(1 + (size_t)total * kCfItem));
-    const int wgs = std::min(kCfGrid, total);
+    // cf_line_kernel's workgroups: one line at a time each, a lane per edge generating its points
+    // serially — latency-bound, so more lines in flight than check_finish_kernel's grid
+    const int wgs = std::min(kCfLineGrid, total);
     PP_HIP(c->cf_pts.reserve((size_t)wgs * 3 * kCfPtsCap));
     PP_HIP(c->cf_etab.reserve((size_t)wgs * 2 * kCfMaxEdges));
     PP_HIP(c->cf_path.reserve((size_t)wgs * kCfWaves * kCfMaxDepth));
