@@ -252,7 +252,7 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
 // the row-major CSR.  A disc within r + dl of AB has its cull box (>= r) within dl of AB, so in
 // one of those cells.  Called by all 64 lanes; returns a wave-uniform class.
 enum : int { kSUnknown = 0, kSClear = 1, kSHit = 2 };
-constexpr int kSMinPts = 24;  // S segments shorter than this many points are walked as they are
+constexpr int kSMinPts = 64;  // S segments shorter than this many points are walked as they are
 template <bool kLds>
 __device__ int s_classify(const SceneDev& sc, double ax, double ay, double bx, double by,
                           double t_lo, double t_hi, double gap, double dl) {
@@ -1055,44 +1055,84 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
         g.perm[np][pos] = j;
         g.ipos[np][j] = pos;
     }
-    for (int qb = wv; qb * kQPB < Ws; qb += NT / 64) {
-        const int p0 = qb * kQPB;
-        double xs[kQPL], ys[kQPL];
-        double x0 = __builtin_inf(), x1 = -__builtin_inf(), y0 = __builtin_inf(), y1 = -__builtin_inf();
+    // every thread takes sorted positions tid, tid + NT, ... (a wave: 64 consecutive positions,
+    // inside one block): the coordinates again from the stream, the position's stores, and the
+    // wave's f32 bounding box into LDS slot pos / 64 (s_hist is free by now); then one thread per
+    // block merges its waves' boxes into the centre o, and every position stores |q - o|^2.  (r03
+    // gave each block to one wave, 8 samples per lane, and 16 waves shared 4-8 blocks: the
+    // sampling workgroup was nn_finalize's long pole, ~30 of its 27-30 us)
+    // s_bb: [kMaxWindow / 64][4] wave boxes (x0, x1, y0, y1), then [kMaxWindow / kQPB][2] block
+    // centres — over s_hist and the head of s_cell, both dead after the scatter
+    float* s_bb = reinterpret_cast<float*>(s_hist);
+    (void)wv;
+    __syncthreads();  // (s_hist's last readers: the scatter above)
+    constexpr int kMaxK = 4;  // positions per thread: both callers run 1024 threads
+    static_assert(kMaxWindow <= 1024 * kMaxK, "samples_role: positions per thread");
+    static_assert((4 * (kMaxWindow / 64) + 2 * (kMaxWindow / kQPB)) * 4 <= 256 * 4 + kMaxWindow,
+                  "samples_role: the box slots fit s_hist and s_cell");
+    double xs[kMaxK], ys[kMaxK];
 #pragma unroll
-        for (int r = 0; r < kQPL; ++r) {
-            const int pos = p0 + r * 64 + lane;
-            xs[r] = ys[r] = 0.0;
-            if (pos < Ws) {
-                const int j = s_j[pos];
-                const uint64_t itj = (uint64_t)(start + j);
-                xs[r] = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
-                ys[r] = gen_range(g.seed, 2 * itj + 1, g.miny, g.maxy);
-                g.perm[np][pos] = j;
-                g.ipos[np][j] = pos;
-                g.sxy[np][pos] = make_float2((float)xs[r], (float)ys[r]);
-                g.ssx[np][pos] = xs[r];
-                g.ssy[np][pos] = ys[r];
-                x0 = fmin(x0, xs[r]);
-                x1 = fmax(x1, xs[r]);
-                y0 = fmin(y0, ys[r]);
-                y1 = fmax(y1, ys[r]);
+    for (int k = 0; k < kMaxK; ++k) {
+        const int pos = tid + k * NT;
+        xs[k] = ys[k] = 0.0;
+        const bool in = pos < Ws;
+        if (in) {
+            const int j = s_j[pos];
+            const uint64_t itj = (uint64_t)(start + j);
+            xs[k] = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
+            ys[k] = gen_range(g.seed, 2 * itj + 1, g.miny, g.maxy);
+            g.perm[np][pos] = j;
+            g.ipos[np][j] = pos;
+            g.sxy[np][pos] = make_float2((float)xs[k], (float)ys[k]);
+            g.ssx[np][pos] = xs[k];
+            g.ssy[np][pos] = ys[k];
+        }
+        const int wbase = pos - lane;  // the wave's first position (uniform)
+        if (wbase < Ws) {
+            const float inff = __builtin_inff();
+            const float bx0 = wave_min_f32(in ? f32_below(xs[k]) : inff);
+            const float bx1 = wave_max_f32(in ? f32_above(xs[k]) : -inff);
+            const float by0 = wave_min_f32(in ? f32_below(ys[k]) : inff);
+            const float by1 = wave_max_f32(in ? f32_above(ys[k]) : -inff);
+            if (lane == 0) {
+                float* b = s_bb + 4 * (wbase >> 6);
+                b[0] = bx0;
+                b[1] = bx1;
+                b[2] = by0;
+                b[3] = by1;
             }
         }
-        x0 = wave_min(x0);
-        x1 = wave_max(x1);
-        y0 = wave_min(y0);
-        y1 = wave_max(y1);
-        const float oxf = (float)(0.5 * (x0 + x1)), oyf = (float)(0.5 * (y0 + y1));
-        if (lane == 0) g.ob[np][qb] = make_float2(oxf, oyf);
-#pragma unroll
-        for (int r = 0; r < kQPL; ++r) {
-            const int pos = p0 + r * 64 + lane;
-            if (pos < Ws) {
-                const float qpx = (float)(xs[r] - (double)oxf), qpy = (float)(ys[r] - (double)oyf);
-                g.sq[np][s_j[pos]] = (double)qpx * (double)qpx + (double)qpy * (double)qpy;
-            }
+        if (NT * (k + 1) >= kMaxWindow) break;
+    }
+    __syncthreads();
+    const int nqb = (Ws + kQPB - 1) / kQPB;
+    if (tid < nqb) {  // block tid's centre: the middle of its samples' box (f32)
+        float x0 = __builtin_inff(), x1 = -__builtin_inff(), y0 = __builtin_inff(), y1 = -__builtin_inff();
+        for (int w = tid * (kQPB / 64); w < (tid + 1) * (kQPB / 64) && w * 64 < Ws; ++w) {
+            const float* b = s_bb + 4 * w;
+            x0 = fminf(x0, b[0]);
+            x1 = fmaxf(x1, b[1]);
+            y0 = fminf(y0, b[2]);
+            y1 = fmaxf(y1, b[3]);
         }
+        const float2 o = make_float2((float)(0.5 * ((double)x0 + (double)x1)),
+                                     (float)(0.5 * ((double)y0 + (double)y1)));
+        g.ob[np][tid] = o;
+        s_bb[4 * (kMaxWindow / 64) + 2 * tid] = o.x;  // (after the wave slots)
+        s_bb[4 * (kMaxWindow / 64) + 2 * tid + 1] = o.y;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) {
+        const int pos = tid + k * NT;
+        if (pos < Ws) {
+            const int qb = pos / kQPB;
+            const float oxf = s_bb[4 * (kMaxWindow / 64) + 2 * qb];
+            const float oyf = s_bb[4 * (kMaxWindow / 64) + 2 * qb + 1];
+            const float qpx = (float)(xs[k] - (double)oxf), qpy = (float)(ys[k] - (double)oyf);
+            g.sq[np][s_j[pos]] = (double)qpx * (double)qpx + (double)qpy * (double)qpy;
+        }
+        if (NT * (k + 1) >= kMaxWindow) break;
     }
 }
 
