@@ -98,6 +98,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-size-sweep", action="store_true")
     ap.add_argument("--no-sub", action="store_true", help="default workload: config 2 only")
+    ap.add_argument("--pmc-run", action="store_true",
+                    help="config3: no profiled plan pass (counter runs: the last walk dispatches "
+                         "are then the profiled extend's)")
     ap.add_argument("--allow-variant-lib", action="store_true",
                     help="accept PP_AMD_LIB pointing at another build (experiments only)")
     return ap.parse_args(argv)
@@ -635,7 +638,7 @@ def run_batch(args, D, star, with_cpu):
     batch.extend(steps)
     sp = batch.stats()
     evals_p = batch.state()[2] if star else batch.state(with_evals=True)[2]
-    if not star:
+    if not star and not args.pmc_run:
         batch.plan()
         extra["plan"]["roofline"] = finish_roofline(batch.stats())
     batch.close()

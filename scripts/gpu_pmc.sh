@@ -13,7 +13,7 @@ SQB="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_
 args() {
   case $1 in
     config2|config4) echo "--workload $1 --steps 20 --warmup 3 --no-cpu-baseline --no-size-sweep" ;;
-    config3) echo "--workload $1 --warmup 3 --no-cpu-baseline" ;;
+    config3) echo "--workload $1 --warmup 3 --no-cpu-baseline --pmc-run" ;;
     config5) echo "--workload $1 --warmup 3 --no-cpu-baseline --max-iter 600" ;;  # (PMC of 2000 steps crashed the profiler)
   esac
 }
