@@ -185,6 +185,7 @@ struct pp_ctx {
     DBuf<double> mq_x, mq_y, mq_yaw, mq_yawbuf, mq_pdbuf;
     DBuf<int> mq_par, mq_n, mq_status, mq_err;
     DBuf<int64_t> mq_it, mq_evals;
+    DBuf<int64_t> mq_itprev;  // the lockstep NN's verdict cache (MqDev::it_prev)
     DBuf<uint64_t> mq_seed;
     DBuf<uint8_t> mq_blocked;
     bool mq_any_blocked = false;
@@ -769,6 +770,8 @@ MqArgs mq_args(pp_ctx* c) {
     a.mq.K = c->mq_K;
     a.mq.target = c->mq_target.p;
     a.mq.nnd2 = c->mq_nnd2.p;
+    a.mq.it_prev = c->mq_itprev.p;
+    a.mq.status = c->mq_status.p;
     a.sc = c->scene_dev();
     a.sc.step_size = c->mq_step;
     a.st = c->mq_state.p;
@@ -814,6 +817,8 @@ MqArgs mq_sub_args(pp_ctx* c, int sub, int nsub) {
     if (a.mq.blocked) a.mq.blocked += q0;
     a.mq.target += q0;
     a.mq.nnd2 += t0;
+    if (a.mq.it_prev) a.mq.it_prev += q0;
+    if (a.mq.status) a.mq.status += t0;
     a.st = c->mq_state.p + 1 + sub;
     a.tasks += t0;
     a.rec += t0;
@@ -1953,6 +1958,7 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
     PP_HIP(ctx->mq_par.reserve(rows));
     PP_HIP(ctx->mq_n.reserve(q));
     PP_HIP(ctx->mq_it.reserve(q));
+    PP_HIP(ctx->mq_itprev.reserve(q));
     PP_HIP(ctx->mq_evals.reserve(q));
     PP_HIP(ctx->mq_seed.reserve(q));
     PP_HIP(ctx->mq_target.reserve(q));
@@ -2001,6 +2007,8 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
         ctx->mq_K = K;
     }
     if ((r = mq_reserve_tasks(ctx, q, ctx->mq_K))) return r;
+    // the verdict cache starts empty: it_prev far below any iteration (0x80.. bytes)
+    PP_HIP(hipMemsetAsync(ctx->mq_itprev.p, 0x80, q * sizeof(int64_t), st));
     ctx->mq_nsub = mq_nsub(q);  // the sub-batch DevStates are written for this split
     if ((r = mq_write_states(ctx, st))) return r;
     PP_HIP(hipMemsetAsync(ctx->mq_err.p, 0, sizeof(int), st));
@@ -2021,6 +2029,8 @@ int pp_batch_set_window(pp_ctx* ctx, int k) {
         int r = mq_reserve_tasks(ctx, ctx->mq_Q, k);
         if (r) return r;
         ctx->mq_K = k;
+        // a new window length: the task region's layout changes, the verdict cache is void
+        PP_HIP(hipMemsetAsync(ctx->mq_itprev.p, 0x80, ctx->mq_Q * sizeof(int64_t), ctx->stream));
         if ((r = mq_write_states(ctx, ctx->stream))) return r;
         PP_HIP(hipStreamSynchronize(ctx->stream));
     }

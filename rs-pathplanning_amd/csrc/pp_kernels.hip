@@ -1889,7 +1889,8 @@ __device__ __forceinline__ void prep_task(const SceneDev& sc, int r, int g0, int
                                           bool act, double x, double y, double px, double py,
                                           double pyaw, int own, double cyaw, int cull, double cbase,
                                           double climit, PrepRec* __restrict__ rec,
-                                          double* yaw_dst, double* __restrict__ cost_out) {
+                                          double* yaw_dst, double* __restrict__ cost_out,
+                                          int force_state = -1) {
     const double step = sc.step_size;
     const double c = 1.0 / sc.turn_radius;
     const double cy_atan = atan2(py - y, px - x);
@@ -2035,6 +2036,9 @@ __device__ __forceinline__ void prep_task(const SceneDev& sc, int r, int g0, int
     }
     // RRT* cull: an edge whose cost cannot beat the limit is settled without its walk
     if (act && cull && !(cbase + bc < climit)) state = kReject;
+    // the query batch's verdict cache (mq_sample_nn): the same child and parent as a task the
+    // previous step walked — its verdict, no walk
+    if (act && force_state >= 0) state = force_state;
     if (write && r == 0) {  // idle batch tasks get a kReject record (act == false)
         PrepRec o;
         o.x = x;
@@ -2110,9 +2114,11 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
         int j = 0, own = 0, cull = 0;
         double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0, cyaw = 0.0;
         double cbase = 0.0, climit = 0.0;
+        int force = -1;
         if (act && tasks) {
             const SteerTask tk = tasks[t];
             act = tk.pnode >= 0;
+            if (tk.literal >= 2) force = tk.literal - 2;  // (a cached verdict, mq_sample_nn)
             x = tk.x;
             y = tk.y;
             px = act ? tk.px : 1.0;
@@ -2134,7 +2140,7 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
         double* yaw_dst = nullptr;
         if (t < total) yaw_dst = (t < W || tasks) ? snap_yaw + t : &cand[t - W].yaw;
         prep_task(sc, r, g0, t, t < total, act, x, y, px, py, pyaw, own, cyaw, cull, cbase, climit,
-                  rec, yaw_dst, cost_out);
+                  rec, yaw_dst, cost_out, force);
     }
 }
 
@@ -4173,11 +4179,25 @@ __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx
         const int64_t it = mq.it[q] + k;
         const bool live = it < mq.target[q];
         const uint64_t seed = mq.seed[q];
+        // the verdict cache: the task region still holds the previous step's window, which
+        // started Tp iterations before this one, so iteration it sat in old slot k + Tp; its
+        // parent and verdict are read before any lane overwrites the region
+        int opn = -1, ost = -1;
+        if (mq.it_prev && g == 0) {
+            const int64_t Tp = mq.it[q] - mq.it_prev[q];
+            if (Tp >= 0 && Tp < K && k + Tp < K) {
+                const int to = q * K + k + (int)Tp;
+                opn = tasks[to].pnode;
+                ost = mq.status[to];
+            }
+        }
         double x = 0.0, y = 0.0;
         if (live) {
             x = gen_range(seed, 2 * (uint64_t)it, minx, maxx);
             y = gen_range(seed, 2 * (uint64_t)it + 1, miny, maxy);
         }
+        // the pre-test first (its loads overlap the scan; its result is used after it)
+        const bool blocked = live && scp && point_blocked<false, kSceneAny>(*scp, x, y);
         const int n = mq.n[q];
         const size_t row = (size_t)q * mq.cap;
         const double* __restrict__ X = mq.x + row;
@@ -4205,17 +4225,22 @@ __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx
             const int t = q * K + k;
             if (!live) {
                 tasks[t].pnode = -1;
-            } else if (scp && point_blocked<false, kSceneAny>(*scp, x, y)) {
+            } else if (blocked) {
                 // the sample lies in an obstacle: rejected whatever its parent (pnode -2: no steer,
                 // and the insert never cuts the window there)
                 tasks[t].x = x;
                 tasks[t].y = y;
                 tasks[t].pnode = -2;
             } else {
-                tasks[t] = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, 0};
+                // the same child (the counter RNG redraws it) and the same parent pose (rows are
+                // never rewritten) as a task the previous step walked: its verdict (kReject 0 /
+                // kAccept 1, as 2 + verdict) rides along and steer_prep writes it as decided
+                const int cached = (opn == bi && (ost == kAccept || ost == kReject)) ? 2 + ost : 0;
+                tasks[t] = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, cached};
                 mq.nnd2[t] = bd;
             }
         }
+        if (mq.it_prev && lane == 0) mq.it_prev[q] = mq.it[q];
     }
 }
 
@@ -4340,10 +4365,7 @@ hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int
     return hipGetLastError();
 }
 
-#ifndef PP_S_BATCH_TASKS
-#define PP_S_BATCH_TASKS 0
-#endif
-constexpr int kSBatchTasks = PP_S_BATCH_TASKS;  // tasks per step from which the batch walk uses s_classify
+constexpr int kBigStepTasks = 32768;  // tasks per step from which the batch walk runs at 6 waves
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int Q = a.mq.Q;
     const int T = Q * a.mq.K;  // tasks per step
@@ -4363,14 +4385,17 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
                                                               nullptr, nullptr, a.rec, a.pdbuf,
                                                               a.yaw, a.tasks);
         if (ev) (void)hipEventRecord(ev[2], s);
-        // the analytic straight segments (s_classify) pay where the walk is throughput-bound:
-        // large steps; a small shard's step is latency-bound and walks without them
-        if (T >= kSBatchTasks)
+        // with the analytic straight segments (s_classify).  A large step is throughput-bound
+        // and walks at 6 waves per SIMD (80 VGPRs); a small shard's step is latency-bound and
+        // walks at 5 (96 VGPRs, the spill 60 -> 12 B per lane): the 1024-query shard 271 ->
+        // 277 M it/s, the 8192-query batch 634 -> 618 M if it did the same (one box)
+        if (T >= kBigStepTasks)
             launch_walk<kWalkMinWBatch, true>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf, nullptr,
                                               a.status, nullptr, nullptr, a.wg_points);
         else
-            launch_walk<kWalkMinWBatch, false>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf, nullptr,
-                                               a.status, nullptr, nullptr, a.wg_points);
+            launch_walk<kWalkMinWBatch - 1, true>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf,
+                                                  nullptr, a.status, nullptr, nullptr,
+                                                  a.wg_points);
         if (ev) (void)hipEventRecord(ev[3], s);
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
                                                     a.lit_scratch, a.lit_locks, a.err);

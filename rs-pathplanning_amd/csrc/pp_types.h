@@ -213,6 +213,11 @@ struct MqDev {
     int K;
     const int64_t* target;  // [Q] iteration this pp_batch_extend call stops at
     double* nnd2;           // [Q * K] exact d2 of each task's snapshot nearest node
+    // the verdict cache of the lockstep steps: it_prev[q] = the iteration of slot 0 of the tasks
+    // now in the task region (the previous step's), so a window that starts T iterations later
+    // finds iteration it + k in old slot k + T; null: no cache (RRT* rows)
+    int64_t* it_prev = nullptr;
+    const int* status = nullptr;  // the previous step's verdicts (the task region's)
 };
 // RRT* batch (BASELINE config 5; build-defined, oracle/pp_oracle.c orc_star_extend, DESIGN.md
 // §3.7): Q independent RRT* trees in the MqDev rows (K = 1), one iteration per query and step in
