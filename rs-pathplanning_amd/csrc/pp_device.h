@@ -291,7 +291,9 @@ __device__ inline int dubins_local(double lex, double ley, double leyaw, double 
 // Literal single-thread restatement of dubins_path_planning (dubins.rs:401-428) writing WORLD
 // points: the slow path for the measure-zero trim cases, and the pp_dubins_batch API.
 // Returns kSteerSome / kSteerNone / kSteerOverflow (cap < n_point or the Rust index panic).
-template <bool kFI = false>
+// kYaw = false: the world yaws are not wrapped back (pyaw keeps the local ones): check_finish's
+// lines need the points only, and pi_2_pi's fmod per point cost more than the points
+template <bool kFI = false, bool kYaw = true>
 __device__ inline int dubins_literal(double sx, double sy, double syaw, double ex0, double ey0,
                                      double eyaw, double turn_radius, double step_size, double* px,
                                      double* py, double* pyaw, int cap, int* n_out, int* word_out,
@@ -311,7 +313,7 @@ __device__ inline int dubins_literal(double sx, double sy, double syaw, double e
         const double x = px[i], y = py[i];
         px[i] = cs * x + sn * y + sx;
         py[i] = -sn * x + cs * y + sy;
-        pyaw[i] = pi_2_pi(pyaw[i] + syaw);
+        if (kYaw) pyaw[i] = pi_2_pi(pyaw[i] + syaw);
     }
     *n_out = len;
     return kSteerSome;

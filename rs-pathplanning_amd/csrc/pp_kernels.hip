@@ -3627,9 +3627,10 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
                 const CfPose a = pose(e), bp = pose(e + 1);
                 int n = 0, word = -1;
                 double cost = 0.0;
-                const int r = dubins_literal(a.x, a.y, a.yaw, bp.x, bp.y, bp.yaw, sc.turn_radius,
-                                             sc.step_size, px + off, py + off, pyw + off, cap, &n,
-                                             &word, &cost);
+                const int r = dubins_literal<false, false>(a.x, a.y, a.yaw, bp.x, bp.y, bp.yaw,
+                                                           sc.turn_radius, sc.step_size, px + off,
+                                                           py + off, pyw + off, cap, &n, &word,
+                                                           &cost);
                 et[2 * e + 1] = r == kSteerSome ? n : 0;
                 if (r != kSteerSome) atomicOr(&s_bad, 2);
             }
