@@ -4162,87 +4162,93 @@ hipError_t launch_cfb_steer(hipStream_t s, const SceneDev& sc, const CfbArgs& a,
 //   steer_prep / steer_walk   the window pipeline's kernels on the Q explicit tasks
 //   mq_insert      the verdict (literal path for the measure-zero trim cases), append, it += 1
 // Queries are independent, so there is no speculation and no resolve.
+// One query's window of the lockstep step (one wave, all 64 lanes): lane l serves window slot
+// k = l % K over node group g = l / K (nodes i = g mod 64/K), so every node row is loaded once per
+// wave, not once per slot.  Space::rand_point of iteration it[q] + k on stream q (rrt.rs:139-146,
+// Q7), the obstacle pre-test, the exact nearest node of tree q as the step found it (rrt.rs:378-391,
+// Q9: lanes stride the rows, lowest index on ties), the verdict cache; the task into
+// tasks[q K + k].
+__device__ __forceinline__ void mq_nn_query(const MqDev& mq, double minx, double maxx, double miny,
+                                            double maxy, SteerTask* __restrict__ tasks,
+                                            const SceneDev* __restrict__ scp, int q, int lane) {
+    const int K = mq.K, G = 64 / K;
+    const int k = lane & (K - 1), g = lane / K;
+    const int64_t it = mq.it[q] + k;
+    const bool live = it < mq.target[q];
+    const uint64_t seed = mq.seed[q];
+    // the verdict cache: the task region still holds the previous step's window, which
+    // started Tp iterations before this one, so iteration it sat in old slot k + Tp; its
+    // parent and verdict are read before any lane overwrites the region
+    int opn = -1, ost = -1;
+    if (mq.it_prev && g == 0) {
+        const int64_t Tp = mq.it[q] - mq.it_prev[q];
+        if (Tp >= 0 && Tp < K && k + Tp < K) {
+            const int to = q * K + k + (int)Tp;
+            opn = tasks[to].pnode;
+            ost = mq.status[to];
+        }
+    }
+    double x = 0.0, y = 0.0;
+    if (live) {
+        x = gen_range(seed, 2 * (uint64_t)it, minx, maxx);
+        y = gen_range(seed, 2 * (uint64_t)it + 1, miny, maxy);
+    }
+    // the pre-test first (its loads overlap the scan; its result is used after it)
+    const bool blocked = live && scp && point_blocked<false, kSceneAny>(*scp, x, y);
+    const int n = mq.n[q];
+    const size_t row = (size_t)q * mq.cap;
+    const double* __restrict__ X = mq.x + row;
+    const double* __restrict__ Y = mq.y + row;
+    double bd = __builtin_inf();
+    int bi = 0x7fffffff;
+#pragma unroll 4
+    for (int i = g; i < n; i += G) {
+        const double dx = x - X[i], dy = y - Y[i];
+        const double d2 = dx * dx + dy * dy;
+        if (d2 < bd) {
+            bd = d2;
+            bi = i;
+        }
+    }
+    for (int m = K; m < 64; m <<= 1) {  // the G lanes of slot k
+        if (m == 16)
+            argmin_swap<false>(bd, bi);
+        else if (m == 32)
+            argmin_swap<true>(bd, bi);
+        else
+            argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
+    }
+    if (g == 0) {
+        const int t = q * K + k;
+        if (!live) {
+            tasks[t].pnode = -1;
+        } else if (blocked) {
+            // the sample lies in an obstacle: rejected whatever its parent (pnode -2: no steer,
+            // and the insert never cuts the window there)
+            tasks[t].x = x;
+            tasks[t].y = y;
+            tasks[t].pnode = -2;
+        } else {
+            // the same child (the counter RNG redraws it) and the same parent pose (rows are
+            // never rewritten) as a task the previous step walked: its verdict (kReject 0 /
+            // kAccept 1, as 2 + verdict) rides along and steer_prep writes it as decided
+            const int cached = (opn == bi && (ost == kAccept || ost == kReject)) ? 2 + ost : 0;
+            tasks[t] = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, cached};
+            mq.nnd2[t] = bd;
+        }
+    }
+    if (mq.it_prev && lane == 0) mq.it_prev[q] = mq.it[q];
+}
+
 __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx, double maxx,
                                                            double miny, double maxy,
                                                            SteerTask* __restrict__ tasks,
                                                            const SceneDev* __restrict__ scp) {
-    // one wave per task t = q * K + k: Space::rand_point of iteration it[q] + k on stream q
-    // (rrt.rs:139-146, Q7) and the exact nearest node of tree q as the step found it
-    // (rrt.rs:378-391, Q9: lanes stride the rows, lowest index on ties)
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    // one wave per query: lane l serves window slot k = l % K over node group g = l / K (nodes
-    // i = g mod 64/K), so every node row is loaded once per wave, not once per slot
-    const int K = mq.K, G = 64 / K;
-    const int k = lane & (K - 1), g = lane / K;
-    for (int q = gw; q < mq.Q; q += nw) {
-        const int64_t it = mq.it[q] + k;
-        const bool live = it < mq.target[q];
-        const uint64_t seed = mq.seed[q];
-        // the verdict cache: the task region still holds the previous step's window, which
-        // started Tp iterations before this one, so iteration it sat in old slot k + Tp; its
-        // parent and verdict are read before any lane overwrites the region
-        int opn = -1, ost = -1;
-        if (mq.it_prev && g == 0) {
-            const int64_t Tp = mq.it[q] - mq.it_prev[q];
-            if (Tp >= 0 && Tp < K && k + Tp < K) {
-                const int to = q * K + k + (int)Tp;
-                opn = tasks[to].pnode;
-                ost = mq.status[to];
-            }
-        }
-        double x = 0.0, y = 0.0;
-        if (live) {
-            x = gen_range(seed, 2 * (uint64_t)it, minx, maxx);
-            y = gen_range(seed, 2 * (uint64_t)it + 1, miny, maxy);
-        }
-        // the pre-test first (its loads overlap the scan; its result is used after it)
-        const bool blocked = live && scp && point_blocked<false, kSceneAny>(*scp, x, y);
-        const int n = mq.n[q];
-        const size_t row = (size_t)q * mq.cap;
-        const double* __restrict__ X = mq.x + row;
-        const double* __restrict__ Y = mq.y + row;
-        double bd = __builtin_inf();
-        int bi = 0x7fffffff;
-#pragma unroll 4
-        for (int i = g; i < n; i += G) {
-            const double dx = x - X[i], dy = y - Y[i];
-            const double d2 = dx * dx + dy * dy;
-            if (d2 < bd) {
-                bd = d2;
-                bi = i;
-            }
-        }
-        for (int m = K; m < 64; m <<= 1) {  // the G lanes of slot k
-            if (m == 16)
-                argmin_swap<false>(bd, bi);
-            else if (m == 32)
-                argmin_swap<true>(bd, bi);
-            else
-                argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
-        }
-        if (g == 0) {
-            const int t = q * K + k;
-            if (!live) {
-                tasks[t].pnode = -1;
-            } else if (blocked) {
-                // the sample lies in an obstacle: rejected whatever its parent (pnode -2: no steer,
-                // and the insert never cuts the window there)
-                tasks[t].x = x;
-                tasks[t].y = y;
-                tasks[t].pnode = -2;
-            } else {
-                // the same child (the counter RNG redraws it) and the same parent pose (rows are
-                // never rewritten) as a task the previous step walked: its verdict (kReject 0 /
-                // kAccept 1, as 2 + verdict) rides along and steer_prep writes it as decided
-                const int cached = (opn == bi && (ost == kAccept || ost == kReject)) ? 2 + ost : 0;
-                tasks[t] = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, cached};
-                mq.nnd2[t] = bd;
-            }
-        }
-        if (mq.it_prev && lane == 0) mq.it_prev[q] = mq.it[q];
-    }
+    for (int q = gw; q < mq.Q; q += nw)
+        mq_nn_query(mq, minx, maxx, miny, maxy, tasks, scp, q, lane);
 }
 
 // the iteration targets of one pp_batch_extend call: n_steps more iterations, at most max_iter
@@ -4367,6 +4373,7 @@ hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int
 }
 
 constexpr int kBigStepTasks = 32768;  // tasks per step from which the batch walk runs at 6 waves
+
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int Q = a.mq.Q;
     const int T = Q * a.mq.K;  // tasks per step
