@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -709,6 +710,8 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     PP_HIP(hipMemcpyAsync(misc, c->cfb_misc.p, sizeof misc, hipMemcpyDeviceToHost, st));
     PP_HIP(hipStreamSynchronize(st));
     const int np = misc[1];
+    if (std::getenv("PP_AMD_CF_VERBOSE"))  // profiling: the items check_finish_kernel takes
+        std::fprintf(stderr, "cf_run_rounds: items %d punted %d rounds %d\n", total, np, rounds);
     CfBatch cb = cb_in;
     cb.ftab = a.ftab;
     cb.gtab = a.gtab;

@@ -2353,6 +2353,13 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
             }
             grid += cnt;
             done = gseg >= 3;
+            // trim1: the last segment's final grid point landed in lane 63 (its next value is
+            // past |L|): end here, so the drop below pops it in this chunk instead of one already
+            // tested (the segment's end, dubins.rs:256, needs no ll: nothing follows)
+            if (trim1 && !done && gseg == 2 && pos > 63 && !(fabs(gpd) <= fabs(L2))) {
+                gseg = 3;
+                done = true;
+            }
         } else {
             const int rem = partial ? 63 : ng - base;
             cnt = rem < 63 ? rem : 63;
@@ -3550,11 +3557,118 @@ __global__ __launch_bounds__(kCfThreads, kCfMinW) void check_finish_kernel(
     }
 }
 
+// dubins_literal<false, false> (dubins.rs:326-428) of one edge by one wave: the WORLD points of
+// the trimmed course into px / py (cap >= n_point), *n_out = their count.  generate_local_course
+// (dubins.rs:200-272) writes the origin at index 0, each segment's grid points from the slot of
+// the previous segment's end on (that end is overwritten), and the last segment's end after its
+// grid points; the rest of the n_point slots stay 0.0.  The grid values of a segment are the
+// serial chain pd, pd + d, ... (every lane runs the uniform chain and keeps its own term, the
+// same rounding sequence), 64 per pass; each lane interpolates its point (dubins.rs:155-198) and
+// moves it to the world frame (dubins.rs:412-422).  The trim (dubins.rs:281-288) keeps the
+// indices below the last one whose local x is nonzero (none: 0), or all n_point when the last
+// slot is written and nonzero.  Returns kSteerSome / kSteerNone / kSteerOverflow like the
+// literal restatement.
+__device__ int line_edge_wave(double sx, double sy, double syaw, double ex0, double ey0,
+                              double eyaw, double turn_radius, double step_size, double* px,
+                              double* py, int cap, int lane, int* n_out) {
+    const double ex = ex0 - sx, ey = ey0 - sy;
+    const double c = 1.0 / turn_radius;
+    const double lex = cos(syaw) * ex + sin(syaw) * ey;
+    const double ley = -(sin(syaw)) * ex + cos(syaw) * ey;
+    const double leyaw = eyaw - syaw;
+    const Steer s = select_word(lex, ley, leyaw, c);
+    if (s.word < 0) return kSteerNone;
+    const double lengths[3] = {s.t, s.p, s.q};
+    double total = 0.0;
+    total += s.t;
+    total += s.p;
+    total += s.q;
+    const double nq = trunc(total / step_size);
+    if (!(nq >= 0.0) || nq > 1.0e8) return kSteerOverflow;
+    const int n_point = (int)nq + 3 + 4;
+    if (n_point > cap) return kSteerOverflow;
+    const double cs = cos(-syaw), sn = sin(-syaw);
+    if (lane == 0) {  // the origin, index 0
+        px[0] = cs * 0.0 + sn * 0.0 + sx;
+        py[0] = -sn * 0.0 + cs * 0.0 + sy;
+    }
+    int ind = 0;      // the last index written
+    int lastnz = -1;  // the last index whose local x is nonzero
+    double lastx = 0.0;
+    Pose o{0.0, 0.0, 0.0};
+    double ll = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        const int m = word_mode(s.word, i);
+        const double l = lengths[i];
+        const double d = (l > 0.0) ? step_size : -step_size;
+        // interp_local's trig of the segment's origin yaw (per point in the serial form, the same
+        // values)
+        const double co = cos(o.yaw), so = sin(o.yaw), cmo = cos(-o.yaw), smo = sin(-o.yaw);
+        const double al = fabs(l);
+        double pd = (i >= 1 && (lengths[i - 1] * lengths[i]) > 0.0) ? (-d - ll) : (d - ll);
+        int base = i == 0 ? 1 : ind;  // the slot of this segment's first grid point
+        ind = base - 1;               // (dubins.rs:227: ind -= 1)
+        for (;;) {
+            double my = 0.0, w = pd;
+            for (int u = 0; u < 64; ++u) {
+                if (lane == u) my = w;
+                w += d;
+            }
+            const uint64_t bad = __ballot(!(fabs(my) <= al));
+            const int cnt = bad ? (int)__builtin_ctzll(bad) : 64;
+            if (cnt > 0 && base + cnt - 1 >= n_point) return kSteerOverflow;
+            if (lane < cnt) {
+                double lx, ly;
+                if (m == kModeS) {
+                    lx = o.x + my / c * co;
+                    ly = o.y + my / c * so;
+                } else {
+                    const double ldx = sin(my) / c;
+                    const double ldy = m == kModeL ? (1.0 - cos(my)) / c : (1.0 - cos(my)) / -c;
+                    lx = o.x + (cmo * ldx + smo * ldy);
+                    ly = o.y + (-smo * ldx + cmo * ldy);
+                }
+                px[base + lane] = cs * lx + sn * ly + sx;
+                py[base + lane] = -sn * lx + cs * ly + sy;
+                const uint64_t nz = __ballot(lx != 0.0);
+                if (nz) lastnz = base + 63 - (int)__builtin_clzll(nz);
+                lastx = lx;
+            }
+            if (cnt > 0) {
+                ind = base + cnt - 1;
+                lastx = readlane_f64(lastx, cnt - 1);
+            }
+            if (cnt < 64) {
+                ll = l - readlane_f64(my, cnt) - d;
+                break;
+            }
+            base += 64;
+            pd = w;
+        }
+        // the segment's end (dubins.rs:262-267) at the next slot; the next segment starts there
+        ind += 1;
+        if (ind >= n_point) return kSteerOverflow;
+        const Pose r = interp_local(m, l, c, o);
+        if (i == 2) {
+            if (lane == 0) {
+                px[ind] = cs * r.x + sn * r.y + sx;
+                py[ind] = -sn * r.x + cs * r.y + sy;
+            }
+            if (r.x != 0.0) lastnz = ind;
+            lastx = r.x;
+        }
+        o = r;
+    }
+    // the trim: every trailing 0.0 (the unwritten slots) and one more element
+    *n_out = (ind == n_point - 1 && lastx != 0.0) ? n_point : (lastnz > 0 ? lastnz : 0);
+    return kSteerSome;
+}
+
 // The lines of check_finish_kernel's line items: workgroup w takes items w, w + grid, ... (item
 // i < grid: the workgroup-i buffers, so a one-node call's line is in workgroup 0's); every
-// edge's literal Dubins points (dubins_literal, a lane per edge) into the workgroup's pts / etab,
-// then l.reverse() and geo's euclidean_length in that order (rrt.rs:538, one lane: a sum of
-// hypot in line order).
+// edge's literal Dubins points (line_edge_wave, a wave per edge) into the workgroup's pts / etab,
+// then l.reverse() and geo's euclidean_length in that order (rrt.rs:538: the hypots in parallel,
+// their sum in line order).
 __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
     SceneDev sc, TreeDev tr_in, const int* __restrict__ nodes, double gx_in, double gy_in,
     double gyaw_in, double gyaw_opt_in, int* __restrict__ ok_out, double* __restrict__ len_out,
@@ -3621,18 +3735,18 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
         if (total < 0) {
             if (tid == 0) s_bad = total == -2 ? 2 : 8;
         } else {
-            for (int e = tid; e < E; e += kCfThreads) {
+            const int lane = tid & 63;
+            for (int e = tid >> 6; e < E; e += kCfThreads / 64) {
                 const int off = et[2 * e];
                 const int cap = (e + 1 < E ? et[2 * e + 2] : total) - off;
                 const CfPose a = pose(e), bp = pose(e + 1);
-                int n = 0, word = -1;
-                double cost = 0.0;
-                const int r = dubins_literal<false, false>(a.x, a.y, a.yaw, bp.x, bp.y, bp.yaw,
-                                                           sc.turn_radius, sc.step_size, px + off,
-                                                           py + off, pyw + off, cap, &n, &word,
-                                                           &cost);
-                et[2 * e + 1] = r == kSteerSome ? n : 0;
-                if (r != kSteerSome) atomicOr(&s_bad, 2);
+                int n = 0;
+                const int r = line_edge_wave(a.x, a.y, a.yaw, bp.x, bp.y, bp.yaw, sc.turn_radius,
+                                             sc.step_size, px + off, py + off, cap, lane, &n);
+                if (lane == 0) {
+                    et[2 * e + 1] = r == kSteerSome ? n : 0;
+                    if (r != kSteerSome) atomicOr(&s_bad, 2);
+                }
             }
         }
         __syncthreads();
@@ -3664,18 +3778,29 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
             }
         }
         __syncthreads();
-        if (tid == 0) {
+        if (tid < 64) {
+            // the reversed sum, wave 0: 64 hypots a load (lane j holds pyw[hi - j], the next
+            // chunk's load in flight), added in lane order by readlane — the serial order
             double len = 0.0;
             int npts = 0;
             const int bad = s_bad;
             if (bad == 0) {
                 for (int e = 0; e < E; ++e) npts += et[2 * e + 1];
-                for (int f = npts - 2; f >= 0; --f) len += pyw[f];
+                int hi = npts - 2;
+                double v = hi - tid >= 0 ? pyw[hi - tid] : 0.0;
+                for (; hi >= 0; hi -= 64) {
+                    const double cur = v;
+                    v = hi - 64 - tid >= 0 ? pyw[hi - 64 - tid] : 0.0;
+                    const int m = hi < 63 ? hi + 1 : 64;
+                    for (int j = 0; j < m; ++j) len += readlane_f64(cur, j);
+                }
             }
-            ok_out[b] = (vok && bad == 0) ? 1 : 0;
-            len_out[b] = bad == 0 ? len : 0.0;
-            npts_out[b] = bad == 0 ? npts : 0;
-            if (bad) atomicOr(err, bad);
+            if (tid == 0) {
+                ok_out[b] = (vok && bad == 0) ? 1 : 0;
+                len_out[b] = bad == 0 ? len : 0.0;
+                npts_out[b] = bad == 0 ? npts : 0;
+                if (bad) atomicOr(err, bad);
+            }
         }
         __syncthreads();  // the buffers and s_off serve the next item
     }
@@ -3968,8 +4093,12 @@ __global__ __launch_bounds__(256) void cfb_emit_b_kernel(CfbArgs a) {
         ok = cfb_chain(a, o, c, a.depth[b], n, pos, s, fnone);
         if (ok) {
             cnt = 1;
+            // (a plain L2 read first: the edges near a query's root are claimed once and read by
+            // most of its items — an exchange each serialised on those few addresses)
             for (int e = 1; e < s; ++e)
-                if (atomicExch(&a.gclaim[o + n[e - 1]], 1) == 0) {
+                if (__hip_atomic_load(&a.gclaim[o + n[e - 1]], __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+                    atomicExch(&a.gclaim[o + n[e - 1]], 1) == 0) {
                     claimed |= 1u << e;
                     ++cnt;
                 }
