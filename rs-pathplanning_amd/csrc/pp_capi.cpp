@@ -608,6 +608,30 @@ int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line,
 // whose verdicts are known, and check_finish_kernel runs the rest (literal paths, errors) with
 // the memo filled.  The same results as cf_run over all items; polygon scenes and batches with
 // a blocked root take cf_run.
+// profiling (PP_AMD_CF_VERBOSE): the walk statuses of a round's tasks
+static void cfb_status_hist(pp_ctx* c, const CfbArgs& a, int round) {
+    DevState ds;
+    if (hipMemcpyAsync(&ds, a.st, sizeof ds, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return;
+    std::vector<int> v((size_t)std::max(ds.W, 0));
+    std::vector<PrepRec> rc((size_t)std::max(ds.W, 0));
+    if (ds.W > 0) {
+        if (hipMemcpy(v.data(), a.status, v.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return;
+        if (hipMemcpy(rc.data(), a.rec, rc.size() * sizeof(PrepRec), hipMemcpyDeviceToHost) != hipSuccess) return;
+    }
+    int h[16] = {0};
+    int trim = 0, lit_trim = 0, none = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+        h[std::min(std::max(v[i] + 4, 0), 15)]++;
+        trim += rc[i].trim1;
+        lit_trim += rc[i].trim1 && v[i] == kLiteral;
+        none += rc[i].state == kPrepNone;
+    }
+    std::fprintf(stderr, "cfb round %d: W %d status(-4..) ", round, ds.W);
+    for (int k = 0; k < 12; ++k) std::fprintf(stderr, "%d:%d ", k - 4, h[k]);
+    std::fprintf(stderr, " trim1 %d (literal %d) none %d\n", trim, lit_trim, none);
+}
+
 int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in, const CfOut& o) {
     const int Q = c->mq_Q;
     const size_t nn = (size_t)total + Q;
@@ -700,10 +724,16 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     for (int r = 0; r < rounds; ++r) {
         PP_HIP(launch_cfb(st, sd, a, kCfbEmitA, r));
         PP_HIP(launch_cfb_steer(st, sd, a, (int)std::min<size_t>(cap_tasks, (size_t)kCfbSpan * nn), false, wpts));
+        PP_HIP(launch_cfb_literal(st, sd, a, (int)std::min<size_t>(cap_tasks, (size_t)kCfbSpan * nn),
+                                  c->api_lit_scratch.p, c->lit_locks.p));
+        if (std::getenv("PP_AMD_CF_VERBOSE")) cfb_status_hist(c, a, r);
         PP_HIP(launch_cfb(st, sd, a, kCfbConsumeA, r));
     }
     PP_HIP(launch_cfb(st, sd, a, kCfbEmitB, 0));
     PP_HIP(launch_cfb_steer(st, sd, a, (int)std::min<size_t>(cap_tasks, 2 * nn), true, wpts));
+    PP_HIP(launch_cfb_literal(st, sd, a, (int)std::min<size_t>(cap_tasks, 2 * nn),
+                              c->api_lit_scratch.p, c->lit_locks.p));
+    if (std::getenv("PP_AMD_CF_VERBOSE")) cfb_status_hist(c, a, 100);
     PP_HIP(launch_cfb(st, sd, a, kCfbStoreB, (int)std::min<size_t>(cap_tasks, 2 * nn)));
     PP_HIP(launch_cfb(st, sd, a, kCfbAssemble, 0, o.ok, o.len, o.npts, c->cf_err.p, c->cf_items.p,
                       c->cfb_plist.p));

@@ -137,6 +137,9 @@ hipError_t launch_cfb(hipStream_t s, const SceneDev& sc, CfbArgs a, int phase, i
                       int* err = nullptr, int* items = nullptr, int* plist = nullptr);
 hipError_t launch_cfb_steer(hipStream_t s, const SceneDev& sc, const CfbArgs& a, int max_tasks,
                             bool own_yaw, long long* wg_points = nullptr);
+// the rounds' literal-path tasks re-run by steer_collide_literal (a scratch slot per wave)
+hipError_t launch_cfb_literal(hipStream_t s, const SceneDev& sc, const CfbArgs& a, int max_tasks,
+                              double* lit_scratch, int* lit_locks);
 hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const SceneDev* scg,
                                const TreeDev& tr,
                                const int* nodes, int k, double gx, double gy, double gyaw,

@@ -4168,6 +4168,43 @@ __global__ __launch_bounds__(256) void cfb_store_b_kernel(CfbArgs a) {
         a.gtab[-1 - n] = s + 1;
 }
 
+// after a rounds walk: the literal-path tasks (the trim cases steer_walk hands back, e.g. the
+// zero-length copy edges at a root, whose points are all 0.0) re-run by steer_collide_literal,
+// as mq_insert does for the extend tasks, so their verdicts reach the memo instead of punting
+// every item whose chain holds them to check_finish_kernel
+__global__ __launch_bounds__(256) void cfb_literal_kernel(CfbArgs a, SceneDev sc,
+                                                          double* __restrict__ lit_scratch,
+                                                          int* __restrict__ lit_locks) {
+    const int W = a.st->W;
+    const int lane = threadIdx.x & 63;
+    const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    for (int base = gw * 64; base < W; base += nw * 64) {
+        const int t = base + lane;
+        const int st = t < W ? a.status[t] : kReject;
+        uint64_t lit = __ballot(st == kLiteral);
+        if (!lit) continue;
+        const int slot = lit_acquire(lit_locks, gw);
+        double* bx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
+        for (; lit; lit &= lit - 1) {
+            const int tt = base + __builtin_ctzll(lit);
+            const SteerTask tk = a.tasks[tt];
+            const int r = steer_collide_literal(sc, tk.x, tk.y, a.yaw[tt], tk.px, tk.py, tk.pyaw,
+                                                bx, bx + kLiteralCap, bx + 2 * kLiteralCap);
+            if (lane == 0) a.status[tt] = r;
+        }
+        lit_release(lit_locks, slot);
+    }
+}
+
+hipError_t launch_cfb_literal(hipStream_t s, const SceneDev& sc, const CfbArgs& a, int max_tasks,
+                              double* lit_scratch, int* lit_locks) {
+    if (max_tasks <= 0) return hipSuccess;
+    const int g = std::min((max_tasks + 255) / 256, 1024);
+    cfb_literal_kernel<<<g, 256, 0, s>>>(a, sc, lit_scratch, lit_locks);
+    return hipGetLastError();
+}
+
 // one lane per item: finalize's verdict from the memo (check_finish_kernel's order and
 // precedence), its outputs or its line item; an item with an unknown verdict goes to plist
 __global__ __launch_bounds__(256) void cfb_assemble_kernel(CfbArgs a, int* __restrict__ ok_out,
