@@ -211,7 +211,7 @@ struct pp_ctx {
     // pp_batch_plan's check_finish in steer rounds (CfbArgs)
     DBuf<int> cfb_nodei;   // [4 (nitems + Q)]: depth, open, tfirst, tcnt
     DBuf<int> cfb_rows;    // [3 rows]: gclaim, tnone, tnone_up
-    DBuf<int> cfb_gotab, cfb_plist, cfb_tnode, cfb_status, cfb_misc;
+    DBuf<int> cfb_gotab, cfb_plist, cfb_tnode, cfb_status, cfb_misc, cfb_lit;
     DBuf<SteerTask> cfb_tasks;
     DBuf<StarTaskExt> cfb_ext;
     DBuf<PrepRec> cfb_rec;
@@ -220,6 +220,7 @@ struct pp_ctx {
     DBuf<long long> cfb_pts;  // profiling: the rounds' walk point tallies
     int64_t cfb_nodes = 0, cfb_edges = 0, cfb_points = 0, cfb_arc = 0;  // profiling
     bool cf_rounds = true;  // pp_batch_plan in steer rounds (PP_AMD_CF_ROUNDS=0: one kernel, A/B)
+    int cfb_span0 = kCfbSpan, cfb_span = kCfbSpan;  // phase A candidates per node: first / later rounds
 
     // ---- RRT* query batch (BASELINE config 5, build-defined: DESIGN.md §3.7)
     bool has_star = false;
@@ -636,7 +637,8 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     const int Q = c->mq_Q;
     const size_t nn = (size_t)total + Q;
     const size_t rows = (size_t)Q * (size_t)cb_in.row_cap;
-    const size_t cap_tasks = std::max<size_t>(4 * nn, 1);  // phase A: <= kCfbSpan per node; B: <= 2 per node
+    // phase A: <= span tasks per node; B: <= 2 per node
+    const size_t cap_tasks = std::max<size_t>((size_t)std::max({c->cfb_span0, c->cfb_span, 2}) * nn, 1);
     hipStream_t st = c->stream;
     PP_HIP(c->cf_err.reserve(2));
     PP_HIP(c->cf_memo.reserve(2 * std::max<size_t>(rows, 1)));
@@ -658,6 +660,7 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     PP_HIP(c->cfb_plist.reserve(std::max(total, 1)));
     PP_HIP(c->cfb_tnode.reserve(cap_tasks));
     PP_HIP(c->cfb_status.reserve(cap_tasks));
+    PP_HIP(c->cfb_lit.reserve(cap_tasks));
     PP_HIP(c->cfb_tasks.reserve(cap_tasks));
     PP_HIP(c->cfb_ext.reserve(cap_tasks));
     PP_HIP(c->cfb_rec.reserve(cap_tasks));
@@ -719,20 +722,24 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     int misc[4] = {0, 0, 0, 0};
     PP_HIP(hipMemcpyAsync(misc, c->cfb_misc.p, sizeof misc, hipMemcpyDeviceToHost, st));
     PP_HIP(hipStreamSynchronize(st));
-    const int rounds = (misc[0] + 1 + kCfbSpan - 1) / kCfbSpan;
+    // round r tests the candidates at depths m0 .. m0 + span - 1 of every open node: the first
+    // round cfb_span0 of them, the later ones cfb_span
     long long* wpts = c->prof ? c->cfb_pts.p : nullptr;
-    for (int r = 0; r < rounds; ++r) {
-        PP_HIP(launch_cfb(st, sd, a, kCfbEmitA, r));
-        PP_HIP(launch_cfb_steer(st, sd, a, (int)std::min<size_t>(cap_tasks, (size_t)kCfbSpan * nn), false, wpts));
-        PP_HIP(launch_cfb_literal(st, sd, a, (int)std::min<size_t>(cap_tasks, (size_t)kCfbSpan * nn),
-                                  c->api_lit_scratch.p, c->lit_locks.p));
-        if (std::getenv("PP_AMD_CF_VERBOSE")) cfb_status_hist(c, a, r);
-        PP_HIP(launch_cfb(st, sd, a, kCfbConsumeA, r));
+    int rounds = 0;
+    for (int m0 = 0; m0 <= misc[0]; ++rounds) {
+        a.span = rounds == 0 ? c->cfb_span0 : c->cfb_span;
+        const int mt = (int)std::min<size_t>(cap_tasks, (size_t)a.span * nn);
+        PP_HIP(launch_cfb(st, sd, a, kCfbEmitA, m0));
+        PP_HIP(launch_cfb_steer(st, sd, a, mt, false, wpts));
+        PP_HIP(launch_cfb_literal(st, sd, a, mt, c->cfb_lit.p, c->cfb_misc.p + 3, c->api_lit_scratch.p));
+        if (std::getenv("PP_AMD_CF_VERBOSE")) cfb_status_hist(c, a, rounds);
+        PP_HIP(launch_cfb(st, sd, a, kCfbConsumeA, m0));
+        m0 += a.span;
     }
     PP_HIP(launch_cfb(st, sd, a, kCfbEmitB, 0));
     PP_HIP(launch_cfb_steer(st, sd, a, (int)std::min<size_t>(cap_tasks, 2 * nn), true, wpts));
-    PP_HIP(launch_cfb_literal(st, sd, a, (int)std::min<size_t>(cap_tasks, 2 * nn),
-                              c->api_lit_scratch.p, c->lit_locks.p));
+    PP_HIP(launch_cfb_literal(st, sd, a, (int)std::min<size_t>(cap_tasks, 2 * nn), c->cfb_lit.p,
+                              c->cfb_misc.p + 3, c->api_lit_scratch.p));
     if (std::getenv("PP_AMD_CF_VERBOSE")) cfb_status_hist(c, a, 100);
     PP_HIP(launch_cfb(st, sd, a, kCfbStoreB, (int)std::min<size_t>(cap_tasks, 2 * nn)));
     PP_HIP(launch_cfb(st, sd, a, kCfbAssemble, 0, o.ok, o.len, o.npts, c->cf_err.p, c->cf_items.p,
@@ -1086,6 +1093,8 @@ int pp_create(int device, pp_ctx** out) {
     pp_ctx* c = new pp_ctx();
     c->device = device;
     if (const char* v = std::getenv("PP_AMD_CF_ROUNDS")) c->cf_rounds = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PP_AMD_CFB_SPAN0")) c->cfb_span0 = std::min(std::max(std::atoi(v), 1), 16);
+    if (const char* v = std::getenv("PP_AMD_CFB_SPAN")) c->cfb_span = std::min(std::max(std::atoi(v), 1), 16);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = c->d_state.reserve(1);
     if (e == hipSuccess) e = c->d_api_state.reserve(1);

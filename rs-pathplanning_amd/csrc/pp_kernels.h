@@ -102,9 +102,11 @@ struct CfBatch {
 // fills ftab for every node, phase B the goal edges (gotab) and copy edges (gtab), the assemble
 // kernel decides every item whose verdicts are all known and lists the others (plist, pcount)
 // for check_finish_kernel.  Node b < nitems is item b, b - nitems < Q query's root.
+constexpr int kCfbSpan = 2;  // phase A candidates per node and round (span A/B: DESIGN §3.3)
 struct CfbArgs {
     TreeDev tr{};
     int row_cap = 0;
+    int span = kCfbSpan;  // phase A candidates per node in the current round
     int nitems = 0, Q = 0;
     const int* qidx = nullptr;
     const int* nodes = nullptr;
@@ -131,7 +133,6 @@ struct CfbArgs {
     int* wsum = nullptr;      // (profiling) += every round's task count
 };
 enum : int { kCfbDepth = 0, kCfbEmitA, kCfbConsumeA, kCfbEmitB, kCfbStoreB, kCfbAssemble };
-constexpr int kCfbSpan = 4;  // phase A candidates per node and round
 hipError_t launch_cfb(hipStream_t s, const SceneDev& sc, CfbArgs a, int phase, int round,
                       int* ok = nullptr, double* len = nullptr, int* npts = nullptr,
                       int* err = nullptr, int* items = nullptr, int* plist = nullptr);
@@ -139,7 +140,7 @@ hipError_t launch_cfb_steer(hipStream_t s, const SceneDev& sc, const CfbArgs& a,
                             bool own_yaw, long long* wg_points = nullptr);
 // the rounds' literal-path tasks re-run by steer_collide_literal (a scratch slot per wave)
 hipError_t launch_cfb_literal(hipStream_t s, const SceneDev& sc, const CfbArgs& a, int max_tasks,
-                              double* lit_scratch, int* lit_locks);
+                              int* list, int* count, double* lit_scratch);
 hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const SceneDev* scg,
                                const TreeDev& tr,
                                const int* nodes, int k, double gx, double gy, double gyaw,

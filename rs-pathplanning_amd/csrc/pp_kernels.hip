@@ -3977,17 +3977,16 @@ __device__ inline int cfb_reserve(int* counter, int cnt, int* wsum) {
     return wb + incl - cnt;
 }
 
-// phase A round r: the next kCfbSpan candidates (depth 4r .. 4r + 3, root first) of every open
+// phase A round r: the next `span` candidates (depth m0 .. m0 + span - 1, root first) of every open
 // node, as explicit (child, parent pose) tasks: child = the node's position (compute_yaw toward
 // the candidate, as Node::new does), parent = the candidate's stored pose
-__global__ __launch_bounds__(256) void cfb_emit_a_kernel(CfbArgs a, int round) {
+__global__ __launch_bounds__(256) void cfb_emit_a_kernel(CfbArgs a, int m0, int span) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     int cnt = 0, q = 0, c = 0, d = 0;
-    const int m0 = round * kCfbSpan;
     if (b < a.nitems + a.Q && a.open[b]) {
         cfb_node(a, b, q, c);
         d = a.depth[b];
-        cnt = min(kCfbSpan, d + 1 - m0);
+        cnt = min(span, d + 1 - m0);
         if (cnt < 0) cnt = 0;
     }
     const int t0 = cfb_reserve(&a.st->W, cnt, a.wsum);
@@ -4021,7 +4020,7 @@ __global__ __launch_bounds__(256) void cfb_emit_a_kernel(CfbArgs a, int round) {
 // rejected — accepted: ftab = 2 + depth (| 1 << 30 for a None steer, finalize's panic); literal
 // path or error: left unknown for check_finish_kernel — or when its last candidate was rejected:
 // ftab = 1 (no candidate)
-__global__ __launch_bounds__(256) void cfb_consume_a_kernel(CfbArgs a, int round) {
+__global__ __launch_bounds__(256) void cfb_consume_a_kernel(CfbArgs a, int m0) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b == 0) a.st->W = 0;  // the next round's counter (every reader of W has finished)
     if (b >= a.nitems + a.Q) return;
@@ -4030,7 +4029,7 @@ __global__ __launch_bounds__(256) void cfb_consume_a_kernel(CfbArgs a, int round
     int q, c;
     cfb_node(a, b, q, c);
     const size_t o = (size_t)q * a.row_cap;
-    const int t0 = a.tfirst[b], m0 = round * kCfbSpan;
+    const int t0 = a.tfirst[b];
     for (int i = 0; i < cnt; ++i) {
         const int s = a.status[t0 + i];
         if (s == kReject) continue;
@@ -4171,37 +4170,39 @@ __global__ __launch_bounds__(256) void cfb_store_b_kernel(CfbArgs a) {
 // after a rounds walk: the literal-path tasks (the trim cases steer_walk hands back, e.g. the
 // zero-length copy edges at a root, whose points are all 0.0) re-run by steer_collide_literal,
 // as mq_insert does for the extend tasks, so their verdicts reach the memo instead of punting
-// every item whose chain holds them to check_finish_kernel
-__global__ __launch_bounds__(256) void cfb_literal_kernel(CfbArgs a, SceneDev sc,
-                                                          double* __restrict__ lit_scratch,
-                                                          int* __restrict__ lit_locks) {
-    const int W = a.st->W;
+// every item whose chain holds them to check_finish_kernel.  The list first, then one wave per
+// listed task (wave w owns scratch slot w: no locks), so the serial generations run side by side
+__global__ __launch_bounds__(256) void cfb_lit_list_kernel(CfbArgs a, int* __restrict__ list,
+                                                           int* __restrict__ count) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < a.st->W && a.status[t] == kLiteral) list[atomicAdd(count, 1)] = t;
+}
+
+__global__ __launch_bounds__(256) void cfb_lit_run_kernel(CfbArgs a, SceneDev sc,
+                                                          const int* __restrict__ list,
+                                                          const int* __restrict__ count,
+                                                          double* __restrict__ lit_scratch) {
     const int lane = threadIdx.x & 63;
     const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    for (int base = gw * 64; base < W; base += nw * 64) {
-        const int t = base + lane;
-        const int st = t < W ? a.status[t] : kReject;
-        uint64_t lit = __ballot(st == kLiteral);
-        if (!lit) continue;
-        const int slot = lit_acquire(lit_locks, gw);
-        double* bx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
-        for (; lit; lit &= lit - 1) {
-            const int tt = base + __builtin_ctzll(lit);
-            const SteerTask tk = a.tasks[tt];
-            const int r = steer_collide_literal(sc, tk.x, tk.y, a.yaw[tt], tk.px, tk.py, tk.pyaw,
-                                                bx, bx + kLiteralCap, bx + 2 * kLiteralCap);
-            if (lane == 0) a.status[tt] = r;
-        }
-        lit_release(lit_locks, slot);
+    double* bx = lit_scratch + (size_t)gw * 3 * kLiteralCap;
+    const int n = *count;
+    for (int i = gw; i < n; i += nw) {
+        const int t = list[i];
+        const SteerTask tk = a.tasks[t];
+        const int r = steer_collide_literal(sc, tk.x, tk.y, a.yaw[t], tk.px, tk.py, tk.pyaw, bx,
+                                            bx + kLiteralCap, bx + 2 * kLiteralCap);
+        if (lane == 0) a.status[t] = r;
     }
 }
 
 hipError_t launch_cfb_literal(hipStream_t s, const SceneDev& sc, const CfbArgs& a, int max_tasks,
-                              double* lit_scratch, int* lit_locks) {
+                              int* list, int* count, double* lit_scratch) {
     if (max_tasks <= 0) return hipSuccess;
-    const int g = std::min((max_tasks + 255) / 256, 1024);
-    cfb_literal_kernel<<<g, 256, 0, s>>>(a, sc, lit_scratch, lit_locks);
+    hipError_t e = hipMemsetAsync(count, 0, sizeof(int), s);
+    if (e != hipSuccess) return e;
+    cfb_lit_list_kernel<<<(max_tasks + 255) / 256, 256, 0, s>>>(a, list, count);
+    cfb_lit_run_kernel<<<kLiteralWaves / 4, 256, 0, s>>>(a, sc, list, count, lit_scratch);
     return hipGetLastError();
 }
 
@@ -4282,7 +4283,7 @@ hipError_t launch_cfb(hipStream_t s, const SceneDev& sc, CfbArgs a, int phase, i
             cfb_tnone_up_kernel<<<g, 256, 0, s>>>(a);
             break;
         case kCfbEmitA:
-            cfb_emit_a_kernel<<<g, 256, 0, s>>>(a, round);
+            cfb_emit_a_kernel<<<g, 256, 0, s>>>(a, round, a.span);  // round: the first depth m0
             break;
         case kCfbConsumeA:
             cfb_consume_a_kernel<<<g, 256, 0, s>>>(a, round);
