@@ -378,12 +378,16 @@ def walk_roofline(sp, pmc, name):
 
 
 def finish_roofline(sp):
-    """check_finish_kernel (goal connection): the optimize candidates' and finalize's edges
-    (steer + verify, the same per-point walk) against the FP64 peak."""
-    r = fp64_roofline("check_finish_kernel", sp.get("finish_ms", 0.0),
+    """check_finish (goal connection): the optimize candidates' and finalize's edges (steer +
+    verify, the same per-point walk) against the FP64 peak.  pp_batch_plan runs it as steer
+    rounds, pp_rrt_plan as check_finish_kernel; both end in cf_line_kernel."""
+    r = fp64_roofline("check_finish", sp.get("finish_ms", 0.0),
                       sp.get("finish_launches", 0), sp.get("finish_points", 0),
                       sp.get("finish_arc_points", 0), None,
-                      "HIP events around check_finish_kernel in a profiled run of the same plan")
+                      "HIP events around the whole check_finish (batch plan: the steer rounds, "
+                      "their literal re-runs, assemble, check_finish_kernel on punted items and "
+                      "cf_line_kernel; single plan: check_finish_kernel + cf_line_kernel) in a "
+                      "profiled run of the same plan")
     if r:
         r["nodes"] = int(sp.get("finish_nodes", 0))
         r["edges"] = int(sp.get("finish_edges", 0))

@@ -165,3 +165,35 @@ def test_batch_plan_rounds_equal_one_kernel(pkg, ctx, monkeypatch):
         assert np.array_equal(a[key], k[key]), key
     assert np.array_equal(a["length"], k["length"])
     assert int((a["best_node"] >= 0).sum()) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("span0,span", [("1", "1"), ("4", "4"), ("1", "3")])
+def test_batch_plan_span_schedules_agree(pkg, ctx, monkeypatch, span0, span):
+    """phase A's span schedule (PP_AMD_CFB_SPAN0 / PP_AMD_CFB_SPAN at context creation, DESIGN.md
+    §3.3) changes which candidates are walked together, never a result: the same best nodes,
+    lengths (bit for bit), point and finish counts as the default schedule on a 256-query
+    config-3 batch"""
+    from pathplanning_amd import rrt, scenes
+
+    raw = scenes.field512()
+    starts, goals, seeds = scenes.config3_queries(raw, 0, 256)
+    out = []
+    for sched in ((None, None), (span0, span)):
+        for name, v in zip(("PP_AMD_CFB_SPAN0", "PP_AMD_CFB_SPAN"), sched):
+            if v is None:
+                monkeypatch.delenv(name, raising=False)
+            else:
+                monkeypatch.setenv(name, v)
+        c = pkg.Context(0)
+        try:
+            b = rrt.RRTBatch(starts, goals, 2000, raw["step_size"], rrt.Space.from_raw(raw),
+                             seeds, ctx=c)
+            b.extend(2000)
+            out.append(b.plan())
+        finally:
+            c.close()
+    a, k = out
+    assert a["checked"] == k["checked"] > 0
+    for key in ("best_node", "n_points", "n_finishes", "length"):
+        assert np.array_equal(a[key], k[key]), key
