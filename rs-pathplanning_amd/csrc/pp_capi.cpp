@@ -514,6 +514,7 @@ int ensure_events(pp_ctx* c, size_t count) {
 static_assert(PP_CF_CHAIN == kCfLevels + 2, "chain row layout");
 constexpr int kCfBatch = 16384;     // nodes per check_finish launch
 constexpr int kCfPtsCap = 1 << 16;  // line points per check_finish workgroup
+static_assert(4 * kCfMaxEdges <= kCfPtsCap, "cf_line_kernel keeps 4 doubles per edge in the hypot buffer");
 constexpr int kCfLineGrid = 2048;   // the batch plan's cf_line_kernel workgroups (1.5 MB each)
 
 // check_finish for nodes[0, k) (device pointer already filled); results on the device

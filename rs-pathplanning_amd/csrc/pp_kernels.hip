@@ -3226,13 +3226,14 @@ __device__ __noinline__ long long cf_edge_check(const SceneDev* __restrict__ scg
 // edge calls
 __device__ __noinline__ double cf_atan2(double y, double x) { return atan2(y, x); }
 
-// n_point of dubins_path_planning(a → b) (dubins.rs:369), 0 when the steer is None
-__device__ inline int cf_npoint(const SceneDev& sc, CfPose a, CfPose b) {
+// n_point of dubins_path_planning(a → b) (dubins.rs:369), 0 when the steer is None; the chosen
+// word in st
+__device__ inline int cf_npoint_steer(const SceneDev& sc, CfPose a, CfPose b, Steer& st) {
     const double ex = b.x - a.x, ey = b.y - a.y;
     const double c = 1.0 / sc.turn_radius;
     const double lex = cos(a.yaw) * ex + sin(a.yaw) * ey;
     const double ley = -(sin(a.yaw)) * ex + cos(a.yaw) * ey;
-    const Steer st = select_word(lex, ley, b.yaw - a.yaw, c);
+    st = select_word(lex, ley, b.yaw - a.yaw, c);
     if (st.word < 0) return 0;
     double tot = 0.0;
     tot += st.t;
@@ -3241,6 +3242,10 @@ __device__ inline int cf_npoint(const SceneDev& sc, CfPose a, CfPose b) {
     const double nq = trunc(tot / sc.step_size);
     if (!(nq >= 0.0) || nq > 1.0e8) return -1;
     return (int)nq + 7;
+}
+__device__ inline int cf_npoint(const SceneDev& sc, CfPose a, CfPose b) {
+    Steer st;
+    return cf_npoint_steer(sc, a, b, st);
 }
 
 __device__ __noinline__ int cf_npoint_ool(const SceneDev* __restrict__ scg, CfPose a, CfPose b) {
@@ -3557,6 +3562,17 @@ __global__ __launch_bounds__(kCfThreads, kCfMinW) void check_finish_kernel(
     }
 }
 
+// cf_line_kernel's workgroup: one wave per line item.  An item's path walk and its ordered length
+// sum are serial, so a 4-wave workgroup left 3 waves waiting at its barriers; one wave per item
+// puts 4x the items in flight at the same occupancy
+constexpr int kCfLineThreads = 64;
+static_assert(kCfLineThreads == 64, "cf_line_kernel: one wave per item (its edge table and sums are wave-wide)");
+#ifdef PP_LINE_TIMING  // diagnostic builds only: phase stamps of cf_line_kernel's items
+#define LT(k) const unsigned long long lt##k = wall_clock64();
+#else
+#define LT(k)
+#endif
+
 // dubins_literal<false, false> (dubins.rs:326-428) of one edge by one wave: the WORLD points of
 // the trimmed course into px / py (cap >= n_point), *n_out = their count.  generate_local_course
 // (dubins.rs:200-272) writes the origin at index 0, each segment's grid points from the slot of
@@ -3568,15 +3584,16 @@ __global__ __launch_bounds__(kCfThreads, kCfMinW) void check_finish_kernel(
 // indices below the last one whose local x is nonzero (none: 0), or all n_point when the last
 // slot is written and nonzero.  Returns kSteerSome / kSteerNone / kSteerOverflow like the
 // literal restatement.
-__device__ int line_edge_wave(double sx, double sy, double syaw, double ex0, double ey0,
-                              double eyaw, double turn_radius, double step_size, double* px,
-                              double* py, int cap, int lane, int* n_out) {
-    const double ex = ex0 - sx, ey = ey0 - sy;
+__device__ int line_edge_wave(double sx, double sy, double syaw, const double* __restrict__ word,
+                              double turn_radius, double step_size, double* px, double* py,
+                              int cap, int lane, int* n_out) {
+    // the word (dubins.rs:333-363) as cf_npoint_steer chose it for this edge: {word, t, p, q}
     const double c = 1.0 / turn_radius;
-    const double lex = cos(syaw) * ex + sin(syaw) * ey;
-    const double ley = -(sin(syaw)) * ex + cos(syaw) * ey;
-    const double leyaw = eyaw - syaw;
-    const Steer s = select_word(lex, ley, leyaw, c);
+    Steer s;
+    s.word = (int)word[0];
+    s.t = word[1];
+    s.p = word[2];
+    s.q = word[3];
     if (s.word < 0) return kSteerNone;
     const double lengths[3] = {s.t, s.p, s.q};
     double total = 0.0;
@@ -3669,7 +3686,7 @@ __device__ int line_edge_wave(double sx, double sy, double syaw, double ex0, dou
 // edge's literal Dubins points (line_edge_wave, a wave per edge) into the workgroup's pts / etab,
 // then l.reverse() and geo's euclidean_length in that order (rrt.rs:538: the hypots in parallel,
 // their sum in line order).
-__global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
+__global__ __launch_bounds__(kCfLineThreads) void cf_line_kernel(
     SceneDev sc, TreeDev tr_in, const int* __restrict__ nodes, double gx_in, double gy_in,
     double gyaw_in, double gyaw_opt_in, int* __restrict__ ok_out, double* __restrict__ len_out,
     int* __restrict__ npts_out, double* __restrict__ pts, int pts_cap, int* __restrict__ etab,
@@ -3686,6 +3703,7 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
     for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
         const int* o = items + 1 + (size_t)it * kCfItem;
         const int b = o[0], s = o[1], vok = o[2];
+        LT(0)
         if (tid < kCfLevels) s_pos[tid] = o[4 + tid];
         const int* pos = s_pos;
         TreeDev tr;
@@ -3698,6 +3716,7 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
         if (tid == 0) s_off = D;
         __syncthreads();
         D = s_off;
+        LT(1)
         const double gyaw_e = s > 0 ? gyaw_opt : gyaw;
         const int ps = s > 0 ? pos[s - 1] : D - 1;
         const int E = 1 + s + ps;
@@ -3714,7 +3733,17 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
             return CfPose{tr.x[node], tr.y[node], tr.yaw[node]};
         };
         if (tid == 0) s_bad = 0;
-        for (int e = tid; e < E; e += kCfThreads) et[2 * e] = cf_npoint(sc, pose(e), pose(e + 1));
+        // every edge's word and point count, a lane per edge; the words wait in the hypot buffer
+        // (4 doubles an edge, 4 kCfMaxEdges <= pts_cap) for the generation below
+        for (int e = tid; e < E; e += kCfLineThreads) {
+            Steer w;
+            et[2 * e] = cf_npoint_steer(sc, pose(e), pose(e + 1), w);
+            double* wd = pyw + 4 * (size_t)e;
+            wd[0] = (double)w.word;
+            wd[1] = w.t;
+            wd[2] = w.p;
+            wd[3] = w.q;
+        }
         __syncthreads();
         if (tid == 0) {  // edge capacities -> offsets
             int off = 0;
@@ -3732,16 +3761,17 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
         }
         __syncthreads();
         const int total = s_off;
+        LT(2)
         if (total < 0) {
             if (tid == 0) s_bad = total == -2 ? 2 : 8;
         } else {
             const int lane = tid & 63;
-            for (int e = tid >> 6; e < E; e += kCfThreads / 64) {
+            for (int e = tid >> 6; e < E; e += kCfLineThreads / 64) {
                 const int off = et[2 * e];
                 const int cap = (e + 1 < E ? et[2 * e + 2] : total) - off;
-                const CfPose a = pose(e), bp = pose(e + 1);
+                const CfPose a = pose(e);
                 int n = 0;
-                const int r = line_edge_wave(a.x, a.y, a.yaw, bp.x, bp.y, bp.yaw, sc.turn_radius,
+                const int r = line_edge_wave(a.x, a.y, a.yaw, pyw + 4 * (size_t)e, sc.turn_radius,
                                              sc.step_size, px + off, py + off, cap, lane, &n);
                 if (lane == 0) {
                     et[2 * e + 1] = r == kSteerSome ? n : 0;
@@ -3756,11 +3786,37 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
         // yaw buffer, by forward index), then one lane adds them in the reversed order — the
         // same operands, the same order of the sum
         const int bad0 = s_bad;
-        if (bad0 == 0) {
+        LT(3)
+        int npts_all = 0;
+        if (bad0 == 0 && E <= 64) {
+            // (one wave, at most 64 edges: the edge table in registers — lane e holds edge e's
+            // offset, count, compact base and the offset of the next edge with points — so the
+            // loop over the edges waits on no table load)
+            const int eoff = tid < E ? et[2 * tid] : 0, en = tid < E ? et[2 * tid + 1] : 0;
+            const uint64_t ne = __ballot(en > 0);
+            const uint64_t above = tid >= 63 ? 0ull : (ne & (~0ull << (tid + 1)));
+            const int nxl = above ? (int)__builtin_ctzll(above) : 0;
+            const int nxo = __shfl(eoff, nxl);
+            const int nx = above ? nxo : -1;
+            const int incl = wave_incl_scan(en);
+            const int cbv = incl - en;
+            npts_all = __builtin_amdgcn_readlane(incl, 63);
+            for (int e = 0; e < E; ++e) {
+                const int off = __builtin_amdgcn_readlane(eoff, e);
+                const int n = __builtin_amdgcn_readlane(en, e);
+                const int cb = __builtin_amdgcn_readlane(cbv, e);
+                const int nxe = __builtin_amdgcn_readlane(nx, e);
+                for (int i = tid; i < n; i += kCfLineThreads) {
+                    const int noff = i + 1 < n ? off + i + 1 : nxe;
+                    if (noff >= 0)
+                        pyw[cb + i] = hypot(px[off + i] - px[noff], py[off + i] - py[noff]);
+                }
+            }
+        } else if (bad0 == 0) {
             int cb = 0;
             for (int e = 0; e < E; ++e) {
                 const int off = et[2 * e], n = et[2 * e + 1];
-                for (int i = tid; i < n; i += kCfThreads) {
+                for (int i = tid; i < n; i += kCfLineThreads) {
                     int noff = -1;
                     if (i + 1 < n) {
                         noff = off + i + 1;
@@ -3776,8 +3832,10 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
                 }
                 cb += n;
             }
+            npts_all = cb;
         }
         __syncthreads();
+        LT(4)
         if (tid < 64) {
             // the reversed sum, wave 0: 64 hypots a load (lane j holds pyw[hi - j], the next
             // chunk's load in flight), added in lane order by readlane — the serial order
@@ -3785,14 +3843,18 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
             int npts = 0;
             const int bad = s_bad;
             if (bad == 0) {
-                for (int e = 0; e < E; ++e) npts += et[2 * e + 1];
+                npts = npts_all;
                 int hi = npts - 2;
                 double v = hi - tid >= 0 ? pyw[hi - tid] : 0.0;
                 for (; hi >= 0; hi -= 64) {
                     const double cur = v;
                     v = hi - 64 - tid >= 0 ? pyw[hi - 64 - tid] : 0.0;
-                    const int m = hi < 63 ? hi + 1 : 64;
-                    for (int j = 0; j < m; ++j) len += readlane_f64(cur, j);
+                    if (hi >= 63) {  // a full chunk: constant lane indices
+#pragma unroll
+                        for (int j = 0; j < 64; ++j) len += readlane_f64(cur, j);
+                    } else {
+                        for (int j = 0; j <= hi; ++j) len += readlane_f64(cur, j);
+                    }
                 }
             }
             if (tid == 0) {
@@ -3803,6 +3865,14 @@ __global__ __launch_bounds__(kCfThreads) void cf_line_kernel(
             }
         }
         __syncthreads();  // the buffers and s_off serve the next item
+#ifdef PP_LINE_TIMING
+        {
+            LT(5)
+            if (tid == 0 && it % 97 == 0)
+                printf("LT it %d D %d E %d path %llu cnt %llu gen %llu hyp %llu sum %llu\n", it, D, E,
+                       lt1 - lt0, lt2 - lt1, lt3 - lt2, lt4 - lt3, lt5 - lt4);
+        }
+#endif
     }
 }
 
@@ -3822,7 +3892,7 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const SceneDe
                                                         chain, lit_scratch, lit_locks, err, tally,
                                                         cb, gpath, items, blist);
     if (want_line && mode != kCfOptimize)
-        cf_line_kernel<<<line_grid > 0 ? line_grid : std::min(grid, k), kCfThreads, 0, st>>>(
+        cf_line_kernel<<<line_grid > 0 ? line_grid : std::min(grid, k), kCfLineThreads, 0, st>>>(
             sc, tr, nodes, gx, gy, gyaw, gyaw_opt, ok, len, npts, pts, pts_cap, etab, err, cb,
             gpath, items);
     return hipGetLastError();
