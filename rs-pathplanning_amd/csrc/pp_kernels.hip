@@ -3604,7 +3604,26 @@ __device__ int line_edge_wave(double sx, double sy, double syaw, const double* _
     if (!(nq >= 0.0) || nq > 1.0e8) return kSteerOverflow;
     const int n_point = (int)nq + 3 + 4;
     if (n_point > cap) return kSteerOverflow;
-    const double cs = cos(-syaw), sn = sin(-syaw);
+    // every sin / cos the edge needs in one lane-parallel round (the same calls on the same
+    // arguments as interp_local and the world transform make, so the same values): lanes 0..2 the
+    // segment origins' yaw trig (S: cos / sin of the yaw; L, R: of minus the yaw), 3..5 sin / cos
+    // of the segment lengths (their end points), 6 the world transform's cos / sin(-syaw)
+    const int m0 = word_mode(s.word, 0), m1 = word_mode(s.word, 1), m2 = word_mode(s.word, 2);
+    const double oy0 = 0.0;  // interpolate's yaw chain, dubins.rs:191-196
+    const double oy1 = m0 == kModeL ? oy0 + s.t : (m0 == kModeR ? oy0 - s.t : oy0);
+    const double oy2 = m1 == kModeL ? oy1 + s.p : (m1 == kModeR ? oy1 - s.p : oy1);
+    double arg = 0.0;
+    if (lane < 3) {
+        const int ms = lane == 0 ? m0 : (lane == 1 ? m1 : m2);
+        const double oys = lane == 0 ? oy0 : (lane == 1 ? oy1 : oy2);
+        arg = ms == kModeS ? oys : -oys;
+    } else if (lane < 6) {
+        arg = lane == 3 ? s.t : (lane == 4 ? s.p : s.q);
+    } else if (lane == 6) {
+        arg = -syaw;
+    }
+    const double sv = sin(arg), cv = cos(arg);
+    const double cs = readlane_f64(cv, 6), sn = readlane_f64(sv, 6);
     if (lane == 0) {  // the origin, index 0
         px[0] = cs * 0.0 + sn * 0.0 + sx;
         py[0] = -sn * 0.0 + cs * 0.0 + sy;
@@ -3619,8 +3638,9 @@ __device__ int line_edge_wave(double sx, double sy, double syaw, const double* _
         const double l = lengths[i];
         const double d = (l > 0.0) ? step_size : -step_size;
         // interp_local's trig of the segment's origin yaw (per point in the serial form, the same
-        // values)
-        const double co = cos(o.yaw), so = sin(o.yaw), cmo = cos(-o.yaw), smo = sin(-o.yaw);
+        // values): S cos / sin(yaw), L / R cos / sin(-yaw)
+        const double ca = readlane_f64(cv, i), sa = readlane_f64(sv, i);
+        const double co = ca, so = sa, cmo = ca, smo = sa;
         const double al = fabs(l);
         double pd = (i >= 1 && (lengths[i - 1] * lengths[i]) > 0.0) ? (-d - ll) : (d - ll);
         int base = i == 0 ? 1 : ind;  // the slot of this segment's first grid point
@@ -3665,7 +3685,19 @@ __device__ int line_edge_wave(double sx, double sy, double syaw, const double* _
         // the segment's end (dubins.rs:262-267) at the next slot; the next segment starts there
         ind += 1;
         if (ind >= n_point) return kSteerOverflow;
-        const Pose r = interp_local(m, l, c, o);
+        // interp_local(m, l, c, o) with the round's values
+        Pose r;
+        if (m == kModeS) {
+            r.x = o.x + l / c * co;
+            r.y = o.y + l / c * so;
+        } else {
+            const double sl = readlane_f64(sv, 3 + i), cl = readlane_f64(cv, 3 + i);
+            const double ldx = sl / c;
+            const double ldy = m == kModeL ? (1.0 - cl) / c : (1.0 - cl) / -c;
+            r.x = o.x + (cmo * ldx + smo * ldy);
+            r.y = o.y + (-smo * ldx + cmo * ldy);
+        }
+        r.yaw = 0.0;  // (the next segment's trig comes from the round)
         if (i == 2) {
             if (lane == 0) {
                 px[ind] = cs * r.x + sn * r.y + sx;
