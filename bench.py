@@ -23,8 +23,10 @@ Sub-results on the same line (the rows of SURVEY.md §8d the driver would not se
                    Robot::new(1.8, 3.0, 0.8), 8000 iterations) (N = 1 only)
 
 `python bench.py --gpus N` without WORLD_SIZE starts N rank processes itself (before anything
-touches the GPU); under torchrun it is one of them.  Prints ONE JSON line (rank 0).  See DESIGN.md
-§5 for the roofline accounting.
+touches the GPU); under torchrun it is one of them.  Rank 0 writes the full record to --detail
+(gpurun_out/bench_detail.json) and prints ONE compact JSON line of at most LINE_MAX bytes (the
+headline keys, the dominant kernel's roofline, the CPU baseline, one short record per sub-result).
+See DESIGN.md §5 for the roofline accounting.
 """
 from __future__ import annotations
 
@@ -87,9 +89,6 @@ def parse(argv=None):
                     help="config3: iterations per query evaluated speculatively per GPU step "
                          "(power of two <= 64; 0 = automatic)")
     ap.add_argument("--max-iter", type=int, default=2000, help="config3/5: RRT.max_iter per query")
-    ap.add_argument("--schedule", choices=("persistent", "lockstep"), default="lockstep",
-                    help="config3: four launches per lockstep step (default) or one persistent "
-                         "launch per extend call (pp_batch_set_schedule; identical trees)")
     ap.add_argument("--window", type=int, default=4096)
     ap.add_argument("--nodes", type=int, default=100_000, help="tree size before timing")
     ap.add_argument("--seed", type=int, default=42)
@@ -101,6 +100,8 @@ def parse(argv=None):
     ap.add_argument("--pmc-run", action="store_true",
                     help="config3: no profiled plan pass (counter runs: the last walk dispatches "
                          "are then the profiled extend's)")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="where the full record goes (stdout gets the compact line)")
     ap.add_argument("--allow-variant-lib", action="store_true",
                     help="accept PP_AMD_LIB pointing at another build (experiments only)")
     return ap.parse_args(argv)
@@ -573,7 +574,7 @@ def run_batch(args, D, star, with_cpu):
             return rrt.RRTStarBatch(starts, args.max_iter, raw["step_size"], space, seeds, k=0,
                                     eta=eta, device=D.device)
         return rrt.RRTBatch(starts, goals, args.max_iter, raw["step_size"], space, seeds,
-                            device=D.device, window=args.batch_window, schedule=args.schedule)
+                            device=D.device, window=args.batch_window)
 
     batch = fresh()
     batch.extend(args.warmup)  # untimed warmup on a throwaway run
@@ -628,13 +629,8 @@ def run_batch(args, D, star, with_cpu):
         extra["rewires_total"] = int(D.allreduce(float(stt[3].sum()), "sum"))
     else:
         ideal = -(-steps // (args.batch_window or auto_batch_window(b - a)))
-        if args.schedule == "persistent":
-            extra["passes"] = {"window_steps_per_query": round(
-                                   st_timed["batch_query_steps"] / max(b - a, 1), 2),
-                               "ideal_steps": ideal, "launches": int(st_timed["batch_passes"])}
-        else:
-            extra["passes"] = {"steps": int(st_timed["batch_steps"]),
-                               "host_passes": int(st_timed["batch_passes"]), "ideal_steps": ideal}
+        extra["passes"] = {"steps": int(st_timed["batch_steps"]),
+                           "host_passes": int(st_timed["batch_passes"]), "ideal_steps": ideal}
     # profiled pass (same workload, same streams): HIP events around every kernel of every step
     batch.close()
     batch = fresh()
@@ -650,13 +646,8 @@ def run_batch(args, D, star, with_cpu):
     # the counter passes were taken on the whole 8192-query batch on one GPU
     pmc = load_profile("batch_pmc.json").get(wl, {}) if args.queries == 8192 and D.world == 1 else {}
     evals_total = float(evals_p.sum())
-    persistent = not star and args.schedule == "persistent"
-    if persistent:
-        roof, nn_roof, phases = persist_rooflines(sp, evals_total, pmc.get("persist", {}))
-    else:
-        roof = walk_roofline(sp, pmc.get("steer_walk", {}), wl)
-        nn_roof = lockstep_nn_roofline(sp, evals_total, star, pmc)
-        phases = None
+    roof = walk_roofline(sp, pmc.get("steer_walk", {}), wl)
+    nn_roof = lockstep_nn_roofline(sp, evals_total, star, pmc)
     res = {
         "value": round(iters_total / t_max, 1),
         "unit": "iterations/s",
@@ -676,14 +667,7 @@ def run_batch(args, D, star, with_cpu):
         "nn_roofline": nn_roof,
         **extra,
     }
-    if persistent:
-        res["schedule"] = "persistent (one launch: every workgroup steps its own queries)"
-        res["phase_share"] = phases
-        res["window_slots"] = {"evaluated": int(sp.get("samples_evaluated", 0)),
-                               "sample_in_obstacle": int(sp.get("samples_blocked", 0)),
-                               "note": "slots whose sample lies in an obstacle are rejected "
-                                       "whatever the parent: no steer_prep / steer_walk, no cut"}
-    elif not star:
+    if not star:
         launches = max(sp["nn_scan_launches"], 1)
         res["schedule"] = "lockstep (four launches per step, two sub-batch streams)"
         res["step_chain_us"] = {"mq_sample_nn": round(1e3 * sp["nn_scan_ms"] / launches, 2),
@@ -712,45 +696,6 @@ def run_batch(args, D, star, with_cpu):
                 raw, starts, goals, seeds, args.max_iter, args.cpu_seconds,
                 allrec[:, 5], allrec[:, 7].view(np.float64))
     return res
-
-
-PHASES = ("serial", "steer_prep", "steer_walk", "idle", "unused")
-
-
-def persist_rooflines(sp, evals_total, pmc):
-    """The persistent batch kernel (one launch per extend call): its walked points' algorithmic
-    FP64 FLOP against the whole launch (HIP events) and against its walk items alone (their share
-    of the waves' time), and the serial phases' f64 row reads (insert + samples + nearest node:
-    an upper bound of the NN's own time)."""
-    cyc = sp.get("persist_cycles") or [0] * 5
-    tot = float(sum(cyc)) or 1.0
-    share = {p: round(c / tot, 4) for p, c in zip(PHASES, cyc) if p != "unused"}
-    r = fp64_roofline("mq_persist_kernel (whole launch: samples + NN, steer_prep, steer_walk, "
-                      "insert)", sp.get("persist_ms", 0.0), sp.get("persist_launches", 0),
-                      sp.get("walk_points", 0), sp.get("walk_arc_points", 0), pmc,
-                      "HIP events around the persistent launch of the profiled pass")
-    if r:
-        wshare = share["steer_walk"] or 1.0
-        r["walk_phase"] = {"share_of_wave_time": wshare,
-                           "achieved": round(r["achieved"] / wshare, 4),
-                           "frac": round(r["frac"] / wshare, 5),
-                           "note": "the same FLOP over the launch time x the walk items' share "
-                                   "of the waves' time"}
-    nn = None
-    launches = max(sp.get("persist_launches", 0), 1)
-    ms = sp.get("persist_ms", 0.0) / launches * share["serial"]
-    if ms > 0:
-        bpe = 16  # f64 x + f64 y of one SoA row (exact NN)
-        ach = evals_total / launches * bpe / (ms * 1e-3) / 1e9
-        nn = {"kernel": "mq_persist_kernel serial items: insert + samples + exact f64 NN",
-              "bound": "hbm",
-              "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-              "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-              "phase_ms_per_launch": round(ms, 5), "bytes_per_eval": bpe,
-              "evals_per_launch": int(evals_total / launches),
-              "note": "time = launch time x the serial items' share of the waves' time (an upper "
-                      "bound of the NN's own time, so frac is a lower bound)"}
-    return r, nn, share
 
 
 def lockstep_nn_roofline(sp, evals_total, star, pmc):
@@ -1033,6 +978,134 @@ def line_json(line):
     return s
 
 
+# The driver reads the LAST stdout line out of an ~8 KB tail that also holds stderr: rounds 3-4's
+# 22-23 KB lines were never parsed.  The full record goes to a side file (--detail) and stdout gets
+# a compact line of at most LINE_MAX bytes.
+LINE_MAX = 4096
+SUB_KEYS = ("config3", "config5", "config4", "polygons", "config1", "config1_polygons", "plan",
+            "example_rrt")
+SHORT_WL = {"config3": "8192 queries, field512, max_iter 2000, sharded (strong)",
+            "config5": "RRT* 8192 queries, 10240 discs, max_iter 2000 (stretch)",
+            "config4": "config2 on a 512x512 occupancy bitmap, 100k nodes",
+            "polygons": "config2 with create_circle polygons, 100k nodes",
+            "config1": "bench6 (benches/all.rs), 8000 iterations, discs",
+            "config1_polygons": "bench6, 8000 iterations, create_circle polygons",
+            "plan": "RRT::plan on bench6_open, 8000 iterations",
+            "example_rrt": "examples/rrt RRT::plan (transit.debug.json), 8000 iterations"}
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def _short_roofline(r):
+    out = _pick(r or {}, ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic",
+                          "avg_launch_ms"))
+    if isinstance(out.get("kernel"), str):
+        out["kernel"] = out["kernel"].split(" (NN screen")[0][:40]
+    return out or None
+
+
+def _short_cpu(c, sample_len=120):
+    if not isinstance(c, dict):
+        return None
+    out = _pick(c, ("value", "unit", "cores", "kind", "same_answer"))
+    if isinstance(c.get("sample"), str):
+        out["sample"] = c["sample"][:sample_len]
+    return out
+
+
+def _short_sub(name, r):
+    if not isinstance(r, dict):
+        return None
+    if "error" in r:
+        return {"error": str(r["error"])[:200]}
+    roof = r.get("roofline") or {}
+    s = {"value": r.get("value"), "unit": r.get("unit"), "workload": SHORT_WL.get(name, name),
+         "frac": roof.get("frac"), "kernel": (roof.get("kernel") or "").split(" (")[0][:28] or None}
+    cpu = r.get("cpu_baseline")
+    if isinstance(cpu, dict):
+        s["cpu"] = cpu.get("value")
+        s["cpu_cores"] = cpu.get("cores")
+        if "same_answer" in cpu:
+            s["same_answer"] = cpu["same_answer"]
+    for k in ("records_digest", "best_length", "check_finish_ms", "n_gpus"):
+        if k in r:
+            s[k] = r[k]
+    if isinstance(r.get("plan"), dict):  # config 3's batch RRT::plan
+        pl = r["plan"]
+        s["plan"] = {"value": pl.get("value"), "check_finish_ms": pl.get("check_finish_ms"),
+                     "cpu_same_answer": (pl.get("cpu_baseline") or {}).get("same_answer")}
+    if isinstance(r.get("passes"), dict):
+        s["steps"] = r["passes"].get("steps")
+    return s
+
+
+def compact_line(line, detail_path=None, with_subs=True):
+    """The stdout line: the contract's headline keys, the dominant kernel's roofline, the CPU
+    baseline and one short record per sub-result (value, roofline frac, CPU value, same answer /
+    records digest); the rest of `line` is in the detail file.  Strict JSON, <= LINE_MAX bytes."""
+    head = _pick(line, ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                        "higher_is_better", "scaling", "vs_baseline", "dtype", "data"))
+    cfg = dict(line.get("config") or {})
+    if isinstance(cfg.get("workload"), str):
+        cfg["workload"] = cfg["workload"][:160]
+    cfg.pop("nn_screen_dtype", None)
+    head["config"] = cfg
+    head["roofline"] = _short_roofline(line.get("roofline"))
+    head["cpu_baseline"] = _short_cpu(line.get("cpu_baseline"))
+    for k in ("node_evals_per_s_per_gpu", "records_digest", "iterations_total", "nodes_total",
+              "rewires_total", "window_per_query", "passes", "best_length", "check_finish_ms",
+              "same_answer"):
+        if k in line:
+            head[k] = line[k]
+    if not with_subs and "records_digest" in line and isinstance(line.get("plan"), dict):
+        pl = line["plan"]  # a config-3 line's batch RRT::plan
+        head["plan"] = {"value": pl.get("value"), "check_finish_ms": pl.get("check_finish_ms"),
+                        "frac": (pl.get("roofline") or {}).get("frac"),
+                        "cpu_same_answer": (pl.get("cpu_baseline") or {}).get("same_answer")}
+    st = line.get("stats")
+    if isinstance(st, dict) and st.get("iterations"):
+        head["samples_blocked_frac"] = round(st.get("samples_blocked", 0) / st["iterations"], 4)
+    wc = line.get("window_chain_us")
+    if isinstance(wc, dict):
+        head["window_chain_us"] = {k: v for k, v in wc.items() if k != "windows"}
+    subs = {k: _short_sub(k, line[k]) for k in SUB_KEYS if with_subs and k in line}
+    if subs:
+        head["sub"] = subs
+    if isinstance(line.get("strong_scaling"), dict):
+        head["strong_scaling"] = _pick(line["strong_scaling"], ("workload", "value", "n_gpus",
+                                                                 "records_digest"))
+    prov = line.get("provenance") or {}
+    head["lib_sha256_16"] = prov.get("lib_sha256_16")
+    if detail_path:
+        head["detail"] = os.path.relpath(detail_path, ROOT)
+    s = line_json(head)
+    # over the cap (long error texts, many sub-results): shed the least important fields first
+    for drop in (("sub", "workload"), ("cpu_baseline", "sample"), ("sub", "kernel"),
+                 ("config", "workload")):
+        if len(s.encode()) <= LINE_MAX:
+            break
+        if drop[0] == "sub":
+            for v in head.get("sub", {}).values():
+                if isinstance(v, dict):
+                    v.pop(drop[1], None)
+        elif isinstance(head.get(drop[0]), dict):
+            head[drop[0]].pop(drop[1], None)
+        s = line_json(head)
+    if len(s.encode()) > LINE_MAX:
+        head.pop("sub", None)
+        head["sub_dropped"] = "over the line cap: see the detail file"
+        s = line_json(head)
+    return s
+
+
+def write_detail(path, s):
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "w") as f:
+        f.write(s + "\n")
+
+
 def tree_line(args, D, workload, raw, res):
     wl = {"config4": "config4: field512 rasterised to a 512x512 bit-packed occupancy grid "
                      "(32 KB, point probes)",
@@ -1160,9 +1233,10 @@ def main():
                                   "unit": "iterations/s", "n_gpus": D.world,
                                   "scaling": "strong",
                                   "records_digest": line["config3"].get("records_digest")}
-    s = line_json(line)
     if D.rank == 0:
-        print(s, flush=True)
+        detail = os.path.abspath(args.detail)
+        write_detail(detail, line_json(line))
+        print(compact_line(line, detail, wl == "default"), flush=True)
     D.close()
     return 0
 

@@ -26,8 +26,12 @@ extern "C" {
 
 /* 2: pp_stats lost the diagnostic stamps and gained the batch / check_finish counters;
  *    pp_rrt_get_stats takes the caller's sizeof(pp_stats); pp_batch_plan added
- * 3: pp_batch_set_schedule (the persistent batch kernel); pp_stats appended its counters */
-#define PP_ABI_VERSION 3
+ * 3: pp_batch_set_schedule, the persistent batch kernel; pp_stats appended its counters
+ * 4: the persistent batch kernel and pp_batch_set_schedule removed (slower than the lockstep
+ *    schedule on every workload measured: DESIGN.md §3.4); its pp_stats counters are reserved
+ *    (always 0, the layout kept); pp_batch_set_finish_schedule replaces the library's former
+ *    environment knobs */
+#define PP_ABI_VERSION 4
 
 #define PP_OK 0
 #define PP_ERR_INVALID_ARGUMENT (-1)
@@ -66,7 +70,8 @@ typedef struct pp_stats {
     int64_t repairs;          /* candidates re-steered in those rounds */
     int64_t literal_repairs;  /* candidates re-run on the literal single-lane path */
     int64_t nn_flagged;       /* samples whose f32 NN screen needed the exact f64 rescan */
-    int64_t node_evals;       /* sample-node distance evaluations of the NN screen */
+    int64_t node_evals;       /* sample-node distance evaluations of the NN screen: screened
+                                 samples (not in an obstacle) x the tree nodes the screen scanned */
     /* HIP events around every kernel of a window / batch step (profiling on), summed over the
      * launches; the batches keep their timed schedule (sub-batch streams) while profiled */
     double nn_scan_ms;        /* window_kernel (the NN screen + the previous window's resolve), or
@@ -87,15 +92,9 @@ typedef struct pp_stats {
     int64_t finish_edges;     /* Dubins edges steered + verified by check_finish (profiling on) */
     int64_t finish_points;    /* polyline points those edges walked (profiling on) */
     int64_t finish_arc_points;  /* ... of them on L / R segments */
-    /* ABI 3: the persistent query-batch kernel (pp_batch_set_schedule) */
-    int64_t batch_query_steps;  /* query batches: window steps summed over the queries */
-    double persist_ms;          /* HIP events around the persistent batch kernel (profiling on) */
-    int64_t persist_launches;
-    int64_t persist_cycles[5];  /* its waves' time (wall_clock64 ticks, 100 MHz, summed over the
-                                   waves; profiling on): serial items (insert, next query, samples
-                                   + nearest nodes), steer_prep passes, steer_walk tasks, idle, 0 */
-    int64_t samples_evaluated;  /* extend samples evaluated (one tree: the iterations; the persistent
-                                   batch: its window slots) */
+    /* ABI 3's persistent query-batch counters, removed in ABI 4: always 0 (layout kept) */
+    int64_t reserved_abi3[8];
+    int64_t samples_evaluated;  /* extend samples evaluated (one tree: the iterations) */
     int64_t samples_blocked;    /* ... of them whose point lies in an obstacle: rejected whatever
                                    the parent, without steer_prep / steer_walk or a pair list */
 } pp_stats;
@@ -257,15 +256,11 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
  * 2048 queries, else 16 while the step holds at most 131072 tasks).  Results do not depend on it: every query's tree equals its one-at-a-time
  * sequential run.  Applies to the current batch and the next ones. */
 int pp_batch_set_window(pp_ctx* ctx, int k);
-/* How pp_batch_extend runs a batch (results are identical):
- *   PP_BATCH_LOCKSTEP (default)    four launches per step over the whole batch (two sub-batch
- *                                  streams), the host topping up queries whose windows stopped;
- *   PP_BATCH_PERSISTENT            one launch per call: every workgroup takes queries from a
- *                                  counter and steps their windows itself (samples + nearest node,
- *                                  steer, collide, insert) until each reaches its target. */
-#define PP_BATCH_PERSISTENT 0
-#define PP_BATCH_LOCKSTEP 1
-int pp_batch_set_schedule(pp_ctx* ctx, int schedule);
+/* How pp_batch_plan runs check_finish (results are identical; for A/B measurement and tests):
+ * rounds = 1 (default) in steer rounds, phase A taking span0 candidate edges per
+ * node in its first round and span in the later ones (0 = the default, else 1..16); rounds = 0:
+ * check_finish_kernel alone, one wave per (query, node).  Applies to the context's later plans. */
+int pp_batch_set_finish_schedule(pp_ctx* ctx, int rounds, int span0, int span);
 /* n_steps lockstep steps: every query runs one plan_one extend iteration (rrt.rs:583-589) per
  * step until it reaches max_iter.  Totals over the batch are returned (may be NULL).  On the
  * GPU a step evaluates up to the batch window's iterations per query at once. */

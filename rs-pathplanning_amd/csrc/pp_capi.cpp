@@ -199,10 +199,7 @@ struct pp_ctx {
     DBuf<PrepRec> mq_rec;
     DBuf<DevState> mq_state;      // [3]: the whole batch, then one per sub-batch (mq_sub_args)
     hipStream_t sub_stream[4] = {};  // sub-batch streams 1.. (0 is `stream`), created on first use
-    int mq_sched = PP_BATCH_LOCKSTEP;  // pp_batch_set_schedule (the faster one: DESIGN.md §3.4)
-    DBuf<int> pq_next;                   // the persistent kernel's query counter
-    DBuf<long long> pq_tally;            // its tally (PqArgs::tally): kPqTally counters
-    DBuf<SceneDev> pq_scene;             // the scene in device memory (PqArgs::sc_global)
+    DBuf<SceneDev> mq_scene;      // the scene in device memory (point_blocked)
     hipEvent_t fork_ev = nullptr;
     std::vector<double> mq_goal;  // 3 per query (RRT::new's goal; pp_batch_plan)
     DBuf<double> mq_goal_d;       // [3Q] the goals on the device (pp_batch_plan)
@@ -219,7 +216,7 @@ struct pp_ctx {
     DBuf<DevState> cfb_state;
     DBuf<long long> cfb_pts;  // profiling: the rounds' walk point tallies
     int64_t cfb_nodes = 0, cfb_edges = 0, cfb_points = 0, cfb_arc = 0;  // profiling
-    bool cf_rounds = true;  // pp_batch_plan in steer rounds (PP_AMD_CF_ROUNDS=0: one kernel, A/B)
+    bool cf_rounds = true;  // pp_batch_plan in steer rounds (pp_batch_set_finish_schedule)
     int cfb_span0 = kCfbSpan, cfb_span = kCfbSpan;  // phase A candidates per node: first / later rounds
 
     // ---- RRT* query batch (BASELINE config 5, build-defined: DESIGN.md §3.7)
@@ -251,8 +248,6 @@ struct pp_ctx {
            insert_ms = 0.0;
     int64_t nn_scan_launches = 0, steer_launches = 0, finish_launches = 0;
     int64_t batch_steps = 0, batch_passes = 0;
-    double persist_ms = 0.0;
-    int64_t persist_launches = 0;
     DBuf<long long> cf_tally;  // check_finish (profiling): nodes, edges, points, arc points
     DBuf<long long> wg_pts;  // walked polyline points per walk workgroup (profiling on)
     long long* prof_points() const { return prof ? wg_pts.p : nullptr; }
@@ -261,11 +256,7 @@ struct pp_ctx {
         nn_scan_ms = steer_ms = finish_ms = finalize_ms = prep_ms = insert_ms = 0.0;
         nn_scan_launches = steer_launches = finish_launches = 0;
         batch_steps = batch_passes = 0;
-        persist_ms = 0.0;
-        persist_launches = 0;
         cfb_nodes = cfb_edges = cfb_points = cfb_arc = 0;
-        if (pq_tally.p && hipMemsetAsync(pq_tally.p, 0, pq_tally.n * sizeof(long long), stream) != hipSuccess)
-            return PP_ERR_HIP;
         if (wg_pts.p && hipMemsetAsync(wg_pts.p, 0, wg_pts.n * sizeof(long long), stream) != hipSuccess)
             return PP_ERR_HIP;
         if (cf_tally.p && hipMemsetAsync(cf_tally.p, 0, cf_tally.n * sizeof(long long), stream) != hipSuccess)
@@ -610,29 +601,6 @@ int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line,
 // whose verdicts are known, and check_finish_kernel runs the rest (literal paths, errors) with
 // the memo filled.  The same results as cf_run over all items; polygon scenes and batches with
 // a blocked root take cf_run.
-// profiling (PP_AMD_CF_VERBOSE): the walk statuses of a round's tasks
-static void cfb_status_hist(pp_ctx* c, const CfbArgs& a, int round) {
-    DevState ds;
-    if (hipMemcpyAsync(&ds, a.st, sizeof ds, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return;
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return;
-    std::vector<int> v((size_t)std::max(ds.W, 0));
-    std::vector<PrepRec> rc((size_t)std::max(ds.W, 0));
-    if (ds.W > 0) {
-        if (hipMemcpy(v.data(), a.status, v.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return;
-        if (hipMemcpy(rc.data(), a.rec, rc.size() * sizeof(PrepRec), hipMemcpyDeviceToHost) != hipSuccess) return;
-    }
-    int h[16] = {0};
-    int trim = 0, lit_trim = 0, none = 0;
-    for (size_t i = 0; i < v.size(); ++i) {
-        h[std::min(std::max(v[i] + 4, 0), 15)]++;
-        trim += rc[i].trim1;
-        lit_trim += rc[i].trim1 && v[i] == kLiteral;
-        none += rc[i].state == kPrepNone;
-    }
-    std::fprintf(stderr, "cfb round %d: W %d status(-4..) ", round, ds.W);
-    for (int k = 0; k < 12; ++k) std::fprintf(stderr, "%d:%d ", k - 4, h[k]);
-    std::fprintf(stderr, " trim1 %d (literal %d) none %d\n", trim, lit_trim, none);
-}
 
 int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in, const CfOut& o) {
     const int Q = c->mq_Q;
@@ -733,7 +701,6 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
         PP_HIP(launch_cfb(st, sd, a, kCfbEmitA, m0));
         PP_HIP(launch_cfb_steer(st, sd, a, mt, false, wpts));
         PP_HIP(launch_cfb_literal(st, sd, a, mt, c->cfb_lit.p, c->cfb_misc.p + 3, c->api_lit_scratch.p));
-        if (std::getenv("PP_AMD_CF_VERBOSE")) cfb_status_hist(c, a, rounds);
         PP_HIP(launch_cfb(st, sd, a, kCfbConsumeA, m0));
         m0 += a.span;
     }
@@ -741,15 +708,12 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     PP_HIP(launch_cfb_steer(st, sd, a, (int)std::min<size_t>(cap_tasks, 2 * nn), true, wpts));
     PP_HIP(launch_cfb_literal(st, sd, a, (int)std::min<size_t>(cap_tasks, 2 * nn), c->cfb_lit.p,
                               c->cfb_misc.p + 3, c->api_lit_scratch.p));
-    if (std::getenv("PP_AMD_CF_VERBOSE")) cfb_status_hist(c, a, 100);
     PP_HIP(launch_cfb(st, sd, a, kCfbStoreB, (int)std::min<size_t>(cap_tasks, 2 * nn)));
     PP_HIP(launch_cfb(st, sd, a, kCfbAssemble, 0, o.ok, o.len, o.npts, c->cf_err.p, c->cf_items.p,
                       c->cfb_plist.p));
     PP_HIP(hipMemcpyAsync(misc, c->cfb_misc.p, sizeof misc, hipMemcpyDeviceToHost, st));
     PP_HIP(hipStreamSynchronize(st));
     const int np = misc[1];
-    if (std::getenv("PP_AMD_CF_VERBOSE"))  // profiling: the items check_finish_kernel takes
-        std::fprintf(stderr, "cf_run_rounds: items %d punted %d rounds %d\n", total, np, rounds);
     CfBatch cb = cb_in;
     cb.ftab = a.ftab;
     cb.gtab = a.gtab;
@@ -825,7 +789,7 @@ MqArgs mq_args(pp_ctx* c) {
     a.lit_locks = c->lit_locks.p;
     a.err = c->mq_err.p;
     a.wg_points = c->prof_points();
-    a.scp = c->pq_scene.p;  // (uploaded by pp_batch_extend)
+    a.scp = c->mq_scene.p;  // (uploaded by pp_batch_extend)
     return a;
 }
 
@@ -1093,9 +1057,6 @@ int pp_create(int device, pp_ctx** out) {
         return set_err(PP_ERR_NO_DEVICE, std::string("built for gfx950, device is ") + prop.gcnArchName);
     pp_ctx* c = new pp_ctx();
     c->device = device;
-    if (const char* v = std::getenv("PP_AMD_CF_ROUNDS")) c->cf_rounds = std::atoi(v) != 0;
-    if (const char* v = std::getenv("PP_AMD_CFB_SPAN0")) c->cfb_span0 = std::min(std::max(std::atoi(v), 1), 16);
-    if (const char* v = std::getenv("PP_AMD_CFB_SPAN")) c->cfb_span = std::min(std::max(std::atoi(v), 1), 16);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = c->d_state.reserve(1);
     if (e == hipSuccess) e = c->d_api_state.reserve(1);
@@ -2080,61 +2041,16 @@ int pp_batch_set_window(pp_ctx* ctx, int k) {
     return PP_OK;
 }
 
-int pp_batch_set_schedule(pp_ctx* ctx, int schedule) {
+int pp_batch_set_finish_schedule(pp_ctx* ctx, int rounds, int span0, int span) {
     if (!ctx) return set_err(PP_ERR_INVALID_ARGUMENT, "null context");
-    if (schedule != PP_BATCH_PERSISTENT && schedule != PP_BATCH_LOCKSTEP)
-        return set_err(PP_ERR_INVALID_ARGUMENT, "schedule must be PP_BATCH_PERSISTENT or PP_BATCH_LOCKSTEP");
-    ctx->mq_sched = schedule;
+    if (rounds != 0 && rounds != 1) return set_err(PP_ERR_INVALID_ARGUMENT, "rounds must be 0 or 1");
+    if (span0 < 0 || span0 > 16 || span < 0 || span > 16)
+        return set_err(PP_ERR_INVALID_ARGUMENT, "span0 / span must be in [0, 16]");
+    ctx->cf_rounds = rounds != 0;
+    ctx->cfb_span0 = span0 ? span0 : kCfbSpan;
+    ctx->cfb_span = span ? span : kCfbSpan;
     return PP_OK;
 }
-
-namespace {
-// pp_batch_extend, persistent schedule: one launch runs every query to its target (the window
-// stops and resumes inside the kernel, so there are no top-up passes)
-int batch_extend_persistent(pp_ctx* ctx, const MqArgs& a) {
-    hipStream_t st = ctx->stream;
-    if (!ctx->pq_next.p) PP_HIP(ctx->pq_next.reserve(1));
-    if (!ctx->pq_tally.p) {
-        PP_HIP(ctx->pq_tally.reserve(kPqTally));
-        PP_HIP(hipMemsetAsync(ctx->pq_tally.p, 0, kPqTally * sizeof(long long), st));
-    }
-    PP_HIP(hipMemsetAsync(ctx->pq_next.p, 0, sizeof(int), st));
-    PqArgs pa;
-    pa.mq = a.mq;
-    pa.sc = a.sc;
-    pa.sc_global = ctx->pq_scene.p;
-    // slots per workgroup: every query in flight at once when the resident workgroups allow it
-    // (a 1024-query shard: 2 per workgroup at 2 workgroups per CU), at most kPqMaxTasks tasks
-    const int K = std::max(1, a.mq.K);
-    const int cap = std::max(1, pq_grid_cap_host(a.sc));
-    pa.slots = std::max(1, std::min({kPqMaxSlots, kPqMaxTasks / K, (a.mq.Q + cap - 1) / cap}));
-    pa.qnext = ctx->pq_next.p;
-    pa.lit_scratch = a.lit_scratch;
-    pa.lit_locks = a.lit_locks;
-    pa.err = a.err;
-    pa.tally = ctx->pq_tally.p;
-    if (ctx->prof) {
-        int r = ensure_events(ctx, 2);
-        if (r) return r;
-        PP_HIP(hipEventRecord(ctx->ev[0], st));
-    }
-    PP_HIP(launch_mq_persist(st, pa));
-    if (ctx->prof) {
-        PP_HIP(hipEventRecord(ctx->ev[1], st));
-        PP_HIP(hipEventSynchronize(ctx->ev[1]));
-        float ms = 0.f;
-        PP_HIP(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
-        ctx->persist_ms += ms;
-        ctx->persist_launches += 1;
-    }
-    int err = 0;
-    PP_HIP(hipMemcpyAsync(&err, ctx->mq_err.p, sizeof(int), hipMemcpyDeviceToHost, st));
-    PP_HIP(hipStreamSynchronize(st));
-    if (err) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
-    ctx->batch_passes += 1;
-    return PP_OK;
-}
-}  // namespace
 
 int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted) {
     int r = check_ctx(ctx, true, false);
@@ -2143,23 +2059,16 @@ int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t
     if (n_steps < 0) return set_err(PP_ERR_INVALID_ARGUMENT, "n_steps < 0");
     int64_t it0 = 0, n0 = 0, it1 = 0, n1 = 0;
     if ((n_iterations || n_accepted) && (r = mq_totals(ctx, &it0, &n0))) return r;
-    {  // the batch's scene in device memory (point_blocked, the persistent kernel's literal path)
-        if (!ctx->pq_scene.p) PP_HIP(ctx->pq_scene.reserve(1));
+    {  // the batch's scene in device memory (point_blocked)
+        if (!ctx->mq_scene.p) PP_HIP(ctx->mq_scene.reserve(1));
         const SceneDev sd = mq_args(ctx).sc;
-        PP_HIP(hipMemcpy(ctx->pq_scene.p, &sd, sizeof sd, hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(ctx->mq_scene.p, &sd, sizeof sd, hipMemcpyHostToDevice));
     }
     MqArgs a = mq_args(ctx);
     const int K = ctx->mq_K, Q = ctx->mq_Q;
     // an earlier call's PP_ERR_STEER_OVERFLOW does not stick to this one
     PP_HIP(hipMemsetAsync(ctx->mq_err.p, 0, sizeof(int), ctx->stream));
     PP_HIP(launch_mq_target(ctx->stream, a.mq, n_steps, ctx->mq_target.p));
-    if (ctx->mq_sched == PP_BATCH_PERSISTENT) {
-        if ((r = batch_extend_persistent(ctx, a))) return r;
-        if ((n_iterations || n_accepted) && (r = mq_totals(ctx, &it1, &n1))) return r;
-        if (n_iterations) *n_iterations = it1 - it0;
-        if (n_accepted) *n_accepted = n1 - n0;
-        return PP_OK;
-    }
     // sub-batches on their own streams (profiled too: the events time the schedule that runs)
     const int nsub = ctx->mq_nsub;
     MqArgs sub[kMaxSub];
@@ -2572,19 +2481,6 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out, uint64_t out_size) {
         s.finish_edges = t[1] + ctx->cfb_edges;
         s.finish_points = t[2] + ctx->cfb_points;
         s.finish_arc_points = t[3] + ctx->cfb_arc;
-    }
-    s.persist_ms = ctx->persist_ms;
-    s.persist_launches = ctx->persist_launches;
-    if (ctx->pq_tally.p) {  // the persistent batch kernel: query-steps, points, phase cycles
-        long long t[kPqTally];
-        PP_HIP(hipMemcpyAsync(t, ctx->pq_tally.p, sizeof t, hipMemcpyDeviceToHost, ctx->stream));
-        PP_HIP(hipStreamSynchronize(ctx->stream));
-        s.batch_query_steps = t[0];
-        s.walk_points += t[1];
-        s.walk_arc_points += t[2];
-        for (int p = 0; p < 5; ++p) s.persist_cycles[p] = t[3 + p];
-        s.samples_evaluated += t[8];
-        s.samples_blocked += t[9];
     }
     std::memcpy(out, &s, (size_t)std::min<uint64_t>(out_size, sizeof s));
     return PP_OK;

@@ -178,32 +178,6 @@ struct MqArgs {
     const SceneDev* scp = nullptr;   // the scene in device memory: point_blocked (or null: none)
 };
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps);
-// Persistent form (round 4): ONE launch runs every query to mq.target.  A workgroup owns `slots`
-// queries at a time (a launch-wide counter hands them out; qnext zeroed before the launch) and its
-// waves step their windows — prep passes and walk tasks taken from per-slot LDS counters, the
-// insert + next samples + nearest nodes on the wave that finished the walk — with the records in
-// LDS.  slots * mq.K <= kPqMaxTasks, K a power of two <= 64.
-constexpr int kPqMaxTasks = 128;
-constexpr int kPqThreads = 512;   // 8 waves per workgroup
-constexpr int kPqMaxSlots = 8;    // queries per workgroup (the insert: one wave each)
-constexpr int kPqTally = 10;
-struct PqArgs {
-    MqDev mq{};
-    SceneDev sc{};
-    const SceneDev* sc_global = nullptr;  // the same scene in device memory (the literal path)
-    int slots = 1;
-    int* qnext = nullptr;
-    double* lit_scratch = nullptr;  // kLiteralWaves buffers
-    int* lit_locks = nullptr;
-    int* err = nullptr;
-    long long* tally = nullptr;  // profiling (or null), kPqTally int64: query-steps, walked points,
-                                 // arc points, the waves' time (wall_clock64 ticks, 100 MHz) in
-                                 // the serial phases, prep passes, walk tasks and idle, 0, window
-                                 // slots evaluated, of them decided by point_blocked
-};
-hipError_t launch_mq_persist(hipStream_t s, const PqArgs& a);
-// resident workgroups of the persistent kernel for a scene (occupancy API)
-int pq_grid_cap_host(const SceneDev& sc);
 hipError_t launch_mq_init(hipStream_t s, const MqDev& mq, const double* starts);
 // the per-query iteration targets of a pp_batch_extend(n_steps) call
 hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int64_t* target);

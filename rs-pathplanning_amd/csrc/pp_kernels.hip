@@ -2958,7 +2958,7 @@ __device__ __attribute__((always_inline)) inline void commit_role(
     const double* __restrict__ wsy, const int* __restrict__ nn_idx,
     const int* __restrict__ snap_status, const double* __restrict__ snap_yaw,
     const int* __restrict__ fin_par, int* __restrict__ cand_cnt, int W, int64_t void_next,
-    char* smem) {
+    int64_t screened, char* smem) {
     constexpr int PER = kMaxWindow / NT;
     static_assert(PER % 4 == 0, "commit: whole int4 loads per thread");
     int* s_node = reinterpret_cast<int*>(smem);
@@ -3025,7 +3025,9 @@ __device__ __attribute__((always_inline)) inline void commit_role(
         st->windows += 1;
         st->truncations += Weff < W;
         st->nn_flagged += st->flag_count;
-        st->node_evals += (int64_t)W * n0;
+        // the screen's distance evaluations: the samples it covered (not in an obstacle) x the
+        // tree nodes it scanned (nodes past n_scan are nn_finalize's, a few per window)
+        st->node_evals += screened;
         if (Weff < W) {
             st->it_spec = it0 + Weff;
             if (void_next >= 0) st->void_seq = void_next;
@@ -3076,7 +3078,8 @@ __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
                 __syncthreads();
                 commit_role<kScanThreads>(st, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.snap_status,
                                           a.snap_yaw, a.fin_par, a.cand_cnt, W,
-                                          a.scan ? a.seq : -1, smem);
+                                          a.scan ? a.seq : -1,
+                                          (int64_t)st->Wsp[q] * st->nsp[q], smem);
             }
         }
         if (threadIdx.x == 0) {  // the screened window's counters start at zero
@@ -3112,7 +3115,8 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_tail_kernel(WinKArgs 
     // (same workgroup: the barrier's workgroup-scope fence orders these stores)
     __syncthreads();
     commit_role<kResolveThreads>(st, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.snap_status,
-                                 a.snap_yaw, a.fin_par, a.cand_cnt, W, a.scan ? a.seq : -1, smem);
+                                 a.snap_yaw, a.fin_par, a.cand_cnt, W, a.scan ? a.seq : -1,
+                                 (int64_t)st->Wsp[q] * st->nsp[q], smem);
     if (threadIdx.x == 0) {
         st->resolve_bail = 0;
         st->flag_count = 0;
@@ -4679,438 +4683,6 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
         if (ev) (void)hipEventRecord(ev[4], s);
     }
     return hipGetLastError();
-}
-
-// ------------------------------------------- persistent query batch (config 3, round 4)
-//
-// One launch runs every query of the batch to its target.  A workgroup owns `slots` queries at a
-// time (taken from a launch-wide counter: one atomic per query, not per task).  A slot's step —
-// one speculative window of K iterations of its query — is a chain of three phases:
-//   prep    steer_prep of the window's K tasks (prep_task, 8 lanes per task: ceil(K / 8) passes
-//           of 8 tasks), the PrepRecs into LDS (they never reach HBM)
-//   walk    steer_walk of the K tasks (walk_rec on the LDS record; the scene image is staged once
-//           per workgroup)
-//   serial  one wave: literal re-runs, the in-order replay of mq_insert_kernel — the window stops
-//           at the first iteration an accepted window sample is strictly nearer to than its
-//           snapshot NN — and the append (rrt.rs:586-589); the next query when this one reached
-//           its target; then the next window's samples (rand_point, rrt.rs:139-146, the query's
-//           stream) and their exact f64 nearest nodes (rrt.rs:378-391, lowest index on ties)
-// There is no workgroup barrier in the loop.  The waves are workers: each takes the next item —
-// a prep pass or a walk task — of any slot from that slot's LDS counter, and the wave that
-// finishes a phase's last item starts the slot's next phase (the serial one itself).  A long path
-// holds only its own slot's step while the other waves walk the other slots' tasks; a cut costs
-// the rest of the window, not a relaunch.
-//
-// Slot protocol (LDS): grab[s] = (epoch << 32) | items taken, one 64-bit atomic, so a worker learns
-// the phase and its item from the same atomic (epoch even: prep, odd: walk; kEpBusy: serial or
-// not started, kEpRetired: no query left); done[s] counts finished items, reset by the finisher
-// before it opens the next epoch.  Workgroup-scope fences order the records, verdicts and tree
-// rows between the waves (all on one CU).
-//
-// Every query's tree is exactly its one-iteration-at-a-time run (the lockstep kernels' rule).
-constexpr int kPqWaves = kPqThreads / 64;
-constexpr int kPqMinW = 4;  // waves per SIMD the register budget allows
-constexpr unsigned kEpBusy = 0xFFFFFFFEu, kEpRetired = 0xFFFFFFFFu;
-
-// The workgroup's LDS after the scene image and the waves' generator slots: slot s's window is
-// tasks [s K, s K + K).
-struct PqLds {
-    PrepRec rec[kPqMaxTasks];
-    double tx[kPqMaxTasks], ty[kPqMaxTasks], td2[kPqMaxTasks];
-    int tpn[kPqMaxTasks], tst[kPqMaxTasks];
-    int tlist[kPqMaxTasks];          // slot s: its window slots that need steering, in order
-    unsigned char tpre[kPqMaxTasks]; // the sample lies in an obstacle (point_blocked)
-    unsigned long long grab[kPqMaxSlots];
-    long long sit[kPqMaxSlots], stg[kPqMaxSlots];
-    int sq[kPqMaxSlots], sn[kPqMaxSlots], done[kPqMaxSlots], nact[kPqMaxSlots];
-    int nretired;
-};
-__host__ __device__ inline int pq_lds_bytes(int scene_bytes) {
-    return scene_bytes + kPqWaves * kGenSlots * 8 + (int)((sizeof(PqLds) + 15) & ~(size_t)15);
-}
-
-// A prep pass out of line: prep_task's transcendental chains need ~160 VGPRs (the standalone
-// steer_prep kernel's allocation); inlined, they would set the whole kernel's budget.  Tasks
-// t0 .. t0 + 7 of the LDS task arrays, one per 8-lane group (all 64 lanes call prep_task); only
-// tasks below t_end are written.  prep_task reads only the step and the radius of the scene.
-__device__ __noinline__ void pq_prep(double step, double turn_radius, int lds_off,
-                                     const double* __restrict__ mx, const double* __restrict__ my,
-                                     const double* __restrict__ myaw, size_t row, int base, int i0,
-                                     int nact) {
-    PqLds& L = *reinterpret_cast<PqLds*>(pp_smem + lds_off);
-    SceneDev sc;
-    sc.step_size = step;
-    sc.turn_radius = turn_radius;
-    const int lane = threadIdx.x & 63;
-    const int i = i0 + lane / 8;  // entry of the slot's task list
-    const bool in = i < nact;
-    const int t = in ? base + L.tlist[base + i] : base;
-    const int pn = in ? L.tpn[t] : -1;
-    double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0;
-    if (in) {
-        x = L.tx[t];
-        y = L.ty[t];
-        px = mx[row + pn];
-        py = my[row + pn];
-        pyaw = myaw[row + pn];
-    }
-    prep_task(sc, lane & 7, lane & ~7, t, in, in, x, y, px, py, pyaw, 0, 0.0, 0, 0.0, 0.0, L.rec,
-              nullptr, nullptr);
-}
-
-// the literal path out of line: it runs once in a few thousand steps, and inlined its registers
-// would set the whole kernel's budget.  The scene comes from its global-memory copy: a reference
-// to the kernel argument would make the compiler copy the whole argument block to the stack.
-__device__ __noinline__ int pq_literal(const SceneDev* __restrict__ sc, const PrepRec* R,
-                                       double* bx) {
-    // (its own inlined copy: a function only these kernels call gets their register budget)
-    return steer_collide_literal_body<true>(*sc, R->x, R->y, R->yaw, R->px, R->py, R->pyaw, bx,
-                                      bx + kLiteralCap, bx + 2 * kLiteralCap, true);
-}
-
-__device__ __forceinline__ unsigned long long lds_load_u64(const unsigned long long* p) {
-    return __atomic_load_n(p, __ATOMIC_RELAXED);
-}
-
-template <bool kLds, int kScene>
-__global__ __launch_bounds__(kPqThreads, kPqMinW) void mq_persist_kernel(PqArgs a) {
-    const MqDev& mq = a.mq;
-    const SceneDev& sc = a.sc;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int K = mq.K, QS = a.slots;
-    if (kLds) stage_scene(sc);
-    double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) + wave * kGenSlots;
-    const int lds_off = (kLds ? sc.lds_bytes : 0) + kPqWaves * kGenSlots * 8;
-    PqLds& L = *reinterpret_cast<PqLds*>(pp_smem + lds_off);
-    if (tid < kPqMaxSlots) {
-        L.grab[tid] = (unsigned long long)kEpBusy << 32;
-        L.done[tid] = 0;
-        L.sq[tid] = -1;
-    }
-    if (tid == 0) L.nretired = 0;
-    __syncthreads();
-    long long npts = 0, napts = 0, qsteps = 0, ntask = 0, npre = 0;
-    long long cyc[4] = {0, 0, 0, 0};  // this wave: serial, prep, walk, idle (profiling)
-    const bool prof = a.tally != nullptr;
-
-    // the serial phase of slot s on this wave: insert the finished window (when `insert`), the
-    // next query when this one is done, the next window's samples and nearest nodes, then open
-    // the prep epoch `ep` (or retire the slot)
-    auto serial = [&](int s, bool insert, unsigned ep) {
-        const int base = s * K;
-        int nact = 0;
-        for (;;) {  // (an all-rejected window is replayed at once)
-        if (insert) {
-            const int q = L.sq[s];
-            const int k = lane;
-            const bool inw = k < K;
-            const int t = base + k;
-            int st = kReject, pn = -1;
-            bool pre = false;
-            double x = 0.0, y = 0.0, yw = 0.0, d2nn = 0.0;
-            if (inw) {
-                pn = L.tpn[t];
-                pre = L.tpre[t];
-                st = pre ? kReject : L.tst[t];
-                x = L.tx[t];
-                y = L.ty[t];
-                yw = pre ? 0.0 : L.rec[t].yaw;
-                d2nn = L.td2[t];
-            }
-            const bool act = inw && pn >= 0;
-            if (uint64_t lit = __ballot(act && st == kLiteral)) {  // measure-zero trim cases
-                const int slot = lit_acquire(a.lit_locks, (int)blockIdx.x * kPqMaxSlots + s);
-                double* bx = a.lit_scratch + (size_t)slot * 3 * kLiteralCap;
-                for (; lit; lit &= lit - 1) {
-                    const int l = __builtin_ctzll(lit);
-                    const int r = pq_literal(a.sc_global, &L.rec[base + l], bx);
-                    if (lane == l) st = r;
-                }
-                lit_release(a.lit_locks, slot);
-            }
-            const bool blocked = mq.blocked && mq.blocked[q];
-            const uint64_t accm = __ballot(act && st == kAccept && !blocked);
-            bool cut = !act;
-            for (int j = 0; j < K; ++j) {
-                const double xj = __shfl(x, j), yj = __shfl(y, j);
-                // (a sample in an obstacle is rejected whatever its parent: never cut there)
-                if (((accm >> j) & 1ull) && k > j && act && !pre) {
-                    const double dx = x - xj, dy = y - yj;
-                    if (dx * dx + dy * dy < d2nn) cut = true;
-                }
-            }
-            const uint64_t kmask = K >= 64 ? ~0ull : ((1ull << K) - 1ull);
-            const uint64_t cutm = __ballot(inw && cut) & kmask;
-            const int Tc = cutm ? (int)__builtin_ctzll(cutm) : K;  // iterations consumed (>= 1)
-            const uint64_t keep = accm & (Tc >= 64 ? ~0ull : ((1ull << Tc) - 1ull));
-            const bool bad = __ballot(k < Tc && act && st == kError) != 0;
-            const int n = L.sn[s];
-            const int before = __popcll(keep & ((1ull << lane) - 1ull));
-            if (!bad && k < Tc && ((keep >> lane) & 1ull)) {
-                const size_t o = (size_t)q * mq.cap + n + before;
-                mq.x[o] = x;
-                mq.y[o] = y;
-                mq.yaw[o] = yw;
-                mq.parent[o] = pn;
-            }
-            // the sequential spec's node-distance evaluations: iteration k scans n + before nodes
-            long long ev = (inw && k < Tc) ? (long long)(n + before) : 0;
-            for (int o = 1; o < 64; o <<= 1) ev += __shfl_xor(ev, o);
-            if (lane == 0) {
-                if (bad) {
-                    atomicOr(a.err, 1);
-                    L.sit[s] = L.stg[s];  // the reference panics: the query stops here
-                } else {
-                    const int nn = n + __popcll(keep);
-                    const long long it = L.sit[s] + Tc;
-                    L.sn[s] = nn;
-                    L.sit[s] = it;
-                    mq.n[q] = nn;
-                    mq.it[q] = it;
-                    mq.evals[q] += ev;
-                }
-            }
-            ++qsteps;
-            __threadfence_block();  // this wave's LDS and tree-row writes before the reads below
-        }
-        // the next query when this one reached its target (lane 0; the counter hands out each
-        // query once)
-        int q = L.sq[s];
-        if (q == -1 || L.sit[s] >= L.stg[s]) {
-            if (lane == 0) {
-                for (;;) {
-                    q = atomicAdd(a.qnext, 1);
-                    if (q >= mq.Q) {
-                        q = -2;
-                        break;
-                    }
-                    const long long it = mq.it[q], tg = mq.target[q];
-                    if (it < tg) {
-                        L.sn[s] = mq.n[q];
-                        L.sit[s] = it;
-                        L.stg[s] = tg;
-                        break;
-                    }
-                }
-                L.sq[s] = q;
-            }
-            q = __shfl(q, 0);
-            __threadfence_block();
-        }
-        if (q < 0) {  // no query left: retire the slot
-            if (lane == 0) {
-                L.grab[s] = (unsigned long long)kEpRetired << 32;
-                atomicAdd(&L.nretired, 1);
-            }
-            return;
-        }
-        // the next window: lane l serves window slot k = l mod K over rows i = l / K mod 64 / K
-        {
-            const int G = 64 / K;
-            const int k = lane & (K - 1), g = lane / K;
-            const long long it = L.sit[s] + k;
-            const bool live = it < L.stg[s];
-            const uint64_t seed = mq.seed[q];
-            double x = 0.0, y = 0.0, bd = __builtin_inf();
-            int bi = 0x7fffffff;
-            if (live) {
-                x = gen_range(seed, 2 * (uint64_t)it, sc.minx, sc.maxx);
-                y = gen_range(seed, 2 * (uint64_t)it + 1, sc.miny, sc.maxy);
-                const size_t row = (size_t)q * mq.cap;
-                const double* __restrict__ X = mq.x + row;
-                const double* __restrict__ Y = mq.y + row;
-                const int n = L.sn[s];
-#pragma unroll 4
-                for (int i = g; i < n; i += G) {
-                    const double dx = x - X[i], dy = y - Y[i];
-                    const double d2 = dx * dx + dy * dy;
-                    if (d2 < bd) {
-                        bd = d2;
-                        bi = i;
-                    }
-                }
-            }
-            for (int m = K; m < 64; m <<= 1) {  // the G lanes of window slot k
-                if (m == 16)
-                    argmin_swap<false>(bd, bi);
-                else if (m == 32)
-                    argmin_swap<true>(bd, bi);
-                else
-                    argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
-            }
-            // the samples in an obstacle are decided here; the others are listed for prep + walk
-            const bool pre = live && point_blocked<kLds, kScene>(sc, x, y);
-            const uint64_t am = __ballot(g == 0 && live && !pre);
-            if (g == 0) {
-                L.tx[base + k] = x;
-                L.ty[base + k] = y;
-                L.tpn[base + k] = live ? bi : -1;
-                L.td2[base + k] = bd;
-                L.tpre[base + k] = pre ? 1 : 0;
-                if (live && !pre) L.tlist[base + __popcll(am & ((1ull << lane) - 1ull))] = k;
-            }
-            nact = __popcll(am);
-            ntask += __popcll(__ballot(g == 0 && live));
-            npre += __popcll(__ballot(g == 0 && pre));
-        }
-        __threadfence_block();
-        if (nact > 0) break;
-        insert = true;
-        }
-        if (lane == 0) L.nact[s] = nact;
-        if (lane == 0) {
-            L.done[s] = 0;
-            __threadfence_block();
-            atomicExch(&L.grab[s], (unsigned long long)ep << 32);  // open the prep epoch
-        }
-    };
-
-    long long c0 = prof ? (long long)wall_clock64() : 0;
-    auto stamp = [&](int ph) {
-        if (prof) {
-            const long long c1 = (long long)wall_clock64();
-            cyc[ph] += c1 - c0;
-            c0 = c1;
-        }
-    };
-    if (wave < QS) {  // every slot's first query and window
-        serial(wave, false, 0u);
-        stamp(0);
-    }
-    for (int rr = 0;; ++rr) {
-        // an item of any slot, starting at this wave's own slot
-        int s = -1, item = 0;
-        unsigned ep = 0;
-        for (int i = 0; i < QS && s < 0; ++i) {
-            const int c = (wave + rr + i) % QS;
-            const unsigned long long v = lds_load_u64(&L.grab[c]);
-            const unsigned e = (unsigned)(v >> 32);
-            if (e >= kEpBusy) continue;
-            const int na = L.nact[c];
-            const unsigned lim = (e & 1u) ? (unsigned)na : (unsigned)((na + 7) / 8);
-            if ((unsigned)v >= lim) continue;  // every item of the phase is taken
-            unsigned long long old = 0;
-            if (lane == 0) old = atomicAdd(&L.grab[c], 1ull);
-            old = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(old >> 32)) << 32) |
-                  (unsigned)__builtin_amdgcn_readfirstlane((int)old);
-            const unsigned e2 = (unsigned)(old >> 32);
-            if (e2 >= kEpBusy) continue;
-            const int na2 = L.nact[c];
-            const unsigned lim2 = (e2 & 1u) ? (unsigned)na2 : (unsigned)((na2 + 7) / 8);
-            if ((unsigned)old < lim2) {
-                s = c;
-                item = (int)(unsigned)old;
-                ep = e2;
-            }
-        }
-        if (s < 0) {
-            if (__atomic_load_n(&L.nretired, __ATOMIC_RELAXED) >= QS) break;
-            __builtin_amdgcn_s_sleep(2);
-            stamp(3);
-            continue;
-        }
-        __threadfence_block();  // the phase's inputs (records, samples) were published before
-        const int base = s * K;
-        const bool walk = ep & 1u;
-        const int nact = L.nact[s];
-        if (walk) {
-            int np = 0, na = 0;
-            const int t = base + L.tlist[base + item];
-            const int st = walk_rec<kLds, kScene>(sc, &L.rec[t], nullptr, gs, np, na);
-            if (lane == 0) L.tst[t] = st;
-            npts += np;
-            napts += na;
-            stamp(2);
-        } else {
-            pq_prep(sc.step_size, sc.turn_radius, lds_off, mq.x, mq.y, mq.yaw,
-                    (size_t)L.sq[s] * mq.cap, base, 8 * item, nact);
-            stamp(1);
-        }
-        __threadfence_block();  // this item's results before it counts as done
-        int d = 0;
-        if (lane == 0) d = atomicAdd(&L.done[s], 1);
-        d = __builtin_amdgcn_readfirstlane(d);
-        if (d != (walk ? nact : (nact + 7) / 8) - 1) continue;
-        // the phase's last item: this wave opens the slot's next phase
-        if (!walk) {
-            if (lane == 0) {
-                L.done[s] = 0;
-                __threadfence_block();
-                atomicExch(&L.grab[s], (unsigned long long)(ep + 1) << 32);  // the walk epoch
-            }
-        } else {
-            if (lane == 0) L.grab[s] = (unsigned long long)kEpBusy << 32;
-            serial(s, true, ep + 1 >= kEpBusy - 1 ? 0u : ep + 1);
-            stamp(0);
-        }
-    }
-    if (prof) {  // [0] query-steps, [1] walked points, [2] their arc points, [3..6] wave time,
-                 // [8] window slots evaluated, [9] of them decided by point_blocked
-        unsigned long long* tl = reinterpret_cast<unsigned long long*>(a.tally);
-        if (lane == 0) {
-            atomicAdd(&tl[0], (unsigned long long)qsteps);
-            atomicAdd(&tl[1], (unsigned long long)npts);
-            atomicAdd(&tl[2], (unsigned long long)napts);
-            for (int p = 0; p < 4; ++p) atomicAdd(&tl[3 + p], (unsigned long long)cyc[p]);
-            atomicAdd(&tl[8], (unsigned long long)ntask);
-            atomicAdd(&tl[9], (unsigned long long)npre);
-        }
-    }
-}
-
-template <typename F>
-inline hipError_t pq_kernel_for(const SceneDev& sc, F&& f) {
-    const bool lds = sc.lds_bytes > 0;
-    switch (scene_kind(sc)) {
-        case kSceneGrid:
-            return lds ? f(mq_persist_kernel<true, kSceneGrid>)
-                       : f(mq_persist_kernel<false, kSceneGrid>);
-        case kScenePoly:
-            return lds ? f(mq_persist_kernel<true, kScenePoly>)
-                       : f(mq_persist_kernel<false, kScenePoly>);
-        default:
-            return lds ? f(mq_persist_kernel<true, kSceneDisc>)
-                       : f(mq_persist_kernel<false, kSceneDisc>);
-    }
-}
-
-// the resident workgroups of the persistent kernel (occupancy API with its dynamic LDS)
-int pq_grid_cap(const SceneDev& sc) {
-    static std::mutex mu;
-    static std::map<std::tuple<int, int, int>, int> cache;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    std::lock_guard<std::mutex> lk(mu);
-    const std::tuple<int, int, int> key{dev, sc.lds_bytes, scene_kind(sc)};
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    int cus = 256, per_cu = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
-        cus = prop.multiProcessorCount;
-    const hipError_t e = pq_kernel_for(sc, [&](auto kern) {
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kPqThreads,
-                                                            pq_lds_bytes(sc.lds_bytes));
-    });
-    if (e != hipSuccess || per_cu < 1) per_cu = 1;
-    const int cap = cus * per_cu;
-    cache[key] = cap;
-    return cap;
-}
-
-int pq_grid_cap_host(const SceneDev& sc) { return pq_grid_cap(sc); }
-
-hipError_t launch_mq_persist(hipStream_t s, const PqArgs& a) {
-    const int K = a.mq.K;
-    if (K < 1 || K > 64 || (K & (K - 1)) || a.slots < 1 || a.slots > kPqMaxSlots ||
-        a.slots * K > kPqMaxTasks)
-        return hipErrorInvalidValue;
-    const int grid = std::min((a.mq.Q + a.slots - 1) / a.slots, pq_grid_cap(a.sc));
-    return pq_kernel_for(a.sc, [&](auto kern) {
-        kern<<<grid, kPqThreads, pq_lds_bytes(a.sc.lds_bytes), s>>>(a);
-        return hipGetLastError();
-    });
 }
 
 // ------------------------------------------------------- RRT* query batch (config 5, §3.7)

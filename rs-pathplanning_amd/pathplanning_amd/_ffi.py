@@ -21,9 +21,7 @@ PP_ERR_STATE = -5
 PP_ERR_STEER_OVERFLOW = -6
 PP_ERR_REFERENCE_PANIC = -7
 PP_CF_CHAIN = 18
-PP_ABI_VERSION = 3
-PP_BATCH_PERSISTENT = 0
-PP_BATCH_LOCKSTEP = 1
+PP_ABI_VERSION = 4
 
 _ERR_NAMES = {
     PP_ERR_INVALID_ARGUMENT: "PP_ERR_INVALID_ARGUMENT", PP_ERR_HIP: "PP_ERR_HIP",
@@ -45,7 +43,7 @@ EXPORTED = [
     "pp_rrt_set_window", "pp_rrt_extend", "pp_rrt_plan_one", "pp_rrt_tree_size",
     "pp_rrt_iteration", "pp_rrt_tree_export", "pp_rrt_get_nearest_node_batch",
     "pp_rrt_verify_node_batch", "pp_rrt_check_finish_batch", "pp_rrt_check_finish",
-    "pp_rrt_plan", "pp_batch_new", "pp_batch_set_window", "pp_batch_set_schedule", "pp_batch_extend", "pp_batch_state", "pp_batch_tree_export",
+    "pp_rrt_plan", "pp_batch_new", "pp_batch_set_window", "pp_batch_set_finish_schedule", "pp_batch_extend", "pp_batch_state", "pp_batch_tree_export",
     "pp_batch_plan",
     "pp_star_new", "pp_star_extend", "pp_star_state", "pp_star_tree_export",
     "pp_rrt_get_stats", "pp_rrt_reset_stats", "pp_set_profiling",
@@ -75,15 +73,12 @@ class StatsC(C.Structure):
         ("finish_ms", C.c_double), ("finish_launches", C.c_int64), ("finish_nodes", C.c_int64),
         ("finish_edges", C.c_int64), ("finish_points", C.c_int64),
         ("finish_arc_points", C.c_int64),
-        ("batch_query_steps", C.c_int64), ("persist_ms", C.c_double),
-        ("persist_launches", C.c_int64), ("persist_cycles", C.c_int64 * 5),
+        ("reserved_abi3", C.c_int64 * 8),
         ("samples_evaluated", C.c_int64), ("samples_blocked", C.c_int64),
     ]
 
     def as_dict(self):
-        d = {k: getattr(self, k) for k, _ in self._fields_}
-        d["persist_cycles"] = list(self.persist_cycles)
-        return d
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved_abi3"}
 
 
 _lock = threading.Lock()
@@ -162,7 +157,7 @@ def lib():
             "pp_batch_new": ([vp, C.c_int, dp, dp, C.POINTER(C.c_uint64), C.c_int64, C.c_double],
                              C.c_int),
             "pp_batch_set_window": ([vp, C.c_int], C.c_int),
-            "pp_batch_set_schedule": ([vp, C.c_int], C.c_int),
+            "pp_batch_set_finish_schedule": ([vp, C.c_int, C.c_int, C.c_int], C.c_int),
             "pp_batch_extend": ([vp, C.c_int64, i64p, i64p], C.c_int),
             "pp_batch_state": ([vp, ip, i64p, i64p], C.c_int),
             "pp_batch_tree_export": ([vp, C.c_int, dp, dp, dp, ip, C.c_int64, i64p], C.c_int),

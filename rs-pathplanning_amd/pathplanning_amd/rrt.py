@@ -229,11 +229,6 @@ class RRT:  # rrt.rs:325-620
         _ffi.check(_ffi.lib().pp_rrt_plan_one(self.ctx.handle, C.byref(acc)))
         return bool(acc.value)
 
-    def set_schedule(self, schedule: str):
-        """"persistent" or "lockstep" for the following extend calls (the trees do not depend
-        on it)."""
-        _ffi.check(_ffi.lib().pp_batch_set_schedule(self.ctx.handle, self.SCHEDULES[schedule]))
-
     def set_window(self, k: int):
         _ffi.check(_ffi.lib().pp_rrt_set_window(self.ctx.handle, int(k)))
 
@@ -423,15 +418,10 @@ class RRTBatch:
     (rrt.rs:335-355) with its own start, goal and sampling stream, advanced in lockstep — one
     plan_one extend iteration (rrt.rs:583-589) of every query per step — on one GPU.  ``window``:
     iterations per query evaluated speculatively per GPU step (a power of two <= 64, 0 =
-    automatic: 16 up to 131072 tasks per step); every query's tree equals its sequential run.
-    ``schedule``: "lockstep" (four launches per step over the whole batch; the default, the faster
-    one here) or "persistent" (one launch per extend call, every workgroup stepping its own
-    queries) — identical trees."""
-
-    SCHEDULES = {"persistent": _ffi.PP_BATCH_PERSISTENT, "lockstep": _ffi.PP_BATCH_LOCKSTEP}
+    automatic: 16 up to 131072 tasks per step); every query's tree equals its sequential run."""
 
     def __init__(self, starts, goals, max_iter, step_size, space: Space, seeds, device: int = 0,
-                 ctx: _ffi.Context | None = None, window: int = 0, schedule: str = "lockstep"):
+                 ctx: _ffi.Context | None = None, window: int = 0):
         self.ctx = ctx or _ffi.Context(device)
         self.space = space
         starts = np.ascontiguousarray(starts, dtype=np.float64).reshape(-1, 3)
@@ -442,7 +432,6 @@ class RRTBatch:
         space._upload(self.ctx)
         # iterations per query evaluated per GPU step (0: automatic); results do not depend on it
         _ffi.check(_ffi.lib().pp_batch_set_window(self.ctx.handle, int(window)))
-        self.set_schedule(schedule)
         dp = C.POINTER(C.c_double)
         _ffi.check(_ffi.lib().pp_batch_new(
             self.ctx.handle, self.q, starts.ctypes.data_as(dp), goals.ctypes.data_as(dp),
@@ -455,10 +444,12 @@ class RRTBatch:
                                               C.byref(acc)))
         return it.value, acc.value
 
-    def set_schedule(self, schedule: str):
-        """"persistent" or "lockstep" for the following extend calls (the trees do not depend
-        on it)."""
-        _ffi.check(_ffi.lib().pp_batch_set_schedule(self.ctx.handle, self.SCHEDULES[schedule]))
+    def set_finish_schedule(self, rounds: bool = True, span0: int = 0, span: int = 0):
+        """How plan() runs check_finish (identical results): steer rounds with span0 / span
+        candidate edges per node in the first / later rounds (0 = default), or rounds=False:
+        check_finish_kernel alone."""
+        _ffi.check(_ffi.lib().pp_batch_set_finish_schedule(self.ctx.handle, int(bool(rounds)),
+                                                           int(span0), int(span)))
 
     def set_window(self, k: int):
         """The window for the following extend calls (a power of two <= 64); the trees do not

@@ -44,6 +44,58 @@ def test_plan_without_finish_is_strict_json():
     assert "Infinity" not in s and "NaN" not in s
 
 
+def test_default_line_fits_the_driver_tail():
+    """Rounds 3-4 printed 22-23 KB lines; the driver reads an ~8 KB stdout tail (stderr shares it)
+    and parsed none of them.  The compact line built from round 4's full default record must be
+    strict JSON of at most LINE_MAX (4 KB) and keep the contract's headline keys and every
+    sub-result's value / frac / CPU value."""
+    bench = _bench()
+    with open(os.path.join(ROOT, "profiles", "r04_final_bench_default.json")) as f:
+        full = json.load(f)
+    assert len(json.dumps(full)) > 20000  # the failure mode this guards
+    s = bench.compact_line(full, os.path.join(ROOT, "gpurun_out", "bench_detail.json"))
+    assert len(s.encode()) <= bench.LINE_MAX <= 8192
+    back = json.loads(s, parse_constant=_refuse)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert back[k] == full[k] or k == "config", k
+    assert back["roofline"]["frac"] == full["roofline"]["frac"]
+    assert {"bound", "achieved", "peak", "unit", "traffic"} <= set(back["roofline"])
+    assert back["cpu_baseline"]["value"] == full["cpu_baseline"]["value"]
+    assert back["cpu_baseline"]["cores"] == full["cpu_baseline"]["cores"]
+    assert set(back["sub"]) == set(bench.SUB_KEYS)
+    for k, v in back["sub"].items():
+        assert v["value"] == full[k]["value"], k
+        assert v["cpu"] == full[k]["cpu_baseline"]["value"], k
+    assert back["sub"]["config3"]["records_digest"] == full["config3"]["records_digest"]
+    assert back["sub"]["plan"]["same_answer"] is True
+    assert back["detail"] == "gpurun_out/bench_detail.json"
+
+
+def test_compact_line_sheds_fields_over_the_cap():
+    """A line swollen by long error texts still fits: the least important fields go first."""
+    bench = _bench()
+    line = {"metric": bench.METRIC, "value": 1.0, "config": {"workload": "w" * 3000}}
+    for k in bench.SUB_KEYS:
+        line[k] = {"error": "E" * 5000}
+    s = bench.compact_line(line)
+    assert len(s.encode()) <= bench.LINE_MAX
+    json.loads(s, parse_constant=_refuse)
+
+
+def test_single_workload_line_keeps_the_multirank_keys():
+    """test_gpu_multirank compares these keys between the 1-rank and 2-rank config-3 lines."""
+    bench = _bench()
+    with open(os.path.join(ROOT, "profiles", "r04_final_bench_config3.json")) as f:
+        full = json.load(f)
+    back = json.loads(bench.compact_line(full, None, with_subs=False), parse_constant=_refuse)
+    for k in ("n_gpus", "iterations_total", "nodes_total", "records_digest"):
+        assert back[k] == full[k], k
+    assert back["config"]["queries_per_rank"] == full["config"]["queries_per_rank"]
+    assert back["config"]["gather"] == full["config"]["gather"]
+    assert "sub" not in back
+
+
 def test_plain_dumps_would_have_failed():
     """The failure mode itself: Python's default json.dumps writes Infinity, which a strict
     parser refuses — line_json must never let that through."""

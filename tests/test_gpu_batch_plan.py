@@ -139,26 +139,23 @@ def test_batch_plan_field512_128(pkg, ctx, oracle_mod):
     _check(got, exp, checked, raw, "field512_128")
 
 
-def test_batch_plan_rounds_equal_one_kernel(pkg, ctx, monkeypatch):
+def test_batch_plan_rounds_equal_one_kernel(pkg, ctx):
     """pp_batch_plan's steer rounds (phase A / B memo fill, lane-per-item assemble, DESIGN.md
-    §3.3) against check_finish_kernel alone (PP_AMD_CF_ROUNDS=0 at context creation): the same
+    §3.3) against check_finish_kernel alone (pp_batch_set_finish_schedule rounds=0): the same
     best node, length (bit for bit), point count and finish count for every query of a
     512-query config-3 batch"""
     from pathplanning_amd import rrt, scenes
 
     raw = scenes.field512()
     starts, goals, seeds = scenes.config3_queries(raw, 0, 512)
+    b = rrt.RRTBatch(starts, goals, 2000, raw["step_size"], rrt.Space.from_raw(raw), seeds,
+                     ctx=ctx)
+    b.extend(2000)
     out = []
-    for mode in ("1", "0"):
-        monkeypatch.setenv("PP_AMD_CF_ROUNDS", mode)
-        c = pkg.Context(0)
-        try:
-            b = rrt.RRTBatch(starts, goals, 2000, raw["step_size"], rrt.Space.from_raw(raw),
-                             seeds, ctx=c)
-            b.extend(2000)
-            out.append(b.plan())
-        finally:
-            c.close()
+    for rounds in (True, False):
+        b.set_finish_schedule(rounds)
+        out.append(b.plan())
+    b.set_finish_schedule(True)
     a, k = out
     assert a["checked"] == k["checked"] > 0
     for key in ("best_node", "n_points", "n_finishes"):
@@ -169,31 +166,59 @@ def test_batch_plan_rounds_equal_one_kernel(pkg, ctx, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("span0,span", [("1", "1"), ("4", "4"), ("1", "3")])
-def test_batch_plan_span_schedules_agree(pkg, ctx, monkeypatch, span0, span):
-    """phase A's span schedule (PP_AMD_CFB_SPAN0 / PP_AMD_CFB_SPAN at context creation, DESIGN.md
-    §3.3) changes which candidates are walked together, never a result: the same best nodes,
+def test_batch_plan_span_schedules_agree(pkg, ctx, span0, span):
+    """phase A's span schedule (pp_batch_set_finish_schedule span0 / span)
+    changes which candidates are walked together, never a result: the same best nodes,
     lengths (bit for bit), point and finish counts as the default schedule on a 256-query
     config-3 batch"""
     from pathplanning_amd import rrt, scenes
 
     raw = scenes.field512()
     starts, goals, seeds = scenes.config3_queries(raw, 0, 256)
+    b = rrt.RRTBatch(starts, goals, 2000, raw["step_size"], rrt.Space.from_raw(raw), seeds,
+                     ctx=ctx)
+    b.extend(2000)
     out = []
-    for sched in ((None, None), (span0, span)):
-        for name, v in zip(("PP_AMD_CFB_SPAN0", "PP_AMD_CFB_SPAN"), sched):
-            if v is None:
-                monkeypatch.delenv(name, raising=False)
-            else:
-                monkeypatch.setenv(name, v)
-        c = pkg.Context(0)
-        try:
-            b = rrt.RRTBatch(starts, goals, 2000, raw["step_size"], rrt.Space.from_raw(raw),
-                             seeds, ctx=c)
-            b.extend(2000)
-            out.append(b.plan())
-        finally:
-            c.close()
+    for sched in ((0, 0), (int(span0), int(span))):
+        b.set_finish_schedule(True, *sched)
+        out.append(b.plan())
+    b.set_finish_schedule(True)
     a, k = out
     assert a["checked"] == k["checked"] > 0
     for key in ("best_node", "n_points", "n_finishes", "length"):
         assert np.array_equal(a[key], k[key]), key
+
+
+@pytest.mark.parametrize("rounds", [True, False])
+def test_batch_plan_none_edges_panic(pkg, ctx, rounds):
+    """A query whose start yaw is NaN makes every edge into its root a None steer; finalize panics
+    on it (rrt.rs:529).  pp_batch_plan must return PP_ERR_REFERENCE_PANIC with the steer rounds
+    (cfb_assemble's panic precedence: fnone of the goal edge, the phase-B memo, tnone_up of the
+    tree edges) and with check_finish_kernel alone — for a batch of NaN-yaw queries and for a
+    mixed batch in which the other queries' chains are ordinary (verified or rejected) — never a
+    plain rejection.  The same batch without the NaN query plans without error."""
+    from pathplanning_amd import _ffi, rrt, scenes
+
+    raw = scenes.bench6_open()
+    starts, goals, seeds = scenes.config3_queries(raw, 0, 24)
+    starts = np.array(starts, dtype=np.float64).reshape(-1, 3)
+    for nan_q in ([5], list(range(24))):
+        st = starts.copy()
+        st[nan_q, 2] = float("nan")
+        b = rrt.RRTBatch(st, goals, 300, raw["step_size"], rrt.Space.from_raw(raw), seeds,
+                         ctx=ctx)
+        b.set_finish_schedule(rounds)
+        b.extend(300)
+        n, _ = b.state()
+        assert int(n[nan_q[0]]) > 2  # the NaN query inserted nodes (straight root edges)
+        with pytest.raises(_ffi.PPError) as e:
+            b.plan()
+        assert e.value.code == _ffi.PP_ERR_REFERENCE_PANIC, nan_q
+        b.set_finish_schedule(True)
+    b = rrt.RRTBatch(starts, goals, 300, raw["step_size"], rrt.Space.from_raw(raw), seeds,
+                     ctx=ctx)
+    b.set_finish_schedule(rounds)
+    b.extend(300)
+    res = b.plan()
+    b.set_finish_schedule(True)
+    assert res["checked"] > 0 and int((res["best_node"] >= 0).sum()) > 0

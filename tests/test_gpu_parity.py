@@ -468,17 +468,16 @@ def test_batch_field512_matches_independent_oracle_runs(pkg, ctx, oracle_mod):
         _assert_same_tree(b.tree(q), exp)
 
 
-@pytest.mark.parametrize("schedule", ["lockstep", "persistent"])
-def test_batch_sub_batch_streams(pkg, ctx, oracle_mod, schedule):
-    """>= 256 queries: the lockstep schedule runs them as two sub-batches on two streams, the
-    persistent one hands them to its workgroups from a counter: spot-checked queries of both
-    halves equal their oracle runs and the batch totals equal the oracle's"""
+def test_batch_sub_batch_streams(pkg, ctx, oracle_mod):
+    """>= 256 queries: the lockstep schedule runs them as two sub-batches on two streams:
+    spot-checked queries of both halves equal their oracle runs and the batch totals equal the
+    oracle's"""
     from pathplanning_amd import rrt, scenes
 
     raw = scenes.bench6_open()
     starts, goals, seeds = scenes.config3_queries(raw, 0, 300)
     b = rrt.RRTBatch(starts, goals, 120, raw["step_size"], rrt.Space.from_raw(raw), seeds,
-                     ctx=ctx, schedule=schedule)
+                     ctx=ctx)
     it, acc = b.extend(120)
     n, its = b.state()
     assert it == 300 * 120 and (its == 120).all()
@@ -556,19 +555,19 @@ def test_grid_batch_and_verify_api(pkg, ctx, oracle_mod):
     assert ok.tolist() == exp
 
 
-@pytest.mark.parametrize("schedule,window", [("persistent", w) for w in (1, 2, 8, 16, 32, 64)] +
-                         [("lockstep", w) for w in (1, 16, 64)])
-def test_batch_windows_equal_sequential_runs(pkg, ctx, oracle_mod, schedule, window):
+@pytest.mark.parametrize("window", [1, 2, 8, 16, 32, 64])
+def test_batch_windows_equal_sequential_runs(pkg, ctx, oracle_mod, window):
     """config 3's per-query speculative windows: every query's tree equals its one-iteration-
-    at-a-time run for any window and either schedule (bench6_open accepts often, so the
-    in-order replay stops windows early; ragged step counts end mid-window)"""
+    at-a-time run for any window (bench6_open accepts often, so the in-order replay stops
+    windows early; ragged step counts end mid-window; windows 2 and 8 exercise the verdict
+    cache's slot remap with fewer steps than the window)"""
     from pathplanning_amd import rrt, scenes
 
     for raw, q0, nq, steps in ((scenes.bench6_open(), 7, 19, (37, 1, 250)),
                                (scenes.field512(), 0, 24, (300,))):
         starts, goals, seeds = scenes.config3_queries(raw, q0, nq)
         b = rrt.RRTBatch(starts, goals, 2000, raw["step_size"], rrt.Space.from_raw(raw), seeds,
-                         ctx=ctx, window=window, schedule=schedule)
+                         ctx=ctx, window=window)
         total = 0
         for s in steps:
             it, _ = b.extend(s)
@@ -579,3 +578,23 @@ def test_batch_windows_equal_sequential_runs(pkg, ctx, oracle_mod, schedule, win
         for q in range(nq):
             exp = _oracle_query(oracle_mod, raw, starts[q], seeds[q], total, 2000)
             _assert_same_tree(b.tree(q), exp)
+
+
+def test_batch_window_changes_between_extend_calls(pkg, ctx, oracle_mod):
+    """set_window between extend calls voids the verdict cache (the task region's layout
+    changes): alternating windows on one batch still builds every query's sequential tree"""
+    from pathplanning_amd import rrt, scenes
+
+    raw = scenes.bench6_open()
+    starts, goals, seeds = scenes.config3_queries(raw, 3, 21)
+    b = rrt.RRTBatch(starts, goals, 2000, raw["step_size"], rrt.Space.from_raw(raw), seeds,
+                     ctx=ctx, window=8)
+    total = 0
+    for w, s in ((8, 13), (2, 5), (64, 70), (1, 3), (16, 41), (8, 1)):
+        b.set_window(w)
+        it, _ = b.extend(s)
+        total += s
+        assert it == 21 * s
+    for q in range(21):
+        exp = _oracle_query(oracle_mod, raw, starts[q], seeds[q], total, 2000)
+        _assert_same_tree(b.tree(q), exp)

@@ -174,15 +174,13 @@ def test_star_large_tree_uncached_knn(pkg, oracle_mod, ctx):
 
 
 def test_star_split_fixed_at_new(pkg, oracle_mod, ctx, monkeypatch):
-    """the sub-batch split (PP_BATCH_STREAMS) is read at pp_star_new only: changing it before
-    pp_star_extend must not leave a sub-batch without its task count"""
+    """the sub-batch split is fixed at pp_star_new (the library reads no environment): a
+    300-query batch runs its sub-batches with their own task counts"""
     from pathplanning_amd import scenes
 
     raw = scenes.bench6_open()
     starts, _, seeds = scenes.config3_queries(raw, 0, 300)
-    monkeypatch.setenv("PP_BATCH_STREAMS", "2")
     b = _batch(pkg, raw, starts, seeds, 60, 0, 0.0, ctx=ctx)
-    monkeypatch.setenv("PP_BATCH_STREAMS", "4")
     b.extend(60)
     n, it, _, rw = b.state()
     assert (it == 60).all()
