@@ -289,6 +289,7 @@ struct pp_ctx {
         s.gx0 = gx0;
         s.gy0 = gy0;
         s.ginv = ginv;
+        s.gcell = 1.0 / ginv;
         s.gnx = gnx;
         s.gny = gny;
         s.goff = d_goff.p;

@@ -42,9 +42,13 @@ typedef __attribute__((address_space(1))) void glb_void;
 // rrt.rs:124-137, Q10).  A disc whose cull box meets the chunk's box shares a cell with it (the
 // cell index is monotone in the coordinate), so the cull is exact.  Must be called by all 64
 // lanes.  Returns true when the chunk rejects the line.
+// (the clamp in the integer domain: v_cvt_i32_f64 saturates — NaN gives 0 — so no f64 bound has
+// to stay live in the walk's registers; the same cell as clamping the double)
 __device__ inline int grid_cell(double v, double v0, double inv, int n) {
     const double f = floor((v - v0) * inv);
-    return f < 0.0 ? 0 : (f >= (double)(n - 1) ? n - 1 : (int)f);
+    int i;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(i) : "v"(f));
+    return min(max(i, 0), n - 1);
 }
 
 // Dynamic LDS of the steer kernels: the scene image (SceneDev::lds_*) when kLds.
@@ -141,7 +145,7 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const float il2f = l2f > 0.0f ? __builtin_amdgcn_rcpf(l2f) : 0.0f;
     // the chunk's bbox in f32, widened by the rounding slack: an item whose cull disc misses it
     // cannot meet any of the chunk's segments
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const float bxl = (float)bx0 - sc.cull_slack, bxh = (float)bx1 + sc.cull_slack;
     const float byl = (float)by0 - sc.cull_slack, byh = (float)by1 + sc.cull_slack;
     // up to 64 items in parallel, one per lane (kk: its index in the item list, valid: a lane with
@@ -256,7 +260,7 @@ constexpr int kSMinPts = 64;  // S segments shorter than this many points are wa
 template <bool kLds>
 __device__ int s_classify(const SceneDev& sc, double ax, double ay, double bx, double by,
                           double t_lo, double t_hi, double gap, double dl) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const double ux0 = bx - ax, uy0 = by - ay;
     const double len = sqrt(ux0 * ux0 + uy0 * uy0);
     if (!(len > 0.0)) return kSUnknown;
@@ -274,7 +278,7 @@ __device__ int s_classify(const SceneDev& sc, double ax, double ay, double bx, d
     int k0v = 0, cntv = 0;
     if (lane < ny) {
         const int gy = cy0 + lane;
-        const double cell = 1.0 / sc.ginv;
+        const double cell = sc.gcell;
         const double ylo = gy == 0 ? -__builtin_inf() : sc.gy0 + gy * cell - dl;
         const double yhi = gy == sc.gny - 1 ? __builtin_inf() : sc.gy0 + (gy + 1) * cell + dl;
         double t0 = 0.0, t1 = 1.0;
@@ -338,7 +342,7 @@ __device__ int s_classify(const SceneDev& sc, double ax, double ay, double bx, d
 // and the first one past (the segment's end, dubins.rs:243-256).  Wave-uniform results.
 __device__ inline void seg_count(double w, double dd, double Ls, double* __restrict__ gs,
                                  long long& n, double& last, double& exitv) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const double aL = fabs(Ls);
     n = 0;
     last = w;
@@ -541,7 +545,7 @@ template <bool kLds>
 __device__ __forceinline__ int steer_walk(const SceneDev& sc, const WalkIn r,
                                           bool junction = true, int* walked = nullptr,
                                           int* walked_arc = nullptr) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     if (r.state == kPrepNone) {  // polyline [(x, y), (px, py)]
         if (walked) *walked += 2;
         const bool has = lane < 2;
@@ -643,7 +647,7 @@ __device__ __forceinline__ int steer_collide_literal_body(const SceneDev& sc, do
                                                           double yaw, double px, double py,
                                                           double pyaw, double* bx, double* by,
                                                           double* byaw, bool junction) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     int n = 0, r = 0;
     if (lane == 0) {
         int word = -1;
@@ -687,7 +691,7 @@ __global__ __launch_bounds__(256) void steer_tasks_kernel(SceneDev sc, TreeDev t
                                                           int n, int* __restrict__ out_status,
                                                           double* __restrict__ out_yaw,
                                                           double* __restrict__ scratch) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     double* bx = scratch ? scratch + (size_t)gw * 3 * kLiteralCap : nullptr;
@@ -989,7 +993,7 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
             // is sorted after the screened samples, out of the screen and the pair grid (counted
             // per wave: one LDS atomic instead of one per sample on a single address)
             const uint64_t mb = __ballot(valid && bks[u]);
-            if ((threadIdx.x & 63) == 0 && mb) atomicAdd(s_nb, (int)__popcll(mb));
+            if ((__lane_id()) == 0 && mb) atomicAdd(s_nb, (int)__popcll(mb));
             if (!valid) continue;
             const double x = xs[u], y = ys[u];
             g.wsx[np][j] = x;
@@ -2102,7 +2106,7 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     // with pnode < 0 is idle; own_yaw: the child keeps its heading cyaw (RRT* rewire edges)
     const int W = st->W;
     const int total = W + st->ncomp;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = __lane_id(), wave = threadIdx.x >> 6;
     const int r = lane & (kPrepLanes - 1), g0 = lane & ~(kPrepLanes - 1);
     constexpr int TPW = 64 / kPrepLanes;  // tasks per wave in phase A
     static_assert(kPrepLanes == 8, "the per-task broadcasts are grp8_bcast (8-lane groups)");
@@ -2177,7 +2181,7 @@ template <bool kLds, int kScene = kSceneAny, bool kS = false>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
                                         const double* __restrict__ pdv, double* __restrict__ gs,
                                         int& npts, int& napts, bool junction = true) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int state = ufl(p->state);
     const double x = ufl(p->x), y = ufl(p->y), px = ufl(p->px), py = ufl(p->py);
     if (state == kPrepNone) {  // steer failed: polyline [(x, y), (px, py)] (rrt.rs:313)
@@ -2509,13 +2513,16 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
                                                          const int* __restrict__ cand_cnt,
                                                          int* __restrict__ pend,
                                                          long long* __restrict__ wg_points) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int W = st->W;
     const int total = W + st->ncomp;
     if ((int)blockIdx.x >= total) return;
+    // (the wave index as a wave-uniform value: threadIdx.x itself need not stay live)
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const bool t0 = threadIdx.x == 0;
     if (kLds) stage_scene(sc);
     double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) +
-                 (threadIdx.x >> 6) * kGenSlots;  // this wave's generator slots
+                 wv * kGenSlots;  // this wave's generator slots
     int npts = 0, napts = 0;
     // Workgroup b walks the tasks b, b + G, b + 2G, ... (G = the grid); its waves take them one
     // at a time from an LDS counter, so a wave that drew short paths takes more of them (a
@@ -2525,7 +2532,7 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
     // slower on config 5's walk.)
     __shared__ int s_next;
     const int G = (int)gridDim.x;
-    if (threadIdx.x == 0) s_next = 0;
+    if (t0) s_next = 0;
     __syncthreads();
     for (;;) {
         int k = 0;
@@ -2546,14 +2553,14 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
     if (wg_points) {  // [b]: points, [kWalkTallySlots + b]: their arc points
         __shared__ int s_np[2][kWalkThreads / 64];
         if (lane == 0) {
-            s_np[0][threadIdx.x >> 6] = npts;
-            s_np[1][threadIdx.x >> 6] = napts;
+            s_np[0][wv] = npts;
+            s_np[1][wv] = napts;
         }
         __syncthreads();
-        if (threadIdx.x < 2) {
+        if (wv == 0 && lane < 2) {
             long long sum = 0;
-            for (int w = 0; w < kWalkThreads / 64; ++w) sum += s_np[threadIdx.x][w];
-            wg_points[blockIdx.x + threadIdx.x * kWalkTallySlots] += sum;
+            for (int w = 0; w < kWalkThreads / 64; ++w) sum += s_np[lane][w];
+            wg_points[blockIdx.x + lane * kWalkTallySlots] += sum;
         }
     }
 }
@@ -2567,16 +2574,19 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
 // batch unchanged).
 // The walk instantiation for a scene: LDS image or not, and its mode (scene_kind), as a callable
 // applied to the kernel (launch or occupancy query).
+// (polygon scenes walk at most 5 waves per SIMD: their edge tests do not fit the 6-wave budget
+// without scratch)
 template <int kMinW, bool kS = false, typename F>
 inline hipError_t walk_kernel_for(const SceneDev& sc, F&& f) {
     const bool lds = sc.lds_bytes > 0;
+    constexpr int kMinWPoly = kMinW > 5 ? 5 : kMinW;
     switch (scene_kind(sc)) {
         case kSceneGrid:
             return lds ? f(steer_walk_kernel<true, kMinW, kSceneGrid, kS>)
                        : f(steer_walk_kernel<false, kMinW, kSceneGrid, kS>);
         case kScenePoly:
-            return lds ? f(steer_walk_kernel<true, kMinW, kScenePoly, kS>)
-                       : f(steer_walk_kernel<false, kMinW, kScenePoly, kS>);
+            return lds ? f(steer_walk_kernel<true, kMinWPoly, kScenePoly, kS>)
+                       : f(steer_walk_kernel<false, kMinWPoly, kScenePoly, kS>);
         default:
             return lds ? f(steer_walk_kernel<true, kMinW, kSceneDisc, kS>)
                        : f(steer_walk_kernel<false, kMinW, kSceneDisc, kS>);
@@ -3162,7 +3172,7 @@ enum : int { kCfPanic = 6 };
 // running wave that releases after its bounded literal walk.  Called by all lanes.
 __device__ __forceinline__ int lit_acquire(int* locks, int hint) {
     int slot = 0;
-    if ((threadIdx.x & 63) == 0)
+    if ((__lane_id()) == 0)
         for (int i = 0;; ++i) {
             const int sl = (hint + i) % kLiteralWaves;
             if (atomicCAS(&locks[sl], 0, 1) == 0) {
@@ -3176,7 +3186,7 @@ __device__ __forceinline__ int lit_acquire(int* locks, int hint) {
 }
 __device__ __forceinline__ void lit_release(int* locks, int slot) {
     __threadfence();
-    if ((threadIdx.x & 63) == 0) atomicExch(&locks[slot], 0);
+    if ((__lane_id()) == 0) atomicExch(&locks[slot], 0);
 }
 
 // returns the verdict | (polyline points walked << 4) | (their arc points << 34)
@@ -3192,7 +3202,7 @@ __device__ __forceinline__ void lit_release(int* locks, int slot) {
 __device__ __noinline__ void cf_prep(const SceneDev* __restrict__ scg, double ax, double ay,
                                      double ayaw, double bx, double by, double byaw,
                                      PrepRec* lrec) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     prep_task(*scg, lane & 7, lane & ~7, 0, lane < 8, true, ax, ay, bx, by, byaw, 1, ayaw, 0,
               0.0, 0.0, lrec, nullptr, nullptr);
 }
@@ -3305,7 +3315,7 @@ __device__ inline void cf_node_setup(const TreeDev& tr_in, const CfBatch& cb, in
 // A node's ancestor path root first into path[0, D) (NodeIter, rrt.rs:253-265, reversed), by the
 // calling wave (lane 0 follows the parents, then the lanes reverse it); -1 past kCfMaxDepth.
 __device__ inline int cf_path(const TreeDev& tr, int node, int* __restrict__ path) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     int d = 0;
     if (lane == 0) {
         int c = node;
@@ -3339,7 +3349,7 @@ __global__ __launch_bounds__(kCfThreads, kCfMinW) void check_finish_kernel(
     __shared__ int s_pos[kCfWaves][kCfLevels];  // the optimize chain's path positions per wave
     __shared__ PrepRec s_rec[kCfWaves];          // the wave's edge record (cf_edge_check)
     const SceneDev& sc = *scg;
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int* path = gpath + ((size_t)blockIdx.x * kCfWaves + wave) * kCfMaxDepth;  // this wave's
     double* gs = s_gs[wave];
@@ -3943,7 +3953,7 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const SceneDe
 __global__ __launch_bounds__(256) void mq_plan_items_kernel(int Q, const int* __restrict__ off,
                                                             int* __restrict__ qidx,
                                                             int* __restrict__ nodes) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     for (int q = gw; q < Q; q += nw) {
@@ -3959,7 +3969,7 @@ __global__ __launch_bounds__(256) void mq_plan_reduce_kernel(
     int Q, const int* __restrict__ off, const int* __restrict__ ok, const double* __restrict__ len,
     const int* __restrict__ npts, int* __restrict__ best_node, double* __restrict__ best_len,
     int* __restrict__ best_npts, int* __restrict__ n_fin) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     for (int q = gw; q < Q; q += nw) {
@@ -4068,7 +4078,7 @@ __global__ __launch_bounds__(256) void cfb_tnone_up_kernel(CfbArgs a) {
 // thread of the workgroup must call it.
 __device__ inline int cfb_reserve(int* counter, int cnt, int* wsum) {
     __shared__ int s_wt[4], s_base;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = __lane_id(), w = threadIdx.x >> 6;
     const int incl = wave_incl_scan(cnt);
     if (lane == 63) s_wt[w] = incl;
     __syncthreads();
@@ -4288,7 +4298,7 @@ __global__ __launch_bounds__(256) void cfb_lit_run_kernel(CfbArgs a, SceneDev sc
                                                           const int* __restrict__ list,
                                                           const int* __restrict__ count,
                                                           double* __restrict__ lit_scratch) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     double* bx = lit_scratch + (size_t)gw * 3 * kLiteralCap;
@@ -4517,7 +4527,7 @@ __global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx
                                                            double miny, double maxy,
                                                            SteerTask* __restrict__ tasks,
                                                            const SceneDev* __restrict__ scp) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     for (int q = gw; q < mq.Q; q += nw)
@@ -4547,7 +4557,7 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
     // snapshot NN (snapshot nodes have lower indices and win ties) — the window stops there and
     // the next step resumes at it; the accepted samples before it are appended in order
     // (rrt.rs:586-589).
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     const int K = mq.K, G = 64 / K;
@@ -4741,7 +4751,7 @@ __device__ __forceinline__ double star_chord_lb(double d2, double curv) {
 __global__ __launch_bounds__(256) void star_sample_kernel(StarDev sd, double minx, double maxx,
                                                           double miny, double maxy,
                                                           SteerTask* __restrict__ tasks) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // the step's round-B / round-C task counters
@@ -4807,7 +4817,7 @@ __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __
     __shared__ double s_d2[kKnnWaves][kKnnCache];
     __shared__ double s_cd[kKnnWaves][64];
     __shared__ int s_ci[kKnnWaves][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = __lane_id(), wave = threadIdx.x >> 6;
     double* cand_d = s_cd[wave];
     int* cand_i = s_ci[wave];
     const MqDev& mq = sd.mq;
@@ -4969,7 +4979,7 @@ __global__ __launch_bounds__(256) void star_knn_kernel(StarDev sd, const int* __
 __device__ __forceinline__ int star_settle(const SceneDev& sc, int st, bool act, double x, double y,
                                            double yaw, double px, double py, double pyaw,
                                            double* lit_scratch, int* locks, int hint) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     uint64_t lit = __ballot(act && st == kLiteral);
     if (!lit) return st;
     const int slot = lit_acquire(locks, hint);
@@ -4991,7 +5001,7 @@ __global__ __launch_bounds__(256) void star_insert_kernel(
     const int* __restrict__ statusB, const double* __restrict__ yawB,
     const double* __restrict__ costB, SteerTask* __restrict__ tasksC,
     StarTaskExt* __restrict__ extC, double* __restrict__ lit_scratch, int* __restrict__ err) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const MqDev& mq = sd.mq;
     const int wave = threadIdx.x >> 6;
@@ -5124,7 +5134,7 @@ __global__ __launch_bounds__(256) void star_rewire_kernel(
     StarDev sd, SceneDev sc, const SteerTask* __restrict__ tasksC,
     const StarTaskExt* __restrict__ extC, const int* __restrict__ statusC,
     const double* __restrict__ costC, double* __restrict__ lit_scratch, int* __restrict__ err) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     const MqDev& mq = sd.mq;
@@ -5433,7 +5443,7 @@ __global__ __launch_bounds__(256) void verify_lines_kernel(SceneDev sc, const do
                                                           const double* __restrict__ Y,
                                                           const int64_t* __restrict__ off, int k,
                                                           uint8_t* __restrict__ ok) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
     for (int i = gw; i < k; i += nw) {

@@ -55,6 +55,7 @@ struct SceneDev {
     // uniform grid over the discs: cell (gx, gy) = floor((v - g0) * ginv), clamped; a disc is
     // listed in every cell its cull box [c - rcull, c + rcull] touches (CSR: off, items)
     double gx0, gy0, ginv;
+    double gcell;  // 1 / ginv (the cell size; s_classify's slabs)
     int gnx, gny;
     const int* goff;    // [gnx * gny + 1]
     const int* gitems;  // disc indices

@@ -10,9 +10,9 @@ for rep in ${REPS:-1}; do
 for wl in ${WLS:-config3}; do
   for v in ${VARIANTS:-base}; do
     if [ "$v" = base ]; then
-      timeout -k 10 300 python -u bench.py --workload $wl --no-cpu-baseline $EXTRA > "$OUT/${wl}_${v}_$rep.json" 2> "$OUT/${wl}_${v}_$rep.err" || { tail -20 "$OUT/${wl}_${v}_$rep.err"; exit 1; }
+      timeout -k 10 300 python -u bench.py --workload $wl --no-cpu-baseline $EXTRA > "$OUT/${wl}_${v}_${rep}${SFX}.json" 2> "$OUT/${wl}_${v}_${rep}${SFX}.err" || { tail -20 "$OUT/${wl}_${v}_${rep}${SFX}.err"; exit 1; }
     else
-      PP_AMD_LIB="$PWD/rs-pathplanning_amd/lib/$v/libpathplanning_amd.so" timeout -k 10 300 python -u bench.py --workload $wl --no-cpu-baseline --allow-variant-lib $EXTRA > "$OUT/${wl}_${v}_$rep.json" 2> "$OUT/${wl}_${v}_$rep.err" || { tail -20 "$OUT/${wl}_${v}_$rep.err"; exit 1; }
+      PP_AMD_LIB="$PWD/rs-pathplanning_amd/lib/$v/libpathplanning_amd.so" timeout -k 10 300 python -u bench.py --workload $wl --no-cpu-baseline --allow-variant-lib $EXTRA > "$OUT/${wl}_${v}_${rep}${SFX}.json" 2> "$OUT/${wl}_${v}_${rep}${SFX}.err" || { tail -20 "$OUT/${wl}_${v}_${rep}${SFX}.err"; exit 1; }
     fi
     echo "done $wl $v $rep"
   done
