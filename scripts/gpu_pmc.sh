@@ -18,7 +18,7 @@ args() {
   esac
 }
 for wl in ${WLS:-config2 config4 config3 config5}; do
-  timeout -k 10 300 python3 "$R/bench.py" $(args $wl) > "$OUT/bench_$wl.json" 2> "$OUT/bench_$wl.err" || { tail -5 "$OUT/bench_$wl.err"; exit 1; }
+  timeout -k 10 300 python3 "$R/bench.py" $(args $wl) --detail "$OUT/detail_$wl.json" > "$OUT/bench_$wl.json" 2> "$OUT/bench_$wl.err" || { tail -5 "$OUT/bench_$wl.err"; exit 1; }
 done
 job() {  # name workload kernel-regex counters...
   local name=$1 wl=$2 k=$3; shift 3

@@ -52,7 +52,11 @@ def avg(job, kernel, last):
 
 
 def line(wl):
-    with open(os.path.join(SRC, f"bench_{wl}.json")) as f:
+    """The workload's full bench record (--detail; the stdout line is the compact one)."""
+    path = os.path.join(SRC, f"detail_{wl}.json")
+    if not os.path.exists(path):
+        path = os.path.join(SRC, f"bench_{wl}.json")
+    with open(path) as f:
         return json.load(f)
 
 
@@ -103,12 +107,14 @@ for wl, tag in (("config2", ""), ("config4", "_config4")):
     d = sq(pre + "_win", "window_kernel", r["launches"], r["evals_per_launch"], "eval")
     d.update(traffic(pre + "_win", "window_kernel", r["launches"]))
     d.update(workload=wl, evals_per_launch=r["evals_per_launch"], note=NOTE,
-             screen_cus=d.get("grid_workgroups", 249) - 1)
+             screen_cus=d.get("grid_workgroups", 249) - 1,
+             lib_sha256_16=L.get("provenance", {}).get("lib_sha256_16"))
     write(f"window_kernel_pmc{tag}.json", d)
     if w:
         d = sq(pre + "_walk", "steer_walk", w["launches"], w["points_per_launch"], "point")
         d.update(traffic(pre + "_walk", "steer_walk", w["launches"]))
-        d.update(workload=wl, points_per_launch=w["points_per_launch"], note=NOTE, cus=256)
+        d.update(workload=wl, points_per_launch=w["points_per_launch"], note=NOTE, cus=256,
+                 lib_sha256_16=L.get("provenance", {}).get("lib_sha256_16"))
         write(f"steer_walk_pmc{tag}.json", d)
 batch = {}
 for wl, pre, nn in (("config3", "c3", "mq_sample_nn"), ("config5", "c5", "star_sample")):
@@ -118,7 +124,8 @@ for wl, pre, nn in (("config3", "c3", "mq_sample_nn"), ("config5", "c5", "star_s
     w, n = L["roofline"], L["nn_roofline"]
     d = sq(pre + "_walk", "steer_walk", w["launches"], w["points_per_launch"], "point")
     d.update(traffic(pre + "_walk", "steer_walk", w["launches"]))
-    d.update(points_per_launch=w["points_per_launch"], cus=256, note=NOTE)
+    d.update(points_per_launch=w["points_per_launch"], cus=256, note=NOTE,
+             lib_sha256_16=L.get("provenance", {}).get("lib_sha256_16"))
     nl = w["launches"] // (3 if wl == "config5" else 1)  # one NN launch per step
     batch[wl] = {"steer_walk": d, "nn": dict(kernel=nn, **traffic(pre + "_nn", nn, nl))}
 if batch:

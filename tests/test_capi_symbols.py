@@ -94,3 +94,12 @@ def test_create_circle_is_the_crate_polygon(built):
                          math.sin(2.0 * math.pi / n * float(i)) * r + cy)
                         for i in range(int(n + 1.0))])
         assert got.shape == exp.shape and np.array_equal(got, exp)
+
+
+def test_integration_binding_declares_every_symbol():
+    """INTEGRATION.md's Rust extern block (the binding a maintainer adds to the crate) names
+    every entry point the header declares, and nothing the header dropped."""
+    with open(os.path.join(ROOT, "INTEGRATION.md")) as f:
+        txt = f.read()
+    bound = set(re.findall(r"pub fn (pp_[a-z0-9_]+)\s*\(", txt))
+    assert bound == set(_declared_symbols())
