@@ -89,6 +89,9 @@ struct HBuf {  // pinned host staging
 };
 
 constexpr int kMaxBatch = 64;  // windows enqueued between two host synchronisations
+// one tree: draw the next window's samples on a second stream beside the window's nn_finalize /
+// steer_prep / steer_walk (off the window chain) instead of in nn_finalize's extra workgroup
+constexpr bool kGenStream = true;
 constexpr int kInsideCells = 2048;  // the inside bitmap's cells per axis (point_blocked)
 constexpr int kScreenPad = 64;  // f32 screen copies: the LDS-DMA reads whole float4s (<= 3 floats past)
 
@@ -201,6 +204,9 @@ struct pp_ctx {
     hipStream_t sub_stream[4] = {};  // sub-batch streams 1.. (0 is `stream`), created on first use
     DBuf<SceneDev> mq_scene;      // the scene in device memory (point_blocked)
     hipEvent_t fork_ev = nullptr;
+    // one tree: the next window's samples on a stream of their own (WindowArgs::gen_stream)
+    hipStream_t gen_stream = nullptr;
+    hipEvent_t gen_fork = nullptr, gen_join = nullptr;
     std::vector<double> mq_goal;  // 3 per query (RRT::new's goal; pp_batch_plan)
     DBuf<double> mq_goal_d;       // [3Q] the goals on the device (pp_batch_plan)
     DBuf<int> mp_off, mp_qidx, mp_nodes, mp_ok, mp_npts, mp_best, mp_bpts, mp_nfin;
@@ -268,6 +274,9 @@ struct pp_ctx {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
+        if (gen_fork) (void)hipEventDestroy(gen_fork);
+        if (gen_join) (void)hipEventDestroy(gen_join);
+        if (gen_stream) (void)hipStreamDestroy(gen_stream);
         for (auto& ss : sub_stream)
             if (ss) (void)hipStreamDestroy(ss);
         if (stream) (void)hipStreamDestroy(stream);
@@ -1570,6 +1579,16 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
         WindowArgs a = ctx->window_args(ctx->d_state.p);
         a.K = K;
         a.target = target;
+        if (kGenStream) {  // the next window's samples beside each window's finalize / prep / walk
+            if (!ctx->gen_stream) {
+                PP_HIP(hipStreamCreateWithFlags(&ctx->gen_stream, hipStreamNonBlocking));
+                PP_HIP(hipEventCreateWithFlags(&ctx->gen_fork, hipEventDisableTiming));
+                PP_HIP(hipEventCreateWithFlags(&ctx->gen_join, hipEventDisableTiming));
+            }
+            a.gen_stream = ctx->gen_stream;
+            a.gen_fork = ctx->gen_fork;
+            a.gen_join = ctx->gen_join;
+        }
         if (ctx->prof && (r = ensure_events(ctx, 5 * (size_t)nw))) return r;
         const int64_t windows_before = ctx->h_state.p[0].windows;
         // windows are pipelined: window w's kernel resolves and commits w - 1; the drain launch

@@ -1492,6 +1492,19 @@ __global__ __launch_bounds__(1024) void window_samples_kernel(DevState* st, Samp
     samples_role(st, g, np, st->it_spec, smem);
 }
 
+// The samples of the window after window `seq` (parity p), into parity 1 - p, drawn beside
+// window seq's nn_finalize / steer_prep / steer_walk on the generator stream (the commit in
+// window seq's kernel already decided where they start): Space::rand_point of the iterations
+// after window seq, or — when that commit voided window seq (a truncation) — after the committed
+// window (it_spec), exactly as nn_finalize's extra workgroup draws them.
+__global__ __launch_bounds__(1024) void next_samples_kernel(DevState* st, SamplesArgs g, int p,
+                                                            int64_t seq) {
+    __shared__ __attribute__((aligned(16))) char smem[kSamplesLds];
+    const bool voided = st->void_seq == seq || st->error;
+    const int64_t start = voided ? st->it_spec : st->wsp[p] + st->Wp[p];
+    samples_role(st, g, 1 - p, start, smem);
+}
+
 // nn_finalize: kFinSamples samples per workgroup, one wave per sample.
 //  1. The wave merges the sample's screen partials (lane c: chunk c) and screens the nodes the
 //     window's screen did not cover — the ones appended since (the previous window's commit) —
@@ -5384,8 +5397,11 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     const int K = a.K;
     const int p = (int)(seq & 1);
     const WinKArgs wk = win_args(a, p, 1, resolve_prev, 1, seq);
-    if (!resolve_prev)  // the batch's first window: its samples (later: the previous window kernel)
+    const bool gs = a.gen_stream != nullptr;
+    if (!resolve_prev)  // the batch's first window: its samples (later: the previous window's draw)
         window_samples_kernel<<<1, 1024, 0, s>>>(a.st, wk.g, p);
+    else if (gs)  // this window's samples, drawn on the generator stream
+        (void)hipStreamWaitEvent(s, a.gen_join, 0);
     double* wsx = a.wsx + (size_t)p * a.Kcap;
     double* wsy = a.wsy + (size_t)p * a.Kcap;
     if (ev) (void)hipEventRecord(ev[0], s);
@@ -5394,12 +5410,18 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     window_kernel<<<1 + kScanGrid, kScanThreads, 0, s>>>(wk);
     if (resolve_prev && !kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
     if (ev) (void)hipEventRecord(ev[1], s);
-    // one workgroup past the samples' draws the next window's samples
-    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples + 1, kFinThreads, 0, s>>>(
+    if (gs) {  // the next window's samples beside this window's finalize, prep and walk
+        (void)hipEventRecord(a.gen_fork, s);
+        (void)hipStreamWaitEvent(a.gen_stream, a.gen_fork, 0);
+        next_samples_kernel<<<1, 1024, 0, a.gen_stream>>>(a.st, wk.g, p, seq);
+        (void)hipEventRecord(a.gen_join, a.gen_stream);
+    }
+    // (without the generator stream: one workgroup past the samples' draws the next window's)
+    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples + (gs ? 0 : 1), kFinThreads, 0, s>>>(
         a.st, p, seq, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, wsx, wsy, a.tr.x32, a.tr.y32,
         a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose,
         pair_grid(wk.g, p, a.eps_coord), a.cand_cnt, a.cand, a.pend, wk.sq[p], wk.g.ipos[p], wk.g,
-        1, wk.g.blk[p]);
+        gs ? 0 : 1, wk.g.blk[p]);
     if (ev) (void)hipEventRecord(ev[2], s);
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K + kPrepThreads / 8 - 1) / (kPrepThreads / 8);
@@ -5417,6 +5439,9 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
 }
 
 hipError_t launch_drain(hipStream_t s, const WindowArgs& a, int64_t seq_next) {
+    // (the last window's draw for a window that will not run: joined, so the generator stream is
+    // idle when the host reads the state)
+    if (a.gen_stream) (void)hipStreamWaitEvent(s, a.gen_join, 0);
     const WinKArgs wk = win_args(a, (int)(seq_next & 1), 1, 1, 0, seq_next);
     window_kernel<<<1, kScanThreads, 0, s>>>(wk);
     if (!kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
