@@ -89,9 +89,6 @@ struct HBuf {  // pinned host staging
 };
 
 constexpr int kMaxBatch = 64;  // windows enqueued between two host synchronisations
-// one tree: draw the next window's samples on a second stream beside the window's nn_finalize /
-// steer_prep / steer_walk (off the window chain) instead of in nn_finalize's extra workgroup
-constexpr bool kGenStream = true;
 constexpr int kInsideCells = 2048;  // the inside bitmap's cells per axis (point_blocked)
 constexpr int kScreenPad = 64;  // f32 screen copies: the LDS-DMA reads whole float4s (<= 3 floats past)
 
@@ -204,9 +201,6 @@ struct pp_ctx {
     hipStream_t sub_stream[4] = {};  // sub-batch streams 1.. (0 is `stream`), created on first use
     DBuf<SceneDev> mq_scene;      // the scene in device memory (point_blocked)
     hipEvent_t fork_ev = nullptr;
-    // one tree: the next window's samples on a stream of their own (WindowArgs::gen_stream)
-    hipStream_t gen_stream = nullptr;
-    hipEvent_t gen_fork = nullptr, gen_join = nullptr;
     std::vector<double> mq_goal;  // 3 per query (RRT::new's goal; pp_batch_plan)
     DBuf<double> mq_goal_d;       // [3Q] the goals on the device (pp_batch_plan)
     DBuf<int> mp_off, mp_qidx, mp_nodes, mp_ok, mp_npts, mp_best, mp_bpts, mp_nfin;
@@ -274,9 +268,6 @@ struct pp_ctx {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
-        if (gen_fork) (void)hipEventDestroy(gen_fork);
-        if (gen_join) (void)hipEventDestroy(gen_join);
-        if (gen_stream) (void)hipStreamDestroy(gen_stream);
         for (auto& ss : sub_stream)
             if (ss) (void)hipStreamDestroy(ss);
         if (stream) (void)hipStreamDestroy(stream);
@@ -516,7 +507,13 @@ static_assert(PP_CF_CHAIN == kCfLevels + 2, "chain row layout");
 constexpr int kCfBatch = 16384;     // nodes per check_finish launch
 constexpr int kCfPtsCap = 1 << 16;  // line points per check_finish workgroup
 static_assert(4 * kCfMaxEdges <= kCfPtsCap, "cf_line_kernel keeps 4 doubles per edge in the hypot buffer");
-constexpr int kCfLineGrid = 2048;   // the batch plan's cf_line_kernel workgroups (1.5 MB each)
+// the batch plan's cf_line_kernel workgroups: 3 x kCfPtsCap doubles of line points each
+// (1.5 MB), 3 GB for the whole grid, allocated on the first batch plan
+constexpr int kCfLineGrid = 2048;
+// phase A's task arrays (status, lists, SteerTask, StarTaskExt, PrepRec, yaw per task) are sized
+// for span x (items + queries) tasks: a span that would need more than this is clamped (the spans
+// change which candidates are walked together, never a result)
+constexpr size_t kCfbTaskBudget = (size_t)4 << 30;
 
 // check_finish for nodes[0, k) (device pointer already filled); results on the device
 // The goal of a check_finish_kernel launch: the planner's (check_finish), or a caller-built goal
@@ -616,8 +613,13 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     const int Q = c->mq_Q;
     const size_t nn = (size_t)total + Q;
     const size_t rows = (size_t)Q * (size_t)cb_in.row_cap;
-    // phase A: <= span tasks per node; B: <= 2 per node
-    const size_t cap_tasks = std::max<size_t>((size_t)std::max({c->cfb_span0, c->cfb_span, 2}) * nn, 1);
+    // phase A: <= span tasks per node; B: <= 2 per node.  The spans are clamped to the task budget
+    // (at least 2: phase B's tasks)
+    const size_t task_bytes = 3 * sizeof(int) + sizeof(SteerTask) + sizeof(StarTaskExt) +
+                              sizeof(PrepRec) + sizeof(double);
+    const int span_cap = (int)std::max<size_t>(2, kCfbTaskBudget / (task_bytes * std::max<size_t>(nn, 1)));
+    const int span0 = std::min(c->cfb_span0, span_cap), span1 = std::min(c->cfb_span, span_cap);
+    const size_t cap_tasks = std::max<size_t>((size_t)std::max({span0, span1, 2}) * nn, 1);
     hipStream_t st = c->stream;
     PP_HIP(c->cf_err.reserve(2));
     PP_HIP(c->cf_memo.reserve(2 * std::max<size_t>(rows, 1)));
@@ -706,7 +708,7 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     long long* wpts = c->prof ? c->cfb_pts.p : nullptr;
     int rounds = 0;
     for (int m0 = 0; m0 <= misc[0]; ++rounds) {
-        a.span = rounds == 0 ? c->cfb_span0 : c->cfb_span;
+        a.span = rounds == 0 ? span0 : span1;
         const int mt = (int)std::min<size_t>(cap_tasks, (size_t)a.span * nn);
         PP_HIP(launch_cfb(st, sd, a, kCfbEmitA, m0));
         PP_HIP(launch_cfb_steer(st, sd, a, mt, false, wpts));
@@ -1579,16 +1581,6 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
         WindowArgs a = ctx->window_args(ctx->d_state.p);
         a.K = K;
         a.target = target;
-        if (kGenStream) {  // the next window's samples beside each window's finalize / prep / walk
-            if (!ctx->gen_stream) {
-                PP_HIP(hipStreamCreateWithFlags(&ctx->gen_stream, hipStreamNonBlocking));
-                PP_HIP(hipEventCreateWithFlags(&ctx->gen_fork, hipEventDisableTiming));
-                PP_HIP(hipEventCreateWithFlags(&ctx->gen_join, hipEventDisableTiming));
-            }
-            a.gen_stream = ctx->gen_stream;
-            a.gen_fork = ctx->gen_fork;
-            a.gen_join = ctx->gen_join;
-        }
         if (ctx->prof && (r = ensure_events(ctx, 5 * (size_t)nw))) return r;
         const int64_t windows_before = ctx->h_state.p[0].windows;
         // windows are pipelined: window w's kernel resolves and commits w - 1; the drain launch

@@ -48,10 +48,6 @@ struct WindowArgs {
     long long* wg_points = nullptr;  // profiling: walked points per walk workgroup (or null)
     const SceneDev* scp = nullptr;  // the scene in device memory (samples_role's point_blocked)
     unsigned char* blk = nullptr;   // [2 * Kcap] sample in an obstacle (null: no pre-test)
-    // the next window's samples on a stream of their own (kGenStream): forked after each window
-    // kernel, joined before the next one (null: drawn by nn_finalize's extra workgroup)
-    hipStream_t gen_stream = nullptr;
-    hipEvent_t gen_fork = nullptr, gen_join = nullptr;
 };
 
 // Enqueue window number `seq` on stream s: its window kernel also resolves and commits window

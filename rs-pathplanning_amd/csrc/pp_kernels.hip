@@ -1226,6 +1226,8 @@ __device__ __attribute__((noinline)) void screen_block_global(const float* __res
     }
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <bool kExp>
 __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& a, int b,
                                                                char* smem) {
@@ -1371,12 +1373,31 @@ __device__ __attribute__((always_inline)) inline void scan_role(const WinKArgs& 
                     pw[4 * v] = aw.x, pw[4 * v + 1] = aw.y, pw[4 * v + 2] = aw.z, pw[4 * v + 3] = aw.w;
                 }
                 float bm[kQPL];
+                if (kExp) {
+                    // two nodes per packed FMA (v_pk_fma_f32: each half the exactly rounded
+                    // fmaf of the scalar form, so the winner re-evaluation below stays
+                    // bit-identical), the pair's minimum folded in by one v_min3
 #pragma unroll
-                for (int u = 0; u < kScanBlk; ++u) {
+                    for (int u = 0; u < kScanBlk; u += 2) {
+                        const f32x2 PX = {px[u], px[u + 1]}, PY = {py[u], py[u + 1]};
+                        const f32x2 PW = {pw[u], pw[u + 1]};
 #pragma unroll
-                    for (int r = 0; r < kQPL; ++r) {
-                        const float d = val(r, px[u], py[u], pw[u]);
-                        bm[r] = u == 0 ? d : __builtin_fminf(bm[r], d);
+                        for (int r = 0; r < kQPL; ++r) {
+                            const f32x2 QX = {qxr[r], qxr[r]}, QY = {qyr[r], qyr[r]};
+                            const f32x2 d = __builtin_elementwise_fma(
+                                QX, PX, __builtin_elementwise_fma(QY, PY, PW));
+                            const float m = __builtin_fminf(d.x, d.y);
+                            bm[r] = u == 0 ? m : __builtin_fminf(bm[r], m);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < kScanBlk; ++u) {
+#pragma unroll
+                        for (int r = 0; r < kQPL; ++r) {
+                            const float d = val(r, px[u], py[u], pw[u]);
+                            bm[r] = u == 0 ? d : __builtin_fminf(bm[r], d);
+                        }
                     }
                 }
                 const int k = c0 + r0 + u0;
@@ -1492,18 +1513,6 @@ __global__ __launch_bounds__(1024) void window_samples_kernel(DevState* st, Samp
     samples_role(st, g, np, st->it_spec, smem);
 }
 
-// The samples of the window after window `seq` (parity p), into parity 1 - p, drawn beside
-// window seq's nn_finalize / steer_prep / steer_walk on the generator stream (the commit in
-// window seq's kernel already decided where they start): Space::rand_point of the iterations
-// after window seq, or — when that commit voided window seq (a truncation) — after the committed
-// window (it_spec), exactly as nn_finalize's extra workgroup draws them.
-__global__ __launch_bounds__(1024) void next_samples_kernel(DevState* st, SamplesArgs g, int p,
-                                                            int64_t seq) {
-    __shared__ __attribute__((aligned(16))) char smem[kSamplesLds];
-    const bool voided = st->void_seq == seq || st->error;
-    const int64_t start = voided ? st->it_spec : st->wsp[p] + st->Wp[p];
-    samples_role(st, g, 1 - p, start, smem);
-}
 
 // nn_finalize: kFinSamples samples per workgroup, one wave per sample.
 //  1. The wave merges the sample's screen partials (lane c: chunk c) and screens the nodes the
@@ -5397,11 +5406,8 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     const int K = a.K;
     const int p = (int)(seq & 1);
     const WinKArgs wk = win_args(a, p, 1, resolve_prev, 1, seq);
-    const bool gs = a.gen_stream != nullptr;
     if (!resolve_prev)  // the batch's first window: its samples (later: the previous window's draw)
         window_samples_kernel<<<1, 1024, 0, s>>>(a.st, wk.g, p);
-    else if (gs)  // this window's samples, drawn on the generator stream
-        (void)hipStreamWaitEvent(s, a.gen_join, 0);
     double* wsx = a.wsx + (size_t)p * a.Kcap;
     double* wsy = a.wsy + (size_t)p * a.Kcap;
     if (ev) (void)hipEventRecord(ev[0], s);
@@ -5410,18 +5416,12 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     window_kernel<<<1 + kScanGrid, kScanThreads, 0, s>>>(wk);
     if (resolve_prev && !kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
     if (ev) (void)hipEventRecord(ev[1], s);
-    if (gs) {  // the next window's samples beside this window's finalize, prep and walk
-        (void)hipEventRecord(a.gen_fork, s);
-        (void)hipStreamWaitEvent(a.gen_stream, a.gen_fork, 0);
-        next_samples_kernel<<<1, 1024, 0, a.gen_stream>>>(a.st, wk.g, p, seq);
-        (void)hipEventRecord(a.gen_join, a.gen_stream);
-    }
-    // (without the generator stream: one workgroup past the samples' draws the next window's)
-    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples + (gs ? 0 : 1), kFinThreads, 0, s>>>(
+    // one workgroup past the samples' draws the next window's samples
+    nn_finalize_kernel<<<(K + kFinSamples - 1) / kFinSamples + 1, kFinThreads, 0, s>>>(
         a.st, p, seq, wk.chunks, a.pbest, a.psecond, a.pidx, a.Kcap, wsx, wsy, a.tr.x32, a.tr.y32,
         a.tr.x, a.tr.y, a.tr.yaw, a.eps_coord, a.nn_idx, a.nn_d2, a.snap_pose,
         pair_grid(wk.g, p, a.eps_coord), a.cand_cnt, a.cand, a.pend, wk.sq[p], wk.g.ipos[p], wk.g,
-        gs ? 0 : 1, wk.g.blk[p]);
+        1, wk.g.blk[p]);
     if (ev) (void)hipEventRecord(ev[2], s);
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K + kPrepThreads / 8 - 1) / (kPrepThreads / 8);
@@ -5439,9 +5439,6 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
 }
 
 hipError_t launch_drain(hipStream_t s, const WindowArgs& a, int64_t seq_next) {
-    // (the last window's draw for a window that will not run: joined, so the generator stream is
-    // idle when the host reads the state)
-    if (a.gen_stream) (void)hipStreamWaitEvent(s, a.gen_join, 0);
     const WinKArgs wk = win_args(a, (int)(seq_next & 1), 1, 1, 0, seq_next);
     window_kernel<<<1, kScanThreads, 0, s>>>(wk);
     if (!kWinRepair) resolve_tail_kernel<<<1, kResolveThreads, 0, s>>>(wk);
