@@ -4677,7 +4677,10 @@ hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int
     return hipGetLastError();
 }
 
-constexpr int kBigStepTasks = 32768;  // tasks per step from which the batch walk runs at 6 waves
+// tasks per step (per sub-batch) from which the batch walk runs at 6 waves per SIMD: with its
+// spill down to 20 B (round 5) the 1024-query shard's 16k-task sub-batch steps gain too
+// (276.8 -> 283.0 M it/s, gpurun_out/r05occ; 3 workgroups per CU instead of 2: no gain)
+constexpr int kBigStepTasks = 16384;
 
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int Q = a.mq.Q;
@@ -4698,10 +4701,9 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
                                                               nullptr, nullptr, a.rec, a.pdbuf,
                                                               a.yaw, a.tasks);
         if (ev) (void)hipEventRecord(ev[2], s);
-        // with the analytic straight segments (s_classify).  A large step is throughput-bound
-        // and walks at 6 waves per SIMD (80 VGPRs); a small shard's step is latency-bound and
-        // walks at 5 (96 VGPRs, the spill 60 -> 12 B per lane): the 1024-query shard 271 ->
-        // 277 M it/s, the 8192-query batch 634 -> 618 M if it did the same (one box)
+        // with the analytic straight segments (s_classify).  Steps of >= kBigStepTasks tasks
+        // walk at 6 waves per SIMD (80 VGPRs, 20 B of spill), smaller ones at 5 (96 VGPRs, no
+        // spill); the 8192-query batch at 5 waves: 641 -> 623 M it/s (round 5, one box)
         if (T >= kBigStepTasks)
             launch_walk<kWalkMinWBatch, true>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf, nullptr,
                                               a.status, nullptr, nullptr, a.wg_points);
