@@ -1541,6 +1541,8 @@ struct PairGrid {
     const int* perm;     // sorted position -> sample
     const int* cofs;     // [257] first sorted position of each cell
     const float2* sxy;   // sorted position -> (x, y) f32
+    const double* ssx;   // sorted position -> x, y f64 (the samples' own coordinates, bit for bit)
+    const double* ssy;
     double minx, miny, fx, fy;  // samples_role's binning: cell = (v - v0) * f, clamped to 0..15
     float slack;         // f32 prefilter margin for the coordinates' magnitude
 };
@@ -1815,12 +1817,16 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
                 for (int cx = cx0; cx <= cx1; ++cx) {
                     const int m = morton16(cx, cy);
                     const int a1 = pg.cofs[m + 1];
+                    // (the cells list only the screened samples, none in an obstacle; a
+                    // candidate's index and f64 coordinates are read by sorted position, beside
+                    // its f32 prefilter, not through perm)
                     for (int pos = pg.cofs[m] + lane; pos < a1; pos += 64) {
                         const float2 v = pg.sxy[pos];
-                        if (!(scan_d2(xjf, yjf, v.x, v.y) <= thr)) continue;
                         const int ii = pg.perm[pos];
-                        if (ii >= j || (blk && blk[ii])) continue;
-                        const double dx = xj - qx[ii], dy = yj - qy[ii];
+                        const double sx = pg.ssx[pos], sy = pg.ssy[pos];
+                        if (!(scan_d2(xjf, yjf, v.x, v.y) <= thr)) continue;
+                        if (ii >= j) continue;
+                        const double dx = xj - sx, dy = yj - sy;
                         const double d2 = dx * dx + dy * dy;
                         if (d2 < D2) {  // strictly nearer than the snapshot NN (which wins ties)
                             const int at = atomicAdd(&s_pc[wave], 1);
@@ -5347,6 +5353,8 @@ PairGrid pair_grid(const SamplesArgs& g, int p, double eps_coord) {
     r.perm = g.perm[p];
     r.cofs = g.cofs[p];
     r.sxy = g.sxy[p];
+    r.ssx = g.ssx[p];
+    r.ssy = g.ssy[p];
     r.minx = g.minx;
     r.miny = g.miny;
     r.fx = 16.0 / (g.maxx - g.minx);  // samples_role's factors, bit for bit
