@@ -3234,15 +3234,19 @@ __device__ __noinline__ void cf_prep(const SceneDev* __restrict__ scg, double ax
     prep_task(*scg, lane & 7, lane & ~7, 0, lane < 8, true, ax, ay, bx, by, byaw, 1, ayaw, 0,
               0.0, 0.0, lrec, nullptr, nullptr);
 }
-__device__ __noinline__ int cf_walk(const SceneDev* __restrict__ scg, const PrepRec* lrec,
-                                    double* gs, bool junction, int& walked, int& walked_arc) {
+// (the walked point tallies go to the wave's LDS slot `tally`: reference out-parameters would
+// live in the caller's stack frame, i.e. scratch)
+__device__ __forceinline__ int cf_walk(const SceneDev* __restrict__ scg, const PrepRec* lrec,
+                                    double* gs, bool junction, int* tally) {
     int w = 0, wa = 0;
     const int st = walk_rec<false, kSceneAny, true>(*scg, lrec, nullptr, gs, w, wa, junction);
-    walked = w;
-    walked_arc = wa;
+    if (__lane_id() == 0) {
+        tally[0] = w;
+        tally[1] = wa;
+    }
     return st;
 }
-__device__ __noinline__ long long cf_edge_check(const SceneDev* __restrict__ scg, double ax,
+__device__ __forceinline__ long long cf_edge_check(const SceneDev* __restrict__ scg, double ax,
                                                 double ay, double ayaw, double bx, double by,
                                                 double byaw, int flags, double* lit_scratch,
                                                 int* lit_locks, double* gs, PrepRec* lrec) {
@@ -3251,8 +3255,11 @@ __device__ __noinline__ long long cf_edge_check(const SceneDev* __restrict__ scg
     cf_prep(scg, ax, ay, ayaw, bx, by, byaw, lrec);
     __builtin_amdgcn_wave_barrier();
     if (!allow_none && ufl(lrec->state) == kPrepNone) return kCfPanic;
-    int walked = 0, walked_arc = 0;
-    int st = cf_walk(scg, lrec, gs, junction, walked, walked_arc);
+    // (lrec's fb_seg / cnt[0] are dead once the walk started: its tallies come back there)
+    int* tally = &lrec->cnt[0];
+    int st = cf_walk(scg, lrec, gs, junction, tally);
+    __builtin_amdgcn_wave_barrier();
+    const long long walked = ufl(tally[0]), walked_arc = ufl(tally[1]);
     if (st == kLiteral) {  // (measure-zero) a scratch buffer from the pool, for this edge only
         const int slot = lit_acquire(lit_locks, (int)blockIdx.x);
         double* sx = lit_scratch + (size_t)slot * 3 * kLiteralCap;
@@ -3260,7 +3267,7 @@ __device__ __noinline__ long long cf_edge_check(const SceneDev* __restrict__ scg
                                    sx + 2 * kLiteralCap, junction);
         lit_release(lit_locks, slot);
     }
-    return (long long)st | ((long long)walked << 4) | ((long long)walked_arc << 34);
+    return (long long)st | (walked << 4) | (walked_arc << 34);
 }
 
 // compute_yaw out of line: check_finish_kernel's own body is bookkeeping, and an inlined ocml
