@@ -336,6 +336,124 @@ __device__ int s_classify(const SceneDev& sc, double ax, double ay, double bx, d
     return res;
 }
 
+// Squared distance of the closed segments a-b and e0-e1: 0 when they cross properly, else the
+// nearest endpoint-to-segment distance (the seg_hits_edge predicate as a distance).
+__device__ __forceinline__ double seg_seg_d2(double ax, double ay, double bx, double by,
+                                             double e0x, double e0y, double e1x, double e1y) {
+    const double d1 = (e1x - e0x) * (ay - e0y) - (e1y - e0y) * (ax - e0x);
+    const double d2 = (e1x - e0x) * (by - e0y) - (e1y - e0y) * (bx - e0x);
+    const double d3 = (bx - ax) * (e0y - ay) - (by - ay) * (e0x - ax);
+    const double d4 = (bx - ax) * (e1y - ay) - (by - ay) * (e1x - ax);
+    if (((d1 > 0.0 && d2 < 0.0) || (d1 < 0.0 && d2 > 0.0)) &&
+        ((d3 > 0.0 && d4 < 0.0) || (d3 < 0.0 && d4 > 0.0)))
+        return 0.0;
+    return fmin(fmin(seg_point_d2(e0x, e0y, e1x, e1y, ax, ay), seg_point_d2(e0x, e0y, e1x, e1y, bx, by)),
+                fmin(seg_point_d2(ax, ay, bx, by, e0x, e0y), seg_point_d2(ax, ay, bx, by, e1x, e1y)));
+}
+
+// s_classify for polygon scenes (Q10p, round 5).  The S points lie within dl of AB and the
+// polyline through them stays within dl of AB (the dl-neighbourhood of a segment is convex), and
+// covers AB's stretch [t_lo, t_hi] continuously (its points advance monotonically along u).  So:
+//   kSClear    A, B dl inside the rectangle; every bounds-ring edge farther than h + dl from AB
+//              and A inside the ring (then every S point is inside and farther than h from the
+//              ring: in_poly_bounds holds); every obstacle edge farther than h + dl from AB (no
+//              polyline segment between S points comes within h: seg_hits_edge is false);
+//   kSHit      some obstacle edge comes within h - 3 dl of the stretch [t_lo, t_hi]: the polyline
+//              segment spanning the nearest point passes within h - 2 dl, so seg_hits_edge holds
+//              for it and verify rejects (rrt.rs:124-137) whatever the other segments;
+//   kSUnknown  otherwise.  (The bounds ring tests points only, so it never gives a sure hit.)
+// The edges come from the item grid exactly as s_classify's discs: an edge within h + dl of AB
+// has a point of its cull box (its h-neighbourhood) within dl of AB.  Wave-uniform result.
+template <bool kLds>
+__device__ int s_classify_poly(const SceneDev& sc, double ax, double ay, double bx, double by,
+                               double t_lo, double t_hi, double dl) {
+    const int lane = __lane_id();
+    const double ux0 = bx - ax, uy0 = by - ay;
+    const double len = sqrt(ux0 * ux0 + uy0 * uy0);
+    if (!(len > 0.0)) return kSUnknown;
+    const double ux = ux0 / len, uy = uy0 / len;
+    int res = (fmin(ax, bx) >= sc.minx + dl && fmax(ax, bx) <= sc.maxx - dl &&
+               fmin(ay, by) >= sc.miny + dl && fmax(ay, by) <= sc.maxy - dl)
+                  ? kSClear
+                  : kSUnknown;
+    const double h = sqrt(sc.h2);
+    const double ro = h + dl, ri = h - 3.0 * dl;
+    if (res == kSClear && sc.nbv > 0) {
+        // the ring, lane-parallel: clearance from every edge and A's crossing parity
+        bool near = false;
+        int par = 0;
+        for (int i0 = 0; i0 < sc.nbv; i0 += 64) {
+            const int i = i0 + lane;
+            bool cr = false;
+            if (i < sc.nbv) {
+                const int j = i + 1 == sc.nbv ? 0 : i + 1;
+                const double xi = sc.bvx[i], yi = sc.bvy[i], xj = sc.bvx[j], yj = sc.bvy[j];
+                near = near || seg_seg_d2(ax, ay, bx, by, xi, yi, xj, yj) <= ro * ro;
+                cr = ray_crosses(ax, ay, xi, yi, xj, yj);
+            }
+            par ^= __popcll(__ballot(cr)) & 1;
+        }
+        if (__any(near) || !par) res = kSUnknown;
+    }
+    if (sc.ne == 0) return res;
+    const bool stretch = t_hi > t_lo && ri > 0.0;
+    const double sax = ax + t_lo * ux, say = ay + t_lo * uy;
+    const double sbx = ax + t_hi * ux, sby = ay + t_hi * uy;
+    const int cy0 = __builtin_amdgcn_readfirstlane(grid_cell(fmin(ay, by) - dl, sc.gy0, sc.ginv, sc.gny));
+    const int cy1 = __builtin_amdgcn_readfirstlane(grid_cell(fmax(ay, by) + dl, sc.gy0, sc.ginv, sc.gny));
+    const int ny = cy1 - cy0 + 1;
+    if (ny > 64) return kSUnknown;
+    const int* goff = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_goff) : sc.goff;
+    const int* items = kLds ? reinterpret_cast<const int*>(pp_smem + sc.lds_items) : sc.gitems;
+    int k0v = 0, cntv = 0;
+    if (lane < ny) {
+        const int gy = cy0 + lane;
+        const double cell = sc.gcell;
+        const double ylo = gy == 0 ? -__builtin_inf() : sc.gy0 + gy * cell - dl;
+        const double yhi = gy == sc.gny - 1 ? __builtin_inf() : sc.gy0 + (gy + 1) * cell + dl;
+        double t0 = 0.0, t1 = 1.0;
+        if (uy0 != 0.0) {
+            double ta = (ylo - ay) / uy0, tb = (yhi - ay) / uy0;
+            if (ta > tb) {
+                const double tt = ta;
+                ta = tb;
+                tb = tt;
+            }
+            t0 = fmax(t0, ta);
+            t1 = fmin(t1, tb);
+        } else if (!(ay >= ylo && ay <= yhi)) {
+            t1 = -1.0;
+        }
+        if (t0 <= t1) {
+            const double xa = ax + t0 * ux0, xb = ax + t1 * ux0;
+            const int ca = grid_cell(fmin(xa, xb) - dl, sc.gx0, sc.ginv, sc.gnx);
+            const int cb = grid_cell(fmax(xa, xb) + dl, sc.gx0, sc.ginv, sc.gnx);
+            k0v = goff[gy * sc.gnx + ca];
+            cntv = goff[gy * sc.gnx + cb + 1] - k0v;
+        }
+    }
+    for (int mb = 0;; mb += 64) {
+        const int m = mb + lane;
+        int kk = -1, run = 0;
+        for (int r = 0; r < ny; ++r) {
+            const int b = __builtin_amdgcn_readlane(k0v, r), n = __builtin_amdgcn_readlane(cntv, r);
+            if (m >= run && m < run + n) kk = b + (m - run);
+            run += n;
+        }
+        bool near = false, hit = false;
+        if (kk >= 0) {
+            const int e = items[kk];
+            const double e0x = sc.ex0[e], e0y = sc.ey0[e], e1x = sc.ex1[e], e1y = sc.ey1[e];
+            near = seg_seg_d2(ax, ay, bx, by, e0x, e0y, e1x, e1y) <= ro * ro;
+            hit = near && stretch && seg_seg_d2(sax, say, sbx, sby, e0x, e0y, e1x, e1y) < ri * ri;
+        }
+        if (__any(hit)) return kSHit;
+        if (__any(near)) res = kSUnknown;
+        if (mb + 64 >= run) break;
+    }
+    return res;
+}
+
 // Count-only run of the `pd += d` generator over one segment from its first value w (the same
 // passes as walk_rec's generator, every lane a value: the closed form inside a binade, else the
 // serial chain through the wave's LDS slots gs): n values with |pd| <= |Ls|, the last of them
@@ -684,40 +802,6 @@ __device__ int steer_collide_literal(const SceneDev& sc, double x, double y, dou
     return steer_collide_literal_body<false>(sc, x, y, yaw, px, py, pyaw, bx, by, byaw, junction);
 }
 
-// Explicit tasks (the verify_node API); waves <= kLiteralWaves so each wave owns one literal
-// scratch buffer.
-__global__ __launch_bounds__(256) void steer_tasks_kernel(SceneDev sc, TreeDev tr,
-                                                          const SteerTask* __restrict__ tasks,
-                                                          int n, int* __restrict__ out_status,
-                                                          double* __restrict__ out_yaw,
-                                                          double* __restrict__ scratch) {
-    const int lane = __lane_id();
-    const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    double* bx = scratch ? scratch + (size_t)gw * 3 * kLiteralCap : nullptr;
-    for (int t = gw; t < n; t += nw) {
-        const SteerTask tk = tasks[t];
-        double px = tk.px, py = tk.py, pyaw = tk.pyaw;
-        if (tk.pnode >= 0) {
-            px = tr.x[tk.pnode];
-            py = tr.y[tk.pnode];
-            pyaw = tr.yaw[tk.pnode];
-        }
-        const double yaw = atan2(py - tk.y, px - tk.x);
-        int s;
-        if (tk.literal && bx)
-            s = steer_collide_literal(sc, tk.x, tk.y, yaw, px, py, pyaw, bx, bx + kLiteralCap,
-                                      bx + 2 * kLiteralCap);
-        else if (tk.literal)
-            s = kError;
-        else
-            s = steer_collide_fast<false>(sc, tk.x, tk.y, yaw, px, py, pyaw);
-        if (lane == 0) {
-            out_status[t] = s;
-            out_yaw[t] = yaw;
-        }
-    }
-}
 
 // --------------------------------------------------------------------------------- dubins
 
@@ -2247,7 +2331,8 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     static_assert(kPdCap % 63 == 0, "stored points end on a chunk boundary");
     double carry_x = x, carry_y = y;
     npts += 1;  // point 0, the child
-    // a long S segment against the discs, analytically (s_classify): a sure hit rejects at once,
+    // a long S segment against the discs (s_classify) or the polygon edges and bounds ring
+    // (s_classify_poly), analytically: a sure hit rejects at once,
     // a sure clearance keeps only its first and last point (s_state 1: counted, s_emit of them
     // placed in lanes so far)
     bool s_clear = false;
@@ -2259,16 +2344,21 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                        (kScene == kSceneDisc ||
                         (kScene == kSceneAny && !sc.bits && sc.ne == 0 && sc.nbv == 0)) &&
                        sc.m > 0;
-    if (discs && partial && ng == 0 && m1 == kModeS && L1 >= kSMinPts * step) {
+    const bool polys = kS && !trim1 &&
+                       (kScene == kScenePoly ||
+                        (kScene == kSceneAny && !sc.bits && (sc.ne > 0 || sc.nbv > 0)));
+    if ((discs || polys) && partial && ng == 0 && m1 == kModeS && L1 >= kSMinPts * step) {
         const double ax = cw * ox1 + sw * oy1 + x, ay = -sw * ox1 + cw * oy1 + y;
         const double pcb = div_by(L1, c, rc);
         const double lxb = ox1 + pcb * ca1, lyb = oy1 + pcb * sa1;
         const double bx = cw * lxb + sw * lyb + x, by = -sw * lxb + cw * lyb + y;
         const double dl = 1.0e-9 * (1.0 + fabs(ax) + fabs(ay) + fabs(bx) + fabs(by));
         const double sp = step * rc;  // the S points' spacing along AB
-        const int cls = s_classify<kLds>(sc, ax, ay, bx, by, 3.0 * sp * (1.0 + 1.0e-9) + dl,
-                                         (L1 - step) * rc * (1.0 - 1.0e-9) - dl,
-                                         sp * (1.0 + 1.0e-9) + 2.0 * dl, dl);
+        const double t_lo = 3.0 * sp * (1.0 + 1.0e-9) + dl;
+        const double t_hi = (L1 - step) * rc * (1.0 - 1.0e-9) - dl;
+        const int cls = polys ? s_classify_poly<kLds>(sc, ax, ay, bx, by, t_lo, t_hi, dl)
+                              : s_classify<kLds>(sc, ax, ay, bx, by, t_lo, t_hi,
+                                                 sp * (1.0 + 1.0e-9) + 2.0 * dl, dl);
         if (cls == kSHit) return kReject;
         s_clear = cls == kSClear;
     }
@@ -2466,7 +2556,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
 // initial state, no stored grid points), walked by walk_rec — the lane-parallel exact `pd`
 // generator instead of the serial one of steer_walk.  junction = false: the polyline ends at the
 // edge's last point (finalize's edge into the root).  gs: this wave's kGenSlots LDS doubles.
-template <bool kLds>
+template <bool kLds, bool kS = false>
 __device__ __forceinline__ int walk_edge(const SceneDev& sc, const SteerPrep& r, double* gs,
                                          bool junction, int& npts, int& napts) {
     if (r.state != kPrepWalk && r.state != kPrepNone) return r.state;
@@ -2508,12 +2598,53 @@ __device__ __forceinline__ int walk_edge(const SceneDev& sc, const SteerPrep& r,
     p.fb_seg = 0;
     p.trim1 = 0;
     p.yaw = p.pyaw = 0.0;
-    return walk_rec<kLds>(sc, &p, nullptr, gs, npts, napts, junction);
+    return walk_rec<kLds, kSceneAny, kS>(sc, &p, nullptr, gs, npts, napts, junction);
 }
 
 // steer_walk, one task per wave (persistent grid, grid-stride over the W + ncomp tasks); kLds:
 // the scene's disc grid is staged into this workgroup's LDS first.
 constexpr int kGenSlots = kGenPts + 3 * kSegRow;  // per-wave LDS doubles of walk_rec
+
+// Explicit tasks (the verify_node API); waves <= kLiteralWaves so each wave owns one literal
+// scratch buffer.  The fast path is the product's walk (walk_rec through walk_edge, with the
+// analytic S segments), so the API's verdicts test the same code the planners run.
+__global__ __launch_bounds__(256) void steer_tasks_kernel(SceneDev sc, TreeDev tr,
+                                                          const SteerTask* __restrict__ tasks,
+                                                          int n, int* __restrict__ out_status,
+                                                          double* __restrict__ out_yaw,
+                                                          double* __restrict__ scratch) {
+    const int lane = __lane_id();
+    const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    double* bx = scratch ? scratch + (size_t)gw * 3 * kLiteralCap : nullptr;
+    __shared__ double s_gen[4][kGenSlots];
+    double* gs = s_gen[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))];
+    int np = 0, na = 0;
+    for (int t = gw; t < n; t += nw) {
+        const SteerTask tk = tasks[t];
+        double px = tk.px, py = tk.py, pyaw = tk.pyaw;
+        if (tk.pnode >= 0) {
+            px = tr.x[tk.pnode];
+            py = tr.y[tk.pnode];
+            pyaw = tr.yaw[tk.pnode];
+        }
+        const double yaw = atan2(py - tk.y, px - tk.x);
+        int s;
+        if (tk.literal && bx)
+            s = steer_collide_literal(sc, tk.x, tk.y, yaw, px, py, pyaw, bx, bx + kLiteralCap,
+                                      bx + 2 * kLiteralCap);
+        else if (tk.literal)
+            s = kError;
+        else
+            s = walk_edge<false, true>(sc, steer_prep(sc, tk.x, tk.y, yaw, px, py, pyaw), gs, true,
+                                       np, na);
+        if (lane == 0) {
+            out_status[t] = s;
+            out_yaw[t] = yaw;
+        }
+    }
+}
+
 constexpr int kWalkMaxWG = 768;  // 3 resident workgroups per CU
 __host__ __device__ inline int walk_lds_bytes(int scene_bytes) {
     return scene_bytes + kWalkThreads / 64 * kGenSlots * 8;
@@ -2603,11 +2734,12 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
 // The walk instantiation for a scene: LDS image or not, and its mode (scene_kind), as a callable
 // applied to the kernel (launch or occupancy query).
 // (polygon scenes walk at most 5 waves per SIMD: their edge tests do not fit the 6-wave budget
-// without scratch)
+// without scratch; with the analytic S segments at most 4: s_classify_poly spills ~80 B at 5)
 template <int kMinW, bool kS = false, typename F>
 inline hipError_t walk_kernel_for(const SceneDev& sc, F&& f) {
     const bool lds = sc.lds_bytes > 0;
-    constexpr int kMinWPoly = kMinW > 5 ? 5 : kMinW;
+    constexpr int kPolyCap = kS ? 4 : 5;
+    constexpr int kMinWPoly = kMinW > kPolyCap ? kPolyCap : kMinW;
     switch (scene_kind(sc)) {
         case kSceneGrid:
             return lds ? f(steer_walk_kernel<true, kMinW, kSceneGrid, kS>)
