@@ -86,9 +86,13 @@ __host__ __device__ inline int scene_kind(const SceneDev& sc) {
     return kSceneDisc;
 }
 
+// box: the lane's point bounds the chunk's item search (default: every lane with a point; the
+// walk leaves out lane 0 when its segment 0 -> 1 is an analytically cleared S chord, which is not
+// tested, so the box need not cover it)
 template <bool kLds, int kScene = kSceneAny>
 __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool check_bounds,
-                                              bool seg_valid, double qx, double qy) {
+                                              bool seg_valid, double qx, double qy,
+                                              bool box = true) {
     bool oob =
         check_bounds && !(qx >= sc.minx && qx <= sc.maxx && qy >= sc.miny && qy <= sc.maxy);
     if (__any(oob)) return true;
@@ -114,10 +118,11 @@ __device__ __forceinline__ bool chunk_rejects(const SceneDev& sc, bool has, bool
     const double ax = shfl_up1_f64(qx);
     const double ay = shfl_up1_f64(qy);
     const float inff = __builtin_inff();
-    const float bx0 = wave_min_f32(has ? f32_below(qx) : inff);
-    const float bx1 = wave_max_f32(has ? f32_above(qx) : -inff);
-    const float by0 = wave_min_f32(has ? f32_below(qy) : inff);
-    const float by1 = wave_max_f32(has ? f32_above(qy) : -inff);
+    const bool inb = has && box;
+    const float bx0 = wave_min_f32(inb ? f32_below(qx) : inff);
+    const float bx1 = wave_max_f32(inb ? f32_above(qx) : -inff);
+    const float by0 = wave_min_f32(inb ? f32_below(qy) : inff);
+    const float by1 = wave_max_f32(inb ? f32_above(qy) : -inff);
     const int cx0 = __builtin_amdgcn_readfirstlane(grid_cell(bx0, sc.gx0, sc.ginv, sc.gnx));
     const int cx1 = __builtin_amdgcn_readfirstlane(grid_cell(bx1, sc.gx0, sc.ginv, sc.gnx));
     const int cy0 = __builtin_amdgcn_readfirstlane(grid_cell(by0, sc.gy0, sc.ginv, sc.gny));
@@ -2366,6 +2371,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         int cnt = 0, my_seg = 0;
         double my_pd = 0.0;
         bool done;
+        bool chord = false;  // lane 1 holds the cleared S segment's last point, lane 0 its first
         const bool gen = partial && base >= ng;
         if (gen) {
             // lane-parallel `pd += d` (dubins.rs:239-255): lane l >= pos replays l - pos
@@ -2382,17 +2388,23 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                         s_first = gpd;
                         s_state = 1;
                     }
+                    // The chord between the two lies within rounding of AB, so it clears and is
+                    // not tested: the chunk ends after the first point, and the next one starts
+                    // with the chord (lanes 0 -> 1), its box without lane 0 — so the long chord
+                    // neither widens a chunk's item search nor meets the exact tests
                     const int n_emit = s_n >= 2 ? 2 : (int)s_n;
                     while (s_emit < n_emit && pos <= 63) {
+                        if (s_emit == 1 && pos > 1) break;
                         if (lane == pos) {
                             my_seg = 1;
                             my_pd = s_emit == 0 ? s_first : s_last;
                         }
+                        if (s_emit == 1) chord = true;
                         ++s_emit;
                         ++pos;
                         ++cnt;
                     }
-                    if (s_emit < n_emit) break;  // the chunk is full: the next one goes on
+                    if (s_emit < n_emit) break;  // the chunk ends: the next one goes on
                     grid += s_n - n_emit;
                     npts += s_n - n_emit;
                     const double ll = L1 - s_exit - gdd;
@@ -2541,10 +2553,13 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         const bool chk = isgrid || isj || (base == 0 && lane == 0);
         npts += cnt + (junction && junction_here ? 1 : 0);
         napts += __popcll(__ballot(isgrid && mm != kModeS));
-        if (chunk_rejects<kLds, kScene>(sc, has, chk, has && lane >= 1, qx, qy)) return kReject;
+        if (chunk_rejects<kLds, kScene>(sc, has, chk, has && lane >= 1 && !(chord && lane == 1),
+                                        qx, qy, !(chord && lane == 0)))
+            return kReject;
         if (junction_here) break;
-        carry_x = readlane_f64(qx, 63);
-        carry_y = readlane_f64(qy, 63);
+        // (the last point: lane 63, or lane cnt of a chunk ended before the chord)
+        carry_x = readlane_f64(qx, cnt);
+        carry_y = readlane_f64(qy, cnt);
     }
     // no trailing zero left for the trim (dubins.rs:281-288): the literal path decides
     if (partial && 1 + grid > (long long)ufl((double)p->n_point) - 2) return kLiteral;
