@@ -2768,7 +2768,8 @@ inline hipError_t walk_kernel_for(const SceneDev& sc, F&& f) {
     }
 }
 
-template <int kMinW = kWalkMinWWindow, int kMaxPerCU = 4>
+// (kS: the instantiation that is launched — the S classes change a polygon walk's budget)
+template <int kMinW = kWalkMinWWindow, int kMaxPerCU = 4, bool kS = false>
 inline int walk_grid_cap(const SceneDev& sc) {
     static std::mutex mu;
     static std::map<std::tuple<int, int, int>, int> cache;
@@ -2782,7 +2783,7 @@ inline int walk_grid_cap(const SceneDev& sc) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
         cus = prop.multiProcessorCount;
-    const hipError_t e = walk_kernel_for<kMinW>(sc, [&](auto kern) {
+    const hipError_t e = walk_kernel_for<kMinW, kS>(sc, [&](auto kern) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kWalkThreads,
                                                             walk_lds_bytes(sc.lds_bytes));
     });
@@ -4611,7 +4612,7 @@ hipError_t launch_cfb_steer(hipStream_t s, const SceneDev& sc, const CfbArgs& a,
                                                   a.rec, nullptr, a.yaw, a.tasks, nullptr,
                                                   own_yaw ? a.ext : nullptr);
     const int wb = std::min(std::max(1, (max_tasks + kWalkThreads / 64 - 1) / (kWalkThreads / 64)),
-                            std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch>(sc)));
+                            std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch, 4, true>(sc)));
     launch_walk<kWalkMinWBatch, true>(s, wb, a.st, sc, a.rec, nullptr, nullptr, a.status, nullptr,
                                       nullptr, wg_points);
     return hipGetLastError();
@@ -4848,7 +4849,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int nn_blocks = std::min((Q + 3) / 4, 4096);  // one wave per query
     const int prep_blocks = std::min((T + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
-                                     std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch, 2>(a.sc)));
+                                     std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch, 2, true>(a.sc)));
     const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
 
     for (int k = 0; k < steps; ++k) {
@@ -5418,11 +5419,11 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
     const int prepA = std::min((Q + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int prepB = std::min((TB + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walkA = std::min((Q + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
-                               std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWStar>(a.sc)));
+                               std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWStar, 4, true>(a.sc)));
     const int lds = a.sc.lds_bytes;
     // a scene read from global memory (no LDS image) makes the walk latency-bound: fill every
     // wave slot the walk's 48 VGPRs allow (4 workgroups of 8 waves per CU)
-    const int walk_cap = lds > 0 ? std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWStar>(a.sc)) : 1024;
+    const int walk_cap = lds > 0 ? std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWStar, 4, true>(a.sc)) : 1024;
     const int walkB = std::min((TB + kWalkThreads / 64 - 1) / (kWalkThreads / 64), walk_cap);
     // ev (profiling): 8 per step — around star_sample, then around each round's walk
     auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, const StarTaskExt* ext,
