@@ -3786,6 +3786,7 @@ __device__ int line_edge_wave(double sx, double sy, double syaw, const double* _
                               int cap, int lane, int* n_out) {
     // the word (dubins.rs:333-363) as cf_npoint_steer chose it for this edge: {word, t, p, q}
     const double c = 1.0 / turn_radius;
+    const double rc = 1.0 / c;
     Steer s;
     s.word = (int)word[0];
     s.t = word[1];
@@ -3844,21 +3845,41 @@ __device__ int line_edge_wave(double sx, double sy, double syaw, const double* _
         ind = base - 1;               // (dubins.rs:227: ind -= 1)
         for (;;) {
             double my = 0.0, w = pd;
-            for (int u = 0; u < 64; ++u) {
-                if (lane == u) my = w;
-                w += d;
+            // walk_rec's closed form first: while the values keep pd's sign and exponent,
+            // fl(w + d) = w + delta exactly (delta = w1 - pd, when the first two steps agree), so
+            // lane k's value is one exact fma; checked over every value up to the first one past
+            // |l| (the one the segment end needs).  Otherwise the serial chain.
+            const double w1 = pd + d, w2 = w1 + d;
+            bool cf = (w1 - pd) == (w2 - w1);
+            if (cf) {
+                const double vc = __builtin_fma((double)lane, w1 - pd, pd);
+                const uint64_t fm = __ballot(!(fabs(vc) <= al));
+                const int fl = fm ? (int)__builtin_ctzll(fm) : 63;
+                cf = __ballot(lane <= fl && (__double2hiint(vc) >> 20) != (__double2hiint(pd) >> 20)) == 0;
+                if (cf) {
+                    my = vc;
+                    w = readlane_f64(vc, 63) + d;
+                }
+            }
+            if (!cf) {
+                for (int u = 0; u < 64; ++u) {
+                    if (lane == u) my = w;
+                    w += d;
+                }
             }
             const uint64_t bad = __ballot(!(fabs(my) <= al));
             const int cnt = bad ? (int)__builtin_ctzll(bad) : 64;
             if (cnt > 0 && base + cnt - 1 >= n_point) return kSteerOverflow;
             if (lane < cnt) {
+                // (x / c as div_by: the correctly rounded quotient, bit-identical to the division)
                 double lx, ly;
                 if (m == kModeS) {
-                    lx = o.x + my / c * co;
-                    ly = o.y + my / c * so;
+                    lx = o.x + div_by(my, c, rc) * co;
+                    ly = o.y + div_by(my, c, rc) * so;
                 } else {
-                    const double ldx = sin(my) / c;
-                    const double ldy = m == kModeL ? (1.0 - cos(my)) / c : (1.0 - cos(my)) / -c;
+                    const double ldx = div_by(sin(my), c, rc);
+                    const double l1 = div_by(1.0 - cos(my), c, rc);
+                    const double ldy = m == kModeL ? l1 : -l1;
                     lx = o.x + (cmo * ldx + smo * ldy);
                     ly = o.y + (-smo * ldx + cmo * ldy);
                 }
