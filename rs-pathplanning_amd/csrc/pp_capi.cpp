@@ -184,7 +184,7 @@ struct pp_ctx {
     int64_t mq_max_iter = 0;
     double mq_step = 0.1;
     DBuf<double> mq_x, mq_y, mq_yaw, mq_yawbuf, mq_pdbuf;
-    DBuf<int> mq_par, mq_n, mq_status, mq_err;
+    DBuf<int> mq_par, mq_n, mq_status, mq_err, mq_alist;
     DBuf<int64_t> mq_it, mq_evals;
     DBuf<int64_t> mq_itprev;  // the lockstep NN's verdict cache (MqDev::it_prev)
     DBuf<uint64_t> mq_seed;
@@ -195,7 +195,7 @@ struct pp_ctx {
     int mq_nsub = 1;              // sub-batches of the current batch (fixed at pp_batch_new)
     DBuf<int64_t> mq_target;      // [Q] iteration targets of the running pp_batch_extend
     DBuf<double> mq_nnd2;         // [Q * kMqMaxK]
-    DBuf<SteerTask> mq_tasks;
+    DBuf<SteerTask> mq_tasks, mq_ctask;
     DBuf<PrepRec> mq_rec;
     DBuf<DevState> mq_state;      // [3]: the whole batch, then one per sub-batch (mq_sub_args)
     hipStream_t sub_stream[4] = {};  // sub-batch streams 1.. (0 is `stream`), created on first use
@@ -789,6 +789,9 @@ MqArgs mq_args(pp_ctx* c) {
     a.mq.nnd2 = c->mq_nnd2.p;
     a.mq.it_prev = c->mq_itprev.p;
     a.mq.status = c->mq_status.p;
+    a.mq.alist = c->mq_alist.p;
+    a.mq.ctask = c->mq_ctask.p;
+    a.mq.tyaw = c->mq_yawbuf.p;
     a.sc = c->scene_dev();
     a.sc.step_size = c->mq_step;
     a.st = c->mq_state.p;
@@ -802,6 +805,7 @@ MqArgs mq_args(pp_ctx* c) {
     a.err = c->mq_err.p;
     a.wg_points = c->prof_points();
     a.scp = c->mq_scene.p;  // (uploaded by pp_batch_extend)
+    a.mq.st = a.st;
     return a;
 }
 
@@ -836,7 +840,11 @@ MqArgs mq_sub_args(pp_ctx* c, int sub, int nsub) {
     a.mq.nnd2 += t0;
     if (a.mq.it_prev) a.mq.it_prev += q0;
     if (a.mq.status) a.mq.status += t0;
+    if (a.mq.alist) a.mq.alist += t0;
+    if (a.mq.ctask) a.mq.ctask += t0;
+    if (a.mq.tyaw) a.mq.tyaw += t0;
     a.st = c->mq_state.p + 1 + sub;
+    a.mq.st = a.st;
     a.tasks += t0;
     a.rec += t0;
     a.pdbuf += t0 * kPdCap;
@@ -849,9 +857,11 @@ MqArgs mq_sub_args(pp_ctx* c, int sub, int nsub) {
 int mq_write_states(pp_ctx* c, hipStream_t st) {
     DevState ds[1 + kMaxSub] = {};
     const int Q = c->mq_Q, nsub = c->mq_nsub;
-    ds[0].W = Q * c->mq_K;
+    // W counts the step's active tasks (mq_sample_nn lists them, the insert resets it): 0 here;
+    // each state's list is its task region's part of mq_alist
+    ds[0].alist = c->mq_alist.p;
     for (int s = 0; s < nsub; ++s)
-        ds[1 + s].W = (int)((int64_t)Q * (s + 1) / nsub - (int64_t)Q * s / nsub) * c->mq_K;
+        ds[1 + s].alist = c->mq_alist.p + (size_t)((int64_t)Q * s / nsub) * c->mq_K;
     PP_HIP(hipMemcpyAsync(c->mq_state.p, ds, sizeof ds, hipMemcpyHostToDevice, st));
     PP_HIP(hipStreamSynchronize(st));  // ds lives on this stack frame
     return PP_OK;
@@ -861,11 +871,13 @@ int mq_write_states(pp_ctx* c, hipStream_t st) {
 int mq_reserve_tasks(pp_ctx* c, int q, int K) {
     const size_t tq = (size_t)q * K;
     PP_HIP(c->mq_tasks.reserve(tq));
+    PP_HIP(c->mq_ctask.reserve(tq));
     PP_HIP(c->mq_status.reserve(tq));
     PP_HIP(c->mq_yawbuf.reserve(tq));
     PP_HIP(c->mq_rec.reserve(tq));
     PP_HIP(c->mq_pdbuf.reserve(tq * kPdCap));
     PP_HIP(c->mq_nnd2.reserve(tq));
+    PP_HIP(c->mq_alist.reserve(tq));
     return PP_OK;
 }
 

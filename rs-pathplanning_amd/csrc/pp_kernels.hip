@@ -2228,16 +2228,21 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     constexpr int TPW = 64 / kPrepLanes;  // tasks per wave in phase A
     static_assert(kPrepLanes == 8, "the per-task broadcasts are grp8_bcast (8-lane groups)");
     constexpr int TPB = kPrepThreads / 64 * TPW;  // tasks per workgroup
+    const int* __restrict__ al = st->alist;  // (the batch's active-task list)
     for (int blk = blockIdx.x; blk * TPB < total; blk += gridDim.x) {
-        const int t = blk * TPB + wave * TPW + lane / kPrepLanes;
+        const int ti = blk * TPB + wave * TPW + lane / kPrepLanes;
+        const bool valid = ti < total;
+        // t: the slot (the yaw's); list mode reads the compacted task and writes the record at ti
+        const int t = (al && valid) ? al[ti] : ti;
+        const int ri = al ? ti : t;
         // (window mode: a sample in an obstacle needs no steer — a kReject record)
-        bool act = t < total && !(blk_in && t < W && blk_in[t]);
+        bool act = valid && !(blk_in && t < W && blk_in[t]);
         int j = 0, own = 0, cull = 0;
         double x = 0.0, y = 0.0, px = 1.0, py = 0.0, pyaw = 0.0, cyaw = 0.0;
         double cbase = 0.0, climit = 0.0;
         int force = -1;
         if (act && tasks) {
-            const SteerTask tk = tasks[t];
+            const SteerTask tk = tasks[ri];
             act = tk.pnode >= 0;
             if (tk.literal >= 2) force = tk.literal - 2;  // (a cached verdict, mq_sample_nn)
             x = tk.x;
@@ -2259,8 +2264,8 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
             y = wsy[j];
         }
         double* yaw_dst = nullptr;
-        if (t < total) yaw_dst = (t < W || tasks) ? snap_yaw + t : &cand[t - W].yaw;
-        prep_task(sc, r, g0, t, t < total, act, x, y, px, py, pyaw, own, cyaw, cull, cbase, climit,
+        if (valid) yaw_dst = (t < W || tasks) ? snap_yaw + t : &cand[t - W].yaw;
+        prep_task(sc, r, g0, ri, valid, act, x, y, px, py, pyaw, own, cyaw, cull, cbase, climit,
                   rec, yaw_dst, cost_out, force);
     }
 }
@@ -2707,15 +2712,18 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
     __shared__ int s_next;
     const int G = (int)gridDim.x;
     if (t0) s_next = 0;
+    const int* __restrict__ al = st->alist;  // (the batch's active-task list)
     __syncthreads();
     for (;;) {
         int k = 0;
         if (lane == 0) k = atomicAdd(&s_next, 1);
-        const int t = (int)blockIdx.x + G * __builtin_amdgcn_readlane(k, 0);
-        if (t >= total) break;
-        const int s = walk_rec<kLds, kScene, kS>(sc, rec + t, pdbuf + (size_t)t * kPdCap, gs, npts, napts);
+        const int ti = (int)blockIdx.x + G * __builtin_amdgcn_readlane(k, 0);
+        if (ti >= total) break;
+        // (list mode: the record is at ti; the slot t only addresses the verdict's store)
+        const int t = al ? al[ti] : ti;
+        const int s = walk_rec<kLds, kScene, kS>(sc, rec + ti, pdbuf + (size_t)ti * kPdCap, gs, npts, napts);
         if (lane == 0) {
-            if (t < W) {
+            if (al || t < W) {
                 snap_status[t] = s;
                 if (pend && s != kAccept && s != kReject && cand_cnt[t] == 0)
                     pend[atomicAdd(&st->npend, 1)] = t;
@@ -4655,9 +4663,10 @@ hipError_t launch_cfb_steer(hipStream_t s, const SceneDev& sc, const CfbArgs& a,
 // Q7), the obstacle pre-test, the exact nearest node of tree q as the step found it (rrt.rs:378-391,
 // Q9: lanes stride the rows, lowest index on ties), the verdict cache; the task into
 // tasks[q K + k].
-__device__ __forceinline__ void mq_nn_query(const MqDev& mq, double minx, double maxx, double miny,
+__device__ __forceinline__ bool mq_nn_query(const MqDev& mq, double minx, double maxx, double miny,
                                             double maxy, SteerTask* __restrict__ tasks,
-                                            const SceneDev* __restrict__ scp, int q, int lane) {
+                                            const SceneDev* __restrict__ scp, int q, int lane,
+                                            SteerTask& tko) {
     const int K = mq.K, G = 64 / K;
     const int k = lane & (K - 1), g = lane / K;
     const int64_t it = mq.it[q] + k;
@@ -4667,12 +4676,14 @@ __device__ __forceinline__ void mq_nn_query(const MqDev& mq, double minx, double
     // started Tp iterations before this one, so iteration it sat in old slot k + Tp; its
     // parent and verdict are read before any lane overwrites the region
     int opn = -1, ost = -1;
+    double oyw = 0.0;
     if (mq.it_prev && g == 0) {
         const int64_t Tp = mq.it[q] - mq.it_prev[q];
         if (Tp >= 0 && Tp < K && k + Tp < K) {
             const int to = q * K + k + (int)Tp;
             opn = tasks[to].pnode;
             ost = mq.status[to];
+            if (mq.tyaw) oyw = mq.tyaw[to];
         }
     }
     double x = 0.0, y = 0.0;
@@ -4705,8 +4716,9 @@ __device__ __forceinline__ void mq_nn_query(const MqDev& mq, double minx, double
         else
             argmin_pair(bd, bi, __shfl_xor(bd, m), __shfl_xor(bi, m));
     }
+    bool need = false;  // the slot needs steer_prep + steer_walk
+    const int t = q * K + k;
     if (g == 0) {
-        const int t = q * K + k;
         if (!live) {
             tasks[t].pnode = -1;
         } else if (blocked) {
@@ -4715,27 +4727,73 @@ __device__ __forceinline__ void mq_nn_query(const MqDev& mq, double minx, double
             tasks[t].x = x;
             tasks[t].y = y;
             tasks[t].pnode = -2;
+            if (mq.alist) mq.status[t] = kReject;
         } else {
             // the same child (the counter RNG redraws it) and the same parent pose (rows are
             // never rewritten) as a task the previous step walked: its verdict (kReject 0 /
-            // kAccept 1, as 2 + verdict) rides along and steer_prep writes it as decided
+            // kAccept 1, as 2 + verdict) — settled here with the old slot's yaw (the same
+            // compute_yaw of the same poses) when the batch lists its active tasks, else
+            // steer_prep writes it as decided
             const int cached = (opn == bi && (ost == kAccept || ost == kReject)) ? 2 + ost : 0;
-            tasks[t] = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, cached};
+            tko = SteerTask{x, y, X[bi], Y[bi], mq.yaw[row + bi], bi, cached};
+            tasks[t] = tko;
             mq.nnd2[t] = bd;
+            if (mq.alist && cached) {
+                mq.status[t] = cached - 2;
+                mq.tyaw[t] = oyw;
+            } else {
+                need = true;
+            }
         }
     }
     if (mq.it_prev && lane == 0) mq.it_prev[q] = mq.it[q];
+    return need;
 }
 
-__global__ __launch_bounds__(256) void mq_sample_nn_kernel(MqDev mq, double minx, double maxx,
-                                                           double miny, double maxy,
-                                                           SteerTask* __restrict__ tasks,
-                                                           const SceneDev* __restrict__ scp) {
+// The listed tasks take one reservation per workgroup (its waves' counts summed in LDS): one
+// atomic per query on the batch's one counter serialised the 8192-query step (642 -> 612 M
+// it/s).  NT: 1024 threads (16 queries) for large sub-batches, 256 for small ones, whose
+// workgroups would otherwise crowd onto a few CUs (a 512-query sub-batch: 32 workgroups).
+template <int NT>
+__global__ __launch_bounds__(NT) void mq_sample_nn_kernel(MqDev mq, double minx,
+                                                                    double maxx, double miny,
+                                                                    double maxy,
+                                                                    SteerTask* __restrict__ tasks,
+                                                                    const SceneDev* __restrict__ scp) {
+    constexpr int kMqNnWaves = NT / 64;
+    __shared__ int s_cnt[kMqNnWaves];
+    __shared__ int s_base;
     const int lane = __lane_id();
-    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-    for (int q = gw; q < mq.Q; q += nw)
-        mq_nn_query(mq, minx, maxx, miny, maxy, tasks, scp, q, lane);
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    // (every wave of the workgroup makes the same trips: the barriers below)
+    for (int qb = (int)blockIdx.x * kMqNnWaves; qb < mq.Q; qb += (int)gridDim.x * kMqNnWaves) {
+        const int q = qb + wave;
+        SteerTask tk{};
+        const bool need =
+            q < mq.Q && mq_nn_query(mq, minx, maxx, miny, maxy, tasks, scp, q, lane, tk);
+        if (mq.alist) {
+            const uint64_t nm = __ballot(need);
+            if (lane == 0) s_cnt[wave] = __popcll(nm);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                int tot = 0;
+                for (int w = 0; w < kMqNnWaves; ++w) {
+                    const int c = s_cnt[w];
+                    s_cnt[w] = tot;
+                    tot += c;
+                }
+                s_base = tot ? atomicAdd(&mq.st->W, tot) : 0;
+            }
+            __syncthreads();
+            if (need) {
+                const int i = s_base + s_cnt[wave] + __popcll(nm & ((1ull << lane) - 1ull));
+                mq.alist[i] = q * mq.K + lane;  // (need: lane = slot k, node group 0)
+                tk.literal = 0;
+                mq.ctask[i] = tk;
+            }
+            __syncthreads();  // (s_cnt / s_base: the next trip)
+        }
+    }
 }
 
 // the iteration targets of one pp_batch_extend call: n_steps more iterations, at most max_iter
@@ -4764,6 +4822,8 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
     const int lane = __lane_id();
     const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+    // the step's steer kernels are done: the next step's mq_sample_nn lists afresh
+    if (mq.alist && gw == 0 && lane == 0) mq.st->W = 0;
     const int K = mq.K, G = 64 / K;
     const int g = lane / K, k = lane - g * K, g0 = g * K;
     const uint64_t gmask = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << g0;
@@ -4867,7 +4927,10 @@ constexpr int kBigStepTasks = 16384;
 hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int Q = a.mq.Q;
     const int T = Q * a.mq.K;  // tasks per step
-    const int nn_blocks = std::min((Q + 3) / 4, 4096);  // one wave per query
+    // one wave per query: 16 per workgroup from 2048 queries (a sub-batch of the full batch), 4 below
+    const bool big_nn = Q >= 2048;
+    const int nn_waves = big_nn ? 16 : 4;
+    const int nn_blocks = std::min((Q + nn_waves - 1) / nn_waves, 4096);
     const int prep_blocks = std::min((T + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
     const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
                                      std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch, 2, true>(a.sc)));
@@ -4876,12 +4939,17 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     for (int k = 0; k < steps; ++k) {
         hipEvent_t* ev = a.ev ? a.ev + 5 * k : nullptr;
         if (ev) (void)hipEventRecord(ev[0], s);
-        mq_sample_nn_kernel<<<nn_blocks, 256, 0, s>>>(a.mq, a.sc.minx, a.sc.maxx, a.sc.miny,
-                                                      a.sc.maxy, a.tasks, a.scp);
+        if (big_nn)
+            mq_sample_nn_kernel<1024><<<nn_blocks, 1024, 0, s>>>(a.mq, a.sc.minx, a.sc.maxx,
+                                                                a.sc.miny, a.sc.maxy, a.tasks, a.scp);
+        else
+            mq_sample_nn_kernel<256><<<nn_blocks, 256, 0, s>>>(a.mq, a.sc.minx, a.sc.maxx,
+                                                              a.sc.miny, a.sc.maxy, a.tasks, a.scp);
         if (ev) (void)hipEventRecord(ev[1], s);
+        // (the listed tasks, compacted by mq_sample_nn)
         steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, nullptr, nullptr,
                                                               nullptr, nullptr, a.rec, a.pdbuf,
-                                                              a.yaw, a.tasks);
+                                                              a.yaw, a.mq.alist ? a.mq.ctask : a.tasks);
         if (ev) (void)hipEventRecord(ev[2], s);
         // with the analytic straight segments (s_classify).  Steps of >= kBigStepTasks tasks
         // walk at 6 waves per SIMD (80 VGPRs, 20 B of spill), smaller ones at 5 (96 VGPRs, no

@@ -137,6 +137,10 @@ struct DevState {
     int64_t iterations, accepted, windows, truncations, repair_rounds, repairs, literal_repairs,
         nn_flagged, node_evals;
     int64_t blocked;  // samples in an obstacle (point_blocked): rejected without steer or pair list
+    // the query batch's active-task list (round 5): steer_prep / steer_walk run over i < W with the
+    // compacted task i (its record and pd slots at i) and store its yaw / verdict at slot
+    // alist[i]; null: task i is slot i (the window pipeline, RRT*, the steer rounds)
+    const int* alist;
 };
 
 // An explicit steer task: child (x, y) steered toward its parent — tree node `pnode` when
@@ -218,7 +222,14 @@ struct MqDev {
     // now in the task region (the previous step's), so a window that starts T iterations later
     // finds iteration it + k in old slot k + T; null: no cache (RRT* rows)
     int64_t* it_prev = nullptr;
-    const int* status = nullptr;  // the previous step's verdicts (the task region's)
+    int* status = nullptr;  // the previous step's verdicts (the task region's)
+    // active-task compaction (round 5): mq_sample_nn settles the blocked and cached slots itself
+    // (status, and tyaw = the cached task's yaw) and lists the slots that need a steer in
+    // alist[0, st->W); the insert resets st->W.  null: every slot goes through the steer
+    int* alist = nullptr;
+    SteerTask* ctask = nullptr;  // the listed tasks, compacted (ctask[i] = tasks[alist[i]])
+    DevState* st = nullptr;
+    double* tyaw = nullptr;
 };
 // RRT* batch (BASELINE config 5; build-defined, oracle/pp_oracle.c orc_star_extend, DESIGN.md
 // §3.7): Q independent RRT* trees in the MqDev rows (K = 1), one iteration per query and step in
