@@ -2020,18 +2020,16 @@ int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
         PP_HIP(ctx->mq_blocked.reserve(q));
         PP_HIP(hipMemcpy(ctx->mq_blocked.p, blk.data(), q, hipMemcpyHostToDevice));
     }
-    // default window: 32 for at most 2048 queries (a 1024-query shard: 176M it/s at 32 against
-    // 171M at 16 and 145M at 64, two streams); else 16 iterations per query and step while that
-    // stays under 131072 tasks (the
-    // throughput saturates there on one GPU; longer windows are cut more often by their own
-    // accepted samples — config 3 measured 219M it/s at K = 16 on the 8192-query batch and on a
-    // 1024-query shard 143M at K = 16 against 111M at K = 64)
+    // default window: 32 iterations per query and step while that stays within 262144 tasks.
+    // With the active-task list (round 5) a cut window's re-drawn slots cost neither a prep nor a
+    // walk, and longer windows pay on the full batch too: 8192 queries 684 M it/s at K = 16
+    // against 712 M at 32; the 1024-query shard 274 M at 16, 339 M at 32 and 64
+    // (gpurun_out/r05kw; rounds 1-4 measured 16 best for the full batch without the list)
     if (ctx->mq_K_user > 0) {
         ctx->mq_K = ctx->mq_K_user;
     } else {
-        int K = 1;
-        while (K < kMqAutoK && (int64_t)q * (K * 2) <= 131072) K *= 2;
-        if (q <= 2048) K = 32;  // a small batch (a rank's shard) needs longer windows to fill the GPU
+        int K = kMqAutoK;
+        while (K > 1 && (int64_t)q * K > 262144) K >>= 1;
         ctx->mq_K = K;
     }
     if ((r = mq_reserve_tasks(ctx, q, ctx->mq_K))) return r;

@@ -264,7 +264,7 @@ struct StarDev {
 };
 
 constexpr int kMqMaxK = 64;  // window limit per query (config 3's strong-scaling parallelism)
-constexpr int kMqAutoK = 16; // the automatic window's limit
+constexpr int kMqAutoK = 32; // the automatic window (halved while Q * K > 262144 tasks)
 
 // Resolve scratch (global, one window; indexed by pending slot / list position).
 struct ResolveScratch {
