@@ -743,13 +743,10 @@ def cpu_baseline_batch_plan(raw, starts, goals, seeds, max_iter, seconds, best, 
 
 
 def auto_batch_window(q):
-    """pp_batch_new's automatic window: 32 for at most 2048 queries, else the largest power of
-    two <= 16 with q * K <= 131072."""
-    if q <= 2048:
-        return 32
-    k = 1
-    while k < 16 and q * k * 2 <= 131072:
-        k *= 2
+    """pp_batch_new's automatic window (round 5): 32, halved while q * K > 262144 tasks."""
+    k = 32
+    while k > 1 and q * k > 262144:
+        k //= 2
     return k
 
 
