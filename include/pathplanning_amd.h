@@ -30,8 +30,10 @@ extern "C" {
  * 4: the persistent batch kernel and pp_batch_set_schedule removed (slower than the lockstep
  *    schedule on every workload measured: DESIGN.md §3.4); its pp_stats counters are reserved
  *    (always 0, the layout kept); pp_batch_set_finish_schedule replaces the library's former
- *    environment knobs */
-#define PP_ABI_VERSION 4
+ *    environment knobs
+ * 5: pp_rrt_extend_samples and pp_rrt_tree_import (the host owns the RNG and the tree); nothing
+ *    else changed */
+#define PP_ABI_VERSION 5
 
 #define PP_OK 0
 #define PP_ERR_INVALID_ARGUMENT (-1)
@@ -190,6 +192,26 @@ int pp_rrt_set_window(pp_ctx* ctx, int k);
 /* n_iter iterations of plan_one's extend (rrt.rs:583-589: rand_point, get_nearest_node,
  * Node::new, verify_node, insert) with the sequential semantics of one rayon thread. */
 int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted);
+/* plan_one's extend (rrt.rs:583-589) over k CALLER-DRAWN samples: iteration it + i takes
+ * (sx[i], sy[i]) as its Space::rand_point (rrt.rs:139-146, 406-412) instead of the seeded stream,
+ * so a host that owns its RNG drives the same speculative GPU windows (SURVEY.md §8(b)'s
+ * pp_extend_batch).  Sequential semantics: sample i sees the tree after samples < i; accepted
+ * samples are inserted in order (rrt.rs:586-589).  Per sample (each output may be NULL):
+ * nearest[i] = get_nearest_node (rrt.rs:378-391) of the tree as it stood, i.e. the parent
+ * Node::new took; yaw[i] = that node's compute_yaw (rrt.rs:169-175, 267-271); ok[i] = 1 when
+ * verify_node (rrt.rs:414-426) accepted and the node was inserted (it then has index
+ * n_before + the number of ok samples before i).  *n_accepted (may be NULL) = the inserts.
+ * Samples must be finite; the iteration counter advances by k.  With samples drawn as
+ * pp_gen_range(seed, 2 it, ..), pp_gen_range(seed, 2 it + 1, ..) the tree equals pp_rrt_extend's. */
+int pp_rrt_extend_samples(pp_ctx* ctx, const double* sx, const double* sy, int64_t k,
+                          int32_t* nearest, double* yaw, uint8_t* ok, int64_t* n_accepted);
+/* replace the planner's tree by n host-owned nodes (root first, as pp_rrt_tree_export returns
+ * them: Node x, y, yaw (rrt.rs:161-166) and parent, -1 for node 0, otherwise an earlier node:
+ * the crate's insertion order, rrt.rs:586-589).  The scene, goal, step size, seed, iteration
+ * counter and statistics stay; later extends continue from this tree.  Export -> import -> extend
+ * equals extend on the original. */
+int pp_rrt_tree_import(pp_ctx* ctx, const double* x, const double* y, const double* yaw,
+                       const int32_t* parent, int64_t n);
 /* one plan_one extend (rrt.rs:583-589); *accepted = 1 when the node was inserted */
 int pp_rrt_plan_one(pp_ctx* ctx, int32_t* accepted);
 int pp_rrt_tree_size(pp_ctx* ctx, int64_t* n);
@@ -252,9 +274,10 @@ int pp_rrt_plan(pp_ctx* ctx, int64_t n_iter, int32_t* best_node, double* best_le
  * the shared max_iter and step_size.  Replaces any previous batch of the context. */
 int pp_batch_new(pp_ctx* ctx, int q, const double* starts, const double* goals,
                  const uint64_t* seeds, int64_t max_iter, double step_size);
-/* speculative iterations per query and step (a power of two <= 64; 0 = automatic: 32 for at most
- * 2048 queries, else 16 while the step holds at most 131072 tasks).  Results do not depend on it: every query's tree equals its one-at-a-time
- * sequential run.  Applies to the current batch and the next ones. */
+/* speculative iterations per query and step (a power of two <= 64; 0 = automatic: 32, halved
+ * while a step would hold more than 262144 tasks, i.e. q * k > 262144).  Results do not depend on
+ * it: every query's tree equals its one-at-a-time sequential run.  Applies to the current batch
+ * and the next ones. */
 int pp_batch_set_window(pp_ctx* ctx, int k);
 /* How pp_batch_plan runs check_finish (results are identical; for A/B measurement and tests):
  * rounds = 1 (default) in steer rounds, phase A taking span0 candidate edges per

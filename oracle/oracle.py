@@ -80,6 +80,10 @@ def lib():
             L.orc_rrt_extend.argtypes = [C.POINTER(Scene), C.POINTER(Tree), C.c_uint64, C.c_int64,
                                          C.c_int64, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int8)]
             L.orc_rrt_extend.restype = C.c_int64
+            L.orc_rrt_extend_samples.argtypes = [C.POINTER(Scene), C.POINTER(Tree), dp, dp,
+                                                 C.c_int64, C.c_int, C.POINTER(C.c_int32), dp,
+                                                 C.POINTER(C.c_int8)]
+            L.orc_rrt_extend_samples.restype = C.c_int64
             L.orc_verify_candidate.argtypes = [C.POINTER(Scene), C.POINTER(Tree), C.c_double,
                                                C.c_double, C.c_int, C.c_int, dp]
             L.orc_verify_candidate.restype = C.c_int
@@ -275,6 +279,24 @@ def rrt_extend(scene: OracleScene, tree: OracleTree, seed: int, it0: int, n_iter
     if acc < 0:
         raise RuntimeError("orc_rrt_extend failed (capacity?)")
     return acc, log_nn, log_acc
+
+
+def rrt_extend_samples(scene: OracleScene, tree: OracleTree, sx, sy, full_reverify: bool = False):
+    """Sequential extend over caller-drawn samples (the host-owned RNG of pp_rrt_extend_samples).
+    Returns (accepted, log_nn, log_yaw, log_acc)."""
+    sx = np.ascontiguousarray(sx, dtype=np.float64)
+    sy = np.ascontiguousarray(sy, dtype=np.float64)
+    n = len(sx)
+    log_nn = np.zeros(n, dtype=np.int32)
+    log_yaw = np.zeros(n)
+    log_acc = np.zeros(n, dtype=np.int8)
+    acc = lib().orc_rrt_extend_samples(C.byref(scene._c), C.byref(tree._c), _dp(sx), _dp(sy), n,
+                                       int(full_reverify),
+                                       log_nn.ctypes.data_as(C.POINTER(C.c_int32)), _dp(log_yaw),
+                                       log_acc.ctypes.data_as(C.POINTER(C.c_int8)))
+    if acc < 0:
+        raise RuntimeError("orc_rrt_extend_samples failed (capacity?)")
+    return acc, log_nn, log_yaw, log_acc
 
 
 def nearest(X, Y, qx, qy):

@@ -614,6 +614,25 @@ static int verify_candidate(const orc_scene* sc, const orc_tree* tr, double x, d
  * rand_point (x then y) → exact NN → Node::new → verify_node → insert.  check_finish is a
  * separate row.  Per-iteration logs: nearest index and accepted flag.
  * Returns the number of accepted nodes, or -1 (allocation / capacity failure). */
+/* One iteration of plan_one's extend on the sample (x, y): exact NN → Node::new → verify_node →
+ * insert (rrt.rs:583-589).  Returns 1 inserted, 0 rejected, -1 allocation / capacity failure;
+ * *nn / *yaw_out: the nearest node and the new node's yaw (compute_yaw toward it). */
+static int extend_one(const orc_scene* sc, orc_tree* tr, double x, double y, int full_reverify,
+                      pbuf* b, dscratch* s, int* nn, double* yaw_out) {
+    int p = orc_nearest(tr->x, tr->y, tr->n, x, y, NULL);
+    *nn = p;
+    *yaw_out = 0.0;
+    if (p < 0) return 0;
+    double yaw = compute_yaw(x, y, tr->x[p], tr->y[p]);
+    *yaw_out = yaw;
+    int ok = verify_candidate(sc, tr, x, y, yaw, p, full_reverify, b, s);
+    if (ok <= 0) return ok;
+    if (tr->n >= tr->cap) return -1;
+    tr->x[tr->n] = x; tr->y[tr->n] = y; tr->yaw[tr->n] = yaw; tr->parent[tr->n] = p;
+    tr->n++;
+    return 1;
+}
+
 int64_t orc_rrt_extend(const orc_scene* sc, orc_tree* tr, uint64_t seed, int64_t it0,
                        int64_t n_iter, int full_reverify, int32_t* log_nn, int8_t* log_acc) {
     pbuf b = {0};
@@ -621,22 +640,39 @@ int64_t orc_rrt_extend(const orc_scene* sc, orc_tree* tr, uint64_t seed, int64_t
     int64_t acc = 0;
     for (int64_t k = 0; k < n_iter; ++k) {
         uint64_t it = (uint64_t)(it0 + k);
+        /* Space::rand_point, rrt.rs:139-146 (Q7: x = draw 2 it, y = draw 2 it + 1) */
         double x = orc_gen_range(seed, 2 * it, sc->minx, sc->maxx);
         double y = orc_gen_range(seed, 2 * it + 1, sc->miny, sc->maxy);
-        int p = orc_nearest(tr->x, tr->y, tr->n, x, y, NULL);
+        int p;
+        double yaw;
+        int ok = extend_one(sc, tr, x, y, full_reverify, &b, &s, &p, &yaw);
         if (log_nn) log_nn[k] = p;
-        int ok = 0;
-        if (p >= 0) {
-            double yaw = compute_yaw(x, y, tr->x[p], tr->y[p]);
-            ok = verify_candidate(sc, tr, x, y, yaw, p, full_reverify, &b, &s);
-            if (ok < 0) { acc = -1; break; }
-            if (ok) {
-                if (tr->n >= tr->cap) { acc = -1; break; }
-                tr->x[tr->n] = x; tr->y[tr->n] = y; tr->yaw[tr->n] = yaw; tr->parent[tr->n] = p;
-                tr->n++;
-                acc++;
-            }
-        }
+        if (ok < 0) { acc = -1; break; }
+        acc += ok;
+        if (log_acc) log_acc[k] = (int8_t)ok;
+    }
+    free(b.x); free(b.y);
+    free(s.px); free(s.py); free(s.pyaw);
+    return acc;
+}
+
+/* The same extend over caller-drawn samples (the host owns the RNG: pp_rrt_extend_samples):
+ * iteration k takes (sx[k], sy[k]) as its rand_point.  Logs per sample: nearest node, yaw (the
+ * node Node::new would build), inserted flag.  Returns the inserts, or -1. */
+int64_t orc_rrt_extend_samples(const orc_scene* sc, orc_tree* tr, const double* sx,
+                               const double* sy, int64_t n, int full_reverify, int32_t* log_nn,
+                               double* log_yaw, int8_t* log_acc) {
+    pbuf b = {0};
+    dscratch s = {0};
+    int64_t acc = 0;
+    for (int64_t k = 0; k < n; ++k) {
+        int p;
+        double yaw;
+        int ok = extend_one(sc, tr, sx[k], sy[k], full_reverify, &b, &s, &p, &yaw);
+        if (ok < 0) { acc = -1; break; }
+        acc += ok;
+        if (log_nn) log_nn[k] = p;
+        if (log_yaw) log_yaw[k] = yaw;
         if (log_acc) log_acc[k] = (int8_t)ok;
     }
     free(b.x); free(b.y);

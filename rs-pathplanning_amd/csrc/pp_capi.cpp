@@ -146,6 +146,10 @@ struct pp_ctx {
     DBuf<int> PAR;
     DBuf<DevState> d_state, d_api_state;
     HBuf<DevState> h_state;
+    // pp_rrt_extend_samples: the caller's samples and the per-iteration record (one chunk)
+    DBuf<double> hs_x, hs_y, hs_yaw;
+    DBuf<int> hs_par;
+    DBuf<uint8_t> hs_ok;
 
     // ---- window buffers (sized for Kcap)
     int K = 4096;
@@ -1558,10 +1562,23 @@ int pp_rrt_set_window(pp_ctx* ctx, int k) {
     return PP_OK;
 }
 
-int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
-    int r = check_ctx(ctx, true, true);
-    if (r) return r;
-    if (n_iter < 0) return set_err(PP_ERR_INVALID_ARGUMENT, "n_iter < 0");
+}  // extern "C"
+
+namespace {
+
+// The extend loop behind pp_rrt_extend (src: null, the seeded stream) and pp_rrt_extend_samples
+// (src: the caller's samples of the iterations [ctx->it, ctx->it + n_iter), on the device, and
+// the per-iteration record).  eps: the f32 screen tolerance of this call (the samples' magnitude).
+struct SampleSrc {
+    const double* x;
+    const double* y;
+    SampleRec rec;
+    bool pretest;  // the obstacle pre-test may settle a sample without its nearest node
+};
+
+int rrt_extend_impl(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted, const SampleSrc* src,
+                    double eps) {
+    int r;
     if ((r = ensure_window(ctx, ctx->K))) return r;
     if (ctx->root_blocked) {  // every iteration rejects: only the iteration counters advance
         DevState& s = ctx->h_state.p[0];
@@ -1593,6 +1610,13 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
         WindowArgs a = ctx->window_args(ctx->d_state.p);
         a.K = K;
         a.target = target;
+        a.eps_coord = eps;
+        if (src) {
+            a.hsx = src->x;
+            a.hsy = src->y;
+            a.hrec = src->rec;
+            if (!src->pretest) a.blk = nullptr;
+        }
         if (ctx->prof && (r = ensure_events(ctx, 5 * (size_t)nw))) return r;
         const int64_t windows_before = ctx->h_state.p[0].windows;
         // windows are pipelined: window w's kernel resolves and commits w - 1; the drain launch
@@ -1625,6 +1649,135 @@ int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
         ctx->n = s.n;
     }
     if (n_accepted) *n_accepted = ctx->n - n_before;
+    return PP_OK;
+}
+
+// pp_rrt_extend_samples' device buffers: samples and records of kHostChunk iterations at a time
+constexpr int64_t kHostChunk = (int64_t)1 << 20;
+
+}  // namespace
+
+extern "C" {
+
+int pp_rrt_extend(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (n_iter < 0) return set_err(PP_ERR_INVALID_ARGUMENT, "n_iter < 0");
+    return rrt_extend_impl(ctx, n_iter, n_accepted, nullptr, ctx->eps_coord);
+}
+
+int pp_rrt_extend_samples(pp_ctx* ctx, const double* sx, const double* sy, int64_t k,
+                          int32_t* nearest, double* yaw, uint8_t* ok, int64_t* n_accepted) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (k < 0 || (k > 0 && (!sx || !sy)))
+        return set_err(PP_ERR_INVALID_ARGUMENT, "bad extend_samples arguments");
+    double mx = 0.0;
+    for (int64_t i = 0; i < k; ++i) {
+        if (!std::isfinite(sx[i]) || !std::isfinite(sy[i]))
+            return set_err(PP_ERR_INVALID_ARGUMENT, "a sample is not finite");
+        mx = std::max({mx, std::fabs(sx[i]), std::fabs(sy[i])});
+    }
+    // the f32 screen's tolerance covers the coordinates it rounds: nodes and these samples
+    const double eps = std::max(ctx->eps_coord, mx * std::ldexp(1.0, -23));
+    int64_t acc_all = 0;
+    if (ctx->root_blocked) {  // nothing is ever inserted: the tree is fixed, every verdict false
+        const int64_t n_before = ctx->n;
+        for (int64_t b = 0; b < k && (nearest || yaw); b += ctx->Kcap) {
+            const int nb = (int)std::min<int64_t>(ctx->Kcap, k - b);
+            std::vector<int32_t> idx((size_t)nb);
+            if ((r = pp_rrt_get_nearest_node_batch(ctx, sx + b, sy + b, nb, idx.data(), nullptr)))
+                return r;
+            std::vector<double> tx((size_t)n_before), ty((size_t)n_before);
+            if (yaw) {
+                PP_HIP(hipMemcpy(tx.data(), ctx->X.p, tx.size() * sizeof(double), hipMemcpyDeviceToHost));
+                PP_HIP(hipMemcpy(ty.data(), ctx->Y.p, ty.size() * sizeof(double), hipMemcpyDeviceToHost));
+            }
+            for (int i = 0; i < nb; ++i) {
+                if (nearest) nearest[b + i] = idx[(size_t)i];
+                if (yaw) yaw[b + i] = std::atan2(ty[(size_t)idx[i]] - sy[b + i], tx[(size_t)idx[i]] - sx[b + i]);
+            }
+        }
+        if (ok) std::memset(ok, 0, (size_t)k);
+        if ((r = rrt_extend_impl(ctx, k, nullptr, nullptr, eps))) return r;
+        if (n_accepted) *n_accepted = 0;
+        return PP_OK;
+    }
+    for (int64_t b = 0; b < k; b += kHostChunk) {
+        const int64_t nb = std::min(kHostChunk, k - b);
+        const size_t z = (size_t)nb;
+        PP_HIP(ctx->hs_x.reserve(z));
+        PP_HIP(ctx->hs_y.reserve(z));
+        if (nearest) PP_HIP(ctx->hs_par.reserve(z));
+        if (yaw) PP_HIP(ctx->hs_yaw.reserve(z));
+        if (ok) PP_HIP(ctx->hs_ok.reserve(z));
+        hipStream_t st = ctx->stream;
+        PP_HIP(hipMemcpyAsync(ctx->hs_x.p, sx + b, z * sizeof(double), hipMemcpyHostToDevice, st));
+        PP_HIP(hipMemcpyAsync(ctx->hs_y.p, sy + b, z * sizeof(double), hipMemcpyHostToDevice, st));
+        SampleSrc src{ctx->hs_x.p, ctx->hs_y.p,
+                      SampleRec{ctx->it, nearest ? ctx->hs_par.p : nullptr,
+                                yaw ? ctx->hs_yaw.p : nullptr, ok ? ctx->hs_ok.p : nullptr},
+                      !nearest && !yaw};
+        int64_t acc = 0;
+        if ((r = rrt_extend_impl(ctx, nb, &acc, &src, eps))) return r;
+        acc_all += acc;
+        if (nearest)
+            PP_HIP(hipMemcpyAsync(nearest + b, ctx->hs_par.p, z * sizeof(int), hipMemcpyDeviceToHost, st));
+        if (yaw) PP_HIP(hipMemcpyAsync(yaw + b, ctx->hs_yaw.p, z * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (ok) PP_HIP(hipMemcpyAsync(ok + b, ctx->hs_ok.p, z, hipMemcpyDeviceToHost, st));
+        PP_HIP(hipStreamSynchronize(st));
+    }
+    if (n_accepted) *n_accepted = acc_all;
+    return PP_OK;
+}
+
+int pp_rrt_tree_import(pp_ctx* ctx, const double* x, const double* y, const double* yaw,
+                       const int32_t* parent, int64_t n) {
+    int r = check_ctx(ctx, true, true);
+    if (r) return r;
+    if (n < 1 || !x || !y || !yaw || !parent)
+        return set_err(PP_ERR_INVALID_ARGUMENT, "a tree has at least its root");
+    if (n > (int64_t)0x7fff0000) return set_err(PP_ERR_CAPACITY, "tree larger than 2^31 nodes");
+    if (parent[0] != -1) return set_err(PP_ERR_INVALID_ARGUMENT, "node 0 must be the root (parent -1)");
+    double mx = std::max({std::fabs(ctx->minx), std::fabs(ctx->maxx), std::fabs(ctx->miny),
+                          std::fabs(ctx->maxy)});
+    for (int64_t i = 0; i < n; ++i) {
+        if (i > 0 && (parent[i] < 0 || parent[i] >= i))
+            return set_err(PP_ERR_INVALID_ARGUMENT,
+                           "parent[i] must be an earlier node (insertion order, rrt.rs:586-589)");
+        if (!std::isfinite(x[i]) || !std::isfinite(y[i]) || !std::isfinite(yaw[i]))
+            return set_err(PP_ERR_INVALID_ARGUMENT, "a node coordinate is not finite");
+        mx = std::max({mx, std::fabs(x[i]), std::fabs(y[i])});
+    }
+    PP_HIP(hipStreamSynchronize(ctx->stream));
+    if ((r = ensure_tree(ctx, n + 1024))) return r;
+    const size_t z = (size_t)n;
+    std::vector<float> fx(z), fy(z);
+    for (size_t i = 0; i < z; ++i) {
+        fx[i] = (float)x[i];
+        fy[i] = (float)y[i];
+    }
+    PP_HIP(hipMemcpy(ctx->x32.p, fx.data(), z * sizeof(float), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->y32.p, fy.data(), z * sizeof(float), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->X.p, x, z * sizeof(double), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->Y.p, y, z * sizeof(double), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->YAW.p, yaw, z * sizeof(double), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(ctx->PAR.p, parent, z * sizeof(int32_t), hipMemcpyHostToDevice));
+    // the planner continues from this tree: its iteration counter and statistics stay
+    DevState& s = ctx->h_state.p[0];
+    PP_HIP(hipMemcpy(&s, ctx->d_state.p, sizeof(DevState), hipMemcpyDeviceToHost));
+    s.n = (int)n;
+    s.n_scan = (int)n;
+    s.it_spec = s.it;
+    s.void_seq = -1;
+    s.kdyn = kMinDynWindow;
+    PP_HIP(hipMemcpy(ctx->d_state.p, &s, sizeof(DevState), hipMemcpyHostToDevice));
+    ctx->n = n;
+    ctx->start[0] = x[0];
+    ctx->start[1] = y[0];
+    ctx->start[2] = yaw[0];
+    ctx->eps_coord = mx * std::ldexp(1.0, -23);
+    ctx->root_blocked = (ctx->ne > 0 || ctx->nbv > 0) && !ctx->point_ok(x[0], y[0]);
     return PP_OK;
 }
 

@@ -48,6 +48,11 @@ struct WindowArgs {
     long long* wg_points = nullptr;  // profiling: walked points per walk workgroup (or null)
     const SceneDev* scp = nullptr;  // the scene in device memory (samples_role's point_blocked)
     unsigned char* blk = nullptr;   // [2 * Kcap] sample in an obstacle (null: no pre-test)
+    // caller-drawn samples (pp_rrt_extend_samples): iteration it's sample is (hsx, hsy)[it -
+    // hrec.base] instead of the seeded stream (null: the stream); hrec: the per-iteration record
+    const double* hsx = nullptr;
+    const double* hsy = nullptr;
+    SampleRec hrec{0, nullptr, nullptr, nullptr};
 };
 
 // Enqueue window number `seq` on stream s: its window kernel also resolves and commits window

@@ -978,7 +978,26 @@ struct SamplesArgs {
     int* ipos[2];     // sample -> sorted position (the screen's partials are stored by position)
     const SceneDev* scp = nullptr;       // the scene in device memory (point_blocked)
     unsigned char* blk[2] = {nullptr, nullptr};  // sample -> its point lies in an obstacle
+    // caller-drawn samples (pp_rrt_extend_samples): iteration it's sample is (hsx, hsy)[it -
+    // hs_base] instead of the seeded stream (null: the stream)
+    const double* hsx = nullptr;
+    const double* hsy = nullptr;
+    int64_t hs_base = 0;
 };
+
+// Space::rand_point of iteration itj (rrt.rs:139-146): the seeded stream (Q7: x = draw 2 it,
+// y = draw 2 it + 1), or the caller's own sample of that iteration
+__device__ __forceinline__ void draw_sample(const SamplesArgs& g, uint64_t itj, double& x,
+                                            double& y) {
+    if (g.hsx) {
+        const int64_t i = (int64_t)itj - g.hs_base;
+        x = g.hsx[i];
+        y = g.hsy[i];
+    } else {
+        x = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
+        y = gen_range(g.seed, 2 * itj + 1, g.miny, g.maxy);
+    }
+}
 
 __device__ inline int morton16(int x, int y) {
     int m = 0;
@@ -1066,9 +1085,7 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
             const int j = j0 + u * NT;
             xs[u] = ys[u] = 0.0;
             if (j < W) {
-                const uint64_t itj = (uint64_t)(start + j);
-                xs[u] = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
-                ys[u] = gen_range(g.seed, 2 * itj + 1, g.miny, g.maxy);
+                draw_sample(g, (uint64_t)(start + j), xs[u], ys[u]);
             }
         }
 #pragma unroll
@@ -1171,9 +1188,7 @@ __device__ void samples_role(DevState* st, const SamplesArgs& g, int np, int64_t
         const bool in = pos < Ws;
         if (in) {
             const int j = s_j[pos];
-            const uint64_t itj = (uint64_t)(start + j);
-            xs[k] = gen_range(g.seed, 2 * itj, g.minx, g.maxx);
-            ys[k] = gen_range(g.seed, 2 * itj + 1, g.miny, g.maxy);
+            draw_sample(g, (uint64_t)(start + j), xs[k], ys[k]);
             g.perm[np][pos] = j;
             g.ipos[np][j] = pos;
             g.sxy[np][pos] = make_float2((float)xs[k], (float)ys[k]);
@@ -1272,6 +1287,7 @@ struct WinKArgs {
     // window mode: workgroup 0 draws the next window's samples (parity 1 - p) after its commit
     int gen_next;
     SamplesArgs g;
+    SampleRec hrec;     // pp_rrt_extend_samples: the commit's per-iteration record
 };
 
 // RRT::get_nearest_node screen (rrt.rs:378-391): f32 SoA nodes x the window's samples.  The
@@ -3152,7 +3168,7 @@ __device__ __attribute__((always_inline)) inline void commit_role(
     const double* __restrict__ wsy, const int* __restrict__ nn_idx,
     const int* __restrict__ snap_status, const double* __restrict__ snap_yaw,
     const int* __restrict__ fin_par, int* __restrict__ cand_cnt, int W, int64_t void_next,
-    int64_t screened, char* smem) {
+    int64_t screened, const SampleRec& hrec, char* smem) {
     constexpr int PER = kMaxWindow / NT;
     static_assert(PER % 4 == 0, "commit: whole int4 loads per thread");
     int* s_node = reinterpret_cast<int*>(smem);
@@ -3210,6 +3226,17 @@ __device__ __attribute__((always_inline)) inline void commit_role(
             tr.parent[nd] = (v[u] & kWinParent) ? s_node[fin_par[j]] : nn_idx[j];
         }
         if (j < W) cand_cnt[j] = 0;  // the next window's pair counts start at zero
+    }
+    if (hrec.par || hrec.yaw || hrec.ok) {  // pp_rrt_extend_samples: every committed iteration
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int j = j0 + u;
+            if (j >= Weff) continue;
+            const int64_t r = it0 + j - hrec.base;
+            if (hrec.ok) hrec.ok[r] = (unsigned char)(v[u] & 1);
+            if (hrec.par) hrec.par[r] = (v[u] & kWinParent) ? s_node[fin_par[j]] : nn_idx[j];
+            if (hrec.yaw) hrec.yaw[r] = snap_yaw[j];
+        }
     }
     if (tid == 0) {
         st->n = n0 + total;
@@ -3273,7 +3300,7 @@ __global__ __launch_bounds__(kScanThreads) void window_kernel(WinKArgs a) {
                 commit_role<kScanThreads>(st, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.snap_status,
                                           a.snap_yaw, a.fin_par, a.cand_cnt, W,
                                           a.scan ? a.seq : -1,
-                                          (int64_t)st->Wsp[q] * st->nsp[q], smem);
+                                          (int64_t)st->Wsp[q] * st->nsp[q], a.hrec, smem);
             }
         }
         if (threadIdx.x == 0) {  // the screened window's counters start at zero
@@ -3310,7 +3337,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_tail_kernel(WinKArgs 
     __syncthreads();
     commit_role<kResolveThreads>(st, a.tr, a.wsx[q], a.wsy[q], a.nn_idx, a.snap_status,
                                  a.snap_yaw, a.fin_par, a.cand_cnt, W, a.scan ? a.seq : -1,
-                                 (int64_t)st->Wsp[q] * st->nsp[q], smem);
+                                 (int64_t)st->Wsp[q] * st->nsp[q], a.hrec, smem);
     if (threadIdx.x == 0) {
         st->resolve_bail = 0;
         st->flag_count = 0;
@@ -4813,8 +4840,8 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
                                                         int* __restrict__ lit_locks,
                                                         int* __restrict__ err) {
     // a wave serves 64 / K queries, K lanes each (lane = g * K + k: the window's iteration
-    // it[q] + k of its g-th query; K a power of two <= 16).  Literal-path re-runs first (rare, the
-    // wave's one scratch buffer), then each query's in-order replay: iteration k keeps its
+    // it[q] + k of its g-th query; K a power of two <= kMqMaxK = 64, automatically 32, halved
+    // while Q * K > 262144).  Literal-path re-runs first (rare, the wave's one scratch buffer), then each query's in-order replay: iteration k keeps its
     // speculative verdict unless an accepted window sample k' < k is strictly nearer than its
     // snapshot NN (snapshot nodes have lower indices and win ties) — the window stops there and
     // the next step resumes at it; the accepted samples before it are appended in order
@@ -5590,6 +5617,9 @@ SamplesArgs samples_args(const WindowArgs& a) {
         g.blk[q] = a.blk ? a.blk + (size_t)q * a.Kcap : nullptr;
     }
     g.scp = a.scp;
+    g.hsx = a.hsx;
+    g.hsy = a.hsy;
+    g.hs_base = a.hrec.base;
     return g;
 }
 PairGrid pair_grid(const SamplesArgs& g, int p, double eps_coord) {
@@ -5650,6 +5680,7 @@ WinKArgs win_args(const WindowArgs& a, int p, int gen, int resolve, int scan, in
     k.lit_scratch = a.lit_scratch;
     k.gen_next = gen && scan;
     k.g = samples_args(a);
+    k.hrec = a.hrec;
     return k;
 }
 }  // namespace

@@ -273,6 +273,17 @@ struct ResolveScratch {
     double* repyaw; // [K]
 };
 
+// pp_rrt_extend_samples' per-iteration record (caller-drawn samples): the commit of a window
+// writes, for every committed iteration it, the nearest node Node::new took as parent (rrt.rs:
+// 169-175, 378-391), the new node's yaw and verify_node's verdict at [it - base]; each pointer
+// may be null (all null: no record)
+struct SampleRec {
+    int64_t base;
+    int* par;
+    double* yaw;
+    unsigned char* ok;
+};
+
 // window status word after the resolve (snap_status of a pending sample is overwritten with it):
 // bit 0 = accepted, bit 2 = its parent is the window sample fin_par[j] (else its snapshot NN)
 constexpr int kWinParent = 4;

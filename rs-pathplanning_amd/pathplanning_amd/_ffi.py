@@ -21,7 +21,7 @@ PP_ERR_STATE = -5
 PP_ERR_STEER_OVERFLOW = -6
 PP_ERR_REFERENCE_PANIC = -7
 PP_CF_CHAIN = 18
-PP_ABI_VERSION = 4
+PP_ABI_VERSION = 5
 
 _ERR_NAMES = {
     PP_ERR_INVALID_ARGUMENT: "PP_ERR_INVALID_ARGUMENT", PP_ERR_HIP: "PP_ERR_HIP",
@@ -40,7 +40,8 @@ EXPORTED = [
     "pp_space_new", "pp_space_set_grid", "pp_space_get_bounds",
     "pp_space_new_polygons", "pp_space_verify_batch",
     "pp_rrt_new",
-    "pp_rrt_set_window", "pp_rrt_extend", "pp_rrt_plan_one", "pp_rrt_tree_size",
+    "pp_rrt_set_window", "pp_rrt_extend", "pp_rrt_extend_samples", "pp_rrt_tree_import",
+    "pp_rrt_plan_one", "pp_rrt_tree_size",
     "pp_rrt_iteration", "pp_rrt_tree_export", "pp_rrt_get_nearest_node_batch",
     "pp_rrt_verify_node_batch", "pp_rrt_check_finish_batch", "pp_rrt_check_finish",
     "pp_rrt_plan", "pp_batch_new", "pp_batch_set_window", "pp_batch_set_finish_schedule", "pp_batch_extend", "pp_batch_state", "pp_batch_tree_export",
@@ -142,6 +143,9 @@ def lib():
                            C.c_int),
             "pp_rrt_set_window": ([vp, C.c_int], C.c_int),
             "pp_rrt_extend": ([vp, C.c_int64, i64p], C.c_int),
+            "pp_rrt_extend_samples": ([vp, dp, dp, C.c_int64, ip, dp, C.POINTER(C.c_uint8), i64p],
+                                      C.c_int),
+            "pp_rrt_tree_import": ([vp, dp, dp, dp, ip, C.c_int64], C.c_int),
             "pp_rrt_plan_one": ([vp, ip], C.c_int),
             "pp_rrt_tree_size": ([vp, i64p], C.c_int),
             "pp_rrt_iteration": ([vp, i64p], C.c_int),

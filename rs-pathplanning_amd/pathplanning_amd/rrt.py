@@ -223,6 +223,46 @@ class RRT:  # rrt.rs:325-620
         _ffi.check(_ffi.lib().pp_rrt_extend(self.ctx.handle, int(n_iter), C.byref(acc)))
         return acc.value
 
+    def extend_samples(self, sx, sy, record: bool = True):
+        """plan_one's extend (rrt.rs:583-589) over caller-drawn samples: iteration it + i takes
+        (sx[i], sy[i]) as its rand_point (rrt.rs:139-146) — the host owns the RNG.  Returns the
+        nodes inserted, or with ``record`` (nearest int32[k], yaw f64[k], ok bool[k]): per sample
+        the nearest node of the tree as it stood (Node::new's parent), its yaw and whether it was
+        inserted.  ``record=False`` lets the obstacle pre-test settle samples without their
+        nearest node (faster)."""
+        sx = np.ascontiguousarray(sx, dtype=np.float64)
+        sy = np.ascontiguousarray(sy, dtype=np.float64)
+        k = len(sx)
+        if len(sy) != k:
+            raise ValueError("sx and sy differ in length")
+        acc = C.c_int64(0)
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        if not record:
+            _ffi.check(_ffi.lib().pp_rrt_extend_samples(
+                self.ctx.handle, sx.ctypes.data_as(dp), sy.ctypes.data_as(dp), k, None, None, None,
+                C.byref(acc)))
+            return acc.value
+        nearest = np.zeros(k, dtype=np.int32)
+        yaw = np.zeros(k)
+        ok = np.zeros(k, dtype=np.uint8)
+        _ffi.check(_ffi.lib().pp_rrt_extend_samples(
+            self.ctx.handle, sx.ctypes.data_as(dp), sy.ctypes.data_as(dp), k,
+            nearest.ctypes.data_as(ip), yaw.ctypes.data_as(dp),
+            ok.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(acc)))
+        return nearest, yaw, ok.astype(bool)
+
+    def tree_import(self, x, y, yaw, parent):
+        """Replace the tree by host-owned nodes (root first, parent -1 for the root, otherwise an
+        earlier node); the iteration counter, scene and goal stay."""
+        x, y, yaw = (np.ascontiguousarray(a, dtype=np.float64) for a in (x, y, yaw))
+        parent = np.ascontiguousarray(parent, dtype=np.int32)
+        if not (len(x) == len(y) == len(yaw) == len(parent)):
+            raise ValueError("tree arrays differ in length")
+        dp = C.POINTER(C.c_double)
+        _ffi.check(_ffi.lib().pp_rrt_tree_import(
+            self.ctx.handle, x.ctypes.data_as(dp), y.ctypes.data_as(dp), yaw.ctypes.data_as(dp),
+            parent.ctypes.data_as(C.POINTER(C.c_int32)), len(x)))
+
     def plan_one(self) -> bool:
         """plan_one's extend (rrt.rs:583-589): True when the node was inserted."""
         acc = C.c_int32(0)
@@ -418,7 +458,8 @@ class RRTBatch:
     (rrt.rs:335-355) with its own start, goal and sampling stream, advanced in lockstep — one
     plan_one extend iteration (rrt.rs:583-589) of every query per step — on one GPU.  ``window``:
     iterations per query evaluated speculatively per GPU step (a power of two <= 64, 0 =
-    automatic: 16 up to 131072 tasks per step); every query's tree equals its sequential run."""
+    automatic: 32, halved while a step would hold more than 262144 tasks); every query's tree
+    equals its sequential run."""
 
     def __init__(self, starts, goals, max_iter, step_size, space: Space, seeds, device: int = 0,
                  ctx: _ffi.Context | None = None, window: int = 0):

@@ -40,7 +40,7 @@ def test_library_holds_gfx950_code(pkg):
 
 
 def test_abi_version(pkg):
-    assert pkg._ffi.lib().pp_abi_version() == 4 == pkg._ffi.PP_ABI_VERSION
+    assert pkg._ffi.lib().pp_abi_version() == 5 == pkg._ffi.PP_ABI_VERSION
 
 
 def test_rng_matches_oracle(pkg, oracle_mod):
