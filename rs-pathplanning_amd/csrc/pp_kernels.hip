@@ -4701,7 +4701,13 @@ __device__ __forceinline__ bool mq_nn_query(const MqDev& mq, double minx, double
     const uint64_t seed = mq.seed[q];
     // the verdict cache: the task region still holds the previous step's window, which
     // started Tp iterations before this one, so iteration it sat in old slot k + Tp; its
-    // parent and verdict are read before any lane overwrites the region
+    // parent, verdict and yaw are read before any lane overwrites the region.  Lane k reads slot
+    // k + Tp, which lane k + Tp of the SAME wave rewrites below (tasks, status, tyaw of slot t):
+    // that is ordered only because all K slots of a query are served by one wave (K <= 64, one
+    // query per K lanes) and every load is issued before the first store: the wave barrier
+    // keeps the compiler from sinking a load past the stores, and one wave's vector memory
+    // requests to an address are served in issue order.  Serving a query's slots from more than
+    // one wave would need a grid-wide ordering instead.
     int opn = -1, ost = -1;
     double oyw = 0.0;
     if (mq.it_prev && g == 0) {
@@ -4713,6 +4719,7 @@ __device__ __forceinline__ bool mq_nn_query(const MqDev& mq, double minx, double
             if (mq.tyaw) oyw = mq.tyaw[to];
         }
     }
+    __builtin_amdgcn_wave_barrier();
     double x = 0.0, y = 0.0;
     if (live) {
         x = gen_range(seed, 2 * (uint64_t)it, minx, maxx);
@@ -4959,8 +4966,11 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int nn_waves = big_nn ? 16 : 4;
     const int nn_blocks = std::min((Q + nn_waves - 1) / nn_waves, 4096);
     const int prep_blocks = std::min((T + kPrepThreads / 8 - 1) / (kPrepThreads / 8), 2048);
+    // the grid cap of the instantiation this step size launches (below)
+    const int walk_cap = T >= kBigStepTasks ? walk_grid_cap<kWalkMinWBatch, 2, true>(a.sc)
+                                            : walk_grid_cap<kWalkMinWBatch - 1, 2, true>(a.sc);
     const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
-                                     std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch, 2, true>(a.sc)));
+                                     std::min(kWalkMaxWG, walk_cap));
     const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
 
     for (int k = 0; k < steps; ++k) {

@@ -351,6 +351,27 @@ def test_100k_tree_properties(pkg, ctx, oracle_mod):
     assert np.array_equal(qx, x[:m]) and np.array_equal(qpar, par[:m])
 
 
+def test_node_evals_counts_screened_samples(pkg, ctx):
+    """pp_stats.node_evals (the config-2 roofline's units) adds, per committed window, the
+    screened samples (not in an obstacle) x the nodes the screen scanned: with no truncated
+    window it lies between (iterations - blocked) x the tree size before and after the windows"""
+    from pathplanning_amd import scenes
+
+    raw = scenes.field512()
+    p = _planner(pkg, raw, 42, 4096, ctx, capacity=1 << 17)
+    while p.tree_size() < 20_000:
+        p.extend(65536)
+    n0 = p.tree_size()
+    p.reset_stats()
+    p.extend(20 * 4096)
+    n1 = p.tree_size()
+    st = p.stats()
+    assert st["truncations"] == 0 and st["iterations"] == 20 * 4096
+    screened = st["iterations"] - st["samples_blocked"]
+    assert st["samples_blocked"] > 0 and screened > 0
+    assert screened * n0 <= st["node_evals"] <= screened * n1, (screened, n0, n1, st["node_evals"])
+
+
 def test_empty_scene_and_blocked_root(pkg, ctx):
     from pathplanning_amd import rrt
 
