@@ -180,6 +180,7 @@ struct pp_ctx {
     HBuf<SteerTask> h_tasks;
     // check_finish
     DBuf<int> cf_nodes, cf_ok, cf_npts, cf_chain, cf_etab, cf_err, cf_path, cf_items;
+    DBuf<int> cf_lpath, cf_spill;  // cf_line_kernel's ancestor paths; tier 1's spill list
     DBuf<int> cf_memo;  // check_finish_kernel's optimize memo (CfBatch::ftab / gtab), per launch
     DBuf<double> cf_len, cf_pts;
     // ---- multi-query batch (config 3)
@@ -211,11 +212,13 @@ struct pp_ctx {
     DBuf<double> mp_len, mp_blen;
     // pp_batch_plan's check_finish in steer rounds (CfbArgs)
     DBuf<int> cfb_nodei;   // [4 (nitems + Q)]: depth, open, tfirst, tcnt
-    DBuf<int> cfb_rows;    // [3 rows]: gclaim, tnone, tnone_up
+    DBuf<int> cfb_rows;    // [rows]: gclaim
+    DBuf<unsigned char> cfb_rows8;  // [2 rows]: tnone, tnone_up
     DBuf<int> cfb_gotab, cfb_plist, cfb_tnode, cfb_status, cfb_misc, cfb_lit;
     DBuf<SteerTask> cfb_tasks;
     DBuf<StarTaskExt> cfb_ext;
     DBuf<PrepRec> cfb_rec;
+    DBuf<unsigned char> cfb_none;
     DBuf<double> cfb_yaw;
     DBuf<DevState> cfb_state;
     DBuf<long long> cfb_pts;  // profiling: the rounds' walk point tallies
@@ -511,13 +514,23 @@ static_assert(PP_CF_CHAIN == kCfLevels + 2, "chain row layout");
 constexpr int kCfBatch = 16384;     // nodes per check_finish launch
 constexpr int kCfPtsCap = 1 << 16;  // line points per check_finish workgroup
 static_assert(4 * kCfMaxEdges <= kCfPtsCap, "cf_line_kernel keeps 4 doubles per edge in the hypot buffer");
-// the batch plan's cf_line_kernel workgroups: 3 x kCfPtsCap doubles of line points each
-// (1.5 MB), 3 GB for the whole grid, allocated on the first batch plan
-constexpr int kCfLineGrid = 2048;
-// phase A's task arrays (status, lists, SteerTask, StarTaskExt, PrepRec, yaw per task) are sized
-// for span x (items + queries) tasks: a span that would need more than this is clamped (the spans
-// change which candidates are walked together, never a result)
-constexpr size_t kCfbTaskBudget = (size_t)4 << 30;
+// cf_line_kernel in two tiers (CfLines): tier 1 runs every line on kCfLineGrid workgroups with
+// room for kCfLinePts1 points and a kCfLinePath1-deep path each (3 x 8192 doubles: 192 KB; the
+// config-3 plan's lines have ~2350 points), tier 2 the few longer or deeper ones at the full
+// capacities (kCfPtsCap points, kCfMaxDepth) on kCfLineGrid2 workgroups (1.5 MB each).  Round 5
+// gave every one of 2048 workgroups the full capacity: 3.2 GB.
+constexpr int kCfLineGrid = 1024;
+constexpr int kCfLinePts1 = 8192;
+constexpr int kCfLinePath1 = 1024;
+constexpr int kCfLineGrid2 = 64;
+constexpr int kCfSpillCap = 1 << 17;  // tier-1 lines handed to tier 2 per launch
+static_assert(4 * (kCfLinePath1 + kCfLevels + 1) <= kCfLinePts1, "tier 1: 4 doubles per edge");
+// phase A's task arrays (status, lists, SteerTask, StarTaskExt, yaw, None flag per task) are
+// sized for span x (items + queries) tasks: a span that would need more than this is clamped (the
+// spans change which candidates are walked together, never a result); the records (PrepRec,
+// 256 B a task) are steered in chunks of kCfbRecChunk tasks
+constexpr size_t kCfbTaskBudget = (size_t)512 << 20;
+constexpr size_t kCfbRecChunk = (size_t)1 << 19;
 
 // check_finish for nodes[0, k) (device pointer already filled); results on the device
 // The goal of a check_finish_kernel launch: the planner's (check_finish), or a caller-built goal
@@ -535,6 +548,33 @@ struct CfOut {
     int* chain;  // may be null
 };
 
+// cf_line_kernel's buffers for a launch of `wgs` tier-1 workgroups (CfLines).  spill == 0: one
+// tier at the full capacities (a one-node call, whose line the host reads from workgroup 0's
+// buffer); else tier 1 hands up to `spill` lines to tier 2.  The spill count is zeroed on the
+// stream.
+int cf_line_buffers(pp_ctx* c, int wgs, int spill, CfLines& L) {
+    const bool two = spill > 0;
+    const int pc1 = two ? kCfLinePts1 : kCfPtsCap, dc1 = two ? kCfLinePath1 : kCfMaxDepth;
+    const int g2 = two ? std::min(kCfLineGrid2, wgs) : 0;
+    const size_t e1 = 2 * (size_t)(dc1 + kCfLevels + 1), e2 = 2 * (size_t)kCfMaxEdges;
+    PP_HIP(c->cf_pts.reserve((size_t)wgs * 3 * pc1 + (size_t)g2 * 3 * kCfPtsCap));
+    PP_HIP(c->cf_etab.reserve((size_t)wgs * e1 + (size_t)g2 * e2));
+    PP_HIP(c->cf_lpath.reserve((size_t)wgs * dc1 + (size_t)g2 * kCfMaxDepth));
+    L.grid1 = wgs;
+    L.t1 = CfLineBufs{c->cf_pts.p, pc1, c->cf_etab.p, c->cf_lpath.p, dc1, nullptr};
+    if (two) {
+        PP_HIP(c->cf_spill.reserve(1 + (size_t)spill * kCfItem));
+        PP_HIP(hipMemsetAsync(c->cf_spill.p, 0, sizeof(int), c->stream));
+        L.t1.spill = c->cf_spill.p;
+        L.t1.spill_cap = spill;
+        L.grid2 = g2;
+        L.t2 = CfLineBufs{c->cf_pts.p + (size_t)wgs * 3 * pc1, kCfPtsCap,
+                          c->cf_etab.p + (size_t)wgs * e1, c->cf_lpath.p + (size_t)wgs * dc1,
+                          kCfMaxDepth, nullptr};
+    }
+    return PP_OK;
+}
+
 // check_finish_kernel over nodes[0, k) (device) with its error handling; the one-tree planner
 // (cb.qidx null: the context's tree, goal g) or a query batch (cb)
 int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line, int grid,
@@ -549,18 +589,20 @@ int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line,
     PP_HIP(hipMemsetAsync(c->cf_memo.p, 0, 2 * rows * sizeof(int), c->stream));
     cb.ftab = c->cf_memo.p;
     cb.gtab = c->cf_memo.p + rows;
-    // the line buffers (one per workgroup of the launch) only when lines are materialised
+    // the line buffers (per workgroup of the line kernel) only when lines are materialised: one
+    // workgroup at the full capacities for a one-node call (the host reads workgroup 0's line),
+    // else the two tiers
     const int wgs = std::min(grid, k);
+    CfLines lines;
     if (want_line) {
-        PP_HIP(c->cf_pts.reserve((size_t)wgs * 3 * kCfPtsCap));
-        PP_HIP(c->cf_etab.reserve((size_t)wgs * 2 * kCfMaxEdges));
         PP_HIP(c->cf_items.reserve(1 + (size_t)k * kCfItem));
         PP_HIP(hipMemsetAsync(c->cf_items.p, 0, sizeof(int), c->stream));
+        int r = cf_line_buffers(c, wgs, wgs > 1 ? std::min(k, kCfSpillCap) : 0, lines);
+        if (r) return r;
     }
-    // the ancestor paths: check_finish_kernel's waves (kCfWaves per workgroup, at most
-    // min(grid, k / kCfWaves) workgroups) and cf_line_kernel's workgroups (min(grid, k), each in
-    // its first wave's region)
-    PP_HIP(c->cf_path.reserve((size_t)wgs * kCfWaves * kCfMaxDepth));
+    // the ancestor paths of check_finish_kernel's waves (kCfWaves per workgroup, at most
+    // min(grid, k / kCfWaves) workgroups)
+    PP_HIP(c->cf_path.reserve((size_t)std::min(grid, (k + kCfWaves - 1) / kCfWaves) * kCfWaves * kCfMaxDepth));
     PP_HIP(c->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
     if (!c->lit_locks.p) {  // the literal scratch pool's slot locks (zero: free)
         PP_HIP(c->lit_locks.reserve(kLiteralWaves));
@@ -585,11 +627,9 @@ int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line,
     }
     PP_HIP(launch_check_finish(c->stream, sd, c->cf_scene.p, tr, nodes, k, g->x, g->y,
                                g->yaw, g->yaw_opt, g->level0, g->mode, want_line, o.ok, o.len,
-                               o.npts, o.chain, c->api_lit_scratch.p, c->lit_locks.p,
-                               want_line ? c->cf_pts.p : nullptr, kCfPtsCap,
-                               want_line ? c->cf_etab.p : nullptr, c->cf_err.p, grid,
-                               c->prof ? c->cf_tally.p : nullptr, cb, c->cf_path.p,
-                               want_line ? c->cf_items.p : nullptr));
+                               o.npts, o.chain, c->api_lit_scratch.p, c->lit_locks.p, lines,
+                               c->cf_err.p, grid, c->prof ? c->cf_tally.p : nullptr, cb,
+                               c->cf_path.p, want_line ? c->cf_items.p : nullptr));
     if (c->prof) PP_HIP(hipEventRecord(c->ev[1], c->stream));
     int err = 0;
     PP_HIP(hipMemcpyAsync(&err, c->cf_err.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -620,7 +660,7 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     // phase A: <= span tasks per node; B: <= 2 per node.  The spans are clamped to the task budget
     // (at least 2: phase B's tasks)
     const size_t task_bytes = 3 * sizeof(int) + sizeof(SteerTask) + sizeof(StarTaskExt) +
-                              sizeof(PrepRec) + sizeof(double);
+                              sizeof(double) + 1;
     const int span_cap = (int)std::max<size_t>(2, kCfbTaskBudget / (task_bytes * std::max<size_t>(nn, 1)));
     const int span0 = std::min(c->cfb_span0, span_cap), span1 = std::min(c->cfb_span, span_cap);
     const size_t cap_tasks = std::max<size_t>((size_t)std::max({span0, span1, 2}) * nn, 1);
@@ -628,19 +668,22 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     PP_HIP(c->cf_err.reserve(2));
     PP_HIP(c->cf_memo.reserve(2 * std::max<size_t>(rows, 1)));
     PP_HIP(c->cf_items.reserve(1 + (size_t)total * kCfItem));
-    // cf_line_kernel's workgroups: one line at a time each, a lane per edge generating its points
-    // serially — latency-bound, so more lines in flight than check_finish_kernel's grid
+    // cf_line_kernel's workgroups: one line at a time each — latency-bound, so more lines in
+    // flight than check_finish_kernel's grid
     const int wgs = std::min(kCfLineGrid, total);
-    PP_HIP(c->cf_pts.reserve((size_t)wgs * 3 * kCfPtsCap));
-    PP_HIP(c->cf_etab.reserve((size_t)wgs * 2 * kCfMaxEdges));
-    PP_HIP(c->cf_path.reserve((size_t)wgs * kCfWaves * kCfMaxDepth));
+    CfLines lines;
+    if (wgs > 0) {
+        int r = cf_line_buffers(c, wgs, std::min(total, kCfSpillCap), lines);
+        if (r) return r;
+    }
     PP_HIP(c->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));
     if (!c->lit_locks.p) {
         PP_HIP(c->lit_locks.reserve(kLiteralWaves));
         PP_HIP(hipMemsetAsync(c->lit_locks.p, 0, kLiteralWaves * sizeof(int), st));
     }
     PP_HIP(c->cfb_nodei.reserve(4 * nn));
-    PP_HIP(c->cfb_rows.reserve(3 * std::max<size_t>(rows, 1)));
+    PP_HIP(c->cfb_rows.reserve(std::max<size_t>(rows, 1)));
+    PP_HIP(c->cfb_rows8.reserve(2 * std::max<size_t>(rows, 1)));
     PP_HIP(c->cfb_gotab.reserve(std::max(total, 1)));
     PP_HIP(c->cfb_plist.reserve(std::max(total, 1)));
     PP_HIP(c->cfb_tnode.reserve(cap_tasks));
@@ -648,9 +691,11 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     PP_HIP(c->cfb_lit.reserve(cap_tasks));
     PP_HIP(c->cfb_tasks.reserve(cap_tasks));
     PP_HIP(c->cfb_ext.reserve(cap_tasks));
-    PP_HIP(c->cfb_rec.reserve(cap_tasks));
+    const size_t rec_cap = std::min(cap_tasks, kCfbRecChunk);
+    PP_HIP(c->cfb_rec.reserve(rec_cap));
+    PP_HIP(c->cfb_none.reserve(cap_tasks));
     PP_HIP(c->cfb_yaw.reserve(cap_tasks));
-    PP_HIP(c->cfb_state.reserve(1));
+    PP_HIP(c->cfb_state.reserve(2));  // [0] the round's, [1] a chunk's
     PP_HIP(c->cfb_misc.reserve(4));
     if (c->prof) PP_HIP(c->cfb_pts.reserve(2 * kWalkTallySlots));
     SceneDev sd = c->scene_dev();
@@ -674,8 +719,8 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     a.gtab = c->cf_memo.p + rows;
     a.gotab = c->cfb_gotab.p;
     a.gclaim = c->cfb_rows.p;
-    a.tnone = c->cfb_rows.p + rows;
-    a.tnone_up = c->cfb_rows.p + 2 * rows;
+    a.tnone = c->cfb_rows8.p;
+    a.tnone_up = c->cfb_rows8.p + rows;
     a.depth = c->cfb_nodei.p;
     a.open = c->cfb_nodei.p + nn;
     a.tfirst = c->cfb_nodei.p + 2 * nn;
@@ -684,6 +729,7 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     a.tasks = c->cfb_tasks.p;
     a.ext = c->cfb_ext.p;
     a.rec = c->cfb_rec.p;
+    a.none = c->cfb_none.p;
     a.status = c->cfb_status.p;
     a.yaw = c->cfb_yaw.p;
     a.st = c->cfb_state.p;
@@ -697,7 +743,7 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     PP_HIP(hipMemsetAsync(c->cf_items.p, 0, sizeof(int), st));
     PP_HIP(hipMemsetAsync(c->cf_err.p, 0, 2 * sizeof(int), st));
     PP_HIP(hipMemsetAsync(c->cfb_misc.p, 0, 4 * sizeof(int), st));
-    PP_HIP(hipMemsetAsync(c->cfb_state.p, 0, sizeof(DevState), st));
+    PP_HIP(hipMemsetAsync(c->cfb_state.p, 0, 2 * sizeof(DevState), st));
     if (c->prof) PP_HIP(hipMemsetAsync(c->cfb_pts.p, 0, 2 * kWalkTallySlots * sizeof(long long), st));
     if (c->prof) {
         if (int r = ensure_events(c, 2)) return r;
@@ -710,18 +756,34 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     // round r tests the candidates at depths m0 .. m0 + span - 1 of every open node: the first
     // round cfb_span0 of them, the later ones cfb_span
     long long* wpts = c->prof ? c->cfb_pts.p : nullptr;
+    // a round's steer over its a.st->W (<= mt) tasks, rec_cap records at a time
+    auto steer = [&](int mt, bool own_yaw) -> int {
+        for (size_t base = 0; base < (size_t)mt; base += rec_cap) {
+            const int cn = (int)std::min(rec_cap, (size_t)mt - base);
+            CfbArgs ac = a;
+            ac.st = c->cfb_state.p + 1;
+            ac.tasks += base;
+            ac.ext += base;
+            ac.status += base;
+            ac.yaw += base;
+            PP_HIP(launch_cfb_chunk(st, a.st, ac.st, (int)base, cn, true, nullptr, nullptr));
+            PP_HIP(launch_cfb_steer(st, sd, ac, cn, own_yaw, wpts));
+            PP_HIP(launch_cfb_chunk(st, a.st, ac.st, (int)base, cn, false, ac.rec, a.none + base));
+        }
+        return PP_OK;
+    };
     int rounds = 0;
     for (int m0 = 0; m0 <= misc[0]; ++rounds) {
         a.span = rounds == 0 ? span0 : span1;
         const int mt = (int)std::min<size_t>(cap_tasks, (size_t)a.span * nn);
         PP_HIP(launch_cfb(st, sd, a, kCfbEmitA, m0));
-        PP_HIP(launch_cfb_steer(st, sd, a, mt, false, wpts));
+        if (int r = steer(mt, false)) return r;
         PP_HIP(launch_cfb_literal(st, sd, a, mt, c->cfb_lit.p, c->cfb_misc.p + 3, c->api_lit_scratch.p));
         PP_HIP(launch_cfb(st, sd, a, kCfbConsumeA, m0));
         m0 += a.span;
     }
     PP_HIP(launch_cfb(st, sd, a, kCfbEmitB, 0));
-    PP_HIP(launch_cfb_steer(st, sd, a, (int)std::min<size_t>(cap_tasks, 2 * nn), true, wpts));
+    if (int r = steer((int)std::min<size_t>(cap_tasks, 2 * nn), true)) return r;
     PP_HIP(launch_cfb_literal(st, sd, a, (int)std::min<size_t>(cap_tasks, 2 * nn), c->cfb_lit.p,
                               c->cfb_misc.p + 3, c->api_lit_scratch.p));
     PP_HIP(launch_cfb(st, sd, a, kCfbStoreB, (int)std::min<size_t>(cap_tasks, 2 * nn)));
@@ -735,11 +797,13 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     cb.gtab = a.gtab;
     cb.gotab = a.gotab;
     // the items left (unknown verdicts) on check_finish_kernel, then every line item's points
+    PP_HIP(c->cf_path.reserve((size_t)std::max(1, std::min(kCfGrid, (np + kCfWaves - 1) / kCfWaves)) *
+                              kCfWaves * kCfMaxDepth));
     PP_HIP(launch_check_finish(st, sd, c->cf_scene.p, tr, c->mp_nodes.p, np, 0.0, 0.0, 0.0, 0.0, 0,
                                kCfCheck, 1, o.ok, o.len, o.npts, nullptr, c->api_lit_scratch.p,
-                               c->lit_locks.p, c->cf_pts.p, kCfPtsCap, c->cf_etab.p, c->cf_err.p,
-                               kCfGrid, c->prof ? c->cf_tally.p : nullptr, cb, c->cf_path.p,
-                               c->cf_items.p, c->cfb_plist.p, wgs));
+                               c->lit_locks.p, lines, c->cf_err.p, kCfGrid,
+                               c->prof ? c->cf_tally.p : nullptr, cb, c->cf_path.p, c->cf_items.p,
+                               c->cfb_plist.p));
     if (c->prof) PP_HIP(hipEventRecord(c->ev[1], st));
     int err = 0;
     PP_HIP(hipMemcpyAsync(&err, c->cf_err.p, sizeof(int), hipMemcpyDeviceToHost, st));

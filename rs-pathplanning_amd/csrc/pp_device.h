@@ -52,6 +52,73 @@ struct Word {
     double t, p, q;
 };
 
+// sin and cos of x, |x| < 2^30, bit for bit the values ROCm's __ocml_sincos_f64 returns (its
+// trigredsmall Cody-Waite reduction by pi/2 in three parts and its sincosred2 polynomials, the
+// same operations in the same order; -ffp-contract=off keeps every plain product a product).
+// The walk's arc points call it with |pd| < 2 pi + step (every L/R segment length is a mod2pi
+// value), so the caller routes any other argument to the literal path.  Why not ocml itself:
+// the compiler hoists ocml's 17 f64 constants out of the walk's chunk loop into VGPRs, and at the
+// 6-waves-per-SIMD budget two of them spilled (20 B per lane).  Here they are read
+// through `tab`, a pointer the caller makes opaque inside the loop (scalar loads from the
+// constant cache, re-issued per chunk) — nothing is loop-invariant to hoist.
+// tab: kSinCosTab, in this order: 2/pi, -pi/2 (hi), -pi/2 (mid), pi/2 (mid), -pi/2 (lo), then the
+// cos polynomial c6..c1 and the sin polynomial s5..s2 and s1.
+__device__ inline void sincos_small(double x, const double* __restrict__ tab, double* sp,
+                                    double* cp) {
+    const double ax = fabs(x);
+    // __ocmlpriv_trigredsmall_f64
+    const double q = __builtin_rint(ax * tab[0]);
+    const double a = __builtin_fma(q, tab[1], ax);
+    const double b = __builtin_fma(q, tab[2], a);
+    const double p = q * tab[3];
+    const double pe = __builtin_fma(q, tab[3], -p);
+    const double t9 = a - p;
+    const double t10 = a - t9;
+    const double t11 = t10 - p;
+    const double t12 = t9 - b;
+    const double t13 = t12 + t11;
+    const double t14 = t13 - pe;
+    const double t15 = __builtin_fma(q, tab[4], t14);
+    const double hi = b + t15;
+    const double t17 = hi - b;
+    const double lo = t15 - t17;
+    const int i = (int)q & 3;
+    // __ocmlpriv_sincosred2_f64(hi, lo)
+    const double x2 = hi * hi;
+    const double hx2 = x2 * 0.5;
+    const double c1 = 1.0 - hx2;
+    const double t6 = 1.0 - c1;
+    const double t7 = t6 - hx2;
+    const double x4 = x2 * x2;
+    double pc = __builtin_fma(x2, tab[5], tab[6]);
+    pc = __builtin_fma(x2, pc, tab[7]);
+    pc = __builtin_fma(x2, pc, tab[8]);
+    pc = __builtin_fma(x2, pc, tab[9]);
+    pc = __builtin_fma(x2, pc, tab[10]);
+    const double t15b = __builtin_fma(hi, -lo, t7);
+    const double t16 = __builtin_fma(x4, pc, t15b);
+    const double cv = c1 + t16;
+    double ps = __builtin_fma(x2, tab[11], tab[12]);
+    ps = __builtin_fma(x2, ps, tab[13]);
+    ps = __builtin_fma(x2, ps, tab[14]);
+    ps = __builtin_fma(x2, ps, tab[15]);
+    const double t23 = hi * -x2;
+    const double t24 = lo * 0.5;
+    const double t25 = __builtin_fma(t23, ps, t24);
+    const double t26 = __builtin_fma(x2, t25, -lo);
+    const double t27 = __builtin_fma(t23, tab[16], t26);
+    const double sv = hi - t27;
+    // __ocml_sincos_f64: quadrant and signs (|x| finite here)
+    const unsigned flip = i > 1 ? 0x80000000u : 0u;
+    const bool even = (i & 1) == 0;
+    const double sm = even ? sv : cv;
+    const double cm = even ? cv : -sv;
+    const unsigned long long xs = (unsigned long long)__double_as_longlong(x) & 0x8000000000000000ull;
+    const unsigned long long fl = (unsigned long long)flip << 32;
+    *sp = __longlong_as_double((long long)((unsigned long long)__double_as_longlong(sm) ^ xs ^ fl));
+    *cp = __longlong_as_double((long long)((unsigned long long)__double_as_longlong(cm) ^ fl));
+}
+
 // The six closed forms share sin/cos(alpha), sin/cos(beta) and cos(alpha - beta); each is
 // computed once here (the reference recomputes identical values per word).
 struct Trig {

@@ -120,8 +120,8 @@ struct CfbArgs {
     int* gtab = nullptr;      // rows
     int* gotab = nullptr;     // [nitems]
     int* gclaim = nullptr;    // rows: copy edge claimed for phase B
-    int* tnone = nullptr;     // rows: the node's own tree edge has a None steer
-    int* tnone_up = nullptr;  // rows: any tree edge from the node down to the root has one
+    unsigned char* tnone = nullptr;     // rows: the node's own tree edge has a None steer
+    unsigned char* tnone_up = nullptr;  // rows: any tree edge from the node down to the root has one
     int* depth = nullptr;     // [nitems + Q]
     int* open = nullptr;      // [nitems + Q] phase A: not settled yet
     int* tfirst = nullptr;    // [nitems + Q] the round's first task of the node
@@ -129,7 +129,8 @@ struct CfbArgs {
     int* tnode = nullptr;     // [tasks] phase A: node b; phase B: item b, or -1 - row (copy edge)
     SteerTask* tasks = nullptr;
     StarTaskExt* ext = nullptr;
-    PrepRec* rec = nullptr;
+    PrepRec* rec = nullptr;   // (one chunk of the round's tasks at a time: launch_cfb_chunk)
+    unsigned char* none = nullptr;  // per task: its steer was None (the record's kPrepNone)
     int* status = nullptr;
     double* yaw = nullptr;
     DevState* st = nullptr;   // st->W: the round's task count (ncomp 0)
@@ -143,17 +144,41 @@ hipError_t launch_cfb(hipStream_t s, const SceneDev& sc, CfbArgs a, int phase, i
                       int* err = nullptr, int* items = nullptr, int* plist = nullptr);
 hipError_t launch_cfb_steer(hipStream_t s, const SceneDev& sc, const CfbArgs& a, int max_tasks,
                             bool own_yaw, long long* wg_points = nullptr);
+// a chunk of a round's steer: begin (the chunk's task count from the round's) or, after its walk,
+// the None flags of its records into none[0, chunk->W)
+hipError_t launch_cfb_chunk(hipStream_t s, const DevState* all, DevState* chunk, int base,
+                            int cap, bool begin, const PrepRec* rec, unsigned char* none);
 // the rounds' literal-path tasks re-run by steer_collide_literal (a scratch slot per wave)
 hipError_t launch_cfb_literal(hipStream_t s, const SceneDev& sc, const CfbArgs& a, int max_tasks,
                               int* list, int* count, double* lit_scratch);
+// cf_line_kernel's per-workgroup buffers: pts (3 x pts_cap doubles: x, y, hypots / words), etab
+// (2 x (path_cap + kCfLevels + 1) ints) and path (path_cap ints) per workgroup.  spill != null
+// (tier 1): a line deeper than path_cap or longer than pts_cap is appended to spill (the items
+// layout, spill[0] its count, zeroed before the launch) instead of failing, and tier 2 — the full
+// capacities (kCfMaxDepth, kCfPtsCap) on a few workgroups — runs the spill list
+struct CfLineBufs {
+    double* pts = nullptr;
+    int pts_cap = 0;
+    int* etab = nullptr;
+    int* path = nullptr;
+    int path_cap = kCfMaxDepth;
+    int* spill = nullptr;
+    int spill_cap = 0;
+};
+struct CfLines {
+    int grid1 = 0;  // 0: no line kernel
+    CfLineBufs t1;
+    int grid2 = 0;  // tier 2 (when t1.spill)
+    CfLineBufs t2;
+};
 hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const SceneDev* scg,
                                const TreeDev& tr,
                                const int* nodes, int k, double gx, double gy, double gyaw,
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,
-                               int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
-                               int grid, long long* tally, const CfBatch& cb, int* gpath,
-                               int* items, const int* blist = nullptr, int line_grid = 0);
+                               int* lit_locks, const CfLines& lines, int* err, int grid,
+                               long long* tally, const CfBatch& cb, int* gpath, int* items,
+                               const int* blist = nullptr);
 constexpr int kCfWaves = 4;                     // check_finish: waves (nodes in flight) per workgroup
 constexpr int kCfItem = 4 + kCfLevels;          // a line item: b, s, verified, 0, pos[kCfLevels]
 

@@ -948,6 +948,15 @@ __device__ inline Top2 merge_top2(Top2 a, Top2 c) {
     return r;
 }
 
+// sincos_small's constants (pp_device.h): __ocml_sincos_f64's, bit for bit
+__constant__ double kSinCosTab[17] = {
+    0x1.45f306dc9c883p-1,  -0x1.921fb54442d18p+0,  -0x1.1a62633145c00p-54,
+    0x1.1a62633145c00p-54, -0x1.b839a252049c0p-104,
+    -0x1.907db46cc5e42p-37, 0x1.1eeb69037ab78p-29, -0x1.27e4fa17f65f6p-22,
+    0x1.a01a019f4ec90p-16,  -0x1.6c16c16c16967p-10, 0x1.5555555555555p-5,
+    0x1.5e0b2f9a43bb8p-33,  -0x1.ae600b42fdfa7p-26, 0x1.71de3796cde01p-19,
+    -0x1.a01a019e83e5cp-13, 0x1.1111111110bb3p-7,   -0x1.5555555555555p-3};
+
 __device__ __forceinline__ float scan_d2(float qx, float qy, float nx, float ny) {
     const float dx = qx - nx, dy = qy - ny;
     return __builtin_fmaf(dy, dy, dx * dx);
@@ -2538,6 +2547,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         double qx = carry_x, qy = carry_y;
         int mm = kModeS;
         bool pop_more = false;  // the popped point's local x is 0.0 too: the trim goes on
+        bool bad_arg = false;   // an arc point's pd outside sincos_small's range
         if (isgen) {
             const double* row = segt + kSegRow * my_seg;
             const double2 o2 = *reinterpret_cast<const double2*>(row);
@@ -2551,8 +2561,14 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                 lx = ox + pc * ca;
                 ly = oy + pc * sa;
             } else {
+                // one argument reduction for both (walk -2..3%): ocml's own sincos, restated with
+                // its constants behind an opaque pointer (sincos_small: no hoisted, spilled
+                // coefficients); |pd| >= 2^30 (never on an L / R segment) goes to the literal path
+                const double* tab = kSinCosTab;
+                asm volatile("" : "+s"(tab));
+                bad_arg = !(fabs(pd) < 0x1p30);
                 double sp, cp;
-                sincos(pd, &sp, &cp);  // one argument reduction for both (walk −2..3%)
+                sincos_small(pd, tab, &sp, &cp);
                 const double ldx = div_by(sp, c, rc);
                 const double ld1 = div_by(1.0 - cp, c, rc);  // (1 - cos) / -c = -((1 - cos) / c)
                 const double ldy = mm == kModeL ? ld1 : -ld1;
@@ -2569,7 +2585,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
             qx = px;
             qy = py;
         }
-        if (__any(pop_more)) return kLiteral;
+        if (__any(pop_more || bad_arg)) return kLiteral;
         const bool has = lane == 0 || isgrid || isj;
         const bool chk = isgrid || isj || (base == 0 && lane == 0);
         npts += cnt + (junction && junction_here ? 1 : 0);
@@ -3532,12 +3548,13 @@ __device__ inline void cf_node_setup(const TreeDev& tr_in, const CfBatch& cb, in
 
 // A node's ancestor path root first into path[0, D) (NodeIter, rrt.rs:253-265, reversed), by the
 // calling wave (lane 0 follows the parents, then the lanes reverse it); -1 past kCfMaxDepth.
-__device__ inline int cf_path(const TreeDev& tr, int node, int* __restrict__ path) {
+__device__ inline int cf_path(const TreeDev& tr, int node, int* __restrict__ path,
+                              int cap = kCfMaxDepth) {
     const int lane = __lane_id();
     int d = 0;
     if (lane == 0) {
         int c = node;
-        while (c >= 0 && d < kCfMaxDepth) {
+        while (c >= 0 && d < cap) {
             path[d++] = c;
             c = tr.parent[c];
         }
@@ -3971,19 +3988,35 @@ __device__ int line_edge_wave(double sx, double sy, double syaw, const double* _
 // edge's literal Dubins points (line_edge_wave, a wave per edge) into the workgroup's pts / etab,
 // then l.reverse() and geo's euclidean_length in that order (rrt.rs:538: the hypots in parallel,
 // their sum in line order).
+// a line item past tier 1's capacities onto the spill list (all 64 lanes of the item's wave)
+// (past the list's capacity: the point-capacity error)
+__device__ inline void cf_spill(const CfLineBufs& lb, const int* __restrict__ o, int tid,
+                                int* __restrict__ err) {
+    int w = 0;
+    if (tid == 0) w = atomicAdd(&lb.spill[0], 1);
+    w = __shfl(w, 0);
+    if (w >= lb.spill_cap) {
+        if (tid == 0) atomicOr(err, 8);
+    } else if (tid < kCfItem) {
+        lb.spill[1 + (size_t)w * kCfItem + tid] = o[tid];
+    }
+}
+
 __global__ __launch_bounds__(kCfLineThreads) void cf_line_kernel(
     SceneDev sc, TreeDev tr_in, const int* __restrict__ nodes, double gx_in, double gy_in,
     double gyaw_in, double gyaw_opt_in, int* __restrict__ ok_out, double* __restrict__ len_out,
-    int* __restrict__ npts_out, double* __restrict__ pts, int pts_cap, int* __restrict__ etab,
-    int* __restrict__ err, CfBatch cb, int* __restrict__ gpath, const int* __restrict__ items) {
+    int* __restrict__ npts_out, CfLineBufs lb, int* __restrict__ err, CfBatch cb,
+    const int* __restrict__ items) {
     __shared__ int s_off, s_bad;
     __shared__ int s_pos[kCfLevels];
     const int tid = threadIdx.x;
-    double* px = pts + (size_t)blockIdx.x * 3 * pts_cap;
+    // this workgroup's buffers: points (x, y, hypots / words), edge table, ancestor path
+    const int pts_cap = lb.pts_cap;
+    double* px = lb.pts + (size_t)blockIdx.x * 3 * pts_cap;
     double* py = px + pts_cap;
     double* pyw = py + pts_cap;
-    int* et = etab + (size_t)blockIdx.x * 2 * kCfMaxEdges;
-    int* path = gpath + (size_t)blockIdx.x * kCfWaves * kCfMaxDepth;  // (wave 0's region)
+    int* et = lb.etab + (size_t)blockIdx.x * 2 * (lb.path_cap + kCfLevels + 1);
+    int* path = lb.path + (size_t)blockIdx.x * lb.path_cap;
     const int n_items = items[0];
     for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
         const int* o = items + 1 + (size_t)it * kCfItem;
@@ -3997,10 +4030,22 @@ __global__ __launch_bounds__(kCfLineThreads) void cf_line_kernel(
         cf_node_setup(tr_in, cb, b, gx_in, gy_in, gyaw_in, gyaw_opt_in, sc.root_blocked, tr, gx,
                       gy, gyaw, gyaw_opt, root_blocked);
         int D = 0;
-        if (tid < 64) D = cf_path(tr, nodes[b], path);
+        if (tid < 64) D = cf_path(tr, nodes[b], path, lb.path_cap);
         if (tid == 0) s_off = D;
         __syncthreads();
         D = s_off;
+        // tier 1: a path deeper than this tier's capacity goes to tier 2 (the spill list); at the
+        // full capacity it is check_finish_kernel's depth error
+        if (D < 0) {
+            if (lb.spill) {
+                cf_spill(lb, o, tid, err);
+            } else if (tid == 0) {
+                ok_out[b] = 0;
+                atomicOr(err, 1);
+            }
+            __syncthreads();
+            continue;
+        }
         LT(1)
         const double gyaw_e = s > 0 ? gyaw_opt : gyaw;
         const int ps = s > 0 ? pos[s - 1] : D - 1;
@@ -4041,12 +4086,18 @@ __global__ __launch_bounds__(kCfLineThreads) void cf_line_kernel(
                 off += c > 0 ? c : 0;
             }
             // a None steer is finalize's panic (rrt.rs:529); an overflowing count or a line
-            // past the point capacity is the capacity error
-            s_off = none ? -2 : (off <= pts_cap && !neg) ? off : -1;
+            // past the point capacity is the capacity error — in tier 1, a line longer than the
+            // tier's capacity goes to tier 2 (-3)
+            s_off = none ? -2 : neg ? -1 : off <= pts_cap ? off : lb.spill ? -3 : -1;
         }
         __syncthreads();
         const int total = s_off;
         LT(2)
+        if (total == -3) {  // spilled: tier 2 writes this item's outputs
+            cf_spill(lb, o, tid, err);
+            __syncthreads();
+            continue;
+        }
         if (total < 0) {
             if (tid == 0) s_bad = total == -2 ? 2 : 8;
         } else {
@@ -4166,20 +4217,26 @@ hipError_t launch_check_finish(hipStream_t st, const SceneDev& sc, const SceneDe
                                const int* nodes, int k, double gx, double gy, double gyaw,
                                double gyaw_opt, int level0, int mode, int want_line, int* ok,
                                double* len, int* npts, int* chain, double* lit_scratch,
-                               int* lit_locks, double* pts, int pts_cap, int* etab, int* err,
-                               int grid, long long* tally, const CfBatch& cb, int* gpath,
-                               int* items, const int* blist, int line_grid) {
-    if (k <= 0 && line_grid <= 0) return hipSuccess;
+                               int* lit_locks, const CfLines& lines, int* err, int grid,
+                               long long* tally, const CfBatch& cb, int* gpath, int* items,
+                               const int* blist) {
+    if (k <= 0 && lines.grid1 <= 0) return hipSuccess;
     const int wgs = std::min(grid, (k + kCfWaves - 1) / kCfWaves);
     if (k > 0)
         check_finish_kernel<<<wgs, kCfThreads, 0, st>>>(scg, tr, nodes, k, gx, gy, gyaw, gyaw_opt,
                                                         level0, mode, want_line, ok, len, npts,
                                                         chain, lit_scratch, lit_locks, err, tally,
                                                         cb, gpath, items, blist);
-    if (want_line && mode != kCfOptimize)
-        cf_line_kernel<<<line_grid > 0 ? line_grid : std::min(grid, k), kCfLineThreads, 0, st>>>(
-            sc, tr, nodes, gx, gy, gyaw, gyaw_opt, ok, len, npts, pts, pts_cap, etab, err, cb,
-            gpath, items);
+    if (want_line && mode != kCfOptimize && lines.grid1 > 0) {
+        cf_line_kernel<<<lines.grid1, kCfLineThreads, 0, st>>>(sc, tr, nodes, gx, gy, gyaw,
+                                                               gyaw_opt, ok, len, npts, lines.t1,
+                                                               err, cb, items);
+        if (lines.t1.spill)  // the lines past tier 1's capacities, at the full ones
+            cf_line_kernel<<<lines.grid2, kCfLineThreads, 0, st>>>(sc, tr, nodes, gx, gy, gyaw,
+                                                                   gyaw_opt, ok, len, npts,
+                                                                   lines.t2, err, cb,
+                                                                   lines.t1.spill);
+    }
     return hipGetLastError();
 }
 
@@ -4297,7 +4354,7 @@ __global__ __launch_bounds__(256) void cfb_depth_kernel(CfbArgs a, SceneDev sc) 
         const CfPose to{a.tr.x[o + p], a.tr.y[o + p], a.tr.yaw[o + p]};
         none = cf_npoint(sc, from, to) == 0 ? 1 : 0;
     }
-    a.tnone[o + c] = none;
+    a.tnone[o + c] = (unsigned char)none;
 }
 
 // tnone_up[c]: any tree edge from c down to the root has a None steer
@@ -4309,7 +4366,7 @@ __global__ __launch_bounds__(256) void cfb_tnone_up_kernel(CfbArgs a) {
     const size_t o = (size_t)q * a.row_cap;
     int any = 0;
     for (int k = c; k > 0; k = a.tr.parent[o + k]) any |= a.tnone[o + k];
-    a.tnone_up[o + c] = any;
+    a.tnone_up[o + c] = (unsigned char)any;
 }
 
 // a thread's task count -> its first task index: one atomic per 256-thread workgroup on the
@@ -4389,7 +4446,7 @@ __global__ __launch_bounds__(256) void cfb_consume_a_kernel(CfbArgs a, int m0) {
         const int s = a.status[t0 + i];
         if (s == kReject) continue;
         if (s == kAccept) {
-            const int fnone = a.rec[t0 + i].state == kPrepNone ? 1 : 0;
+            const int fnone = a.none[t0 + i];
             a.ftab[o + c] = (2 + m0 + i) | (fnone << 30);
         }
         a.open[b] = 0;
@@ -4513,7 +4570,7 @@ __global__ __launch_bounds__(256) void cfb_store_b_kernel(CfbArgs a) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.st->W) return;
     int s = a.status[t];
-    if (a.rec[t].state == kPrepNone) s = kCfPanic;
+    if (a.none[t]) s = kCfPanic;
     else if (s != kAccept && s != kReject) return;
     const int n = a.tnode[t];
     if (n >= 0)
@@ -4656,6 +4713,33 @@ hipError_t launch_cfb(hipStream_t s, const SceneDev& sc, CfbArgs a, int phase, i
         default:
             return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// the steer rounds' records in chunks of `cap` tasks: chunk [base, base + cap) of the round's
+// a.st->W tasks gets its own task count (cfb_chunk_begin), and after its walk the None flags of
+// its records (consume A / store B read them once every chunk's record is overwritten)
+__global__ void cfb_chunk_begin_kernel(const DevState* __restrict__ all, DevState* __restrict__ chunk,
+                                       int base, int cap) {
+    const int w = all->W - base;
+    chunk->W = w < 0 ? 0 : (w < cap ? w : cap);
+    chunk->ncomp = 0;
+    chunk->alist = nullptr;
+}
+
+__global__ __launch_bounds__(256) void cfb_chunk_none_kernel(const DevState* __restrict__ chunk,
+                                                             const PrepRec* __restrict__ rec,
+                                                             unsigned char* __restrict__ none) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < chunk->W) none[t] = rec[t].state == kPrepNone ? 1 : 0;
+}
+
+hipError_t launch_cfb_chunk(hipStream_t s, const DevState* all, DevState* chunk, int base,
+                            int cap, bool begin, const PrepRec* rec, unsigned char* none) {
+    if (begin)
+        cfb_chunk_begin_kernel<<<1, 1, 0, s>>>(all, chunk, base, cap);
+    else
+        cfb_chunk_none_kernel<<<(cap + 255) / 256, 256, 0, s>>>(chunk, rec, none);
     return hipGetLastError();
 }
 

@@ -15,7 +15,7 @@ IFS=';' read -ra JOBS <<< "$RUNS"
 for rep in ${REPS:-1}; do
   for j in "${JOBS[@]}"; do
     IFS='|' read -r name var args <<< "$j"
-    f="$OUT/${name}_$rep"
+    f="$OUT/${name}_${var}_$rep"
     if [ "$var" = base ]; then
       echo "python -u bench.py $args" > "$f.cmd"
       timeout -k 10 ${LIMIT:-400} python -u bench.py $args > "$f.json" 2> "$f.err" || { echo "FAILED $name"; tail -20 "$f.err"; exit 1; }
