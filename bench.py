@@ -284,6 +284,16 @@ def host_info():
                                "SURVEY.md K7); the CPU baseline is the build's C port (oracle/)"}
 
 
+def device_free_bytes(device):
+    """free device memory (hipMemGetInfo through torch, the process's one HIP runtime), or None"""
+    try:
+        import torch
+
+        return int(torch.cuda.mem_get_info(device)[0])
+    except Exception:
+        return None
+
+
 def oracle_mod():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # noqa: E402  (cpu_baseline leg: the oracle is the timed CPU port here)
@@ -594,11 +604,14 @@ def run_batch(args, D, star, with_cpu):
     if not star:
         # RRT::plan of every query (check_finish of every accepted node, the first minimum
         # length): the per-query record of SURVEY §8e — (ok, n_nodes, path_len, cost, iterations)
+        free0 = device_free_bytes(D.device)
         D.barrier()
         t0 = time.perf_counter()
         pr = batch.plan()
         t_plan_local = time.perf_counter() - t0
         D.barrier()
+        # the plan's device reservations (its buffers stay with the batch's context)
+        plan_reserved = None if free0 is None else free0 - device_free_bytes(D.device)
         t_plan = D.allreduce(t_plan_local, "max")
         cols += [(pr["best_node"] >= 0).astype(np.int64), pr["best_node"].astype(np.int64),
                  pr["n_points"].astype(np.int64), pr["length"].view(np.int64),
@@ -622,6 +635,7 @@ def run_batch(args, D, star, with_cpu):
             "queries_with_path": int(ok.sum()),
             "finishes_total": int(allrec[:, 8].sum()),
             "mean_length": round(float(lens.mean()), 4) if len(lens) else None,
+            "device_reserved_mb": None if plan_reserved is None else round(plan_reserved / 2**20, 1),
             "record": "per query: (query, iterations, n_nodes, tree digest, ok, best node, "
                       "path points, length bits, finishes), gathered with the extend records",
         }
@@ -1032,6 +1046,7 @@ def _short_sub(name, r):
     if isinstance(r.get("plan"), dict):  # config 3's batch RRT::plan
         pl = r["plan"]
         s["plan"] = {"value": pl.get("value"), "check_finish_ms": pl.get("check_finish_ms"),
+                     "device_reserved_mb": pl.get("device_reserved_mb"),
                      "cpu_same_answer": (pl.get("cpu_baseline") or {}).get("same_answer")}
     if isinstance(r.get("passes"), dict):
         s["steps"] = r["passes"].get("steps")
@@ -1059,6 +1074,7 @@ def compact_line(line, detail_path=None, with_subs=True):
     if not with_subs and "records_digest" in line and isinstance(line.get("plan"), dict):
         pl = line["plan"]  # a config-3 line's batch RRT::plan
         head["plan"] = {"value": pl.get("value"), "check_finish_ms": pl.get("check_finish_ms"),
+                        "device_reserved_mb": pl.get("device_reserved_mb"),
                         "frac": (pl.get("roofline") or {}).get("frac"),
                         "cpu_same_answer": (pl.get("cpu_baseline") or {}).get("same_answer")}
     st = line.get("stats")

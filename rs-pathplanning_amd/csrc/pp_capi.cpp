@@ -518,8 +518,10 @@ static_assert(4 * kCfMaxEdges <= kCfPtsCap, "cf_line_kernel keeps 4 doubles per 
 // room for kCfLinePts1 points and a kCfLinePath1-deep path each (3 x 8192 doubles: 192 KB; the
 // config-3 plan's lines have ~2350 points), tier 2 the few longer or deeper ones at the full
 // capacities (kCfPtsCap points, kCfMaxDepth) on kCfLineGrid2 workgroups (1.5 MB each).  Round 5
-// gave every one of 2048 workgroups the full capacity: 3.2 GB.
-constexpr int kCfLineGrid = 1024;
+// gave every one of 2048 workgroups the full capacity: 3.2 GB.  1024 tier-1
+// workgroups (200 MB) cost the config-3 plan ~0.5 ms of its 12.5 (one wave per line: the lines in
+// flight are the workgroups), so the grid stays at 2048 (400 MB).
+constexpr int kCfLineGrid = 2048;
 constexpr int kCfLinePts1 = 8192;
 constexpr int kCfLinePath1 = 1024;
 constexpr int kCfLineGrid2 = 64;
@@ -530,7 +532,7 @@ static_assert(4 * (kCfLinePath1 + kCfLevels + 1) <= kCfLinePts1, "tier 1: 4 doub
 // spans change which candidates are walked together, never a result); the records (PrepRec,
 // 256 B a task) are steered in chunks of kCfbRecChunk tasks
 constexpr size_t kCfbTaskBudget = (size_t)512 << 20;
-constexpr size_t kCfbRecChunk = (size_t)1 << 19;
+constexpr size_t kCfbRecChunk = (size_t)1 << 20;
 
 // check_finish for nodes[0, k) (device pointer already filled); results on the device
 // The goal of a check_finish_kernel launch: the planner's (check_finish), or a caller-built goal
@@ -584,7 +586,9 @@ int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line,
     // optimize's memo: two ints per tree row (the batch's Q * row_cap rows, or the tree's nodes),
     // zeroed for this launch
     CfBatch cb = cb_in;
-    const size_t rows = cb.qidx ? (size_t)c->mq_Q * (size_t)cb.row_cap : (size_t)c->n;
+    // (a batch's memo rows are compact: its items plus a root per query)
+    const size_t rows = cb.qidx ? (cb.moff ? (size_t)k + c->mq_Q : (size_t)c->mq_Q * (size_t)cb.row_cap)
+                                : (size_t)c->n;
     PP_HIP(c->cf_memo.reserve(2 * std::max<size_t>(rows, 1)));
     PP_HIP(hipMemsetAsync(c->cf_memo.p, 0, 2 * rows * sizeof(int), c->stream));
     cb.ftab = c->cf_memo.p;
@@ -656,7 +660,7 @@ int cf_run(pp_ctx* c, const TreeDev& tr, const int* nodes, int k, int want_line,
 int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in, const CfOut& o) {
     const int Q = c->mq_Q;
     const size_t nn = (size_t)total + Q;
-    const size_t rows = (size_t)Q * (size_t)cb_in.row_cap;
+    const size_t rows = nn;  // the compact memo rows (cb_in.moff): every item and root
     // phase A: <= span tasks per node; B: <= 2 per node.  The spans are clamped to the task budget
     // (at least 2: phase B's tasks)
     const size_t task_bytes = 3 * sizeof(int) + sizeof(SteerTask) + sizeof(StarTaskExt) +
@@ -715,6 +719,7 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     a.qidx = cb_in.qidx;
     a.nodes = c->mp_nodes.p;
     a.goals = cb_in.goals;
+    a.moff = cb_in.moff;
     a.ftab = c->cf_memo.p;
     a.gtab = c->cf_memo.p + rows;
     a.gotab = c->cfb_gotab.p;
@@ -1640,6 +1645,21 @@ struct SampleSrc {
     bool pretest;  // the obstacle pre-test may settle a sample without its nearest node
 };
 
+#ifdef PP_FIN_STAMPS
+// diagnostic builds: append the last nn_finalize launch's phase stamps (per workgroup) to
+// gpurun_out/fin_stamps.txt, one line per batch of windows: tree size, windows, then the stamps
+void dump_fin_stamps(int64_t n, int nw) {
+    std::vector<unsigned long long> v(kFinStampSlots * kFinStampWGs);
+    if (fin_stamps_copy(v.data(), v.size()) != hipSuccess) return;
+    FILE* f = std::fopen("gpurun_out/fin_stamps.txt", "a");
+    if (!f) return;
+    std::fprintf(f, "%lld %d", (long long)n, nw);
+    for (unsigned long long x : v) std::fprintf(f, " %llu", x);
+    std::fprintf(f, "\n");
+    std::fclose(f);
+}
+#endif
+
 int rrt_extend_impl(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted, const SampleSrc* src,
                     double eps) {
     int r;
@@ -1711,6 +1731,9 @@ int rrt_extend_impl(pp_ctx* ctx, int64_t n_iter, int64_t* n_accepted, const Samp
         }
         ctx->it = s.it;
         ctx->n = s.n;
+#ifdef PP_FIN_STAMPS
+        dump_fin_stamps(ctx->n, nw);
+#endif
     }
     if (n_accepted) *n_accepted = ctx->n - n_before;
     return PP_OK;
@@ -2452,6 +2475,7 @@ int pp_batch_plan(pp_ctx* ctx, int32_t* best_node, double* length, int32_t* n_po
         cb.row_cap = ctx->mq_cap;
         cb.goals = ctx->mq_goal_d.p;
         cb.blocked = ctx->mq_any_blocked ? ctx->mq_blocked.p : nullptr;
+        cb.moff = ctx->mp_off.p;  // compact memo rows
         TreeDev tr{};  // the batch's SoA rows (query q: offset q * mq_cap, cb.row_cap)
         tr.x = ctx->mq_x.p;
         tr.y = ctx->mq_y.p;

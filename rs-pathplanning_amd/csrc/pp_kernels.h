@@ -60,6 +60,12 @@ struct WindowArgs {
 // events: before the window kernel, then after it, nn_finalize, steer_prep and steer_walk.
 hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int64_t seq,
                          int resolve_prev);
+// PP_FIN_STAMPS diagnostic builds: nn_finalize's wall-clock phase stamps per workgroup
+constexpr int kFinStampSlots = 10, kFinStampWGs = 512;
+#ifdef PP_FIN_STAMPS
+hipError_t fin_stamps_copy(unsigned long long* out, size_t n);
+#endif
+
 // Resolve and commit the last enqueued window (seq_next - 1): ends a batch.
 hipError_t launch_drain(hipStream_t s, const WindowArgs& a, int64_t seq_next);
 
@@ -101,6 +107,9 @@ struct CfBatch {
     int* gtab = nullptr;
     // the batch plan's goal-edge verdicts per item (0 unknown, else 1 + verdict; may be null)
     const int* gotab = nullptr;
+    // compact memo rows (may be null: q * row_cap): query q's nodes at moff[q] + q, moff = the
+    // exclusive scan of the queries' items (n_q - 1)
+    const int* moff = nullptr;
 };
 
 // check_finish of a query batch in steer rounds (pp_batch_plan, see pp_kernels.hip): phase A
@@ -116,6 +125,7 @@ struct CfbArgs {
     const int* qidx = nullptr;
     const int* nodes = nullptr;
     const double* goals = nullptr;
+    const int* moff = nullptr;  // compact memo rows: query q's nodes at moff[q] + q
     int* ftab = nullptr;      // rows (the memo of CfBatch)
     int* gtab = nullptr;      // rows
     int* gotab = nullptr;     // [nitems]

@@ -1687,6 +1687,22 @@ __device__ inline Top2 wave_top2(Top2 t) {
     return top2_swap<true>(t);
 }
 
+#ifdef PP_FIN_STAMPS  // diagnostic builds only: wall-clock phase stamps of nn_finalize per workgroup
+__device__ unsigned long long g_fin_stamps[kFinStampSlots * kFinStampWGs];
+#define FS(k)                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < kFinStampWGs)                                 \
+        g_fin_stamps[kFinStampSlots * blockIdx.x + (k)] = wall_clock64();
+#define FSW(k)                                                                         \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < kFinStampWGs)                         \
+        atomicMax(&g_fin_stamps[kFinStampSlots * blockIdx.x + (k)], wall_clock64());
+hipError_t fin_stamps_copy(unsigned long long* out, size_t n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fin_stamps), n * sizeof(unsigned long long));
+}
+#else
+#define FS(k)
+#define FSW(k)
+#endif
+
 // 8 waves per SIMD (<= 64 VGPRs): two 1024-thread workgroups per CU, so the extra sampling
 // workgroup (the grid's last) runs beside the others instead of waiting for a CU to drain.
 __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
@@ -1710,6 +1726,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
     __shared__ double s_rd[kFinWaves];
     __shared__ int s_ri[kFinWaves];
     __shared__ float2 s_dn[kFinDelta];   // nodes appended after the screen's snapshot (f32)
+    FS(0)
     const bool voided = st->void_seq == seq || st->error;
     if (gen_next && blockIdx.x == gridDim.x - 1) {
         // the extra workgroup: Space::rand_point of the window after this one, into the parity
@@ -1720,6 +1737,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
         __shared__ __attribute__((aligned(16))) char s_gen[kSamplesLds];
         const int64_t start = voided ? st->it_spec : st->wsp[p] + st->Wp[p];
         samples_role(st, gen, 1 - p, start, s_gen);
+        FS(9)
         return;
     }
     const int W = voided ? 0 : st->Wp[p];
@@ -1744,6 +1762,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
     if (tid < kFinSamples) s_pc[tid] = 0;
     if (tid == 0) s_fmask = 0;
     __syncthreads();
+    FS(1)
     // ---- 1. the sample's nearest node
     if (in) {
         const int n_chunks = scan_chunks_used(ns, chunks);
@@ -1759,6 +1778,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
             ci = pidx[o];
             t = Top2{(float)((double)cb + qq), (float)((double)cs + qq), ci};
         }
+        FSW(2)
         const double xq = qx[q], yq = qy[q];
         const float fx = (float)xq, fy = (float)yq;
         for (int k = lane; k < D; k += 64) {  // appended nodes: exact top-2 per lane
@@ -1791,10 +1811,12 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
                 if (t.s < __builtin_inff()) flag = !((double)t.s - (double)t.b > 2.0 * E);
             }
         }
+        FSW(3)
         if (!flag) {
             const int bi = t.i;
             const double dx = xq - X[bi], dy = yq - Y[bi];
             const double bd = dx * dx + dy * dy;
+            FSW(4)
             if (lane == 0) {
                 out_idx[q] = bi;
                 out_d2[q] = bd;
@@ -1860,6 +1882,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
         }
     }
     __syncthreads();
+    FS(5)
     // near-ties: the workgroup's exact f64 brute force, over the screen chunks whose f32 minimum
     // could hide the exact nearest (f32 distance within the rounding bound of the f32 winner)
     // and over the appended nodes; lowest index on exact ties (rrt.rs:378-391, Q9)
@@ -1913,6 +1936,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
         __syncthreads();
     }
     if (!cand) return;  // nearest-only launch (no window)
+    FS(6)
     // ---- 2. window pairs
     {
         // wave w: sample j = q0 + w against the window samples i < j of the Morton cells its
@@ -1955,6 +1979,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
         }
     }
     __syncthreads();
+    FS(7)
     if (wave == 0) {
         const int j = q0 + lane;
         const bool jin = lane < kFinSamples && j < W;
@@ -1979,6 +2004,7 @@ __global__ __launch_bounds__(kFinThreads, 8) void nn_finalize_kernel(
             const uint64_t bm = __ballot(jin && blk[j]);
             if (lane == 0 && bm) atomicAdd((unsigned long long*)&st->blocked, (unsigned long long)__popcll(bm));
         }
+        FS(8)
     }
 }
 
@@ -3541,8 +3567,10 @@ __device__ inline void cf_node_setup(const TreeDev& tr_in, const CfBatch& cb, in
         gy = cb.goals[3 * q + 1];
         gyaw = gyaw_opt = cb.goals[3 * q + 2];
         root_blocked = cb.blocked ? cb.blocked[q] : 0;
-        if (ftab && *ftab) *ftab += o;
-        if (gtab && *gtab) *gtab += o;
+        // the memo rows are compact: query q's n_q nodes at mo(q) = its items before + q
+        const size_t m = cb.moff ? (size_t)cb.moff[q] + q : o;
+        if (ftab && *ftab) *ftab += m;
+        if (gtab && *gtab) *gtab += m;
     }
 }
 
@@ -4324,6 +4352,12 @@ hipError_t launch_mq_plan_reduce(hipStream_t s, int Q, const int* off, const int
 // of precedence (a panic anywhere wins over a rejection; verify decides the rest).
 
 // phase A node list: b < nitems is item b (qidx[b], nodes[b]); b - nitems < Q is query's root
+// query q's first memo row: the memo tables are compact, q's n_q nodes after the nodes of the
+// queries before it (their items plus their roots)
+__device__ inline size_t cfb_memo_row(const CfbArgs& a, int q) {
+    return (size_t)a.moff[q] + q;
+}
+
 __device__ inline void cfb_node(const CfbArgs& a, int b, int& q, int& c) {
     if (b < a.nitems) {
         q = a.qidx[b];
@@ -4354,7 +4388,7 @@ __global__ __launch_bounds__(256) void cfb_depth_kernel(CfbArgs a, SceneDev sc) 
         const CfPose to{a.tr.x[o + p], a.tr.y[o + p], a.tr.yaw[o + p]};
         none = cf_npoint(sc, from, to) == 0 ? 1 : 0;
     }
-    a.tnone[o + c] = (unsigned char)none;
+    a.tnone[cfb_memo_row(a, q) + c] = (unsigned char)none;
 }
 
 // tnone_up[c]: any tree edge from c down to the root has a None steer
@@ -4365,8 +4399,9 @@ __global__ __launch_bounds__(256) void cfb_tnone_up_kernel(CfbArgs a) {
     cfb_node(a, b, q, c);
     const size_t o = (size_t)q * a.row_cap;
     int any = 0;
-    for (int k = c; k > 0; k = a.tr.parent[o + k]) any |= a.tnone[o + k];
-    a.tnone_up[o + c] = (unsigned char)any;
+    const size_t m = cfb_memo_row(a, q);
+    for (int k = c; k > 0; k = a.tr.parent[o + k]) any |= a.tnone[m + k];
+    a.tnone_up[m + c] = (unsigned char)any;
 }
 
 // a thread's task count -> its first task index: one atomic per 256-thread workgroup on the
@@ -4440,20 +4475,19 @@ __global__ __launch_bounds__(256) void cfb_consume_a_kernel(CfbArgs a, int m0) {
     if (cnt == 0) return;
     int q, c;
     cfb_node(a, b, q, c);
-    const size_t o = (size_t)q * a.row_cap;
     const int t0 = a.tfirst[b];
     for (int i = 0; i < cnt; ++i) {
         const int s = a.status[t0 + i];
         if (s == kReject) continue;
         if (s == kAccept) {
             const int fnone = a.none[t0 + i];
-            a.ftab[o + c] = (2 + m0 + i) | (fnone << 30);
+            a.ftab[cfb_memo_row(a, q) + c] = (2 + m0 + i) | (fnone << 30);
         }
         a.open[b] = 0;
         return;
     }
     if (m0 + cnt > a.depth[b]) {
-        a.ftab[o + c] = 1;
+        a.ftab[cfb_memo_row(a, q) + c] = 1;
         a.open[b] = 0;
     }
 }
@@ -4461,14 +4495,14 @@ __global__ __launch_bounds__(256) void cfb_consume_a_kernel(CfbArgs a, int m0) {
 // an item's optimize chain from ftab (check_finish_kernel's level loop): n[0] = the item's node,
 // n[l + 1] = its level-l candidate (pos[l] = that node's depth); false when an entry on the way
 // is unknown
-__device__ inline bool cfb_chain(const CfbArgs& a, size_t o, int c, int d, int* n, int* pos,
-                                 int& s, int& fnone) {
+__device__ inline bool cfb_chain(const CfbArgs& a, size_t o, size_t mr, int c, int d, int* n,
+                                 int* pos, int& s, int& fnone) {
     s = 0;
     fnone = 0;
     n[0] = c;
     int cur = c, curd = d;
     for (int level = 0; level < kCfLevels; ++level) {
-        const int fm = a.ftab[o + cur];
+        const int fm = a.ftab[mr + cur];
         if (fm == 0) return false;
         if (fm == 1) break;
         const int found = (fm & 0x3fffffff) - 2;
@@ -4495,21 +4529,22 @@ __global__ __launch_bounds__(256) void cfb_emit_b_kernel(CfbArgs a) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     int n[kCfLevels + 1], pos[kCfLevels];
     int s = 0, fnone = 0, cnt = 0, q = 0, c = 0;
-    size_t o = 0;
+    size_t o = 0, mr = 0;
     bool ok = false;
     unsigned claimed = 0;  // bit e: this item steers copy edge e (1 <= e < s)
     if (b < a.nitems) {
         cfb_node(a, b, q, c);
         o = (size_t)q * a.row_cap;
-        ok = cfb_chain(a, o, c, a.depth[b], n, pos, s, fnone);
+        mr = cfb_memo_row(a, q);
+        ok = cfb_chain(a, o, mr, c, a.depth[b], n, pos, s, fnone);
         if (ok) {
             cnt = 1;
             // (a plain L2 read first: the edges near a query's root are claimed once and read by
             // most of its items — an exchange each serialised on those few addresses)
             for (int e = 1; e < s; ++e)
-                if (__hip_atomic_load(&a.gclaim[o + n[e - 1]], __ATOMIC_RELAXED,
+                if (__hip_atomic_load(&a.gclaim[mr + n[e - 1]], __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                    atomicExch(&a.gclaim[o + n[e - 1]], 1) == 0) {
+                    atomicExch(&a.gclaim[mr + n[e - 1]], 1) == 0) {
                     claimed |= 1u << e;
                     ++cnt;
                 }
@@ -4559,7 +4594,7 @@ __global__ __launch_bounds__(256) void cfb_emit_b_kernel(CfbArgs a) {
         ct.literal = 0;
         a.tasks[t] = ct;
         a.ext[t] = StarTaskExt{};
-        a.tnode[t] = -1 - (int)(o + v);
+        a.tnode[t] = -1 - (int)(mr + v);
         ++t;
     }
 }
@@ -4630,10 +4665,10 @@ __global__ __launch_bounds__(256) void cfb_assemble_kernel(CfbArgs a, int* __res
     if (b >= a.nitems) return;
     int q, c;
     cfb_node(a, b, q, c);
-    const size_t o = (size_t)q * a.row_cap;
+    const size_t o = (size_t)q * a.row_cap, mr = cfb_memo_row(a, q);
     int n[kCfLevels + 1], pos[kCfLevels];
     int s = 0, fnone = 0;
-    bool known = cfb_chain(a, o, c, a.depth[b], n, pos, s, fnone);
+    bool known = cfb_chain(a, o, mr, c, a.depth[b], n, pos, s, fnone);
     // verdicts in finalize's order: 0 accept, 1 reject, 2 panic (the first non-accepted decides,
     // a None steer anywhere wins over a rejection)
     int first = 0;
@@ -4645,7 +4680,7 @@ __global__ __launch_bounds__(256) void cfb_assemble_kernel(CfbArgs a, int* __res
         any_none = g == 1 + kCfPanic;
     }
     for (int e = 1; known && e < s; ++e) {
-        const int g = a.gtab[o + n[e - 1]];
+        const int g = a.gtab[mr + n[e - 1]];
         known = g == 1 + kAccept || g == 1 + kReject || g == 1 + kCfPanic;
         if (known && g != 1 + kAccept && first == 0) first = g == 1 + kReject ? 1 : 2;
         any_none |= g == 1 + kCfPanic;
@@ -4658,7 +4693,7 @@ __global__ __launch_bounds__(256) void cfb_assemble_kernel(CfbArgs a, int* __res
         any_none = true;
         if (first == 0) first = 2;
     }
-    const bool tree_none = a.tnone_up[o + n[s]] != 0;  // edges s + 1 .. E - 1
+    const bool tree_none = a.tnone_up[mr + n[s]] != 0;  // edges s + 1 .. E - 1
     int bad = 0;
     bool vok = false;
     if (first == 2) {
