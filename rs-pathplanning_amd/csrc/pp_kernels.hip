@@ -4139,7 +4139,10 @@ __global__ __launch_bounds__(kCfLineThreads) void cf_line_kernel(
                                              sc.step_size, px + off, py + off, cap, lane, &n);
                 if (lane == 0) {
                     et[2 * e + 1] = r == kSteerSome ? n : 0;
-                    if (r != kSteerSome) atomicOr(&s_bad, 2);
+                    // a None steer is finalize's panic (rrt.rs:529); an n_point overflow is the
+                    // steer-overflow error (round 5 reported both as the panic)
+                    if (r == kSteerNone) atomicOr(&s_bad, 2);
+                    else if (r != kSteerSome) atomicOr(&s_bad, 4);
                 }
             }
         }
