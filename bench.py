@@ -279,7 +279,11 @@ def host_info():
                     break
     except OSError:
         pass
-    return {"cpu_model": model, "nproc_visible": os.cpu_count(),
+    vis = os.cpu_count() or 1
+    return {"cpu_model": model, "nproc_visible": vis,
+            "machine_share": f"{host_threads()} of {vis} visible cores "
+                             f"({100.0 * host_threads() / vis:.1f}%: the GPU lease's "
+                             f"OMP_NUM_THREADS share; single-core legs use 1)",
             "reference_crate": "not buildable here (Rust, no cargo/rustc, crates not vendored: "
                                "SURVEY.md K7); the CPU baseline is the build's C port (oracle/)"}
 
@@ -1021,6 +1025,7 @@ def _short_cpu(c, sample_len=120):
     if not isinstance(c, dict):
         return None
     out = _pick(c, ("value", "unit", "cores", "kind", "same_answer"))
+    out["cores_visible"] = os.cpu_count()
     if isinstance(c.get("sample"), str):
         out["sample"] = c["sample"][:sample_len]
     return out

@@ -16,6 +16,10 @@ for rep in ${REPS:-1}; do
   for j in "${JOBS[@]}"; do
     IFS='|' read -r name var args <<< "$j"
     f="$OUT/${name}_${var}_$rep"
+    lib="$R/rs-pathplanning_amd/lib/libpathplanning_amd.so"
+    [ "$var" = base ] || lib="$R/rs-pathplanning_amd/lib/$var/libpathplanning_amd.so"
+    # the library's hash before the run, so a run that fails before its line still names its build
+    echo "lib_sha256_16 $(sha256sum "$lib" | cut -c1-16)" > "$f.lib"
     if [ "$var" = base ]; then
       echo "python -u bench.py $args" > "$f.cmd"
       timeout -k 10 ${LIMIT:-400} python -u bench.py $args > "$f.json" 2> "$f.err" || { echo "FAILED $name"; tail -20 "$f.err"; exit 1; }
