@@ -349,7 +349,7 @@ def screen_roofline(sp, pmc):
     return r
 
 
-def fp64_roofline(kernel, ms, launches, points, arc_points, pmc=None, measured=""):
+def fp64_roofline(kernel, ms, launches, points, arc_points, pmc=None, measured="", tasks=0):
     """A walk-type kernel (f64 Dubins interpolation + collision per polyline point): the
     algorithmic FLOP of the points it walked (walk_flop) / its HIP-event time against the FP64
     vector peak; the PMC VALU count per point (when a counter pass exists) beside it."""
@@ -382,6 +382,14 @@ def fp64_roofline(kernel, ms, launches, points, arc_points, pmc=None, measured="
                       "note": "the measured VALU instruction count per point at one wave64 "
                               "instruction per 2 cycles per SIMD: the instruction-issue ceiling "
                               "of the code as compiled"}
+    if tasks:
+        # the walk's own unit: one (child, parent) edge per wave at a time, 63-point chunks
+        tpl = tasks / launches
+        r["tasks"] = {"tasks_per_launch": int(tpl), "points_per_task": round(points / tasks, 2),
+                      "tasks_per_s": round(tpl / (avg_ms * 1e-3), 1),
+                      "us_per_launch_per_1k_tasks": round(1e3 * avg_ms / max(tpl / 1e3, 1e-9), 3)}
+        if vpp:
+            r["tasks"]["valu_insts_per_task"] = round(vpp * points / tasks, 1)
     return r
 
 
@@ -389,7 +397,8 @@ def walk_roofline(sp, pmc, name):
     return fp64_roofline(f"steer_walk ({name})", sp["steer_ms"], sp["steer_launches"],
                          sp.get("walk_points", 0), sp.get("walk_arc_points", 0), pmc,
                          f"HIP events around steer_walk, {sp['steer_launches']} launches of the "
-                         "profiled pass (the timed schedule's streams)")
+                         "profiled pass (the timed schedule's streams)",
+                         tasks=sp.get("walk_tasks", 0))
 
 
 def finish_roofline(sp):

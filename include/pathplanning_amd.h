@@ -99,6 +99,7 @@ typedef struct pp_stats {
     int64_t samples_evaluated;  /* extend samples evaluated (one tree: the iterations) */
     int64_t samples_blocked;    /* ... of them whose point lies in an obstacle: rejected whatever
                                    the parent, without steer_prep / steer_walk or a pair list */
+    int64_t walk_tasks;         /* steer_walk tasks walked (profiling on; ABI 5, appended) */
 } pp_stats;
 
 int pp_abi_version(void);

@@ -701,7 +701,7 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     PP_HIP(c->cfb_yaw.reserve(cap_tasks));
     PP_HIP(c->cfb_state.reserve(2));  // [0] the round's, [1] a chunk's
     PP_HIP(c->cfb_misc.reserve(4));
-    if (c->prof) PP_HIP(c->cfb_pts.reserve(2 * kWalkTallySlots));
+    if (c->prof) PP_HIP(c->cfb_pts.reserve(3 * kWalkTallySlots));
     SceneDev sd = c->scene_dev();
     sd.step_size = c->mq_step;
     // the kernel's scene in device memory (cf_run's upload)
@@ -749,7 +749,7 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     PP_HIP(hipMemsetAsync(c->cf_err.p, 0, 2 * sizeof(int), st));
     PP_HIP(hipMemsetAsync(c->cfb_misc.p, 0, 4 * sizeof(int), st));
     PP_HIP(hipMemsetAsync(c->cfb_state.p, 0, 2 * sizeof(DevState), st));
-    if (c->prof) PP_HIP(hipMemsetAsync(c->cfb_pts.p, 0, 2 * kWalkTallySlots * sizeof(long long), st));
+    if (c->prof) PP_HIP(hipMemsetAsync(c->cfb_pts.p, 0, 3 * kWalkTallySlots * sizeof(long long), st));
     if (c->prof) {
         if (int r = ensure_events(c, 2)) return r;
         PP_HIP(hipEventRecord(c->ev[0], st));
@@ -821,9 +821,10 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
         c->finish_launches += 1;
         c->cfb_nodes += total - np;
         c->cfb_edges += misc[2];
-        std::vector<long long> v(2 * kWalkTallySlots);
+        std::vector<long long> v(3 * kWalkTallySlots);
         PP_HIP(hipMemcpy(v.data(), c->cfb_pts.p, v.size() * sizeof(long long), hipMemcpyDeviceToHost));
-        for (size_t i = 0; i < v.size(); ++i) (i < (size_t)kWalkTallySlots ? c->cfb_points : c->cfb_arc) += v[i];
+        for (size_t i = 0; i < 2 * (size_t)kWalkTallySlots; ++i)
+            (i < (size_t)kWalkTallySlots ? c->cfb_points : c->cfb_arc) += v[i];
     }
     if (err & 2) return set_err(PP_ERR_REFERENCE_PANIC, "finalize: a Dubins edge has no feasible word (rrt.rs:529 panics)");
     if (err & 4) return set_err(PP_ERR_STEER_OVERFLOW, "generate_local_course would index past n_point");
@@ -2733,7 +2734,10 @@ int pp_rrt_get_stats(pp_ctx* ctx, pp_stats* out, uint64_t out_size) {
         std::vector<long long> v(ctx->wg_pts.n);
         PP_HIP(hipMemcpyAsync(v.data(), ctx->wg_pts.p, v.size() * sizeof(long long), hipMemcpyDeviceToHost, ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
-        for (size_t i = 0; i < v.size(); ++i) (i < (size_t)kWalkTallySlots ? s.walk_points : s.walk_arc_points) += v[i];
+        for (size_t i = 0; i < v.size(); ++i) {
+            const size_t k = i / (size_t)kWalkTallySlots;  // points, arc points, tasks
+            (k == 0 ? s.walk_points : k == 1 ? s.walk_arc_points : s.walk_tasks) += v[i];
+        }
     }
     if (ctx->cf_tally.p) {
         long long t[4];
@@ -2770,8 +2774,8 @@ int pp_set_profiling(pp_ctx* ctx, int enabled) {
     int r = check_ctx(ctx, false, false);
     if (r) return r;
     if (enabled && !ctx->wg_pts.p) {  // one tally slot per walk workgroup (any walk grid)
-        PP_HIP(ctx->wg_pts.reserve(2 * kWalkTallySlots));
-        PP_HIP(hipMemsetAsync(ctx->wg_pts.p, 0, 2 * kWalkTallySlots * sizeof(long long), ctx->stream));
+        PP_HIP(ctx->wg_pts.reserve(3 * kWalkTallySlots));
+        PP_HIP(hipMemsetAsync(ctx->wg_pts.p, 0, 3 * kWalkTallySlots * sizeof(long long), ctx->stream));
         PP_HIP(hipStreamSynchronize(ctx->stream));
     }
     if (enabled && !ctx->cf_tally.p) {

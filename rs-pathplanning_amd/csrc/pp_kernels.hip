@@ -2760,7 +2760,7 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
     if (kLds) stage_scene(sc);
     double* gs = reinterpret_cast<double*>(pp_smem + (kLds ? sc.lds_bytes : 0)) +
                  wv * kGenSlots;  // this wave's generator slots
-    int npts = 0, napts = 0;
+    int npts = 0, napts = 0, ntasks = 0;
     // Workgroup b walks the tasks b, b + G, b + 2G, ... (G = the grid); its waves take them one
     // at a time from an LDS counter, so a wave that drew short paths takes more of them (a
     // workgroup's share is a sum of dozens of tasks: far more even than a wave's handful under a
@@ -2780,6 +2780,7 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
         // (list mode: the record is at ti; the slot t only addresses the verdict's store)
         const int t = al ? al[ti] : ti;
         const int s = walk_rec<kLds, kScene, kS>(sc, rec + ti, pdbuf + (size_t)ti * kPdCap, gs, npts, napts);
+        ++ntasks;
         if (lane == 0) {
             if (al || t < W) {
                 snap_status[t] = s;
@@ -2790,14 +2791,15 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
             }
         }
     }
-    if (wg_points) {  // [b]: points, [kWalkTallySlots + b]: their arc points
-        __shared__ int s_np[2][kWalkThreads / 64];
+    if (wg_points) {  // [b]: points, [kWalkTallySlots + b]: their arc points, [2 kWalkTallySlots + b]: tasks
+        __shared__ int s_np[3][kWalkThreads / 64];
         if (lane == 0) {
             s_np[0][wv] = npts;
             s_np[1][wv] = napts;
+            s_np[2][wv] = ntasks;
         }
         __syncthreads();
-        if (wv == 0 && lane < 2) {
+        if (wv == 0 && lane < 3) {
             long long sum = 0;
             for (int w = 0; w < kWalkThreads / 64; ++w) sum += s_np[lane][w];
             wg_points[blockIdx.x + lane * kWalkTallySlots] += sum;

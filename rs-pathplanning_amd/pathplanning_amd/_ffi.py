@@ -76,6 +76,7 @@ class StatsC(C.Structure):
         ("finish_arc_points", C.c_int64),
         ("reserved_abi3", C.c_int64 * 8),
         ("samples_evaluated", C.c_int64), ("samples_blocked", C.c_int64),
+        ("walk_tasks", C.c_int64),
     ]
 
     def as_dict(self):

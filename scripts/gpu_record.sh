@@ -11,4 +11,4 @@ echo default-ok
 timeout -k 10 300 python -u bench.py --workload config3 --queries 1024 --detail $OUT/detail_c3s.json > $OUT/bench_config3_shard1024.json 2> $OUT/c3s.err || { tail -30 $OUT/c3s.err; exit 1; }
 timeout -k 10 300 python -u bench.py --workload config5 --queries 1024 --detail $OUT/detail_c5s.json > $OUT/bench_config5_shard1024.json 2> $OUT/c5s.err || { tail -30 $OUT/c5s.err; exit 1; }
 echo shards-ok
-TAG=${TTAG:-record_trace} RUNS="c2|base|--workload config2 --no-cpu-baseline --no-size-sweep;c4|base|--workload config4 --no-cpu-baseline --no-size-sweep;c3|base|--workload config3 --no-cpu-baseline;c3s|base|--workload config3 --queries 1024 --no-cpu-baseline;c5|base|--workload config5 --no-cpu-baseline;ex|base|--workload example_rrt --no-cpu-baseline;pl|base|--workload plan --no-cpu-baseline" bash scripts/gpu_trace_var.sh
+TAG=${TTAG:-record_trace} RUNS="def|base|;c2|base|--workload config2 --no-cpu-baseline --no-size-sweep;c4|base|--workload config4 --no-cpu-baseline --no-size-sweep;c3|base|--workload config3 --no-cpu-baseline;c3s|base|--workload config3 --queries 1024 --no-cpu-baseline;c5|base|--workload config5 --no-cpu-baseline;ex|base|--workload example_rrt --no-cpu-baseline;pl|base|--workload plan --no-cpu-baseline" bash scripts/gpu_trace_var.sh

@@ -30,6 +30,7 @@ int main(void) {
     OFF(pp_stats, walk_points); OFF(pp_stats, batch_steps); OFF(pp_stats, batch_passes);
     OFF(pp_stats, finish_ms); OFF(pp_stats, finish_nodes); OFF(pp_stats, finish_points);
     OFF(pp_stats, reserved_abi3); OFF(pp_stats, samples_evaluated); OFF(pp_stats, samples_blocked);
+    OFF(pp_stats, walk_tasks);
     printf("\"rc_circle\": %d, \"rc_small\": %d, \"n_small\": %d, \"n\": %d, ", rc_circle,
            rc_small, n_small, n);
     printf("\"xy\": [");
