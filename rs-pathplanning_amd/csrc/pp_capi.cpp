@@ -515,14 +515,14 @@ constexpr int kCfBatch = 16384;     // nodes per check_finish launch
 constexpr int kCfPtsCap = 1 << 16;  // line points per check_finish workgroup
 static_assert(4 * kCfMaxEdges <= kCfPtsCap, "cf_line_kernel keeps 4 doubles per edge in the hypot buffer");
 // cf_line_kernel in two tiers (CfLines): tier 1 runs every line on kCfLineGrid workgroups with
-// room for kCfLinePts1 points and a kCfLinePath1-deep path each (3 x 8192 doubles: 192 KB; the
-// config-3 plan's lines have ~2350 points), tier 2 the few longer or deeper ones at the full
+// room for kCfLinePts1 points and a kCfLinePath1-deep path each (3 x 6144 doubles: 144 KB; the
+// config-3 plan's lines have ~2400 points), tier 2 the few longer or deeper ones at the full
 // capacities (kCfPtsCap points, kCfMaxDepth) on kCfLineGrid2 workgroups (1.5 MB each).  Round 5
 // gave every one of 2048 workgroups the full capacity: 3.2 GB.  1024 tier-1
-// workgroups (200 MB) cost the config-3 plan ~0.5 ms of its 12.5 (one wave per line: the lines in
-// flight are the workgroups), so the grid stays at 2048 (400 MB).
+// workgroups cost the config-3 plan ~0.5 ms of its 12.5 (one wave per line: the lines in flight
+// are the workgroups), so the grid stays at 2048 (300 MB).
 constexpr int kCfLineGrid = 2048;
-constexpr int kCfLinePts1 = 8192;
+constexpr int kCfLinePts1 = 6144;
 constexpr int kCfLinePath1 = 1024;
 constexpr int kCfLineGrid2 = 64;
 constexpr int kCfSpillCap = 1 << 17;  // tier-1 lines handed to tier 2 per launch
