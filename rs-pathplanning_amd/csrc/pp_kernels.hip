@@ -308,7 +308,23 @@ __device__ int s_classify(const SceneDev& sc, double ax, double ay, double bx, d
         }
     }
     // the rows' item ranges dealt to the lanes as one list, 64 at a time (a disc listed in
-    // several cells is tested several times)
+    // several cells is tested several times).  Each disc is tested in f32 from its cull record
+    // (LDS when the image holds it: no f64 loads, no f64 square roots), with margins that make
+    // both answers conservative.  e = 2 cull_slack bounds the f32 error of a distance or of a
+    // projection t here (cull_slack covers the rounding of the scene's coordinates, both ends
+    // of a difference, both axes), and of D.w = fl(r + width / 2):
+    //  - near: the f32 distance to AB within D.w + dl + 2e — every disc truly within r + dl;
+    //  - hit: the f32 chord of radius ri = D.w - dl - 2e (<= the exact r - dl - e), shortened by
+    //    e at each end, lies inside the exact (r - dl) chord, so its overlap with [t_lo, t_hi]
+    //    of at least gap + 2e is an exact one of at least gap: an S point lies in the disc.
+    // A disc the f32 test cannot decide either way only costs the walk its points (kSUnknown).
+    const float4* d4 = (kLds && sc.lds_d4 >= 0)
+                           ? reinterpret_cast<const float4*>(pp_smem + sc.lds_d4)
+                           : sc.d4;
+    const float e = 2.0f * sc.cull_slack;
+    const float axf = (float)ax, ayf = (float)ay, uxf = (float)ux, uyf = (float)uy;
+    const float lenf = (float)len, dlf = (float)dl;
+    const float t_lof = (float)t_lo, t_hif = (float)t_hi, gapf = (float)gap + 2.0f * e;
     for (int mb = 0;; mb += 64) {
         const int m = mb + lane;
         int kk = -1, run = 0;
@@ -319,19 +335,18 @@ __device__ int s_classify(const SceneDev& sc, double ax, double ay, double bx, d
         }
         bool near = false, hit = false;
         if (kk >= 0) {
-            const int d = items[kk];
-            const double wx = sc.cx[d] - ax, wy = sc.cy[d] - ay;
-            const double t = wx * ux + wy * uy;
-            const double tc = fmin(fmax(t, 0.0), len);
-            const double ex = wx - tc * ux, ey = wy - tc * uy;
-            const double rr = sqrt(sc.r2[d]);
-            const double ro = rr + dl;
+            const float4 D = d4[items[kk]];
+            const float wx = D.x - axf, wy = D.y - ayf;
+            const float t = wx * uxf + wy * uyf;
+            const float tc = __builtin_fminf(__builtin_fmaxf(t, 0.0f), lenf);
+            const float ex = wx - tc * uxf, ey = wy - tc * uyf;
+            const float ro = D.w + dlf + 2.0f * e;
             near = ex * ex + ey * ey <= ro * ro;
-            const double px = wx - t * ux, py = wy - t * uy;
-            const double p2 = px * px + py * py, ri = rr - dl;
-            if (ri > 0.0 && p2 < ri * ri) {
-                const double h = sqrt(ri * ri - p2) - dl;
-                hit = fmin(t + h, t_hi) - fmax(t - h, t_lo) >= gap;
+            const float px = wx - t * uxf, py = wy - t * uyf;
+            const float p2 = px * px + py * py, ri = D.w - dlf - 2.0f * e;
+            if (ri > 0.0f && p2 < ri * ri) {
+                const float h = __builtin_sqrtf(ri * ri - p2) - e;
+                hit = __builtin_fminf(t + h, t_hif) - __builtin_fmaxf(t - h, t_lof) >= gapf;
             }
         }
         if (__any(hit)) return kSHit;

@@ -24,6 +24,7 @@ SRC = os.path.join(ROOT, "rs-pathplanning_amd", "csrc")
 OUTLIB = os.path.join(ROOT, "rs-pathplanning_amd", "lib", "walktl", "libpathplanning_amd.so")
 BUILD = os.path.join(ROOT, "build", "walktl")
 CAP = 1 << 19  # records
+REC = 24       # u64 words per record
 
 KERNEL_DECL = r"""
 // ---- diagnostic timeline (scripts/diag_walk_timeline.py) ----
@@ -52,20 +53,45 @@ PATCHES_K = [
     __syncthreads();
     const unsigned long long tl_st = __builtin_amdgcn_s_memrealtime();
     __shared__ int s_tl_tasks;
-    if (t0) s_tl_tasks = 0;"""),
+    __shared__ unsigned s_tl_max, s_tl_wmin, s_tl_h[8], s_tl_hd[8];
+    if (t0) {
+        s_tl_tasks = 0;
+        s_tl_max = 0;
+        s_tl_wmin = 0xffffffffu;
+        for (int i = 0; i < 8; ++i) s_tl_h[i] = s_tl_hd[i] = 0;
+    }"""),
+    ("""        const int t = al ? al[ti] : ti;
+        const int s = walk_rec<kLds, kScene, kS>(""",
+     """        const int t = al ? al[ti] : ti;
+        const unsigned long long tl_t = __builtin_amdgcn_s_memrealtime();
+        const int tl_np0 = npts;
+        const int s = walk_rec<kLds, kScene, kS>("""),
     ("""        ++ntasks;
         if (lane == 0) {
             if (al || t < W) {""",
      """        ++ntasks;
-        if (lane == 0) atomicAdd(&s_tl_tasks, 1);
+        if (lane == 0) {
+            atomicAdd(&s_tl_tasks, 1);
+            const unsigned dur = (unsigned)(__builtin_amdgcn_s_memrealtime() - tl_t);
+            atomicMax(&s_tl_max, dur);
+            const int dp = npts - tl_np0;
+            const int hb = dp <= 0 ? 0 : (dp <= 8 ? 1 : (dp <= 16 ? 2 : (dp <= 32 ? 3 : (dp <= 64 ? 4 : (dp <= 128 ? 5 : (dp <= 256 ? 6 : 7))))));
+            atomicAdd(&s_tl_h[hb], 1u);
+            atomicAdd(&s_tl_hd[hb], dur);
+        }
         if (lane == 0) {
             if (al || t < W) {"""),
     ("""    if (wg_points) {  // [b]: points, [kWalkTallySlots + b]: their arc points, [2 kWalkTallySlots + b]: tasks""",
-     """    __syncthreads();
+     """    if (lane == 0) atomicMin(&s_tl_wmin, (unsigned)(__builtin_amdgcn_s_memrealtime() - tl_st));
+    __syncthreads();
     if (g_tl && t0) {
         const unsigned slot = atomicAdd(&g_tl_n, 1u);
         if (slot < %d) {
-            unsigned long long* r = g_tl + 8 * (size_t)slot;
+            unsigned long long* r = g_tl + REC_WORDS * (size_t)slot;
+            for (int i = 0; i < 8; ++i) {
+                r[8 + i] = s_tl_h[i];
+                r[16 + i] = s_tl_hd[i];
+            }
             r[0] = tl_in;
             r[1] = tl_st;
             r[2] = __builtin_amdgcn_s_memrealtime();
@@ -73,10 +99,10 @@ PATCHES_K = [
             r[4] = (unsigned long long)(size_t)st;
             r[5] = (unsigned long long)(unsigned)total | ((unsigned long long)(unsigned)s_tl_tasks << 32);
             r[6] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
-            r[7] = 0;
+            r[7] = (unsigned long long)s_tl_max | ((unsigned long long)s_tl_wmin << 32);
         }
     }
-    if (wg_points) {  // [b]: points, [kWalkTallySlots + b]: their arc points, [2 kWalkTallySlots + b]: tasks""" % CAP),
+    if (wg_points) {  // [b]: points, [kWalkTallySlots + b]: their arc points, [2 kWalkTallySlots + b]: tasks""".replace("REC_WORDS", str(REC)) % CAP),
 ]
 
 CAPI_TAIL = r"""
@@ -84,35 +110,51 @@ CAPI_TAIL = r"""
 extern "C" void pptl_setup(void* buf);
 extern "C" unsigned pptl_count();
 static void* g_tl_buf = nullptr;
-extern "C" int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted) {
+static void tl_begin() {
+    if (!getenv("PP_DIAG_OUT")) return;
+    if (!g_tl_buf) (void)hipMalloc(&g_tl_buf, (size_t)CAPV * RECB);
+    (void)hipDeviceSynchronize();
+    pptl_setup(g_tl_buf);
+    (void)hipDeviceSynchronize();
+}
+static void tl_end(unsigned tag) {
     const char* path = getenv("PP_DIAG_OUT");
-    if (path) {
-        if (!g_tl_buf) (void)hipMalloc(&g_tl_buf, (size_t)%d * 64);
-        (void)hipDeviceSynchronize();
-        pptl_setup(g_tl_buf);
-        (void)hipDeviceSynchronize();
+    if (!path || !g_tl_buf) return;
+    (void)hipDeviceSynchronize();
+    unsigned n = pptl_count();
+    if (n > CAPV) n = CAPV;
+    std::vector<unsigned long long> h((size_t)n * RECW);
+    if (n) (void)hipMemcpy(h.data(), g_tl_buf, (size_t)n * RECB, hipMemcpyDeviceToHost);
+    FILE* f = fopen(path, "ab");
+    if (f) {
+        fwrite(&n, 4, 1, f);
+        fwrite(&tag, 4, 1, f);
+        if (n) fwrite(h.data(), RECB, n, f);
+        fclose(f);
     }
+    pptl_setup(nullptr);
+    (void)hipDeviceSynchronize();
+}
+extern "C" int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted) {
+    tl_begin();
     const int r = pp_batch_extend_impl(ctx, n_steps, n_iterations, n_accepted);
-    if (path && g_tl_buf) {
-        (void)hipDeviceSynchronize();
-        unsigned n = pptl_count();
-        if (n > %d) n = %d;
-        std::vector<unsigned long long> h((size_t)n * 8);
-        if (n) (void)hipMemcpy(h.data(), g_tl_buf, (size_t)n * 64, hipMemcpyDeviceToHost);
-        FILE* f = fopen(path, "ab");
-        if (f) {
-            fwrite(&n, 4, 1, f);
-            if (n) fwrite(h.data(), 64, n, f);
-            fclose(f);
-        }
-        pptl_setup(nullptr);
-        (void)hipDeviceSynchronize();
-    }
+    tl_end(0);
     return r;
 }
-""" % (CAP, CAP, CAP)
+extern "C" int pp_batch_plan(pp_ctx* ctx, int32_t* best_node, double* length, int32_t* n_points,
+                             int32_t* n_finishes, int64_t* n_checked) {
+    tl_begin();
+    const int r = pp_batch_plan_impl(ctx, best_node, length, n_points, n_finishes, n_checked);
+    tl_end(1);
+    return r;
+}
+""".replace("CAPV", str(CAP)).replace("RECB", str(REC * 8)).replace("RECW", str(REC))
 
 PATCHES_C = [
+    ("""int pp_batch_plan(pp_ctx* ctx, int32_t* best_node, double* length, int32_t* n_points,
+                  int32_t* n_finishes, int64_t* n_checked) {""",
+     """static int pp_batch_plan_impl(pp_ctx* ctx, int32_t* best_node, double* length, int32_t* n_points,
+                  int32_t* n_finishes, int64_t* n_checked) {"""),
     ("int pp_batch_extend(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted) {",
      "static int pp_batch_extend_impl(pp_ctx* ctx, int64_t n_steps, int64_t* n_iterations, int64_t* n_accepted) {"),
 ]
@@ -149,8 +191,9 @@ def load(path):
             if len(b) < 4:
                 break
             n = int(np.frombuffer(b, dtype=np.uint32)[0])
-            a = np.frombuffer(f.read(n * 64), dtype=np.uint64).reshape(n, 8)
-            calls.append(a)
+            tag = int(np.frombuffer(f.read(4), dtype=np.uint32)[0])
+            a = np.frombuffer(f.read(n * REC * 8), dtype=np.uint64).reshape(n, REC)
+            calls.append((tag, a))
     return calls
 
 
@@ -176,11 +219,11 @@ def launches(a):
 
 
 def report(path):
-    for ci, a in enumerate(load(path)):
+    for ci, (tag, a) in enumerate(load(path)):
         if len(a) == 0:
             continue
         L = launches(a)
-        print(f"call {ci}: {len(a)} workgroup records, {len(L)} launches")
+        print(f"call {ci} ({'batch_plan' if tag else 'batch_extend'}): {len(a)} workgroup records, {len(L)} launches")
         rows = []
         for x in L:
             t_in, t_st, t_end = x[:, 0].astype(np.int64), x[:, 1].astype(np.int64), x[:, 2].astype(np.int64)
@@ -188,24 +231,44 @@ def report(path):
             total = int(x[0, 5] & 0xffffffff)
             tasks = (x[:, 5] >> 32).astype(np.int64)
             last = int(np.argmax(t_end))
-            rows.append(dict(total=total, wgs=len(x), span=(t_end.max() - t0) / 100.0,
+            tmax = (x[:, 7] & 0xffffffff).astype(np.int64)
+            wmin = (x[:, 7] >> 32).astype(np.int64)
+            hist = x[:, 8:16].sum(axis=0).astype(np.float64)
+            hdur = x[:, 16:24].sum(axis=0).astype(np.float64)
+            rows.append(dict(hist=hist, hdur=hdur, total=total, wgs=len(x), span=(t_end.max() - t0) / 100.0,
                              ramp=(t_in.max() - t0) / 100.0, stage=float(np.mean(t_st - t_in)) / 100.0,
                              work_mean=float(np.mean(t_end - t_st)) / 100.0,
                              work_max=float(np.max(t_end - t_st)) / 100.0,
                              last_in=(t_in[last] - t0) / 100.0, last_tasks=int(tasks[last]),
-                             tasks_max=int(tasks.max()), tasks_mean=float(tasks.mean())))
+                             tasks_max=int(tasks.max()), tasks_mean=float(tasks.mean()),
+                             task_max=float(tmax.max()) / 100.0, task_max_wg_mean=float(tmax.mean()) / 100.0,
+                             last_task_max=tmax[last] / 100.0,
+                             wave_spread=float(np.mean((t_end - t_st) - wmin)) / 100.0,
+                             last_wave_spread=((t_end[last] - t_st[last]) - wmin[last]) / 100.0,
+                             work_p50=float(np.percentile(t_end - t_st, 50)) / 100.0,
+                             work_p90=float(np.percentile(t_end - t_st, 90)) / 100.0))
         # size classes by task count
         for lo, hi in ((0, 1), (1, 1000), (1000, 4000), (4000, 8000), (8000, 16000), (16000, 40000),
                        (40000, 1 << 30)):
             sel = [r for r in rows if lo <= r["total"] < hi]
             if not sel:
                 continue
-            m = {k: float(np.mean([r[k] for r in sel])) for k in sel[0]}
+            m = {k: float(np.mean([r[k] for r in sel])) for k in sel[0] if k not in ("hist", "hdur")}
+            h = np.sum([r["hist"] for r in sel], axis=0)
+            hd = np.sum([r["hdur"] for r in sel], axis=0)
             print(f"  tasks [{lo}, {hi}): {len(sel)} launches; mean: tasks {m['total']:.0f}, wgs {m['wgs']:.0f}, "
                   f"span {m['span']:.1f} us, ramp {m['ramp']:.1f}, stage {m['stage']:.1f}, "
                   f"wg work mean {m['work_mean']:.1f} max {m['work_max']:.1f}, last wg entered at "
                   f"{m['last_in']:.1f} with {m['last_tasks']:.1f} tasks (wg max {m['tasks_max']:.1f}, "
                   f"mean {m['tasks_mean']:.1f})")
+            print(f"      longest task {m['task_max']:.1f} us (per-wg longest, mean {m['task_max_wg_mean']:.1f}; "
+                  f"the last wg's {m['last_task_max']:.1f}); wave exit spread in a wg {m['wave_spread']:.1f} "
+                  f"(last wg {m['last_wave_spread']:.1f}); wg work p50 {m['work_p50']:.1f} p90 {m['work_p90']:.1f}")
+            names = ["0", "1-8", "9-16", "17-32", "33-64", "65-128", "129-256", ">256"]
+            tot, totd = max(h.sum(), 1), max(hd.sum(), 1)
+            print("      points per task: " + "  ".join(
+                f"{names[i]}: {h[i] / tot * 100:.1f}% of tasks, {hd[i] / totd * 100:.1f}% of task time, "
+                f"{hd[i] / max(h[i], 1) / 100.0:.2f} us" for i in range(8) if h[i] > 0))
 
 
 if __name__ == "__main__":
