@@ -163,7 +163,6 @@ struct pp_ctx {
     DBuf<int> pidx, nn_idx, cand_cnt, snap_status;
     DBuf<CandEntry> cand;
     DBuf<PrepRec> rec;   // per-task steer records
-    DBuf<double> pdbuf;  // per-task grid-point distances (kPdCap per task)
     DBuf<int> r_order, r_rep, pend, fin_par;
     DBuf<unsigned char> blk;   // [2 Kcap] window samples in an obstacle (point_blocked)
     DBuf<SceneDev> d_scene;    // the scene in device memory (samples_role, the literal paths)
@@ -188,8 +187,8 @@ struct pp_ctx {
     int mq_Q = 0, mq_cap = 0;
     int64_t mq_max_iter = 0;
     double mq_step = 0.1;
-    DBuf<double> mq_x, mq_y, mq_yaw, mq_yawbuf, mq_pdbuf;
-    DBuf<int> mq_par, mq_n, mq_status, mq_err, mq_alist;
+    DBuf<double> mq_x, mq_y, mq_yaw, mq_yawbuf;
+    DBuf<int> mq_par, mq_n, mq_status, mq_err, mq_alist, mq_lstat;
     DBuf<int64_t> mq_it, mq_evals;
     DBuf<int64_t> mq_itprev;  // the lockstep NN's verdict cache (MqDev::it_prev)
     DBuf<uint64_t> mq_seed;
@@ -246,7 +245,6 @@ struct pp_ctx {
     DBuf<int> sr_sA, sr_sB, sr_sC;
     DBuf<double> sr_yA, sr_yB, sr_yC, sr_cA, sr_cB, sr_cC;
     DBuf<PrepRec> sr_rec;
-    DBuf<double> sr_pdbuf;
 
     // ---- profiling
     bool prof = false;
@@ -401,7 +399,6 @@ struct pp_ctx {
         a.snap_yaw = snap_yaw.p;
         a.snap_pose = snap_pose.p;
         a.rec = rec.p;
-        a.pdbuf = pdbuf.p;
         a.pend = pend.p;
         a.fin_par = fin_par.p;
         a.rs.order = r_order.p;
@@ -451,7 +448,6 @@ int ensure_window(pp_ctx* c, int K) {
     PP_HIP(c->cand_cnt.reserve(k));
     PP_HIP(c->cand.reserve(k * kCandCap));
     PP_HIP(c->rec.reserve(k + k * kCandCap));
-    PP_HIP(c->pdbuf.reserve((k + k * kCandCap) * kPdCap));
     PP_HIP(c->snap_status.reserve(k));
     PP_HIP(c->snap_yaw.reserve(k));
     PP_HIP(c->snap_pose.reserve(3 * k));
@@ -865,13 +861,13 @@ MqArgs mq_args(pp_ctx* c) {
     a.mq.status = c->mq_status.p;
     a.mq.alist = c->mq_alist.p;
     a.mq.ctask = c->mq_ctask.p;
+    a.mq.lstat = c->mq_lstat.p;
     a.mq.tyaw = c->mq_yawbuf.p;
     a.sc = c->scene_dev();
     a.sc.step_size = c->mq_step;
     a.st = c->mq_state.p;
     a.tasks = c->mq_tasks.p;
     a.rec = c->mq_rec.p;
-    a.pdbuf = c->mq_pdbuf.p;
     a.status = c->mq_status.p;
     a.yaw = c->mq_yawbuf.p;
     a.lit_scratch = c->api_lit_scratch.p;
@@ -888,6 +884,7 @@ MqArgs mq_args(pp_ctx* c) {
 // own streams and one's small kernels overlap another's walk.  Results do not depend on the
 // split: queries are independent.
 constexpr int kMaxSub = 4;
+constexpr size_t kLstatPad = 1024;  // >= the walk's grid (kWalkMaxWG)
 // streams: 2 for the extend batch (2: 289M it/s at 8192 queries, 177M on a 1024-query shard; 3:
 // 291M / 160M; 4: 244M / 109M), 3 for RRT* (11 kernels a step: 16.4M / 4.5M against 15.0M / 4.2M
 // with 2; 4 streams collapse to 10.7M / 2.4M, the box runs 4 hardware queues per process)
@@ -916,12 +913,13 @@ MqArgs mq_sub_args(pp_ctx* c, int sub, int nsub) {
     if (a.mq.status) a.mq.status += t0;
     if (a.mq.alist) a.mq.alist += t0;
     if (a.mq.ctask) a.mq.ctask += t0;
+    // (a sub-batch's verdict array spans its tasks plus one walk grid: DevState::lper rounds up)
+    if (a.mq.lstat) a.mq.lstat += t0 + (size_t)sub * kLstatPad;
     if (a.mq.tyaw) a.mq.tyaw += t0;
     a.st = c->mq_state.p + 1 + sub;
     a.mq.st = a.st;
     a.tasks += t0;
     a.rec += t0;
-    a.pdbuf += t0 * kPdCap;
     a.status += t0;
     a.yaw += t0;
     return a;
@@ -949,9 +947,9 @@ int mq_reserve_tasks(pp_ctx* c, int q, int K) {
     PP_HIP(c->mq_status.reserve(tq));
     PP_HIP(c->mq_yawbuf.reserve(tq));
     PP_HIP(c->mq_rec.reserve(tq));
-    PP_HIP(c->mq_pdbuf.reserve(tq * kPdCap));
     PP_HIP(c->mq_nnd2.reserve(tq));
     PP_HIP(c->mq_alist.reserve(tq));
+    PP_HIP(c->mq_lstat.reserve(tq + (size_t)kMaxSub * kLstatPad));
     return PP_OK;
 }
 
@@ -1025,7 +1023,6 @@ StarArgs star_args(pp_ctx* c) {
     a.cB = c->sr_cB.p;
     a.cC = c->sr_cC.p;
     a.rec = c->sr_rec.p;
-    a.pdbuf = c->sr_pdbuf.p;
     a.lit_scratch = c->api_lit_scratch.p;
     a.err = c->sr_err.p;
     a.wg_points = c->prof_points();
@@ -1084,7 +1081,6 @@ StarArgs star_sub_args(pp_ctx* c, int sub, int nsub) {
     a.cB += b0;
     a.cC += b0;
     a.rec += b0;
-    a.pdbuf += b0 * kPdCap;
     return a;
 }
 
@@ -2543,7 +2539,6 @@ int pp_star_new(pp_ctx* ctx, int q, const double* starts, const uint64_t* seeds,
     PP_HIP(ctx->sr_sC.reserve(tb));
     for (auto* b : {&ctx->sr_yB, &ctx->sr_yC, &ctx->sr_cB, &ctx->sr_cC}) PP_HIP(b->reserve(tb));
     PP_HIP(ctx->sr_rec.reserve(tb));
-    PP_HIP(ctx->sr_pdbuf.reserve(tb * kPdCap));
     PP_HIP(ctx->sr_state.reserve(3 * (1 + kMaxSub)));
     PP_HIP(ctx->sr_err.reserve(1));
     PP_HIP(ctx->api_lit_scratch.reserve((size_t)kLiteralWaves * 3 * kLiteralCap));

@@ -40,7 +40,6 @@ struct WindowArgs {
     double* snap_yaw = nullptr;
     double* snap_pose = nullptr;  // [3K] parent pose of each unflagged sample (nn_finalize)
     PrepRec* rec = nullptr;       // [K + K * kCandCap] per-task steer records
-    double* pdbuf = nullptr;      // [(K + K * kCandCap) * kPdCap] grid-point distances
     int* pend = nullptr;          // [K] samples queued for the resolve's round passes
     int* fin_par = nullptr;       // [K] window parent of a resolved sample (kWinParent)
     ResolveScratch rs{};
@@ -206,7 +205,6 @@ struct MqArgs {
     DevState* st = nullptr;  // W = Q, ncomp = 0 (the steer kernels' task count)
     SteerTask* tasks = nullptr;
     PrepRec* rec = nullptr;
-    double* pdbuf = nullptr;
     int* status = nullptr;
     double* yaw = nullptr;
     double* lit_scratch = nullptr;  // kLiteralWaves buffers
@@ -223,7 +221,7 @@ hipError_t launch_mq_init(hipStream_t s, const MqDev& mq, const double* starts);
 hipError_t launch_mq_target(hipStream_t s, const MqDev& mq, int64_t n_steps, int64_t* target);
 
 // RRT* query batch (config 5): `steps` lockstep RRT* iterations of every query.  Task arrays of
-// round A hold Q entries, rounds B and C Q * kStarKMax; rec / pdbuf are shared by the rounds.
+// round A hold Q entries, rounds B and C Q * kStarKMax; rec is shared by the rounds.
 struct StarArgs {
     StarDev sd{};
     SceneDev sc{};
@@ -233,7 +231,6 @@ struct StarArgs {
     double *yA = nullptr, *yB = nullptr, *yC = nullptr;     // child yaw of each task
     double *cA = nullptr, *cB = nullptr, *cC = nullptr;     // Dubins cost of each task
     PrepRec* rec = nullptr;
-    double* pdbuf = nullptr;
     double* lit_scratch = nullptr;  // kLiteralWaves buffers
     int* err = nullptr;
     hipEvent_t* ev = nullptr;  // optional: 8 per step, around star_sample and each round's walk

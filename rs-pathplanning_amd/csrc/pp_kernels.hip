@@ -2281,8 +2281,7 @@ __device__ __forceinline__ void prep_task(const SceneDev& sc, int r, int g0, int
 __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
     const DevState* __restrict__ st, SceneDev sc, const double* __restrict__ wsx,
     const double* __restrict__ wsy, const double* __restrict__ snap_pose,
-    CandEntry* __restrict__ cand, PrepRec* __restrict__ rec, double* __restrict__ pdbuf,
-    double* __restrict__ snap_yaw, const SteerTask* __restrict__ tasks,
+    CandEntry* __restrict__ cand, PrepRec* __restrict__ rec, double* __restrict__ snap_yaw, const SteerTask* __restrict__ tasks,
     double* __restrict__ cost_out = nullptr, const StarTaskExt* __restrict__ ext = nullptr,
     const unsigned char* __restrict__ blk_in = nullptr) {
     // tasks != nullptr: explicit (child, parent pose) tasks [0, W) (multi-query batch); a task
@@ -2339,10 +2338,9 @@ __global__ __launch_bounds__(kPrepThreads) void steer_prep_kernel(
 // steer_walk for one PrepRec (called by all 64 lanes; the record is wave-uniform).  Chunks of 63
 // grid points: lane k >= 1 interpolates grid point base + k - 1 (interpolate, dubins.rs:155-198,
 // then the world transform dubins.rs:412-422), lane 0 carries the previous chunk's last point,
-// and the junction to the parent follows the last grid point.  A kPrepWalk task reads its pd
-// values from pdbuf; a kPrepFallback task (more than kPdCap points) reads its first kPdCap there
-// and continues with the uniform serial `pd += d` walk from the state steer_prep kept, each lane
-// capturing its own point.  npts (wave-uniform) += the polyline points generated and verified
+// and the junction to the parent follows the last grid point.  The grid points' pd values come
+// from the lane-parallel `pd += d` generator below, started from the state steer_prep kept
+// (segment 0, pd = d), each lane capturing its own point.  npts (wave-uniform) += the polyline points generated and verified
 // (grid points plus the junction; the profiled walk roofline's unit).
 //
 // gs: the wave's kGenSlots LDS doubles — the generator's kGenPts value slots, then the task's
@@ -2367,8 +2365,8 @@ constexpr int kGenPts = 68;  // generator slots: 63 points + 4 overshoot + 1
 constexpr int kSegRow = 6;   // segment-table row (16-byte aligned rows: ds_read_b128)
 template <bool kLds, int kScene = kSceneAny, bool kS = false>
 __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __restrict__ p,
-                                        const double* __restrict__ pdv, double* __restrict__ gs,
-                                        int& npts, int& napts, bool junction = true) {
+                                        double* __restrict__ gs, int& npts, int& napts,
+                                        bool junction = true) {
     const int lane = __lane_id();
     const int state = ufl(p->state);
     const double x = ufl(p->x), y = ufl(p->y), px = ufl(p->px), py = ufl(p->py);
@@ -2378,8 +2376,8 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         npts += 2;
         return chunk_rejects<kLds, kScene>(sc, has, has, lane == 1, qx, qy) ? kReject : kAccept;
     }
-    if (state != kPrepWalk && state != kPrepFallback) return state;
-    const bool partial = state == kPrepFallback;  // pdbuf holds the first ng points only (0 or kPdCap)
+    // (steer_prep stores no grid points: every walkable record is kPrepFallback at point 0)
+    if (state != kPrepFallback) return state == kPrepWalk ? kError : state;
     const double step = sc.step_size;
     const double c = ufl(p->c), cw = ufl(p->cw), sw = ufl(p->sw);
     const double ox1 = ufl(p->ox[1]), oy1 = ufl(p->oy[1]), ox2 = ufl(p->ox[2]), oy2 = ufl(p->oy[2]);
@@ -2387,7 +2385,6 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     const double sa0 = ufl(p->sa[0]), sa1 = ufl(p->sa[1]), sa2 = ufl(p->sa[2]);
     const double L0 = ufl(p->L[0]), L1 = ufl(p->L[1]), L2 = ufl(p->L[2]);
     const int m0 = ufl(p->m[0]), m1 = ufl(p->m[1]), m2 = ufl(p->m[2]);
-    const int n0 = ufl(p->cnt[0]), n01 = n0 + ufl(p->cnt[1]), ng = n01 + ufl(p->cnt[2]);
     const double rc = 1.0 / c;
     double* segt = gs + kGenPts;
     if (lane < 3) {
@@ -2399,12 +2396,11 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         row[4] = (double)(lane == 0 ? m0 : (lane == 1 ? m1 : m2));
     }
     __builtin_amdgcn_wave_barrier();
-    // serial generator (kPrepFallback past the stored points), resumed where steer_prep stopped
+    // the generator's initial state (segment 0, pd = d - 0.0, dubins.rs:239-241), from steer_prep
     int gseg = ufl(p->fb_seg);
     double gdd = ufl(p->fb_dd);
     double gpd = ufl(p->fb_pd);
-    long long grid = ng;  // grid points stored by steer_prep (0 or kPdCap for kPrepFallback)
-    static_assert(kPdCap % 63 == 0, "stored points end on a chunk boundary");
+    long long grid = 0;  // grid points generated (and counted) so far
     double carry_x = x, carry_y = y;
     npts += 1;  // point 0, the child
     // a long S segment against the discs (s_classify) or the polygon edges and bounds ring
@@ -2423,7 +2419,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
     const bool polys = kS && !trim1 &&
                        (kScene == kScenePoly ||
                         (kScene == kSceneAny && !sc.bits && (sc.ne > 0 || sc.nbv > 0)));
-    if ((discs || polys) && partial && ng == 0 && m1 == kModeS && L1 >= kSMinPts * step) {
+    if ((discs || polys) && m1 == kModeS && L1 >= kSMinPts * step) {
         const double ax = cw * ox1 + sw * oy1 + x, ay = -sw * ox1 + cw * oy1 + y;
         const double pcb = div_by(L1, c, rc);
         const double lxb = ox1 + pcb * ca1, lyb = oy1 + pcb * sa1;
@@ -2443,8 +2439,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         double my_pd = 0.0;
         bool done;
         bool chord = false;  // lane 1 holds the cleared S segment's last point, lane 0 its first
-        const bool gen = partial && base >= ng;
-        if (gen) {
+        {
             // lane-parallel `pd += d` (dubins.rs:239-255): lane l >= pos replays l - pos
             // additions from the uniform start value — the serial walk's exact rounding
             // sequence — and the first lane whose |pd| exceeds |L| ends the segment (its value
@@ -2565,15 +2560,6 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
                 gseg = 3;
                 done = true;
             }
-        } else {
-            const int rem = partial ? 63 : ng - base;
-            cnt = rem < 63 ? rem : 63;
-            done = rem < 63;
-            const int g = base + lane - 1;
-            if (lane >= 1 && lane <= cnt) {
-                my_pd = pdv[g];
-                my_seg = g < n0 ? 0 : (g < n01 ? 1 : 2);
-            }
         }
         // trim1 (prep_task): the chunk where the last segment ends pops its last grid point with
         // the endpoint; one generated in the previous chunk was tested already: literal path
@@ -2640,7 +2626,7 @@ __device__ __forceinline__ int walk_rec(const SceneDev& sc, const PrepRec* __res
         carry_y = readlane_f64(qy, cnt);
     }
     // no trailing zero left for the trim (dubins.rs:281-288): the literal path decides
-    if (partial && 1 + grid > (long long)ufl((double)p->n_point) - 2) return kLiteral;
+    if (1 + grid > (long long)ufl((double)p->n_point) - 2) return kLiteral;
     return kAccept;
 }
 
@@ -2691,7 +2677,7 @@ __device__ __forceinline__ int walk_edge(const SceneDev& sc, const SteerPrep& r,
     p.fb_seg = 0;
     p.trim1 = 0;
     p.yaw = p.pyaw = 0.0;
-    return walk_rec<kLds, kSceneAny, kS>(sc, &p, nullptr, gs, npts, napts, junction);
+    return walk_rec<kLds, kSceneAny, kS>(sc, &p, gs, npts, napts, junction);
 }
 
 // steer_walk, one task per wave (persistent grid, grid-stride over the W + ncomp tasks); kLds:
@@ -2759,7 +2745,6 @@ template <bool kLds, int kMinW, int kScene, bool kS>
 __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevState* __restrict__ st,
                                                          SceneDev sc,
                                                          const PrepRec* __restrict__ rec,
-                                                         const double* __restrict__ pdbuf,
                                                          CandEntry* __restrict__ cand,
                                                          int* __restrict__ snap_status,
                                                          const int* __restrict__ cand_cnt,
@@ -2786,6 +2771,11 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
     const int G = (int)gridDim.x;
     if (t0) s_next = 0;
     const int* __restrict__ al = st->alist;  // (the batch's active-task list)
+    const int lper = (total + G - 1) / G;
+    if (al && blockIdx.x == 0 && t0) {
+        st->lgrid = G;
+        st->lper = lper;
+    }
     __syncthreads();
     for (;;) {
         int k = 0;
@@ -2794,11 +2784,12 @@ __global__ __launch_bounds__(kWalkThreads, kMinW) void steer_walk_kernel(DevStat
         if (ti >= total) break;
         // (list mode: the record is at ti; the slot t only addresses the verdict's store)
         const int t = al ? al[ti] : ti;
-        const int s = walk_rec<kLds, kScene, kS>(sc, rec + ti, pdbuf + (size_t)ti * kPdCap, gs, npts, napts);
+        const int s = walk_rec<kLds, kScene, kS>(sc, rec + ti, gs, npts, napts);
         ++ntasks;
         if (lane == 0) {
             if (al || t < W) {
-                snap_status[t] = s;
+                // (list mode: the workgroup's run of verdicts, DevState::lgrid / lper)
+                snap_status[al ? (int)blockIdx.x * lper + (ti - (int)blockIdx.x) / G : t] = s;
                 if (pend && s != kAccept && s != kReject && cand_cnt[t] == 0)
                     pend[atomicAdd(&st->npend, 1)] = t;
             } else {
@@ -2880,11 +2871,11 @@ inline int walk_grid_cap(const SceneDev& sc) {
 // steer_walk_kernel over a task set on stream s (its instantiation for the scene)
 template <int kMinW, bool kS = false>
 inline void launch_walk(hipStream_t s, int blocks, DevState* st, const SceneDev& sc,
-                        const PrepRec* rec, const double* pdbuf, CandEntry* cand, int* status,
+                        const PrepRec* rec, CandEntry* cand, int* status,
                         const int* cand_cnt, int* pend, long long* wg_points) {
     (void)walk_kernel_for<kMinW, kS>(sc, [&](auto kern) {
         kern<<<blocks, kWalkThreads, walk_lds_bytes(sc.lds_bytes), s>>>(
-            st, sc, rec, pdbuf, cand, status, cand_cnt, pend, wg_points);
+            st, sc, rec, cand, status, cand_cnt, pend, wg_points);
         return hipSuccess;
     });
 }
@@ -3481,7 +3472,7 @@ __device__ __noinline__ void cf_prep(const SceneDev* __restrict__ scg, double ax
 __device__ __forceinline__ int cf_walk(const SceneDev* __restrict__ scg, const PrepRec* lrec,
                                     double* gs, bool junction, int* tally) {
     int w = 0, wa = 0;
-    const int st = walk_rec<false, kSceneAny, true>(*scg, lrec, nullptr, gs, w, wa, junction);
+    const int st = walk_rec<false, kSceneAny, true>(*scg, lrec, gs, w, wa, junction);
     if (__lane_id() == 0) {
         tally[0] = w;
         tally[1] = wa;
@@ -4804,12 +4795,12 @@ hipError_t launch_cfb_steer(hipStream_t s, const SceneDev& sc, const CfbArgs& a,
     if (max_tasks <= 0) return hipSuccess;
     const int pb = std::min((max_tasks + 31) / 32, 8192);
     steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(a.st, sc, nullptr, nullptr, nullptr, nullptr,
-                                                  a.rec, nullptr, a.yaw, a.tasks, nullptr,
+                                                  a.rec, a.yaw, a.tasks, nullptr,
                                                   own_yaw ? a.ext : nullptr);
     const int wb = std::min(std::max(1, (max_tasks + kWalkThreads / 64 - 1) / (kWalkThreads / 64)),
                             std::min(kWalkMaxWG, walk_grid_cap<kWalkMinWBatch, 4, true>(sc)));
-    launch_walk<kWalkMinWBatch, true>(s, wb, a.st, sc, a.rec, nullptr, nullptr, a.status, nullptr,
-                                      nullptr, wg_points);
+    launch_walk<kWalkMinWBatch, true>(s, wb, a.st, sc, a.rec, nullptr, a.status, nullptr, nullptr,
+                                      wg_points);
     return hipGetLastError();
 }
 
@@ -4961,6 +4952,7 @@ __global__ __launch_bounds__(NT) void mq_sample_nn_kernel(MqDev mq, double minx,
             if (need) {
                 const int i = s_base + s_cnt[wave] + __popcll(nm & ((1ull << lane) - 1ull));
                 mq.alist[i] = q * mq.K + lane;  // (need: lane = slot k, node group 0)
+                mq.status[q * mq.K + lane] = -2 - i;  // (the walk's verdict: lstat[i])
                 tk.literal = 0;
                 mq.ctask[i] = tk;
             }
@@ -4980,7 +4972,7 @@ __global__ __launch_bounds__(256) void mq_target_kernel(MqDev mq, int64_t n_step
 
 __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
                                                         const SteerTask* __restrict__ tasks,
-                                                        const int* __restrict__ status,
+                                                        int* __restrict__ status,
                                                         const double* __restrict__ yaw,
                                                         double* __restrict__ lit_scratch,
                                                         int* __restrict__ lit_locks,
@@ -5011,6 +5003,11 @@ __global__ __launch_bounds__(256) void mq_insert_kernel(MqDev mq, SceneDev sc,
             tk = tasks[t];
             st = status[t];
             yw = yaw[t];
+            if (st <= -2) {  // a listed slot: the walk's verdict, kept for the next step's cache
+                const int i = -2 - st, lg = mq.st->lgrid;
+                st = mq.lstat[(i % lg) * mq.st->lper + i / lg];
+                status[t] = st;
+            }
         }
         const bool live = in && tk.pnode != -1;  // (pnode -2: a sample in an obstacle)
         const bool act = in && tk.pnode >= 0;
@@ -5111,6 +5108,7 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
     const int walk_blocks = std::min((T + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
                                      std::min(kWalkMaxWG, walk_cap));
     const int ins_blocks = std::min((Q + 4 * (64 / a.mq.K) - 1) / (4 * (64 / a.mq.K)), 4096);
+    int* wstat = a.mq.alist ? a.mq.lstat : a.status;  // the walk's verdicts (list order)
 
     for (int k = 0; k < steps; ++k) {
         hipEvent_t* ev = a.ev ? a.ev + 5 * k : nullptr;
@@ -5124,19 +5122,18 @@ hipError_t launch_mq_steps(hipStream_t s, const MqArgs& a, int steps) {
         if (ev) (void)hipEventRecord(ev[1], s);
         // (the listed tasks, compacted by mq_sample_nn)
         steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, nullptr, nullptr,
-                                                              nullptr, nullptr, a.rec, a.pdbuf,
-                                                              a.yaw, a.mq.alist ? a.mq.ctask : a.tasks);
+                                                              nullptr, nullptr, a.rec, a.yaw,
+                                                              a.mq.alist ? a.mq.ctask : a.tasks);
         if (ev) (void)hipEventRecord(ev[2], s);
         // with the analytic straight segments (s_classify).  Steps of >= kBigStepTasks tasks
         // walk at 6 waves per SIMD (80 VGPRs, 20 B of spill), smaller ones at 5 (96 VGPRs, no
         // spill); the 8192-query batch at 5 waves: 641 -> 623 M it/s (round 5, one box)
         if (T >= kBigStepTasks)
-            launch_walk<kWalkMinWBatch, true>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf, nullptr,
-                                              a.status, nullptr, nullptr, a.wg_points);
+            launch_walk<kWalkMinWBatch, true>(s, walk_blocks, a.st, a.sc, a.rec, nullptr, wstat,
+                                              nullptr, nullptr, a.wg_points);
         else
-            launch_walk<kWalkMinWBatch - 1, true>(s, walk_blocks, a.st, a.sc, a.rec, a.pdbuf,
-                                                  nullptr, a.status, nullptr, nullptr,
-                                                  a.wg_points);
+            launch_walk<kWalkMinWBatch - 1, true>(s, walk_blocks, a.st, a.sc, a.rec, nullptr,
+                                                  wstat, nullptr, nullptr, a.wg_points);
         if (ev) (void)hipEventRecord(ev[3], s);
         mq_insert_kernel<<<ins_blocks, 256, 0, s>>>(a.mq, a.sc, a.tasks, a.status, a.yaw,
                                                     a.lit_scratch, a.lit_locks, a.err);
@@ -5694,11 +5691,11 @@ hipError_t launch_star_steps(hipStream_t s, const StarArgs& a, int steps) {
     auto round = [&](DevState* st, int pb, int wb, const SteerTask* t, const StarTaskExt* ext,
                      int* status, double* yaw, double* cost, hipEvent_t* ev) {
         steer_prep_kernel<<<pb, kPrepThreads, 0, s>>>(st, a.sc, nullptr, nullptr, nullptr, nullptr,
-                                                      a.rec, a.pdbuf, yaw, t, cost, ext);
+                                                      a.rec, yaw, t, cost, ext);
         if (ev) (void)hipEventRecord(ev[0], s);
         // (the analytic straight segments, s_classify: config 5 21.9 -> 25.1 M it/s, same digest)
-        launch_walk<kWalkMinWStar, true>(s, wb, st, a.sc, a.rec, a.pdbuf, nullptr, status,
-                                         nullptr, nullptr, a.wg_points);
+        launch_walk<kWalkMinWStar, true>(s, wb, st, a.sc, a.rec, nullptr, status, nullptr, nullptr,
+                                         a.wg_points);
         if (ev) (void)hipEventRecord(ev[1], s);
     };
     for (int k = 0; k < steps; ++k) {
@@ -5860,14 +5857,14 @@ hipError_t launch_window(hipStream_t s, const WindowArgs& a, hipEvent_t* ev, int
     // snapshot and candidate tasks together: prep covers 2K tasks per pass, walk 4 per workgroup
     const int prep_blocks = (2 * K + kPrepThreads / 8 - 1) / (kPrepThreads / 8);
     steer_prep_kernel<<<prep_blocks, kPrepThreads, 0, s>>>(a.st, a.sc, wsx, wsy, a.snap_pose, a.cand,
-                                                  a.rec, a.pdbuf, a.snap_yaw, nullptr, nullptr,
-                                                  nullptr, wk.g.blk[p]);
+                                                  a.rec, a.snap_yaw, nullptr, nullptr, nullptr,
+                                                  wk.g.blk[p]);
     if (ev) (void)hipEventRecord(ev[3], s);
     // snapshot tasks plus the usual few candidate tasks in one round of waves
     const int nwg = std::min((K + K / 4 + kWalkThreads / 64 - 1) / (kWalkThreads / 64),
                              std::min(kWalkMaxWG, walk_grid_cap(a.sc)));
-    launch_walk<kWalkMinWWindow>(s, nwg, a.st, a.sc, a.rec, a.pdbuf, a.cand, a.snap_status,
-                                 a.cand_cnt, a.pend, a.wg_points);
+    launch_walk<kWalkMinWWindow>(s, nwg, a.st, a.sc, a.rec, a.cand, a.snap_status, a.cand_cnt,
+                                 a.pend, a.wg_points);
     if (ev) (void)hipEventRecord(ev[4], s);
     return hipGetLastError();
 }

@@ -26,7 +26,6 @@ constexpr int kResolveThreads = 512;  // resolve_tail_kernel (8 waves, 256 VGPRs
 constexpr int kMaxWindow = 4096;     // K limit: the resolve keeps the window's state in LDS
 constexpr int kMinDynWindow = 128;   // the adaptive window's floor (DevState.kdyn)
 constexpr int kSteerPrepBytes = 152; // sizeof(SteerPrep) (checked in pp_kernels.hip)
-constexpr int kPdCap = 63;           // grid points per task stored by steer_prep (one walk chunk)
 constexpr int kPrepLanes = 8;        // lanes per task in steer_prep's phase A
 constexpr int kPrepThreads = 256;    // steer_prep workgroup: 32 tasks (8 per wave)
 constexpr int kWalkThreads = 512;    // steer_walk workgroup: 8 tasks at a time (3 workgroups per CU)
@@ -138,9 +137,13 @@ struct DevState {
         nn_flagged, node_evals;
     int64_t blocked;  // samples in an obstacle (point_blocked): rejected without steer or pair list
     // the query batch's active-task list (round 5): steer_prep / steer_walk run over i < W with the
-    // compacted task i (its record and pd slots at i) and store its yaw / verdict at slot
-    // alist[i]; null: task i is slot i (the window pipeline, RRT*, the steer rounds)
+    // compacted task i (its record at i) and store its yaw at slot alist[i], its verdict in list
+    // order (MqDev::lstat); null: task i is slot i (the window pipeline, RRT*, the steer rounds)
     const int* alist;
+    // list mode: the walk's verdict of task i sits at (i % lgrid) * lper + i / lgrid, so each
+    // walk workgroup (it takes i = b, b + lgrid, ...) stores one contiguous run and a line of the
+    // array is written back from one XCD's L2; the walk sets both for the insert
+    int lgrid, lper;
 };
 
 // An explicit steer task: child (x, y) steered toward its parent — tree node `pnode` when
@@ -174,21 +177,20 @@ struct CandEntry {
 };
 
 // Per-task steer record of the window pipeline, written by steer_prep (8 lanes per task) and read
-// by steer_walk (one wave per task) with scalar loads.  The task's grid-point distances (the
-// `pd` values of generate_local_course, dubins.rs:239-255) sit in pdbuf[t * kPdCap + g]; a task
-// with more than kPdCap grid points (kPrepFallback) stores its first kPdCap and the walk's state
-// there, and steer_walk generates the rest lane-parallel (only if the first chunk did not reject).
+// by steer_walk (one wave per task) with scalar loads.  No grid points are stored: steer_walk
+// generates the `pd` values of generate_local_course (dubins.rs:239-255) lane-parallel from the
+// generator's initial state kept here (kPrepFallback; cnt[] is always 0, kept for the layout).
 struct PrepRec {
     double x, y, px, py, yaw, pyaw;  // child (point 0), parent (the junction) and their headings
     double c, cw, sw;                // curvature, cos/sin(-yaw) of the world transform
     double ox[3], oy[3];             // segment origins in the local frame
     double ca[3], sa[3];             // segment trig: S cos/sin(o.yaw), L/R cos/sin(-o.yaw)
     double L[3];                     // segment lengths (the serial walk of kPrepFallback)
-    double fb_pd, fb_dd;             // kPrepFallback: the walk's state at point kPdCap (pd, d)
+    double fb_pd, fb_dd;             // kPrepFallback: the generator's initial state (pd, d)
     long long n_point;               // dubins.rs:369
-    int m[3], cnt[3];                // segment modes, grid points per segment (of the stored ones)
-    int state, fb_seg;               // kPrepWalk / kPrepNone / kPrepFallback or a verdict; the
-                                     // kPrepFallback walk's segment at point kPdCap
+    int m[3], cnt[3];                // segment modes; cnt: unused (0)
+    int state, fb_seg;               // kPrepNone / kPrepFallback or a verdict; the generator's
+                                     // initial segment (0)
     int trim1;                       // the endpoint's local x is 0.0: the trim also pops the last
                                      // grid point (dubins.rs:281-288; the walk checks its x)
 };
@@ -228,6 +230,9 @@ struct MqDev {
     // alist[0, st->W); the insert resets st->W.  null: every slot goes through the steer
     int* alist = nullptr;
     SteerTask* ctask = nullptr;  // the listed tasks, compacted (ctask[i] = tasks[alist[i]])
+    // the listed tasks' verdicts in list order (the walk's stores stay contiguous); a listed
+    // slot's status holds -2 - i until mq_insert resolves it from lstat[i]
+    int* lstat = nullptr;
     DevState* st = nullptr;
     double* tyaw = nullptr;
 };
