@@ -20,6 +20,7 @@ for f in sorted(glob.glob(os.path.join(d, "*.json"))):
         continue
     sub = j.get("config3") or {}
     plan = (sub.get("plan") or {}) if isinstance(sub, dict) else {}
+    plan = plan or j.get("plan") or {}
     rows[(parts[0], parts[1])].append((j.get("value"), j.get("records_digest") or (sub or {}).get("records_digest"),
                                        plan.get("check_finish_ms"), j.get("lib_sha256_16")))
 for (n, v), r in sorted(rows.items()):
