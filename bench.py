@@ -670,8 +670,10 @@ def run_batch(args, D, star, with_cpu):
         extra["plan"]["roofline"] = finish_roofline(batch.stats())
     batch.close()
     wl = "config5" if star else "config3"
-    # the counter passes were taken on the whole 8192-query batch on one GPU
-    pmc = load_profile("batch_pmc.json").get(wl, {}) if args.queries == 8192 and D.world == 1 else {}
+    # the counter passes were taken on one GPU: the whole 8192-query batch, and config 3's
+    # 1024-query shard (an 8-GPU rank's share)
+    pkey = wl if args.queries == 8192 else f"{wl}_q{args.queries}"
+    pmc = load_profile("batch_pmc.json").get(pkey, {}) if D.world == 1 else {}
     evals_total = float(evals_p.sum())
     roof = walk_roofline(sp, pmc.get("steer_walk", {}), wl)
     nn_roof = lockstep_nn_roofline(sp, evals_total, star, pmc)
@@ -1091,6 +1093,12 @@ def compact_line(line, detail_path=None, with_subs=True):
                         "device_reserved_mb": pl.get("device_reserved_mb"),
                         "frac": (pl.get("roofline") or {}).get("frac"),
                         "cpu_same_answer": (pl.get("cpu_baseline") or {}).get("same_answer")}
+    if not with_subs:  # a batch workload line: its step chain and NN roofline
+        sc = line.get("step_chain_us")
+        if isinstance(sc, dict):
+            head["step_chain_us"] = {k: v for k, v in sc.items() if k != "note"}
+        if isinstance(line.get("nn_roofline"), dict):
+            head["nn_roofline"] = _short_roofline(line["nn_roofline"])
     st = line.get("stats")
     if isinstance(st, dict) and st.get("iterations"):
         head["samples_blocked_frac"] = round(st.get("samples_blocked", 0) / st["iterations"], 4)

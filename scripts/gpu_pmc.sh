@@ -14,6 +14,7 @@ args() {
   case $1 in
     config2|config4) echo "--workload $1 --steps 20 --warmup 3 --no-cpu-baseline --no-size-sweep" ;;
     config3) echo "--workload $1 --warmup 3 --no-cpu-baseline --pmc-run" ;;
+    config3s) echo "--workload config3 --queries 1024 --warmup 3 --no-cpu-baseline --pmc-run" ;;
     config5) echo "--workload $1 --warmup 3 --no-cpu-baseline --max-iter 600" ;;  # (PMC of 2000 steps crashed the profiler)
   esac
 }
@@ -51,6 +52,14 @@ if [[ " ${WLS:-config2 config4 config3 config5} " == *" config3 "* ]]; then
   job c3_walk_W config3 steer_walk WRITE_SIZE
   job c3_nn_F config3 mq_sample_nn FETCH_SIZE
   job c3_nn_W config3 mq_sample_nn WRITE_SIZE
+fi
+if [[ " ${WLS:-config2 config4 config3 config5} " == *" config3s "* ]]; then
+  job c3s_walk_A config3s steer_walk $SQA
+  job c3s_walk_B config3s steer_walk $SQB
+  job c3s_walk_F config3s steer_walk FETCH_SIZE
+  job c3s_walk_W config3s steer_walk WRITE_SIZE
+  job c3s_nn_F config3s mq_sample_nn FETCH_SIZE
+  job c3s_nn_W config3s mq_sample_nn WRITE_SIZE
 fi
 if [[ " ${WLS:-config2 config4 config3 config5} " == *" config5 "* ]]; then
   job c5_walk_A config5 steer_walk $SQA

@@ -116,10 +116,16 @@ for wl, tag in (("config2", ""), ("config4", "_config4")):
         d.update(workload=wl, points_per_launch=w["points_per_launch"], note=NOTE, cus=256,
                  lib_sha256_16=L.get("provenance", {}).get("lib_sha256_16"))
         write(f"steer_walk_pmc{tag}.json", d)
-batch = {}
-for wl, pre, nn in (("config3", "c3", "mq_sample_nn"), ("config5", "c5", "star_sample")):
+# (keys this pass did not measure keep their earlier record; each names its library)
+_bp = os.path.join(PROF, "batch_pmc.json")
+batch = json.load(open(_bp)) if os.path.exists(_bp) else {}
+_new = False
+for wl, pre, nn, key in (("config3", "c3", "mq_sample_nn", "config3"),
+                         ("config3s", "c3s", "mq_sample_nn", "config3_q1024"),
+                         ("config5", "c5", "star_sample", "config5")):
     if not os.path.exists(os.path.join(SRC, f"bench_{wl}.json")):
         continue
+    _new = True
     L = line(wl)
     w, n = L["roofline"], L["nn_roofline"]
     d = sq(pre + "_walk", "steer_walk", w["launches"], w["points_per_launch"], "point")
@@ -127,6 +133,6 @@ for wl, pre, nn in (("config3", "c3", "mq_sample_nn"), ("config5", "c5", "star_s
     d.update(points_per_launch=w["points_per_launch"], cus=256, note=NOTE,
              lib_sha256_16=L.get("provenance", {}).get("lib_sha256_16"))
     nl = w["launches"] // (3 if wl == "config5" else 1)  # one NN launch per step
-    batch[wl] = {"steer_walk": d, "nn": dict(kernel=nn, **traffic(pre + "_nn", nn, nl))}
-if batch:
+    batch[key] = {"steer_walk": d, "nn": dict(kernel=nn, **traffic(pre + "_nn", nn, nl))}
+if _new:
     write("batch_pmc.json", batch)
