@@ -4636,6 +4636,43 @@ __global__ __launch_bounds__(256) void cfb_lit_list_kernel(CfbArgs a, int* __res
     if (t < a.st->W && a.status[t] == kLiteral) list[atomicAdd(count, 1)] = t;
 }
 
+// steer_collide_literal with the literal course generated by the whole wave: the word of
+// dubins_path_planning(child → parent) as cf_npoint_steer chooses it, then line_edge_wave (the
+// line kernel's lane-parallel restatement of dubins_literal: the same points, the same trim), then
+// the same chunk test.  A long trim-case course (thousands of points) no longer runs on one lane.
+__device__ int steer_collide_literal_wave(const SceneDev& sc, double x, double y, double yaw,
+                                          double px, double py, double pyaw, double* bx,
+                                          double* by) {
+    const int lane = __lane_id();
+    Steer st;
+    (void)cf_npoint_steer(sc, CfPose{x, y, yaw}, CfPose{px, py, pyaw}, st);
+    const double w[4] = {(double)st.word, st.t, st.p, st.q};
+    int n = 0;
+    const int r = line_edge_wave(x, y, yaw, w, sc.turn_radius, sc.step_size, bx, by,
+                                 kLiteralCap - 1, lane, &n);
+    if (r == kSteerOverflow) return kError;
+    if (lane == 0) {
+        if (r == kSteerNone) {  // polyline [(x, y), (px, py)] (rrt.rs:313)
+            bx[0] = x;
+            by[0] = y;
+            n = 1;
+        }
+        bx[n] = px;
+        by[n] = py;
+    }
+    if (r == kSteerNone) n = 1;
+    __threadfence_block();  // the wave's points before it reads them back
+    const int np = n + 1;   // the junction point is bounds-checked too
+    for (int base = 0; base == 0 || base + 1 < np; base += 63) {
+        const int i = base + lane;
+        const bool has = i < np;
+        const double qx = has ? bx[i] : x, qy = has ? by[i] : y;
+        if (chunk_rejects<false>(sc, has, has && (lane >= 1 || base == 0), has && lane >= 1, qx, qy))
+            return kReject;
+    }
+    return kAccept;
+}
+
 __global__ __launch_bounds__(256) void cfb_lit_run_kernel(CfbArgs a, SceneDev sc,
                                                           const int* __restrict__ list,
                                                           const int* __restrict__ count,
@@ -4648,8 +4685,8 @@ __global__ __launch_bounds__(256) void cfb_lit_run_kernel(CfbArgs a, SceneDev sc
     for (int i = gw; i < n; i += nw) {
         const int t = list[i];
         const SteerTask tk = a.tasks[t];
-        const int r = steer_collide_literal(sc, tk.x, tk.y, a.yaw[t], tk.px, tk.py, tk.pyaw, bx,
-                                            bx + kLiteralCap, bx + 2 * kLiteralCap);
+        const int r = steer_collide_literal_wave(sc, tk.x, tk.y, a.yaw[t], tk.px, tk.py, tk.pyaw,
+                                                 bx, bx + kLiteralCap);
         if (lane == 0) a.status[t] = r;
     }
 }
