@@ -102,3 +102,20 @@ def test_plain_dumps_would_have_failed():
     s = json.dumps({"best_length": math.inf})
     with pytest.raises(ValueError):
         json.loads(s, parse_constant=_refuse)
+
+
+def test_shard_line_carries_chain_and_nn_roofline():
+    """A batch workload line (`--workload config3 --queries 1024`, an 8-GPU rank's shard) keeps
+    its step chain and NN roofline in the compact line (they were in the detail
+    file only); built from round 6's shard record."""
+    bench = _bench()
+    with open(os.path.join(ROOT, "profiles", "r06_bench_config3_shard1024_detail.json")) as f:
+        full = json.load(f)
+    s = bench.compact_line(full, None, with_subs=False)
+    assert len(s.encode()) <= bench.LINE_MAX
+    back = json.loads(s, parse_constant=_refuse)
+    chain = back["step_chain_us"]
+    assert set(chain) >= {"mq_sample_nn", "steer_prep", "steer_walk", "mq_insert"}
+    assert "note" not in chain
+    assert back["nn_roofline"]["kernel"].startswith("mq_sample_nn")
+    assert back["passes"]["steps"] >= back["passes"]["ideal_steps"]
