@@ -318,6 +318,71 @@ def test_straight_segment_shortcut_vs_oracle(pkg, ctx, oracle_mod):
     assert 0 < int(np.sum(ok)) < len(ok)
 
 
+def test_arc_shortcut_vs_oracle(pkg, ctx, oracle_mod):
+    """The walk's analytic arc classes (a_classify: a sure clearance keeps an L / R segment's
+    first and last point) must not change a verdict: candidates whose child's turning circle (left
+    or right, radius R, heading toward the parent) touches an inflated disc from outside or from
+    inside at |C - D| = R +- (r + eps), eps from -1e-2 to 1e-2 and exactly 0, against the oracle's
+    full verify."""
+    from pathplanning_amd import scenes
+
+    raw = scenes.field512()
+    p = _planner(pkg, raw, 8, 4096, ctx)
+    p.extend(8000)
+    x, y, yaw, par = p.tree()
+    sc = oracle_mod.OracleScene.from_raw(raw)
+    otr = oracle_mod.OracleTree(raw["start"], len(x) + 1)
+    otr.x[:len(x)], otr.y[:len(x)], otr.yaw[:len(x)], otr.parent[:len(x)] = x, y, yaw, par
+    otr._c.n = len(x)
+    circ = np.asarray(raw["circles"], dtype=np.float64).reshape(-1, 3)
+    half = raw["robot"][0] / 2.0
+    R = float(raw["robot"][2]) if len(raw["robot"]) > 2 else 4.0
+    rng = np.random.default_rng(11)
+    epss = [0.0, 1e-12, -1e-12, 1e-9, -1e-9, 1e-6, -1e-6, 1e-4, -1e-4, 1e-2, -1e-2]
+    cx, cy, cp = [], [], []
+    tries = 0
+    while len(cx) < 6000 and tries < 200000:
+        tries += 1
+        d = int(rng.integers(0, len(circ)))
+        dx, dy, rr = circ[d, 0], circ[d, 1], circ[d, 2] + half
+        near = np.nonzero(np.hypot(x - dx, y - dy) < 40.0)[0]
+        if len(near) == 0:
+            continue
+        i = int(near[int(rng.integers(0, len(near)))])
+        eps = epss[len(cx) % len(epss)]
+        inner = rng.random() < 0.3 and rr < R
+        target = (R - rr - eps) if inner else (R + rr + eps)
+        th = rng.uniform(-math.pi, math.pi)
+        side = 1.0 if rng.random() < 0.5 else -1.0  # left / right circle
+        # child c = p - s (cos th, sin th) heads toward the parent p; its circle centre is
+        # c + side R (-sin th, cos th): solve |centre(s) - D| = target for s > 0
+        ux, uy = math.cos(th), math.sin(th)
+        ox = x[i] + side * R * (-uy) - dx
+        oy = y[i] + side * R * ux - dy
+        # |o - s u|^2 = target^2  ->  s^2 - 2 s (o.u) + |o|^2 - target^2 = 0
+        b = ox * ux + oy * uy
+        disc = b * b - (ox * ox + oy * oy - target * target)
+        if disc < 0.0:
+            continue
+        for sgn in (1.0, -1.0):
+            s_ = b + sgn * math.sqrt(disc)
+            if not (0.3 < s_ < 60.0):
+                continue
+            qx, qy = x[i] - s_ * ux, y[i] - s_ * uy
+            if 0.5 < qx < 511.5 and 0.5 < qy < 511.5:
+                cx.append(qx)
+                cy.append(qy)
+                cp.append(i)
+                break
+    cx, cy, cp = np.array(cx), np.array(cy), np.array(cp, dtype=np.int32)
+    assert len(cx) >= 3000
+    ok, _ = p.verify_node_batch(cx, cy, cp)
+    bad = [i for i in range(len(cx))
+           if bool(ok[i]) != oracle_mod.verify_candidate(sc, otr, cx[i], cy[i], int(cp[i]))[0]]
+    assert not bad, (len(bad), bad[:10])
+    assert 0 < int(np.sum(ok)) < len(ok)
+
+
 # ------------------------------------------------------------------------- full-size properties
 def test_100k_tree_properties(pkg, ctx, oracle_mod):
     """BASELINE config 2 at full size: grow past 100k nodes, then check size-independent
