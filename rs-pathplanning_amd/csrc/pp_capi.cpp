@@ -213,7 +213,7 @@ struct pp_ctx {
     DBuf<int> cfb_nodei;   // [4 (nitems + Q)]: depth, open, tfirst, tcnt
     DBuf<int> cfb_rows;    // [rows]: gclaim
     DBuf<unsigned char> cfb_rows8;  // [2 rows]: tnone, tnone_up
-    DBuf<int> cfb_gotab, cfb_plist, cfb_tnode, cfb_status, cfb_misc, cfb_lit;
+    DBuf<int> cfb_gotab, cfb_plist, cfb_tnode, cfb_status, cfb_misc, cfb_lit, cfb_dhist;
     DBuf<SteerTask> cfb_tasks;
     DBuf<StarTaskExt> cfb_ext;
     DBuf<PrepRec> cfb_rec;
@@ -697,6 +697,7 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     PP_HIP(c->cfb_yaw.reserve(cap_tasks));
     PP_HIP(c->cfb_state.reserve(2));  // [0] the round's, [1] a chunk's
     PP_HIP(c->cfb_misc.reserve(4));
+    PP_HIP(c->cfb_dhist.reserve(kCfbDepthBins));
     if (c->prof) PP_HIP(c->cfb_pts.reserve(3 * kWalkTallySlots));
     SceneDev sd = c->scene_dev();
     sd.step_size = c->mq_step;
@@ -737,6 +738,7 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     a.maxdepth = c->cfb_misc.p;
     a.pcount = c->cfb_misc.p + 1;
     a.wsum = c->cfb_misc.p + 2;  // (the rounds' task counts: profiling)
+    a.dhist = c->cfb_dhist.p;
     // per launch: memo, goal verdicts, claims, line items, error bits, counters, DevState
     PP_HIP(hipMemsetAsync(c->cf_memo.p, 0, 2 * rows * sizeof(int), st));
     PP_HIP(hipMemsetAsync(c->cfb_gotab.p, 0, (size_t)total * sizeof(int), st));
@@ -744,6 +746,7 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     PP_HIP(hipMemsetAsync(c->cf_items.p, 0, sizeof(int), st));
     PP_HIP(hipMemsetAsync(c->cf_err.p, 0, 2 * sizeof(int), st));
     PP_HIP(hipMemsetAsync(c->cfb_misc.p, 0, 4 * sizeof(int), st));
+    PP_HIP(hipMemsetAsync(c->cfb_dhist.p, 0, kCfbDepthBins * sizeof(int), st));
     PP_HIP(hipMemsetAsync(c->cfb_state.p, 0, 2 * sizeof(DevState), st));
     if (c->prof) PP_HIP(hipMemsetAsync(c->cfb_pts.p, 0, 3 * kWalkTallySlots * sizeof(long long), st));
     if (c->prof) {
@@ -752,8 +755,20 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     }
     PP_HIP(launch_cfb(st, sd, a, kCfbDepth, 0));
     int misc[4] = {0, 0, 0, 0};
+    int dh[kCfbDepthBins];
     PP_HIP(hipMemcpyAsync(misc, c->cfb_misc.p, sizeof misc, hipMemcpyDeviceToHost, st));
+    PP_HIP(hipMemcpyAsync(dh, c->cfb_dhist.p, sizeof dh, hipMemcpyDeviceToHost, st));
     PP_HIP(hipStreamSynchronize(st));
+    // a bound on round (m0, span)'s tasks: a node of depth d emits min(span, d + 1 - m0) of them
+    // (fewer once it settled); the last bin's nodes (that depth or more) count span each
+    auto round_bound = [&](int m0, int span) -> size_t {
+        size_t t = 0;
+        for (int d = 0; d < kCfbDepthBins; ++d) {
+            const int e = d == kCfbDepthBins - 1 ? span : std::min(span, d + 1 - m0);
+            if (e > 0) t += (size_t)e * (size_t)dh[d];
+        }
+        return t;
+    };
     // round r tests the candidates at depths m0 .. m0 + span - 1 of every open node: the first
     // round cfb_span0 of them, the later ones cfb_span
     long long* wpts = c->prof ? c->cfb_pts.p : nullptr;
@@ -776,7 +791,8 @@ int cf_run_rounds(pp_ctx* c, const TreeDev& tr, int total, const CfBatch& cb_in,
     int rounds = 0;
     for (int m0 = 0; m0 <= misc[0]; ++rounds) {
         a.span = rounds == 0 ? span0 : span1;
-        const int mt = (int)std::min<size_t>(cap_tasks, (size_t)a.span * nn);
+        const int mt = (int)std::min<size_t>(cap_tasks, std::min<size_t>((size_t)a.span * nn,
+                                                                         round_bound(m0, a.span)));
         PP_HIP(launch_cfb(st, sd, a, kCfbEmitA, m0));
         if (int r = steer(mt, false)) return r;
         PP_HIP(launch_cfb_literal(st, sd, a, mt, c->cfb_lit.p, c->cfb_misc.p + 3, c->api_lit_scratch.p));

@@ -146,7 +146,9 @@ struct CfbArgs {
     int* maxdepth = nullptr;
     int* pcount = nullptr;
     int* wsum = nullptr;      // (profiling) += every round's task count
+    int* dhist = nullptr;     // [kCfbDepthBins] nodes per depth (the last bin: that depth or more)
 };
+constexpr int kCfbDepthBins = 64;
 enum : int { kCfbDepth = 0, kCfbEmitA, kCfbConsumeA, kCfbEmitB, kCfbStoreB, kCfbAssemble };
 hipError_t launch_cfb(hipStream_t s, const SceneDev& sc, CfbArgs a, int phase, int round,
                       int* ok = nullptr, double* len = nullptr, int* npts = nullptr,

@@ -4382,14 +4382,30 @@ __device__ inline void cfb_node(const CfbArgs& a, int b, int& q, int& c) {
 // depth of every phase-A node, its own tree edge's None flag (the steer from its pose to its
 // parent's, rrt.rs:313 / 529), and the open state; maxdepth for the host
 __global__ __launch_bounds__(256) void cfb_depth_kernel(CfbArgs a, SceneDev sc) {
+    // (the depth histogram per workgroup in LDS, then one atomic per nonzero bin: the host bounds
+    // each steer round's task count by it)
+    __shared__ int s_h[kCfbDepthBins];
+    if (threadIdx.x < kCfbDepthBins) s_h[threadIdx.x] = 0;
+    __syncthreads();
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= a.nitems + a.Q) return;
+    const bool in = b < a.nitems + a.Q;
+    if (in) {
+        int q0, c0;
+        cfb_node(a, b, q0, c0);
+        const size_t o0 = (size_t)q0 * a.row_cap;
+        int d0 = 0;
+        for (int k = c0; a.tr.parent[o0 + k] >= 0; k = a.tr.parent[o0 + k]) ++d0;
+        atomicAdd(&s_h[min(d0, kCfbDepthBins - 1)], 1);
+        a.depth[b] = d0;
+    }
+    __syncthreads();
+    if (a.dhist && threadIdx.x < kCfbDepthBins && s_h[threadIdx.x])
+        atomicAdd(&a.dhist[threadIdx.x], s_h[threadIdx.x]);
+    if (!in) return;
     int q, c;
     cfb_node(a, b, q, c);
     const size_t o = (size_t)q * a.row_cap;
-    int d = 0;
-    for (int k = c; a.tr.parent[o + k] >= 0; k = a.tr.parent[o + k]) ++d;
-    a.depth[b] = d;
+    const int d = a.depth[b];
     a.open[b] = 1;
     atomicMax(a.maxdepth, d);
     int none = 0;
